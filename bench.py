@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""Throughput bench of the Ballé-2017 codec hot path on MI355X (BASELINE.json metric).
+
+One step = encode+decode of one batch of synthetic 256×256×3 images per GPU, N = 192:
+    conv1+GDN → conv2+GDN → conv3+round+rate → deconv1+IGDN → deconv2+IGDN → deconv3+clamp
+    → deterministic per-batch bit reduction (bpp)
+with inputs already resident in HBM. Images shard by batch across ranks (no collective in the
+data path; "weak" scaling). Prints ONE JSON line on rank 0.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from iclr_17_compression_amd import kernels, synth  # noqa: E402
+from iclr_17_compression_amd.model import ImageCompressor  # noqa: E402
+
+METRIC = "Mpixels/s encode+decode at 1/2/4/8 GPU; bpp & PSNR parity on Kodak"
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 dense peak
+HBM_PEAK_GBS = 8000.0
+
+LAYERS = ("conv1_gdn1", "conv2_gdn2", "conv3_quant_rate", "deconv1_igdn1", "deconv2_igdn2",
+          "deconv3_clamp", "bits_reduce")
+
+
+def layer_flops(N: int, H: int, W: int) -> dict:
+    """Algorithmic FLOPs per image (2·MAC) of each fused kernel."""
+    h1, w1, h2, w2, h3, w3 = H // 4, W // 4, H // 8, W // 8, H // 16, W // 16
+    mac = {
+        "conv1_gdn1": h1 * w1 * N * 3 * 81 + h1 * w1 * N * N,
+        "conv2_gdn2": h2 * w2 * N * N * 25 + h2 * w2 * N * N,
+        "conv3_quant_rate": h3 * w3 * N * N * 25,
+        "deconv1_igdn1": h3 * w3 * N * N * 25 + h2 * w2 * N * N,
+        "deconv2_igdn2": h2 * w2 * N * N * 25 + h1 * w1 * N * N,
+        "deconv3_clamp": h1 * w1 * N * 3 * 81,
+        "bits_reduce": 0,
+    }
+    return {k: 2.0 * v for k, v in mac.items()}
+
+
+def layer_bytes(N: int, H: int, W: int) -> dict:
+    """Algorithmic HBM bytes per image of each fused kernel (fp32 NHWC activations read once,
+    written once; weights amortised over the batch and ignored)."""
+    h1, w1, h2, w2, h3, w3 = H // 4, W // 4, H // 8, W // 8, H // 16, W // 16
+    f = 4
+    return {
+        "conv1_gdn1": f * (3 * H * W + h1 * w1 * N),
+        "conv2_gdn2": f * (h1 * w1 * N + h2 * w2 * N),
+        "conv3_quant_rate": f * (h2 * w2 * N + h3 * w3 * N),
+        "deconv1_igdn1": f * (h3 * w3 * N + h2 * w2 * N),
+        "deconv2_igdn2": f * (h2 * w2 * N + h1 * w1 * N),
+        "deconv3_clamp": f * (h1 * w1 * N + 3 * H * W),
+        "bits_reduce": 0,
+    }
+
+
+class Step:
+    """The fused forward of ImageCompressor.forward (model.py:47-80), layer by layer, with
+    optional HIP-event brackets on the launching stream for per-kernel timing."""
+
+    def __init__(self, net: ImageCompressor, x: torch.Tensor):
+        self.net, self.x = net, x
+        B, _, H, W = x.shape
+        self.scale = 1.0 / (B * H * W)
+        self.N = net.out_channel_N
+        self.enc = net.Encoder.packed()
+        self.dec = net.Decoder.packed()
+        self.rate = net.bitEstimator.packed()
+
+    def __call__(self, events=None):
+        net, N = self.net, self.N
+        w1, w2, w3, g1, g2 = self.enc
+        d1, d2, d3, q1, q2 = self.dec
+        ev = (lambda i: events[i].record()) if events is not None else (lambda i: None)
+        ev(0)
+        h = kernels.conv1_gdn(self.x, w1, net.Encoder.conv1.bias, g1[0], g1[1], N)
+        ev(1)
+        h = kernels.conv2_gdn(h, w2, net.Encoder.conv2.bias, g2[0], g2[1])
+        ev(2)
+        y_hat, partial = kernels.conv3_quant_rate(h, w3, self.rate)
+        ev(3)
+        h = kernels.deconv_igdn(y_hat, d1, net.Decoder.deconv1.bias, q1[0], q1[1])
+        ev(4)
+        h = kernels.deconv_igdn(h, d2, net.Decoder.deconv2.bias, q2[0], q2[1])
+        ev(5)
+        clipped, _, _ = kernels.deconv3(h, d3, net.Decoder.deconv3.bias)
+        ev(6)
+        _, bpp = kernels.reduce_partials(partial, self.scale, per_image=False)
+        ev(7)
+        return clipped, y_hat, bpp
+
+
+def cpu_baseline(N: int, H: int, W: int, budget_s: float) -> dict:
+    """The oracle (op-for-op restatement of the reference forward, bit-identical to it on the
+    build host) timed on this host's cores on a bounded sample."""
+    from oracle import codec_ref as oracle
+    cores = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(cores)
+    sd = oracle.state_dict_to_torch(synth.trained_like_state_dict(N, 1))
+    B = 4
+    x = torch.from_numpy(synth.to_unit_float(synth.image_u8(99, B, H, W)))
+    with torch.no_grad():
+        oracle.codec_forward(x[:1], sd)  # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            oracle.codec_forward(x, sd)
+            n += 1
+            if time.perf_counter() - t0 > budget_s:
+                break
+        dt = time.perf_counter() - t0
+    return {"value": round(n * B * H * W / dt / 1e6, 4), "unit": "Mpix/s", "cores": cores,
+            "kind": "port",
+            "sample": f"{n} x eval forward of B={B} {H}x{W} images, N={N}, fp32 torch CPU "
+                      f"({dt:.1f} s, {platform.processor() or platform.machine()})"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64, help="images per GPU")
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--N", type=int, default=192)
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    N, S, B = args.N, args.size, args.batch
+    net = ImageCompressor(out_channel_N=N)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in synth.trained_like_state_dict(N, 1).items()})
+    net = net.to(dev).eval()
+    # each rank encodes its own shard of the global batch (images are independent)
+    x = torch.from_numpy(synth.to_unit_float(synth.image_u8(1000 + rank, B, S, S))).to(dev)
+    step = Step(net, x)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        # per-kernel durations: HIP events on the launching stream, a second pass of the same
+        # K steps (kept out of the wall-clock region so the brackets cannot perturb it)
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(8)] for _ in range(args.steps)]
+        for i in range(args.steps):
+            _, _, bpp = step(evs[i])
+        torch.cuda.synchronize()
+    per_layer_ms = {name: float(np.mean([evs[i][j].elapsed_time(evs[i][j + 1]) for i in range(args.steps)]))
+                    for j, name in enumerate(LAYERS)}
+
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = t.item()
+    pixels = world * B * S * S * args.steps
+    value = pixels / elapsed / 1e6
+    ms_per_step = elapsed / args.steps * 1e3
+
+    flops = layer_flops(N, S, S)
+    bytes_ = layer_bytes(N, S, S)
+    dominant = max(LAYERS, key=lambda k: per_layer_ms[k])
+    achieved = flops[dominant] * B / (per_layer_ms[dominant] * 1e-3) / 1e12
+    layers = {k: {"ms": round(per_layer_ms[k], 4),
+                  "tflops": round(flops[k] * B / (per_layer_ms[k] * 1e-3) / 1e12, 2) if flops[k] else None,
+                  "gbs": round(bytes_[k] * B / (per_layer_ms[k] * 1e-3) / 1e9, 1) if bytes_[k] else None}
+              for k in LAYERS}
+    total_flops = sum(flops.values()) * B
+    result = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "Mpix/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (splitmix64 uint8/255 images, seeded trained-like weights)",
+        "config": {"workload": f"eval encode+decode (round quantiser + rate), {B} x {S}x{S}x3 images per GPU, N={N}",
+                   "N": N, "image": f"{S}x{S}x3", "batch_per_gpu": B, "global_batch": B * world,
+                   "quant": "round", "precision": "fp32 (exact-f32 MFMA)",
+                   "parallelism": f"dp{world} (images sharded by rank, no data-path collective)"},
+        "roofline": {"bound": "mfma", "kernel": dominant, "achieved": round(achieved, 2),
+                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                     "flop_per_launch": flops[dominant] * B,
+                     "whole_step_tflops": round(total_flops / (ms_per_step * 1e-3) / 1e12, 2)},
+        "layers": layers,
+        "bpp_last": round(bpp.item(), 6),
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(N, S, S, args.cpu_budget)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

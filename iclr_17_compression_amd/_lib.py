@@ -1,0 +1,108 @@
+"""ctypes binding of libiclr17.so (C ABI declared in include/iclr17.h).
+
+The library is the ONLY compute path of this package: there is no PyTorch or CPU fallback.
+Loading fails loudly (ImportError-style RuntimeError) when the shared object is missing; every
+op fails loudly on non-GPU tensors.
+
+torch is imported first on purpose: torch ships its own libamdhip64.so (same SONAME as the
+system ROCm's), so importing it first makes libiclr17.so bind to the HIP runtime that owns
+torch's streams and allocations instead of loading a second runtime into the process.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("ICLR17_LIB", os.path.join(_HERE, "libiclr17.so"))
+
+ICLR17_QUANT_ROUND = 0
+ICLR17_QUANT_NOISE = 1
+ICLR17_LAYOUT_NCHW = 0
+ICLR17_LAYOUT_NHWC = 1
+ICLR17_W_CONV1 = 0
+ICLR17_W_CONV5 = 1
+ICLR17_W_DECONV5 = 2
+ICLR17_W_DECONV9 = 3
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_I64 = ctypes.c_int64
+_D = ctypes.c_double
+_F = ctypes.c_float
+_SZ = ctypes.c_size_t
+
+# name: (restype, argtypes) — one line per entry point of include/iclr17.h
+SIGNATURES = {
+    "iclr17_version": (_I, []),
+    "iclr17_last_error": (_I, [ctypes.c_char_p, _SZ]),
+    "iclr17_packed_weight_size": (_SZ, [_I, _I]),
+    "iclr17_pack_weight": (_I, [_I, _P, _P, _I, _P]),
+    "iclr17_pack_gdn": (_I, [_P, _P, _P, _P, _I, _F, _F, _F, _P]),
+    "iclr17_pack_rate": (_I, [_P] * 12 + [_I, _P]),
+    "iclr17_analysis_conv1_gdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_analysis_conv2_gdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_analysis_conv3_quant_rate": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P]),
+    "iclr17_analysis_conv3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P]),
+    "iclr17_rate_partials_per_image": (_I, [_I, _I, _I]),
+    "iclr17_synthesis_deconv_igdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_synthesis_deconv3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_output_partials_per_image": (_I, [_I, _I]),
+    "iclr17_reduce_partials": (_I, [_P, _I, _I, _P, _P, _D, _P]),
+    "iclr17_gdn": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "iclr17_bit_estimator": (_I, [_P, _I64, _I, _I64, _P, _P, _P]),
+    "iclr17_bitparm": (_I, [_P, _I64, _I, _I64, _P, _P, _P, _P, _P]),
+    "iclr17_rate_bits": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "iclr17_rate_bits_partials": (_I, [_I, _I, _I]),
+}
+
+
+class Iclr17Error(RuntimeError):
+    pass
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libiclr17.so once; raise if it is missing (no fallback exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise Iclr17Error(
+                f"iclr17: HIP library not found at {LIB_PATH}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` or `make -C "
+                "iclr_17_compression_amd/csrc` (there is no CPU fallback)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def last_error() -> str:
+    buf = ctypes.create_string_buffer(512)
+    load().iclr17_last_error(buf, len(buf))
+    return buf.value.decode(errors="replace")
+
+
+def call(name: str, *args) -> int:
+    """Invoke an entry point; non-zero return → Iclr17Error with the library's message."""
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        raise Iclr17Error(last_error() or f"{name} failed with code {rc}")
+    return rc
+
+
+def query(name: str, *args):
+    return getattr(load(), name)(*args)

@@ -1,0 +1,307 @@
+// Parameter packing, the factorised rate model as stand-alone kernels, and deterministic
+// partial-sum reductions (gfx950). All memory-bound / parameter-sized work.
+#include <string.h>
+
+#include "common.h"
+
+namespace iclr17 {
+
+void deconv_phase_taps(int K, int s, int p, int ry, int rx, int* kh_out, int* kw_out, int* count);
+
+namespace {
+
+hipStream_t S(void* s) { return (hipStream_t)s; }
+
+struct TapList {
+  int kh[25];
+  int kw[25];
+};
+
+// conv1 [N][3][9][9] → [64 quads][N][4], k = c·81 + kh·9 + kw, k ≥ 243 zero.
+__global__ void pack_conv1_kernel(const float* __restrict__ w, float* __restrict__ out, int N) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 256 * N) return;
+  const int e = i & 3, n = (i >> 2) % N, q = (i >> 2) / N;
+  const int k = 4 * q + e;
+  out[i] = k < 243 ? w[(long)n * 243 + k] : 0.f;
+}
+
+// conv k5 [co][ci][5][5] → [25 taps][ci/4][co][4], tap = kh·5 + kw.
+__global__ void pack_conv5_kernel(const float* __restrict__ w, float* __restrict__ out, int N) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = 25L * N * N;
+  if (i >= total) return;
+  const int e = i & 3;
+  const int co = (i >> 2) % N;
+  const long r = (i >> 2) / N;
+  const int q = r % (N / 4), tap = r / (N / 4);
+  const int ci = 4 * q + e;
+  out[i] = w[((long)co * N + ci) * 25 + tap];
+}
+
+// deconv k5 [ci][co][5][5] → phase-major taps [25][ci/4][co][4].
+__global__ void pack_deconv5_kernel(const float* __restrict__ w, float* __restrict__ out, int N,
+                                    TapList tl) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = 25L * N * N;
+  if (i >= total) return;
+  const int e = i & 3;
+  const int co = (i >> 2) % N;
+  const long r = (i >> 2) / N;
+  const int q = r % (N / 4), tap = r / (N / 4);
+  const int ci = 4 * q + e;
+  out[i] = w[((long)ci * N + co) * 25 + tl.kh[tap] * 5 + tl.kw[tap]];
+}
+
+// deconv3 [ci][3][9][9] → all-phase [9 neighbours][ci/4][48][4]; column n = co·16 + ry·4 + rx,
+// neighbour (dy, dx) ∈ {-1,0,1}², kernel tap k = r + 4 − 4d (zero outside 0..8).
+__global__ void pack_deconv9_kernel(const float* __restrict__ w, float* __restrict__ out, int N) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = 9L * N * 48;
+  if (i >= total) return;
+  const int e = i & 3;
+  const int n = (i >> 2) % 48;
+  const long r = (i >> 2) / 48;
+  const int q = r % (N / 4), nb = r / (N / 4);
+  const int ci = 4 * q + e;
+  const int co = n >> 4, ry = (n >> 2) & 3, rx = n & 3;
+  const int dy = nb / 3 - 1, dx = nb % 3 - 1;
+  const int kh = ry + 4 - 4 * dy, kw = rx + 4 - 4 * dx;
+  float v = 0.f;
+  if (kh >= 0 && kh < 9 && kw >= 0 && kw < 9) v = w[(((long)ci * 3 + co) * 9 + kh) * 9 + kw];
+  out[i] = v;
+}
+
+// models/GDN.py:73-79 reparametrisation; gamma packed [C/4][C][4] (packed[q][i][e] = γ[i][4q+e]).
+__global__ void pack_gdn_kernel(const float* __restrict__ beta, const float* __restrict__ gamma,
+                                float* __restrict__ beta_eff, float* __restrict__ gp, int C,
+                                float bbound, float gbound, float ped) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < C) {
+    const float m = fmaxf(beta[i], bbound);
+    beta_eff[i] = m * m - ped;
+  }
+  if (i < C * C) {
+    const int e = i & 3, row = (i >> 2) % C, q = (i >> 2) / C;
+    const float m = fmaxf(gamma[(long)row * C + 4 * q + e], gbound);
+    gp[i] = m * m - ped;
+  }
+}
+
+struct RatePtrs {
+  const float* p[11];  // h1 b1 a1 h2 b2 a2 h3 b3 a3 h4 b4
+};
+
+__device__ __forceinline__ float softplus_ref(float x) {
+  // torch.nn.functional.softplus(beta=1, threshold=20)
+  return x > 20.f ? x : log1pf(expf(x));
+}
+
+__global__ void pack_rate_kernel(RatePtrs rp, float* __restrict__ out, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  for (int k = 0; k < 3; ++k) {
+    out[(3 * k + 0) * C + c] = softplus_ref(rp.p[3 * k + 0][c]);
+    out[(3 * k + 1) * C + c] = rp.p[3 * k + 1][c];
+    out[(3 * k + 2) * C + c] = tanhf(rp.p[3 * k + 2][c]);
+  }
+  out[9 * C + c] = softplus_ref(rp.p[9][c]);
+  out[10 * C + c] = rp.p[10][c];
+}
+
+__global__ void bit_estimator_kernel(const float* __restrict__ x, int64_t n, int C, int64_t inner,
+                                     const float* __restrict__ rp, float* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)((i / inner) % C);
+    out[i] = bitparm_cdf(x[i], rp, C, c);
+  }
+}
+
+// One Bitparm layer (bitEstimator.py:20-25): ta == nullptr selects the final (sigmoid) form.
+__global__ void bitparm_kernel(const float* __restrict__ x, int64_t n, int C, int64_t inner,
+                               const float* __restrict__ sp, const float* __restrict__ bb,
+                               const float* __restrict__ ta, float* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)((i / inner) % C);
+    const float t = x[i] * sp[c] + bb[c];
+    out[i] = ta == nullptr ? 1.0f / (1.0f + expf(-t)) : t + tanhf(t) * ta[c];
+  }
+}
+
+__global__ void softplus_tanh_kernel(const float* __restrict__ h, const float* __restrict__ a,
+                                     float* __restrict__ sp, float* __restrict__ ta, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  sp[c] = softplus_ref(h[c]);
+  if (a != nullptr) ta[c] = tanhf(a[c]);
+}
+
+constexpr int kRateChunk = 4096;  // latents per partial (fixed → deterministic sums)
+
+// Σ bits over a fixed 4096-element chunk of one image's latent; partial[b][chunk].
+__global__ void rate_bits_kernel(const float* __restrict__ z, int C, int HW, int layout,
+                                 const float* __restrict__ rp, double* __restrict__ partial,
+                                 int chunks) {
+  __shared__ float red[4];
+  const int b = blockIdx.x / chunks, ch = blockIdx.x % chunks;
+  const long per_image = (long)C * HW;
+  const long lo = (long)ch * kRateChunk;
+  const long hi = lo + kRateChunk < per_image ? lo + kRateChunk : per_image;
+  float s = 0.f;
+  for (long j = lo + threadIdx.x; j < hi; j += 256) {
+    const int c = layout == ICLR17_LAYOUT_NCHW ? (int)(j / HW) : (int)(j % C);
+    s += element_bits(z[(long)b * per_image + j], rp, C, c);
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < 4; ++w) t += (double)red[w];
+    partial[(long)b * chunks + ch] = t;
+  }
+}
+
+__global__ void reduce_partials_kernel(const double* __restrict__ partial, int B, int T,
+                                       double* per_image, float* total, double scale) {
+  __shared__ double img[1024];
+  double acc = 0.0;
+  for (int b0 = 0; b0 < B; b0 += 1024) {
+    const int nb = B - b0 < 1024 ? B - b0 : 1024;
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+      double s = 0.0;
+      const double* p = partial + (long)(b0 + b) * T;
+      for (int t = 0; t < T; ++t) s += p[t];
+      img[b] = s;
+      if (per_image) per_image[b0 + b] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int b = 0; b < nb; ++b) acc += img[b];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && total) *total = (float)(acc * scale);
+}
+
+}  // namespace
+}  // namespace iclr17
+
+using namespace iclr17;
+
+extern "C" {
+
+size_t iclr17_packed_weight_size(int which, int N) {
+  switch (which) {
+    case ICLR17_W_CONV1: return (size_t)256 * N;
+    case ICLR17_W_CONV5:
+    case ICLR17_W_DECONV5: return (size_t)25 * N * N;
+    case ICLR17_W_DECONV9: return (size_t)9 * N * 48;
+    default: return 0;
+  }
+}
+
+int iclr17_pack_weight(int which, const float* w, float* packed, int N, void* stream) {
+  ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "pack_weight: N=%d unsupported", N);
+  ICLR17_REQUIRE(w && packed, ICLR17_EINVAL, "pack_weight: null pointer");
+  const size_t total = iclr17_packed_weight_size(which, N);
+  ICLR17_REQUIRE(total > 0, ICLR17_EINVAL, "pack_weight: unknown weight kind %d", which);
+  const dim3 grid((unsigned)((total + 255) / 256));
+  hipStream_t st = S(stream);
+  switch (which) {
+    case ICLR17_W_CONV1: hipLaunchKernelGGL(pack_conv1_kernel, grid, dim3(256), 0, st, w, packed, N); break;
+    case ICLR17_W_CONV5: hipLaunchKernelGGL(pack_conv5_kernel, grid, dim3(256), 0, st, w, packed, N); break;
+    case ICLR17_W_DECONV5: {
+      TapList tl;
+      int n = 0;
+      for (int ry = 0; ry < 2; ++ry)
+        for (int rx = 0; rx < 2; ++rx) {
+          int c = 0;
+          deconv_phase_taps(5, 2, 2, ry, rx, tl.kh + n, tl.kw + n, &c);
+          n += c;
+        }
+      ICLR17_REQUIRE(n == 25, ICLR17_EINVAL, "pack_weight: deconv tap count %d", n);
+      hipLaunchKernelGGL(pack_deconv5_kernel, grid, dim3(256), 0, st, w, packed, N, tl);
+      break;
+    }
+    case ICLR17_W_DECONV9: hipLaunchKernelGGL(pack_deconv9_kernel, grid, dim3(256), 0, st, w, packed, N); break;
+  }
+  return check_launch("pack_weight");
+}
+
+int iclr17_pack_gdn(const float* beta, const float* gamma, float* beta_eff, float* gamma_packed,
+                    int C, float beta_bound, float gamma_bound, float pedestal, void* stream) {
+  ICLR17_REQUIRE(C > 0 && C % 4 == 0, ICLR17_EINVAL, "pack_gdn: C=%d must be a multiple of 4", C);
+  ICLR17_REQUIRE(beta && gamma && beta_eff && gamma_packed, ICLR17_EINVAL, "pack_gdn: null pointer");
+  const int total = C * C;
+  hipLaunchKernelGGL(pack_gdn_kernel, dim3((total + 255) / 256), dim3(256), 0, S(stream), beta,
+                     gamma, beta_eff, gamma_packed, C, beta_bound, gamma_bound, pedestal);
+  return check_launch("pack_gdn");
+}
+
+int iclr17_pack_rate(const float* h1, const float* b1, const float* a1, const float* h2,
+                     const float* b2, const float* a2, const float* h3, const float* b3,
+                     const float* a3, const float* h4, const float* b4, float* packed, int C,
+                     void* stream) {
+  RatePtrs rp = {{h1, b1, a1, h2, b2, a2, h3, b3, a3, h4, b4}};
+  for (int i = 0; i < 11; ++i) ICLR17_REQUIRE(rp.p[i], ICLR17_EINVAL, "pack_rate: null parameter %d", i);
+  ICLR17_REQUIRE(packed && C > 0, ICLR17_EINVAL, "pack_rate: bad output");
+  hipLaunchKernelGGL(pack_rate_kernel, dim3((C + 255) / 256), dim3(256), 0, S(stream), rp, packed, C);
+  return check_launch("pack_rate");
+}
+
+int iclr17_bit_estimator(const float* x, int64_t n, int C, int64_t inner,
+                         const float* rate_packed, float* out, void* stream) {
+  ICLR17_REQUIRE(n >= 0 && C > 0 && inner > 0, ICLR17_EINVAL, "bit_estimator: bad shape");
+  if (n == 0) return ICLR17_OK;
+  ICLR17_REQUIRE(x && rate_packed && out, ICLR17_EINVAL, "bit_estimator: null pointer");
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(bit_estimator_kernel, dim3((unsigned)blocks), dim3(256), 0, S(stream), x, n,
+                     C, inner, rate_packed, out);
+  return check_launch("bit_estimator");
+}
+
+int iclr17_bitparm(const float* x, int64_t n, int C, int64_t inner, const float* h,
+                   const float* b, const float* a, float* work, float* out, void* stream) {
+  ICLR17_REQUIRE(n >= 0 && C > 0 && inner > 0, ICLR17_EINVAL, "bitparm: bad shape");
+  if (n == 0) return ICLR17_OK;
+  ICLR17_REQUIRE(x && h && b && work && out, ICLR17_EINVAL, "bitparm: null pointer");
+  hipStream_t st = S(stream);
+  float* sp = work;
+  float* ta = a != nullptr ? work + C : nullptr;
+  hipLaunchKernelGGL(softplus_tanh_kernel, dim3((C + 255) / 256), dim3(256), 0, st, h, a, sp, ta, C);
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(bitparm_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, n, C, inner, sp,
+                     b, ta, out);
+  return check_launch("bitparm");
+}
+
+int iclr17_rate_bits_partials(int C, int h, int w) {
+  const long n = (long)C * h * w;
+  return (int)((n + kRateChunk - 1) / kRateChunk);
+}
+
+int iclr17_rate_bits(const float* z, int B, int C, int h, int w, int layout,
+                     const float* rate_packed, double* bits_partial, void* stream) {
+  ICLR17_REQUIRE(B > 0 && C > 0 && h > 0 && w > 0, ICLR17_EINVAL, "rate_bits: bad shape");
+  ICLR17_REQUIRE(layout == ICLR17_LAYOUT_NCHW || layout == ICLR17_LAYOUT_NHWC, ICLR17_EINVAL,
+                 "rate_bits: bad layout");
+  ICLR17_REQUIRE(z && rate_packed && bits_partial, ICLR17_EINVAL, "rate_bits: null pointer");
+  const int chunks = iclr17_rate_bits_partials(C, h, w);
+  hipLaunchKernelGGL(rate_bits_kernel, dim3(B * chunks), dim3(256), 0, S(stream), z, C, h * w,
+                     layout, rate_packed, bits_partial, chunks);
+  return check_launch("rate_bits");
+}
+
+int iclr17_reduce_partials(const double* partial, int B, int T, double* per_image, float* total,
+                           double scale, void* stream) {
+  ICLR17_REQUIRE(partial && B > 0 && T > 0, ICLR17_EINVAL, "reduce_partials: bad arguments");
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(256), 0, S(stream), partial, B, T,
+                     per_image, total, scale);
+  return check_launch("reduce_partials");
+}
+
+}  // extern "C"

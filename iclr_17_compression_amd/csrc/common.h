@@ -1,0 +1,73 @@
+// Shared device/host helpers for the iclr17 gfx950 kernels.
+//
+// Numerics contract (fp32 parity mode): every contraction runs on the exact-f32 MFMA
+// (v_mfma_f32_16x16x4_f32: a k-ordered fmaf chain, no reduced-precision internals); every
+// elementwise step the reference evaluates as separate PyTorch ops (mul, add, sqrt, div …)
+// is evaluated as separate correctly-rounded ops here too — the library is compiled with
+// -ffp-contract=off so no mul+add pair is silently fused.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include "../../include/iclr17.h"
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+namespace iclr17 {
+
+// ----------------------------------------------------------------------------- errors
+void set_error(int code, const char* fmt, ...);
+int check_launch(const char* what);
+
+#define ICLR17_REQUIRE(cond, code, ...)          \
+  do {                                           \
+    if (!(cond)) {                               \
+      ::iclr17::set_error((code), __VA_ARGS__);  \
+      return (code);                             \
+    }                                            \
+  } while (0)
+
+// ----------------------------------------------------------------------------- MFMA
+__device__ __forceinline__ f4 mfma16(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// ----------------------------------------------------------------------------- rate model
+// Packed per-channel BitEstimator parameters, rows of C floats:
+//   0..2  softplus(h1), b1, tanh(a1)     3..5  layer 2     6..8  layer 3
+//   9,10  softplus(h4), b4
+constexpr int kRateRows = 11;
+
+__device__ __forceinline__ float bitparm_cdf(float v, const float* __restrict__ rp, int C, int c) {
+  // models/bitEstimator.py:20-25, evaluated as the reference's separate fp32 ops
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float sp = rp[(3 * k + 0) * C + c];
+    const float bb = rp[(3 * k + 1) * C + c];
+    const float ta = rp[(3 * k + 2) * C + c];
+    const float t = v * sp + bb;          // x * softplus(h) + b
+    v = t + tanhf(t) * ta;                // x + tanh(x) * tanh(a)
+  }
+  const float t = v * rp[9 * C + c] + rp[10 * C + c];
+  return 1.0f / (1.0f + expf(-t));        // torch.sigmoid
+}
+
+// model.py:71-73 per element: clamp(-log(F(z+.5) - F(z-.5) + 1e-10) / ln 2, 0, 50)
+__device__ __forceinline__ float element_bits(float z, const float* __restrict__ rp, int C, int c) {
+  const float hi = bitparm_cdf(z + 0.5f, rp, C, c);
+  const float lo = bitparm_cdf(z - 0.5f, rp, C, c);
+  const float prob = hi - lo;
+  float bits = (-1.0f * logf(prob + 1e-10f)) / 0.693147182464599609375f;  // float(math.log(2))
+  bits = fminf(fmaxf(bits, 0.0f), 50.0f);
+  return bits;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+}  // namespace iclr17

@@ -1,0 +1,947 @@
+// Implicit-GEMM convolution engine for the Ballé-2017 codec on gfx950 (fp32 parity mode).
+//
+// One engine covers every layer of the hot path:
+//   analysis  conv2/conv3 (k5 s2 p2)            — forward conv, 25 taps, base grid = output grid
+//   synthesis deconv1/deconv2 (k5 s2 p2 op1)    — stride-phase decomposition: 4 dense sub-convs
+//                                                 (3×3 / 3×2 / 2×3 / 2×2 taps), no zero insertion
+//   synthesis deconv3 (k9 s4 p4 op3, N→3)       — "all-phase" GEMM: the 16 output phases × 3
+//                                                 channels share one 3×3 input neighbourhood, so
+//                                                 they form a dense N = 48 GEMM (K = 9·N)
+//   analysis  conv1 (3→N, k9 s4)                — own A-loader (NCHW patch staged in LDS, K = 243)
+//
+// Tile: 64 output pixels (an 8×8 block of the base grid) × BN output channels per 256-thread
+// workgroup (4 waves). GEMM mapping: M = pixels, N = output channels, K = (tap, input channel).
+// MFMA: v_mfma_f32_16x16x4_f32 (exact f32). A fragments come from an LDS tile (double
+// buffered, register staged so out-of-image taps become zeros); B fragments (packed weights,
+// [tap][Cin/4][Cout][4]) are read straight from L2 into registers, one step ahead — with the
+// waves split along N no two waves share a B fragment, so B never touches LDS.
+//
+// "float4 k-trick": a lane loads 4 consecutive input channels of its pixel with one 16-byte
+// read and feeds them to 4 successive MFMAs; MFMA e of a 16-deep k-block therefore covers
+// channels {16kb + 4g + e : g = 0..3}. The weight packing [Cin/4][Cout][4] makes the matching B
+// fragment a 16-byte read as well.
+//
+// Epilogues are fused: bias + GDN/IGDN (a second channel-contraction GEMM over an LDS x² tile
+// and the packed γ, then x/√n or x·√n), conv3's quantiser + factorised rate (per-tile bit sums),
+// and deconv3's bias + clamp (+ per-tile SSE against the input image). Outputs leave through
+// LDS as coalesced 16-byte row stores.
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "common.h"
+
+namespace iclr17 {
+
+constexpr int BM = 64;        // output pixels per tile
+constexpr int KC = 32;        // input channels per k-step
+constexpr int ASTR = KC + 4;  // LDS row stride of the A tile (floats)
+
+enum Epi : int { EPI_GDN = 0, EPI_IGDN = 1, EPI_QUANT = 2, EPI_OUT3 = 3, EPI_PLAIN = 4 };
+
+struct TapTable {
+  int npx;            // phases along x
+  int nph;            // total phases
+  int begin[17];      // taps of phase p: [begin[p], begin[p+1])
+  signed char dy[64];
+  signed char dx[64];
+};
+
+struct EngineArgs {
+  const float* in;      // NHWC [B][Hin][Win][CI]   (conv1: NCHW image)
+  const float* w;       // packed weights
+  const float* bias;    // [CO] or nullptr
+  const float* gbeta;   // GDN effective beta [CO]
+  const float* ggamma;  // GDN effective gamma, packed [CO/4][CO][4]
+  float* out;           // NHWC [B][Hout][Wout][CO]   (deconv3: clipped NCHW image)
+  float* pre;           // optional pre-activation output (same layout as out)
+  int B, Hin, Win, Hout, Wout;
+  int gh, gw;           // base grid per phase
+  int tiles_x, tiles_y;
+  int sin, sout;        // input / output stride applied to base coordinates
+  TapTable tt;
+  // conv3 quantiser + rate
+  int qmode;
+  const float* noise;   // NCHW [B][CO][Hout][Wout]
+  const float* rate;    // packed [11][CO]
+  float* yhat;          // NHWC
+  double* partial;      // per-tile partial sums
+  int partials_per_image;
+  // deconv3
+  const float* xref;    // NCHW input image (SSE) or nullptr
+  float* recon;         // unclipped NCHW or nullptr
+};
+
+struct TileInfo {
+  int b, ty, tx, py, px, nb;
+};
+
+__device__ __forceinline__ TileInfo decode_tile(const EngineArgs& a) {
+  TileInfo t;
+  int bid = blockIdx.x;
+  t.tx = bid % a.tiles_x;
+  bid /= a.tiles_x;
+  t.ty = bid % a.tiles_y;
+  bid /= a.tiles_y;
+  const int ph = bid % a.tt.nph;
+  t.b = bid / a.tt.nph;
+  t.py = ph / a.tt.npx;
+  t.px = ph % a.tt.npx;
+  t.nb = blockIdx.y;
+  return t;
+}
+
+// Row m of a tile → output pixel (NHWC row offset in pixels) or -1 when outside the grid.
+__device__ __forceinline__ long out_pixel(const EngineArgs& a, const TileInfo& t, int m) {
+  const int gy = t.ty * 8 + (m >> 3), gx = t.tx * 8 + (m & 7);
+  if (gy >= a.gh || gx >= a.gw) return -1;
+  const int oy = gy * a.sout + t.py, ox = gx * a.sout + t.px;
+  return ((long)t.b * a.Hout + oy) * a.Wout + ox;
+}
+
+// Store a [BM][BN] tile held in LDS (row stride ld) to NHWC rows of CO floats at column
+// offset col0, 16 bytes per lane, rows outside the grid skipped.
+template <int BN>
+__device__ __forceinline__ void store_tile_rows(const EngineArgs& a, const TileInfo& t,
+                                                const float* s, int ld, float* dst, int CO,
+                                                int col0) {
+  constexpr int C4 = BN / 4;
+  for (int idx = threadIdx.x; idx < BM * C4; idx += 256) {
+    const int m = idx / C4, c4 = idx % C4;
+    const long p = out_pixel(a, t, m);
+    if (p < 0) continue;
+    const f4 v = *(const f4*)(s + m * ld + c4 * 4);
+    *(f4*)(dst + p * CO + col0 + c4 * 4) = v;
+  }
+}
+
+// Load the B fragments of one 32-deep k-step: packed weights [.][CIq][CO][4], quad rows
+// q0 .. q0+7, columns ncol0 + nt*16 + (lane & 15).
+template <int NT, int CO>
+__device__ __forceinline__ void load_bfrag(f4 (&bf)[2][NT], const float* __restrict__ wp, int q0,
+                                           int ncol0, int lane) {
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int q = q0 + kk * 4 + (lane >> 4);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int n = ncol0 + nt * 16 + (lane & 15);
+      bf[kk][nt] = *(const f4*)(wp + ((long)q * CO + n) * 4);
+    }
+  }
+}
+
+template <int MT, int NT>
+__device__ __forceinline__ void mfma_block(f4 (&acc)[MT][NT], const f4 (&af)[MT], const f4 (&bf)[NT]) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16(af[mt][e], bf[nt][e], acc[mt][nt]);
+}
+
+// ----------------------------------------------------------------------------- GDN epilogue
+// x (bias already added) in accumulator layout → GDN(x) (or IGDN) left in LDS sX[BM][CO+4].
+// models/GDN.py:83-90: n = conv2d(x², γ, β) = β + Σ_j γ[i][j]·x_j²;  y = x / √n | x·√n.
+// The caller guarantees smem is free on entry; on return every wave has passed a barrier after
+// the last sX write.
+template <int CO, int MT, int NT, bool INVERSE>
+__device__ __forceinline__ void gdn_core(const f4 (&x)[MT][NT], float* sX,
+                                         const float* __restrict__ gbeta,
+                                         const float* __restrict__ gp, int wm, int ncol0,
+                                         int lane) {
+  constexpr int XS = CO + 4;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * MT * 16 + mt * 16 + 4 * (lane >> 4) + r;
+        const int col = ncol0 + nt * 16 + (lane & 15);
+        const float v = x[mt][nt][r];
+        sX[row * XS + col] = v * v;
+      }
+  __syncthreads();
+  f4 nacc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) nacc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
+  f4 g[NT], gn[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+    g[nt] = *(const f4*)(gp + ((long)(lane >> 4) * CO + ncol0 + nt * 16 + (lane & 15)) * 4);
+  constexpr int KB = CO / 16;
+  for (int kb = 0; kb < KB; ++kb) {
+    if (kb + 1 < KB) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        gn[nt] = *(const f4*)(gp + ((long)((kb + 1) * 4 + (lane >> 4)) * CO + ncol0 + nt * 16 +
+                                    (lane & 15)) * 4);
+    }
+    f4 af[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+      af[mt] = *(const f4*)(sX + (wm * MT * 16 + mt * 16 + (lane & 15)) * XS + kb * 16 +
+                            4 * (lane >> 4));
+    mfma_block<MT, NT>(nacc, af, g);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) g[nt] = gn[nt];
+  }
+  __syncthreads();  // all reads of x² done
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * MT * 16 + mt * 16 + 4 * (lane >> 4) + r;
+        const int col = ncol0 + nt * 16 + (lane & 15);
+        const float n = nacc[mt][nt][r] + gbeta[col];
+        const float s = sqrtf(n);
+        sX[row * XS + col] = INVERSE ? x[mt][nt][r] * s : x[mt][nt][r] / s;
+      }
+  __syncthreads();
+}
+
+// Accumulator-layout values → LDS tile [BM][ld] (caller synchronises).
+template <int MT, int NT>
+__device__ __forceinline__ void acc_to_lds(const f4 (&v)[MT][NT], float* s, int ld, int wm,
+                                           int col0, int lane) {
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * MT * 16 + mt * 16 + 4 * (lane >> 4) + r;
+        s[row * ld + col0 + nt * 16 + (lane & 15)] = v[mt][nt][r];
+      }
+}
+
+template <int CO, int MT, int NT, bool INVERSE>
+__device__ __forceinline__ void gdn_epilogue(f4 (&x)[MT][NT], float* smem, const EngineArgs& a,
+                                             const TileInfo& t, int wm, int ncol0, int lane) {
+  constexpr int XS = CO + 4;
+  gdn_core<CO, MT, NT, INVERSE>(x, smem, a.gbeta, a.ggamma, wm, ncol0, lane);
+  store_tile_rows<CO>(a, t, smem, XS, a.out, CO, 0);
+  if (a.pre != nullptr) {
+    __syncthreads();
+    acc_to_lds<MT, NT>(x, smem, XS, wm, ncol0, lane);
+    __syncthreads();
+    store_tile_rows<CO>(a, t, smem, XS, a.pre, CO, 0);
+  }
+}
+
+// ------------------------------------------------------------------- quantiser + rate epilogue
+// model.py:48-56 (ŷ = round(y) | y + noise) and model.py:71-73 (bits per element), summed per
+// tile; y and ŷ stored NHWC.
+template <int CO, int BN, int MT, int NT, int WN>
+__device__ __forceinline__ void quant_epilogue(f4 (&acc)[MT][NT], float* smem, const EngineArgs& a,
+                                               const TileInfo& t, int wm, int ncol0, int lane,
+                                               int wave) {
+  constexpr int OS = BN + 4;
+  float* sO = smem;
+  float bits = 0.f;
+  const int cbase = t.nb * BN;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * MT * 16 + mt * 16 + 4 * (lane >> 4) + r;
+        const int lcol = ncol0 - cbase + nt * 16 + (lane & 15);
+        const int col = cbase + lcol;
+        const int gy = t.ty * 8 + (row >> 3), gx = t.tx * 8 + (row & 7);
+        const bool ok = gy < a.gh && gx < a.gw;
+        const float y = acc[mt][nt][r];
+        float yh;
+        if (a.qmode == ICLR17_QUANT_ROUND) {
+          yh = rintf(y);
+        } else {
+          const float u = ok ? a.noise[(((long)t.b * CO + col) * a.Hout + gy) * a.Wout + gx] : 0.f;
+          yh = y + u;
+        }
+        if (ok) bits += element_bits(yh, a.rate, CO, col);
+        sO[row * OS + lcol] = yh;
+      }
+  __syncthreads();
+  store_tile_rows<BN>(a, t, sO, OS, a.yhat, CO, cbase);
+  if (a.out != nullptr) {
+    __syncthreads();
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * MT * 16 + mt * 16 + 4 * (lane >> 4) + r;
+          const int lcol = ncol0 - cbase + nt * 16 + (lane & 15);
+          sO[row * OS + lcol] = acc[mt][nt][r];
+        }
+    __syncthreads();
+    store_tile_rows<BN>(a, t, sO, OS, a.out, CO, cbase);
+  }
+  // deterministic tile sum: lanes → wave (xor tree) → waves in order
+  bits = wave_sum(bits);
+  __syncthreads();
+  if (lane == 0) sO[wave] = bits;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int w = 0; w < 4; ++w) s += (double)sO[w];
+    const int tile = (t.ty * a.tiles_x + t.tx) * gridDim.y + t.nb;
+    a.partial[(long)t.b * a.partials_per_image + tile] = s;
+  }
+}
+
+// --------------------------------------------------------------- deconv3 (all-phase) epilogue
+// Column n = co*16 + ry*4 + rx; row m = base pixel q (8×8 block). Output pixel
+// (4·qy + ry, 4·qx + rx) of channel co. synthesis_17.py:23 + model.py:59 clamp(0, 1).
+template <int MT, int NT>
+__device__ __forceinline__ void out3_epilogue(f4 (&acc)[MT][NT], float* smem, const EngineArgs& a,
+                                              const TileInfo& t, int wm, int lane, int wave) {
+  constexpr int SS = 33;  // padded row of the 32×32 output block
+  float* sO = smem;       // [3][32][33]
+  const int H = a.Hout, W = a.Wout;  // image dims
+  float vals[MT][NT][4];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) vals[mt][nt][r] = acc[mt][nt][r] + a.bias[nt];
+  float sse = 0.f;
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass == 1 && a.recon == nullptr) break;
+    float* dst = pass == 0 ? a.out : a.recon;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = wm * MT * 16 + mt * 16 + 4 * (lane >> 4) + r;
+          const int ph = lane & 15;
+          const int oyl = (m >> 3) * 4 + (ph >> 2), oxl = (m & 7) * 4 + (ph & 3);
+          float v = vals[mt][nt][r];
+          if (pass == 0) v = fminf(fmaxf(v, 0.0f), 1.0f);
+          sO[(nt * 32 + oyl) * SS + oxl] = v;
+        }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < 3 * 32 * 8; idx += 256) {
+      const int c4 = idx & 7, row = (idx >> 3) & 31, co = idx >> 8;
+      const int oy = t.ty * 32 + row, ox = t.tx * 32 + c4 * 4;
+      if (oy >= H || ox >= W) continue;
+      const float* s = sO + (co * 32 + row) * SS + c4 * 4;
+      const f4 v = f4{s[0], s[1], s[2], s[3]};
+      const long off = (((long)t.b * 3 + co) * H + oy) * W + ox;
+      *(f4*)(dst + off) = v;
+      if (pass == 0 && a.xref != nullptr) {
+        const f4 xr = *(const f4*)(a.xref + off);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = v[e] - xr[e];
+          sse += d * d;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (a.xref != nullptr) {
+    sse = wave_sum(sse);
+    if (lane == 0) sO[wave] = sse;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s = 0.0;
+      for (int w = 0; w < 4; ++w) s += (double)sO[w];
+      a.partial[(long)t.b * a.partials_per_image + t.ty * a.tiles_x + t.tx] = s;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------- the engine kernel
+template <int CI, int CO, int BN, int WM, int WN, int EPI>
+__global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
+  constexpr int MT = BM / WM / 16;
+  constexpr int NT = BN / WN / 16;
+  constexpr int NCH = CI / KC;
+  constexpr int LDS_A = 2 * BM * ASTR;
+  constexpr int LDS_X = (EPI == EPI_GDN || EPI == EPI_IGDN) ? BM * (CO + 4) : 0;
+  constexpr int LDS_O = BM * (BN + 4) + 8;
+  constexpr int LDS_3 = 3 * 32 * 33 + 8;
+  constexpr int L1 = LDS_A > LDS_X ? LDS_A : LDS_X;
+  constexpr int L2 = LDS_O > LDS_3 ? LDS_O : LDS_3;
+  constexpr int LDS_FLOATS = L1 > L2 ? L1 : L2;
+  static_assert(MT * WM * 16 == BM && NT * WN * 16 == BN, "tile shape");
+  static_assert(WM * WN == 4, "4 waves");
+  __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const TileInfo t = decode_tile(a);
+  const int ph = t.py * a.tt.npx + t.px;
+  const int t0 = a.tt.begin[ph];
+  const int nsteps = (a.tt.begin[ph + 1] - t0) * NCH;
+  const int ncol0 = t.nb * BN + wn * (BN / WN);
+
+  // A staging assignment: 2 float4 per thread, row = idx>>3, 16-byte column c4 = idx&7
+  int sgy[2], sgx[2], soff[2];
+  bool sval[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = tid + 256 * i;
+    const int row = idx >> 3;
+    sgy[i] = t.ty * 8 + (row >> 3);
+    sgx[i] = t.tx * 8 + (row & 7);
+    sval[i] = sgy[i] < a.gh && sgx[i] < a.gw;
+    soff[i] = row * ASTR + (idx & 7) * 4;
+    sgy[i] *= a.sin;
+    sgx[i] *= a.sin;
+  }
+  const float* __restrict__ inb = a.in + (long)t.b * a.Hin * a.Win * CI + (tid & 7) * 4;
+
+  auto load_a = [&](int s, f4 (&r)[2]) {
+    const int tap = t0 + s / NCH, cc = s - (s / NCH) * NCH;
+    const int dy = a.tt.dy[tap], dx = a.tt.dx[tap];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int iy = sgy[i] + dy, ix = sgx[i] + dx;
+      const bool ok = sval[i] && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
+      r[i] = ok ? *(const f4*)(inb + ((long)iy * a.Win + ix) * CI + cc * KC) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto load_b = [&](int s, f4 (&bf)[2][NT]) {
+    const int tap = t0 + s / NCH, cc = s - (s / NCH) * NCH;
+    load_bfrag<NT, CO>(bf, a.w + (long)tap * CI * CO, cc * 8, ncol0, lane);
+  };
+
+  f4 acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
+
+  f4 ra[2];
+  f4 bcur[2][NT], bnxt[2][NT];
+  load_a(0, ra);
+  load_b(0, bcur);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) *(f4*)(smem + soff[i]) = ra[i];
+  __syncthreads();
+
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    const bool more = s + 1 < nsteps;
+    if (more) {
+      load_a(s + 1, ra);
+      load_b(s + 1, bnxt);
+    }
+    const float* As = smem + cur * BM * ASTR;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      f4 af[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        af[mt] = *(const f4*)(As + (wm * MT * 16 + mt * 16 + (lane & 15)) * ASTR + kk * 16 +
+                              4 * (lane >> 4));
+      mfma_block<MT, NT>(acc, af, bcur[kk]);
+    }
+    if (more) {
+      float* An = smem + (cur ^ 1) * BM * ASTR;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) *(f4*)(An + soff[i]) = ra[i];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) bcur[kk][nt] = bnxt[kk][nt];
+    }
+    __syncthreads();
+  }
+
+  if constexpr (EPI == EPI_GDN || EPI == EPI_IGDN) {
+    static_assert(BN == CO, "GDN fusion needs every channel of a pixel in the workgroup");
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[mt][nt][r] += a.bias[ncol0 + nt * 16 + (lane & 15)];
+    gdn_epilogue<CO, MT, NT, EPI == EPI_IGDN>(acc, smem, a, t, wm, ncol0, lane);
+  } else if constexpr (EPI == EPI_QUANT) {
+    quant_epilogue<CO, BN, MT, NT, WN>(acc, smem, a, t, wm, ncol0, lane, wave);
+  } else if constexpr (EPI == EPI_OUT3) {
+    out3_epilogue<MT, NT>(acc, smem, a, t, wm, lane, wave);
+  } else {
+    constexpr int OS = BN + 4;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * MT * 16 + mt * 16 + 4 * (lane >> 4) + r;
+          const int lcol = wn * (BN / WN) + nt * 16 + (lane & 15);
+          float v = acc[mt][nt][r];
+          if (a.bias != nullptr) v += a.bias[t.nb * BN + lcol];
+          smem[row * OS + lcol] = v;
+        }
+    __syncthreads();
+    store_tile_rows<BN>(a, t, smem, OS, a.out, CO, t.nb * BN);
+  }
+}
+
+// ------------------------------------------------------------------------------ conv1 kernel
+// Conv2d(3, N, 9, stride 4, pad 4) on the NCHW image with GDN fused. The 37×37×3 input patch of
+// an 8×8 output block is staged once in LDS; K = 243 = (c, kh, kw) padded to 256, each A element
+// gathered from the patch through a k → offset table (k ≥ 243 reads a zero slot).
+constexpr int P1 = 37;                    // patch side: 8·4 + 9 − 4
+constexpr int P1PLANE = P1 * P1;
+constexpr int P1ZERO = 3 * P1PLANE;       // index of the zero slot
+
+template <int CO, bool INVERSE_UNUSED = false>
+__global__ void __launch_bounds__(256) conv1_gdn_kernel(const EngineArgs a) {
+  constexpr int WN = 4;
+  constexpr int MT = BM / 16;
+  constexpr int NT = CO / WN / 16;
+  constexpr int LDS_P = P1ZERO + 1 + 256 + 64 + 3;  // patch + zero + k table + m table
+  constexpr int LDS_X = BM * (CO + 4);
+  constexpr int LDS_FLOATS = LDS_P > LDS_X ? LDS_P : LDS_X;
+  __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
+  int* ktab = (int*)(smem + P1ZERO + 4);
+  int* mtab = ktab + 256;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = 0, wn = wave;
+  const TileInfo t = decode_tile(a);
+  const int ncol0 = wn * (CO / WN);
+  const int H = a.Hin, W = a.Win;
+  const int iy0 = t.ty * 32 - 4, ix0 = t.tx * 32 - 4;
+
+  // B fragments of step 0 early (global latency overlaps the patch staging)
+  f4 bcur[2][NT], bnxt[2][NT];
+  load_bfrag<NT, CO>(bcur, a.w, 0, ncol0, lane);
+
+  for (int idx = tid; idx < 3 * P1PLANE; idx += 256) {
+    const int c = idx / P1PLANE, rem = idx - c * P1PLANE;
+    const int r = rem / P1, col = rem - r * P1;
+    const int iy = iy0 + r, ix = ix0 + col;
+    float v = 0.f;
+    if (iy >= 0 && iy < H && ix >= 0 && ix < W) v = a.in[(((long)t.b * 3 + c) * H + iy) * W + ix];
+    smem[idx] = v;
+  }
+  if (tid == 0) smem[P1ZERO] = 0.f;
+  {
+    const int k = tid;  // 256 threads ↔ 256 k values
+    int off = P1ZERO;
+    if (k < 243) {
+      const int c = k / 81, kh = (k % 81) / 9, kw = k % 9;
+      off = c * P1PLANE + kh * P1 + kw;
+    }
+    ktab[k] = off;
+    if (tid < 64) mtab[tid] = (tid >> 3) * 4 * P1 + (tid & 7) * 4;
+  }
+  __syncthreads();
+
+  f4 acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
+
+  int moff[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) moff[mt] = mtab[mt * 16 + (lane & 15)];
+
+  for (int s = 0; s < 8; ++s) {
+    if (s + 1 < 8) load_bfrag<NT, CO>(bnxt, a.w, (s + 1) * 8, ncol0, lane);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int kbase = s * 32 + kk * 16 + 4 * (lane >> 4);
+      int ko[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ko[e] = ktab[kbase + e];
+      f4 af[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int o = ko[e] == P1ZERO ? P1ZERO : ko[e] + moff[mt];
+          af[mt][e] = smem[o];
+        }
+      mfma_block<MT, NT>(acc, af, bcur[kk]);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) bcur[kk][nt] = bnxt[kk][nt];
+  }
+  __syncthreads();  // patch reads done before the epilogue reuses LDS
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[mt][nt][r] += a.bias[ncol0 + nt * 16 + (lane & 15)];
+  gdn_epilogue<CO, MT, NT, false>(acc, smem, a, t, wm, ncol0, lane);
+}
+
+// --------------------------------------------------------------------- stand-alone GDN / IGDN
+// GDN.forward (models/GDN.py:64-94) on a [B,C,H,W] tensor stored NCHW or NHWC: 64 pixels of one
+// image per workgroup (linear pixel order), all C channels, the same fused core as the layers.
+template <int C, bool INVERSE, int LAYOUT>
+__global__ void __launch_bounds__(256) gdn_kernel(const float* __restrict__ x, int HW,
+                                                  const float* __restrict__ beta,
+                                                  const float* __restrict__ gp, float* y) {
+  constexpr int XS = C + 4;
+  constexpr int WN = 4, MT = 4, NT = C / WN / 16;
+  __shared__ __attribute__((aligned(16))) float smem[BM * XS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles = (HW + BM - 1) / BM;
+  const int b = blockIdx.x / tiles, p0 = (blockIdx.x % tiles) * BM;
+  const int np = HW - p0 < BM ? HW - p0 : BM;
+  const int ncol0 = wave * (C / WN);
+  if constexpr (LAYOUT == ICLR17_LAYOUT_NCHW) {
+    for (int idx = tid; idx < BM * C; idx += 256) {
+      const int c = idx / BM, pl = idx % BM;
+      smem[pl * XS + c] = pl < np ? x[((long)b * C + c) * HW + p0 + pl] : 0.f;
+    }
+  } else {
+    for (int idx = tid; idx < BM * (C / 4); idx += 256) {
+      const int pl = idx / (C / 4), c4 = idx % (C / 4);
+      const f4 v = pl < np ? *(const f4*)(x + ((long)b * HW + p0 + pl) * C + c4 * 4) : f4{0.f, 0.f, 0.f, 0.f};
+      *(f4*)(smem + pl * XS + c4 * 4) = v;
+    }
+  }
+  __syncthreads();
+  f4 v[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        v[mt][nt][r] = smem[(mt * 16 + 4 * (lane >> 4) + r) * XS + ncol0 + nt * 16 + (lane & 15)];
+  __syncthreads();
+  gdn_core<C, MT, NT, INVERSE>(v, smem, beta, gp, 0, ncol0, lane);
+  if constexpr (LAYOUT == ICLR17_LAYOUT_NCHW) {
+    for (int idx = tid; idx < BM * C; idx += 256) {
+      const int c = idx / BM, pl = idx % BM;
+      if (pl < np) y[((long)b * C + c) * HW + p0 + pl] = smem[pl * XS + c];
+    }
+  } else {
+    for (int idx = tid; idx < BM * (C / 4); idx += 256) {
+      const int pl = idx / (C / 4), c4 = idx % (C / 4);
+      if (pl < np) *(f4*)(y + ((long)b * HW + p0 + pl) * C + c4 * 4) = *(const f4*)(smem + pl * XS + c4 * 4);
+    }
+  }
+}
+
+// ====================================================================================== host
+namespace {
+
+thread_local char g_err[512];
+
+int check_dims(int B, int H, int W, int N) {
+  ICLR17_REQUIRE(B > 0 && H > 0 && W > 0, ICLR17_EINVAL, "bad shape B=%d H=%d W=%d", B, H, W);
+  ICLR17_REQUIRE(H % 16 == 0 && W % 16 == 0, ICLR17_EINVAL,
+                 "image height/width must be multiples of 16 (got %dx%d)", H, W);
+  ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "channel count N=%d unsupported (128, 192)", N);
+  return ICLR17_OK;
+}
+
+void fill_conv5_taps(TapTable& tt) {
+  memset(&tt, 0, sizeof(tt));
+  tt.npx = 1;
+  tt.nph = 1;
+  tt.begin[0] = 0;
+  tt.begin[1] = 25;
+  for (int kh = 0; kh < 5; ++kh)
+    for (int kw = 0; kw < 5; ++kw) {
+      tt.dy[kh * 5 + kw] = (signed char)(kh - 2);
+      tt.dx[kh * 5 + kw] = (signed char)(kw - 2);
+    }
+}
+
+// ConvTranspose2d(k, stride s, pad p): output o = s·q + r receives input q + d through kernel
+// tap k = r + p − s·d (0 ≤ k < K). Phase-major tap order; the packing kernel uses the same order.
+void fill_deconv_taps(TapTable& tt, int K, int s, int p) {
+  memset(&tt, 0, sizeof(tt));
+  tt.npx = s;
+  tt.nph = s * s;
+  int n = 0;
+  for (int ry = 0; ry < s; ++ry)
+    for (int rx = 0; rx < s; ++rx) {
+      tt.begin[ry * s + rx] = n;
+      for (int dy = 2; dy >= -2; --dy) {
+        const int kh = ry + p - s * dy;
+        if (kh < 0 || kh >= K) continue;
+        for (int dx = 2; dx >= -2; --dx) {
+          const int kw = rx + p - s * dx;
+          if (kw < 0 || kw >= K) continue;
+          tt.dy[n] = (signed char)dy;
+          tt.dx[n] = (signed char)dx;
+          ++n;
+        }
+      }
+    }
+  tt.begin[s * s] = n;
+}
+
+void fill_neigh3_taps(TapTable& tt) {
+  memset(&tt, 0, sizeof(tt));
+  tt.npx = 1;
+  tt.nph = 1;
+  tt.begin[1] = 9;
+  for (int i = 0; i < 9; ++i) {
+    tt.dy[i] = (signed char)(i / 3 - 1);
+    tt.dx[i] = (signed char)(i % 3 - 1);
+  }
+}
+
+hipStream_t S(void* s) { return (hipStream_t)s; }
+
+}  // namespace
+
+void set_error(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  int n = snprintf(g_err, sizeof(g_err), "iclr17 error %d: ", code);
+  if (n < 0) n = 0;
+  vsnprintf(g_err + n, sizeof(g_err) - n, fmt, ap);
+  va_end(ap);
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(ICLR17_ELAUNCH, "%s: %s", what, hipGetErrorString(e));
+    return ICLR17_ELAUNCH;
+  }
+  return ICLR17_OK;
+}
+
+// exposed to aux.hip for its launches
+const char* last_error_buf() { return g_err; }
+
+// tap-table helpers shared with the packing code
+void deconv_phase_taps(int K, int s, int p, int ry, int rx, int* kh_out, int* kw_out, int* count) {
+  int n = 0;
+  for (int dy = 2; dy >= -2; --dy) {
+    const int kh = ry + p - s * dy;
+    if (kh < 0 || kh >= K) continue;
+    for (int dx = 2; dx >= -2; --dx) {
+      const int kw = rx + p - s * dx;
+      if (kw < 0 || kw >= K) continue;
+      kh_out[n] = kh;
+      kw_out[n] = kw;
+      ++n;
+    }
+  }
+  *count = n;
+}
+
+template <int N>
+int launch_conv1(const float* x, int B, int H, int W, const float* wp, const float* bias,
+                 const float* beta, const float* gamma, float* out, float* pre, hipStream_t st) {
+  EngineArgs a;
+  memset(&a, 0, sizeof(a));
+  a.in = x; a.w = wp; a.bias = bias; a.gbeta = beta; a.ggamma = gamma; a.out = out; a.pre = pre;
+  a.B = B; a.Hin = H; a.Win = W; a.Hout = H / 4; a.Wout = W / 4;
+  a.gh = H / 4; a.gw = W / 4; a.tiles_y = (a.gh + 7) / 8; a.tiles_x = (a.gw + 7) / 8;
+  a.sin = 4; a.sout = 1;
+  a.tt.npx = 1; a.tt.nph = 1;
+  dim3 grid(a.tiles_x * a.tiles_y * B, 1);
+  hipLaunchKernelGGL((conv1_gdn_kernel<N>), grid, dim3(256), 0, st, a);
+  return check_launch("conv1_gdn");
+}
+
+template <int N, int EPI>
+int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, const float* bias,
+                 const float* beta, const float* gamma, float* out, float* pre, int qmode,
+                 const float* noise, const float* rate, float* yhat, double* partial,
+                 hipStream_t st) {
+  EngineArgs a;
+  memset(&a, 0, sizeof(a));
+  a.in = in; a.w = wp; a.bias = bias; a.gbeta = beta; a.ggamma = gamma; a.out = out; a.pre = pre;
+  a.B = B; a.Hin = Hin; a.Win = Win; a.Hout = Hin / 2; a.Wout = Win / 2;
+  a.gh = a.Hout; a.gw = a.Wout; a.tiles_y = (a.gh + 7) / 8; a.tiles_x = (a.gw + 7) / 8;
+  a.sin = 2; a.sout = 1;
+  fill_conv5_taps(a.tt);
+  a.qmode = qmode; a.noise = noise; a.rate = rate; a.yhat = yhat; a.partial = partial;
+  if constexpr (EPI == EPI_QUANT) {
+    constexpr int BN = 64;
+    a.partials_per_image = a.tiles_x * a.tiles_y * (N / BN);
+    dim3 grid(a.tiles_x * a.tiles_y * B, N / BN);
+    hipLaunchKernelGGL((engine_kernel<N, N, BN, 1, 4, EPI_QUANT>), grid, dim3(256), 0, st, a);
+    return check_launch("conv3_quant_rate");
+  } else if constexpr (EPI == EPI_PLAIN) {
+    constexpr int BN = 64;
+    dim3 grid(a.tiles_x * a.tiles_y * B, N / BN);
+    hipLaunchKernelGGL((engine_kernel<N, N, BN, 1, 4, EPI_PLAIN>), grid, dim3(256), 0, st, a);
+    return check_launch("conv3");
+  } else {
+    dim3 grid(a.tiles_x * a.tiles_y * B, 1);
+    hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI>), grid, dim3(256), 0, st, a);
+    return check_launch("conv2_gdn");
+  }
+}
+
+template <int N>
+int launch_deconv5(const float* in, int B, int h, int w, const float* wp, const float* bias,
+                   const float* beta, const float* gamma, float* out, float* pre, hipStream_t st) {
+  EngineArgs a;
+  memset(&a, 0, sizeof(a));
+  a.in = in; a.w = wp; a.bias = bias; a.gbeta = beta; a.ggamma = gamma; a.out = out; a.pre = pre;
+  a.B = B; a.Hin = h; a.Win = w; a.Hout = 2 * h; a.Wout = 2 * w;
+  a.gh = h; a.gw = w; a.tiles_y = (h + 7) / 8; a.tiles_x = (w + 7) / 8;
+  a.sin = 1; a.sout = 2;
+  fill_deconv_taps(a.tt, 5, 2, 2);
+  dim3 grid(a.tiles_x * a.tiles_y * 4 * B, 1);
+  hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI_IGDN>), grid, dim3(256), 0, st, a);
+  return check_launch("deconv_igdn");
+}
+
+template <int N>
+int launch_deconv3(const float* in, int B, int H, int W, const float* wp, const float* bias,
+                   const float* x, float* clipped, float* recon, double* partial, hipStream_t st) {
+  EngineArgs a;
+  memset(&a, 0, sizeof(a));
+  a.in = in; a.w = wp; a.bias = bias; a.out = clipped; a.recon = recon; a.xref = x;
+  a.partial = partial;
+  a.B = B; a.Hin = H / 4; a.Win = W / 4; a.Hout = H; a.Wout = W;
+  a.gh = H / 4; a.gw = W / 4; a.tiles_y = (a.gh + 7) / 8; a.tiles_x = (a.gw + 7) / 8;
+  a.partials_per_image = a.tiles_x * a.tiles_y;
+  a.sin = 1; a.sout = 4;
+  fill_neigh3_taps(a.tt);
+  dim3 grid(a.tiles_x * a.tiles_y * B, 1);
+  hipLaunchKernelGGL((engine_kernel<N, 48, 48, 4, 1, EPI_OUT3>), grid, dim3(256), 0, st, a);
+  return check_launch("deconv3");
+}
+
+}  // namespace iclr17
+
+using namespace iclr17;
+
+extern "C" {
+
+int iclr17_version(void) { return 1; }
+
+int iclr17_last_error(char* buf, size_t len) {
+  const size_t n = strlen(g_err);
+  if (buf != nullptr && len > 0) {
+    const size_t c = n < len - 1 ? n : len - 1;
+    memcpy(buf, g_err, c);
+    buf[c] = 0;
+  }
+  return (int)n;
+}
+
+int iclr17_analysis_conv1_gdn(const float* x, int B, int H, int W, int N, const float* w_packed,
+                              const float* bias, const float* beta_eff, const float* gamma_packed,
+                              float* out, float* pre_out, void* stream) {
+  int rc = check_dims(B, H, W, N);
+  if (rc) return rc;
+  ICLR17_REQUIRE(x && w_packed && bias && beta_eff && gamma_packed && out, ICLR17_EINVAL,
+                 "conv1_gdn: null pointer");
+  return N == 192 ? launch_conv1<192>(x, B, H, W, w_packed, bias, beta_eff, gamma_packed, out, pre_out, S(stream))
+                  : launch_conv1<128>(x, B, H, W, w_packed, bias, beta_eff, gamma_packed, out, pre_out, S(stream));
+}
+
+int iclr17_analysis_conv2_gdn(const float* in, int B, int H, int W, int N, const float* w_packed,
+                              const float* bias, const float* beta_eff, const float* gamma_packed,
+                              float* out, float* pre_out, void* stream) {
+  int rc = check_dims(B, H, W, N);
+  if (rc) return rc;
+  ICLR17_REQUIRE(in && w_packed && bias && beta_eff && gamma_packed && out, ICLR17_EINVAL,
+                 "conv2_gdn: null pointer");
+  const int h = H / 4, w = W / 4;
+  return N == 192 ? launch_conv5<192, EPI_GDN>(in, B, h, w, w_packed, bias, beta_eff, gamma_packed, out, pre_out, 0, nullptr, nullptr, nullptr, nullptr, S(stream))
+                  : launch_conv5<128, EPI_GDN>(in, B, h, w, w_packed, bias, beta_eff, gamma_packed, out, pre_out, 0, nullptr, nullptr, nullptr, nullptr, S(stream));
+}
+
+int iclr17_rate_partials_per_image(int H, int W, int N) {
+  const int gh = H / 16, gw = W / 16;
+  return ((gh + 7) / 8) * ((gw + 7) / 8) * (N / 64);
+}
+
+int iclr17_analysis_conv3_quant_rate(const float* in, int B, int H, int W, int N,
+                                     const float* w_packed, int quant_mode, const float* noise,
+                                     const float* rate_packed, float* y_out, float* y_hat,
+                                     double* bits_partial, void* stream) {
+  int rc = check_dims(B, H, W, N);
+  if (rc) return rc;
+  ICLR17_REQUIRE(in && w_packed && rate_packed && y_hat && bits_partial, ICLR17_EINVAL,
+                 "conv3_quant_rate: null pointer");
+  ICLR17_REQUIRE(quant_mode == ICLR17_QUANT_ROUND || (quant_mode == ICLR17_QUANT_NOISE && noise),
+                 ICLR17_EINVAL, "conv3_quant_rate: bad quant mode %d / missing noise", quant_mode);
+  const int h = H / 8, w = W / 8;
+  return N == 192 ? launch_conv5<192, EPI_QUANT>(in, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream))
+                  : launch_conv5<128, EPI_QUANT>(in, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream));
+}
+
+int iclr17_analysis_conv3(const float* in, int B, int H, int W, int N, const float* w_packed,
+                          float* y_out, void* stream) {
+  int rc = check_dims(B, H, W, N);
+  if (rc) return rc;
+  ICLR17_REQUIRE(in && w_packed && y_out, ICLR17_EINVAL, "conv3: null pointer");
+  const int h = H / 8, w = W / 8;
+  return N == 192 ? launch_conv5<192, EPI_PLAIN>(in, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, 0, nullptr, nullptr, nullptr, nullptr, S(stream))
+                  : launch_conv5<128, EPI_PLAIN>(in, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, 0, nullptr, nullptr, nullptr, nullptr, S(stream));
+}
+
+int iclr17_synthesis_deconv_igdn(const float* in, int B, int h, int w, int N,
+                                 const float* w_packed, const float* bias, const float* beta_eff,
+                                 const float* gamma_packed, float* out, float* pre_out,
+                                 void* stream) {
+  ICLR17_REQUIRE(B > 0 && h > 0 && w > 0, ICLR17_EINVAL, "deconv_igdn: bad shape");
+  ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "channel count N=%d unsupported", N);
+  ICLR17_REQUIRE(in && w_packed && bias && beta_eff && gamma_packed && out, ICLR17_EINVAL,
+                 "deconv_igdn: null pointer");
+  return N == 192 ? launch_deconv5<192>(in, B, h, w, w_packed, bias, beta_eff, gamma_packed, out, pre_out, S(stream))
+                  : launch_deconv5<128>(in, B, h, w, w_packed, bias, beta_eff, gamma_packed, out, pre_out, S(stream));
+}
+
+int iclr17_output_partials_per_image(int H, int W) {
+  return ((H / 4 + 7) / 8) * ((W / 4 + 7) / 8);
+}
+
+int iclr17_synthesis_deconv3(const float* in, int B, int H, int W, int N, const float* w_packed,
+                             const float* bias, const float* x, float* clipped, float* recon,
+                             double* sse_partial, void* stream) {
+  int rc = check_dims(B, H, W, N);
+  if (rc) return rc;
+  ICLR17_REQUIRE(in && w_packed && bias && clipped, ICLR17_EINVAL, "deconv3: null pointer");
+  ICLR17_REQUIRE(x == nullptr || sse_partial != nullptr, ICLR17_EINVAL,
+                 "deconv3: sse_partial required with x");
+  return N == 192 ? launch_deconv3<192>(in, B, H, W, w_packed, bias, x, clipped, recon, sse_partial, S(stream))
+                  : launch_deconv3<128>(in, B, H, W, w_packed, bias, x, clipped, recon, sse_partial, S(stream));
+}
+
+int iclr17_gdn(const float* x, int B, int C, int H, int W, int layout, int inverse,
+               const float* beta_eff, const float* gamma_packed, float* y, void* stream) {
+  ICLR17_REQUIRE(B > 0 && H > 0 && W > 0, ICLR17_EINVAL, "gdn: bad shape");
+  ICLR17_REQUIRE(C == 128 || C == 192, ICLR17_EUNSUPPORTED, "gdn: C=%d unsupported (128, 192)", C);
+  ICLR17_REQUIRE(layout == ICLR17_LAYOUT_NCHW || layout == ICLR17_LAYOUT_NHWC, ICLR17_EINVAL,
+                 "gdn: bad layout %d", layout);
+  ICLR17_REQUIRE(x && beta_eff && gamma_packed && y, ICLR17_EINVAL, "gdn: null pointer");
+  const int HW = H * W;
+  dim3 grid(B * ((HW + BM - 1) / BM));
+  hipStream_t st = S(stream);
+#define ICLR17_GDN_LAUNCH(CC, INV, LAY) \
+  hipLaunchKernelGGL((gdn_kernel<CC, INV, LAY>), grid, dim3(256), 0, st, x, HW, beta_eff, gamma_packed, y)
+  if (C == 192) {
+    if (inverse) { if (layout == ICLR17_LAYOUT_NCHW) ICLR17_GDN_LAUNCH(192, true, 0); else ICLR17_GDN_LAUNCH(192, true, 1); }
+    else { if (layout == ICLR17_LAYOUT_NCHW) ICLR17_GDN_LAUNCH(192, false, 0); else ICLR17_GDN_LAUNCH(192, false, 1); }
+  } else {
+    if (inverse) { if (layout == ICLR17_LAYOUT_NCHW) ICLR17_GDN_LAUNCH(128, true, 0); else ICLR17_GDN_LAUNCH(128, true, 1); }
+    else { if (layout == ICLR17_LAYOUT_NCHW) ICLR17_GDN_LAUNCH(128, false, 0); else ICLR17_GDN_LAUNCH(128, false, 1); }
+  }
+#undef ICLR17_GDN_LAUNCH
+  return check_launch("gdn");
+}
+
+}  // extern "C"

@@ -1,0 +1,305 @@
+"""Tensor-level wrappers over the C ABI (include/iclr17.h).
+
+Each function validates shapes / dtypes / devices, allocates outputs with PyTorch's caching
+allocator, and enqueues the HIP kernel on the current stream of the tensors' device. There
+is no CPU path: a non-GPU tensor raises.
+
+Activations between layers are NHWC tensors (shape [B, h, w, N], contiguous); the image and
+the reconstruction are NCHW. Parameters stay in their reference (NCHW / PyTorch) layout and
+are packed into kernel layouts by the ``pack_*`` helpers (derived caches).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import Iclr17Error, call, query
+
+Tensor = torch.Tensor
+
+# models/GDN.py:46-49 default bounds as the fp32 values ones_like(x) * bound produces
+DEFAULT_BETA_BOUND = float(np.float32((1e-6 + 2.0 ** -36) ** 0.5))
+DEFAULT_GAMMA_BOUND = float(np.float32(2.0 ** -18))
+DEFAULT_PEDESTAL = float(np.float32(2.0 ** -36))
+
+
+def _check(t: Tensor, name: str, ndim: Optional[int] = None) -> None:
+    if not isinstance(t, torch.Tensor):
+        raise Iclr17Error(f"iclr17: {name} must be a torch.Tensor")
+    if t.device.type != "cuda":
+        raise Iclr17Error(
+            f"iclr17: {name} is on {t.device}; this framework runs only on a ROCm GPU "
+            "(MI355X / gfx950) — there is no CPU implementation")
+    if t.dtype != torch.float32:
+        raise Iclr17Error(f"iclr17: {name} must be float32 (got {t.dtype})")
+    if ndim is not None and t.dim() != ndim:
+        raise Iclr17Error(f"iclr17: {name} must be {ndim}-D (got shape {tuple(t.shape)})")
+
+
+def _p(t: Optional[Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(t: Tensor):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _check_image_dims(H: int, W: int) -> None:
+    if H <= 0 or W <= 0 or H % 16 or W % 16:
+        raise Iclr17Error(f"iclr17: image height/width must be positive multiples of 16, got {H}x{W} "
+                          "(model.py:48 builds the latent grid with //16; crop first)")
+
+
+def _check_channels(N: int) -> None:
+    if N not in (128, 192):
+        raise Iclr17Error(f"iclr17: channel count N={N} unsupported (kernels are built for 128 and 192)")
+
+
+# ------------------------------------------------------------------------------ packing
+def pack_weight(which: int, w: Tensor, N: int) -> Tensor:
+    _check(w, "weight", 4)
+    w = w.detach().contiguous()
+    size = query("iclr17_packed_weight_size", which, N)
+    out = torch.empty(size, device=w.device, dtype=torch.float32)
+    call("iclr17_pack_weight", which, _p(w), _p(out), N, _stream(w))
+    return out
+
+
+def pack_gdn(beta: Tensor, gamma: Tensor, beta_bound: float = DEFAULT_BETA_BOUND,
+             gamma_bound: float = DEFAULT_GAMMA_BOUND,
+             pedestal: float = DEFAULT_PEDESTAL) -> Tuple[Tensor, Tensor]:
+    _check(beta, "beta", 1)
+    _check(gamma, "gamma", 2)
+    C = beta.shape[0]
+    if tuple(gamma.shape) != (C, C):
+        raise Iclr17Error(f"iclr17: gamma must be [{C},{C}] (got {tuple(gamma.shape)})")
+    beta = beta.detach().contiguous()
+    gamma = gamma.detach().contiguous()
+    beta_eff = torch.empty(C, device=beta.device, dtype=torch.float32)
+    gp = torch.empty(C * C, device=beta.device, dtype=torch.float32)
+    call("iclr17_pack_gdn", _p(beta), _p(gamma), _p(beta_eff), _p(gp), C,
+         ctypes.c_float(beta_bound), ctypes.c_float(gamma_bound), ctypes.c_float(pedestal),
+         _stream(beta))
+    return beta_eff, gp
+
+
+def pack_rate(params: Sequence[Tensor]) -> Tensor:
+    """params: h1 b1 a1 h2 b2 a2 h3 b3 a3 h4 b4 (each (1,C,1,1) or (C,))."""
+    if len(params) != 11:
+        raise Iclr17Error("iclr17: pack_rate needs 11 parameter tensors")
+    ps = [p.detach().reshape(-1).contiguous() for p in params]
+    for i, p in enumerate(ps):
+        _check(p, f"rate param {i}")
+    C = ps[0].numel()
+    out = torch.empty(11 * C, device=ps[0].device, dtype=torch.float32)
+    call("iclr17_pack_rate", *[_p(p) for p in ps], _p(out), C, _stream(ps[0]))
+    return out
+
+
+# ------------------------------------------------------------------------------ layers
+def conv1_gdn(x: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Tensor, N: int,
+              want_pre: bool = False):
+    """analysis_17.py:14-17,33: x NCHW [B,3,H,W] → NHWC [B,H/4,W/4,N] (+ pre-GDN)."""
+    _check(x, "image", 4)
+    B, C, H, W = x.shape
+    if C != 3:
+        raise Iclr17Error(f"iclr17: the analysis transform takes 3-channel images (got {C})")
+    _check_image_dims(H, W)
+    _check_channels(N)
+    x = x.contiguous()
+    out = torch.empty(B, H // 4, W // 4, N, device=x.device, dtype=torch.float32)
+    pre = torch.empty_like(out) if want_pre else None
+    call("iclr17_analysis_conv1_gdn", _p(x), B, H, W, N, _p(wp), _p(bias), _p(beta_eff), _p(gp),
+         _p(out), _p(pre), _stream(x))
+    return (out, pre) if want_pre else out
+
+
+def conv2_gdn(h: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Tensor,
+              want_pre: bool = False):
+    """analysis_17.py:18-21,34: NHWC [B,H/4,W/4,N] → [B,H/8,W/8,N]."""
+    _check(h, "activation", 4)
+    B, h4, w4, N = h.shape
+    _check_channels(N)
+    H, W = 4 * h4, 4 * w4
+    _check_image_dims(H, W)
+    out = torch.empty(B, h4 // 2, w4 // 2, N, device=h.device, dtype=torch.float32)
+    pre = torch.empty_like(out) if want_pre else None
+    call("iclr17_analysis_conv2_gdn", _p(h.contiguous()), B, H, W, N, _p(wp), _p(bias),
+         _p(beta_eff), _p(gp), _p(out), _p(pre), _stream(h))
+    return (out, pre) if want_pre else out
+
+
+def conv3(h: Tensor, wp: Tensor) -> Tensor:
+    """analysis_17.py:22,35 (no quantiser): NHWC [B,H/8,W/8,N] → y NHWC [B,H/16,W/16,N]."""
+    _check(h, "activation", 4)
+    B, h8, w8, N = h.shape
+    _check_channels(N)
+    H, W = 8 * h8, 8 * w8
+    _check_image_dims(H, W)
+    y = torch.empty(B, h8 // 2, w8 // 2, N, device=h.device, dtype=torch.float32)
+    call("iclr17_analysis_conv3", _p(h.contiguous()), B, H, W, N, _p(wp), _p(y), _stream(h))
+    return y
+
+
+def rate_partials_per_image(H: int, W: int, N: int) -> int:
+    return query("iclr17_rate_partials_per_image", H, W, N)
+
+
+def conv3_quant_rate(h: Tensor, wp: Tensor, rate_packed: Tensor, noise: Optional[Tensor] = None,
+                     want_y: bool = False):
+    """analysis_17.py:22 + model.py:48-56,71-73. Returns (y_hat NHWC, bits_partial [B,T], y?).
+
+    noise (training) is NCHW [B,N,H/16,W/16], the shape model.py:48 draws."""
+    _check(h, "activation", 4)
+    B, h8, w8, N = h.shape
+    _check_channels(N)
+    H, W = 8 * h8, 8 * w8
+    _check_image_dims(H, W)
+    mode = _lib.ICLR17_QUANT_ROUND
+    if noise is not None:
+        _check(noise, "noise", 4)
+        if tuple(noise.shape) != (B, N, h8 // 2, w8 // 2):
+            raise Iclr17Error(f"iclr17: noise must be {(B, N, h8 // 2, w8 // 2)} (got {tuple(noise.shape)})")
+        noise = noise.contiguous()
+        mode = _lib.ICLR17_QUANT_NOISE
+    y_hat = torch.empty(B, h8 // 2, w8 // 2, N, device=h.device, dtype=torch.float32)
+    y = torch.empty_like(y_hat) if want_y else None
+    T = rate_partials_per_image(H, W, N)
+    partial = torch.empty(B, T, device=h.device, dtype=torch.float64)
+    call("iclr17_analysis_conv3_quant_rate", _p(h.contiguous()), B, H, W, N, _p(wp), mode,
+         _p(noise), _p(rate_packed), _p(y), _p(y_hat), _p(partial), _stream(h))
+    return (y_hat, partial, y) if want_y else (y_hat, partial)
+
+
+def deconv_igdn(h: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Tensor,
+                want_pre: bool = False):
+    """synthesis_17.py:15-22: NHWC [B,h,w,N] → [B,2h,2w,N]."""
+    _check(h, "activation", 4)
+    B, hh, ww, N = h.shape
+    _check_channels(N)
+    out = torch.empty(B, 2 * hh, 2 * ww, N, device=h.device, dtype=torch.float32)
+    pre = torch.empty_like(out) if want_pre else None
+    call("iclr17_synthesis_deconv_igdn", _p(h.contiguous()), B, hh, ww, N, _p(wp), _p(bias),
+         _p(beta_eff), _p(gp), _p(out), _p(pre), _stream(h))
+    return (out, pre) if want_pre else out
+
+
+def output_partials_per_image(H: int, W: int) -> int:
+    return query("iclr17_output_partials_per_image", H, W)
+
+
+def deconv3(h: Tensor, wp: Tensor, bias: Tensor, x_ref: Optional[Tensor] = None,
+            want_recon: bool = False):
+    """synthesis_17.py:23-25 + model.py:59: NHWC [B,H/4,W/4,N] → clipped NCHW [B,3,H,W].
+
+    Returns (clipped, recon_unclipped | None, sse_partial [B,T] | None)."""
+    _check(h, "activation", 4)
+    B, h4, w4, N = h.shape
+    _check_channels(N)
+    H, W = 4 * h4, 4 * w4
+    _check_image_dims(H, W)
+    clipped = torch.empty(B, 3, H, W, device=h.device, dtype=torch.float32)
+    recon = torch.empty_like(clipped) if want_recon else None
+    partial = None
+    if x_ref is not None:
+        _check(x_ref, "reference image", 4)
+        if tuple(x_ref.shape) != (B, 3, H, W):
+            raise Iclr17Error("iclr17: reference image shape mismatch")
+        x_ref = x_ref.contiguous()
+        partial = torch.empty(B, output_partials_per_image(H, W), device=h.device, dtype=torch.float64)
+    call("iclr17_synthesis_deconv3", _p(h.contiguous()), B, H, W, N, _p(wp), _p(bias), _p(x_ref),
+         _p(clipped), _p(recon), _p(partial), _stream(h))
+    return clipped, recon, partial
+
+
+def reduce_partials(partial: Tensor, scale: float = 1.0, per_image: bool = True):
+    """Deterministic per-image sums (float64 [B]) and scale·Σ (float32 0-dim)."""
+    _check_f64(partial)
+    B, T = partial.shape
+    per = torch.empty(B, device=partial.device, dtype=torch.float64) if per_image else None
+    total = torch.empty((), device=partial.device, dtype=torch.float32)
+    call("iclr17_reduce_partials", _p(partial.contiguous()), B, T, _p(per), _p(total),
+         ctypes.c_double(scale), _stream(partial))
+    return per, total
+
+
+def _check_f64(t: Tensor) -> None:
+    if t.device.type != "cuda" or t.dtype != torch.float64 or t.dim() != 2:
+        raise Iclr17Error("iclr17: partial sums must be a 2-D float64 GPU tensor")
+
+
+# ------------------------------------------------------------------------------ modules
+def gdn(x: Tensor, beta_eff: Tensor, gp: Tensor, inverse: bool) -> Tensor:
+    """GDN.forward (models/GDN.py:64-94) on a 4-D tensor; keeps the input's memory format."""
+    _check(x, "input", 4)
+    B, C, H, W = x.shape
+    _check_channels(C)
+    if x.is_contiguous():
+        layout, src = _lib.ICLR17_LAYOUT_NCHW, x
+        y = torch.empty_like(x)
+    elif x.is_contiguous(memory_format=torch.channels_last):
+        layout, src = _lib.ICLR17_LAYOUT_NHWC, x
+        y = torch.empty_like(x, memory_format=torch.channels_last)
+    else:
+        layout, src = _lib.ICLR17_LAYOUT_NCHW, x.contiguous()
+        y = torch.empty_like(src)
+    call("iclr17_gdn", _p(src), B, C, H, W, layout, int(bool(inverse)), _p(beta_eff), _p(gp),
+         _p(y), _stream(x))
+    return y
+
+
+def _layout_inner(x: Tensor) -> Tuple[Tensor, int]:
+    """(tensor, inner) such that channel of flat element i is (i // inner) % C."""
+    if x.dim() == 4 and not x.is_contiguous() and x.is_contiguous(memory_format=torch.channels_last):
+        return x, 1
+    x = x.contiguous()
+    inner = int(np.prod(x.shape[2:])) if x.dim() > 2 else 1
+    return x, inner
+
+
+def bit_estimator(x: Tensor, rate_packed: Tensor, C: int) -> Tensor:
+    """BitEstimator.forward (bitEstimator.py:38-42): elementwise CDF, channel dim 1."""
+    _check(x, "input")
+    if x.dim() < 2 or x.shape[1] != C:
+        raise Iclr17Error(f"iclr17: BitEstimator input needs {C} channels in dim 1")
+    src, inner = _layout_inner(x)
+    out = torch.empty_like(src)
+    call("iclr17_bit_estimator", _p(src), src.numel(), C, inner, _p(rate_packed), _p(out),
+         _stream(x))
+    return out
+
+
+def bitparm(x: Tensor, h: Tensor, b: Tensor, a: Optional[Tensor]) -> Tensor:
+    """One Bitparm layer (bitEstimator.py:20-25)."""
+    _check(x, "input")
+    C = h.numel()
+    if x.dim() < 2 or x.shape[1] != C:
+        raise Iclr17Error(f"iclr17: Bitparm input needs {C} channels in dim 1")
+    src, inner = _layout_inner(x)
+    out = torch.empty_like(src)
+    work = torch.empty(2 * C, device=x.device, dtype=torch.float32)
+    hc, bc = h.detach().reshape(-1).contiguous(), b.detach().reshape(-1).contiguous()
+    ac = a.detach().reshape(-1).contiguous() if a is not None else None
+    call("iclr17_bitparm", _p(src), src.numel(), C, inner, _p(hc), _p(bc), _p(ac), _p(work),
+         _p(out), _stream(x))
+    return out
+
+
+def rate_bits(z: Tensor, rate_packed: Tensor) -> Tensor:
+    """model.py:71-73 on a 4-D latent: per-image Σ bits partials [B, T] (float64)."""
+    _check(z, "latent", 4)
+    B, C, h, w = z.shape
+    if z.is_contiguous():
+        layout, src = _lib.ICLR17_LAYOUT_NCHW, z
+    elif z.is_contiguous(memory_format=torch.channels_last):
+        layout, src = _lib.ICLR17_LAYOUT_NHWC, z
+    else:
+        layout, src = _lib.ICLR17_LAYOUT_NCHW, z.contiguous()
+    T = query("iclr17_rate_bits_partials", C, h, w)
+    partial = torch.empty(B, T, device=z.device, dtype=torch.float64)
+    call("iclr17_rate_bits", _p(src), B, C, h, w, layout, _p(rate_packed), _p(partial), _stream(z))
+    return partial

@@ -1,0 +1,103 @@
+"""Top-level codec — surface of the reference model.py:1-81.
+
+``ImageCompressor(out_channel_N=128)`` owns ``Encoder`` (Analysis_net_17), ``Decoder``
+(Synthesis_net_17) and ``bitEstimator`` (BitEstimator) with the reference's state_dict keys,
+and ``forward(x) -> (clipped_recon, y_hat, bpp)`` (model.py:47-80). The forward is one chain
+of fused gfx950 kernels:
+
+    conv1+GDN → conv2+GDN → conv3+quantise+rate → deconv1+IGDN → deconv2+IGDN →
+    deconv3+bias+clamp → deterministic bit reduction
+
+``save_model`` / ``load_model`` keep the reference's file naming and merge semantics
+(model.py:18-35).
+"""
+from __future__ import annotations
+
+import logging  # noqa: F401  (re-exported: train.py uses it via `from model import *`)
+import math  # noqa: F401
+import os
+from typing import Dict, Optional
+
+import numpy as np  # noqa: F401  (re-exported, train.py:117)
+import torch
+import torch.nn as nn
+
+from . import kernels
+from .models import *  # noqa: F401,F403
+from .models import Analysis_net_17, BitEstimator, Synthesis_net_17
+
+
+def save_model(model, iter, name):
+    """model.py:18-19"""
+    torch.save(model.state_dict(), os.path.join(name, "iter_{}.pth.tar".format(iter)))
+
+
+def load_model(model, f):
+    """model.py:22-35: merge the checkpoint's matching keys; always returns step 0 (D7)."""
+    with open(f, "rb") as fh:
+        pretrained_dict = torch.load(fh, map_location="cpu", weights_only=True)
+        model_dict = model.state_dict()
+        pretrained_dict = {k: v for k, v in pretrained_dict.items() if k in model_dict}
+        model_dict.update(pretrained_dict)
+        model.load_state_dict(model_dict)
+    return 0
+
+
+class ImageCompressor(nn.Module):
+    def __init__(self, out_channel_N=128):
+        super().__init__()
+        self.Encoder = Analysis_net_17(out_channel_N=out_channel_N)
+        self.Decoder = Synthesis_net_17(out_channel_N=out_channel_N)
+        self.bitEstimator = BitEstimator(channel=out_channel_N)
+        self.out_channel_N = out_channel_N
+
+    # -------------------------------------------------------------------------------------
+    def _latent_noise(self, x: torch.Tensor) -> torch.Tensor:
+        # model.py:48-49: U(-0.5, 0.5) of shape [B, N, H//16, W//16] on the device RNG
+        B, _, H, W = x.shape
+        return torch.empty(B, self.out_channel_N, H // 16, W // 16, device=x.device,
+                           dtype=torch.float32).uniform_(-0.5, 0.5)
+
+    def run(self, x: torch.Tensor, noise: Optional[torch.Tensor] = None, training: Optional[bool] = None,
+            x_ref_sse: bool = False, want_recon: bool = False) -> Dict[str, torch.Tensor]:
+        """The fused forward. Returns a dict with ``clipped`` (NCHW), ``y_hat`` (NHWC), bits
+        partials and, on request, per-image SSE partials (vs x) and the unclipped recon."""
+        kernels._check(x, "image", 4)
+        training = self.training if training is None else training
+        if training and noise is None:
+            noise = self._latent_noise(x)
+        if not training:
+            noise = None
+        x = x.contiguous()
+        w1, w2, w3, g1, g2 = self.Encoder.packed()
+        N = self.out_channel_N
+        h = kernels.conv1_gdn(x, w1, self.Encoder.conv1.bias, g1[0], g1[1], N)
+        h = kernels.conv2_gdn(h, w2, self.Encoder.conv2.bias, g2[0], g2[1])
+        y_hat, bits_partial = kernels.conv3_quant_rate(h, w3, self.bitEstimator.packed(), noise)
+        clipped, recon, sse_partial = self.Decoder.decode(y_hat, x_ref=x if x_ref_sse else None,
+                                                          want_recon=want_recon)
+        return {"clipped": clipped, "y_hat": y_hat, "bits_partial": bits_partial,
+                "sse_partial": sse_partial, "recon": recon}
+
+    def forward(self, input_image, noise: Optional[torch.Tensor] = None):
+        from .autograd import no_backward
+        B, _, H, W = input_image.shape
+        out = self.run(input_image, noise=noise)
+        _, bpp = kernels.reduce_partials(out["bits_partial"], scale=1.0 / (B * H * W), per_image=False)
+        y_hat = out["y_hat"].permute(0, 3, 1, 2)
+        clipped = no_backward(out["clipped"], "ImageCompressor", list(self.parameters()), input_image)
+        return clipped, y_hat, bpp
+
+    @torch.no_grad()
+    def evaluate(self, x: torch.Tensor) -> Dict[str, torch.Tensor]:
+        """testKodak-style per-image metrics (train.py:157-190): bpp, MSE of the clipped
+        reconstruction and PSNR per image, all from deterministic on-device reductions."""
+        B, _, H, W = x.shape
+        out = self.run(x, training=False, x_ref_sse=True)
+        bits, _ = kernels.reduce_partials(out["bits_partial"])
+        sse, _ = kernels.reduce_partials(out["sse_partial"])
+        bpp = bits / (H * W)
+        mse = sse / (3 * H * W)
+        psnr = 10.0 * torch.log10(1.0 / mse)
+        return {"clipped": out["clipped"], "y_hat": out["y_hat"].permute(0, 3, 1, 2),
+                "bpp": bpp, "mse": mse, "psnr": psnr}

@@ -1,0 +1,78 @@
+"""GDN / IGDN module — surface of the reference models/GDN.py:10-94.
+
+Same constructor, parameters (``beta`` [C], ``gamma`` [C, C]) and re-parametrisation; the
+forward runs the fused gfx950 kernel (per-pixel channel contraction β + γ·x² on the exact-f32
+MFMA, then x/√n or x·√n) through libiclr17.so. Effective (bounded, squared) parameters are
+computed by a packing kernel and cached until the parameters change.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+from torch import nn
+from torch.autograd import Function
+
+from .. import kernels
+from ..packcache import PackCache
+
+
+class LowerBound(Function):
+    """models/GDN.py:10-24: forward max(x, bound); backward passes g where x ≥ bound or g < 0.
+    (Parameter-sized; the GDN hot path applies the bound inside its packing kernel.)"""
+
+    @staticmethod
+    def forward(ctx, inputs, bound):
+        b = torch.ones_like(inputs) * bound
+        ctx.save_for_backward(inputs, b)
+        return torch.max(inputs, b)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        inputs, b = ctx.saved_tensors
+        pass_through = (inputs >= b) | (grad_output < 0)
+        return pass_through.type(grad_output.dtype) * grad_output, None
+
+
+class GDN(nn.Module):
+    """Generalized divisive normalization: y[i] = x[i] / sqrt(beta[i] + sum_j gamma[i, j] x[j]^2)
+    (the conv2d semantics of the reference, GDN.py:80-83; ``inverse`` multiplies instead)."""
+
+    def __init__(self, ch, inverse=False, beta_min=1e-6, gamma_init=0.1, reparam_offset=2 ** -18):
+        super().__init__()
+        self.inverse = inverse
+        self.beta_min = beta_min
+        self.gamma_init = gamma_init
+        self.reparam_offset = reparam_offset
+        self.build(ch)
+        self._pack = PackCache()
+
+    def build(self, ch):
+        # GDN.py:46-62
+        self.pedestal = self.reparam_offset ** 2
+        self.beta_bound = (self.beta_min + self.reparam_offset ** 2) ** 0.5
+        self.gamma_bound = self.reparam_offset
+        self.beta = nn.Parameter(torch.sqrt(torch.ones(ch) + self.pedestal))
+        self.gamma = nn.Parameter(torch.sqrt(self.gamma_init * torch.eye(ch) + self.pedestal))
+
+    def bounds_f32(self):
+        """The fp32 values ones_like(x) * bound evaluates to in the reference."""
+        return (float(np.float32(self.beta_bound)), float(np.float32(self.gamma_bound)),
+                float(np.float32(self.pedestal)))
+
+    def effective_params(self, force: bool = False):
+        """(beta_eff [C], gamma_packed [C*C]) on the parameters' device."""
+        bb, gb, ped = self.bounds_f32()
+        return self._pack.get("gdn", (self.beta, self.gamma),
+                              lambda: kernels.pack_gdn(self.beta, self.gamma, bb, gb, ped),
+                              force=force or self.training)
+
+    def forward(self, inputs):
+        unfold = inputs.dim() == 5
+        if unfold:  # GDN.py:65-69
+            bs, ch, d, w, h = inputs.size()
+            inputs = inputs.reshape(bs, ch, d * w, h)
+        from ..autograd import gdn_apply
+        outputs = gdn_apply(inputs, self)
+        if unfold:
+            outputs = outputs.reshape(bs, ch, d, w, h)
+        return outputs

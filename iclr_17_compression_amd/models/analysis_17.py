@@ -1,0 +1,61 @@
+"""Analysis transform g_a — surface of the reference models/analysis_17.py:8-39.
+
+Layers (and their init, analysis_17.py:14-23) are the reference's: conv9×9/s4 → GDN →
+conv5×5/s2 → GDN → conv5×5/s2 (no bias). ``forward`` runs three fused gfx950 kernels
+(conv1+GDN, conv2+GDN, conv3) on NHWC activations and returns y as an NCHW-shaped
+channels-last tensor.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+from .. import _lib, kernels
+from ..packcache import PackCache
+from .GDN import GDN
+
+
+class Analysis_net_17(nn.Module):
+    """Analysis net"""
+
+    def __init__(self, out_channel_N=192):
+        super().__init__()
+        N = out_channel_N
+        self.conv1 = nn.Conv2d(3, N, 9, stride=4, padding=4)
+        torch.nn.init.xavier_normal_(self.conv1.weight.data, math.sqrt(2 * (3 + N) / 6))
+        torch.nn.init.constant_(self.conv1.bias.data, 0.01)
+        self.gdn1 = GDN(N)
+        self.conv2 = nn.Conv2d(N, N, 5, stride=2, padding=2)
+        torch.nn.init.xavier_normal_(self.conv2.weight.data, math.sqrt(2))
+        torch.nn.init.constant_(self.conv2.bias.data, 0.01)
+        self.gdn2 = GDN(N)
+        self.conv3 = nn.Conv2d(N, N, 5, stride=2, padding=2, bias=False)
+        torch.nn.init.xavier_normal_(self.conv3.weight.data, math.sqrt(2))
+        self.out_channel_N = N
+        self._pack = PackCache()
+
+    def packed(self, force: bool = False):
+        N, f = self.out_channel_N, force or self.training
+        w1 = self._pack.get("w1", (self.conv1.weight,),
+                            lambda: kernels.pack_weight(_lib.ICLR17_W_CONV1, self.conv1.weight, N), f)
+        w2 = self._pack.get("w2", (self.conv2.weight,),
+                            lambda: kernels.pack_weight(_lib.ICLR17_W_CONV5, self.conv2.weight, N), f)
+        w3 = self._pack.get("w3", (self.conv3.weight,),
+                            lambda: kernels.pack_weight(_lib.ICLR17_W_CONV5, self.conv3.weight, N), f)
+        g1 = self.gdn1.effective_params(force)
+        g2 = self.gdn2.effective_params(force)
+        return w1, w2, w3, g1, g2
+
+    def features(self, x):
+        """conv1+gdn1 → conv2+gdn2 as NHWC (the input of conv3); no autograd."""
+        w1, w2, _, g1, g2 = self.packed()
+        h = kernels.conv1_gdn(x, w1, self.conv1.bias, g1[0], g1[1], self.out_channel_N)
+        return kernels.conv2_gdn(h, w2, self.conv2.bias, g2[0], g2[1])
+
+    def forward(self, x):
+        from ..autograd import no_backward
+        _, _, w3, _, _ = self.packed()
+        y = kernels.conv3(self.features(x), w3).permute(0, 3, 1, 2)
+        return no_backward(y, "Analysis_net_17", list(self.parameters()), x)

@@ -1,0 +1,69 @@
+"""Synthesis transform g_s — surface of the reference models/synthesis_17.py:8-31.
+
+Layers and init (synthesis_17.py:15-25): deconv5×5/s2 → IGDN → deconv5×5/s2 → IGDN →
+deconv9×9/s4 → 3 channels. ``forward`` runs two fused deconv+IGDN kernels (stride-phase
+decomposed, no zero insertion) and the all-phase deconv3 kernel; returns the UNclipped
+reconstruction, NCHW, exactly like the reference module.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+from .. import _lib, kernels
+from ..packcache import PackCache
+from .GDN import GDN
+
+
+class Synthesis_net_17(nn.Module):
+    """Decode synthesis"""
+
+    def __init__(self, out_channel_N=192):
+        super().__init__()
+        N = out_channel_N
+        self.deconv1 = nn.ConvTranspose2d(N, N, 5, stride=2, padding=2, output_padding=1)
+        torch.nn.init.xavier_normal_(self.deconv1.weight.data, math.sqrt(2 * 1))
+        torch.nn.init.constant_(self.deconv1.bias.data, 0.01)
+        self.igdn1 = GDN(N, inverse=True)
+        self.deconv2 = nn.ConvTranspose2d(N, N, 5, stride=2, padding=2, output_padding=1)
+        torch.nn.init.xavier_normal_(self.deconv2.weight.data, math.sqrt(2 * 1))
+        torch.nn.init.constant_(self.deconv2.bias.data, 0.01)
+        self.igdn2 = GDN(N, inverse=True)
+        self.deconv3 = nn.ConvTranspose2d(N, 3, 9, stride=4, padding=4, output_padding=3)
+        torch.nn.init.xavier_normal_(self.deconv3.weight.data, math.sqrt(2 * 1))
+        torch.nn.init.constant_(self.deconv3.bias.data, 0.01)
+        self.out_channel_N = N
+        self._pack = PackCache()
+
+    def packed(self, force: bool = False):
+        N, f = self.out_channel_N, force or self.training
+        d1 = self._pack.get("d1", (self.deconv1.weight,),
+                            lambda: kernels.pack_weight(_lib.ICLR17_W_DECONV5, self.deconv1.weight, N), f)
+        d2 = self._pack.get("d2", (self.deconv2.weight,),
+                            lambda: kernels.pack_weight(_lib.ICLR17_W_DECONV5, self.deconv2.weight, N), f)
+        d3 = self._pack.get("d3", (self.deconv3.weight,),
+                            lambda: kernels.pack_weight(_lib.ICLR17_W_DECONV9, self.deconv3.weight, N), f)
+        return d1, d2, d3, self.igdn1.effective_params(force), self.igdn2.effective_params(force)
+
+    @staticmethod
+    def to_nhwc(y):
+        """NCHW-shaped latent (any memory format) → contiguous NHWC [B, h, w, N] (no copy when
+        the latent is already channels-last, e.g. the Encoder's own output)."""
+        return y.permute(0, 2, 3, 1).contiguous()
+
+    def decode(self, y_nhwc, x_ref=None, want_recon=True):
+        """NHWC latent → (clipped NCHW, unclipped NCHW | None, SSE partials | None)."""
+        d1, d2, d3, g1, g2 = self.packed()
+        h = kernels.deconv_igdn(y_nhwc, d1, self.deconv1.bias, g1[0], g1[1])
+        h = kernels.deconv_igdn(h, d2, self.deconv2.bias, g2[0], g2[1])
+        return kernels.deconv3(h, d3, self.deconv3.bias, x_ref=x_ref, want_recon=want_recon)
+
+    def forward(self, x):
+        from ..autograd import no_backward
+        kernels._check(x, "latent", 4)
+        if x.shape[1] != self.out_channel_N:
+            raise kernels.Iclr17Error(f"iclr17: Synthesis_net_17 expects {self.out_channel_N} channels")
+        _, recon, _ = self.decode(self.to_nhwc(x), want_recon=True)
+        return no_backward(recon, "Synthesis_net_17", list(self.parameters()), x)

@@ -1,0 +1,65 @@
+"""The C-ABI library: loads on a GPU-less host, exports every entry point include/iclr17.h
+declares, and its host-side validation rejects bad arguments before any launch."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+from iclr_17_compression_amd import _lib, kernels
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "iclr17.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(iclr17_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    lib = _lib.load()
+    names = declared_functions()
+    assert len(names) >= 20
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    # the Python binding declares a signature for every entry point, and nothing else
+    assert sorted(_lib.SIGNATURES) == names
+
+
+def test_version_and_size_queries():
+    lib = _lib.load()
+    assert lib.iclr17_version() >= 1
+    assert _lib.query("iclr17_packed_weight_size", _lib.ICLR17_W_CONV5, 192) == 25 * 192 * 192
+    assert _lib.query("iclr17_packed_weight_size", _lib.ICLR17_W_CONV1, 128) == 256 * 128
+    assert _lib.query("iclr17_packed_weight_size", _lib.ICLR17_W_DECONV9, 192) == 9 * 192 * 48
+    assert _lib.query("iclr17_rate_partials_per_image", 256, 256, 192) == 4 * 3
+    assert _lib.query("iclr17_output_partials_per_image", 256, 256) == 64
+    assert _lib.query("iclr17_rate_bits_partials", 192, 16, 16) == 12
+
+
+def test_argument_validation_without_gpu():
+    # every check below fires on the host before a kernel could be launched
+    with pytest.raises(_lib.Iclr17Error, match="multiples of 16"):
+        _lib.call("iclr17_analysis_conv1_gdn", ctypes.c_void_p(16), 1, 250, 256, 192,
+                  *[ctypes.c_void_p(16)] * 5, None, None)
+    with pytest.raises(_lib.Iclr17Error, match="unsupported"):
+        _lib.call("iclr17_analysis_conv2_gdn", ctypes.c_void_p(16), 1, 256, 256, 96,
+                  *[ctypes.c_void_p(16)] * 5, None, None)
+    with pytest.raises(_lib.Iclr17Error, match="null pointer"):
+        _lib.call("iclr17_synthesis_deconv3", None, 1, 256, 256, 192, *[None] * 6, None)
+    with pytest.raises(_lib.Iclr17Error, match="quant mode"):
+        _lib.call("iclr17_analysis_conv3_quant_rate", ctypes.c_void_p(16), 1, 256, 256, 192,
+                  ctypes.c_void_p(16), 1, None, ctypes.c_void_p(16), None, ctypes.c_void_p(16),
+                  ctypes.c_void_p(16), None)
+    assert "quant mode" in _lib.last_error()
+
+
+def test_cpu_tensors_fail_loudly():
+    from iclr_17_compression_amd.model import ImageCompressor
+    net = ImageCompressor(128).eval()
+    with pytest.raises(_lib.Iclr17Error, match="ROCm GPU"):
+        net(torch.rand(1, 3, 32, 32))
+    with pytest.raises(_lib.Iclr17Error, match="ROCm GPU"):
+        kernels.gdn(torch.rand(1, 128, 4, 4), torch.zeros(128), torch.zeros(128 * 128), False)

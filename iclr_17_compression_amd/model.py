@@ -59,7 +59,8 @@ class ImageCompressor(nn.Module):
                            dtype=torch.float32).uniform_(-0.5, 0.5)
 
     def run(self, x: torch.Tensor, noise: Optional[torch.Tensor] = None, training: Optional[bool] = None,
-            x_ref_sse: bool = False, want_recon: bool = False) -> Dict[str, torch.Tensor]:
+            x_ref_sse: bool = False, want_recon: bool = False,
+            want_y: bool = False) -> Dict[str, torch.Tensor]:
         """The fused forward. Returns a dict with ``clipped`` (NCHW), ``y_hat`` (NHWC), bits
         partials and, on request, per-image SSE partials (vs x) and the unclipped recon."""
         kernels._check(x, "image", 4)
@@ -73,11 +74,12 @@ class ImageCompressor(nn.Module):
         N = self.out_channel_N
         h = kernels.conv1_gdn(x, w1, self.Encoder.conv1.bias, g1[0], g1[1], N)
         h = kernels.conv2_gdn(h, w2, self.Encoder.conv2.bias, g2[0], g2[1])
-        y_hat, bits_partial = kernels.conv3_quant_rate(h, w3, self.bitEstimator.packed(), noise)
+        q = kernels.conv3_quant_rate(h, w3, self.bitEstimator.packed(), noise, want_y=want_y)
+        y_hat, bits_partial = q[0], q[1]
         clipped, recon, sse_partial = self.Decoder.decode(y_hat, x_ref=x if x_ref_sse else None,
                                                           want_recon=want_recon)
         return {"clipped": clipped, "y_hat": y_hat, "bits_partial": bits_partial,
-                "sse_partial": sse_partial, "recon": recon}
+                "sse_partial": sse_partial, "recon": recon, "y": q[2] if want_y else None}
 
     def forward(self, input_image, noise: Optional[torch.Tensor] = None):
         from .autograd import no_backward
@@ -89,15 +91,18 @@ class ImageCompressor(nn.Module):
         return clipped, y_hat, bpp
 
     @torch.no_grad()
-    def evaluate(self, x: torch.Tensor) -> Dict[str, torch.Tensor]:
+    def evaluate(self, x: torch.Tensor, want_y: bool = False) -> Dict[str, torch.Tensor]:
         """testKodak-style per-image metrics (train.py:157-190): bpp, MSE of the clipped
         reconstruction and PSNR per image, all from deterministic on-device reductions."""
         B, _, H, W = x.shape
-        out = self.run(x, training=False, x_ref_sse=True)
+        out = self.run(x, training=False, x_ref_sse=True, want_y=want_y)
         bits, _ = kernels.reduce_partials(out["bits_partial"])
         sse, _ = kernels.reduce_partials(out["sse_partial"])
         bpp = bits / (H * W)
         mse = sse / (3 * H * W)
         psnr = 10.0 * torch.log10(1.0 / mse)
-        return {"clipped": out["clipped"], "y_hat": out["y_hat"].permute(0, 3, 1, 2),
-                "bpp": bpp, "mse": mse, "psnr": psnr}
+        res = {"clipped": out["clipped"], "y_hat": out["y_hat"].permute(0, 3, 1, 2),
+               "bpp": bpp, "mse": mse, "psnr": psnr}
+        if want_y:
+            res["y"] = out["y"].permute(0, 3, 1, 2)
+        return res

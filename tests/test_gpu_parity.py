@@ -143,6 +143,21 @@ def flips(a, b):
     return int((a.detach().cpu() != b.detach().cpu()).sum().item())
 
 
+def check_latents(y_hat, y, r_yhat, r_y, max_rate=1e-4):
+    """ŷ must equal round(y_ref) bit for bit except at near-ties: a flip is legitimate only
+    where the reference latent lies within the observed fp32 summation-order noise
+    (max |y − y_ref| over the tensor) of a rounding boundary k + ½. Returns the flip count."""
+    y_hat, y = y_hat.detach().cpu(), y.detach().cpu()
+    diff = y_hat != r_yhat
+    n = int(diff.sum())
+    if n:
+        noise = (y - r_y).abs().max().item()
+        dist = (r_y[diff] - (torch.floor(r_y[diff]) + 0.5)).abs()
+        assert dist.max().item() <= noise, (n, dist.max().item(), noise)
+        assert n <= max_rate * r_yhat.numel(), n
+    return n
+
+
 def test_c1_golden_end_to_end(device, golden_dir):
     g = np.load(os.path.join(golden_dir, "g3_c1_n192_256px.npz"), allow_pickle=False)
     meta = json.load(open(os.path.join(golden_dir, "g3_c1_n192_256px.json")))
@@ -174,8 +189,9 @@ def test_module_shapes_vs_oracle(device, N, B, H, W):
     x = image(7, B, H, W)
     with torch.no_grad():
         clipped, y_hat, bpp = net(x.to(device))
-    r_clipped, r_yhat, r_bpp, _, _ = oracle.codec_forward(x, sd)
-    assert flips(y_hat, r_yhat) == 0
+        y = net.run(x.to(device), want_y=True)["y"].permute(0, 3, 1, 2)
+    r_clipped, r_yhat, r_bpp, _, r_y = oracle.codec_forward(x, sd)
+    check_latents(y_hat, y, r_yhat, r_y)
     assert bpp.item() == pytest.approx(r_bpp.item(), rel=METRIC_REL)
     assert rel_err(clipped, r_clipped) < REL
 
@@ -200,11 +216,12 @@ def test_kodak_synth_subset(device, golden_dir):
     for row in [meta["images"][i] for i in (0, 3, 9, 23)]:
         x = torch.from_numpy(synth.to_unit_float(
             synth.smooth_image_u8(meta["image_seed_base"] + row["index"], row["height"], row["width"])))[None]
-        ev = net.evaluate(x.to(device))
+        ev = net.evaluate(x.to(device), want_y=True)
         assert ev["bpp"][0].item() == pytest.approx(row["bpp"], rel=METRIC_REL)
         assert ev["psnr"][0].item() == pytest.approx(row["psnr"], rel=METRIC_REL)
-        _, r_yhat, _, _, _ = oracle.codec_forward(x, sd)
-        assert flips(ev["y_hat"], r_yhat) == 0
+        _, r_yhat, _, _, r_y = oracle.codec_forward(x, sd)
+        n = check_latents(ev["y_hat"], ev["y"], r_yhat, r_y)
+        print(f"kodak-synth[{row['index']}]: {n} near-tie latent flips of {r_yhat.numel()}")
 
 
 def test_determinism_and_batch_independence(device):

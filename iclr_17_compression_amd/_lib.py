@@ -41,7 +41,7 @@ SIGNATURES = {
     "iclr17_last_error": (_I, [ctypes.c_char_p, _SZ]),
     "iclr17_packed_weight_size": (_SZ, [_I, _I]),
     "iclr17_pack_weight": (_I, [_I, _P, _P, _I, _P]),
-    "iclr17_pack_gdn": (_I, [_P, _P, _P, _P, _I, _F, _F, _F, _P]),
+    "iclr17_pack_gdn": (_I, [_P, _P, _P, _P, _P, _I, _F, _F, _F, _P]),
     "iclr17_pack_rate": (_I, [_P] * 12 + [_I, _P]),
     "iclr17_analysis_conv1_gdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_analysis_conv2_gdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
@@ -49,7 +49,7 @@ SIGNATURES = {
     "iclr17_analysis_conv3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P]),
     "iclr17_rate_partials_per_image": (_I, [_I, _I, _I]),
     "iclr17_synthesis_deconv_igdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
-    "iclr17_synthesis_deconv3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_synthesis_deconv3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P]),
     "iclr17_output_partials_per_image": (_I, [_I, _I]),
     "iclr17_reduce_partials": (_I, [_P, _I, _I, _P, _P, _D, _P]),
     "iclr17_gdn": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
@@ -57,6 +57,21 @@ SIGNATURES = {
     "iclr17_bitparm": (_I, [_P, _I64, _I, _I64, _P, _P, _P, _P, _P]),
     "iclr17_rate_bits": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "iclr17_rate_bits_partials": (_I, [_I, _I, _I]),
+    "iclr17_grad_recon": (_I, [_P, _P, _P, _P, _I64, _P, _P]),
+    "iclr17_bwd_deconv3_igdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_bwd_deconv_igdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_bwd_deconv_rate": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _F, _P, _P, _P]),
+    "iclr17_rate_bwd_partials": (_I, [_I, _I]),
+    "iclr17_bwd_conv_gdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_wgrad_workspace_size": (_SZ, [_I, _I, _I, _I, _I, _I]),
+    "iclr17_wgrad_k5": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "iclr17_wgrad_k9": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P]),
+    "iclr17_gdn_wgrad_workspace_size": (_SZ, [ctypes.c_long, _I]),
+    "iclr17_gdn_wgrad": (_I, [_P, _P, ctypes.c_long, _I, _P, _P, _P, _P]),
+    "iclr17_gdn_param_chain": (_I, [_P, _P, _P, _P, _I, _F, _F, _P, _P, _P]),
+    "iclr17_bias_grad_nhwc": (_I, [_P, ctypes.c_long, _I, _P, _P, _P]),
+    "iclr17_bias_grad_nchw": (_I, [_P, _I, _I, ctypes.c_long, _P, _P, _P]),
+    "iclr17_rate_param_grad": (_I, [_P, _I, _I] + [_P] * 7 + [_P] * 11 + [_P]),
 }
 
 

@@ -1,15 +1,22 @@
-"""Autograd glue for the HIP kernels.
+"""Autograd glue for the HIP kernels (forward and backward both run in libiclr17.so).
 
-Forward passes always run on libiclr17.so. Where a backward kernel is not wired yet the output
-carries a grad_fn that raises a clear error instead of silently producing wrong gradients.
+* ``CodecTrainFn`` — the fused training step of ImageCompressor (model.py:47-80 with the loss
+  terms train.py:97-102 intends): outputs (clipped, ỹ, bpp, mse_unclipped); its backward is the
+  reference autograd graph of ``rd_loss.backward()`` (train.py:105) as fused kernels.
+* ``AnalysisFn`` / ``SynthesisFn`` — Encoder / Decoder used on their own (NewTests-style
+  callers, train_decoder_new.py:66-105 trains a Decoder alone).
+* Where a backward kernel is not wired yet (stand-alone GDN / BitEstimator modules), outputs
+  carry a grad_fn that raises instead of silently producing wrong gradients.
 """
 from __future__ import annotations
 
-from typing import Sequence
+from typing import Dict, List, Optional, Sequence
 
 import torch
 
-from . import kernels
+from . import _lib, kernels
+
+Tensor = torch.Tensor
 
 
 class _NoBackward(torch.autograd.Function):
@@ -23,14 +30,182 @@ class _NoBackward(torch.autograd.Function):
         raise NotImplementedError(f"iclr17: backward of {ctx.name} is not implemented by the HIP path yet")
 
 
-def no_backward(out: torch.Tensor, name: str, params: Sequence[torch.Tensor], x: torch.Tensor):
+def no_backward(out: Tensor, name: str, params: Sequence[Tensor], x: Tensor):
     needs = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params))
     if not needs:
         return out
     return _NoBackward.apply(name, out, x, *params)
 
 
-def gdn_apply(x: torch.Tensor, module) -> torch.Tensor:
+def gdn_apply(x: Tensor, module) -> Tensor:
     beta_eff, gp = module.effective_params()
     out = kernels.gdn(x, beta_eff, gp, module.inverse)
     return no_backward(out, "GDN", (module.beta, module.gamma), x)
+
+
+def needs_grad(x: Optional[Tensor], params: Sequence[Tensor]) -> bool:
+    return torch.is_grad_enabled() and ((x is not None and x.requires_grad) or
+                                        any(p.requires_grad for p in params))
+
+
+# ------------------------------------------------------------------------------ analysis
+def analysis_features_train(enc, x: Tensor):
+    """conv1+GDN1, conv2+GDN2 keeping the pre-activations the backward needs."""
+    w1, w2, _, g1, g2 = enc.packed()
+    N = enc.out_channel_N
+    a1, u1 = kernels.conv1_gdn(x, w1, enc.conv1.bias, g1[0], g1[1], N, want_pre=True)
+    a2, u2 = kernels.conv2_gdn(a1, w2, enc.conv2.bias, g2[0], g2[1], want_pre=True)
+    return a2, {"x": x, "u1": u1, "a1": a1, "u2": u2, "a2": a2}
+
+
+def analysis_backward(enc, saved: Dict[str, Tensor], g_y: Tensor) -> Dict[str, Tensor]:
+    """∂L/∂y (NHWC) → parameter gradients of Analysis_net_17 (analysis_17.py:14-39)."""
+    bb1, gb1, _ = enc.gdn1.bounds_f32()
+    bb2, gb2, _ = enc.gdn2.bounds_f32()
+    w3t = kernels.pack_weight(_lib.ICLR17_W_DECONV5, enc.conv3.weight, enc.out_channel_N)
+    w2t = kernels.pack_weight(_lib.ICLR17_W_DECONV5, enc.conv2.weight, enc.out_channel_N)
+    p2 = enc.gdn2.effective_params_bwd()
+    p1 = enc.gdn1.effective_params_bwd()
+    g_u2, dn2 = kernels.bwd_conv_gdn(g_y, w3t, saved["u2"], *p2)
+    dW3 = kernels.wgrad_k5(g_y, saved["a2"])
+    g_u1, dn1 = kernels.bwd_conv_gdn(g_u2, w2t, saved["u1"], *p1)
+    dW2 = kernels.wgrad_k5(g_u2, saved["a1"])
+    db2 = kernels.bias_grad_nhwc(g_u2)
+    dW1 = kernels.wgrad_k9(g_u1, saved["x"])
+    db1 = kernels.bias_grad_nhwc(g_u1)
+    dbeta2, dgamma2 = kernels.gdn_param_grads(dn2, saved["u2"], enc.gdn2.beta, enc.gdn2.gamma, bb2, gb2)
+    dbeta1, dgamma1 = kernels.gdn_param_grads(dn1, saved["u1"], enc.gdn1.beta, enc.gdn1.gamma, bb1, gb1)
+    return {"conv1.weight": dW1, "conv1.bias": db1, "gdn1.beta": dbeta1, "gdn1.gamma": dgamma1,
+            "conv2.weight": dW2, "conv2.bias": db2, "gdn2.beta": dbeta2, "gdn2.gamma": dgamma2,
+            "conv3.weight": dW3}
+
+
+# ----------------------------------------------------------------------------- synthesis
+def synthesis_forward_train(dec, y_nhwc: Tensor, x_ref: Optional[Tensor] = None):
+    d1, d2, d3, q1, q2 = dec.packed()
+    s1, v1 = kernels.deconv_igdn(y_nhwc, d1, dec.deconv1.bias, q1[0], q1[1], want_pre=True)
+    s2, v2 = kernels.deconv_igdn(s1, d2, dec.deconv2.bias, q2[0], q2[1], want_pre=True)
+    clipped, recon, sse = kernels.deconv3(s2, d3, dec.deconv3.bias, x_ref=x_ref, want_recon=True,
+                                          sse_unclipped=x_ref is not None)
+    return clipped, recon, sse, {"y": y_nhwc, "v1": v1, "s1": s1, "v2": v2, "s2": s2}
+
+
+def synthesis_backward(dec, saved: Dict[str, Tensor], g_recon: Tensor, g_bpp: Optional[Tensor] = None,
+                       rate_packed: Optional[Tensor] = None, count: float = 0.0):
+    """∂L/∂recon (NCHW) → (∂L/∂ỹ NHWC incl. the rate term when g_bpp is given, parameter
+    gradients of Synthesis_net_17, rate-parameter partials)."""
+    N = dec.out_channel_N
+    bq1, gq1, _ = dec.igdn1.bounds_f32()
+    bq2, gq2, _ = dec.igdn2.bounds_f32()
+    d3c = kernels.pack_weight(_lib.ICLR17_W_CONV1, dec.deconv3.weight, N)
+    d2c = kernels.pack_weight(_lib.ICLR17_W_CONV5, dec.deconv2.weight, N)
+    d1c = kernels.pack_weight(_lib.ICLR17_W_CONV5, dec.deconv1.weight, N)
+    q2 = dec.igdn2.effective_params_bwd()
+    q1 = dec.igdn1.effective_params_bwd()
+    g_v2, dnq2 = kernels.bwd_deconv3_igdn(g_recon, d3c, saved["v2"], *q2)
+    dWd3 = kernels.wgrad_k9(saved["s2"], g_recon)
+    dbd3 = kernels.bias_grad_nchw(g_recon)
+    g_v1, dnq1 = kernels.bwd_deconv_igdn(g_v2, d2c, saved["v1"], *q1)
+    dWd2 = kernels.wgrad_k5(saved["s1"], g_v2)
+    dbd2 = kernels.bias_grad_nhwc(g_v2)
+    y = saved["y"]
+    B, h, w, _ = y.shape
+    g_y, rpart = kernels.bwd_deconv_rate(g_v1, d1c, y if g_bpp is not None else None, rate_packed,
+                                         g_bpp, count, h, w)
+    dWd1 = kernels.wgrad_k5(y, g_v1)
+    dbd1 = kernels.bias_grad_nhwc(g_v1)
+    dbq2, dgq2 = kernels.gdn_param_grads(dnq2, saved["v2"], dec.igdn2.beta, dec.igdn2.gamma, bq2, gq2)
+    dbq1, dgq1 = kernels.gdn_param_grads(dnq1, saved["v1"], dec.igdn1.beta, dec.igdn1.gamma, bq1, gq1)
+    grads = {"deconv1.weight": dWd1, "deconv1.bias": dbd1, "igdn1.beta": dbq1, "igdn1.gamma": dgq1,
+             "deconv2.weight": dWd2, "deconv2.bias": dbd2, "igdn2.beta": dbq2, "igdn2.gamma": dgq2,
+             "deconv3.weight": dWd3, "deconv3.bias": dbd3}
+    return g_y, grads, rpart
+
+
+def _ordered(module, prefix: str, grads: Dict[str, Tensor]) -> List[Optional[Tensor]]:
+    return [grads.get(name) for name, _ in module.named_parameters()]
+
+
+# --------------------------------------------------------------------------- Functions
+class CodecTrainFn(torch.autograd.Function):
+    """ImageCompressor training forward: (clipped, ỹ NCHW-view, bpp, mse of unclipped recon)."""
+
+    @staticmethod
+    def forward(ctx, x, noise, net, *params):
+        ctx.set_materialize_grads(False)
+        enc, dec, be = net.Encoder, net.Decoder, net.bitEstimator
+        B, _, H, W = x.shape
+        a2, saved_a = analysis_features_train(enc, x)
+        _, _, w3, _, _ = enc.packed()
+        rate = be.packed()
+        y_tilde, bits_part = kernels.conv3_quant_rate(a2, w3, rate, noise)
+        clipped, recon, sse_part, saved_s = synthesis_forward_train(dec, y_tilde, x_ref=x)
+        _, bpp = kernels.reduce_partials(bits_part, 1.0 / (B * H * W), per_image=False)
+        _, mse = kernels.reduce_partials(sse_part, 1.0 / (B * 3 * H * W), per_image=False)
+        ctx.net = net
+        ctx.saved_a, ctx.saved_s = saved_a, saved_s
+        ctx.recon, ctx.x, ctx.rate, ctx.count = recon, x, rate, float(B * H * W)
+        return clipped, y_tilde.permute(0, 3, 1, 2), bpp, mse
+
+    @staticmethod
+    def backward(ctx, g_clipped, g_ytilde, g_bpp, g_mse):
+        net = ctx.net
+        enc, dec, be = net.Encoder, net.Decoder, net.bitEstimator
+        grads: List[Optional[Tensor]] = []
+        if g_clipped is None and g_mse is None:
+            g_recon = torch.zeros_like(ctx.recon)
+        else:
+            g_recon = kernels.grad_recon(ctx.recon, ctx.x, g_mse, g_clipped)
+        g_y, gs, rpart = synthesis_backward(dec, ctx.saved_s, g_recon, g_bpp, ctx.rate, ctx.count)
+        if g_ytilde is not None:
+            g_y = g_y + g_ytilde.permute(0, 2, 3, 1)
+        ga = analysis_backward(enc, ctx.saved_a, g_y.contiguous())
+        rg = kernels.rate_param_grads(rpart, be.params_in_order()) if g_bpp is not None else [None] * 11
+        grads += _ordered(enc, "Encoder.", ga)
+        grads += _ordered(dec, "Decoder.", gs)
+        names = [n for n, _ in be.named_parameters()]
+        order = ["f1.h", "f1.b", "f1.a", "f2.h", "f2.b", "f2.a", "f3.h", "f3.b", "f3.a", "f4.h", "f4.b"]
+        rmap = dict(zip(order, rg))
+        grads += [rmap[n] for n in names]
+        ctx.saved_a = ctx.saved_s = ctx.recon = None
+        return (None, None, None, *grads)
+
+
+class AnalysisFn(torch.autograd.Function):
+    """Analysis_net_17.forward with autograd: y (NCHW view of NHWC storage)."""
+
+    @staticmethod
+    def forward(ctx, x, enc, *params):
+        ctx.set_materialize_grads(False)
+        a2, saved = analysis_features_train(enc, x)
+        _, _, w3, _, _ = enc.packed()
+        ctx.enc, ctx.saved = enc, saved
+        return kernels.conv3(a2, w3).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, g_y):
+        if g_y is None:
+            return (None, None) + (None,) * len(list(ctx.enc.parameters()))
+        ga = analysis_backward(ctx.enc, ctx.saved, g_y.permute(0, 2, 3, 1).contiguous())
+        ctx.saved = None
+        return (None, None, *_ordered(ctx.enc, "", ga))
+
+
+class SynthesisFn(torch.autograd.Function):
+    """Synthesis_net_17.forward with autograd: unclipped reconstruction (NCHW)."""
+
+    @staticmethod
+    def forward(ctx, y, dec, *params):
+        ctx.set_materialize_grads(False)
+        _, recon, _, saved = synthesis_forward_train(dec, dec.to_nhwc(y))
+        ctx.dec, ctx.saved = dec, saved
+        return recon
+
+    @staticmethod
+    def backward(ctx, g_recon):
+        n_params = len(list(ctx.dec.parameters()))
+        if g_recon is None:
+            return (None, None) + (None,) * n_params
+        g_y, gs, _ = synthesis_backward(ctx.dec, ctx.saved, g_recon.contiguous())
+        ctx.saved = None
+        return (g_y.permute(0, 3, 1, 2), None, *_ordered(ctx.dec, "", gs))

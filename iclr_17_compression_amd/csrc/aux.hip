@@ -74,8 +74,9 @@ __global__ void pack_deconv9_kernel(const float* __restrict__ w, float* __restri
 
 // models/GDN.py:73-79 reparametrisation; gamma packed [C/4][C][4] (packed[q][i][e] = γ[i][4q+e]).
 __global__ void pack_gdn_kernel(const float* __restrict__ beta, const float* __restrict__ gamma,
-                                float* __restrict__ beta_eff, float* __restrict__ gp, int C,
-                                float bbound, float gbound, float ped) {
+                                float* __restrict__ beta_eff, float* __restrict__ gp,
+                                float* __restrict__ gpt, int C, float bbound, float gbound,
+                                float ped) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < C) {
     const float m = fmaxf(beta[i], bbound);
@@ -85,6 +86,10 @@ __global__ void pack_gdn_kernel(const float* __restrict__ beta, const float* __r
     const int e = i & 3, row = (i >> 2) % C, q = (i >> 2) / C;
     const float m = fmaxf(gamma[(long)row * C + 4 * q + e], gbound);
     gp[i] = m * m - ped;
+    if (gpt != nullptr) {
+      const float mt = fmaxf(gamma[(long)(4 * q + e) * C + row], gbound);
+      gpt[i] = mt * mt - ped;
+    }
   }
 }
 
@@ -185,6 +190,72 @@ __global__ void reduce_partials_kernel(const double* __restrict__ partial, int B
   if (threadIdx.x == 0 && total) *total = (float)(acc * scale);
 }
 
+// ∂L/∂recon of train.py's intended loss (mse of the unclipped recon, model.py:61) plus an optional
+// gradient arriving at the clipped output (clamp(0,1) backward mask), as autograd evaluates them:
+//   mean backward g/numel, pow backward ·(2·d), clamp backward · [0 ≤ r ≤ 1].
+__global__ void grad_recon_kernel(const float* __restrict__ recon, const float* __restrict__ x,
+                                  const float* __restrict__ g_mse, const float* __restrict__ g_clip,
+                                  long n, float numel, float* __restrict__ out) {
+  const float gm = g_mse != nullptr ? g_mse[0] / numel : 0.0f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float r = recon[i];
+    float g = 0.0f;
+    if (g_mse != nullptr) g = gm * (2.0f * (r - x[i]));
+    if (g_clip != nullptr && r >= 0.0f && r <= 1.0f) g = g + g_clip[i];
+    out[i] = g;
+  }
+}
+
+// GDN.py:73-79 backward: β_eff = lb(β)² − ped, LowerBound passes g where x ≥ bound or g < 0.
+__global__ void gdn_param_chain_kernel(const float* __restrict__ beta, const float* __restrict__ gamma,
+                                       const float* __restrict__ dbeta_eff,
+                                       const float* __restrict__ dgamma_eff, int C, float bbound,
+                                       float gbound, float* __restrict__ dbeta,
+                                       float* __restrict__ dgamma) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < C) {
+    const float x = beta[i], lb = fmaxf(x, bbound);
+    const float g = dbeta_eff[i] * (2.0f * lb);
+    dbeta[i] = (x >= bbound || g < 0.0f) ? g : 0.0f;
+  }
+  if (i < C * C) {
+    const float x = gamma[i], lb = fmaxf(x, gbound);
+    const float g = dgamma_eff[i] * (2.0f * lb);
+    dgamma[i] = (x >= gbound || g < 0.0f) ? g : 0.0f;
+  }
+}
+
+// Rate-model parameter gradients from per-tile partials [T][11][C] (fixed-order sum) through
+// softplus (h) and tanh (a): outputs in the order h1 b1 a1 h2 b2 a2 h3 b3 a3 h4 b4.
+struct RateGradPtrs {
+  float* p[11];
+};
+
+__global__ void rate_param_chain_kernel(const float* __restrict__ part, int T, int C, RatePtrs rp,
+                                        RateGradPtrs out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  for (int k = 0; k < 11; ++k) {
+    double s = 0.0;
+    for (int t = 0; t < T; ++t) s += (double)part[((long)t * 11 + k) * C + c];
+    const float g = (float)s;
+    const int layer = k / 3, role = k % 3;
+    float v;
+    if (role == 0) {  // d softplus(h) → dh : torch softplus_backward (beta 1, threshold 20)
+      const float h = rp.p[k][c];
+      const float z = expf(h);
+      v = h > 20.0f ? g : g * z / (z + 1.0f);
+    } else if (role == 1) {
+      v = g;
+    } else {          // d tanh(a) → da : tanh_backward on the forward output
+      const float ta = tanhf(rp.p[k][c]);
+      v = g * (1.0f - ta * ta);
+    }
+    (void)layer;
+    out.p[k][c] = v;
+  }
+}
+
 }  // namespace
 }  // namespace iclr17
 
@@ -231,12 +302,13 @@ int iclr17_pack_weight(int which, const float* w, float* packed, int N, void* st
 }
 
 int iclr17_pack_gdn(const float* beta, const float* gamma, float* beta_eff, float* gamma_packed,
-                    int C, float beta_bound, float gamma_bound, float pedestal, void* stream) {
+                    float* gamma_packed_t, int C, float beta_bound, float gamma_bound,
+                    float pedestal, void* stream) {
   ICLR17_REQUIRE(C > 0 && C % 4 == 0, ICLR17_EINVAL, "pack_gdn: C=%d must be a multiple of 4", C);
   ICLR17_REQUIRE(beta && gamma && beta_eff && gamma_packed, ICLR17_EINVAL, "pack_gdn: null pointer");
   const int total = C * C;
   hipLaunchKernelGGL(pack_gdn_kernel, dim3((total + 255) / 256), dim3(256), 0, S(stream), beta,
-                     gamma, beta_eff, gamma_packed, C, beta_bound, gamma_bound, pedestal);
+                     gamma, beta_eff, gamma_packed, gamma_packed_t, C, beta_bound, gamma_bound, pedestal);
   return check_launch("pack_gdn");
 }
 
@@ -302,6 +374,41 @@ int iclr17_reduce_partials(const double* partial, int B, int T, double* per_imag
   hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(256), 0, S(stream), partial, B, T,
                      per_image, total, scale);
   return check_launch("reduce_partials");
+}
+
+int iclr17_grad_recon(const float* recon, const float* x, const float* g_mse, const float* g_clip,
+                      int64_t n, float* g_recon, void* stream) {
+  ICLR17_REQUIRE(recon && x && g_recon && n > 0, ICLR17_EINVAL, "grad_recon: bad arguments");
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(grad_recon_kernel, dim3((unsigned)blocks), dim3(256), 0, S(stream), recon, x,
+                     g_mse, g_clip, (long)n, (float)n, g_recon);
+  return check_launch("grad_recon");
+}
+
+int iclr17_gdn_param_chain(const float* beta, const float* gamma, const float* dbeta_eff,
+                           const float* dgamma_eff, int C, float beta_bound, float gamma_bound,
+                           float* dbeta, float* dgamma, void* stream) {
+  ICLR17_REQUIRE(beta && gamma && dbeta_eff && dgamma_eff && dbeta && dgamma && C > 0,
+                 ICLR17_EINVAL, "gdn_param_chain: bad arguments");
+  hipLaunchKernelGGL(gdn_param_chain_kernel, dim3((C * C + 255) / 256), dim3(256), 0, S(stream),
+                     beta, gamma, dbeta_eff, dgamma_eff, C, beta_bound, gamma_bound, dbeta, dgamma);
+  return check_launch("gdn_param_chain");
+}
+
+int iclr17_rate_param_grad(const float* partial, int T, int C, const float* h1, const float* a1,
+                           const float* h2, const float* a2, const float* h3, const float* a3,
+                           const float* h4, float* dh1, float* db1, float* da1, float* dh2,
+                           float* db2, float* da2, float* dh3, float* db3, float* da3, float* dh4,
+                           float* db4, void* stream) {
+  RatePtrs rp = {{h1, nullptr, a1, h2, nullptr, a2, h3, nullptr, a3, h4, nullptr}};
+  RateGradPtrs o = {{dh1, db1, da1, dh2, db2, da2, dh3, db3, da3, dh4, db4}};
+  for (int i = 0; i < 11; ++i) ICLR17_REQUIRE(o.p[i], ICLR17_EINVAL, "rate_param_grad: null output %d", i);
+  ICLR17_REQUIRE(partial && T > 0 && C > 0 && h1 && a1 && h2 && a2 && h3 && a3 && h4, ICLR17_EINVAL,
+                 "rate_param_grad: bad arguments");
+  hipLaunchKernelGGL(rate_param_chain_kernel, dim3((C + 255) / 256), dim3(256), 0, S(stream),
+                     partial, T, C, rp, o);
+  return check_launch("rate_param_grad");
 }
 
 }  // extern "C"

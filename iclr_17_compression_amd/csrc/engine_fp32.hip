@@ -37,7 +37,10 @@ constexpr int BM = 64;        // output pixels per tile
 constexpr int KC = 32;        // input channels per k-step
 constexpr int ASTR = KC + 4;  // LDS row stride of the A tile (floats)
 
-enum Epi : int { EPI_GDN = 0, EPI_IGDN = 1, EPI_QUANT = 2, EPI_OUT3 = 3, EPI_PLAIN = 4 };
+enum Epi : int {
+  EPI_GDN = 0, EPI_IGDN = 1, EPI_QUANT = 2, EPI_OUT3 = 3, EPI_PLAIN = 4,
+  EPI_GDN_BWD = 5, EPI_IGDN_BWD = 6, EPI_RATE_BWD = 7
+};
 
 struct TapTable {
   int npx;            // phases along x
@@ -70,6 +73,15 @@ struct EngineArgs {
   // deconv3
   const float* xref;    // NCHW input image (SSE) or nullptr
   float* recon;         // unclipped NCHW or nullptr
+  int sse_unclipped;    // SSE of (recon − x) instead of (clipped − x) (training MSE, model.py:61)
+  // backward epilogues
+  const float* saved;   // GDN/IGDN bwd: the layer's saved pre-activation u (NHWC, output grid);
+                        // rate bwd: ỹ (NHWC)
+  const float* ggammaT; // γ packed transposed: packed[q][j][e] = γ[4q+e][j]
+  float* tout;          // GDN bwd: dn = ∂L/∂n (NHWC) for the parameter gradients
+  const float* gscale;  // rate bwd: device scalar ∂L/∂bpp (nullptr → no rate term)
+  float count;          // rate bwd: B·H·W (bpp denominator, model.py:78)
+  float* rpart;         // rate bwd: per-tile parameter partials [tiles][11][CO]
 };
 
 struct TileInfo {
@@ -115,6 +127,20 @@ __device__ __forceinline__ void store_tile_rows(const EngineArgs& a, const TileI
   }
 }
 
+// Inverse of store_tile_rows: NHWC rows of the tile's pixels → LDS (zeros outside the grid).
+template <int BN>
+__device__ __forceinline__ void load_tile_rows(const EngineArgs& a, const TileInfo& t,
+                                               const float* __restrict__ src, float* s, int ld,
+                                               int CO, int col0) {
+  constexpr int C4 = BN / 4;
+  for (int idx = threadIdx.x; idx < BM * C4; idx += 256) {
+    const int m = idx / C4, c4 = idx % C4;
+    const long p = out_pixel(a, t, m);
+    const f4 v = p < 0 ? f4{0.f, 0.f, 0.f, 0.f} : *(const f4*)(src + p * CO + col0 + c4 * 4);
+    *(f4*)(s + m * ld + c4 * 4) = v;
+  }
+}
+
 // Load the B fragments of one 32-deep k-step: packed weights [.][CIq][CO][4], quad rows
 // q0 .. q0+7, columns ncol0 + nt*16 + (lane & 15).
 template <int NT, int CO>
@@ -142,6 +168,43 @@ __device__ __forceinline__ void mfma_block(f4 (&acc)[MT][NT], const f4 (&af)[MT]
 }
 
 // ----------------------------------------------------------------------------- GDN epilogue
+// Channel contraction of an LDS tile: out[m][i] = Σ_j sX[m][j] · B[j][i], B packed
+// [CO/4][CO][4] (packed[q][i][e] = B[4q+e][i]) and read straight from L2, one k-block ahead.
+template <int CO, int MT, int NT, bool SQ = false>
+__device__ __forceinline__ void chan_gemm(f4 (&acc)[MT][NT], const float* sX,
+                                          const float* __restrict__ bp, int wm, int ncol0,
+                                          int lane) {
+  constexpr int XS = CO + 4;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
+  f4 g[NT], gn[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+    g[nt] = *(const f4*)(bp + ((long)(lane >> 4) * CO + ncol0 + nt * 16 + (lane & 15)) * 4);
+  constexpr int KB = CO / 16;
+#pragma unroll 2
+  for (int kb = 0; kb < KB; ++kb) {
+    if (kb + 1 < KB) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        gn[nt] = *(const f4*)(bp + ((long)((kb + 1) * 4 + (lane >> 4)) * CO + ncol0 + nt * 16 +
+                                    (lane & 15)) * 4);
+    }
+    f4 af[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      af[mt] = *(const f4*)(sX + (wm * MT * 16 + mt * 16 + (lane & 15)) * XS + kb * 16 +
+                            4 * (lane >> 4));
+      if (SQ) af[mt] = af[mt] * af[mt];
+    }
+    mfma_block<MT, NT>(acc, af, g);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) g[nt] = gn[nt];
+  }
+}
+
 // x (bias already added) in accumulator layout → GDN(x) (or IGDN) left in LDS sX[BM][CO+4].
 // models/GDN.py:83-90: n = conv2d(x², γ, β) = β + Σ_j γ[i][j]·x_j²;  y = x / √n | x·√n.
 // The caller guarantees smem is free on entry; on return every wave has passed a barrier after
@@ -165,31 +228,7 @@ __device__ __forceinline__ void gdn_core(const f4 (&x)[MT][NT], float* sX,
       }
   __syncthreads();
   f4 nacc[MT][NT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) nacc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
-  f4 g[NT], gn[NT];
-#pragma unroll
-  for (int nt = 0; nt < NT; ++nt)
-    g[nt] = *(const f4*)(gp + ((long)(lane >> 4) * CO + ncol0 + nt * 16 + (lane & 15)) * 4);
-  constexpr int KB = CO / 16;
-  for (int kb = 0; kb < KB; ++kb) {
-    if (kb + 1 < KB) {
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-        gn[nt] = *(const f4*)(gp + ((long)((kb + 1) * 4 + (lane >> 4)) * CO + ncol0 + nt * 16 +
-                                    (lane & 15)) * 4);
-    }
-    f4 af[MT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-      af[mt] = *(const f4*)(sX + (wm * MT * 16 + mt * 16 + (lane & 15)) * XS + kb * 16 +
-                            4 * (lane >> 4));
-    mfma_block<MT, NT>(nacc, af, g);
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) g[nt] = gn[nt];
-  }
+  chan_gemm<CO, MT, NT>(nacc, sX, gp, wm, ncol0, lane);
   __syncthreads();  // all reads of x² done
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
@@ -232,6 +271,157 @@ __device__ __forceinline__ void gdn_epilogue(f4 (&x)[MT][NT], float* smem, const
     acc_to_lds<MT, NT>(x, smem, XS, wm, ncol0, lane);
     __syncthreads();
     store_tile_rows<CO>(a, t, smem, XS, a.pre, CO, 0);
+  }
+}
+
+// ------------------------------------------------------------------ GDN / IGDN backward epilogue
+// g = ∂L/∂(GDN output) in accumulator layout (the dgrad GEMM of the NEXT layer); u = the saved
+// GDN input (pre-activation). Mirrors the autograd of models/GDN.py:83-90 op for op:
+//   n = β + γ·u², s = √n
+//   GDN : ∂u = g/s + 2u·(γᵀ dn),  dn = ((−g·u)/(s·s)) / (2s)      (div, sqrt backward)
+//   IGDN: ∂u = g·s + 2u·(γᵀ dn),  dn = (g·u) / (2s)               (mul, sqrt backward)
+// Stores ∂u (a.out) and dn (a.tout; dγ = Σ_p dn ⊗ u², dβ = Σ_p dn are reduced later).
+template <int CO, int MT, int NT, bool INVERSE>
+__device__ __forceinline__ void gdn_bwd_epilogue(f4 (&g)[MT][NT], float* smem, const EngineArgs& a,
+                                                 const TileInfo& t, int wm, int ncol0, int lane) {
+  constexpr int XS = CO + 4;
+  float* sX = smem;
+  load_tile_rows<CO>(a, t, a.saved, sX, XS, CO, 0);   // u, kept in LDS through GEMM 1
+  __syncthreads();
+  f4 acc2[MT][NT];
+  chan_gemm<CO, MT, NT, true>(acc2, sX, a.ggamma, wm, ncol0, lane);  // Σ_j γ[i][j] u_j² (fp32 square)
+  __syncthreads();
+  f4 u[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = ncol0 + nt * 16 + (lane & 15);
+        const int idx = (wm * MT * 16 + mt * 16 + 4 * (lane >> 4) + r) * XS + col;
+        const float uu = sX[idx];  // read, then rewritten by the same lane: no barrier needed
+        const float n = acc2[mt][nt][r] + a.gbeta[col];
+        const float sq = sqrtf(n);
+        const float gg = g[mt][nt][r];
+        float dn;
+        if (INVERSE) {
+          g[mt][nt][r] = gg * sq;
+          dn = (gg * uu) / (2.0f * sq);
+        } else {
+          g[mt][nt][r] = gg / sq;
+          dn = ((-gg * uu) / (sq * sq)) / (2.0f * sq);
+        }
+        u[mt][nt][r] = uu;
+        sX[idx] = dn;
+      }
+  __syncthreads();
+  chan_gemm<CO, MT, NT>(acc2, sX, a.ggammaT, wm, ncol0, lane);  // w_j = Σ_i γ[i][j] dn_i
+  store_tile_rows<CO>(a, t, sX, XS, a.tout, CO, 0);
+  __syncthreads();
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int idx = (wm * MT * 16 + mt * 16 + 4 * (lane >> 4) + r) * XS + ncol0 + nt * 16 + (lane & 15);
+        sX[idx] = g[mt][nt][r] + acc2[mt][nt][r] * (2.0f * u[mt][nt][r]);
+      }
+  __syncthreads();
+  store_tile_rows<CO>(a, t, sX, XS, a.out, CO, 0);
+}
+
+// ------------------------------------------------------------------------- rate backward epilogue
+// ∂L/∂ỹ = (decoder dgrad in acc) + ∂L/∂bpp / (B·H·W) · ∂bits/∂ỹ, and the per-channel parameter
+// gradients of the factorised model, as the autograd of model.py:71-78 / bitEstimator.py:20-25
+// evaluates them (per element; summed per tile here, over tiles later).
+__device__ __forceinline__ float rate_bwd_element(float z, const float* __restrict__ rp, int C,
+                                                  int c, float gsc, float (&pg)[11]) {
+  float xs[2][4], Ts[2][3], F[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float x = h == 0 ? z + 0.5f : z - 0.5f;
+    xs[h][0] = x;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float t = x * rp[(3 * k) * C + c] + rp[(3 * k + 1) * C + c];
+      const float T = tanhf(t);
+      x = t + T * rp[(3 * k + 2) * C + c];
+      Ts[h][k] = T;
+      xs[h][k + 1] = x;
+    }
+    const float t4 = x * rp[9 * C + c] + rp[10 * C + c];
+    F[h] = 1.0f / (1.0f + expf(-t4));
+  }
+  const float prob = F[0] - F[1];
+  const float raw = (-1.0f * logf(prob + 1e-10f)) / 0.693147182464599609375f;
+  const bool pass = raw >= 0.0f && raw <= 50.0f;          // clamp(·, 0, 50) backward mask
+  const float g0 = pass ? gsc : 0.0f;
+  const float gl = ((g0 / 0.693147182464599609375f) * -1.0f) / (prob + 1e-10f);
+  float dz = 0.0f;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const float gF = h == 0 ? gl : -gl;
+    const float gt4 = (gF * (1.0f - F[h])) * F[h];        // sigmoid backward
+    pg[10] += gt4;                                          // b4
+    pg[9] += gt4 * xs[h][3];                                // softplus(h4)
+    float gx = gt4 * rp[9 * C + c];
+#pragma unroll
+    for (int k = 2; k >= 0; --k) {
+      const float T = Ts[h][k];
+      const float gT = gx * rp[(3 * k + 2) * C + c];
+      pg[3 * k + 2] += gx * T;                              // tanh(a_k)
+      const float gt = gx + gT * (1.0f - T * T);            // tanh backward
+      pg[3 * k + 1] += gt;                                  // b_k
+      pg[3 * k] += gt * xs[h][k];                           // softplus(h_k)
+      gx = gt * rp[(3 * k) * C + c];
+    }
+    dz += gx;
+  }
+  return dz;
+}
+
+template <int CO, int BN, int MT, int NT>
+__device__ __forceinline__ void rate_bwd_epilogue(f4 (&acc)[MT][NT], float* smem, const EngineArgs& a,
+                                                  const TileInfo& t, int wm, int ncol0, int lane) {
+  constexpr int OS = BN + 4;
+  float* sO = smem;
+  const int cbase = t.nb * BN;
+  const bool rate = a.gscale != nullptr;
+  if (rate) load_tile_rows<BN>(a, t, a.saved, sO, OS, CO, cbase);
+  __syncthreads();
+  const float gsc = rate ? a.gscale[0] / a.count : 0.0f;
+  float pg[NT][11];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int k = 0; k < 11; ++k) pg[nt][k] = 0.0f;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * MT * 16 + mt * 16 + 4 * (lane >> 4) + r;
+        const int lcol = ncol0 - cbase + nt * 16 + (lane & 15);
+        float v = acc[mt][nt][r];
+        if (rate && out_pixel(a, t, row) >= 0)
+          v += rate_bwd_element(sO[row * OS + lcol], a.rate, CO, cbase + lcol, gsc, pg[nt]);
+        sO[row * OS + lcol] = v;
+      }
+  __syncthreads();
+  store_tile_rows<BN>(a, t, sO, OS, a.out, CO, cbase);
+  if (rate) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int k = 0; k < 11; ++k) {
+        float v = pg[nt][k];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        if (lane < 16) a.rpart[((long)blockIdx.x * 11 + k) * CO + ncol0 + nt * 16 + lane] = v;
+      }
   }
 }
 
@@ -340,7 +530,7 @@ __device__ __forceinline__ void out3_epilogue(f4 (&acc)[MT][NT], float* smem, co
       const f4 v = f4{s[0], s[1], s[2], s[3]};
       const long off = (((long)t.b * 3 + co) * H + oy) * W + ox;
       *(f4*)(dst + off) = v;
-      if (pass == 0 && a.xref != nullptr) {
+      if (pass == (a.sse_unclipped ? 1 : 0) && a.xref != nullptr) {
         const f4 xr = *(const f4*)(a.xref + off);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -370,7 +560,8 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
   constexpr int NT = BN / WN / 16;
   constexpr int NCH = CI / KC;
   constexpr int LDS_A = 2 * BM * ASTR;
-  constexpr int LDS_X = (EPI == EPI_GDN || EPI == EPI_IGDN) ? BM * (CO + 4) : 0;
+  constexpr int LDS_X = (EPI == EPI_GDN || EPI == EPI_IGDN || EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD)
+                            ? BM * (CO + 4) : 0;
   constexpr int LDS_O = BM * (BN + 4) + 8;
   constexpr int LDS_3 = 3 * 32 * 33 + 8;
   constexpr int L1 = LDS_A > LDS_X ? LDS_A : LDS_X;
@@ -475,6 +666,11 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
     quant_epilogue<CO, BN, MT, NT, WN>(acc, smem, a, t, wm, ncol0, lane, wave);
   } else if constexpr (EPI == EPI_OUT3) {
     out3_epilogue<MT, NT>(acc, smem, a, t, wm, lane, wave);
+  } else if constexpr (EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD) {
+    static_assert(BN == CO, "GDN backward needs every channel of a pixel in the workgroup");
+    gdn_bwd_epilogue<CO, MT, NT, EPI == EPI_IGDN_BWD>(acc, smem, a, t, wm, ncol0, lane);
+  } else if constexpr (EPI == EPI_RATE_BWD) {
+    rate_bwd_epilogue<CO, BN, MT, NT>(acc, smem, a, t, wm, ncol0, lane);
   } else {
     constexpr int OS = BN + 4;
 #pragma unroll
@@ -502,7 +698,10 @@ constexpr int P1 = 37;                    // patch side: 8·4 + 9 − 4
 constexpr int P1PLANE = P1 * P1;
 constexpr int P1ZERO = 3 * P1PLANE;       // index of the zero slot
 
-template <int CO, bool INVERSE_UNUSED = false>
+// EPI_GDN: analysis conv1 + bias + GDN1 (forward). EPI_IGDN_BWD: the same contraction is the
+// input gradient of the synthesis deconv3 (its adjoint: conv2d(g_recon, W, stride 4, pad 4)),
+// fused with the IGDN2 backward.
+template <int CO, int EPI>
 __global__ void __launch_bounds__(256) conv1_gdn_kernel(const EngineArgs a) {
   constexpr int WN = 4;
   constexpr int MT = BM / 16;
@@ -580,13 +779,18 @@ __global__ void __launch_bounds__(256) conv1_gdn_kernel(const EngineArgs a) {
       for (int nt = 0; nt < NT; ++nt) bcur[kk][nt] = bnxt[kk][nt];
   }
   __syncthreads();  // patch reads done before the epilogue reuses LDS
+  if constexpr (EPI == EPI_GDN) {
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
+      for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[mt][nt][r] += a.bias[ncol0 + nt * 16 + (lane & 15)];
-  gdn_epilogue<CO, MT, NT, false>(acc, smem, a, t, wm, ncol0, lane);
+        for (int r = 0; r < 4; ++r) acc[mt][nt][r] += a.bias[ncol0 + nt * 16 + (lane & 15)];
+    gdn_epilogue<CO, MT, NT, false>(acc, smem, a, t, wm, ncol0, lane);
+  } else {
+    static_assert(EPI == EPI_IGDN_BWD, "conv1 kernel epilogues: GDN fwd, IGDN bwd");
+    gdn_bwd_epilogue<CO, MT, NT, true>(acc, smem, a, t, wm, ncol0, lane);
+  }
 }
 
 // --------------------------------------------------------------------- stand-alone GDN / IGDN
@@ -744,28 +948,31 @@ void deconv_phase_taps(int K, int s, int p, int ry, int rx, int* kh_out, int* kw
   *count = n;
 }
 
-template <int N>
+template <int N, int EPI = EPI_GDN>
 int launch_conv1(const float* x, int B, int H, int W, const float* wp, const float* bias,
-                 const float* beta, const float* gamma, float* out, float* pre, hipStream_t st) {
+                 const float* beta, const float* gamma, float* out, float* pre, hipStream_t st,
+                 const EngineArgs* bwd = nullptr) {
   EngineArgs a;
   memset(&a, 0, sizeof(a));
+  if (bwd) a = *bwd;
   a.in = x; a.w = wp; a.bias = bias; a.gbeta = beta; a.ggamma = gamma; a.out = out; a.pre = pre;
   a.B = B; a.Hin = H; a.Win = W; a.Hout = H / 4; a.Wout = W / 4;
   a.gh = H / 4; a.gw = W / 4; a.tiles_y = (a.gh + 7) / 8; a.tiles_x = (a.gw + 7) / 8;
   a.sin = 4; a.sout = 1;
   a.tt.npx = 1; a.tt.nph = 1;
   dim3 grid(a.tiles_x * a.tiles_y * B, 1);
-  hipLaunchKernelGGL((conv1_gdn_kernel<N>), grid, dim3(256), 0, st, a);
-  return check_launch("conv1_gdn");
+  hipLaunchKernelGGL((conv1_gdn_kernel<N, EPI>), grid, dim3(256), 0, st, a);
+  return check_launch(EPI == EPI_GDN ? "conv1_gdn" : "bwd_deconv3_igdn");
 }
 
 template <int N, int EPI>
 int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, const float* bias,
                  const float* beta, const float* gamma, float* out, float* pre, int qmode,
                  const float* noise, const float* rate, float* yhat, double* partial,
-                 hipStream_t st) {
+                 hipStream_t st, const EngineArgs* bwd = nullptr) {
   EngineArgs a;
   memset(&a, 0, sizeof(a));
+  if (bwd) a = *bwd;
   a.in = in; a.w = wp; a.bias = bias; a.gbeta = beta; a.ggamma = gamma; a.out = out; a.pre = pre;
   a.B = B; a.Hin = Hin; a.Win = Win; a.Hout = Hin / 2; a.Wout = Win / 2;
   a.gh = a.Hout; a.gw = a.Wout; a.tiles_y = (a.gh + 7) / 8; a.tiles_x = (a.gw + 7) / 8;
@@ -778,11 +985,11 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
     dim3 grid(a.tiles_x * a.tiles_y * B, N / BN);
     hipLaunchKernelGGL((engine_kernel<N, N, BN, 1, 4, EPI_QUANT>), grid, dim3(256), 0, st, a);
     return check_launch("conv3_quant_rate");
-  } else if constexpr (EPI == EPI_PLAIN) {
+  } else if constexpr (EPI == EPI_PLAIN || EPI == EPI_RATE_BWD) {
     constexpr int BN = 64;
     dim3 grid(a.tiles_x * a.tiles_y * B, N / BN);
-    hipLaunchKernelGGL((engine_kernel<N, N, BN, 1, 4, EPI_PLAIN>), grid, dim3(256), 0, st, a);
-    return check_launch("conv3");
+    hipLaunchKernelGGL((engine_kernel<N, N, BN, 1, 4, EPI>), grid, dim3(256), 0, st, a);
+    return check_launch(EPI == EPI_PLAIN ? "conv3" : "bwd_deconv1_rate");
   } else {
     dim3 grid(a.tiles_x * a.tiles_y * B, 1);
     hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI>), grid, dim3(256), 0, st, a);
@@ -790,26 +997,30 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
   }
 }
 
-template <int N>
+template <int N, int EPI = EPI_IGDN>
 int launch_deconv5(const float* in, int B, int h, int w, const float* wp, const float* bias,
-                   const float* beta, const float* gamma, float* out, float* pre, hipStream_t st) {
+                   const float* beta, const float* gamma, float* out, float* pre, hipStream_t st,
+                   const EngineArgs* bwd = nullptr) {
   EngineArgs a;
   memset(&a, 0, sizeof(a));
+  if (bwd) a = *bwd;
   a.in = in; a.w = wp; a.bias = bias; a.gbeta = beta; a.ggamma = gamma; a.out = out; a.pre = pre;
   a.B = B; a.Hin = h; a.Win = w; a.Hout = 2 * h; a.Wout = 2 * w;
   a.gh = h; a.gw = w; a.tiles_y = (h + 7) / 8; a.tiles_x = (w + 7) / 8;
   a.sin = 1; a.sout = 2;
   fill_deconv_taps(a.tt, 5, 2, 2);
   dim3 grid(a.tiles_x * a.tiles_y * 4 * B, 1);
-  hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI_IGDN>), grid, dim3(256), 0, st, a);
-  return check_launch("deconv_igdn");
+  hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI>), grid, dim3(256), 0, st, a);
+  return check_launch(EPI == EPI_IGDN ? "deconv_igdn" : "bwd_conv_gdn");
 }
 
 template <int N>
 int launch_deconv3(const float* in, int B, int H, int W, const float* wp, const float* bias,
-                   const float* x, float* clipped, float* recon, double* partial, hipStream_t st) {
+                   const float* x, float* clipped, float* recon, double* partial, int sse_unclipped,
+                   hipStream_t st) {
   EngineArgs a;
   memset(&a, 0, sizeof(a));
+  a.sse_unclipped = sse_unclipped;
   a.in = in; a.w = wp; a.bias = bias; a.out = clipped; a.recon = recon; a.xref = x;
   a.partial = partial;
   a.B = B; a.Hin = H / 4; a.Win = W / 4; a.Hout = H; a.Wout = W;
@@ -911,14 +1122,80 @@ int iclr17_output_partials_per_image(int H, int W) {
 
 int iclr17_synthesis_deconv3(const float* in, int B, int H, int W, int N, const float* w_packed,
                              const float* bias, const float* x, float* clipped, float* recon,
-                             double* sse_partial, void* stream) {
+                             double* sse_partial, int sse_unclipped, void* stream) {
   int rc = check_dims(B, H, W, N);
   if (rc) return rc;
   ICLR17_REQUIRE(in && w_packed && bias && clipped, ICLR17_EINVAL, "deconv3: null pointer");
   ICLR17_REQUIRE(x == nullptr || sse_partial != nullptr, ICLR17_EINVAL,
                  "deconv3: sse_partial required with x");
-  return N == 192 ? launch_deconv3<192>(in, B, H, W, w_packed, bias, x, clipped, recon, sse_partial, S(stream))
-                  : launch_deconv3<128>(in, B, H, W, w_packed, bias, x, clipped, recon, sse_partial, S(stream));
+  ICLR17_REQUIRE(!sse_unclipped || recon != nullptr, ICLR17_EINVAL,
+                 "deconv3: the unclipped SSE needs the recon output");
+  return N == 192 ? launch_deconv3<192>(in, B, H, W, w_packed, bias, x, clipped, recon, sse_partial, sse_unclipped, S(stream))
+                  : launch_deconv3<128>(in, B, H, W, w_packed, bias, x, clipped, recon, sse_partial, sse_unclipped, S(stream));
+}
+
+static EngineArgs bwd_args(const float* saved, const float* gammaT, float* tout) {
+  EngineArgs a;
+  memset(&a, 0, sizeof(a));
+  a.saved = saved;
+  a.ggammaT = gammaT;
+  a.tout = tout;
+  return a;
+}
+
+int iclr17_bwd_deconv3_igdn(const float* g_recon, int B, int H, int W, int N,
+                            const float* w_packed, const float* v_saved, const float* beta_eff,
+                            const float* gamma_packed, const float* gamma_packed_t, float* g_v,
+                            float* dn, void* stream) {
+  int rc = check_dims(B, H, W, N);
+  if (rc) return rc;
+  ICLR17_REQUIRE(g_recon && w_packed && v_saved && beta_eff && gamma_packed && gamma_packed_t &&
+                     g_v && dn, ICLR17_EINVAL, "bwd_deconv3_igdn: null pointer");
+  EngineArgs b = bwd_args(v_saved, gamma_packed_t, dn);
+  return N == 192 ? launch_conv1<192, EPI_IGDN_BWD>(g_recon, B, H, W, w_packed, nullptr, beta_eff, gamma_packed, g_v, nullptr, S(stream), &b)
+                  : launch_conv1<128, EPI_IGDN_BWD>(g_recon, B, H, W, w_packed, nullptr, beta_eff, gamma_packed, g_v, nullptr, S(stream), &b);
+}
+
+int iclr17_bwd_deconv_igdn(const float* g_v, int B, int h, int w, int N, const float* w_packed,
+                           const float* v_prev, const float* beta_eff, const float* gamma_packed,
+                           const float* gamma_packed_t, float* g_v_prev, float* dn, void* stream) {
+  ICLR17_REQUIRE(B > 0 && h > 0 && w > 0, ICLR17_EINVAL, "bwd_deconv_igdn: bad shape");
+  ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "channel count N=%d unsupported", N);
+  ICLR17_REQUIRE(g_v && w_packed && v_prev && beta_eff && gamma_packed && gamma_packed_t &&
+                     g_v_prev && dn, ICLR17_EINVAL, "bwd_deconv_igdn: null pointer");
+  EngineArgs b = bwd_args(v_prev, gamma_packed_t, dn);
+  return N == 192 ? launch_conv5<192, EPI_IGDN_BWD>(g_v, B, 2 * h, 2 * w, w_packed, nullptr, beta_eff, gamma_packed, g_v_prev, nullptr, 0, nullptr, nullptr, nullptr, nullptr, S(stream), &b)
+                  : launch_conv5<128, EPI_IGDN_BWD>(g_v, B, 2 * h, 2 * w, w_packed, nullptr, beta_eff, gamma_packed, g_v_prev, nullptr, 0, nullptr, nullptr, nullptr, nullptr, S(stream), &b);
+}
+
+int iclr17_rate_bwd_partials(int h, int w) { return ((h + 7) / 8) * ((w + 7) / 8); }
+
+int iclr17_bwd_deconv_rate(const float* g_v, int B, int h, int w, int N, const float* w_packed,
+                           const float* y_tilde, const float* rate_packed, const float* g_bpp,
+                           float count, float* g_y, float* rate_partial, void* stream) {
+  ICLR17_REQUIRE(B > 0 && h > 0 && w > 0, ICLR17_EINVAL, "bwd_deconv_rate: bad shape");
+  ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "channel count N=%d unsupported", N);
+  ICLR17_REQUIRE(g_v && w_packed && g_y, ICLR17_EINVAL, "bwd_deconv_rate: null pointer");
+  ICLR17_REQUIRE(g_bpp == nullptr || (y_tilde && rate_packed && rate_partial && count > 0),
+                 ICLR17_EINVAL, "bwd_deconv_rate: rate term needs y_tilde, rate params, partials");
+  EngineArgs b = bwd_args(y_tilde, nullptr, nullptr);
+  b.gscale = g_bpp;
+  b.count = count;
+  b.rpart = rate_partial;
+  return N == 192 ? launch_conv5<192, EPI_RATE_BWD>(g_v, B, 2 * h, 2 * w, w_packed, nullptr, nullptr, nullptr, g_y, nullptr, 0, nullptr, rate_packed, nullptr, nullptr, S(stream), &b)
+                  : launch_conv5<128, EPI_RATE_BWD>(g_v, B, 2 * h, 2 * w, w_packed, nullptr, nullptr, nullptr, g_y, nullptr, 0, nullptr, rate_packed, nullptr, nullptr, S(stream), &b);
+}
+
+int iclr17_bwd_conv_gdn(const float* g_u, int B, int h, int w, int N, const float* w_packed,
+                        const float* u_prev, const float* beta_eff, const float* gamma_packed,
+                        const float* gamma_packed_t, float* g_u_prev, float* dn, void* stream) {
+  ICLR17_REQUIRE(B > 0 && h > 0 && w > 0, ICLR17_EINVAL, "bwd_conv_gdn: bad shape");
+  ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "channel count N=%d unsupported", N);
+  ICLR17_REQUIRE(g_u && w_packed && u_prev && beta_eff && gamma_packed && gamma_packed_t &&
+                     g_u_prev && dn, ICLR17_EINVAL, "bwd_conv_gdn: null pointer");
+  EngineArgs b = bwd_args(u_prev, gamma_packed_t, dn);
+  return N == 192 ? launch_deconv5<192, EPI_GDN_BWD>(g_u, B, h, w, w_packed, nullptr, beta_eff, gamma_packed, g_u_prev, nullptr, S(stream), &b)
+                  : launch_deconv5<128, EPI_GDN_BWD>(g_u, B, h, w, w_packed, nullptr, beta_eff, gamma_packed, g_u_prev, nullptr, S(stream), &b);
 }
 
 int iclr17_gdn(const float* x, int B, int C, int H, int W, int layout, int inverse,

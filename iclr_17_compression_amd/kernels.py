@@ -70,8 +70,9 @@ def pack_weight(which: int, w: Tensor, N: int) -> Tensor:
 
 
 def pack_gdn(beta: Tensor, gamma: Tensor, beta_bound: float = DEFAULT_BETA_BOUND,
-             gamma_bound: float = DEFAULT_GAMMA_BOUND,
-             pedestal: float = DEFAULT_PEDESTAL) -> Tuple[Tensor, Tensor]:
+             gamma_bound: float = DEFAULT_GAMMA_BOUND, pedestal: float = DEFAULT_PEDESTAL,
+             transposed: bool = False):
+    """(beta_eff, gamma_packed[, gamma_packed_t]) — GDN.py:73-79 effective parameters."""
     _check(beta, "beta", 1)
     _check(gamma, "gamma", 2)
     C = beta.shape[0]
@@ -81,10 +82,11 @@ def pack_gdn(beta: Tensor, gamma: Tensor, beta_bound: float = DEFAULT_BETA_BOUND
     gamma = gamma.detach().contiguous()
     beta_eff = torch.empty(C, device=beta.device, dtype=torch.float32)
     gp = torch.empty(C * C, device=beta.device, dtype=torch.float32)
-    call("iclr17_pack_gdn", _p(beta), _p(gamma), _p(beta_eff), _p(gp), C,
+    gpt = torch.empty(C * C, device=beta.device, dtype=torch.float32) if transposed else None
+    call("iclr17_pack_gdn", _p(beta), _p(gamma), _p(beta_eff), _p(gp), _p(gpt), C,
          ctypes.c_float(beta_bound), ctypes.c_float(gamma_bound), ctypes.c_float(pedestal),
          _stream(beta))
-    return beta_eff, gp
+    return (beta_eff, gp, gpt) if transposed else (beta_eff, gp)
 
 
 def pack_rate(params: Sequence[Tensor]) -> Tensor:
@@ -193,7 +195,7 @@ def output_partials_per_image(H: int, W: int) -> int:
 
 
 def deconv3(h: Tensor, wp: Tensor, bias: Tensor, x_ref: Optional[Tensor] = None,
-            want_recon: bool = False):
+            want_recon: bool = False, sse_unclipped: bool = False):
     """synthesis_17.py:23-25 + model.py:59: NHWC [B,H/4,W/4,N] → clipped NCHW [B,3,H,W].
 
     Returns (clipped, recon_unclipped | None, sse_partial [B,T] | None)."""
@@ -212,7 +214,7 @@ def deconv3(h: Tensor, wp: Tensor, bias: Tensor, x_ref: Optional[Tensor] = None,
         x_ref = x_ref.contiguous()
         partial = torch.empty(B, output_partials_per_image(H, W), device=h.device, dtype=torch.float64)
     call("iclr17_synthesis_deconv3", _p(h.contiguous()), B, H, W, N, _p(wp), _p(bias), _p(x_ref),
-         _p(clipped), _p(recon), _p(partial), _stream(h))
+         _p(clipped), _p(recon), _p(partial), int(sse_unclipped), _stream(h))
     return clipped, recon, partial
 
 
@@ -303,3 +305,134 @@ def rate_bits(z: Tensor, rate_packed: Tensor) -> Tensor:
     partial = torch.empty(B, T, device=z.device, dtype=torch.float64)
     call("iclr17_rate_bits", _p(src), B, C, h, w, layout, _p(rate_packed), _p(partial), _stream(z))
     return partial
+
+
+# ------------------------------------------------------------------------------ backward
+def grad_recon(recon: Tensor, x: Tensor, g_mse: Optional[Tensor], g_clip: Optional[Tensor]) -> Tensor:
+    """∂L/∂recon for L using mean((recon−x)²) (g_mse, 0-dim) and/or clamp(recon,0,1) (g_clip)."""
+    _check(recon, "recon")
+    out = torch.empty_like(recon)
+    gm = g_mse.detach().reshape(()).contiguous() if g_mse is not None else None
+    gc = g_clip.detach().contiguous() if g_clip is not None else None
+    call("iclr17_grad_recon", _p(recon), _p(x.contiguous()), _p(gm), _p(gc), recon.numel(),
+         _p(out), _stream(recon))
+    return out
+
+
+def bwd_deconv3_igdn(g_recon: Tensor, wp_conv1form: Tensor, v_saved: Tensor, beta_eff: Tensor,
+                     gp: Tensor, gpt: Tensor):
+    """deconv3 input-gradient fused with IGDN2 backward → (g_v2 NHWC, dn NHWC)."""
+    B, _, H, W = g_recon.shape
+    N = v_saved.shape[3]
+    g_v = torch.empty_like(v_saved)
+    dn = torch.empty_like(v_saved)
+    call("iclr17_bwd_deconv3_igdn", _p(g_recon.contiguous()), B, H, W, N, _p(wp_conv1form),
+         _p(v_saved), _p(beta_eff), _p(gp), _p(gpt), _p(g_v), _p(dn), _stream(g_recon))
+    return g_v, dn
+
+
+def bwd_deconv_igdn(g_v: Tensor, wp_conv5form: Tensor, v_prev: Tensor, beta_eff: Tensor, gp: Tensor,
+                    gpt: Tensor):
+    """deconv2 input-gradient fused with IGDN1 backward → (g_v1 NHWC, dn NHWC)."""
+    B, h, w, N = v_prev.shape
+    g_prev = torch.empty_like(v_prev)
+    dn = torch.empty_like(v_prev)
+    call("iclr17_bwd_deconv_igdn", _p(g_v.contiguous()), B, h, w, N, _p(wp_conv5form), _p(v_prev),
+         _p(beta_eff), _p(gp), _p(gpt), _p(g_prev), _p(dn), _stream(g_v))
+    return g_prev, dn
+
+
+def bwd_deconv_rate(g_v1: Tensor, wp_conv5form: Tensor, y_tilde: Optional[Tensor],
+                    rate_packed: Optional[Tensor], g_bpp: Optional[Tensor], count: float,
+                    h: int, w: int):
+    """deconv1 input-gradient (+ rate backward when g_bpp is given) → (g_y NHWC, rate partials)."""
+    B, _, _, N = g_v1.shape
+    g_y = torch.empty(B, h, w, N, device=g_v1.device, dtype=torch.float32)
+    part = None
+    gb = None
+    if g_bpp is not None:
+        T = query("iclr17_rate_bwd_partials", h, w)
+        part = torch.empty(B * T, 11, N, device=g_v1.device, dtype=torch.float32)
+        gb = g_bpp.detach().reshape(()).contiguous()
+    call("iclr17_bwd_deconv_rate", _p(g_v1.contiguous()), B, h, w, N, _p(wp_conv5form), _p(y_tilde),
+         _p(rate_packed), _p(gb), ctypes.c_float(count), _p(g_y), _p(part), _stream(g_v1))
+    return g_y, part
+
+
+def bwd_conv_gdn(g_u: Tensor, wp_deconv5form: Tensor, u_prev: Tensor, beta_eff: Tensor, gp: Tensor,
+                 gpt: Tensor):
+    """conv3/conv2 input-gradient fused with GDN2/GDN1 backward → (g_u_prev NHWC, dn NHWC)."""
+    B, h, w, N = g_u.shape
+    g_prev = torch.empty_like(u_prev)
+    dn = torch.empty_like(u_prev)
+    call("iclr17_bwd_conv_gdn", _p(g_u.contiguous()), B, h, w, N, _p(wp_deconv5form), _p(u_prev),
+         _p(beta_eff), _p(gp), _p(gpt), _p(g_prev), _p(dn), _stream(g_u))
+    return g_prev, dn
+
+
+def wgrad_k5(G: Tensor, X: Tensor) -> Tensor:
+    """dW [M][C][5][5] = Σ G[b,o,m] · X[b,2o−2+k,c] (NHWC G [B,Ho,Wo,M], X [B,2Ho,2Wo,C])."""
+    B, Ho, Wo, M = G.shape
+    C = X.shape[3]
+    ws = torch.empty(query("iclr17_wgrad_workspace_size", 5, B, Ho, Wo, M, C), device=G.device,
+                     dtype=torch.float32)
+    dW = torch.empty(M, C, 5, 5, device=G.device, dtype=torch.float32)
+    call("iclr17_wgrad_k5", _p(G.contiguous()), _p(X.contiguous()), B, Ho, Wo, M, C, _p(ws), _p(dW),
+         _stream(G))
+    return dW
+
+
+def wgrad_k9(G: Tensor, X: Tensor) -> Tensor:
+    """dW [M][3][9][9] = Σ G[b,o,m] · X[b,c,4o−4+k] (G NHWC [B,Ho,Wo,M], X NCHW [B,3,4Ho,4Wo])."""
+    B, Ho, Wo, M = G.shape
+    ws = torch.empty(query("iclr17_wgrad_workspace_size", 9, B, Ho, Wo, M, 3), device=G.device,
+                     dtype=torch.float32)
+    dW = torch.empty(M, 3, 9, 9, device=G.device, dtype=torch.float32)
+    call("iclr17_wgrad_k9", _p(G.contiguous()), _p(X.contiguous()), B, Ho, Wo, M, _p(ws), _p(dW),
+         _stream(G))
+    return dW
+
+
+def gdn_param_grads(dn: Tensor, u: Tensor, beta: Tensor, gamma: Tensor,
+                    beta_bound: float = DEFAULT_BETA_BOUND, gamma_bound: float = DEFAULT_GAMMA_BOUND):
+    """GDN parameter gradients (dβ, dγ) in the raw-parameter space (through GDN.py:73-79)."""
+    C = dn.shape[-1]
+    P = dn.numel() // C
+    ws = torch.empty(query("iclr17_gdn_wgrad_workspace_size", P, C), device=dn.device, dtype=torch.float32)
+    dge = torch.empty(C, C, device=dn.device, dtype=torch.float32)
+    dbe = torch.empty(C, device=dn.device, dtype=torch.float32)
+    call("iclr17_gdn_wgrad", _p(dn.contiguous()), _p(u.contiguous()), P, C, _p(ws), _p(dge), _p(dbe),
+         _stream(dn))
+    db = torch.empty_like(dbe)
+    dg = torch.empty_like(dge)
+    call("iclr17_gdn_param_chain", _p(beta.detach().contiguous()), _p(gamma.detach().contiguous()),
+         _p(dbe), _p(dge), C, ctypes.c_float(beta_bound), ctypes.c_float(gamma_bound), _p(db), _p(dg),
+         _stream(dn))
+    return db, dg
+
+
+def bias_grad_nhwc(G: Tensor) -> Tensor:
+    C = G.shape[-1]
+    P = G.numel() // C
+    ws = torch.empty(64 * C, device=G.device, dtype=torch.float32)
+    db = torch.empty(C, device=G.device, dtype=torch.float32)
+    call("iclr17_bias_grad_nhwc", _p(G.contiguous()), P, C, _p(ws), _p(db), _stream(G))
+    return db
+
+
+def bias_grad_nchw(G: Tensor) -> Tensor:
+    B, C, H, W = G.shape
+    ws = torch.empty(B * C, device=G.device, dtype=torch.float32)
+    db = torch.empty(C, device=G.device, dtype=torch.float32)
+    call("iclr17_bias_grad_nchw", _p(G.contiguous()), B, C, H * W, _p(ws), _p(db), _stream(G))
+    return db
+
+
+def rate_param_grads(partial: Tensor, params: Sequence[Tensor]):
+    """BitEstimator grads (h1 b1 a1 h2 b2 a2 h3 b3 a3 h4 b4) from rate partials [T,11,C]."""
+    T, _, C = partial.shape
+    h1, b1, a1, h2, b2, a2, h3, b3, a3, h4, b4 = [p.detach().reshape(-1).contiguous() for p in params]
+    outs = [torch.empty(C, device=partial.device, dtype=torch.float32) for _ in range(11)]
+    call("iclr17_rate_param_grad", _p(partial), T, C, _p(h1), _p(a1), _p(h2), _p(a2), _p(h3), _p(a3),
+         _p(h4), *[_p(o) for o in outs], _stream(partial))
+    return [o.view(1, C, 1, 1) for o in outs]

@@ -82,13 +82,34 @@ class ImageCompressor(nn.Module):
                 "sse_partial": sse_partial, "recon": recon, "y": q[2] if want_y else None}
 
     def forward(self, input_image, noise: Optional[torch.Tensor] = None):
-        from .autograd import no_backward
+        """model.py:47-80 → (clipped_recon, ŷ or ỹ, bpp). In training mode with autograd on, the
+        fused training kernels run and every output is differentiable."""
+        from .autograd import CodecTrainFn, needs_grad, no_backward
+        params = list(self.parameters())
+        if self.training and needs_grad(input_image, params):
+            clipped, y_tilde, bpp, _ = self._train_outputs(input_image, noise, params)
+            return clipped, y_tilde, bpp
         B, _, H, W = input_image.shape
         out = self.run(input_image, noise=noise)
         _, bpp = kernels.reduce_partials(out["bits_partial"], scale=1.0 / (B * H * W), per_image=False)
         y_hat = out["y_hat"].permute(0, 3, 1, 2)
-        clipped = no_backward(out["clipped"], "ImageCompressor", list(self.parameters()), input_image)
+        clipped = no_backward(out["clipped"], "ImageCompressor (eval mode)", params, input_image)
         return clipped, y_hat, bpp
+
+    def _train_outputs(self, x, noise, params):
+        from .autograd import CodecTrainFn
+        kernels._check(x, "image", 4)
+        if x.requires_grad:
+            raise kernels.Iclr17Error("iclr17: gradients w.r.t. the input image are not implemented")
+        if noise is None:
+            noise = self._latent_noise(x)
+        return CodecTrainFn.apply(x.contiguous(), noise.contiguous(), self, *params)
+
+    def forward_train(self, input_image, noise: Optional[torch.Tensor] = None):
+        """The tuple train.py:97 unpacks, as model.py:81 intends:
+        (clipped_recon, mse of the UNclipped recon (model.py:61), bpp), all differentiable."""
+        clipped, _, bpp, mse = self._train_outputs(input_image, noise, list(self.parameters()))
+        return clipped, mse, bpp
 
     @torch.no_grad()
     def evaluate(self, x: torch.Tensor, want_y: bool = False) -> Dict[str, torch.Tensor]:

@@ -66,6 +66,11 @@ class GDN(nn.Module):
                               lambda: kernels.pack_gdn(self.beta, self.gamma, bb, gb, ped),
                               force=force or self.training)
 
+    def effective_params_bwd(self):
+        """(beta_eff, gamma_packed, gamma_packed_transposed) for the backward kernels."""
+        bb, gb, ped = self.bounds_f32()
+        return kernels.pack_gdn(self.beta, self.gamma, bb, gb, ped, transposed=True)
+
     def forward(self, inputs):
         unfold = inputs.dim() == 5
         if unfold:  # GDN.py:65-69

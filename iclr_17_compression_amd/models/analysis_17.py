@@ -55,7 +55,12 @@ class Analysis_net_17(nn.Module):
         return kernels.conv2_gdn(h, w2, self.conv2.bias, g2[0], g2[1])
 
     def forward(self, x):
-        from ..autograd import no_backward
+        from ..autograd import AnalysisFn, needs_grad
+        kernels._check(x, "image", 4)
+        params = list(self.parameters())
+        if needs_grad(x, params):
+            if x.requires_grad:
+                raise kernels.Iclr17Error("iclr17: gradients w.r.t. the input image are not implemented")
+            return AnalysisFn.apply(x.contiguous(), self, *params)
         _, _, w3, _, _ = self.packed()
-        y = kernels.conv3(self.features(x), w3).permute(0, 3, 1, 2)
-        return no_backward(y, "Analysis_net_17", list(self.parameters()), x)
+        return kernels.conv3(self.features(x), w3).permute(0, 3, 1, 2)

@@ -61,9 +61,12 @@ class Synthesis_net_17(nn.Module):
         return kernels.deconv3(h, d3, self.deconv3.bias, x_ref=x_ref, want_recon=want_recon)
 
     def forward(self, x):
-        from ..autograd import no_backward
+        from ..autograd import SynthesisFn, needs_grad
         kernels._check(x, "latent", 4)
         if x.shape[1] != self.out_channel_N:
             raise kernels.Iclr17Error(f"iclr17: Synthesis_net_17 expects {self.out_channel_N} channels")
+        params = list(self.parameters())
+        if needs_grad(x, params):
+            return SynthesisFn.apply(x, self, *params)
         _, recon, _ = self.decode(self.to_nhwc(x), want_recon=True)
-        return no_backward(recon, "Synthesis_net_17", list(self.parameters()), x)
+        return recon

@@ -63,10 +63,12 @@ int iclr17_pack_weight(int which, const float* w, float* packed, int N, void* st
 /* GDN.py:46-49,73-83: beta_eff[C] = max(beta, beta_bound)² − pedestal and
  * gamma_eff = max(gamma, gamma_bound)² − pedestal, the latter packed for the channel
  * contraction ([C/4][C][4]: packed[q][i][e] = gamma_eff[i][4q+e]); gamma_packed holds C*C
- * floats. Bounds/pedestal are the fp32 values the reference's ones_like(x)*bound produce
- * (defaults: float(sqrt(1e-6 + 2^-36)), 2^-18, 2^-36). */
+ * floats; gamma_packed_t (nullable, backward only) the transpose (packed[q][j][e] =
+ * gamma_eff[4q+e][j]). Bounds/pedestal are the fp32 values the reference's ones_like(x)*bound
+ * produce (defaults: float(sqrt(1e-6 + 2^-36)), 2^-18, 2^-36). */
 int iclr17_pack_gdn(const float* beta, const float* gamma, float* beta_eff, float* gamma_packed,
-                    int C, float beta_bound, float gamma_bound, float pedestal, void* stream);
+                    float* gamma_packed_t, int C, float beta_bound, float gamma_bound,
+                    float pedestal, void* stream);
 /* bitEstimator.py:13-25: rows softplus(h_k), b_k, tanh(a_k) for k = 1..3 then softplus(h_4),
  * b_4 → packed[11][C]. h/b/a are the (1,C,1,1) parameters of f1..f4 (a4 absent). */
 int iclr17_pack_rate(const float* h1, const float* b1, const float* a1, const float* h2,
@@ -107,11 +109,12 @@ int iclr17_synthesis_deconv_igdn(const float* in, int B, int h, int w, int N,
                                  void* stream);
 /* synthesis_17.py:23-25,30 + model.py:59 : deconv3 (N→3, k9, s4, p4, op3) + bias, clamp[0,1].
  * in NHWC [B,H/4,W/4,N] → clipped NCHW [B,3,H,W]; recon (nullable) gets the unclipped
- * output; if x (NCHW image, nullable) is given, Σ(clipped−x)² per tile goes to
+ * output; if x (NCHW image, nullable) is given, Σ(clipped−x)² per tile (Σ(recon−x)² with
+ * sse_unclipped, the training MSE of model.py:61) goes to
  * sse_partial[B * iclr17_output_partials_per_image(H,W)]. */
 int iclr17_synthesis_deconv3(const float* in, int B, int H, int W, int N, const float* w_packed,
                              const float* bias, const float* x, float* clipped, float* recon,
-                             double* sse_partial, void* stream);
+                             double* sse_partial, int sse_unclipped, void* stream);
 int iclr17_output_partials_per_image(int H, int W);
 
 /* Deterministic fixed-order sums: per_image[b] = Σ_t partial[b*T + t] (nullable);
@@ -136,6 +139,71 @@ int iclr17_bitparm(const float* x, int64_t n, int C, int64_t inner, const float*
 int iclr17_rate_bits(const float* z, int B, int C, int h, int w, int layout,
                      const float* rate_packed, double* bits_partial, void* stream);
 int iclr17_rate_bits_partials(int C, int h, int w);
+
+/* ------------------------------------------------------------------ backward (training)
+ * The autograd of the reference hot path (train.py:105 rd_loss.backward()) as fused kernels.
+ * Input gradients reuse the forward engine (conv dgrad = transposed conv and vice versa), each
+ * fused with the backward of the GDN/IGDN that precedes it; dn = ∂L/∂n (the GDN norm pool)
+ * feeds the GDN parameter gradients. Weight packing for the dgrads: deconv weights with
+ * ICLR17_W_CONV5 (deconv1/2) or ICLR17_W_CONV1 (deconv3), conv weights with ICLR17_W_DECONV5. */
+
+/* ∂recon of λ·mean((recon−x)²) (model.py:61) and/or of a gradient on clamp(recon,0,1)
+ * (model.py:59): g_mse, g_clip nullable (device scalar / NCHW tensor). */
+int iclr17_grad_recon(const float* recon, const float* x, const float* g_mse, const float* g_clip,
+                      int64_t n, float* g_recon, void* stream);
+/* synthesis_17.py:23,30 + :22,29 backward: g_v = IGDN2ᵀ(conv2d(g_recon, W3, s4, p4)).
+ * g_recon NCHW [B,3,H,W]; v_saved = deconv2 output (pre-IGDN2) NHWC [B,H/4,W/4,N]. */
+int iclr17_bwd_deconv3_igdn(const float* g_recon, int B, int H, int W, int N,
+                            const float* w_packed, const float* v_saved, const float* beta_eff,
+                            const float* gamma_packed, const float* gamma_packed_t, float* g_v,
+                            float* dn, void* stream);
+/* synthesis_17.py:19-22 / :18 backward: g_v_prev = IGDNᵀ(conv2d(g_v, Wd, s2, p2)).
+ * g_v NHWC [B,2h,2w,N]; v_prev = the previous deconv's pre-IGDN output NHWC [B,h,w,N]. */
+int iclr17_bwd_deconv_igdn(const float* g_v, int B, int h, int w, int N, const float* w_packed,
+                           const float* v_prev, const float* beta_eff, const float* gamma_packed,
+                           const float* gamma_packed_t, float* g_v_prev, float* dn, void* stream);
+/* synthesis_17.py:15 backward + model.py:71-78 rate backward:
+ * g_y = conv2d(g_v1, Wd1, s2, p2) + (*g_bpp / count)·∂bits/∂ỹ; per-tile rate parameter partials
+ * rate_partial[B * iclr17_rate_bwd_partials(h,w)][11][N]. g_bpp == NULL → no rate term. */
+int iclr17_bwd_deconv_rate(const float* g_v, int B, int h, int w, int N, const float* w_packed,
+                           const float* y_tilde, const float* rate_packed, const float* g_bpp,
+                           float count, float* g_y, float* rate_partial, void* stream);
+int iclr17_rate_bwd_partials(int h, int w);
+/* analysis_17.py:22 / :18 backward fused with GDN2 / GDN1 backward:
+ * g_u_prev = GDNᵀ(conv_transpose2d(g_u, W, s2, p2, op1)); g_u NHWC [B,h,w,N] (conv output grid),
+ * u_prev = the previous conv's pre-GDN output NHWC [B,2h,2w,N]. */
+int iclr17_bwd_conv_gdn(const float* g_u, int B, int h, int w, int N, const float* w_packed,
+                        const float* u_prev, const float* beta_eff, const float* gamma_packed,
+                        const float* gamma_packed_t, float* g_u_prev, float* dn, void* stream);
+/* Weight gradients in PyTorch layout [m][c][kh][kw] (split-K, fixed-order reduction):
+ * k5: G NHWC [B,Ho,Wo,M], X NHWC [B,2Ho,2Wo,C], kind 5 (k5 s2 p2) — conv2/conv3 (G=∂u, X=input)
+ *     and deconv1/deconv2 (G=input, X=∂output);
+ * k9: G NHWC [B,Ho,Wo,M], X NCHW [B,3,4Ho,4Wo] (k9 s4 p4) — conv1 (G=∂u1, X=image) and
+ *     deconv3 (G=s2, X=∂recon). Workspace sizes in floats (kind 5, 9; 1 = GDN). */
+size_t iclr17_wgrad_workspace_size(int kind, int B, int Ho, int Wo, int M, int C);
+int iclr17_wgrad_k5(const float* G, const float* X, int B, int Ho, int Wo, int M, int C,
+                    float* workspace, float* dW, void* stream);
+int iclr17_wgrad_k9(const float* G, const float* X, int B, int Ho, int Wo, int M,
+                    float* workspace, float* dW, void* stream);
+/* GDN.py:83 parameter gradients: dgamma_eff[i][j] = Σ_p dn[p][i]·u[p][j]², dbeta_eff = Σ_p dn. */
+size_t iclr17_gdn_wgrad_workspace_size(long P, int C);
+int iclr17_gdn_wgrad(const float* dn, const float* u, long P, int C, float* workspace,
+                     float* dgamma_eff, float* dbeta_eff, void* stream);
+/* GDN.py:10-24,73-79 chain: dβ = LowerBoundᵀ(dβ_eff · 2·max(β, bβ)), same for γ. */
+int iclr17_gdn_param_chain(const float* beta, const float* gamma, const float* dbeta_eff,
+                           const float* dgamma_eff, int C, float beta_bound, float gamma_bound,
+                           float* dbeta, float* dgamma, void* stream);
+/* Bias gradients: Σ over pixels of an NHWC [P][C] or NCHW [B][C][HW] gradient.
+ * Workspace: 64*C floats (NHWC), B*C floats (NCHW). */
+int iclr17_bias_grad_nhwc(const float* G, long P, int C, float* workspace, float* db, void* stream);
+int iclr17_bias_grad_nchw(const float* G, int B, int C, long HW, float* workspace, float* db,
+                          void* stream);
+/* BitEstimator parameter gradients (bitEstimator.py:13-25) from the rate partials [T][11][C]. */
+int iclr17_rate_param_grad(const float* partial, int T, int C, const float* h1, const float* a1,
+                           const float* h2, const float* a2, const float* h3, const float* a3,
+                           const float* h4, float* dh1, float* db1, float* da1, float* dh2,
+                           float* db2, float* da2, float* dh3, float* db3, float* da3, float* dh4,
+                           float* db4, void* stream);
 
 #ifdef __cplusplus
 }

@@ -48,7 +48,7 @@ def test_argument_validation_without_gpu():
         _lib.call("iclr17_analysis_conv2_gdn", ctypes.c_void_p(16), 1, 256, 256, 96,
                   *[ctypes.c_void_p(16)] * 5, None, None)
     with pytest.raises(_lib.Iclr17Error, match="null pointer"):
-        _lib.call("iclr17_synthesis_deconv3", None, 1, 256, 256, 192, *[None] * 6, None)
+        _lib.call("iclr17_synthesis_deconv3", None, 1, 256, 256, 192, *[None] * 6, 0, None)
     with pytest.raises(_lib.Iclr17Error, match="quant mode"):
         _lib.call("iclr17_analysis_conv3_quant_rate", ctypes.c_void_p(16), 1, 256, 256, 192,
                   ctypes.c_void_p(16), 1, None, ctypes.c_void_p(16), None, ctypes.c_void_p(16),

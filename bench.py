@@ -104,6 +104,75 @@ class Step:
         return clipped, y_hat, bpp
 
 
+def train_flops(N: int, H: int, W: int) -> float:
+    """Algorithmic FLOPs of one training step per image: forward + input gradients (no conv1
+    dgrad) + weight gradients + GDN backward (two channel contractions + the parameter GEMM)."""
+    h1, w1, h2, w2, h3, w3 = H // 4, W // 4, H // 8, W // 8, H // 16, W // 16
+    conv = {"c1": h1 * w1 * N * 243, "c2": h2 * w2 * N * N * 25, "c3": h3 * w3 * N * N * 25,
+            "d1": h3 * w3 * N * N * 25, "d2": h2 * w2 * N * N * 25, "d3": h1 * w1 * N * 243}
+    gdn = {"g1": h1 * w1 * N * N, "g2": h2 * w2 * N * N, "q1": h2 * w2 * N * N, "q2": h1 * w1 * N * N}
+    fwd = sum(conv.values()) + sum(gdn.values())
+    dgrad = sum(v for k, v in conv.items() if k != "c1")
+    wgrad = sum(conv.values())
+    gdn_bwd = 3 * sum(gdn.values())
+    return 2.0 * (fwd + dgrad + wgrad + gdn_bwd)
+
+
+def run_train(args, net, x, world, dev):
+    """C3/C4: fused training step (forward_train + backward + bucketed all-reduce over RCCL +
+    ±5 clamp + Adam), λ = 0.01·255² (train_lambda 650.25)."""
+    from iclr_17_compression_amd import dist as idist
+    from iclr_17_compression_amd.train import clip_gradient
+    net.train()
+    params = list(net.parameters())
+    opt = torch.optim.Adam(params, lr=1e-4)
+    lam = 0.01 * 255.0 ** 2
+    B, _, S, _ = x.shape
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        _, mse, bpp = net.forward_train(x)
+        (lam * mse + bpp).backward()
+        idist.allreduce_grads(params)
+        clip_gradient(params, 5)
+        opt.step()
+        return bpp
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        bpp = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = idist.max_over_ranks(time.perf_counter() - t0, dev)
+    ms = elapsed / args.steps * 1e3
+    flops = train_flops(args.N, S, S) * B
+    tflops = flops / (ms * 1e-3) / 1e12
+    return {
+        "metric": "Mpixels/s training (fwd+bwd+Adam), " + METRIC,
+        "value": round(world * B * S * S * args.steps / elapsed / 1e6, 2),
+        "unit": "Mpix/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (splitmix64 uint8/255 images, seeded trained-like weights)",
+        "config": {"workload": f"train step, {B} x {S}x{S}x3 crops per GPU, N={args.N}, lambda=0.01",
+                   "N": args.N, "batch_per_gpu": B, "global_batch": B * world,
+                   "parallelism": f"dp{world} (RCCL bucketed grad all-reduce)"},
+        "roofline": {"bound": "mfma", "kernel": "whole training step", "achieved": round(tflops, 2),
+                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(tflops / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                     "flop_per_step": flops},
+        "bpp_last": round(bpp.item(), 6),
+    }
+
+
 def cpu_baseline(N: int, H: int, W: int, budget_s: float) -> dict:
     """The oracle (op-for-op restatement of the reference forward, bit-identical to it on the
     build host) timed on this host's cores on a bounded sample."""
@@ -138,6 +207,7 @@ def main() -> None:
     ap.add_argument("--N", type=int, default=192)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", choices=("eval", "train"), default="eval")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -154,6 +224,13 @@ def main() -> None:
     net = net.to(dev).eval()
     # each rank encodes its own shard of the global batch (images are independent)
     x = torch.from_numpy(synth.to_unit_float(synth.image_u8(1000 + rank, B, S, S))).to(dev)
+    if args.mode == "train":
+        result = run_train(args, net, x, world, dev)
+        if rank == 0:
+            print(json.dumps(result), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     step = Step(net, x)
 
     with torch.no_grad():

@@ -1,0 +1,111 @@
+"""Multi-GPU plumbing: one process per GPU, torch.distributed over RCCL ("nccl") on MI355X.
+
+* Inference / evaluation shards images by rank — images are independent, so there is no
+  collective in the data path; per-image metrics come back with one all-gather at the end.
+* Training is data parallel (the reference's DataParallel, train.py:228, re-done as one process
+  per GPU): each rank holds a replica, runs the fused forward/backward on its shard, and the
+  gradients are averaged with bucketed all-reduces (flat fp32 buckets sized for the xGMI ring)
+  before the ±5 clamp (train.py:106-111) and the Adam step.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Sequence
+
+import torch
+import torch.distributed as dist
+
+Tensor = torch.Tensor
+
+
+def world() -> int:
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def rank() -> int:
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
+def init_from_env(backend: str = "nccl") -> torch.device:
+    """Initialise from torchrun's RANK / WORLD_SIZE / LOCAL_RANK (MASTER_ADDR 127.0.0.1)."""
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
+    if ws > 1 and not dist.is_initialized():
+        kw = {"device_id": dev} if backend == "nccl" else {}
+        dist.init_process_group(backend, **kw)
+    return dev
+
+
+def shard_range(n: int, r: int, w: int):
+    """Contiguous, balanced split of n items over w ranks: rank r gets [lo, hi)."""
+    base, extra = divmod(n, w)
+    lo = r * base + min(r, extra)
+    return lo, lo + base + (1 if r < extra else 0)
+
+
+def shard_batch(x: Tensor, r: int = None, w: int = None) -> Tensor:
+    r = rank() if r is None else r
+    w = world() if w is None else w
+    lo, hi = shard_range(x.shape[0], r, w)
+    return x[lo:hi]
+
+
+def gather_rows(t: Tensor, n_total: int) -> Tensor:
+    """All-gather per-image rows (1-D or 2-D) whose shards follow shard_range; returns the
+    full [n_total, ...] tensor on every rank in image order."""
+    w = world()
+    if w == 1:
+        return t
+    sizes = [shard_range(n_total, r, w)[1] - shard_range(n_total, r, w)[0] for r in range(w)]
+    m = max(sizes)
+    pad = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    pad[: t.shape[0]] = t
+    out = [torch.empty_like(pad) for _ in range(w)]
+    dist.all_gather(out, pad)
+    return torch.cat([o[:s] for o, s in zip(out, sizes)], dim=0)
+
+
+def bucketize(params: Sequence[Tensor], bucket_bytes: int) -> List[List[Tensor]]:
+    """Group parameters (in order) into buckets of at most ~bucket_bytes of fp32 gradient."""
+    buckets, cur, size = [], [], 0
+    for p in params:
+        nb = p.numel() * 4
+        if cur and size + nb > bucket_bytes:
+            buckets.append(cur)
+            cur, size = [], 0
+        cur.append(p)
+        size += nb
+    if cur:
+        buckets.append(cur)
+    return buckets
+
+
+def allreduce_grads(params: Sequence[Tensor], bucket_mb: float = 4.0) -> None:
+    """Average .grad over ranks: flatten each bucket, all-reduce (sum) once, scale by 1/world.
+    Ranks must call with the same parameter order (they hold identical replicas)."""
+    w = world()
+    if w == 1:
+        return
+    ps = [p for p in params if p.grad is not None]
+    for bucket in bucketize(ps, int(bucket_mb * 2 ** 20)):
+        flat = torch.cat([p.grad.reshape(-1) for p in bucket])
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+        flat.mul_(1.0 / w)
+        off = 0
+        for p in bucket:
+            n = p.numel()
+            p.grad.copy_(flat[off:off + n].view_as(p.grad))
+            off += n
+
+
+def max_over_ranks(value: float, device) -> float:
+    if world() == 1:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.item()

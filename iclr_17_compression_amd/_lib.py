@@ -58,16 +58,18 @@ SIGNATURES = {
     "iclr17_rate_bits": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "iclr17_rate_bits_partials": (_I, [_I, _I, _I]),
     "iclr17_grad_recon": (_I, [_P, _P, _P, _P, _I64, _P, _P]),
-    "iclr17_bwd_deconv3_igdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
-    "iclr17_bwd_deconv_igdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_bwd_deconv3_igdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_bwd_deconv_igdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_bwd_deconv_rate": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _F, _P, _P, _P]),
     "iclr17_rate_bwd_partials": (_I, [_I, _I]),
-    "iclr17_bwd_conv_gdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_bwd_conv_gdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_bwd_tiles": (_I, [_I, _I, _I]),
+    "iclr17_sum_rows": (_I, [_P, _I, _I, _P, _P]),
     "iclr17_wgrad_workspace_size": (_SZ, [_I, _I, _I, _I, _I, _I]),
     "iclr17_wgrad_k5": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "iclr17_wgrad_k9": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P]),
     "iclr17_gdn_wgrad_workspace_size": (_SZ, [ctypes.c_long, _I]),
-    "iclr17_gdn_wgrad": (_I, [_P, _P, ctypes.c_long, _I, _P, _P, _P, _P]),
+    "iclr17_gdn_wgrad": (_I, [_P, _P, ctypes.c_long, _I, _P, _P, _P]),
     "iclr17_gdn_param_chain": (_I, [_P, _P, _P, _P, _I, _F, _F, _P, _P, _P]),
     "iclr17_bias_grad_nhwc": (_I, [_P, ctypes.c_long, _I, _P, _P, _P]),
     "iclr17_bias_grad_nchw": (_I, [_P, _I, _I, ctypes.c_long, _P, _P, _P]),

@@ -66,15 +66,13 @@ def analysis_backward(enc, saved: Dict[str, Tensor], g_y: Tensor) -> Dict[str, T
     w2t = kernels.pack_weight(_lib.ICLR17_W_DECONV5, enc.conv2.weight, enc.out_channel_N)
     p2 = enc.gdn2.effective_params_bwd()
     p1 = enc.gdn1.effective_params_bwd()
-    g_u2, dn2 = kernels.bwd_conv_gdn(g_y, w3t, saved["u2"], *p2)
+    g_u2, dn2, db2, dbe2 = kernels.bwd_conv_gdn(g_y, w3t, saved["u2"], *p2)
     dW3 = kernels.wgrad_k5(g_y, saved["a2"])
-    g_u1, dn1 = kernels.bwd_conv_gdn(g_u2, w2t, saved["u1"], *p1)
+    g_u1, dn1, db1, dbe1 = kernels.bwd_conv_gdn(g_u2, w2t, saved["u1"], *p1)
     dW2 = kernels.wgrad_k5(g_u2, saved["a1"])
-    db2 = kernels.bias_grad_nhwc(g_u2)
     dW1 = kernels.wgrad_k9(g_u1, saved["x"])
-    db1 = kernels.bias_grad_nhwc(g_u1)
-    dbeta2, dgamma2 = kernels.gdn_param_grads(dn2, saved["u2"], enc.gdn2.beta, enc.gdn2.gamma, bb2, gb2)
-    dbeta1, dgamma1 = kernels.gdn_param_grads(dn1, saved["u1"], enc.gdn1.beta, enc.gdn1.gamma, bb1, gb1)
+    dbeta2, dgamma2 = kernels.gdn_param_grads(dn2, saved["u2"], dbe2, enc.gdn2.beta, enc.gdn2.gamma, bb2, gb2)
+    dbeta1, dgamma1 = kernels.gdn_param_grads(dn1, saved["u1"], dbe1, enc.gdn1.beta, enc.gdn1.gamma, bb1, gb1)
     return {"conv1.weight": dW1, "conv1.bias": db1, "gdn1.beta": dbeta1, "gdn1.gamma": dgamma1,
             "conv2.weight": dW2, "conv2.bias": db2, "gdn2.beta": dbeta2, "gdn2.gamma": dgamma2,
             "conv3.weight": dW3}
@@ -102,20 +100,18 @@ def synthesis_backward(dec, saved: Dict[str, Tensor], g_recon: Tensor, g_bpp: Op
     d1c = kernels.pack_weight(_lib.ICLR17_W_CONV5, dec.deconv1.weight, N)
     q2 = dec.igdn2.effective_params_bwd()
     q1 = dec.igdn1.effective_params_bwd()
-    g_v2, dnq2 = kernels.bwd_deconv3_igdn(g_recon, d3c, saved["v2"], *q2)
+    g_v2, dnq2, dbd2, dbeq2 = kernels.bwd_deconv3_igdn(g_recon, d3c, saved["v2"], *q2)
     dWd3 = kernels.wgrad_k9(saved["s2"], g_recon)
     dbd3 = kernels.bias_grad_nchw(g_recon)
-    g_v1, dnq1 = kernels.bwd_deconv_igdn(g_v2, d2c, saved["v1"], *q1)
+    g_v1, dnq1, dbd1, dbeq1 = kernels.bwd_deconv_igdn(g_v2, d2c, saved["v1"], *q1)
     dWd2 = kernels.wgrad_k5(saved["s1"], g_v2)
-    dbd2 = kernels.bias_grad_nhwc(g_v2)
     y = saved["y"]
     B, h, w, _ = y.shape
     g_y, rpart = kernels.bwd_deconv_rate(g_v1, d1c, y if g_bpp is not None else None, rate_packed,
                                          g_bpp, count, h, w)
     dWd1 = kernels.wgrad_k5(y, g_v1)
-    dbd1 = kernels.bias_grad_nhwc(g_v1)
-    dbq2, dgq2 = kernels.gdn_param_grads(dnq2, saved["v2"], dec.igdn2.beta, dec.igdn2.gamma, bq2, gq2)
-    dbq1, dgq1 = kernels.gdn_param_grads(dnq1, saved["v1"], dec.igdn1.beta, dec.igdn1.gamma, bq1, gq1)
+    dbq2, dgq2 = kernels.gdn_param_grads(dnq2, saved["v2"], dbeq2, dec.igdn2.beta, dec.igdn2.gamma, bq2, gq2)
+    dbq1, dgq1 = kernels.gdn_param_grads(dnq1, saved["v1"], dbeq1, dec.igdn1.beta, dec.igdn1.gamma, bq1, gq1)
     grads = {"deconv1.weight": dWd1, "deconv1.bias": dbd1, "igdn1.beta": dbq1, "igdn1.gamma": dgq1,
              "deconv2.weight": dWd2, "deconv2.bias": dbd2, "igdn2.beta": dbq2, "igdn2.gamma": dgq2,
              "deconv3.weight": dWd3, "deconv3.bias": dbd3}

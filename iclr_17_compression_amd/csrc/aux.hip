@@ -231,29 +231,34 @@ struct RateGradPtrs {
   float* p[11];
 };
 
+// One workgroup per (parameter k, 64 channels): T rows split over 4 lane groups, combined in
+// fixed order, then the softplus / tanh chain rule (torch softplus_backward, tanh_backward).
 __global__ void rate_param_chain_kernel(const float* __restrict__ part, int T, int C, RatePtrs rp,
                                         RateGradPtrs out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  for (int k = 0; k < 11; ++k) {
-    double s = 0.0;
-    for (int t = 0; t < T; ++t) s += (double)part[((long)t * 11 + k) * C + c];
-    const float g = (float)s;
-    const int layer = k / 3, role = k % 3;
-    float v;
-    if (role == 0) {  // d softplus(h) → dh : torch softplus_backward (beta 1, threshold 20)
-      const float h = rp.p[k][c];
-      const float z = expf(h);
-      v = h > 20.0f ? g : g * z / (z + 1.0f);
-    } else if (role == 1) {
-      v = g;
-    } else {          // d tanh(a) → da : tanh_backward on the forward output
-      const float ta = tanhf(rp.p[k][c]);
-      v = g * (1.0f - ta * ta);
-    }
-    (void)layer;
-    out.p[k][c] = v;
+  __shared__ double red[4][64];
+  const int k = blockIdx.y;
+  const int cl = threadIdx.x & 63, gq = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double s = 0.0;
+  if (c < C)
+    for (int t = gq; t < T; t += 4) s += (double)part[((long)t * 11 + k) * C + c];
+  red[gq][cl] = s;
+  __syncthreads();
+  if (gq != 0 || c >= C) return;
+  const float g = (float)(((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl]);
+  const int role = k % 3;
+  float v;
+  if (role == 0) {        // d softplus(h) → dh (beta 1, threshold 20)
+    const float h = rp.p[k][c];
+    const float z = expf(h);
+    v = h > 20.0f ? g : g * z / (z + 1.0f);
+  } else if (role == 1) {
+    v = g;
+  } else {                // d tanh(a) → da
+    const float ta = tanhf(rp.p[k][c]);
+    v = g * (1.0f - ta * ta);
   }
+  out.p[k][c] = v;
 }
 
 }  // namespace
@@ -406,7 +411,7 @@ int iclr17_rate_param_grad(const float* partial, int T, int C, const float* h1, 
   for (int i = 0; i < 11; ++i) ICLR17_REQUIRE(o.p[i], ICLR17_EINVAL, "rate_param_grad: null output %d", i);
   ICLR17_REQUIRE(partial && T > 0 && C > 0 && h1 && a1 && h2 && a2 && h3 && a3 && h4, ICLR17_EINVAL,
                  "rate_param_grad: bad arguments");
-  hipLaunchKernelGGL(rate_param_chain_kernel, dim3((C + 255) / 256), dim3(256), 0, S(stream),
+  hipLaunchKernelGGL(rate_param_chain_kernel, dim3((C + 63) / 64, 11), dim3(256), 0, S(stream),
                      partial, T, C, rp, o);
   return check_launch("rate_param_grad");
 }

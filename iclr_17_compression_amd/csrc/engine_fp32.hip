@@ -82,6 +82,8 @@ struct EngineArgs {
   const float* gscale;  // rate bwd: device scalar ∂L/∂bpp (nullptr → no rate term)
   float count;          // rate bwd: B·H·W (bpp denominator, model.py:78)
   float* rpart;         // rate bwd: per-tile parameter partials [tiles][11][CO]
+  float* colsum_out;    // GDN bwd: per-tile column sums of ∂u (the conv bias gradient) [tiles][CO]
+  float* colsum_t;      // GDN bwd: per-tile column sums of dn (∂β_eff) [tiles][CO]
 };
 
 struct TileInfo {
@@ -138,6 +140,17 @@ __device__ __forceinline__ void load_tile_rows(const EngineArgs& a, const TileIn
     const long p = out_pixel(a, t, m);
     const f4 v = p < 0 ? f4{0.f, 0.f, 0.f, 0.f} : *(const f4*)(src + p * CO + col0 + c4 * 4);
     *(f4*)(s + m * ld + c4 * 4) = v;
+  }
+}
+
+// Column sums of an LDS tile [BM][ld] (rows outside the grid hold zeros) → dst[blockIdx.x][CO],
+// fixed row order (deterministic). Feeds bias / β gradients without another pass over HBM.
+template <int CO>
+__device__ __forceinline__ void tile_colsum(const float* s, int ld, float* dst) {
+  for (int c = threadIdx.x; c < CO; c += 256) {
+    float acc = 0.f;
+    for (int m = 0; m < BM; ++m) acc += s[m * ld + c];
+    dst[(long)blockIdx.x * CO + c] = acc;
   }
 }
 
@@ -318,6 +331,7 @@ __device__ __forceinline__ void gdn_bwd_epilogue(f4 (&g)[MT][NT], float* smem, c
   __syncthreads();
   chan_gemm<CO, MT, NT>(acc2, sX, a.ggammaT, wm, ncol0, lane);  // w_j = Σ_i γ[i][j] dn_i
   store_tile_rows<CO>(a, t, sX, XS, a.tout, CO, 0);
+  if (a.colsum_t != nullptr) tile_colsum<CO>(sX, XS, a.colsum_t);
   __syncthreads();
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
@@ -330,6 +344,7 @@ __device__ __forceinline__ void gdn_bwd_epilogue(f4 (&g)[MT][NT], float* smem, c
       }
   __syncthreads();
   store_tile_rows<CO>(a, t, sX, XS, a.out, CO, 0);
+  if (a.colsum_out != nullptr) tile_colsum<CO>(sX, XS, a.colsum_out);
 }
 
 // ------------------------------------------------------------------------- rate backward epilogue
@@ -1146,29 +1161,42 @@ static EngineArgs bwd_args(const float* saved, const float* gammaT, float* tout)
 int iclr17_bwd_deconv3_igdn(const float* g_recon, int B, int H, int W, int N,
                             const float* w_packed, const float* v_saved, const float* beta_eff,
                             const float* gamma_packed, const float* gamma_packed_t, float* g_v,
-                            float* dn, void* stream) {
+                            float* dn, float* colsum_gv, float* colsum_dn, void* stream) {
   int rc = check_dims(B, H, W, N);
   if (rc) return rc;
   ICLR17_REQUIRE(g_recon && w_packed && v_saved && beta_eff && gamma_packed && gamma_packed_t &&
                      g_v && dn, ICLR17_EINVAL, "bwd_deconv3_igdn: null pointer");
   EngineArgs b = bwd_args(v_saved, gamma_packed_t, dn);
+  b.colsum_out = colsum_gv;
+  b.colsum_t = colsum_dn;
   return N == 192 ? launch_conv1<192, EPI_IGDN_BWD>(g_recon, B, H, W, w_packed, nullptr, beta_eff, gamma_packed, g_v, nullptr, S(stream), &b)
                   : launch_conv1<128, EPI_IGDN_BWD>(g_recon, B, H, W, w_packed, nullptr, beta_eff, gamma_packed, g_v, nullptr, S(stream), &b);
 }
 
 int iclr17_bwd_deconv_igdn(const float* g_v, int B, int h, int w, int N, const float* w_packed,
                            const float* v_prev, const float* beta_eff, const float* gamma_packed,
-                           const float* gamma_packed_t, float* g_v_prev, float* dn, void* stream) {
+                           const float* gamma_packed_t, float* g_v_prev, float* dn,
+                           float* colsum_gv, float* colsum_dn, void* stream) {
   ICLR17_REQUIRE(B > 0 && h > 0 && w > 0, ICLR17_EINVAL, "bwd_deconv_igdn: bad shape");
   ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "channel count N=%d unsupported", N);
   ICLR17_REQUIRE(g_v && w_packed && v_prev && beta_eff && gamma_packed && gamma_packed_t &&
                      g_v_prev && dn, ICLR17_EINVAL, "bwd_deconv_igdn: null pointer");
   EngineArgs b = bwd_args(v_prev, gamma_packed_t, dn);
+  b.colsum_out = colsum_gv;
+  b.colsum_t = colsum_dn;
   return N == 192 ? launch_conv5<192, EPI_IGDN_BWD>(g_v, B, 2 * h, 2 * w, w_packed, nullptr, beta_eff, gamma_packed, g_v_prev, nullptr, 0, nullptr, nullptr, nullptr, nullptr, S(stream), &b)
                   : launch_conv5<128, EPI_IGDN_BWD>(g_v, B, 2 * h, 2 * w, w_packed, nullptr, beta_eff, gamma_packed, g_v_prev, nullptr, 0, nullptr, nullptr, nullptr, nullptr, S(stream), &b);
 }
 
 int iclr17_rate_bwd_partials(int h, int w) { return ((h + 7) / 8) * ((w + 7) / 8); }
+
+/* Workgroups (= column-sum partial rows) per image of each fused backward kernel. */
+int iclr17_bwd_tiles(int kind, int h, int w) {
+  // kind 0: conv-type over an output grid h×w (bwd_deconv_igdn, bwd_deconv3_igdn: pass H/4, W/4)
+  // kind 1: deconv-type over an input grid h×w (bwd_conv_gdn): 4 stride phases
+  const int t = ((h + 7) / 8) * ((w + 7) / 8);
+  return kind == 1 ? 4 * t : t;
+}
 
 int iclr17_bwd_deconv_rate(const float* g_v, int B, int h, int w, int N, const float* w_packed,
                            const float* y_tilde, const float* rate_packed, const float* g_bpp,
@@ -1188,12 +1216,15 @@ int iclr17_bwd_deconv_rate(const float* g_v, int B, int h, int w, int N, const f
 
 int iclr17_bwd_conv_gdn(const float* g_u, int B, int h, int w, int N, const float* w_packed,
                         const float* u_prev, const float* beta_eff, const float* gamma_packed,
-                        const float* gamma_packed_t, float* g_u_prev, float* dn, void* stream) {
+                        const float* gamma_packed_t, float* g_u_prev, float* dn,
+                        float* colsum_gu, float* colsum_dn, void* stream) {
   ICLR17_REQUIRE(B > 0 && h > 0 && w > 0, ICLR17_EINVAL, "bwd_conv_gdn: bad shape");
   ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "channel count N=%d unsupported", N);
   ICLR17_REQUIRE(g_u && w_packed && u_prev && beta_eff && gamma_packed && gamma_packed_t &&
                      g_u_prev && dn, ICLR17_EINVAL, "bwd_conv_gdn: null pointer");
   EngineArgs b = bwd_args(u_prev, gamma_packed_t, dn);
+  b.colsum_out = colsum_gu;
+  b.colsum_t = colsum_dn;
   return N == 192 ? launch_deconv5<192, EPI_GDN_BWD>(g_u, B, h, w, w_packed, nullptr, beta_eff, gamma_packed, g_u_prev, nullptr, S(stream), &b)
                   : launch_deconv5<128, EPI_GDN_BWD>(g_u, B, h, w, w_packed, nullptr, beta_eff, gamma_packed, g_u_prev, nullptr, S(stream), &b);
 }

@@ -246,6 +246,20 @@ __global__ void sum_splits_kernel(const float* __restrict__ part, int nsplit, lo
   }
 }
 
+// out[c] = Σ_t part[t][c]: 64 columns per workgroup, T split over 4 lane groups (strided), the 4
+// partial sums combined in order through LDS — fixed order, bitwise reproducible.
+__global__ void sum_rows_kernel(const float* __restrict__ part, int T, int C, float* __restrict__ out) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float s = 0.f;
+  if (c < C)
+    for (int t = g; t < T; t += 4) s += part[(long)t * C + c];
+  red[g][cl] = s;
+  __syncthreads();
+  if (g == 0 && c < C) out[c] = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
+}
+
 // Column sums of a [P][C] row-major matrix (NHWC activations): part[chunk][c].
 __global__ void colsum_kernel(const float* __restrict__ A, long P, int C, int chunk,
                               float* __restrict__ part) {
@@ -287,6 +301,8 @@ int wgrad_splits(long P, int tiles) {
 using namespace iclr17;
 
 extern "C" {
+
+int iclr17_sum_rows(const float* part, int T, int C, float* out, void* stream);
 
 size_t iclr17_wgrad_workspace_size(int kind, int B, int Ho, int Wo, int M, int C) {
   const long P = (long)B * Ho * Wo;
@@ -338,15 +354,15 @@ int iclr17_wgrad_k9(const float* G, const float* X, int B, int Ho, int Wo, int M
 }
 
 size_t iclr17_gdn_wgrad_workspace_size(long P, int C) {
-  return (size_t)wgrad_splits(P, C / 64) * C * C + (size_t)64 * C;
+  return (size_t)wgrad_splits(P, C / 64) * C * C;
 }
 
 // GDN.py:83 parameter gradients from dn (∂L/∂n, NHWC [P][C]) and the saved input u:
 //   dgamma_eff[i][j] = Σ_p dn[p][i] · u[p][j]²,  dbeta_eff[i] = Σ_p dn[p][i].
 int iclr17_gdn_wgrad(const float* dn, const float* u, long P, int C, float* workspace,
-                     float* dgamma_eff, float* dbeta_eff, void* stream) {
+                     float* dgamma_eff, void* stream) {
   ICLR17_REQUIRE(P > 0 && (C == 128 || C == 192), ICLR17_EUNSUPPORTED, "gdn_wgrad: C=%d", C);
-  ICLR17_REQUIRE(dn && u && workspace && dgamma_eff && dbeta_eff, ICLR17_EINVAL, "gdn_wgrad: null pointer");
+  ICLR17_REQUIRE(dn && u && workspace && dgamma_eff, ICLR17_EINVAL, "gdn_wgrad: null pointer");
   const int ns = wgrad_splits(P, C / 64);
   hipStream_t st = S(stream);
   dim3 grid(C / 64, ns);
@@ -359,29 +375,26 @@ int iclr17_gdn_wgrad(const float* dn, const float* u, long P, int C, float* work
   if (rc) return rc;
   const long n = (long)C * C;
   hipLaunchKernelGGL(sum_splits_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, workspace, ns, n, dgamma_eff);
-  rc = check_launch("gdn_wgrad_sum");
-  if (rc) return rc;
-  // dβ: column sums in 64 fixed chunks
-  float* cpart = workspace + (size_t)ns * C * C;
-  const int chunk = (int)((P + 63) / 64);
-  hipLaunchKernelGGL(colsum_kernel, dim3((C + 255) / 256, 64), dim3(256), 0, st, dn, P, C, chunk, cpart);
-  rc = check_launch("gdn_colsum");
-  if (rc) return rc;
-  hipLaunchKernelGGL(sum_splits_kernel, dim3(1), dim3(256), 0, st, cpart, 64, (long)C, dbeta_eff);
-  return check_launch("gdn_colsum_sum");
+  return check_launch("gdn_wgrad_sum");
+}
+
+// out[c] = Σ_t part[t][c] (fixed order; T rows split over 4 thread groups, combined in order).
+int iclr17_sum_rows(const float* part, int T, int C, float* out, void* stream) {
+  ICLR17_REQUIRE(part && out && T > 0 && C > 0, ICLR17_EINVAL, "sum_rows: bad arguments");
+  hipLaunchKernelGGL(sum_rows_kernel, dim3((C + 63) / 64), dim3(256), 0, S(stream), part, T, C, out);
+  return check_launch("sum_rows");
 }
 
 // Bias gradient of a layer whose output gradient is NHWC [P][C]: db[c] = Σ_p G[p][c].
-// workspace: 64*C floats.
+// workspace: 1024*C floats (1024 fixed row chunks, then iclr17_sum_rows).
 int iclr17_bias_grad_nhwc(const float* G, long P, int C, float* workspace, float* db, void* stream) {
   ICLR17_REQUIRE(P > 0 && C > 0 && G && workspace && db, ICLR17_EINVAL, "bias_grad_nhwc: bad arguments");
   hipStream_t st = S(stream);
-  const int chunk = (int)((P + 63) / 64);
-  hipLaunchKernelGGL(colsum_kernel, dim3((C + 255) / 256, 64), dim3(256), 0, st, G, P, C, chunk, workspace);
+  const int chunk = (int)((P + 1023) / 1024);
+  hipLaunchKernelGGL(colsum_kernel, dim3((C + 255) / 256, 1024), dim3(256), 0, st, G, P, C, chunk, workspace);
   int rc = check_launch("bias_grad_nhwc");
   if (rc) return rc;
-  hipLaunchKernelGGL(sum_splits_kernel, dim3((C + 255) / 256), dim3(256), 0, st, workspace, 64, (long)C, db);
-  return check_launch("bias_grad_nhwc_sum");
+  return iclr17_sum_rows(workspace, 1024, C, db, stream);
 }
 
 // Bias gradient from an NCHW gradient [B][C][HW] (deconv3 output): workspace B*C floats.
@@ -392,9 +405,8 @@ int iclr17_bias_grad_nchw(const float* G, int B, int C, long HW, float* workspac
   hipLaunchKernelGGL(plane_sum_kernel, dim3(B * C), dim3(256), 0, st, G, C, HW, workspace);
   int rc = check_launch("bias_grad_nchw");
   if (rc) return rc;
-  // part is [B][C] → sum over b for each c (stride C)
-  hipLaunchKernelGGL(sum_splits_kernel, dim3(1), dim3(256), 0, st, workspace, B, (long)C, db);
-  return check_launch("bias_grad_nchw_sum");
+  // part is [B][C] → sum over b for each c
+  return iclr17_sum_rows(workspace, B, C, db, stream);
 }
 
 }  // extern "C"

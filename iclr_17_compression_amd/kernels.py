@@ -319,27 +319,47 @@ def grad_recon(recon: Tensor, x: Tensor, g_mse: Optional[Tensor], g_clip: Option
     return out
 
 
+def _colsum_buffers(t: Tensor, kind: int, h: int, w: int):
+    B, N = t.shape[0], t.shape[-1]
+    T = B * query("iclr17_bwd_tiles", kind, h, w)
+    return (torch.empty(T, N, device=t.device, dtype=torch.float32),
+            torch.empty(T, N, device=t.device, dtype=torch.float32))
+
+
+def sum_rows(part: Tensor) -> Tensor:
+    """Fixed-order column sums of a [T, C] float32 partial buffer."""
+    T, C = part.shape
+    out = torch.empty(C, device=part.device, dtype=torch.float32)
+    call("iclr17_sum_rows", _p(part), T, C, _p(out), _stream(part))
+    return out
+
+
 def bwd_deconv3_igdn(g_recon: Tensor, wp_conv1form: Tensor, v_saved: Tensor, beta_eff: Tensor,
                      gp: Tensor, gpt: Tensor):
-    """deconv3 input-gradient fused with IGDN2 backward → (g_v2 NHWC, dn NHWC)."""
+    """deconv3 input-gradient fused with IGDN2 backward →
+    (g_v2 NHWC, dn NHWC, Σ g_v2 = ∂bias of deconv2, Σ dn = ∂β_eff of IGDN2)."""
     B, _, H, W = g_recon.shape
     N = v_saved.shape[3]
     g_v = torch.empty_like(v_saved)
     dn = torch.empty_like(v_saved)
+    cs_g, cs_d = _colsum_buffers(v_saved, 0, H // 4, W // 4)
     call("iclr17_bwd_deconv3_igdn", _p(g_recon.contiguous()), B, H, W, N, _p(wp_conv1form),
-         _p(v_saved), _p(beta_eff), _p(gp), _p(gpt), _p(g_v), _p(dn), _stream(g_recon))
-    return g_v, dn
+         _p(v_saved), _p(beta_eff), _p(gp), _p(gpt), _p(g_v), _p(dn), _p(cs_g), _p(cs_d),
+         _stream(g_recon))
+    return g_v, dn, sum_rows(cs_g), sum_rows(cs_d)
 
 
 def bwd_deconv_igdn(g_v: Tensor, wp_conv5form: Tensor, v_prev: Tensor, beta_eff: Tensor, gp: Tensor,
                     gpt: Tensor):
-    """deconv2 input-gradient fused with IGDN1 backward → (g_v1 NHWC, dn NHWC)."""
+    """deconv2 input-gradient fused with IGDN1 backward →
+    (g_v1 NHWC, dn NHWC, Σ g_v1 = ∂bias of deconv1, Σ dn = ∂β_eff of IGDN1)."""
     B, h, w, N = v_prev.shape
     g_prev = torch.empty_like(v_prev)
     dn = torch.empty_like(v_prev)
+    cs_g, cs_d = _colsum_buffers(v_prev, 0, h, w)
     call("iclr17_bwd_deconv_igdn", _p(g_v.contiguous()), B, h, w, N, _p(wp_conv5form), _p(v_prev),
-         _p(beta_eff), _p(gp), _p(gpt), _p(g_prev), _p(dn), _stream(g_v))
-    return g_prev, dn
+         _p(beta_eff), _p(gp), _p(gpt), _p(g_prev), _p(dn), _p(cs_g), _p(cs_d), _stream(g_v))
+    return g_prev, dn, sum_rows(cs_g), sum_rows(cs_d)
 
 
 def bwd_deconv_rate(g_v1: Tensor, wp_conv5form: Tensor, y_tilde: Optional[Tensor],
@@ -361,13 +381,15 @@ def bwd_deconv_rate(g_v1: Tensor, wp_conv5form: Tensor, y_tilde: Optional[Tensor
 
 def bwd_conv_gdn(g_u: Tensor, wp_deconv5form: Tensor, u_prev: Tensor, beta_eff: Tensor, gp: Tensor,
                  gpt: Tensor):
-    """conv3/conv2 input-gradient fused with GDN2/GDN1 backward → (g_u_prev NHWC, dn NHWC)."""
+    """conv3/conv2 input-gradient fused with GDN2/GDN1 backward →
+    (g_u_prev NHWC, dn NHWC, Σ g_u_prev = ∂bias of the previous conv, Σ dn = ∂β_eff)."""
     B, h, w, N = g_u.shape
     g_prev = torch.empty_like(u_prev)
     dn = torch.empty_like(u_prev)
+    cs_g, cs_d = _colsum_buffers(g_u, 1, h, w)
     call("iclr17_bwd_conv_gdn", _p(g_u.contiguous()), B, h, w, N, _p(wp_deconv5form), _p(u_prev),
-         _p(beta_eff), _p(gp), _p(gpt), _p(g_prev), _p(dn), _stream(g_u))
-    return g_prev, dn
+         _p(beta_eff), _p(gp), _p(gpt), _p(g_prev), _p(dn), _p(cs_g), _p(cs_d), _stream(g_u))
+    return g_prev, dn, sum_rows(cs_g), sum_rows(cs_d)
 
 
 def wgrad_k5(G: Tensor, X: Tensor) -> Tensor:
@@ -393,16 +415,15 @@ def wgrad_k9(G: Tensor, X: Tensor) -> Tensor:
     return dW
 
 
-def gdn_param_grads(dn: Tensor, u: Tensor, beta: Tensor, gamma: Tensor,
+def gdn_param_grads(dn: Tensor, u: Tensor, dbe: Tensor, beta: Tensor, gamma: Tensor,
                     beta_bound: float = DEFAULT_BETA_BOUND, gamma_bound: float = DEFAULT_GAMMA_BOUND):
-    """GDN parameter gradients (dβ, dγ) in the raw-parameter space (through GDN.py:73-79)."""
+    """GDN parameter gradients (dβ, dγ) in the raw-parameter space (through GDN.py:73-79);
+    dbe = ∂β_eff (Σ dn, from the backward kernel's column sums)."""
     C = dn.shape[-1]
     P = dn.numel() // C
     ws = torch.empty(query("iclr17_gdn_wgrad_workspace_size", P, C), device=dn.device, dtype=torch.float32)
     dge = torch.empty(C, C, device=dn.device, dtype=torch.float32)
-    dbe = torch.empty(C, device=dn.device, dtype=torch.float32)
-    call("iclr17_gdn_wgrad", _p(dn.contiguous()), _p(u.contiguous()), P, C, _p(ws), _p(dge), _p(dbe),
-         _stream(dn))
+    call("iclr17_gdn_wgrad", _p(dn.contiguous()), _p(u.contiguous()), P, C, _p(ws), _p(dge), _stream(dn))
     db = torch.empty_like(dbe)
     dg = torch.empty_like(dge)
     call("iclr17_gdn_param_chain", _p(beta.detach().contiguous()), _p(gamma.detach().contiguous()),
@@ -414,7 +435,7 @@ def gdn_param_grads(dn: Tensor, u: Tensor, beta: Tensor, gamma: Tensor,
 def bias_grad_nhwc(G: Tensor) -> Tensor:
     C = G.shape[-1]
     P = G.numel() // C
-    ws = torch.empty(64 * C, device=G.device, dtype=torch.float32)
+    ws = torch.empty(1024 * C, device=G.device, dtype=torch.float32)
     db = torch.empty(C, device=G.device, dtype=torch.float32)
     call("iclr17_bias_grad_nhwc", _p(G.contiguous()), P, C, _p(ws), _p(db), _stream(G))
     return db

@@ -156,12 +156,13 @@ int iclr17_grad_recon(const float* recon, const float* x, const float* g_mse, co
 int iclr17_bwd_deconv3_igdn(const float* g_recon, int B, int H, int W, int N,
                             const float* w_packed, const float* v_saved, const float* beta_eff,
                             const float* gamma_packed, const float* gamma_packed_t, float* g_v,
-                            float* dn, void* stream);
+                            float* dn, float* colsum_gv, float* colsum_dn, void* stream);
 /* synthesis_17.py:19-22 / :18 backward: g_v_prev = IGDNᵀ(conv2d(g_v, Wd, s2, p2)).
  * g_v NHWC [B,2h,2w,N]; v_prev = the previous deconv's pre-IGDN output NHWC [B,h,w,N]. */
 int iclr17_bwd_deconv_igdn(const float* g_v, int B, int h, int w, int N, const float* w_packed,
                            const float* v_prev, const float* beta_eff, const float* gamma_packed,
-                           const float* gamma_packed_t, float* g_v_prev, float* dn, void* stream);
+                           const float* gamma_packed_t, float* g_v_prev, float* dn,
+                           float* colsum_gv, float* colsum_dn, void* stream);
 /* synthesis_17.py:15 backward + model.py:71-78 rate backward:
  * g_y = conv2d(g_v1, Wd1, s2, p2) + (*g_bpp / count)·∂bits/∂ỹ; per-tile rate parameter partials
  * rate_partial[B * iclr17_rate_bwd_partials(h,w)][11][N]. g_bpp == NULL → no rate term. */
@@ -174,7 +175,14 @@ int iclr17_rate_bwd_partials(int h, int w);
  * u_prev = the previous conv's pre-GDN output NHWC [B,2h,2w,N]. */
 int iclr17_bwd_conv_gdn(const float* g_u, int B, int h, int w, int N, const float* w_packed,
                         const float* u_prev, const float* beta_eff, const float* gamma_packed,
-                        const float* gamma_packed_t, float* g_u_prev, float* dn, void* stream);
+                        const float* gamma_packed_t, float* g_u_prev, float* dn,
+                        float* colsum_gu, float* colsum_dn, void* stream);
+/* The three GDN-backward kernels above also emit (nullable) per-workgroup column sums of their
+ * two outputs, [B * iclr17_bwd_tiles(kind, h, w)][N] floats: Σ ∂u is the preceding layer's bias
+ * gradient and Σ dn is ∂β_eff. kind 0 (bwd_deconv3_igdn with (H/4, W/4), bwd_deconv_igdn with
+ * (h, w)), kind 1 (bwd_conv_gdn with (h, w)). Reduce them with iclr17_sum_rows. */
+int iclr17_bwd_tiles(int kind, int h, int w);
+int iclr17_sum_rows(const float* part, int T, int C, float* out, void* stream);
 /* Weight gradients in PyTorch layout [m][c][kh][kw] (split-K, fixed-order reduction):
  * k5: G NHWC [B,Ho,Wo,M], X NHWC [B,2Ho,2Wo,C], kind 5 (k5 s2 p2) — conv2/conv3 (G=∂u, X=input)
  *     and deconv1/deconv2 (G=input, X=∂output);
@@ -185,16 +193,17 @@ int iclr17_wgrad_k5(const float* G, const float* X, int B, int Ho, int Wo, int M
                     float* workspace, float* dW, void* stream);
 int iclr17_wgrad_k9(const float* G, const float* X, int B, int Ho, int Wo, int M,
                     float* workspace, float* dW, void* stream);
-/* GDN.py:83 parameter gradients: dgamma_eff[i][j] = Σ_p dn[p][i]·u[p][j]², dbeta_eff = Σ_p dn. */
+/* GDN.py:83 weight gradient: dgamma_eff[i][j] = Σ_p dn[p][i]·u[p][j]² (dβ_eff = Σ_p dn comes
+ * from the backward kernels' column sums). */
 size_t iclr17_gdn_wgrad_workspace_size(long P, int C);
 int iclr17_gdn_wgrad(const float* dn, const float* u, long P, int C, float* workspace,
-                     float* dgamma_eff, float* dbeta_eff, void* stream);
+                     float* dgamma_eff, void* stream);
 /* GDN.py:10-24,73-79 chain: dβ = LowerBoundᵀ(dβ_eff · 2·max(β, bβ)), same for γ. */
 int iclr17_gdn_param_chain(const float* beta, const float* gamma, const float* dbeta_eff,
                            const float* dgamma_eff, int C, float beta_bound, float gamma_bound,
                            float* dbeta, float* dgamma, void* stream);
 /* Bias gradients: Σ over pixels of an NHWC [P][C] or NCHW [B][C][HW] gradient.
- * Workspace: 64*C floats (NHWC), B*C floats (NCHW). */
+ * Workspace: 1024*C floats (NHWC), B*C floats (NCHW). */
 int iclr17_bias_grad_nhwc(const float* G, long P, int C, float* workspace, float* db, void* stream);
 int iclr17_bias_grad_nchw(const float* G, int B, int C, long HW, float* workspace, float* db,
                           void* stream);

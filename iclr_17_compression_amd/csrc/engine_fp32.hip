@@ -143,13 +143,17 @@ __device__ __forceinline__ void load_tile_rows(const EngineArgs& a, const TileIn
   }
 }
 
-// Column sums of an LDS tile [BM][ld] (rows outside the grid hold zeros) → dst[blockIdx.x][CO],
+// Column sums of an LDS tile [BM][ld] over the rows inside the output grid → dst[blockIdx.x][CO],
 // fixed row order (deterministic). Feeds bias / β gradients without another pass over HBM.
 template <int CO>
-__device__ __forceinline__ void tile_colsum(const float* s, int ld, float* dst) {
+__device__ __forceinline__ void tile_colsum(const EngineArgs& a, const TileInfo& t, const float* s,
+                                            int ld, float* dst) {
+  const int gy0 = t.ty * 8, gx0 = t.tx * 8;
+  const int rows = a.gh - gy0 < 8 ? a.gh - gy0 : 8, cols = a.gw - gx0 < 8 ? a.gw - gx0 : 8;
   for (int c = threadIdx.x; c < CO; c += 256) {
     float acc = 0.f;
-    for (int m = 0; m < BM; ++m) acc += s[m * ld + c];
+    for (int my = 0; my < rows; ++my)
+      for (int mx = 0; mx < cols; ++mx) acc += s[(my * 8 + mx) * ld + c];
     dst[(long)blockIdx.x * CO + c] = acc;
   }
 }
@@ -331,7 +335,7 @@ __device__ __forceinline__ void gdn_bwd_epilogue(f4 (&g)[MT][NT], float* smem, c
   __syncthreads();
   chan_gemm<CO, MT, NT>(acc2, sX, a.ggammaT, wm, ncol0, lane);  // w_j = Σ_i γ[i][j] dn_i
   store_tile_rows<CO>(a, t, sX, XS, a.tout, CO, 0);
-  if (a.colsum_t != nullptr) tile_colsum<CO>(sX, XS, a.colsum_t);
+  if (a.colsum_t != nullptr) tile_colsum<CO>(a, t, sX, XS, a.colsum_t);
   __syncthreads();
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
@@ -344,7 +348,7 @@ __device__ __forceinline__ void gdn_bwd_epilogue(f4 (&g)[MT][NT], float* smem, c
       }
   __syncthreads();
   store_tile_rows<CO>(a, t, sX, XS, a.out, CO, 0);
-  if (a.colsum_out != nullptr) tile_colsum<CO>(sX, XS, a.colsum_out);
+  if (a.colsum_out != nullptr) tile_colsum<CO>(a, t, sX, XS, a.colsum_out);
 }
 
 // ------------------------------------------------------------------------- rate backward epilogue

@@ -35,7 +35,8 @@ namespace iclr17 {
 
 constexpr int BM = 64;        // output pixels per tile
 constexpr int KC = 32;        // input channels per k-step
-constexpr int ASTR = KC + 4;  // LDS row stride of the A tile (floats)
+constexpr int ASTR = KC + 8;  // LDS row stride of the A tile (floats): 40 makes the
+                              // ds_read_b128 fragment reads bank-conflict free
 
 enum Epi : int {
   EPI_GDN = 0, EPI_IGDN = 1, EPI_QUANT = 2, EPI_OUT3 = 3, EPI_PLAIN = 4,
@@ -46,9 +47,11 @@ struct TapTable {
   int npx;            // phases along x
   int nph;            // total phases
   int begin[17];      // taps of phase p: [begin[p], begin[p+1])
-  signed char dy[64];
-  signed char dx[64];
+  int dydx[64];       // (dy + 128) | (dx + 128) << 8 — dword entries so the wave-uniform lookup
+                      // is a scalar kernarg load (a byte array becomes a VMEM load + vmcnt(0))
 };
+
+__host__ __device__ inline int pack_tap(int dy, int dx) { return (dy + 128) | ((dx + 128) << 8); }
 
 struct EngineArgs {
   const float* in;      // NHWC [B][Hin][Win][CI]   (conv1: NCHW image)
@@ -191,7 +194,7 @@ template <int CO, int MT, int NT, bool SQ = false>
 __device__ __forceinline__ void chan_gemm(f4 (&acc)[MT][NT], const float* sX,
                                           const float* __restrict__ bp, int wm, int ncol0,
                                           int lane) {
-  constexpr int XS = CO + 4;
+  constexpr int XS = CO + 8;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -231,7 +234,7 @@ __device__ __forceinline__ void gdn_core(const f4 (&x)[MT][NT], float* sX,
                                          const float* __restrict__ gbeta,
                                          const float* __restrict__ gp, int wm, int ncol0,
                                          int lane) {
-  constexpr int XS = CO + 4;
+  constexpr int XS = CO + 8;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -280,7 +283,7 @@ __device__ __forceinline__ void acc_to_lds(const f4 (&v)[MT][NT], float* s, int 
 template <int CO, int MT, int NT, bool INVERSE>
 __device__ __forceinline__ void gdn_epilogue(f4 (&x)[MT][NT], float* smem, const EngineArgs& a,
                                              const TileInfo& t, int wm, int ncol0, int lane) {
-  constexpr int XS = CO + 4;
+  constexpr int XS = CO + 8;
   gdn_core<CO, MT, NT, INVERSE>(x, smem, a.gbeta, a.ggamma, wm, ncol0, lane);
   store_tile_rows<CO>(a, t, smem, XS, a.out, CO, 0);
   if (a.pre != nullptr) {
@@ -301,7 +304,7 @@ __device__ __forceinline__ void gdn_epilogue(f4 (&x)[MT][NT], float* smem, const
 template <int CO, int MT, int NT, bool INVERSE>
 __device__ __forceinline__ void gdn_bwd_epilogue(f4 (&g)[MT][NT], float* smem, const EngineArgs& a,
                                                  const TileInfo& t, int wm, int ncol0, int lane) {
-  constexpr int XS = CO + 4;
+  constexpr int XS = CO + 8;
   float* sX = smem;
   load_tile_rows<CO>(a, t, a.saved, sX, XS, CO, 0);   // u, kept in LDS through GEMM 1
   __syncthreads();
@@ -580,7 +583,7 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
   constexpr int NCH = CI / KC;
   constexpr int LDS_A = 2 * BM * ASTR;
   constexpr int LDS_X = (EPI == EPI_GDN || EPI == EPI_IGDN || EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD)
-                            ? BM * (CO + 4) : 0;
+                            ? BM * (CO + 8) : 0;
   constexpr int LDS_O = BM * (BN + 4) + 8;
   constexpr int LDS_3 = 3 * 32 * 33 + 8;
   constexpr int L1 = LDS_A > LDS_X ? LDS_A : LDS_X;
@@ -614,19 +617,31 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
   }
   const float* __restrict__ inb = a.in + (long)t.b * a.Hin * a.Win * CI + (tid & 7) * 4;
 
-  auto load_a = [&](int s, f4 (&r)[2]) {
+  // Branchless staging loads: out-of-image taps read a valid address and are zeroed by a
+  // select, so no exec-masked branch (and no conservative s_waitcnt) enters the k-loop.
+  // The zero-select is applied when the registers are written to LDS (store_a), after the
+  // MFMA block, so nothing before the MFMAs consumes the loaded values.
+  auto load_a = [&](int s, f4 (&r)[2], bool (&okr)[2]) {
     const int tap = t0 + s / NCH, cc = s - (s / NCH) * NCH;
-    const int dy = a.tt.dy[tap], dx = a.tt.dx[tap];
+    const int td = a.tt.dydx[tap];
+    const int dy = (td & 0xff) - 128, dx = ((td >> 8) & 0xff) - 128;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int iy = sgy[i] + dy, ix = sgx[i] + dx;
       const bool ok = sval[i] && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
-      r[i] = ok ? *(const f4*)(inb + ((long)iy * a.Win + ix) * CI + cc * KC) : f4{0.f, 0.f, 0.f, 0.f};
+      const long off = ok ? ((long)iy * a.Win + ix) * CI + cc * KC : 0;
+      r[i] = *(const f4*)(inb + off);
+      okr[i] = ok;
     }
   };
   auto load_b = [&](int s, f4 (&bf)[2][NT]) {
     const int tap = t0 + s / NCH, cc = s - (s / NCH) * NCH;
     load_bfrag<NT, CO>(bf, a.w + (long)tap * CI * CO, cc * 8, ncol0, lane);
+  };
+  auto store_a = [&](int buf, const f4 (&r)[2], const bool (&okr)[2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      *(f4*)(smem + buf * BM * ASTR + soff[i]) = okr[i] ? r[i] : f4{0.f, 0.f, 0.f, 0.f};
   };
 
   f4 acc[MT][NT];
@@ -635,22 +650,8 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
 
-  f4 ra[2];
-  f4 bcur[2][NT], bnxt[2][NT];
-  load_a(0, ra);
-  load_b(0, bcur);
-#pragma unroll
-  for (int i = 0; i < 2; ++i) *(f4*)(smem + soff[i]) = ra[i];
-  __syncthreads();
-
-  for (int s = 0; s < nsteps; ++s) {
-    const int cur = s & 1;
-    const bool more = s + 1 < nsteps;
-    if (more) {
-      load_a(s + 1, ra);
-      load_b(s + 1, bnxt);
-    }
-    const float* As = smem + cur * BM * ASTR;
+  auto compute = [&](int buf, const f4 (&bf)[2][NT]) {
+    const float* As = smem + buf * BM * ASTR;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       f4 af[MT];
@@ -658,17 +659,43 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
       for (int mt = 0; mt < MT; ++mt)
         af[mt] = *(const f4*)(As + (wm * MT * 16 + mt * 16 + (lane & 15)) * ASTR + kk * 16 +
                               4 * (lane >> 4));
-      mfma_block<MT, NT>(acc, af, bcur[kk]);
+      mfma_block<MT, NT>(acc, af, bf[kk]);
     }
-    if (more) {
-      float* An = smem + (cur ^ 1) * BM * ASTR;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) *(f4*)(An + soff[i]) = ra[i];
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) bcur[kk][nt] = bnxt[kk][nt];
-    }
+  };
+
+  // k-loop unrolled by two with ping-pong B-fragment registers (no register copies): step s
+  // computes from LDS buffer s&1 while step s+1's A tile and B fragments are in flight.
+  f4 ra[2];
+  bool oka[2];
+  f4 b0[2][NT], b1[2][NT];
+  load_a(0, ra, oka);
+  load_b(0, b0);
+  store_a(0, ra, oka);
+  __syncthreads();
+  int s = 0;
+  for (; s + 1 < nsteps; s += 2) {
+    load_a(s + 1, ra, oka);
+    load_b(s + 1, b1);
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the MFMAs (the scheduler
+                                        // would otherwise sink it to its use, exposing latency)
+    compute(0, b0);
+    __builtin_amdgcn_sched_barrier(0);  // and keep the MFMAs ahead of the LDS store + barrier
+                                        // (register-only MFMAs may otherwise move past them)
+    store_a(1, ra, oka);
+    __syncthreads();
+    // the step-(s+2) prefetch is issued unconditionally (clamped to a valid step) so the loop
+    // body is branch free; past the end its data is simply not used
+    const int sn = s + 2 < nsteps ? s + 2 : nsteps - 1;
+    load_a(sn, ra, oka);
+    load_b(sn, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    store_a(0, ra, oka);
+    __syncthreads();
+  }
+  if (s < nsteps) {
+    compute(0, b0);
     __syncthreads();
   }
 
@@ -726,7 +753,7 @@ __global__ void __launch_bounds__(256) conv1_gdn_kernel(const EngineArgs a) {
   constexpr int MT = BM / 16;
   constexpr int NT = CO / WN / 16;
   constexpr int LDS_P = P1ZERO + 1 + 256 + 64 + 3;  // patch + zero + k table + m table
-  constexpr int LDS_X = BM * (CO + 4);
+  constexpr int LDS_X = BM * (CO + 8);
   constexpr int LDS_FLOATS = LDS_P > LDS_X ? LDS_P : LDS_X;
   __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
   int* ktab = (int*)(smem + P1ZERO + 4);
@@ -883,10 +910,7 @@ void fill_conv5_taps(TapTable& tt) {
   tt.begin[0] = 0;
   tt.begin[1] = 25;
   for (int kh = 0; kh < 5; ++kh)
-    for (int kw = 0; kw < 5; ++kw) {
-      tt.dy[kh * 5 + kw] = (signed char)(kh - 2);
-      tt.dx[kh * 5 + kw] = (signed char)(kw - 2);
-    }
+    for (int kw = 0; kw < 5; ++kw) tt.dydx[kh * 5 + kw] = pack_tap(kh - 2, kw - 2);
 }
 
 // ConvTranspose2d(k, stride s, pad p): output o = s·q + r receives input q + d through kernel
@@ -905,8 +929,7 @@ void fill_deconv_taps(TapTable& tt, int K, int s, int p) {
         for (int dx = 2; dx >= -2; --dx) {
           const int kw = rx + p - s * dx;
           if (kw < 0 || kw >= K) continue;
-          tt.dy[n] = (signed char)dy;
-          tt.dx[n] = (signed char)dx;
+          tt.dydx[n] = pack_tap(dy, dx);
           ++n;
         }
       }
@@ -919,10 +942,7 @@ void fill_neigh3_taps(TapTable& tt) {
   tt.npx = 1;
   tt.nph = 1;
   tt.begin[1] = 9;
-  for (int i = 0; i < 9; ++i) {
-    tt.dy[i] = (signed char)(i / 3 - 1);
-    tt.dx[i] = (signed char)(i % 3 - 1);
-  }
+  for (int i = 0; i < 9; ++i) tt.dydx[i] = pack_tap(i / 3 - 1, i % 3 - 1);
 }
 
 hipStream_t S(void* s) { return (hipStream_t)s; }

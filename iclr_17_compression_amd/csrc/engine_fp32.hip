@@ -846,7 +846,7 @@ template <int C, bool INVERSE, int LAYOUT>
 __global__ void __launch_bounds__(256) gdn_kernel(const float* __restrict__ x, int HW,
                                                   const float* __restrict__ beta,
                                                   const float* __restrict__ gp, float* y) {
-  constexpr int XS = C + 4;
+  constexpr int XS = C + 8;   // must match gdn_core's row stride
   constexpr int WN = 4, MT = 4, NT = C / WN / 16;
   __shared__ __attribute__((aligned(16))) float smem[BM * XS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;

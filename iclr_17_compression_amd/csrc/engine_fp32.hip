@@ -580,8 +580,13 @@ template <int CI, int CO, int BN, int WM, int WN, int EPI>
 __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
   constexpr int MT = BM / WM / 16;
   constexpr int NT = BN / WN / 16;
-  constexpr int NCH = CI / KC;
-  constexpr int LDS_A = 2 * BM * ASTR;
+  constexpr int KCH = CI % 64 == 0 ? 64 : 32;   // input channels per k-step
+  constexpr int KK = KCH / 16;                   // 16-deep MFMA k-blocks per step
+  constexpr int AS = KCH + 8;                    // A row stride: ≡ 8 (mod 64) → conflict free
+  constexpr int NCH = CI / KCH;
+  constexpr int C4 = KCH / 4;                    // 16-byte chunks per A row
+  constexpr int AL = BM * C4 / 256;              // A staging loads per thread per step
+  constexpr int LDS_A = 2 * BM * AS;
   constexpr int LDS_X = (EPI == EPI_GDN || EPI == EPI_IGDN || EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD)
                             ? BM * (CO + 8) : 0;
   constexpr int LDS_O = BM * (BN + 4) + 8;
@@ -591,6 +596,7 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
   constexpr int LDS_FLOATS = L1 > L2 ? L1 : L2;
   static_assert(MT * WM * 16 == BM && NT * WN * 16 == BN, "tile shape");
   static_assert(WM * WN == 4, "4 waves");
+  static_assert(AL * 256 == BM * C4, "staging split");
   __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -601,47 +607,57 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
   const int nsteps = (a.tt.begin[ph + 1] - t0) * NCH;
   const int ncol0 = t.nb * BN + wn * (BN / WN);
 
-  // A staging assignment: 2 float4 per thread, row = idx>>3, 16-byte column c4 = idx&7
-  int sgy[2], sgx[2], soff[2];
-  bool sval[2];
+  // A staging: thread owns AL rows (pixels) × one 16-byte column chunk. All per-thread address
+  // arithmetic is hoisted; a step adds one wave-uniform offset (tap shift + channel chunk).
+  int iy0[AL], ix0[AL], pbase[AL], soff[AL];
+  bool rval[AL];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < AL; ++i) {
     const int idx = tid + 256 * i;
-    const int row = idx >> 3;
-    sgy[i] = t.ty * 8 + (row >> 3);
-    sgx[i] = t.tx * 8 + (row & 7);
-    sval[i] = sgy[i] < a.gh && sgx[i] < a.gw;
-    soff[i] = row * ASTR + (idx & 7) * 4;
-    sgy[i] *= a.sin;
-    sgx[i] *= a.sin;
+    const int row = idx / C4, c4 = idx % C4;
+    const int gy = t.ty * 8 + (row >> 3), gx = t.tx * 8 + (row & 7);
+    rval[i] = gy < a.gh && gx < a.gw;
+    iy0[i] = gy * a.sin;
+    ix0[i] = gx * a.sin;
+    pbase[i] = (iy0[i] * a.Win + ix0[i]) * CI + c4 * 4;
+    soff[i] = row * AS + c4 * 4;
   }
-  const float* __restrict__ inb = a.in + (long)t.b * a.Hin * a.Win * CI + (tid & 7) * 4;
+  const float* __restrict__ inb = a.in + (long)t.b * a.Hin * a.Win * CI;
+  // B fragment lane offsets (floats) within one step's packed weight slice
+  int boff[KK][NT];
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+      boff[kk][nt] = ((kk * 4 + (lane >> 4)) * CO + ncol0 + nt * 16 + (lane & 15)) * 4;
 
-  // Branchless staging loads: out-of-image taps read a valid address and are zeroed by a
-  // select, so no exec-masked branch (and no conservative s_waitcnt) enters the k-loop.
-  // The zero-select is applied when the registers are written to LDS (store_a), after the
-  // MFMA block, so nothing before the MFMAs consumes the loaded values.
-  auto load_a = [&](int s, f4 (&r)[2], bool (&okr)[2]) {
+  // Branchless staging loads (out-of-image taps read a valid address; the zero-select happens
+  // at the LDS store, after the MFMA block, so nothing before the MFMAs waits on them).
+  auto load_a = [&](int s, f4 (&r)[AL], bool (&okr)[AL]) {
     const int tap = t0 + s / NCH, cc = s - (s / NCH) * NCH;
     const int td = a.tt.dydx[tap];
     const int dy = (td & 0xff) - 128, dx = ((td >> 8) & 0xff) - 128;
+    const int so = (dy * a.Win + dx) * CI + cc * KCH;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int iy = sgy[i] + dy, ix = sgx[i] + dx;
-      const bool ok = sval[i] && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
-      const long off = ok ? ((long)iy * a.Win + ix) * CI + cc * KC : 0;
-      r[i] = *(const f4*)(inb + off);
+    for (int i = 0; i < AL; ++i) {
+      const bool ok = rval[i] && (unsigned)(iy0[i] + dy) < (unsigned)a.Hin &&
+                      (unsigned)(ix0[i] + dx) < (unsigned)a.Win;
+      r[i] = *(const f4*)(inb + (ok ? pbase[i] + so : 0));
       okr[i] = ok;
     }
   };
-  auto load_b = [&](int s, f4 (&bf)[2][NT]) {
+  auto load_b = [&](int s, f4 (&bf)[KK][NT]) {
     const int tap = t0 + s / NCH, cc = s - (s / NCH) * NCH;
-    load_bfrag<NT, CO>(bf, a.w + (long)tap * CI * CO, cc * 8, ncol0, lane);
-  };
-  auto store_a = [&](int buf, const f4 (&r)[2], const bool (&okr)[2]) {
+    const float* __restrict__ ws = a.w + ((long)tap * CI + cc * KCH) * CO;   // uniform base
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      *(f4*)(smem + buf * BM * ASTR + soff[i]) = okr[i] ? r[i] : f4{0.f, 0.f, 0.f, 0.f};
+    for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) bf[kk][nt] = *(const f4*)(ws + boff[kk][nt]);
+  };
+  auto store_a = [&](int buf, const f4 (&r)[AL], const bool (&okr)[AL]) {
+#pragma unroll
+    for (int i = 0; i < AL; ++i)
+      *(f4*)(smem + buf * BM * AS + soff[i]) = okr[i] ? r[i] : f4{0.f, 0.f, 0.f, 0.f};
   };
 
   f4 acc[MT][NT];
@@ -650,24 +666,23 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](int buf, const f4 (&bf)[2][NT]) {
-    const float* As = smem + buf * BM * ASTR;
+  auto compute = [&](int buf, const f4 (&bf)[KK][NT]) {
+    const float* As = smem + buf * BM * AS + (wm * MT * 16 + (lane & 15)) * AS + 4 * (lane >> 4);
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < KK; ++kk) {
       f4 af[MT];
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-        af[mt] = *(const f4*)(As + (wm * MT * 16 + mt * 16 + (lane & 15)) * ASTR + kk * 16 +
-                              4 * (lane >> 4));
+      for (int mt = 0; mt < MT; ++mt) af[mt] = *(const f4*)(As + mt * 16 * AS + kk * 16);
       mfma_block<MT, NT>(acc, af, bf[kk]);
     }
   };
 
   // k-loop unrolled by two with ping-pong B-fragment registers (no register copies): step s
-  // computes from LDS buffer s&1 while step s+1's A tile and B fragments are in flight.
-  f4 ra[2];
-  bool oka[2];
-  f4 b0[2][NT], b1[2][NT];
+  // computes from LDS buffer s&1 while step s+1's A tile and B fragments are in flight. The
+  // sched_barriers pin the prefetch ahead of, and the LDS store + barrier behind, the MFMAs.
+  f4 ra[AL];
+  bool oka[AL];
+  f4 b0[KK][NT], b1[KK][NT];
   load_a(0, ra, oka);
   load_b(0, b0);
   store_a(0, ra, oka);
@@ -676,16 +691,12 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
   for (; s + 1 < nsteps; s += 2) {
     load_a(s + 1, ra, oka);
     load_b(s + 1, b1);
-    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the MFMAs (the scheduler
-                                        // would otherwise sink it to its use, exposing latency)
+    __builtin_amdgcn_sched_barrier(0);
     compute(0, b0);
-    __builtin_amdgcn_sched_barrier(0);  // and keep the MFMAs ahead of the LDS store + barrier
-                                        // (register-only MFMAs may otherwise move past them)
+    __builtin_amdgcn_sched_barrier(0);
     store_a(1, ra, oka);
     __syncthreads();
-    // the step-(s+2) prefetch is issued unconditionally (clamped to a valid step) so the loop
-    // body is branch free; past the end its data is simply not used
-    const int sn = s + 2 < nsteps ? s + 2 : nsteps - 1;
+    const int sn = s + 2 < nsteps ? s + 2 : nsteps - 1;   // branch-free: clamp the prefetch
     load_a(sn, ra, oka);
     load_b(sn, b0);
     __builtin_amdgcn_sched_barrier(0);

@@ -33,6 +33,12 @@
 
 namespace iclr17 {
 
+// Diagnostic ablation builds only (tools/ablate.sh): -DICLR17_ABL=bitmask
+//   1 = no A global loads, 2 = no B loads, 4 = no A LDS stores/barriers, 8 = no epilogue math
+#ifndef ICLR17_ABL
+#define ICLR17_ABL 0
+#endif
+
 constexpr int BM = 64;        // output pixels per tile
 constexpr int KC = 32;        // input channels per k-step
 constexpr int ASTR = KC + 8;  // LDS row stride of the A tile (floats): 40 makes the
@@ -642,7 +648,10 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
     for (int i = 0; i < AL; ++i) {
       const bool ok = rval[i] && (unsigned)(iy0[i] + dy) < (unsigned)a.Hin &&
                       (unsigned)(ix0[i] + dx) < (unsigned)a.Win;
-      r[i] = *(const f4*)(inb + (ok ? pbase[i] + so : 0));
+      if (ICLR17_ABL & 1)
+        r[i] = f4{(float)so, 1.f, 2.f, 3.f};
+      else
+        r[i] = *(const f4*)(inb + (ok ? pbase[i] + so : 0));
       okr[i] = ok;
     }
   };
@@ -652,9 +661,19 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk)
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) bf[kk][nt] = *(const f4*)(ws + boff[kk][nt]);
+      for (int nt = 0; nt < NT; ++nt) {
+        if (ICLR17_ABL & 2)
+          bf[kk][nt] = f4{(float)(s + kk), (float)nt, 1.f, 2.f};
+        else
+          bf[kk][nt] = *(const f4*)(ws + boff[kk][nt]);
+      }
   };
   auto store_a = [&](int buf, const f4 (&r)[AL], const bool (&okr)[AL]) {
+    if (ICLR17_ABL & 4) {
+#pragma unroll
+      for (int i = 0; i < AL; ++i) asm volatile("" :: "v"(r[i]), "v"(okr[i]));
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < AL; ++i)
       *(f4*)(smem + buf * BM * AS + soff[i]) = okr[i] ? r[i] : f4{0.f, 0.f, 0.f, 0.f};
@@ -695,7 +714,7 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
     compute(0, b0);
     __builtin_amdgcn_sched_barrier(0);
     store_a(1, ra, oka);
-    __syncthreads();
+    if (!(ICLR17_ABL & 4)) __syncthreads();
     const int sn = s + 2 < nsteps ? s + 2 : nsteps - 1;   // branch-free: clamp the prefetch
     load_a(sn, ra, oka);
     load_b(sn, b0);
@@ -703,7 +722,16 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
     compute(1, b1);
     __builtin_amdgcn_sched_barrier(0);
     store_a(0, ra, oka);
-    __syncthreads();
+    if (!(ICLR17_ABL & 4)) __syncthreads();
+  }
+  if (ICLR17_ABL & 8) {   // diagnostic: keep the accumulators live, skip the epilogue
+    float sum = 0.f;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) sum += acc[mt][nt][0] + acc[mt][nt][1] + acc[mt][nt][2] + acc[mt][nt][3];
+    if (sum == 12345.f) a.out[0] = sum;
+    return;
   }
   if (s < nsteps) {
     compute(0, b0);

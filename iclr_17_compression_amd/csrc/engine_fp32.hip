@@ -11,10 +11,10 @@
 //
 // Tile: 64 output pixels (an 8×8 block of the base grid) × BN output channels per 256-thread
 // workgroup (4 waves). GEMM mapping: M = pixels, N = output channels, K = (tap, input channel).
-// MFMA: v_mfma_f32_16x16x4_f32 (exact f32). A fragments come from an LDS tile (double
-// buffered, register staged so out-of-image taps become zeros); B fragments (packed weights,
-// [tap][Cin/4][Cout][4]) are read straight from L2 into registers, one step ahead — with the
-// waves split along N no two waves share a B fragment, so B never touches LDS.
+// MFMA: v_mfma_f32_16x16x4_f32 (exact f32). Both operands are staged in LDS by LDS-DMA
+// (global_load_lds): the A tile (input pixels × 32 channels of one tap; out-of-image taps DMA
+// from a zero line) and the B tile (packed weights [tap][Cin/4][Cout][4] of the same step),
+// double buffered, one barrier per k-step.
 //
 // "float4 k-trick": a lane loads 4 consecutive input channels of its pixel with one 16-byte
 // read and feeds them to 4 successive MFMAs; MFMA e of a 16-deep k-block therefore covers
@@ -33,16 +33,12 @@
 
 namespace iclr17 {
 
-// Diagnostic ablation builds only (tools/ablate.sh): -DICLR17_ABL=bitmask
-//   1 = no A global loads, 2 = no B loads, 4 = no A LDS stores/barriers, 8 = no epilogue math
+// Diagnostic ablation builds only (tools/ablate.sh): -DICLR17_ABL=8 skips the engine epilogue
 #ifndef ICLR17_ABL
 #define ICLR17_ABL 0
 #endif
 
 constexpr int BM = 64;        // output pixels per tile
-constexpr int KC = 32;        // input channels per k-step
-constexpr int ASTR = KC + 8;  // LDS row stride of the A tile (floats): 40 makes the
-                              // ds_read_b128 fragment reads bank-conflict free
 
 enum Epi : int {
   EPI_GDN = 0, EPI_IGDN = 1, EPI_QUANT = 2, EPI_OUT3 = 3, EPI_PLAIN = 4,
@@ -582,17 +578,35 @@ __device__ __forceinline__ void out3_epilogue(f4 (&acc)[MT][NT], float* smem, co
 }
 
 // ------------------------------------------------------------------------- the engine kernel
+// Zero source for glds lanes whose tap falls outside the image (padding).
+__device__ __attribute__((aligned(16))) float g_zero16[4] = {0.f, 0.f, 0.f, 0.f};
+
+__device__ __forceinline__ void glds16(const float* src, float* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+// Main loop: both operands reach LDS by LDS-DMA (global_load_lds_dwordx4), so no staging VGPRs
+// and no ds_write pass. A step is 32 input channels of one tap:
+//   A image [BM][32] floats, 128-byte rows, 16-byte chunk c stored at c ^ (row & 7) — the swizzle
+//     lives in the per-lane SOURCE address (glds writes lane-linear), and makes the fragment
+//     reads (16 rows × one chunk per lane group) bank-conflict free;
+//   B image [8 quads][BN][4] floats: the packed weights of the step, copied linearly.
+// Two LDS stages, one barrier per step: the DMA of step s+1 is in flight while step s computes.
 template <int CI, int CO, int BN, int WM, int WN, int EPI>
 __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
   constexpr int MT = BM / WM / 16;
   constexpr int NT = BN / WN / 16;
-  constexpr int KCH = CI % 64 == 0 ? 64 : 32;   // input channels per k-step
-  constexpr int KK = KCH / 16;                   // 16-deep MFMA k-blocks per step
-  constexpr int AS = KCH + 8;                    // A row stride: ≡ 8 (mod 64) → conflict free
+  constexpr int KCH = 32;                        // input channels per k-step
   constexpr int NCH = CI / KCH;
-  constexpr int C4 = KCH / 4;                    // 16-byte chunks per A row
-  constexpr int AL = BM * C4 / 256;              // A staging loads per thread per step
-  constexpr int LDS_A = 2 * BM * AS;
+  constexpr int SA = BM * KCH;                   // A image floats per stage
+  constexpr int SB = KCH * BN;                   // B image floats per stage
+  constexpr int STAGE = SA + SB;
+  constexpr int NAI = SA * 4 / 1024;             // A glds wave-instructions per step (8)
+  constexpr int NBI = SB * 4 / 1024;             // B glds wave-instructions per step
+  constexpr int AI_W = NAI / 4;                  // per wave
+  constexpr int BI_W = (NBI + 3) / 4;
+  constexpr int LDS_A = 2 * STAGE;
   constexpr int LDS_X = (EPI == EPI_GDN || EPI == EPI_IGDN || EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD)
                             ? BM * (CO + 8) : 0;
   constexpr int LDS_O = BM * (BN + 4) + 8;
@@ -602,7 +616,9 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
   constexpr int LDS_FLOATS = L1 > L2 ? L1 : L2;
   static_assert(MT * WM * 16 == BM && NT * WN * 16 == BN, "tile shape");
   static_assert(WM * WN == 4, "4 waves");
-  static_assert(AL * 256 == BM * C4, "staging split");
+  static_assert(CI % KCH == 0 && NAI % 4 == 0, "k-step split");
+  static_assert(BN == CO || BN == 64, "B image: whole rows, or one 1 KB piece per quad row");
+  static_assert((SB * 4) % 1024 == 0, "B image in whole wave-instructions");
   __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -613,70 +629,48 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
   const int nsteps = (a.tt.begin[ph + 1] - t0) * NCH;
   const int ncol0 = t.nb * BN + wn * (BN / WN);
 
-  // A staging: thread owns AL rows (pixels) × one 16-byte column chunk. All per-thread address
-  // arithmetic is hoisted; a step adds one wave-uniform offset (tap shift + channel chunk).
-  int iy0[AL], ix0[AL], pbase[AL], soff[AL];
-  bool rval[AL];
+  // A DMA: wave-instruction i covers rows 8i .. 8i+7; lane → (row, physical chunk lane & 7),
+  // fetching logical chunk (lane & 7) ^ (row & 7).
+  int iy0[AI_W], ix0[AI_W], pbase[AI_W];
+  bool rval[AI_W];
 #pragma unroll
-  for (int i = 0; i < AL; ++i) {
-    const int idx = tid + 256 * i;
-    const int row = idx / C4, c4 = idx % C4;
+  for (int j = 0; j < AI_W; ++j) {
+    const int row = (wave * AI_W + j) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (row & 7);
     const int gy = t.ty * 8 + (row >> 3), gx = t.tx * 8 + (row & 7);
-    rval[i] = gy < a.gh && gx < a.gw;
-    iy0[i] = gy * a.sin;
-    ix0[i] = gx * a.sin;
-    pbase[i] = (iy0[i] * a.Win + ix0[i]) * CI + c4 * 4;
-    soff[i] = row * AS + c4 * 4;
+    rval[j] = gy < a.gh && gx < a.gw;
+    iy0[j] = gy * a.sin;
+    ix0[j] = gx * a.sin;
+    pbase[j] = (iy0[j] * a.Win + ix0[j]) * CI + c * 4;
   }
   const float* __restrict__ inb = a.in + (long)t.b * a.Hin * a.Win * CI;
-  // B fragment lane offsets (floats) within one step's packed weight slice
-  int boff[KK][NT];
+  // B DMA: wave-instruction i copies 1 KB; source offset (floats) within the step's slice
+  int bsrc[BI_W];
 #pragma unroll
-  for (int kk = 0; kk < KK; ++kk)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-      boff[kk][nt] = ((kk * 4 + (lane >> 4)) * CO + ncol0 + nt * 16 + (lane & 15)) * 4;
+  for (int j = 0; j < BI_W; ++j) {
+    const int i = wave + 4 * j;
+    bsrc[j] = (BN == CO) ? i * 256 + lane * 4 : (i * CO + t.nb * BN) * 4 + lane * 4;
+  }
 
-  // Branchless staging loads (out-of-image taps read a valid address; the zero-select happens
-  // at the LDS store, after the MFMA block, so nothing before the MFMAs waits on them).
-  auto load_a = [&](int s, f4 (&r)[AL], bool (&okr)[AL]) {
+  auto issue = [&](int s, int buf) {
     const int tap = t0 + s / NCH, cc = s - (s / NCH) * NCH;
     const int td = a.tt.dydx[tap];
     const int dy = (td & 0xff) - 128, dx = ((td >> 8) & 0xff) - 128;
     const int so = (dy * a.Win + dx) * CI + cc * KCH;
+    float* sa = smem + buf * STAGE;
 #pragma unroll
-    for (int i = 0; i < AL; ++i) {
-      const bool ok = rval[i] && (unsigned)(iy0[i] + dy) < (unsigned)a.Hin &&
-                      (unsigned)(ix0[i] + dx) < (unsigned)a.Win;
-      if (ICLR17_ABL & 1)
-        r[i] = f4{(float)so, 1.f, 2.f, 3.f};
-      else
-        r[i] = *(const f4*)(inb + (ok ? pbase[i] + so : 0));
-      okr[i] = ok;
+    for (int j = 0; j < AI_W; ++j) {
+      const bool ok = rval[j] && (unsigned)(iy0[j] + dy) < (unsigned)a.Hin &&
+                      (unsigned)(ix0[j] + dx) < (unsigned)a.Win;
+      glds16(ok ? inb + pbase[j] + so : g_zero16, sa + (wave * AI_W + j) * 256);
     }
-  };
-  auto load_b = [&](int s, f4 (&bf)[KK][NT]) {
-    const int tap = t0 + s / NCH, cc = s - (s / NCH) * NCH;
     const float* __restrict__ ws = a.w + ((long)tap * CI + cc * KCH) * CO;   // uniform base
+    float* sb = sa + SA;
 #pragma unroll
-    for (int kk = 0; kk < KK; ++kk)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        if (ICLR17_ABL & 2)
-          bf[kk][nt] = f4{(float)(s + kk), (float)nt, 1.f, 2.f};
-        else
-          bf[kk][nt] = *(const f4*)(ws + boff[kk][nt]);
-      }
-  };
-  auto store_a = [&](int buf, const f4 (&r)[AL], const bool (&okr)[AL]) {
-    if (ICLR17_ABL & 4) {
-#pragma unroll
-      for (int i = 0; i < AL; ++i) asm volatile("" :: "v"(r[i]), "v"(okr[i]));
-      return;
+    for (int j = 0; j < BI_W; ++j) {
+      const int i = wave + 4 * j;
+      if (NBI % 4 == 0 || i < NBI) glds16(ws + bsrc[j], sb + i * 256);
     }
-#pragma unroll
-    for (int i = 0; i < AL; ++i)
-      *(f4*)(smem + buf * BM * AS + soff[i]) = okr[i] ? r[i] : f4{0.f, 0.f, 0.f, 0.f};
   };
 
   f4 acc[MT][NT];
@@ -685,45 +679,38 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](int buf, const f4 (&bf)[KK][NT]) {
-    const float* As = smem + buf * BM * AS + (wm * MT * 16 + (lane & 15)) * AS + 4 * (lane >> 4);
+  // fragment read offsets (floats) within a stage
+  int aoff[2][MT];
 #pragma unroll
-    for (int kk = 0; kk < KK; ++kk) {
-      f4 af[MT];
+  for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) af[mt] = *(const f4*)(As + mt * 16 * AS + kk * 16);
-      mfma_block<MT, NT>(acc, af, bf[kk]);
+    for (int mt = 0; mt < MT; ++mt) {
+      const int row = wm * MT * 16 + mt * 16 + (lane & 15);
+      aoff[kk][mt] = row * KCH + (((kk * 4 + (lane >> 4)) ^ (row & 7)) * 4);
+    }
+  const int boff0 = ((lane >> 4) * BN + wn * (BN / WN) + (lane & 15)) * 4;
+
+  auto compute = [&](int buf) {
+    const float* sa = smem + buf * STAGE;
+    const float* sb = sa + SA + boff0;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      f4 af[MT], bf[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) bf[nt] = *(const f4*)(sb + kk * 16 * BN + nt * 64);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) af[mt] = *(const f4*)(sa + aoff[kk][mt]);
+      mfma_block<MT, NT>(acc, af, bf);
     }
   };
 
-  // k-loop unrolled by two with ping-pong B-fragment registers (no register copies): step s
-  // computes from LDS buffer s&1 while step s+1's A tile and B fragments are in flight. The
-  // sched_barriers pin the prefetch ahead of, and the LDS store + barrier behind, the MFMAs.
-  f4 ra[AL];
-  bool oka[AL];
-  f4 b0[KK][NT], b1[KK][NT];
-  load_a(0, ra, oka);
-  load_b(0, b0);
-  store_a(0, ra, oka);
-  __syncthreads();
-  int s = 0;
-  for (; s + 1 < nsteps; s += 2) {
-    load_a(s + 1, ra, oka);
-    load_b(s + 1, b1);
-    __builtin_amdgcn_sched_barrier(0);
-    compute(0, b0);
-    __builtin_amdgcn_sched_barrier(0);
-    store_a(1, ra, oka);
-    if (!(ICLR17_ABL & 4)) __syncthreads();
-    const int sn = s + 2 < nsteps ? s + 2 : nsteps - 1;   // branch-free: clamp the prefetch
-    load_a(sn, ra, oka);
-    load_b(sn, b0);
-    __builtin_amdgcn_sched_barrier(0);
-    compute(1, b1);
-    __builtin_amdgcn_sched_barrier(0);
-    store_a(0, ra, oka);
-    if (!(ICLR17_ABL & 4)) __syncthreads();
+  issue(0, 0);
+  for (int s = 0; s < nsteps; ++s) {
+    __syncthreads();   // vmcnt(0) + barrier: step s landed for every wave; stage (s+1)&1 is free
+    if (s + 1 < nsteps) issue(s + 1, (s + 1) & 1);
+    compute(s & 1);
   }
+  __syncthreads();     // last stage reads done before the epilogue reuses LDS
   if (ICLR17_ABL & 8) {   // diagnostic: keep the accumulators live, skip the epilogue
     float sum = 0.f;
 #pragma unroll
@@ -732,10 +719,6 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
       for (int nt = 0; nt < NT; ++nt) sum += acc[mt][nt][0] + acc[mt][nt][1] + acc[mt][nt][2] + acc[mt][nt][3];
     if (sum == 12345.f) a.out[0] = sum;
     return;
-  }
-  if (s < nsteps) {
-    compute(0, b0);
-    __syncthreads();
   }
 
   if constexpr (EPI == EPI_GDN || EPI == EPI_IGDN) {

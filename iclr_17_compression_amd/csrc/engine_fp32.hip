@@ -89,6 +89,7 @@ struct EngineArgs {
   float* rpart;         // rate bwd: per-tile parameter partials [tiles][11][CO]
   float* colsum_out;    // GDN bwd: per-tile column sums of ∂u (the conv bias gradient) [tiles][CO]
   float* colsum_t;      // GDN bwd: per-tile column sums of dn (∂β_eff) [tiles][CO]
+  int phase_loop;       // 1: a workgroup runs every stride phase of its base block in turn
 };
 
 struct TileInfo {
@@ -102,8 +103,8 @@ __device__ __forceinline__ TileInfo decode_tile(const EngineArgs& a) {
   bid /= a.tiles_x;
   t.ty = bid % a.tiles_y;
   bid /= a.tiles_y;
-  const int ph = bid % a.tt.nph;
-  t.b = bid / a.tt.nph;
+  const int ph = a.phase_loop ? 0 : bid % a.tt.nph;
+  t.b = a.phase_loop ? bid : bid / a.tt.nph;
   t.py = ph / a.tt.npx;
   t.px = ph % a.tt.npx;
   t.nb = blockIdx.y;
@@ -593,7 +594,7 @@ __device__ __forceinline__ void glds16(const float* src, float* lds_wave_base) {
 //     reads (16 rows × one chunk per lane group) bank-conflict free;
 //   B image [8 quads][BN][4] floats: the packed weights of the step, copied linearly.
 // Two LDS stages, one barrier per step: the DMA of step s+1 is in flight while step s computes.
-template <int CI, int CO, int BN, int WM, int WN, int EPI>
+template <int CI, int CO, int BN, int WM, int WN, int EPI, bool PL = false>
 __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
   constexpr int MT = BM / WM / 16;
   constexpr int NT = BN / WN / 16;
@@ -623,10 +624,9 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const TileInfo t = decode_tile(a);
-  const int ph = t.py * a.tt.npx + t.px;
-  const int t0 = a.tt.begin[ph];
-  const int nsteps = (a.tt.begin[ph + 1] - t0) * NCH;
+  TileInfo t = decode_tile(a);
+  const int ph_first = t.py * a.tt.npx + t.px;
+  const int ph_end = PL ? a.tt.nph : ph_first + 1;   // PL: the phase loop (a.phase_loop = 1)
   const int ncol0 = t.nb * BN + wn * (BN / WN);
 
   // A DMA: wave-instruction i covers rows 8i .. 8i+7; lane → (row, physical chunk lane & 7),
@@ -652,6 +652,7 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
     bsrc[j] = (BN == CO) ? i * 256 + lane * 4 : (i * CO + t.nb * BN) * 4 + lane * 4;
   }
 
+  int t0 = 0;
   auto issue = [&](int s, int buf) {
     const int tap = t0 + s / NCH, cc = s - (s / NCH) * NCH;
     const int td = a.tt.dydx[tap];
@@ -674,11 +675,6 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
   };
 
   f4 acc[MT][NT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
-
   // fragment read offsets (floats) within a stage
   int aoff[2][MT];
 #pragma unroll
@@ -704,6 +700,16 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
     }
   };
 
+  for (int ph = ph_first; ph < ph_end; ++ph) {
+  t.py = ph / a.tt.npx;
+  t.px = ph - t.py * a.tt.npx;
+  t0 = a.tt.begin[ph];
+  const int nsteps = (a.tt.begin[ph + 1] - t0) * NCH;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
+
   issue(0, 0);
   for (int s = 0; s < nsteps; ++s) {
     __syncthreads();   // vmcnt(0) + barrier: step s landed for every wave; stage (s+1)&1 is free
@@ -718,7 +724,7 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) sum += acc[mt][nt][0] + acc[mt][nt][1] + acc[mt][nt][2] + acc[mt][nt][3];
     if (sum == 12345.f) a.out[0] = sum;
-    return;
+    continue;
   }
 
   if constexpr (EPI == EPI_GDN || EPI == EPI_IGDN) {
@@ -756,6 +762,8 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
     __syncthreads();
     store_tile_rows<BN>(a, t, smem, OS, a.out, CO, t.nb * BN);
   }
+  if (ph + 1 < ph_end) __syncthreads();   // epilogue LDS reads done before the next phase's DMA
+  }  // phase loop
 }
 
 // ------------------------------------------------------------------------------ conv1 kernel
@@ -1070,8 +1078,19 @@ int launch_deconv5(const float* in, int B, int h, int w, const float* wp, const 
   a.gh = h; a.gw = w; a.tiles_y = (h + 7) / 8; a.tiles_x = (w + 7) / 8;
   a.sin = 1; a.sout = 2;
   fill_deconv_taps(a.tt, 5, 2, 2);
-  dim3 grid(a.tiles_x * a.tiles_y * 4 * B, 1);
-  hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI>), grid, dim3(256), 0, st, a);
+  // Forward: one workgroup per base block running the 4 phases (9/6/6/4 taps) in turn — equal
+  // work per workgroup, shared input neighbourhood — when that still fills 2 workgroups per CU.
+  const int base_tiles = a.tiles_x * a.tiles_y * B;
+  a.phase_loop = (EPI == EPI_IGDN && base_tiles >= 512) ? 1 : 0;
+  if constexpr (EPI == EPI_IGDN) {
+    if (a.phase_loop) {
+      hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI, true>), dim3(base_tiles), dim3(256),
+                         0, st, a);
+      return check_launch("deconv_igdn");
+    }
+  }
+    hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI>), dim3(base_tiles * 4), dim3(256), 0,
+                       st, a);
   return check_launch(EPI == EPI_IGDN ? "deconv_igdn" : "bwd_conv_gdn");
 }
 

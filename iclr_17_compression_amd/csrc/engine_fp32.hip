@@ -228,6 +228,61 @@ __device__ __forceinline__ void chan_gemm(f4 (&acc)[MT][NT], const float* sX,
   }
 }
 
+// Zero source for glds lanes whose tap falls outside the image (padding).
+__device__ __attribute__((aligned(16))) float g_zero16[4] = {0.f, 0.f, 0.f, 0.f};
+
+__device__ __forceinline__ void glds16(const float* src, float* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+// The same contraction with γ streamed through LDS by LDS-DMA: 16-row k-blocks ([4][CO][4],
+// contiguous in the packed layout), two stages at sG, one barrier per k-block. Entry: the
+// caller's sX writes are complete in program order (the first loop barrier publishes them);
+// exit: no barrier after the last k-block (callers add one before reusing sX or sG).
+constexpr int GSTAGE_FLOATS(int CO) { return 2 * 16 * CO; }
+
+template <int CO, int MT, int NT, bool SQ = false>
+__device__ __forceinline__ void chan_gemm_lds(f4 (&acc)[MT][NT], const float* sX,
+                                              const float* __restrict__ bp, float* sG, int wm,
+                                              int ncol0, int lane, int wave) {
+  constexpr int XS = CO + 8;
+  constexpr int GST = 16 * CO;          // floats per stage
+  constexpr int NGI = GST * 4 / 1024;   // glds wave-instructions per stage
+  constexpr int GI_W = (NGI + 3) / 4;
+  constexpr int KB = CO / 16;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
+  auto issue = [&](int kb, int buf) {
+    const float* src = bp + kb * GST + lane * 4;
+#pragma unroll
+    for (int j = 0; j < GI_W; ++j) {
+      const int i = wave + 4 * j;
+      if (NGI % 4 == 0 || i < NGI) glds16(src + i * 256, sG + buf * GST + i * 256);
+    }
+  };
+  const int goff = ((lane >> 4) * CO + ncol0 + (lane & 15)) * 4;
+  const float* xrow = sX + (wm * MT * 16 + (lane & 15)) * XS + 4 * (lane >> 4);
+  issue(0, 0);
+#pragma unroll 2
+  for (int kb = 0; kb < KB; ++kb) {
+    __syncthreads();
+    if (kb + 1 < KB) issue(kb + 1, (kb + 1) & 1);
+    const float* g = sG + (kb & 1) * GST + goff;
+    f4 bf[NT], af[MT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) bf[nt] = *(const f4*)(g + nt * 64);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      af[mt] = *(const f4*)(xrow + mt * 16 * XS + kb * 16);
+      if (SQ) af[mt] = af[mt] * af[mt];
+    }
+    mfma_block<MT, NT>(acc, af, bf);
+  }
+}
+
 // x (bias already added) in accumulator layout → GDN(x) (or IGDN) left in LDS sX[BM][CO+4].
 // models/GDN.py:83-90: n = conv2d(x², γ, β) = β + Σ_j γ[i][j]·x_j²;  y = x / √n | x·√n.
 // The caller guarantees smem is free on entry; on return every wave has passed a barrier after
@@ -249,9 +304,8 @@ __device__ __forceinline__ void gdn_core(const f4 (&x)[MT][NT], float* sX,
         const float v = x[mt][nt][r];
         sX[row * XS + col] = v * v;
       }
-  __syncthreads();
   f4 nacc[MT][NT];
-  chan_gemm<CO, MT, NT>(nacc, sX, gp, wm, ncol0, lane);
+  chan_gemm_lds<CO, MT, NT>(nacc, sX, gp, sX + BM * XS, wm, ncol0, lane, threadIdx.x >> 6);
   __syncthreads();  // all reads of x² done
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
@@ -309,10 +363,11 @@ __device__ __forceinline__ void gdn_bwd_epilogue(f4 (&g)[MT][NT], float* smem, c
                                                  const TileInfo& t, int wm, int ncol0, int lane) {
   constexpr int XS = CO + 8;
   float* sX = smem;
+  float* sG = smem + BM * XS;
+  const int wave = threadIdx.x >> 6;
   load_tile_rows<CO>(a, t, a.saved, sX, XS, CO, 0);   // u, kept in LDS through GEMM 1
-  __syncthreads();
   f4 acc2[MT][NT];
-  chan_gemm<CO, MT, NT, true>(acc2, sX, a.ggamma, wm, ncol0, lane);  // Σ_j γ[i][j] u_j² (fp32 square)
+  chan_gemm_lds<CO, MT, NT, true>(acc2, sX, a.ggamma, sG, wm, ncol0, lane, wave);  // Σ_j γ[i][j] u_j²
   __syncthreads();
   f4 u[MT][NT];
 #pragma unroll
@@ -338,8 +393,7 @@ __device__ __forceinline__ void gdn_bwd_epilogue(f4 (&g)[MT][NT], float* smem, c
         u[mt][nt][r] = uu;
         sX[idx] = dn;
       }
-  __syncthreads();
-  chan_gemm<CO, MT, NT>(acc2, sX, a.ggammaT, wm, ncol0, lane);  // w_j = Σ_i γ[i][j] dn_i
+  chan_gemm_lds<CO, MT, NT>(acc2, sX, a.ggammaT, sG, wm, ncol0, lane, wave);  // w_j = Σ_i γ[i][j] dn_i
   store_tile_rows<CO>(a, t, sX, XS, a.tout, CO, 0);
   if (a.colsum_t != nullptr) tile_colsum<CO>(a, t, sX, XS, a.colsum_t);
   __syncthreads();
@@ -579,14 +633,6 @@ __device__ __forceinline__ void out3_epilogue(f4 (&acc)[MT][NT], float* smem, co
 }
 
 // ------------------------------------------------------------------------- the engine kernel
-// Zero source for glds lanes whose tap falls outside the image (padding).
-__device__ __attribute__((aligned(16))) float g_zero16[4] = {0.f, 0.f, 0.f, 0.f};
-
-__device__ __forceinline__ void glds16(const float* src, float* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
-}
-
 // Main loop: both operands reach LDS by LDS-DMA (global_load_lds_dwordx4), so no staging VGPRs
 // and no ds_write pass. A step is 32 input channels of one tap:
 //   A image [BM][32] floats, 128-byte rows, 16-byte chunk c stored at c ^ (row & 7) — the swizzle
@@ -609,7 +655,7 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
   constexpr int BI_W = (NBI + 3) / 4;
   constexpr int LDS_A = 2 * STAGE;
   constexpr int LDS_X = (EPI == EPI_GDN || EPI == EPI_IGDN || EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD)
-                            ? BM * (CO + 8) : 0;
+                            ? BM * (CO + 8) + GSTAGE_FLOATS(CO) : 0;
   constexpr int LDS_O = BM * (BN + 4) + 8;
   constexpr int LDS_3 = 3 * 32 * 33 + 8;
   constexpr int L1 = LDS_A > LDS_X ? LDS_A : LDS_X;
@@ -783,7 +829,7 @@ __global__ void __launch_bounds__(256) conv1_gdn_kernel(const EngineArgs a) {
   constexpr int MT = BM / 16;
   constexpr int NT = CO / WN / 16;
   constexpr int LDS_P = P1ZERO + 1 + 256 + 64 + 3;  // patch + zero + k table + m table
-  constexpr int LDS_X = BM * (CO + 8);
+  constexpr int LDS_X = BM * (CO + 8) + GSTAGE_FLOATS(CO);
   constexpr int LDS_FLOATS = LDS_P > LDS_X ? LDS_P : LDS_X;
   __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
   int* ktab = (int*)(smem + P1ZERO + 4);
@@ -878,7 +924,7 @@ __global__ void __launch_bounds__(256) gdn_kernel(const float* __restrict__ x, i
                                                   const float* __restrict__ gp, float* y) {
   constexpr int XS = C + 8;   // must match gdn_core's row stride
   constexpr int WN = 4, MT = 4, NT = C / WN / 16;
-  __shared__ __attribute__((aligned(16))) float smem[BM * XS];
+  __shared__ __attribute__((aligned(16))) float smem[BM * XS + GSTAGE_FLOATS(C)];   // + γ stages
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tiles = (HW + BM - 1) / BM;
   const int b = blockIdx.x / tiles, p0 = (blockIdx.x % tiles) * BM;

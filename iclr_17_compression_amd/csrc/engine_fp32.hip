@@ -33,7 +33,8 @@
 
 namespace iclr17 {
 
-// Diagnostic ablation builds only (tools/ablate.sh): -DICLR17_ABL=8 skips the engine epilogue
+// Diagnostic ablation builds only (tools/ablate.sh): -DICLR17_ABL=mask — 8 skips the engine
+// epilogue, 16 replaces conv1's patch gather by constants, 32 skips conv1's epilogue
 #ifndef ICLR17_ABL
 #define ICLR17_ABL 0
 #endif
@@ -817,8 +818,11 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
 // an 8×8 output block is staged once in LDS; K = 243 = (c, kh, kw) padded to 256, each A element
 // gathered from the patch through a k → offset table (k ≥ 243 reads a zero slot).
 constexpr int P1 = 37;                    // patch side: 8·4 + 9 − 4
-constexpr int P1PLANE = P1 * P1;
-constexpr int P1ZERO = 3 * P1PLANE;       // index of the zero slot
+constexpr int P1RS = 40;                  // LDS row stride: 10 16-byte pieces (cols 37..39 unused)
+constexpr int P1PLANE = P1 * P1RS;
+constexpr int P1PIECES = 3 * P1 * 10;     // 16-byte pieces of the patch (1110)
+constexpr int P1NI = (P1PIECES + 63) / 64;  // glds wave-instructions (18)
+constexpr int P1ZERO = P1NI * 256;        // zero slot, after the DMA'd region
 
 // EPI_GDN: analysis conv1 + bias + GDN1 (forward). EPI_IGDN_BWD: the same contraction is the
 // input gradient of the synthesis deconv3 (its adjoint: conv2d(g_recon, W, stride 4, pad 4)),
@@ -828,7 +832,8 @@ __global__ void __launch_bounds__(256) conv1_gdn_kernel(const EngineArgs a) {
   constexpr int WN = 4;
   constexpr int MT = BM / 16;
   constexpr int NT = CO / WN / 16;
-  constexpr int LDS_P = P1ZERO + 1 + 256 + 64 + 3;  // patch + zero + k table + m table
+  constexpr int LDS_PB = P1ZERO + 4 + 256 + 64;   // patch + zero slot + k/m tables
+  constexpr int LDS_P = LDS_PB + 2 * 32 * CO;                        // + two B stages
   constexpr int LDS_X = BM * (CO + 8) + GSTAGE_FLOATS(CO);
   constexpr int LDS_FLOATS = LDS_P > LDS_X ? LDS_P : LDS_X;
   __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
@@ -842,17 +847,36 @@ __global__ void __launch_bounds__(256) conv1_gdn_kernel(const EngineArgs a) {
   const int H = a.Hin, W = a.Win;
   const int iy0 = t.ty * 32 - 4, ix0 = t.tx * 32 - 4;
 
-  // B fragments of step 0 early (global latency overlaps the patch staging)
-  f4 bcur[2][NT], bnxt[2][NT];
-  load_bfrag<NT, CO>(bcur, a.w, 0, ncol0, lane);
+  // B tiles (32 k-rows × CO, contiguous in the packed [64][CO][4] layout) by LDS-DMA into two
+  // stages after the patch; step 0's DMA overlaps the patch staging.
+  constexpr int SB = 32 * CO;
+  constexpr int NBI = SB * 4 / 1024;
+  constexpr int BI_W = (NBI + 3) / 4;
+  float* sB = smem + LDS_PB;
+  auto issue = [&](int s, int buf) {
+    const float* src = a.w + s * SB + lane * 4;
+#pragma unroll
+    for (int j = 0; j < BI_W; ++j) {
+      const int i = wave + 4 * j;
+      if (NBI % 4 == 0 || i < NBI) glds16(src + i * 256, sB + buf * SB + i * 256);
+    }
+  };
+  issue(0, 0);
 
-  for (int idx = tid; idx < 3 * P1PLANE; idx += 256) {
-    const int c = idx / P1PLANE, rem = idx - c * P1PLANE;
-    const int r = rem / P1, col = rem - r * P1;
-    const int iy = iy0 + r, ix = ix0 + col;
-    float v = 0.f;
-    if (iy >= 0 && iy < H && ix >= 0 && ix < W) v = a.in[(((long)t.b * 3 + c) * H + iy) * W + ix];
-    smem[idx] = v;
+  // Patch by LDS-DMA, one 16-byte piece per lane: piece (c, r, q) holds columns 4q .. 4q+3 of
+  // patch row r of channel c. The patch origin ix0 ≡ 0 (mod 4) and W ≡ 0 (mod 16), so a piece is
+  // wholly inside or wholly outside the image; outside pieces copy the zero line.
+#pragma unroll
+  for (int j = 0; j < (P1NI + 3) / 4; ++j) {
+    const int i = wave + 4 * j;
+    if (i < P1NI) {
+      const int pc = i * 64 + lane;
+      const int cr = pc / 10, q = pc - cr * 10;
+      const int c = cr / P1, r = cr - c * P1;
+      const int iy = iy0 + r, ix = ix0 + 4 * q;
+      const bool ok = pc < P1PIECES && iy >= 0 && iy < H && ix >= 0 && ix < W;
+      glds16(ok ? a.in + (((long)t.b * 3 + c) * H + iy) * W + ix : g_zero16, smem + i * 256);
+    }
   }
   if (tid == 0) smem[P1ZERO] = 0.f;
   {
@@ -860,10 +884,10 @@ __global__ void __launch_bounds__(256) conv1_gdn_kernel(const EngineArgs a) {
     int off = P1ZERO;
     if (k < 243) {
       const int c = k / 81, kh = (k % 81) / 9, kw = k % 9;
-      off = c * P1PLANE + kh * P1 + kw;
+      off = c * P1PLANE + kh * P1RS + kw;
     }
     ktab[k] = off;
-    if (tid < 64) mtab[tid] = (tid >> 3) * 4 * P1 + (tid & 7) * 4;
+    if (tid < 64) mtab[tid] = (tid >> 3) * 4 * P1RS + (tid & 7) * 4;
   }
   __syncthreads();
 
@@ -877,10 +901,16 @@ __global__ void __launch_bounds__(256) conv1_gdn_kernel(const EngineArgs a) {
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) moff[mt] = mtab[mt * 16 + (lane & 15)];
 
+  const int boff = ((lane >> 4) * CO + ncol0 + (lane & 15)) * 4;
   for (int s = 0; s < 8; ++s) {
-    if (s + 1 < 8) load_bfrag<NT, CO>(bnxt, a.w, (s + 1) * 8, ncol0, lane);
+    __syncthreads();   // B stage s landed (and, at s = 0, the patch); stage (s+1)&1 is free
+    if (s + 1 < 8) issue(s + 1, (s + 1) & 1);
+    const float* bs = sB + (s & 1) * SB + boff;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
+      f4 bf[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) bf[nt] = *(const f4*)(bs + kk * 16 * CO + nt * 64);
       const int kbase = s * 32 + kk * 16 + 4 * (lane >> 4);
       int ko[4];
 #pragma unroll
@@ -891,16 +921,21 @@ __global__ void __launch_bounds__(256) conv1_gdn_kernel(const EngineArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int o = ko[e] == P1ZERO ? P1ZERO : ko[e] + moff[mt];
-          af[mt][e] = smem[o];
+          af[mt][e] = (ICLR17_ABL & 16) ? (float)(o + e) : smem[o];
         }
-      mfma_block<MT, NT>(acc, af, bcur[kk]);
+      mfma_block<MT, NT>(acc, af, bf);
     }
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) bcur[kk][nt] = bnxt[kk][nt];
   }
   __syncthreads();  // patch reads done before the epilogue reuses LDS
+  if (ICLR17_ABL & 32) {   // diagnostic: skip the epilogue
+    float sum = 0.f;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) sum += acc[mt][nt][0] + acc[mt][nt][1] + acc[mt][nt][2] + acc[mt][nt][3];
+    if (sum == 12345.f) a.out[0] = sum;
+    return;
+  }
   if constexpr (EPI == EPI_GDN) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)

@@ -1,10 +1,10 @@
 #!/bin/bash
 # Diagnostic: build ablation variants of the library (-DICLR17_ABL=mask) and time conv2+GDN
-# and deconv2+IGDN with each (separate processes). Runs on the GPU box.
+# and deconv2+IGDN (+conv1+GDN1) with each (separate processes). Runs on the GPU box.
 set -u
 R=$(pwd)
 mkdir -p gpurun_out/abl
-for m in 0 1 2 3 4 7 8 15; do
+for m in ${MASKS:-0 8 16 32 48}; do
   d=/tmp/abl$m; mkdir -p $d
   for f in engine_fp32 aux wgrad_fp32; do
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -DICLR17_ABL=$m \

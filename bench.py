@@ -13,6 +13,7 @@ data path; "weak" scaling). Prints ONE JSON line on rank 0.
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import platform
@@ -197,6 +198,21 @@ def cpu_baseline(N: int, H: int, W: int, budget_s: float) -> dict:
                       f"({dt:.1f} s, {platform.processor() or platform.machine()})"}
 
 
+def pmc_traffic(layer: str, N: int, S: int, B: int):
+    """HBM bytes per launch of `layer` from the newest committed PMC summary
+    (profiles/*_traffic.json, made by tools/pmc.sh + tools/pmc_summary.py on the B=64 256² N=192
+    eval workload — counters cannot be collected inside this process). None for other shapes."""
+    if (N, S, B) != (192, 256, 64):
+        return None, None
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                                          "*_traffic.json")))
+    for f in reversed(files):
+        d = json.load(open(f))
+        if layer in d.get("layers", {}):
+            return d["layers"][layer]["traffic_bytes"], f"profiles/{os.path.basename(f)} (build {d.get('build')})"
+    return None, None
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -274,6 +290,7 @@ def main() -> None:
                   "gbs": round(bytes_[k] * B / (per_layer_ms[k] * 1e-3) / 1e9, 1) if bytes_[k] else None}
               for k in LAYERS}
     total_flops = sum(flops.values()) * B
+    traffic, traffic_src = pmc_traffic(dominant, N, S, B)
     result = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -293,7 +310,9 @@ def main() -> None:
                    "parallelism": f"dp{world} (images sharded by rank, no data-path collective)"},
         "roofline": {"bound": "mfma", "kernel": dominant, "achieved": round(achieved, 2),
                      "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                     "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                     "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": bytes_[dominant] * B,
                      "flop_per_launch": flops[dominant] * B,
                      "whole_step_tflops": round(total_flops / (ms_per_step * 1e-3) / 1e12, 2)},
         "layers": layers,

@@ -14,6 +14,8 @@
 #include "../../include/iclr17.h"
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef unsigned u4 __attribute__((ext_vector_type(4)));   // 8 packed bf16
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
 
 namespace iclr17 {
 

@@ -91,6 +91,11 @@ struct EngineArgs {
   float* colsum_out;    // GDN bwd: per-tile column sums of ∂u (the conv bias gradient) [tiles][CO]
   float* colsum_t;      // GDN bwd: per-tile column sums of dn (∂β_eff) [tiles][CO]
   int phase_loop;       // 1: a workgroup runs every stride phase of its base block in turn
+  // x6 mode: activations as three bf16 planes (hi, mid, lo; x = hi + mid + lo exactly)
+  const unsigned short* in_split;   // [3][B][Hin][Win][CI]
+  long in_plane;                    // plane stride (elements)
+  unsigned short* out_split;        // [3][B][Hout][Wout][CO] or nullptr
+  long out_plane;
 };
 
 struct TileInfo {
@@ -152,6 +157,46 @@ __device__ __forceinline__ void load_tile_rows(const EngineArgs& a, const TileIn
 
 // Column sums of an LDS tile [BM][ld] over the rows inside the output grid → dst[blockIdx.x][CO],
 // fixed row order (deterministic). Feeds bias / β gradients without another pass over HBM.
+// Exact three-way bf16 split of 8 floats: x = hi + mid + lo, each part a bf16 (truncation
+// split: hi = the top 8 significand bits, mid the next 8, lo the last 8, all exact in fp32).
+// Packed as bf16x8 fragments (u4 = 8 × 16 bits).
+__device__ __forceinline__ void split8(const f4& x0, const f4& x1, u4& hi, u4& mi, u4& lo) {
+  const float x[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+  unsigned h[8], m[8], l[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    h[i] = __float_as_uint(x[i]) & 0xffff0000u;
+    const float r = x[i] - __uint_as_float(h[i]);
+    m[i] = __float_as_uint(r) & 0xffff0000u;
+    l[i] = __float_as_uint(r - __uint_as_float(m[i]));
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    hi[i] = __builtin_amdgcn_perm(h[2 * i + 1], h[2 * i], 0x07060302u);
+    mi[i] = __builtin_amdgcn_perm(m[2 * i + 1], m[2 * i], 0x07060302u);
+    lo[i] = __builtin_amdgcn_perm(l[2 * i + 1], l[2 * i], 0x07060302u);
+  }
+}
+
+// Store a [BM][BN] LDS tile (row stride ld) as the three bf16 planes of the x6 activation
+// format (rows of CO channels, columns col0 ..), 8 channels (16 bytes per plane) per lane.
+template <int BN>
+__device__ __forceinline__ void store_tile_rows_split(const EngineArgs& a, const TileInfo& t,
+                                                      const float* s, int ld, int CO, int col0) {
+  constexpr int C8 = BN / 8;
+  for (int idx = threadIdx.x; idx < BM * C8; idx += 256) {
+    const int m = idx / C8, c8 = idx % C8;
+    const long p = out_pixel(a, t, m);
+    if (p < 0) continue;
+    u4 hi, mi, lo;
+    split8(*(const f4*)(s + m * ld + c8 * 8), *(const f4*)(s + m * ld + c8 * 8 + 4), hi, mi, lo);
+    unsigned short* d = a.out_split + p * CO + col0 + c8 * 8;
+    *(u4*)d = hi;
+    *(u4*)(d + a.out_plane) = mi;
+    *(u4*)(d + 2 * a.out_plane) = lo;
+  }
+}
+
 template <int CO>
 __device__ __forceinline__ void tile_colsum(const EngineArgs& a, const TileInfo& t, const float* s,
                                             int ld, float* dst) {
@@ -343,7 +388,8 @@ __device__ __forceinline__ void gdn_epilogue(f4 (&x)[MT][NT], float* smem, const
                                              const TileInfo& t, int wm, int ncol0, int lane) {
   constexpr int XS = CO + 8;
   gdn_core<CO, MT, NT, INVERSE>(x, smem, a.gbeta, a.ggamma, wm, ncol0, lane);
-  store_tile_rows<CO>(a, t, smem, XS, a.out, CO, 0);
+  if (a.out != nullptr) store_tile_rows<CO>(a, t, smem, XS, a.out, CO, 0);
+  if (a.out_split != nullptr) store_tile_rows_split<CO>(a, t, smem, XS, CO, 0);
   if (a.pre != nullptr) {
     __syncthreads();
     acc_to_lds<MT, NT>(x, smem, XS, wm, ncol0, lane);
@@ -540,6 +586,7 @@ __device__ __forceinline__ void quant_epilogue(f4 (&acc)[MT][NT], float* smem, c
       }
   __syncthreads();
   store_tile_rows<BN>(a, t, sO, OS, a.yhat, CO, cbase);
+  if (a.out_split != nullptr) store_tile_rows_split<BN>(a, t, sO, OS, CO, cbase);   // ŷ, x6 form
   if (a.out != nullptr) {
     __syncthreads();
 #pragma unroll
@@ -641,16 +688,23 @@ __device__ __forceinline__ void out3_epilogue(f4 (&acc)[MT][NT], float* smem, co
 //     reads (16 rows × one chunk per lane group) bank-conflict free;
 //   B image [8 quads][BN][4] floats: the packed weights of the step, copied linearly.
 // Two LDS stages, one barrier per step: the DMA of step s+1 is in flight while step s computes.
-template <int CI, int CO, int BN, int WM, int WN, int EPI, bool PL = false>
-__global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
+//
+// X6 (the bf16x6 mode): the A operand arrives as three bf16 planes (hi, mid, lo — the exact split
+// written by the producing layer's epilogue), A image [3][BM][32] bf16 with 64-byte rows whose
+// 16-byte piece g sits at g ^ ((row >> 1) & 3); B stays fp32 in LDS and each wave splits its own
+// columns in VALU. One 32-deep step = per 16×16 tile six v_mfma_f32_16x16x32_bf16:
+// lo·hi + hi·lo + mid·mid + mid·hi + hi·mid + hi·hi (the dropped mid·lo, lo·mid, lo·lo terms are
+// below 2^-24 of the product), accumulated in fp32.
+template <int CI, int CO, int BN, int WM, int WN, int EPI, bool PL, bool X6>
+__device__ __forceinline__ void engine_body(const EngineArgs& a) {
   constexpr int MT = BM / WM / 16;
   constexpr int NT = BN / WN / 16;
   constexpr int KCH = 32;                        // input channels per k-step
   constexpr int NCH = CI / KCH;
-  constexpr int SA = BM * KCH;                   // A image floats per stage
+  constexpr int SA = X6 ? 3 * BM * KCH / 2 : BM * KCH;   // A image floats per stage
   constexpr int SB = KCH * BN;                   // B image floats per stage
   constexpr int STAGE = SA + SB;
-  constexpr int NAI = SA * 4 / 1024;             // A glds wave-instructions per step (8)
+  constexpr int NAI = SA * 4 / 1024;             // A glds wave-instructions per step (8 | 12)
   constexpr int NBI = SB * 4 / 1024;             // B glds wave-instructions per step
   constexpr int AI_W = NAI / 4;                  // per wave
   constexpr int BI_W = (NBI + 3) / 4;
@@ -676,21 +730,26 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
   const int ph_end = PL ? a.tt.nph : ph_first + 1;   // PL: the phase loop (a.phase_loop = 1)
   const int ncol0 = t.nb * BN + wn * (BN / WN);
 
-  // A DMA: wave-instruction i covers rows 8i .. 8i+7; lane → (row, physical chunk lane & 7),
-  // fetching logical chunk (lane & 7) ^ (row & 7).
+  // A DMA. fp32: wave-instruction i covers rows 8i .. 8i+7; lane → (row, physical chunk
+  // lane & 7), fetching logical chunk (lane & 7) ^ (row & 7). X6: instruction i covers plane
+  // i >> 2, rows 16(i & 3) .. +15; lane → (row, physical piece lane & 3), fetching logical piece
+  // (lane & 3) ^ ((row >> 1) & 3) (8 bf16 channels).
   int iy0[AI_W], ix0[AI_W], pbase[AI_W];
   bool rval[AI_W];
 #pragma unroll
   for (int j = 0; j < AI_W; ++j) {
-    const int row = (wave * AI_W + j) * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ (row & 7);
+    const int i = wave * AI_W + j;
+    const int row = X6 ? 16 * (i & 3) + (lane >> 2) : i * 8 + (lane >> 3);
+    const int c = X6 ? (lane & 3) ^ ((row >> 1) & 3) : (lane & 7) ^ (row & 7);
     const int gy = t.ty * 8 + (row >> 3), gx = t.tx * 8 + (row & 7);
     rval[j] = gy < a.gh && gx < a.gw;
     iy0[j] = gy * a.sin;
     ix0[j] = gx * a.sin;
-    pbase[j] = (iy0[j] * a.Win + ix0[j]) * CI + c * 4;
+    pbase[j] = (iy0[j] * a.Win + ix0[j]) * CI + c * (X6 ? 8 : 4);
   }
-  const float* __restrict__ inb = a.in + (long)t.b * a.Hin * a.Win * CI;
+  const long img = (long)t.b * a.Hin * a.Win * CI;
+  const float* __restrict__ inb = a.in + img;
+  const unsigned short* __restrict__ inb6 = a.in_split + img;
   // B DMA: wave-instruction i copies 1 KB; source offset (floats) within the step's slice
   int bsrc[BI_W];
 #pragma unroll
@@ -718,7 +777,13 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
     for (int j = 0; j < AI_W; ++j) {
       const bool ok = rval[j] && (unsigned)(iy0[j] + dy) < (unsigned)a.Hin &&
                       (unsigned)(ix0[j] + dx) < (unsigned)a.Win;
-      glds16(ok ? inb + pbase[j] + so : g_zero16, sa + (wave * AI_W + j) * 256);
+      const int i = wave * AI_W + j;
+      if constexpr (X6) {
+        const unsigned short* src = inb6 + (i >> 2) * a.in_plane + pbase[j] + so;
+        glds16(ok ? (const float*)src : g_zero16, sa + i * 256);
+      } else {
+        glds16(ok ? inb + pbase[j] + so : g_zero16, sa + i * 256);
+      }
     }
     const float* __restrict__ ws = a.w + ((long)tap * CI + cc * KCH) * CO;   // uniform base
     float* sb = sa + SA;
@@ -741,7 +806,50 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
     }
   const int boff0 = ((lane >> 4) * BN + wn * (BN / WN) + (lane & 15)) * 4;
 
+  // X6 fragment offsets: A piece (bf16 elements) per mt; B quads 2g, 2g+1 (floats)
+  int aoff6[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int row = wm * MT * 16 + mt * 16 + (lane & 15);
+    aoff6[mt] = (row * 4 + ((lane >> 4) ^ ((row >> 1) & 3))) * 8;
+  }
+  const int boff6 = (2 * (lane >> 4) * BN + wn * (BN / WN) + (lane & 15)) * 4;
+
+  auto compute6 = [&](int buf) {
+    const unsigned short* sa = (const unsigned short*)(smem + buf * STAGE);
+    const float* sb = smem + buf * STAGE + SA + boff6;
+    bf8 Bh[NT], Bm[NT], Bl[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      u4 bh, bm, bl;
+      split8(*(const f4*)(sb + nt * 64), *(const f4*)(sb + BN * 4 + nt * 64), bh, bm, bl);
+      Bh[nt] = __builtin_bit_cast(bf8, bh);
+      Bm[nt] = __builtin_bit_cast(bf8, bm);
+      Bl[nt] = __builtin_bit_cast(bf8, bl);
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const bf8 Ah = __builtin_bit_cast(bf8, *(const u4*)(sa + aoff6[mt]));
+      const bf8 Am = __builtin_bit_cast(bf8, *(const u4*)(sa + BM * KCH + aoff6[mt]));
+      const bf8 Al = __builtin_bit_cast(bf8, *(const u4*)(sa + 2 * BM * KCH + aoff6[mt]));
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        f4 c = acc[mt][nt];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al, Bh[nt], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bl[nt], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bm[nt], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bh[nt], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bm[nt], c, 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bh[nt], c, 0, 0, 0);
+      }
+    }
+  };
+
   auto compute = [&](int buf) {
+    if constexpr (X6) {
+      compute6(buf);
+      return;
+    }
     const float* sa = smem + buf * STAGE;
     const float* sb = sa + SA + boff0;
 #pragma unroll
@@ -820,6 +928,18 @@ __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
   }
   if (ph + 1 < ph_end) __syncthreads();   // epilogue LDS reads done before the next phase's DMA
   }  // phase loop
+}
+
+template <int CI, int CO, int BN, int WM, int WN, int EPI, bool PL = false, bool X6 = false>
+__global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
+  engine_body<CI, CO, BN, WM, WN, EPI, PL, X6>(a);
+}
+
+// The same kernel held to 256 VGPRs (2 waves per SIMD) where the compiler would otherwise just
+// exceed it (the phase-loop x6 IGDN instance).
+template <int CI, int CO, int BN, int WM, int WN, int EPI, bool PL = false, bool X6 = false>
+__global__ void __launch_bounds__(256, 2) engine_kernel_occ2(const EngineArgs a) {
+  engine_body<CI, CO, BN, WM, WN, EPI, PL, X6>(a);
 }
 
 // ------------------------------------------------------------------------------ conv1 kernel
@@ -1107,13 +1227,28 @@ void deconv_phase_taps(int K, int s, int p, int ry, int rx, int* kh_out, int* kw
   *count = n;
 }
 
+// x6 activation-format arguments of a launch (all null/0: fp32 in, fp32 out)
+struct SplitIO {
+  const unsigned short* in = nullptr;
+  long in_plane = 0;
+  unsigned short* out = nullptr;
+  long out_plane = 0;
+};
+
+static void apply_split(EngineArgs& a, const SplitIO* x6) {
+  if (x6 == nullptr) return;
+  a.in_split = x6->in; a.in_plane = x6->in_plane;
+  a.out_split = x6->out; a.out_plane = x6->out_plane;
+}
+
 template <int N, int EPI = EPI_GDN>
 int launch_conv1(const float* x, int B, int H, int W, const float* wp, const float* bias,
                  const float* beta, const float* gamma, float* out, float* pre, hipStream_t st,
-                 const EngineArgs* bwd = nullptr) {
+                 const EngineArgs* bwd = nullptr, const SplitIO* x6 = nullptr) {
   EngineArgs a;
   memset(&a, 0, sizeof(a));
   if (bwd) a = *bwd;
+  apply_split(a, x6);
   a.in = x; a.w = wp; a.bias = bias; a.gbeta = beta; a.ggamma = gamma; a.out = out; a.pre = pre;
   a.B = B; a.Hin = H; a.Win = W; a.Hout = H / 4; a.Wout = W / 4;
   a.gh = H / 4; a.gw = W / 4; a.tiles_y = (a.gh + 7) / 8; a.tiles_x = (a.gw + 7) / 8;
@@ -1128,10 +1263,12 @@ template <int N, int EPI>
 int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, const float* bias,
                  const float* beta, const float* gamma, float* out, float* pre, int qmode,
                  const float* noise, const float* rate, float* yhat, double* partial,
-                 hipStream_t st, const EngineArgs* bwd = nullptr) {
+                 hipStream_t st, const EngineArgs* bwd = nullptr, const SplitIO* x6 = nullptr) {
   EngineArgs a;
   memset(&a, 0, sizeof(a));
   if (bwd) a = *bwd;
+  apply_split(a, x6);
+  const bool X6in = a.in_split != nullptr;
   a.in = in; a.w = wp; a.bias = bias; a.gbeta = beta; a.ggamma = gamma; a.out = out; a.pre = pre;
   a.B = B; a.Hin = Hin; a.Win = Win; a.Hout = Hin / 2; a.Wout = Win / 2;
   a.gh = a.Hout; a.gw = a.Wout; a.tiles_y = (a.gh + 7) / 8; a.tiles_x = (a.gw + 7) / 8;
@@ -1142,7 +1279,11 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
     constexpr int BN = 64;
     a.partials_per_image = a.tiles_x * a.tiles_y * (N / BN);
     dim3 grid(a.tiles_x * a.tiles_y * B, N / BN);
-    hipLaunchKernelGGL((engine_kernel<N, N, BN, 1, 4, EPI_QUANT>), grid, dim3(256), 0, st, a);
+    if (X6in)
+      hipLaunchKernelGGL((engine_kernel<N, N, BN, 1, 4, EPI_QUANT, false, true>), grid, dim3(256),
+                         0, st, a);
+    else
+      hipLaunchKernelGGL((engine_kernel<N, N, BN, 1, 4, EPI_QUANT>), grid, dim3(256), 0, st, a);
     return check_launch("conv3_quant_rate");
   } else if constexpr (EPI == EPI_PLAIN || EPI == EPI_RATE_BWD) {
     constexpr int BN = 64;
@@ -1151,6 +1292,13 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
     return check_launch(EPI == EPI_PLAIN ? "conv3" : "bwd_deconv1_rate");
   } else {
     dim3 grid(a.tiles_x * a.tiles_y * B, 1);
+    if constexpr (EPI == EPI_GDN) {
+      if (X6in) {
+        hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI, false, true>), grid, dim3(256), 0,
+                           st, a);
+        return check_launch("conv2_gdn");
+      }
+    }
     hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI>), grid, dim3(256), 0, st, a);
     return check_launch("conv2_gdn");
   }
@@ -1159,10 +1307,11 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
 template <int N, int EPI = EPI_IGDN>
 int launch_deconv5(const float* in, int B, int h, int w, const float* wp, const float* bias,
                    const float* beta, const float* gamma, float* out, float* pre, hipStream_t st,
-                   const EngineArgs* bwd = nullptr) {
+                   const EngineArgs* bwd = nullptr, const SplitIO* x6 = nullptr) {
   EngineArgs a;
   memset(&a, 0, sizeof(a));
   if (bwd) a = *bwd;
+  apply_split(a, x6);
   a.in = in; a.w = wp; a.bias = bias; a.gbeta = beta; a.ggamma = gamma; a.out = out; a.pre = pre;
   a.B = B; a.Hin = h; a.Win = w; a.Hout = 2 * h; a.Wout = 2 * w;
   a.gh = h; a.gw = w; a.tiles_y = (h + 7) / 8; a.tiles_x = (w + 7) / 8;
@@ -1173,11 +1322,17 @@ int launch_deconv5(const float* in, int B, int h, int w, const float* wp, const 
   const int base_tiles = a.tiles_x * a.tiles_y * B;
   a.phase_loop = (EPI == EPI_IGDN && base_tiles >= 512) ? 1 : 0;
   if constexpr (EPI == EPI_IGDN) {
-    if (a.phase_loop) {
+    const bool X6in = a.in_split != nullptr;
+    if (a.phase_loop && X6in)
+      hipLaunchKernelGGL((engine_kernel_occ2<N, N, N, 1, 4, EPI, true, true>), dim3(base_tiles),
+                         dim3(256), 0, st, a);
+    else if (a.phase_loop)
       hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI, true>), dim3(base_tiles), dim3(256),
                          0, st, a);
-      return check_launch("deconv_igdn");
-    }
+    else if (X6in)
+      hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI, false, true>), dim3(base_tiles * 4),
+                         dim3(256), 0, st, a);
+    if (a.phase_loop || X6in) return check_launch("deconv_igdn");
   }
     hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI>), dim3(base_tiles * 4), dim3(256), 0,
                        st, a);
@@ -1201,6 +1356,19 @@ int launch_deconv3(const float* in, int B, int H, int W, const float* wp, const 
   dim3 grid(a.tiles_x * a.tiles_y * B, 1);
   hipLaunchKernelGGL((engine_kernel<N, 48, 48, 4, 1, EPI_OUT3>), grid, dim3(256), 0, st, a);
   return check_launch("deconv3");
+}
+
+// x → three exact bf16 planes (x6 activation format), 8 values per thread
+__global__ void __launch_bounds__(256) split_planes_kernel(const float* __restrict__ x, long n8,
+                                                           unsigned short* __restrict__ planes,
+                                                           long plane) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    u4 hi, mi, lo;
+    split8(*(const f4*)(x + 8 * i), *(const f4*)(x + 8 * i + 4), hi, mi, lo);
+    *(u4*)(planes + 8 * i) = hi;
+    *(u4*)(planes + plane + 8 * i) = mi;
+    *(u4*)(planes + 2 * plane + 8 * i) = lo;
+  }
 }
 
 }  // namespace iclr17
@@ -1302,6 +1470,88 @@ int iclr17_synthesis_deconv3(const float* in, int B, int H, int W, int N, const 
                  "deconv3: the unclipped SSE needs the recon output");
   return N == 192 ? launch_deconv3<192>(in, B, H, W, w_packed, bias, x, clipped, recon, sse_partial, sse_unclipped, S(stream))
                   : launch_deconv3<128>(in, B, H, W, w_packed, bias, x, clipped, recon, sse_partial, sse_unclipped, S(stream));
+}
+
+// ------------------------------------------------------------------ x6 (bf16x6) precision mode
+int iclr17_split_planes(const float* x, long n, uint16_t* planes, void* stream) {
+  ICLR17_REQUIRE(x && planes && n > 0 && n % 8 == 0, ICLR17_EINVAL,
+                 "split_planes: null pointer or n=%ld not a positive multiple of 8", n);
+  const long n8 = n / 8;
+  const int blocks = (int)((n8 + 255) / 256 < 4096 ? (n8 + 255) / 256 : 4096);
+  hipLaunchKernelGGL(split_planes_kernel, dim3(blocks), dim3(256), 0, S(stream), x, n8,
+                     (unsigned short*)planes, n);
+  return check_launch("split_planes");
+}
+
+int iclr17_analysis_conv1_gdn_x6(const float* x, int B, int H, int W, int N,
+                                 const float* w_packed, const float* bias, const float* beta_eff,
+                                 const float* gamma_packed, float* out, uint16_t* out_split,
+                                 float* pre_out, void* stream) {
+  int rc = check_dims(B, H, W, N);
+  if (rc) return rc;
+  ICLR17_REQUIRE(x && w_packed && bias && beta_eff && gamma_packed && (out || out_split),
+                 ICLR17_EINVAL, "conv1_gdn_x6: null pointer");
+  SplitIO io;
+  io.out = (unsigned short*)out_split;
+  io.out_plane = (long)B * (H / 4) * (W / 4) * N;
+  return N == 192 ? launch_conv1<192>(x, B, H, W, w_packed, bias, beta_eff, gamma_packed, out, pre_out, S(stream), nullptr, &io)
+                  : launch_conv1<128>(x, B, H, W, w_packed, bias, beta_eff, gamma_packed, out, pre_out, S(stream), nullptr, &io);
+}
+
+int iclr17_analysis_conv2_gdn_x6(const uint16_t* in_split, int B, int H, int W, int N,
+                                 const float* w_packed, const float* bias, const float* beta_eff,
+                                 const float* gamma_packed, float* out, uint16_t* out_split,
+                                 float* pre_out, void* stream) {
+  int rc = check_dims(B, H, W, N);
+  if (rc) return rc;
+  ICLR17_REQUIRE(in_split && w_packed && bias && beta_eff && gamma_packed && (out || out_split),
+                 ICLR17_EINVAL, "conv2_gdn_x6: null pointer");
+  const int h = H / 4, w = W / 4;
+  SplitIO io;
+  io.in = (const unsigned short*)in_split;
+  io.in_plane = (long)B * h * w * N;
+  io.out = (unsigned short*)out_split;
+  io.out_plane = (long)B * (h / 2) * (w / 2) * N;
+  return N == 192 ? launch_conv5<192, EPI_GDN>(nullptr, B, h, w, w_packed, bias, beta_eff, gamma_packed, out, pre_out, 0, nullptr, nullptr, nullptr, nullptr, S(stream), nullptr, &io)
+                  : launch_conv5<128, EPI_GDN>(nullptr, B, h, w, w_packed, bias, beta_eff, gamma_packed, out, pre_out, 0, nullptr, nullptr, nullptr, nullptr, S(stream), nullptr, &io);
+}
+
+int iclr17_analysis_conv3_quant_rate_x6(const uint16_t* in_split, int B, int H, int W, int N,
+                                        const float* w_packed, int quant_mode, const float* noise,
+                                        const float* rate_packed, float* y_out, float* y_hat,
+                                        uint16_t* y_hat_split, double* bits_partial,
+                                        void* stream) {
+  int rc = check_dims(B, H, W, N);
+  if (rc) return rc;
+  ICLR17_REQUIRE(in_split && w_packed && rate_packed && y_hat && bits_partial, ICLR17_EINVAL,
+                 "conv3_quant_rate_x6: null pointer");
+  ICLR17_REQUIRE(quant_mode == ICLR17_QUANT_ROUND || (quant_mode == ICLR17_QUANT_NOISE && noise),
+                 ICLR17_EINVAL, "conv3_quant_rate_x6: bad quant mode %d / missing noise", quant_mode);
+  const int h = H / 8, w = W / 8;
+  SplitIO io;
+  io.in = (const unsigned short*)in_split;
+  io.in_plane = (long)B * h * w * N;
+  io.out = (unsigned short*)y_hat_split;
+  io.out_plane = (long)B * (h / 2) * (w / 2) * N;
+  return N == 192 ? launch_conv5<192, EPI_QUANT>(nullptr, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io)
+                  : launch_conv5<128, EPI_QUANT>(nullptr, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io);
+}
+
+int iclr17_synthesis_deconv_igdn_x6(const uint16_t* in_split, int B, int h, int w, int N,
+                                    const float* w_packed, const float* bias,
+                                    const float* beta_eff, const float* gamma_packed, float* out,
+                                    uint16_t* out_split, float* pre_out, void* stream) {
+  ICLR17_REQUIRE(B > 0 && h > 0 && w > 0, ICLR17_EINVAL, "deconv_igdn_x6: bad shape");
+  ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "channel count N=%d unsupported", N);
+  ICLR17_REQUIRE(in_split && w_packed && bias && beta_eff && gamma_packed && (out || out_split),
+                 ICLR17_EINVAL, "deconv_igdn_x6: null pointer");
+  SplitIO io;
+  io.in = (const unsigned short*)in_split;
+  io.in_plane = (long)B * h * w * N;
+  io.out = (unsigned short*)out_split;
+  io.out_plane = (long)B * (2 * h) * (2 * w) * N;
+  return N == 192 ? launch_deconv5<192>(nullptr, B, h, w, w_packed, bias, beta_eff, gamma_packed, out, pre_out, S(stream), nullptr, &io)
+                  : launch_deconv5<128>(nullptr, B, h, w, w_packed, bias, beta_eff, gamma_packed, out, pre_out, S(stream), nullptr, &io);
 }
 
 static EngineArgs bwd_args(const float* saved, const float* gammaT, float* tout) {

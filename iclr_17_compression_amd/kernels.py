@@ -190,6 +190,111 @@ def deconv_igdn(h: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Tenso
     return (out, pre) if want_pre else out
 
 
+# ------------------------------------------------------------- x6 (bf16x6) precision mode
+# A split-form activation is an int16 tensor [3, B, h, w, N]: the bf16 bit patterns of the exact
+# parts hi, mid, lo (x = hi + mid + lo) of an NHWC fp32 activation.
+def _check_split(s: Tensor, what: str):
+    if not isinstance(s, Tensor) or s.dtype != torch.int16 or s.dim() != 5 or s.shape[0] != 3:
+        raise Iclr17Error(f"iclr17: {what} must be a split-form int16 tensor [3,B,h,w,N]")
+    if not s.is_cuda:
+        raise Iclr17Error(f"iclr17: {what} must be a device tensor (there is no CPU path)")
+    if not s.is_contiguous():
+        raise Iclr17Error(f"iclr17: {what} must be contiguous")
+
+
+def split_planes(x: Tensor) -> Tensor:
+    """fp32 tensor → split form [3, *x.shape] (exact: hi + mid + lo == x)."""
+    _check(x, "tensor", x.dim())
+    x = x.contiguous()
+    out = torch.empty((3,) + tuple(x.shape), device=x.device, dtype=torch.int16)
+    call("iclr17_split_planes", _p(x), x.numel(), _p(out), _stream(x))
+    return out
+
+
+def merge_planes(s: Tensor) -> Tensor:
+    """Split form → fp32 (hi + mid + lo, exact). Test/debug helper (torch ops)."""
+    u = s.to(torch.int32) & 0xFFFF
+    parts = (u << 16).view(torch.float32)
+    return parts[0] + parts[1] + parts[2]
+
+
+def conv1_gdn_x6(x: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Tensor, N: int,
+                 want_f32: bool = False, want_pre: bool = False):
+    """conv1_gdn with the output in split form (+ fp32 / pre-GDN on request)."""
+    _check(x, "image", 4)
+    B, C, H, W = x.shape
+    if C != 3:
+        raise Iclr17Error(f"iclr17: the analysis transform takes 3-channel images (got {C})")
+    _check_image_dims(H, W)
+    _check_channels(N)
+    x = x.contiguous()
+    split = torch.empty(3, B, H // 4, W // 4, N, device=x.device, dtype=torch.int16)
+    out = torch.empty(B, H // 4, W // 4, N, device=x.device) if want_f32 else None
+    pre = torch.empty(B, H // 4, W // 4, N, device=x.device) if want_pre else None
+    call("iclr17_analysis_conv1_gdn_x6", _p(x), B, H, W, N, _p(wp), _p(bias), _p(beta_eff),
+         _p(gp), _p(out), _p(split), _p(pre), _stream(x))
+    return split, out, pre
+
+
+def conv2_gdn_x6(hs: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Tensor,
+                 want_f32: bool = False, want_pre: bool = False):
+    """conv2_gdn on a split-form input; returns (split, fp32 | None, pre | None)."""
+    _check_split(hs, "activation")
+    _, B, h4, w4, N = hs.shape
+    _check_channels(N)
+    H, W = 4 * h4, 4 * w4
+    _check_image_dims(H, W)
+    split = torch.empty(3, B, h4 // 2, w4 // 2, N, device=hs.device, dtype=torch.int16)
+    out = torch.empty(B, h4 // 2, w4 // 2, N, device=hs.device) if want_f32 else None
+    pre = torch.empty(B, h4 // 2, w4 // 2, N, device=hs.device) if want_pre else None
+    call("iclr17_analysis_conv2_gdn_x6", _p(hs), B, H, W, N, _p(wp), _p(bias), _p(beta_eff),
+         _p(gp), _p(out), _p(split), _p(pre), _stream(hs))
+    return split, out, pre
+
+
+def conv3_quant_rate_x6(hs: Tensor, wp: Tensor, rate_packed: Tensor,
+                        noise: Optional[Tensor] = None, want_y: bool = False):
+    """conv3_quant_rate on a split-form input. Returns (y_hat, bits_partial, y | None,
+    y_hat_split)."""
+    _check_split(hs, "activation")
+    _, B, h8, w8, N = hs.shape
+    _check_channels(N)
+    H, W = 8 * h8, 8 * w8
+    _check_image_dims(H, W)
+    mode = _lib.ICLR17_QUANT_ROUND
+    if noise is not None:
+        _check(noise, "noise", 4)
+        if tuple(noise.shape) != (B, N, h8 // 2, w8 // 2):
+            raise Iclr17Error(f"iclr17: noise must be {(B, N, h8 // 2, w8 // 2)} (got {tuple(noise.shape)})")
+        noise = noise.contiguous()
+        mode = _lib.ICLR17_QUANT_NOISE
+    y_hat = torch.empty(B, h8 // 2, w8 // 2, N, device=hs.device, dtype=torch.float32)
+    y_hat_split = torch.empty(3, B, h8 // 2, w8 // 2, N, device=hs.device, dtype=torch.int16)
+    y = torch.empty_like(y_hat) if want_y else None
+    T = rate_partials_per_image(H, W, N)
+    partial = torch.empty(B, T, device=hs.device, dtype=torch.float64)
+    call("iclr17_analysis_conv3_quant_rate_x6", _p(hs), B, H, W, N, _p(wp), mode, _p(noise),
+         _p(rate_packed), _p(y), _p(y_hat), _p(y_hat_split), _p(partial), _stream(hs))
+    return y_hat, partial, y, y_hat_split
+
+
+def deconv_igdn_x6(hs: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Tensor,
+                   want_split: bool = True, want_f32: bool = False, want_pre: bool = False):
+    """deconv_igdn on a split-form input; returns (split | None, fp32 | None, pre | None)."""
+    _check_split(hs, "activation")
+    _, B, hh, ww, N = hs.shape
+    _check_channels(N)
+    if not (want_split or want_f32):
+        raise Iclr17Error("iclr17: deconv_igdn_x6 needs an output")
+    split = (torch.empty(3, B, 2 * hh, 2 * ww, N, device=hs.device, dtype=torch.int16)
+             if want_split else None)
+    out = torch.empty(B, 2 * hh, 2 * ww, N, device=hs.device) if want_f32 else None
+    pre = torch.empty(B, 2 * hh, 2 * ww, N, device=hs.device) if want_pre else None
+    call("iclr17_synthesis_deconv_igdn_x6", _p(hs), B, hh, ww, N, _p(wp), _p(bias), _p(beta_eff),
+         _p(gp), _p(out), _p(split), _p(pre), _stream(hs))
+    return split, out, pre
+
+
 def output_partials_per_image(H: int, W: int) -> int:
     return query("iclr17_output_partials_per_image", H, W)
 

@@ -117,6 +117,39 @@ int iclr17_synthesis_deconv3(const float* in, int B, int H, int W, int N, const 
                              double* sse_partial, int sse_unclipped, void* stream);
 int iclr17_output_partials_per_image(int H, int W);
 
+/* ------------------------------------------------------------------ x6 precision mode
+ * The same layers with the conv contractions on v_mfma_f32_16x16x32_bf16 in the bf16x6 scheme:
+ * every fp32 operand is split exactly into three bf16 parts (x = hi + mid + lo; truncation
+ * split) and each product is formed from the six significant part products (hi·hi, hi·mid,
+ * mid·hi, hi·lo, mid·mid, lo·hi — the dropped terms are below 2^-24 of the product), with
+ * fp32 accumulation. Activations travel between layers in "split form": three bf16 planes
+ * [3][B][h][w][N] (uint16 bf16 bits, plane stride B·h·w·N), written by the producing layer's
+ * epilogue. conv1 (3-channel NCHW image) and deconv3 keep exact-f32 products. out / out_split
+ * are each nullable, not both. */
+/* x[n] (n % 8 == 0) → planes[3][n]. */
+int iclr17_split_planes(const float* x, long n, uint16_t* planes, void* stream);
+/* iclr17_analysis_conv1_gdn with the output also (or only) in split form. */
+int iclr17_analysis_conv1_gdn_x6(const float* x, int B, int H, int W, int N,
+                                 const float* w_packed, const float* bias, const float* beta_eff,
+                                 const float* gamma_packed, float* out, uint16_t* out_split,
+                                 float* pre_out, void* stream);
+/* iclr17_analysis_conv2_gdn on a split-form input. */
+int iclr17_analysis_conv2_gdn_x6(const uint16_t* in_split, int B, int H, int W, int N,
+                                 const float* w_packed, const float* bias, const float* beta_eff,
+                                 const float* gamma_packed, float* out, uint16_t* out_split,
+                                 float* pre_out, void* stream);
+/* iclr17_analysis_conv3_quant_rate on a split-form input; ŷ also in split form (nullable). */
+int iclr17_analysis_conv3_quant_rate_x6(const uint16_t* in_split, int B, int H, int W, int N,
+                                        const float* w_packed, int quant_mode, const float* noise,
+                                        const float* rate_packed, float* y_out, float* y_hat,
+                                        uint16_t* y_hat_split, double* bits_partial,
+                                        void* stream);
+/* iclr17_synthesis_deconv_igdn on a split-form input. */
+int iclr17_synthesis_deconv_igdn_x6(const uint16_t* in_split, int B, int h, int w, int N,
+                                    const float* w_packed, const float* bias,
+                                    const float* beta_eff, const float* gamma_packed, float* out,
+                                    uint16_t* out_split, float* pre_out, void* stream);
+
 /* Deterministic fixed-order sums: per_image[b] = Σ_t partial[b*T + t] (nullable);
  * *total = (float)(scale · Σ_b per_image[b]) (nullable). model.py:73,78 bits→bpp. */
 int iclr17_reduce_partials(const double* partial, int B, int T, double* per_image, float* total,

@@ -32,6 +32,9 @@ from iclr_17_compression_amd.model import ImageCompressor  # noqa: E402
 
 METRIC = "Mpixels/s encode+decode at 1/2/4/8 GPU; bpp & PSNR parity on Kodak"
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 dense peak
+BF16_MFMA_PEAK_TFLOPS = 2516.6  # 256 CU x 4 SIMD x 1024 FLOP/clk (16x16x32 bf16, 16 cyc) x 2.4 GHz
+X6_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6   # fp32-equivalent: 6 bf16 part products per MAC
+X6_LAYERS = ("conv2_gdn2", "conv3_quant_rate", "deconv1_igdn1", "deconv2_igdn2")
 HBM_PEAK_GBS = 8000.0
 
 LAYERS = ("conv1_gdn1", "conv2_gdn2", "conv3_quant_rate", "deconv1_igdn1", "deconv2_igdn2",
@@ -88,16 +91,29 @@ class Step:
         d1, d2, d3, q1, q2 = self.dec
         ev = (lambda i: events[i].record()) if events is not None else (lambda i: None)
         ev(0)
-        h = kernels.conv1_gdn(self.x, w1, net.Encoder.conv1.bias, g1[0], g1[1], N)
-        ev(1)
-        h = kernels.conv2_gdn(h, w2, net.Encoder.conv2.bias, g2[0], g2[1])
-        ev(2)
-        y_hat, partial = kernels.conv3_quant_rate(h, w3, self.rate)
-        ev(3)
-        h = kernels.deconv_igdn(y_hat, d1, net.Decoder.deconv1.bias, q1[0], q1[1])
-        ev(4)
-        h = kernels.deconv_igdn(h, d2, net.Decoder.deconv2.bias, q2[0], q2[1])
-        ev(5)
+        if kernels.precision() == "x6":
+            hs, _, _ = kernels.conv1_gdn_x6(self.x, w1, net.Encoder.conv1.bias, g1[0], g1[1], N)
+            ev(1)
+            hs, _, _ = kernels.conv2_gdn_x6(hs, w2, net.Encoder.conv2.bias, g2[0], g2[1])
+            ev(2)
+            y_hat, partial, _, ys = kernels.conv3_quant_rate_x6(hs, w3, self.rate)
+            ev(3)
+            hs, _, _ = kernels.deconv_igdn_x6(ys, d1, net.Decoder.deconv1.bias, q1[0], q1[1])
+            ev(4)
+            _, h, _ = kernels.deconv_igdn_x6(hs, d2, net.Decoder.deconv2.bias, q2[0], q2[1],
+                                             want_split=False, want_f32=True)
+            ev(5)
+        else:
+            h = kernels.conv1_gdn(self.x, w1, net.Encoder.conv1.bias, g1[0], g1[1], N)
+            ev(1)
+            h = kernels.conv2_gdn(h, w2, net.Encoder.conv2.bias, g2[0], g2[1])
+            ev(2)
+            y_hat, partial = kernels.conv3_quant_rate(h, w3, self.rate)
+            ev(3)
+            h = kernels.deconv_igdn(y_hat, d1, net.Decoder.deconv1.bias, q1[0], q1[1])
+            ev(4)
+            h = kernels.deconv_igdn(h, d2, net.Decoder.deconv2.bias, q2[0], q2[1])
+            ev(5)
         clipped, _, _ = kernels.deconv3(h, d3, net.Decoder.deconv3.bias)
         ev(6)
         _, bpp = kernels.reduce_partials(partial, self.scale, per_image=False)
@@ -198,7 +214,7 @@ def cpu_baseline(N: int, H: int, W: int, budget_s: float) -> dict:
                       f"({dt:.1f} s, {platform.processor() or platform.machine()})"}
 
 
-def pmc_traffic(layer: str, N: int, S: int, B: int):
+def pmc_traffic(layer: str, N: int, S: int, B: int, prec: str):
     """HBM bytes per launch of `layer` from the newest committed PMC summary
     (profiles/*_traffic.json, made by tools/pmc.sh + tools/pmc_summary.py on the B=64 256² N=192
     eval workload — counters cannot be collected inside this process). None for other shapes."""
@@ -208,7 +224,7 @@ def pmc_traffic(layer: str, N: int, S: int, B: int):
                                           "*_traffic.json")))
     for f in reversed(files):
         d = json.load(open(f))
-        if layer in d.get("layers", {}):
+        if d.get("precision", "fp32") == prec and layer in d.get("layers", {}):
             return d["layers"][layer]["traffic_bytes"], f"profiles/{os.path.basename(f)} (build {d.get('build')})"
     return None, None
 
@@ -224,7 +240,11 @@ def main() -> None:
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=("eval", "train"), default="eval")
+    ap.add_argument("--precision", choices=kernels.PRECISIONS, default=None,
+                    help="inference contraction mode (default: ICLR17_PRECISION or x6)")
     args = ap.parse_args()
+    if args.precision:
+        kernels.set_precision(args.precision)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -290,7 +310,11 @@ def main() -> None:
                   "gbs": round(bytes_[k] * B / (per_layer_ms[k] * 1e-3) / 1e9, 1) if bytes_[k] else None}
               for k in LAYERS}
     total_flops = sum(flops.values()) * B
-    traffic, traffic_src = pmc_traffic(dominant, N, S, B)
+    x6 = kernels.precision() == "x6"
+    traffic, traffic_src = pmc_traffic(dominant, N, S, B, kernels.precision())
+    peak = X6_PEAK_TFLOPS if (x6 and dominant in X6_LAYERS) else FP32_MFMA_PEAK_TFLOPS
+    peak_note = ("bf16 dense MFMA peak / 6 (bf16x6: six bf16 part products per fp32 MAC)"
+                 if peak == X6_PEAK_TFLOPS else "fp32 MFMA dense peak (exact-f32 products)")
     result = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -306,11 +330,14 @@ def main() -> None:
         "data": "synthetic (splitmix64 uint8/255 images, seeded trained-like weights)",
         "config": {"workload": f"eval encode+decode (round quantiser + rate), {B} x {S}x{S}x3 images per GPU, N={N}",
                    "N": N, "image": f"{S}x{S}x3", "batch_per_gpu": B, "global_batch": B * world,
-                   "quant": "round", "precision": "fp32 (exact-f32 MFMA)",
+                   "quant": "round",
+                   "precision": ("x6: fp32 operands split exactly into 3 bf16 parts, 6 part products "
+                                 "on v_mfma_f32_16x16x32_bf16, fp32 accumulate (conv1/deconv3/GDN "
+                                 "contractions exact-f32)") if x6 else "fp32 (exact-f32 MFMA products)",
                    "parallelism": f"dp{world} (images sharded by rank, no data-path collective)"},
         "roofline": {"bound": "mfma", "kernel": dominant, "achieved": round(achieved, 2),
-                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                     "peak": round(peak, 1), "unit": "TFLOP/s", "peak_basis": peak_note,
+                     "frac": round(achieved / peak, 4), "traffic": traffic,
                      "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": bytes_[dominant] * B,
                      "flop_per_launch": flops[dominant] * B,

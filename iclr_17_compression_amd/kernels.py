@@ -11,6 +11,7 @@ are packed into kernel layouts by the ``pack_*`` helpers (derived caches).
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional, Sequence, Tuple
 
 import numpy as np
@@ -191,6 +192,25 @@ def deconv_igdn(h: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Tenso
 
 
 # ------------------------------------------------------------- x6 (bf16x6) precision mode
+PRECISIONS = ("x6", "fp32")
+_precision = os.environ.get("ICLR17_PRECISION", "x6")
+
+
+def precision() -> str:
+    """Inference contraction mode: "x6" (bf16x6 split products on the bf16 MFMA, fp32-accurate;
+    default) or "fp32" (exact-f32 MFMA products). Training kernels are fp32 in both."""
+    if _precision not in PRECISIONS:
+        raise Iclr17Error(f"iclr17: ICLR17_PRECISION must be one of {PRECISIONS} (got {_precision!r})")
+    return _precision
+
+
+def set_precision(mode: str) -> None:
+    global _precision
+    if mode not in PRECISIONS:
+        raise Iclr17Error(f"iclr17: precision must be one of {PRECISIONS} (got {mode!r})")
+    _precision = mode
+
+
 # A split-form activation is an int16 tensor [3, B, h, w, N]: the bf16 bit patterns of the exact
 # parts hi, mid, lo (x = hi + mid + lo) of an NHWC fp32 activation.
 def _check_split(s: Tensor, what: str):

@@ -72,12 +72,19 @@ class ImageCompressor(nn.Module):
         x = x.contiguous()
         w1, w2, w3, g1, g2 = self.Encoder.packed()
         N = self.out_channel_N
-        h = kernels.conv1_gdn(x, w1, self.Encoder.conv1.bias, g1[0], g1[1], N)
-        h = kernels.conv2_gdn(h, w2, self.Encoder.conv2.bias, g2[0], g2[1])
-        q = kernels.conv3_quant_rate(h, w3, self.bitEstimator.packed(), noise, want_y=want_y)
+        if kernels.precision() == "x6":
+            hs, _, _ = kernels.conv1_gdn_x6(x, w1, self.Encoder.conv1.bias, g1[0], g1[1], N)
+            hs, _, _ = kernels.conv2_gdn_x6(hs, w2, self.Encoder.conv2.bias, g2[0], g2[1])
+            q = kernels.conv3_quant_rate_x6(hs, w3, self.bitEstimator.packed(), noise, want_y=want_y)
+            y_split = q[3]
+        else:
+            h = kernels.conv1_gdn(x, w1, self.Encoder.conv1.bias, g1[0], g1[1], N)
+            h = kernels.conv2_gdn(h, w2, self.Encoder.conv2.bias, g2[0], g2[1])
+            q = kernels.conv3_quant_rate(h, w3, self.bitEstimator.packed(), noise, want_y=want_y)
+            y_split = None
         y_hat, bits_partial = q[0], q[1]
         clipped, recon, sse_partial = self.Decoder.decode(y_hat, x_ref=x if x_ref_sse else None,
-                                                          want_recon=want_recon)
+                                                          want_recon=want_recon, y_split=y_split)
         return {"clipped": clipped, "y_hat": y_hat, "bits_partial": bits_partial,
                 "sse_partial": sse_partial, "recon": recon, "y": q[2] if want_y else None}
 

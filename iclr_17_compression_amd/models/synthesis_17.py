@@ -53,11 +53,17 @@ class Synthesis_net_17(nn.Module):
         the latent is already channels-last, e.g. the Encoder's own output)."""
         return y.permute(0, 2, 3, 1).contiguous()
 
-    def decode(self, y_nhwc, x_ref=None, want_recon=True):
-        """NHWC latent → (clipped NCHW, unclipped NCHW | None, SSE partials | None)."""
+    def decode(self, y_nhwc, x_ref=None, want_recon=True, y_split=None):
+        """NHWC latent → (clipped NCHW, unclipped NCHW | None, SSE partials | None).
+        With ``y_split`` (the latent in x6 split form) deconv1/deconv2 run in the x6 mode."""
         d1, d2, d3, g1, g2 = self.packed()
-        h = kernels.deconv_igdn(y_nhwc, d1, self.deconv1.bias, g1[0], g1[1])
-        h = kernels.deconv_igdn(h, d2, self.deconv2.bias, g2[0], g2[1])
+        if y_split is not None:
+            hs, _, _ = kernels.deconv_igdn_x6(y_split, d1, self.deconv1.bias, g1[0], g1[1])
+            _, h, _ = kernels.deconv_igdn_x6(hs, d2, self.deconv2.bias, g2[0], g2[1],
+                                             want_split=False, want_f32=True)
+        else:
+            h = kernels.deconv_igdn(y_nhwc, d1, self.deconv1.bias, g1[0], g1[1])
+            h = kernels.deconv_igdn(h, d2, self.deconv2.bias, g2[0], g2[1])
         return kernels.deconv3(h, d3, self.deconv3.bias, x_ref=x_ref, want_recon=want_recon)
 
     def forward(self, x):
@@ -68,5 +74,7 @@ class Synthesis_net_17(nn.Module):
         params = list(self.parameters())
         if needs_grad(x, params):
             return SynthesisFn.apply(x, self, *params)
-        _, recon, _ = self.decode(self.to_nhwc(x), want_recon=True)
+        y = self.to_nhwc(x)
+        split = kernels.split_planes(y) if kernels.precision() == "x6" else None
+        _, recon, _ = self.decode(y, want_recon=True, y_split=split)
         return recon

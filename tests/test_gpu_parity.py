@@ -48,6 +48,75 @@ def nhwc(t):
     return t.permute(0, 2, 3, 1)
 
 
+@pytest.fixture(params=["x6", "fp32"])
+def precision(request):
+    """Run a test in each inference contraction mode (kernels.set_precision)."""
+    old = kernels.precision()
+    kernels.set_precision(request.param)
+    yield request.param
+    kernels.set_precision(old)
+
+
+def test_split_planes_exact(device):
+    """The x6 split is exact: hi + mid + lo == x bit for bit, each part a bf16."""
+    x = torch.from_numpy(synth.normal_like(3, (4096,), 2.0)) * torch.from_numpy(
+        np.exp(synth.uniform(4, (4096,), -30, 30)).astype(np.float32))
+    x[:8] = torch.tensor([0.0, -0.0, 1.0, -1.0, 3.0e38, -1e-30, 0.1, 1 / 3])
+    s = kernels.split_planes(x.to(device))
+    assert s.shape == (3, 4096) and s.dtype == torch.int16
+    assert torch.equal(kernels.merge_planes(s).cpu(), x)
+    # each part is a bf16 (its fp32 image has zero low 16 bits) and |mid| ≤ 2^-8 |hi|
+    parts = ((s.to(torch.int32) & 0xFFFF) << 16).view(torch.float32).cpu()
+    hi, mid = parts[0].double(), parts[1].double()
+    assert bool(((mid.abs() <= hi.abs() * 2.0 ** -7) | (hi == 0)).all())
+
+
+@pytest.mark.parametrize("N", [192, 128])
+def test_x6_layers(device, N):
+    """x6-mode layers (split-form in/out) against the oracle, each from the oracle's input."""
+    net, sd = net_for(N, 1, device), sd_for(N, 1)
+    F = torch.nn.functional
+    x = image(11, 2, 64, 96)
+    w1, w2, w3, g1, g2 = net.Encoder.packed()
+    rate = net.bitEstimator.packed()
+    with torch.no_grad():
+        a1s, a1, u1 = kernels.conv1_gdn_x6(x.to(device), w1, net.Encoder.conv1.bias, g1[0], g1[1], N,
+                                           want_f32=True, want_pre=True)
+        r_u1 = F.conv2d(x, sd["Encoder.conv1.weight"], sd["Encoder.conv1.bias"], stride=4, padding=4)
+        r_a1 = oracle.gdn(r_u1, sd["Encoder.gdn1.beta"], sd["Encoder.gdn1.gamma"], False)
+        assert rel_err(a1, nhwc(r_a1)) < REL and rel_err(u1, nhwc(r_u1)) < REL
+        assert torch.equal(kernels.merge_planes(a1s), a1)
+        a2s, a2, u2 = kernels.conv2_gdn_x6(kernels.split_planes(nhwc(r_a1).contiguous().to(device)), w2,
+                                           net.Encoder.conv2.bias, g2[0], g2[1], want_f32=True, want_pre=True)
+        r_u2 = F.conv2d(r_a1, sd["Encoder.conv2.weight"], sd["Encoder.conv2.bias"], stride=2, padding=2)
+        r_a2 = oracle.gdn(r_u2, sd["Encoder.gdn2.beta"], sd["Encoder.gdn2.gamma"], False)
+        assert rel_err(u2, nhwc(r_u2)) < REL and rel_err(a2, nhwc(r_a2)) < REL
+        assert torch.equal(kernels.merge_planes(a2s), a2)
+        y_hat, _, y, y_hat_s = kernels.conv3_quant_rate_x6(kernels.split_planes(nhwc(r_a2).contiguous().to(device)),
+                                                           w3, rate, want_y=True)
+        r_y = F.conv2d(r_a2, sd["Encoder.conv3.weight"], None, stride=2, padding=2)
+        assert rel_err(y, nhwc(r_y)) < REL
+        assert torch.equal(kernels.merge_planes(y_hat_s), y_hat)
+        check_latents(y_hat.permute(0, 3, 1, 2), y.permute(0, 3, 1, 2), torch.round(r_y), r_y)
+        # synthesis
+        yq = torch.round(torch.from_numpy(synth.uniform(5, (2, N, 4, 6), -4, 4)))
+        d1, d2, _, q1, q2 = net.Decoder.packed()
+        s1s, s1, v1 = kernels.deconv_igdn_x6(kernels.split_planes(nhwc(yq).contiguous().to(device)), d1,
+                                             net.Decoder.deconv1.bias, q1[0], q1[1],
+                                             want_f32=True, want_pre=True)
+        r_v1 = F.conv_transpose2d(yq, sd["Decoder.deconv1.weight"], sd["Decoder.deconv1.bias"], stride=2, padding=2,
+                                  output_padding=1)
+        r_s1 = oracle.gdn(r_v1, sd["Decoder.igdn1.beta"], sd["Decoder.igdn1.gamma"], True)
+        assert rel_err(v1, nhwc(r_v1)) < REL and rel_err(s1, nhwc(r_s1)) < REL
+        assert torch.equal(kernels.merge_planes(s1s), s1)
+        _, s2, _ = kernels.deconv_igdn_x6(kernels.split_planes(nhwc(r_s1).contiguous().to(device)), d2,
+                                          net.Decoder.deconv2.bias, q2[0], q2[1], want_split=False, want_f32=True)
+        r_s2 = oracle.gdn(F.conv_transpose2d(r_s1, sd["Decoder.deconv2.weight"], sd["Decoder.deconv2.bias"],
+                                             stride=2, padding=2, output_padding=1),
+                          sd["Decoder.igdn2.beta"], sd["Decoder.igdn2.gamma"], True)
+        assert rel_err(s2, nhwc(r_s2)) < REL
+
+
 # ------------------------------------------------------------------------------------ layers
 @pytest.mark.parametrize("N", [192, 128])
 def test_analysis_layers(device, N):
@@ -158,7 +227,7 @@ def check_latents(y_hat, y, r_yhat, r_y, max_rate=1e-4):
     return n
 
 
-def test_c1_golden_end_to_end(device, golden_dir):
+def test_c1_golden_end_to_end(device, precision, golden_dir):
     g = np.load(os.path.join(golden_dir, "g3_c1_n192_256px.npz"), allow_pickle=False)
     meta = json.load(open(os.path.join(golden_dir, "g3_c1_n192_256px.json")))
     net = net_for(192, 1, device)
@@ -184,7 +253,7 @@ def test_c1_golden_end_to_end(device, golden_dir):
 
 
 @pytest.mark.parametrize("N,B,H,W", [(192, 3, 48, 80), (128, 2, 16, 16), (192, 1, 16, 48), (128, 2, 96, 64)])
-def test_module_shapes_vs_oracle(device, N, B, H, W):
+def test_module_shapes_vs_oracle(device, precision, N, B, H, W):
     net, sd = net_for(N, 4, device), sd_for(N, 4)
     x = image(7, B, H, W)
     with torch.no_grad():
@@ -196,7 +265,7 @@ def test_module_shapes_vs_oracle(device, N, B, H, W):
     assert rel_err(clipped, r_clipped) < REL
 
 
-def test_training_mode_noise(device):
+def test_training_mode_noise(device, precision):
     N = 192
     net, sd = net_for(N, 1, device), sd_for(N, 1)
     x = image(3, 2, 64, 64)
@@ -210,7 +279,7 @@ def test_training_mode_noise(device):
     assert rel_err(clipped, r_clipped) < REL
 
 
-def test_kodak_synth_subset(device, golden_dir):
+def test_kodak_synth_subset(device, precision, golden_dir):
     meta = json.load(open(os.path.join(golden_dir, "g5_kodak24_synth_n192.json")))
     net, sd = net_for(meta["N"], meta["weight_seed"], device), sd_for(meta["N"], meta["weight_seed"])
     for row in [meta["images"][i] for i in (0, 3, 9, 23)]:
@@ -221,10 +290,10 @@ def test_kodak_synth_subset(device, golden_dir):
         assert ev["psnr"][0].item() == pytest.approx(row["psnr"], rel=METRIC_REL)
         _, r_yhat, _, _, r_y = oracle.codec_forward(x, sd)
         n = check_latents(ev["y_hat"], ev["y"], r_yhat, r_y)
-        print(f"kodak-synth[{row['index']}]: {n} near-tie latent flips of {r_yhat.numel()}")
+        print(f"kodak-synth[{row['index']}] {precision}: {n} near-tie latent flips of {r_yhat.numel()}")
 
 
-def test_determinism_and_batch_independence(device):
+def test_determinism_and_batch_independence(device, precision):
     net = net_for(192, 1, device)
     x = image(21, 4, 64, 64).to(device)
     ev1 = net.evaluate(x)

@@ -4,7 +4,7 @@ FETCH_SIZE / WRITE_SIZE are rocprofv3's KB counters, averaged over the dispatche
 gfx950 counts half the bytes of wide (16 B/lane) streaming reads in FETCH_SIZE (MI355X_MICROARCH.md
 §HBM), so read bytes = 2 × FETCH_SIZE × 1024; write bytes = WRITE_SIZE × 1024.
 
-    python tools/pmc_summary.py gpurun_out/pmc r02_fwd_fp32_b64
+    python tools/pmc_summary.py gpurun_out/pmc r02_fwd_x6_b64 [x6|fp32]
 """
 import csv
 import glob
@@ -16,12 +16,22 @@ import sys
 
 # bench.py layer name → kernel (B=64 eval at 256², N=192: each name is unique in that run)
 LAYER_KERNELS = {
-    "conv1_gdn1": r"conv1_gdn_kernel<192, 0>",
-    "conv2_gdn2": r"engine_kernel<192, 192, 192, 1, 4, 0, false>",
-    "conv3_quant_rate": r"engine_kernel<192, 192, 64, 1, 4, 2, false>",
-    "deconv1_igdn1": r"engine_kernel<192, 192, 192, 1, 4, 1, false>",
-    "deconv2_igdn2": r"engine_kernel<192, 192, 192, 1, 4, 1, true>",
-    "deconv3_clamp": r"engine_kernel<192, 48, 48, 4, 1, 3, false>",
+    "fp32": {
+        "conv1_gdn1": r"conv1_gdn_kernel<192, 0>",
+        "conv2_gdn2": r"engine_kernel<192, 192, 192, 1, 4, 0, false, false>",
+        "conv3_quant_rate": r"engine_kernel<192, 192, 64, 1, 4, 2, false, false>",
+        "deconv1_igdn1": r"engine_kernel<192, 192, 192, 1, 4, 1, false, false>",
+        "deconv2_igdn2": r"engine_kernel<192, 192, 192, 1, 4, 1, true, false>",
+        "deconv3_clamp": r"engine_kernel<192, 48, 48, 4, 1, 3, false, false>",
+    },
+    "x6": {
+        "conv1_gdn1": r"conv1_gdn_kernel<192, 0>",
+        "conv2_gdn2": r"engine_kernel<192, 192, 192, 1, 4, 0, false, true>",
+        "conv3_quant_rate": r"engine_kernel<192, 192, 64, 1, 4, 2, false, true>",
+        "deconv1_igdn1": r"engine_kernel<192, 192, 192, 1, 4, 1, false, true>",
+        "deconv2_igdn2": r"engine_kernel_occ2<192, 192, 192, 1, 4, 1, true, true>",
+        "deconv3_clamp": r"engine_kernel<192, 48, 48, 4, 1, 3, false, false>",
+    },
 }
 
 
@@ -33,6 +43,7 @@ def norm(name: str) -> str:
 
 def main() -> None:
     src, tag = sys.argv[1], sys.argv[2]
+    prec = sys.argv[3] if len(sys.argv) > 3 else "x6"
     per = {}   # kernel → counter → [values]
     for f in sorted(glob.glob(os.path.join(src, "p*", "pmc_counter_collection.csv"))):
         for row in csv.DictReader(open(f)):
@@ -40,7 +51,7 @@ def main() -> None:
             per.setdefault(k, {}).setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
     kernels = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in per.items()}
     layers = {}
-    for layer, pat in LAYER_KERNELS.items():
+    for layer, pat in LAYER_KERNELS[prec].items():
         hits = [k for k in kernels if pat in k]
         if len(hits) != 1:
             continue
@@ -57,7 +68,7 @@ def main() -> None:
         rev = "unknown"
     out = {"note": "rocprofv3 --pmc, separate passes (tools/pmc.sh) of bench.py; mean per dispatch. "
                    "read_bytes = 2 x FETCH_SIZE (gfx950 half-count of wide reads), write_bytes = WRITE_SIZE.",
-           "build": rev, "layers": layers, "kernels": kernels}
+           "build": rev, "precision": prec, "layers": layers, "kernels": kernels}
     path = os.path.join("profiles", f"{tag}_traffic.json")
     json.dump(out, open(path, "w"), indent=1, sort_keys=True)
     print(path, {k: round(v["traffic_bytes"] / 2**20, 1) for k, v in layers.items()}, "MiB/launch")

@@ -33,8 +33,8 @@
 
 namespace iclr17 {
 
-// Diagnostic ablation builds only (tools/ablate.sh): -DICLR17_ABL=mask — 8 skips the engine
-// epilogue, 16 replaces conv1's patch gather by constants, 32 skips conv1's epilogue
+// Diagnostic ablation builds only (tools/ablate.sh, tools/ab.sh): -DICLR17_ABL=mask — 8 skips
+// the engine epilogue, 16 replaces conv1's patch gather by constants, 32 skips conv1's epilogue
 #ifndef ICLR17_ABL
 #define ICLR17_ABL 0
 #endif
@@ -100,10 +100,13 @@ struct EngineArgs {
 
 struct TileInfo {
   int b, ty, tx, py, px, nb;
+  int th;   // tile height in base-grid rows (tile = th × 8 base pixels)
 };
 
+template <int TH = 8>
 __device__ __forceinline__ TileInfo decode_tile(const EngineArgs& a) {
   TileInfo t;
+  t.th = TH;
   int bid = blockIdx.x;
   t.tx = bid % a.tiles_x;
   bid /= a.tiles_x;
@@ -119,20 +122,20 @@ __device__ __forceinline__ TileInfo decode_tile(const EngineArgs& a) {
 
 // Row m of a tile → output pixel (NHWC row offset in pixels) or -1 when outside the grid.
 __device__ __forceinline__ long out_pixel(const EngineArgs& a, const TileInfo& t, int m) {
-  const int gy = t.ty * 8 + (m >> 3), gx = t.tx * 8 + (m & 7);
+  const int gy = t.ty * t.th + (m >> 3), gx = t.tx * 8 + (m & 7);
   if (gy >= a.gh || gx >= a.gw) return -1;
   const int oy = gy * a.sout + t.py, ox = gx * a.sout + t.px;
   return ((long)t.b * a.Hout + oy) * a.Wout + ox;
 }
 
-// Store a [BM][BN] tile held in LDS (row stride ld) to NHWC rows of CO floats at column
-// offset col0, 16 bytes per lane, rows outside the grid skipped.
-template <int BN>
+// Store an [R][BN] tile held in LDS (row stride ld) to NHWC rows of CO floats at column
+// offset col0, 16 bytes per lane, rows outside the grid skipped (T threads).
+template <int BN, int R = BM, int T = 256>
 __device__ __forceinline__ void store_tile_rows(const EngineArgs& a, const TileInfo& t,
                                                 const float* s, int ld, float* dst, int CO,
                                                 int col0) {
   constexpr int C4 = BN / 4;
-  for (int idx = threadIdx.x; idx < BM * C4; idx += 256) {
+  for (int idx = threadIdx.x; idx < R * C4; idx += T) {
     const int m = idx / C4, c4 = idx % C4;
     const long p = out_pixel(a, t, m);
     if (p < 0) continue;
@@ -155,8 +158,6 @@ __device__ __forceinline__ void load_tile_rows(const EngineArgs& a, const TileIn
   }
 }
 
-// Column sums of an LDS tile [BM][ld] over the rows inside the output grid → dst[blockIdx.x][CO],
-// fixed row order (deterministic). Feeds bias / β gradients without another pass over HBM.
 // Exact three-way bf16 split of 8 floats: x = hi + mid + lo, each part a bf16 (truncation
 // split: hi = the top 8 significand bits, mid the next 8, lo the last 8, all exact in fp32).
 // Packed as bf16x8 fragments (u4 = 8 × 16 bits).
@@ -180,11 +181,11 @@ __device__ __forceinline__ void split8(const f4& x0, const f4& x1, u4& hi, u4& m
 
 // Store a [BM][BN] LDS tile (row stride ld) as the three bf16 planes of the x6 activation
 // format (rows of CO channels, columns col0 ..), 8 channels (16 bytes per plane) per lane.
-template <int BN>
+template <int BN, int R = BM, int T = 256>
 __device__ __forceinline__ void store_tile_rows_split(const EngineArgs& a, const TileInfo& t,
                                                       const float* s, int ld, int CO, int col0) {
   constexpr int C8 = BN / 8;
-  for (int idx = threadIdx.x; idx < BM * C8; idx += 256) {
+  for (int idx = threadIdx.x; idx < R * C8; idx += T) {
     const int m = idx / C8, c8 = idx % C8;
     const long p = out_pixel(a, t, m);
     if (p < 0) continue;
@@ -197,6 +198,8 @@ __device__ __forceinline__ void store_tile_rows_split(const EngineArgs& a, const
   }
 }
 
+// Column sums of an LDS tile [BM][ld] over the rows inside the output grid → dst[blockIdx.x][CO],
+// fixed row order (deterministic). Feeds bias / β gradients without another pass over HBM.
 template <int CO>
 __device__ __forceinline__ void tile_colsum(const EngineArgs& a, const TileInfo& t, const float* s,
                                             int ld, float* dst) {
@@ -288,14 +291,14 @@ __device__ __forceinline__ void glds16(const float* src, float* lds_wave_base) {
 // exit: no barrier after the last k-block (callers add one before reusing sX or sG).
 constexpr int GSTAGE_FLOATS(int CO) { return 2 * 16 * CO; }
 
-template <int CO, int MT, int NT, bool SQ = false>
+template <int CO, int MT, int NT, bool SQ = false, int NW = 4>
 __device__ __forceinline__ void chan_gemm_lds(f4 (&acc)[MT][NT], const float* sX,
                                               const float* __restrict__ bp, float* sG, int wm,
                                               int ncol0, int lane, int wave) {
   constexpr int XS = CO + 8;
   constexpr int GST = 16 * CO;          // floats per stage
   constexpr int NGI = GST * 4 / 1024;   // glds wave-instructions per stage
-  constexpr int GI_W = (NGI + 3) / 4;
+  constexpr int GI_W = (NGI + NW - 1) / NW;
   constexpr int KB = CO / 16;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
@@ -305,8 +308,8 @@ __device__ __forceinline__ void chan_gemm_lds(f4 (&acc)[MT][NT], const float* sX
     const float* src = bp + kb * GST + lane * 4;
 #pragma unroll
     for (int j = 0; j < GI_W; ++j) {
-      const int i = wave + 4 * j;
-      if (NGI % 4 == 0 || i < NGI) glds16(src + i * 256, sG + buf * GST + i * 256);
+      const int i = wave + NW * j;
+      if (NGI % NW == 0 || i < NGI) glds16(src + i * 256, sG + buf * GST + i * 256);
     }
   };
   const int goff = ((lane >> 4) * CO + ncol0 + (lane & 15)) * 4;
@@ -333,7 +336,7 @@ __device__ __forceinline__ void chan_gemm_lds(f4 (&acc)[MT][NT], const float* sX
 // models/GDN.py:83-90: n = conv2d(x², γ, β) = β + Σ_j γ[i][j]·x_j²;  y = x / √n | x·√n.
 // The caller guarantees smem is free on entry; on return every wave has passed a barrier after
 // the last sX write.
-template <int CO, int MT, int NT, bool INVERSE>
+template <int CO, int MT, int NT, bool INVERSE, int R = BM, int T = 256>
 __device__ __forceinline__ void gdn_core(const f4 (&x)[MT][NT], float* sX,
                                          const float* __restrict__ gbeta,
                                          const float* __restrict__ gp, int wm, int ncol0,
@@ -351,7 +354,8 @@ __device__ __forceinline__ void gdn_core(const f4 (&x)[MT][NT], float* sX,
         sX[row * XS + col] = v * v;
       }
   f4 nacc[MT][NT];
-  chan_gemm_lds<CO, MT, NT>(nacc, sX, gp, sX + BM * XS, wm, ncol0, lane, threadIdx.x >> 6);
+  chan_gemm_lds<CO, MT, NT, false, T / 64>(nacc, sX, gp, sX + R * XS, wm, ncol0, lane,
+                                           __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
   __syncthreads();  // all reads of x² done
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
@@ -383,18 +387,18 @@ __device__ __forceinline__ void acc_to_lds(const f4 (&v)[MT][NT], float* s, int 
       }
 }
 
-template <int CO, int MT, int NT, bool INVERSE>
+template <int CO, int MT, int NT, bool INVERSE, int R = BM, int T = 256>
 __device__ __forceinline__ void gdn_epilogue(f4 (&x)[MT][NT], float* smem, const EngineArgs& a,
                                              const TileInfo& t, int wm, int ncol0, int lane) {
   constexpr int XS = CO + 8;
-  gdn_core<CO, MT, NT, INVERSE>(x, smem, a.gbeta, a.ggamma, wm, ncol0, lane);
-  if (a.out != nullptr) store_tile_rows<CO>(a, t, smem, XS, a.out, CO, 0);
-  if (a.out_split != nullptr) store_tile_rows_split<CO>(a, t, smem, XS, CO, 0);
+  gdn_core<CO, MT, NT, INVERSE, R, T>(x, smem, a.gbeta, a.ggamma, wm, ncol0, lane);
+  if (a.out != nullptr) store_tile_rows<CO, R, T>(a, t, smem, XS, a.out, CO, 0);
+  if (a.out_split != nullptr) store_tile_rows_split<CO, R, T>(a, t, smem, XS, CO, 0);
   if (a.pre != nullptr) {
     __syncthreads();
     acc_to_lds<MT, NT>(x, smem, XS, wm, ncol0, lane);
     __syncthreads();
-    store_tile_rows<CO>(a, t, smem, XS, a.pre, CO, 0);
+    store_tile_rows<CO, R, T>(a, t, smem, XS, a.pre, CO, 0);
   }
 }
 
@@ -723,7 +727,8 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   static_assert((SB * 4) % 1024 == 0, "B image in whole wave-instructions");
   __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (scalar branches)
   const int wm = wave / WN, wn = wave % WN;
   TileInfo t = decode_tile(a);
   const int ph_first = t.py * a.tt.npx + t.px;

@@ -4,7 +4,7 @@
 set -u
 mkdir -p gpurun_out/ab
 for v in $VARIANTS; do
-  n=${v%%:*}; f=${v#*:}; d=/tmp/ab_$n; mkdir -p $d
+  n=${v%%:*}; f=${v#*:}; f=${f//,/ }; d=/tmp/ab_$n; mkdir -p $d
   for s in engine_fp32 aux wgrad_fp32; do
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off $f \
       -c iclr_17_compression_amd/csrc/$s.hip -o $d/$s.o || exit 1
@@ -14,7 +14,7 @@ done
 for r in $(seq ${ROUNDS:-2}); do
   for v in $VARIANTS; do
     n=${v%%:*}
-    ICLR17_LIB=/tmp/ab_$n/libiclr17.so timeout -k 10 120 python tools/time_layers.py --tag $n 2>/dev/null \
+    TAG=$n X6_TIME_ONLY=1 ICLR17_LIB=/tmp/ab_$n/libiclr17.so timeout -k 10 120 python ${TOOL:-tools/time_layers.py} --tag $n 2>/dev/null \
       | tee -a gpurun_out/ab/results.txt || exit 1
   done
 done

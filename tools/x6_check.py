@@ -60,20 +60,28 @@ def timeit(fn, n=10):
     return sorted(ts)[n // 2]
 
 
-with torch.no_grad():
+TIME_ONLY = os.environ.get("X6_TIME_ONLY") == "1"
+TAG = os.environ.get("TAG", "")
+
+
+def numerics():
     nb = 4   # numerics on a slice (fp64 reference cost)
     r2 = ref_conv2(a1[:nb])
     f32 = kernels.conv2_gdn(a1[:nb].contiguous(), w2, net.Encoder.conv2.bias, g2[0], g2[1])
-    x6s, x6f, _ = kernels.conv2_gdn_x6(kernels.split_planes(a1[:nb].contiguous()), w2, net.Encoder.conv2.bias,
-                                       g2[0], g2[1], want_f32=True)
+    x6s, x6f, _ = kernels.conv2_gdn_x6(kernels.split_planes(a1[:nb].contiguous()), w2,
+                                       net.Encoder.conv2.bias, g2[0], g2[1], want_f32=True)
     print("conv2_gdn  fp32:", err(f32, r2))
     print("conv2_gdn  x6  :", err(x6f, r2), " split==f32:", torch.equal(kernels.merge_planes(x6s), x6f))
     rd = ref_deconv2(s1[:nb])
     f32 = kernels.deconv_igdn(s1[:nb].contiguous(), d2, net.Decoder.deconv2.bias, q2[0], q2[1])
-    _, x6f, _ = kernels.deconv_igdn_x6(kernels.split_planes(s1[:nb].contiguous()), d2, net.Decoder.deconv2.bias,
-                                       q2[0], q2[1], want_split=False, want_f32=True)
+    _, x6f, _ = kernels.deconv_igdn_x6(kernels.split_planes(s1[:nb].contiguous()), d2,
+                                       net.Decoder.deconv2.bias, q2[0], q2[1], want_split=False,
+                                       want_f32=True)
     print("deconv2_igdn fp32:", err(f32, rd))
     print("deconv2_igdn x6  :", err(x6f, rd))
+
+
+def timings():
     fl2 = 2.0 * B * (32 * 32 * N * N * 25 + 32 * 32 * N * N)
     fld = 2.0 * B * (32 * 32 * N * N * 25 + 64 * 64 * N * N)
     t = {
@@ -83,4 +91,10 @@ with torch.no_grad():
         "deconv2 x6": (timeit(lambda: kernels.deconv_igdn_x6(s1s, d2, net.Decoder.deconv2.bias, q2[0], q2[1],
                                                              want_split=False, want_f32=True)), fld),
     }
-    print(" ".join(f"{k}={v[0]:.3f}ms({v[1] / v[0] / 1e9:.1f}TF)" for k, v in t.items()), flush=True)
+    print(TAG, " ".join(f"{k}={v[0]:.3f}ms({v[1] / v[0] / 1e9:.1f}TF)" for k, v in t.items()), flush=True)
+
+
+with torch.no_grad():
+    if not TIME_ONLY:
+        numerics()
+    timings()

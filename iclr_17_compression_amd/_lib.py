@@ -58,6 +58,8 @@ SIGNATURES = {
                                                  _P, _P]),
     "iclr17_synthesis_deconv_igdn_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_reduce_partials": (_I, [_P, _I, _I, _P, _P, _D, _P]),
+    "iclr17_ms_ssim_workspace_size": (_SZ, [_I, _I, _I]),
+    "iclr17_ms_ssim": (_I, [_P, _P, _I, _I, _I, _F, _P, _SZ, _P, _P]),
     "iclr17_gdn": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "iclr17_bit_estimator": (_I, [_P, _I64, _I, _I64, _P, _P, _P]),
     "iclr17_bitparm": (_I, [_P, _I64, _I, _I64, _P, _P, _P, _P, _P]),

@@ -315,6 +315,25 @@ def deconv_igdn_x6(hs: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: T
     return split, out, pre
 
 
+def ms_ssim(x: Tensor, y: Tensor, data_range: float = 1.0) -> Tensor:
+    """Per-image MS-SSIM [B] of NCHW fp32 image batches (models/ms_ssim_torch.py:123-196 as
+    train.py:178 calls it), on the GPU."""
+    _check(x, "image", 4)
+    _check(y, "image", 4)
+    if x.shape != y.shape or x.shape[1] != 3:
+        raise Iclr17Error(f"iclr17: ms_ssim needs two [B,3,H,W] batches of one shape "
+                          f"(got {tuple(x.shape)} and {tuple(y.shape)})")
+    B, _, H, W = x.shape
+    nbytes = query("iclr17_ms_ssim_workspace_size", B, H, W)
+    if nbytes == 0:
+        raise Iclr17Error(f"iclr17: ms_ssim: {H}x{W} is too small for 5 levels of an 11-tap window")
+    ws = torch.empty(nbytes, device=x.device, dtype=torch.uint8)
+    out = torch.empty(B, device=x.device, dtype=torch.float32)
+    call("iclr17_ms_ssim", _p(x.contiguous()), _p(y.contiguous()), B, H, W, float(data_range),
+         _p(ws), nbytes, _p(out), _stream(x))
+    return out
+
+
 def output_partials_per_image(H: int, W: int) -> int:
     return query("iclr17_output_partials_per_image", H, W)
 

@@ -119,9 +119,11 @@ class ImageCompressor(nn.Module):
         return clipped, mse, bpp
 
     @torch.no_grad()
-    def evaluate(self, x: torch.Tensor, want_y: bool = False) -> Dict[str, torch.Tensor]:
+    def evaluate(self, x: torch.Tensor, want_y: bool = False,
+                 want_msssim: bool = False) -> Dict[str, torch.Tensor]:
         """testKodak-style per-image metrics (train.py:157-190): bpp, MSE of the clipped
-        reconstruction and PSNR per image, all from deterministic on-device reductions."""
+        reconstruction and PSNR per image, all from deterministic on-device reductions; with
+        ``want_msssim`` also MS-SSIM (train.py:178, on the GPU) and MS-SSIM-DB (train.py:179)."""
         B, _, H, W = x.shape
         out = self.run(x, training=False, x_ref_sse=True, want_y=want_y)
         bits, _ = kernels.reduce_partials(out["bits_partial"])
@@ -133,4 +135,8 @@ class ImageCompressor(nn.Module):
                "bpp": bpp, "mse": mse, "psnr": psnr}
         if want_y:
             res["y"] = out["y"].permute(0, 3, 1, 2)
+        if want_msssim:
+            ms = kernels.ms_ssim(out["clipped"], x, data_range=1.0)
+            res["ms_ssim"] = ms
+            res["ms_ssim_db"] = -10 * (torch.log(1 - ms) / math.log(10))
         return res

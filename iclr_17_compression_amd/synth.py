@@ -153,3 +153,12 @@ STATE_DICT_KEYS = (
     "bitEstimator.f3.h", "bitEstimator.f3.b", "bitEstimator.f3.a",
     "bitEstimator.f4.h", "bitEstimator.f4.b",
 )
+
+
+def noisy_pair_u8(B: int, H: int, W: int, seed_img: int, seed_noise: int, div: int):
+    """(x, y) uint8 image pair [B,3,H,W]: x a smooth synthetic image, y = clip(x + noise // div)
+    with centred uint8 noise — integer arithmetic only (the MS-SSIM fixture G6)."""
+    x8 = np.stack([smooth_image_u8(seed_img + b, H, W) for b in range(B)])
+    n8 = image_u8(seed_noise, B, H, W).astype(np.int32) - 128
+    y8 = np.clip(x8.astype(np.int32) + n8 // div, 0, 255).astype(np.uint8)
+    return x8, y8

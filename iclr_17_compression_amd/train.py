@@ -142,18 +142,21 @@ def kodak_images(test_dir):
 
 @torch.no_grad()
 def test_kodak(net, test_dir, device, step=0):
-    """testKodak, train.py:157-198: per-image bpp / PSNR (clipped recon), dataset averages."""
+    """testKodak, train.py:157-198: per-image bpp / PSNR / MS-SSIM / MS-SSIM-DB of the clipped
+    reconstruction (MS-SSIM on the GPU instead of the reference's per-image CPU call at :178),
+    the same log lines, dataset averages."""
     net.eval()
     rows = []
     for name, img in kodak_images(test_dir):
-        ev = net.evaluate(img[None].to(device))
-        bpp, psnr = ev["bpp"][0].item(), ev["psnr"][0].item()
-        rows.append((bpp, psnr))
-        logger.info("Bpp:{:.6f}, PSNR:{:.6f}".format(bpp, psnr))
+        ev = net.evaluate(img[None].to(device), want_msssim=True)
+        r = tuple(ev[k][0].item() for k in ("bpp", "psnr", "ms_ssim", "ms_ssim_db"))
+        rows.append(r)
+        logger.info("Bpp:{:.6f}, PSNR:{:.6f}, MS-SSIM:{:.6f}, MS-SSIM-DB:{:.6f}".format(*r))
     if rows:
         logger.info("Test on Kodak dataset: model-{}".format(step))
-        logger.info("Dataset Average result---Bpp:{:.6f}, PSNR:{:.6f}".format(
-            float(np.mean([r[0] for r in rows])), float(np.mean([r[1] for r in rows]))))
+        avg = [float(np.mean([r[i] for r in rows])) for i in range(4)]
+        logger.info("Dataset Average result---Bpp:{:.6f}, PSNR:{:.6f}, MS-SSIM:{:.6f}, "
+                    "MS-SSIM-DB:{:.6f}".format(*avg))
     return rows
 
 

@@ -150,6 +150,14 @@ int iclr17_synthesis_deconv_igdn_x6(const uint16_t* in_split, int B, int h, int 
                                     const float* beta_eff, const float* gamma_packed, float* out,
                                     uint16_t* out_split, float* pre_out, void* stream);
 
+/* testKodak's MS-SSIM (train.py:178 → models/ms_ssim_torch.py:123-196): per-image
+ * ms_ssim(x, y, data_range) of NCHW [B,3,H,W] fp32 images, 11-tap σ=1.5 window, 5 levels (each
+ * level must be ≥ 11×11: H, W ≥ 161 or so), the reference's level weights and final product.
+ * workspace: iclr17_ms_ssim_workspace_size(B,H,W) bytes (0 = shape unsupported). out: [B]. */
+size_t iclr17_ms_ssim_workspace_size(int B, int H, int W);
+int iclr17_ms_ssim(const float* x, const float* y, int B, int H, int W, float data_range,
+                   void* workspace, size_t workspace_bytes, float* out, void* stream);
+
 /* Deterministic fixed-order sums: per_image[b] = Σ_t partial[b*T + t] (nullable);
  * *total = (float)(scale · Σ_b per_image[b]) (nullable). model.py:73,78 bits→bpp. */
 int iclr17_reduce_partials(const double* partial, int B, int T, double* per_image, float* total,

@@ -161,5 +161,61 @@ def psnr(clipped: Tensor, x: Tensor) -> Tensor:
     return 10 * (torch.log(1.0 / mse) / math.log(10))
 
 
+# ------------------------------------------------------------------------------ MS-SSIM
+# models/ms_ssim_torch.py as train.py:178 calls it: ms_ssim(clipped, x, data_range=1.0,
+# size_average=True) with the default 11-tap, σ = 1.5 window and the 5 default level weights.
+MSSSIM_WEIGHTS = (0.0448, 0.2856, 0.3001, 0.2363, 0.1333)   # ms_ssim_torch.py:153-154
+
+
+def gauss_window(size: int = 11, sigma: float = 1.5) -> Tensor:
+    """ms_ssim_torch.py:5-18: normalised 1-D Gaussian, fp32, centred at size // 2."""
+    t = torch.arange(size).to(dtype=torch.float) - size // 2
+    g = torch.exp(-(t ** 2) / (2 * sigma ** 2))
+    return g / g.sum()
+
+
+def _blur(z: Tensor, g: Tensor) -> Tensor:
+    """ms_ssim_torch.py:21-34: depthwise 'valid' filtering, first along W, then along H."""
+    C = z.shape[1]
+    kw = g.reshape(1, 1, 1, -1).repeat(C, 1, 1, 1)
+    z = F.conv2d(z, kw, groups=C)
+    return F.conv2d(z, kw.transpose(2, 3), groups=C)
+
+
+def ssim_and_cs(X: Tensor, Y: Tensor, g: Tensor, data_range: float) -> Tuple[Tensor, Tensor]:
+    """ms_ssim_torch.py:37-80 (size_average=False, full=True): per-image means over C,H,W of
+    the SSIM map and the contrast-structure map."""
+    c1, c2 = (0.01 * data_range) ** 2, (0.03 * data_range) ** 2
+    mx, my = _blur(X, g), _blur(Y, g)
+    mxx, myy, mxy = mx.pow(2), my.pow(2), mx * my
+    vx = 1.0 * (_blur(X * X, g) - mxx)
+    vy = 1.0 * (_blur(Y * Y, g) - myy)
+    cxy = 1.0 * (_blur(X * Y, g) - mxy)
+    cs_map = (2 * cxy + c2) / (vx + vy + c2)
+    ssim_map = ((2 * mxy + c1) / (mxx + myy + c1)) * cs_map
+    per_image = lambda m: m.mean(-1).mean(-1).mean(-1)  # noqa: E731
+    return per_image(ssim_map), per_image(cs_map)
+
+
+def ms_ssim(X: Tensor, Y: Tensor, data_range: float = 1.0) -> Tensor:
+    """ms_ssim_torch.py:123-196 → per-image MS-SSIM [B]. Five levels, 2×2 average pooling with
+    one padding row/column on odd sizes (counted in the average, avg_pool2d's default). Like the
+    reference, the final product multiplies the LAST level's SSIM term into every one of the
+    first four levels (ms_ssim_torch.py:189-190), so it enters as ssim_5^(4·w_5), and the last
+    level's cs is not used."""
+    w = torch.tensor(MSSSIM_WEIGHTS, dtype=X.dtype)
+    g = gauss_window()
+    mcs = []
+    s = None
+    for _ in range(len(MSSSIM_WEIGHTS)):
+        s, cs = ssim_and_cs(X, Y, g, data_range)
+        mcs.append(cs)
+        pad = (X.shape[2] % 2, X.shape[3] % 2)
+        X = F.avg_pool2d(X, kernel_size=2, padding=pad)
+        Y = F.avg_pool2d(Y, kernel_size=2, padding=pad)
+    mcs = torch.stack(mcs, dim=0)
+    return torch.prod((mcs[:-1] ** w[:-1].unsqueeze(1)) * (s ** w[-1]), dim=0)
+
+
 def state_dict_to_torch(sd) -> Dict[str, Tensor]:
     return {k: torch.as_tensor(v).float().contiguous() for k, v in sd.items()}

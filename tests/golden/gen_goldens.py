@@ -220,6 +220,33 @@ def g5_kodak_synth(ref_model, ref_models, out):
         json.dump({"N": N, "weight_seed": seed, "image_seed_base": 100, "images": rows}, f, indent=1)
 
 
+G6_CASES = [  # (B, H, W, image seed, noise seed, noise divisor): all integer-built, regenerable
+    (1, 512, 768, 300, 400, 8), (2, 192, 256, 301, 401, 4), (1, 200, 176, 302, 402, 16),
+    (1, 352, 208, 303, 403, 2)]
+
+
+def g6_pair(B, H, W, s_img, s_noise, div):
+    x8, y8 = synth.noisy_pair_u8(B, H, W, s_img, s_noise, div)
+    return torch.from_numpy(synth.to_unit_float(x8)), torch.from_numpy(synth.to_unit_float(y8))
+
+
+def g6_ms_ssim(ref_models, out):
+    """MS-SSIM (models/ms_ssim_torch.py:123-196, as train.py:178 calls it) on G6 pairs; the
+    reference is evaluated per image (its NaN check at :194 only works on a scalar)."""
+    rows = []
+    for (B, H, W, si, sn, div) in G6_CASES:
+        x, y = g6_pair(B, H, W, si, sn, div)
+        ref = torch.stack([ref_models.ms_ssim(y[b:b + 1], x[b:b + 1], data_range=1.0,
+                                              size_average=True) for b in range(B)])
+        check_equal(f"g6[{B}x{H}x{W}]", oracle.ms_ssim(y, x, 1.0), ref)
+        rows.append({"B": B, "H": H, "W": W, "image_seed": si, "noise_seed": sn, "noise_div": div,
+                     "ms_ssim": [float(v) for v in ref]})
+        print("g6", rows[-1])
+    with open(os.path.join(out, "g6_ms_ssim.json"), "w") as f:
+        json.dump({"note": "reference ms_ssim(y, x, data_range=1.0) per image; pairs from "
+                           "gen_goldens.g6_pair", "cases": rows}, f, indent=1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default="/root/reference")
@@ -231,7 +258,8 @@ def main():
              "g2": lambda: g2_bit_estimator(ref_models, HERE),
              "g3": lambda: g3_c1(ref_model, HERE),
              "g4": lambda: g4_train(ref_model, HERE),
-             "g5": lambda: g5_kodak_synth(ref_model, ref_models, HERE)}
+             "g5": lambda: g5_kodak_synth(ref_model, ref_models, HERE),
+             "g6": lambda: g6_ms_ssim(ref_models, HERE)}
     for k, fn in steps.items():
         if not args.only or k in args.only.split(","):
             fn()

@@ -285,9 +285,16 @@ def test_kodak_synth_subset(device, precision, golden_dir):
     for row in [meta["images"][i] for i in (0, 3, 9, 23)]:
         x = torch.from_numpy(synth.to_unit_float(
             synth.smooth_image_u8(meta["image_seed_base"] + row["index"], row["height"], row["width"])))[None]
-        ev = net.evaluate(x.to(device), want_y=True)
+        ev = net.evaluate(x.to(device), want_y=True, want_msssim=True)
         assert ev["bpp"][0].item() == pytest.approx(row["bpp"], rel=METRIC_REL)
         assert ev["psnr"][0].item() == pytest.approx(row["psnr"], rel=METRIC_REL)
+        # MS-SSIM kernel parity on the same pair (GPU recon, x) against the oracle restatement
+        r_ms = oracle.ms_ssim(ev["clipped"].cpu(), x, 1.0)
+        assert ev["ms_ssim"][0].item() == pytest.approx(r_ms.item(), rel=1e-5)
+        # end to end against the reference's value: these ~6.6 dB reconstructions give
+        # MS-SSIM ≈ 0.02, a product whose relative error is Σ w_l·δcs_l / cs_l with small cs_l,
+        # so recon-level fp32 differences are amplified; the bar is 1e-3 relative here
+        assert ev["ms_ssim"][0].item() == pytest.approx(row["ms_ssim"], rel=1e-3)
         _, r_yhat, _, _, r_y = oracle.codec_forward(x, sd)
         n = check_latents(ev["y_hat"], ev["y"], r_yhat, r_y)
         print(f"kodak-synth[{row['index']}] {precision}: {n} near-tie latent flips of {r_yhat.numel()}")
@@ -306,6 +313,30 @@ def test_determinism_and_batch_independence(device, precision):
         assert torch.equal(evi["y_hat"][0], ev1["y_hat"][i])
         assert torch.equal(evi["bpp"][0], ev1["bpp"][i])
         assert torch.equal(evi["clipped"][0], ev1["clipped"][i])
+
+
+def test_ms_ssim_vs_reference_fixture(device, golden_dir):
+    """GPU MS-SSIM against the reference's values on the G6 pairs (incl. odd pyramid levels and
+    B = 2). The fp32 filter sums run in another order than oneDNN's, so the bar is 1e-5 rel."""
+    meta = json.load(open(os.path.join(golden_dir, "g6_ms_ssim.json")))
+    for c in meta["cases"]:
+        x8, y8 = synth.noisy_pair_u8(c["B"], c["H"], c["W"], c["image_seed"], c["noise_seed"], c["noise_div"])
+        x, y = (torch.from_numpy(synth.to_unit_float(a)).to(device) for a in (x8, y8))
+        got = kernels.ms_ssim(y, x, 1.0).cpu()
+        assert got.tolist() == pytest.approx(c["ms_ssim"], rel=1e-5), (c, got)
+        assert torch.equal(kernels.ms_ssim(y, x, 1.0).cpu(), got)   # deterministic
+
+
+def test_ms_ssim_vs_oracle(device):
+    """Random pairs, three sizes, against the oracle restatement."""
+    for (B, H, W) in [(3, 176, 192), (1, 256, 256), (2, 333, 181)]:
+        x = torch.from_numpy(synth.uniform(31, (B, 3, H, W)))
+        y = (x + torch.from_numpy(synth.normal_like(32, (B, 3, H, W), 0.05))).clamp(0, 1)
+        ref = oracle.ms_ssim(y, x, 1.0)
+        got = kernels.ms_ssim(y.to(device), x.to(device), 1.0).cpu()
+        assert got.tolist() == pytest.approx(ref.tolist(), rel=1e-5), (B, H, W, got, ref)
+    with pytest.raises(_lib.Iclr17Error, match="too small"):
+        kernels.ms_ssim(torch.rand(1, 3, 64, 64, device=device), torch.rand(1, 3, 64, 64, device=device))
 
 
 def test_errors_are_loud(device):

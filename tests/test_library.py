@@ -63,3 +63,15 @@ def test_cpu_tensors_fail_loudly():
         net(torch.rand(1, 3, 32, 32))
     with pytest.raises(_lib.Iclr17Error, match="ROCm GPU"):
         kernels.gdn(torch.rand(1, 128, 4, 4), torch.zeros(128), torch.zeros(128 * 128), False)
+
+
+def test_msssim_window_matches_reference():
+    """csrc/msssim.hip embeds the reference's fp32 Gaussian window (ms_ssim_torch.py:5-18) as hex
+    constants; they must equal the oracle's (reference-identical) window bit for bit."""
+    import re
+    from oracle import codec_ref as oracle
+    text = open(os.path.join(os.path.dirname(_lib.LIB_PATH), "csrc", "msssim.hip")).read()
+    block = text[text.index("c_gauss[WIN] = {"):]
+    block = block[:block.index("};")]
+    consts = [float.fromhex(h[:-1]) for h in re.findall(r"-?0x[0-9a-fp.+-]+f", block)]
+    assert consts == oracle.gauss_window().tolist()

@@ -78,3 +78,24 @@ def test_g5_kodak_synth_subset(golden_dir):
         clipped, y_hat, bpp, _, _ = oracle.codec_forward(x, sd)
         assert bpp.item() == pytest.approx(row["bpp"], rel=1e-6)
         assert oracle.psnr(clipped, x).item() == pytest.approx(row["psnr"], rel=1e-6)
+
+
+def test_g6_ms_ssim(golden_dir):
+    """The oracle's MS-SSIM restatement against the reference's values (models/ms_ssim_torch.py)."""
+    meta = json.load(open(os.path.join(golden_dir, "g6_ms_ssim.json")))
+    for c in meta["cases"]:
+        x8, y8 = synth.noisy_pair_u8(c["B"], c["H"], c["W"], c["image_seed"], c["noise_seed"], c["noise_div"])
+        x, y = (torch.from_numpy(synth.to_unit_float(a)) for a in (x8, y8))
+        got = oracle.ms_ssim(y, x, 1.0)
+        assert got.tolist() == pytest.approx(c["ms_ssim"], rel=0, abs=0), (c, got)
+
+
+def test_g5_ms_ssim(golden_dir):
+    """MS-SSIM of a Kodak-size reconstruction (G5: the reference's clipped output vs x)."""
+    meta = json.load(open(os.path.join(golden_dir, "g5_kodak24_synth_n192.json")))
+    sd = oracle.state_dict_to_torch(synth.trained_like_state_dict(meta["N"], meta["weight_seed"]))
+    row = meta["images"][1]
+    x = torch.from_numpy(synth.to_unit_float(
+        synth.smooth_image_u8(meta["image_seed_base"] + row["index"], row["height"], row["width"])))[None]
+    clipped = oracle.codec_forward(x, sd)[0]
+    assert oracle.ms_ssim(clipped, x, 1.0).item() == row["ms_ssim"]

@@ -190,6 +190,66 @@ def run_train(args, net, x, world, dev):
     }
 
 
+KODAK_PORTRAIT = (3, 8, 9, 16, 17, 18)   # kodim04/09/10/17/18/19: 512 wide x 768 tall
+
+
+def kodak_synth_images(meta):
+    """The G5 synthetic Kodak-24 set (tests/golden/gen_goldens.py: smooth_image_u8(100+i))."""
+    out = []
+    for row in meta["images"]:
+        x = synth.to_unit_float(synth.smooth_image_u8(meta["image_seed_base"] + row["index"],
+                                                      row["height"], row["width"]))
+        out.append(torch.from_numpy(x)[None])
+    return out
+
+
+def run_kodak(args, dev):
+    """C2 (BASELINE configs[1]): Kodak-24 encode/decode at N=192 with testKodak's per-image
+    metrics (bpp, PSNR, MS-SSIM on the GPU), synthetic Kodak images (no network), seeded
+    trained-like weights; parity against the reference's own values (tests/golden/G5)."""
+    meta = json.load(open(os.path.join(REPO, "tests", "golden", "g5_kodak24_synth_n192.json")))
+    net = ImageCompressor(out_channel_N=meta["N"])
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in
+                         synth.trained_like_state_dict(meta["N"], meta["weight_seed"]).items()})
+    net = net.to(dev).eval()
+    imgs = kodak_synth_images(meta)
+    land = torch.cat([imgs[i] for i in range(24) if i not in KODAK_PORTRAIT]).to(dev)
+    port = torch.cat([imgs[i] for i in KODAK_PORTRAIT]).to(dev)
+
+    def step():
+        return net.evaluate(land, want_msssim=True), net.evaluate(port, want_msssim=True)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            ev_l, ev_p = step()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+    land_idx = [i for i in range(24) if i not in KODAK_PORTRAIT]
+    per = {}
+    for ev, idx in ((ev_l, land_idx), (ev_p, list(KODAK_PORTRAIT))):
+        for j, i in enumerate(idx):
+            per[i] = {k: ev[k][j].item() for k in ("bpp", "psnr", "ms_ssim")}
+    rel = {k: max(abs(per[i][k] - meta["images"][i][k]) / abs(meta["images"][i][k]) for i in range(24))
+           for k in ("bpp", "psnr", "ms_ssim")}
+    pixels = 24 * 512 * 768 * args.steps
+    return {
+        "metric": "Mpixels/s Kodak-24 encode+decode with per-image bpp/PSNR/MS-SSIM (C2)",
+        "value": round(pixels / elapsed / 1e6, 2), "unit": "Mpix/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic Kodak-24 (18 x 512x768 + 6 x 768x512, G5 generator), seeded trained-like weights",
+        "config": {"workload": "Kodak-24 eval: encode, round, rate, decode, clamp, per-image bpp/PSNR/MS-SSIM",
+                   "N": meta["N"], "precision": kernels.precision()},
+        "parity_vs_reference_G5": {"max_rel_" + k: v for k, v in rel.items()},
+        "dataset_average": {k: sum(per[i][k] for i in range(24)) / 24 for k in ("bpp", "psnr", "ms_ssim")},
+    }
+
+
 def cpu_baseline(N: int, H: int, W: int, budget_s: float) -> dict:
     """The oracle (op-for-op restatement of the reference forward, bit-identical to it on the
     build host) timed on this host's cores on a bounded sample."""
@@ -239,7 +299,7 @@ def main() -> None:
     ap.add_argument("--N", type=int, default=192)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", choices=("eval", "train"), default="eval")
+    ap.add_argument("--mode", choices=("eval", "train", "kodak"), default="eval")
     ap.add_argument("--precision", choices=kernels.PRECISIONS, default=None,
                     help="inference contraction mode (default: ICLR17_PRECISION or x6)")
     args = ap.parse_args()
@@ -254,6 +314,10 @@ def main() -> None:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
+    if args.mode == "kodak":
+        if rank == 0:
+            print(json.dumps(run_kodak(args, dev)), flush=True)
+        return
     N, S, B = args.N, args.size, args.batch
     net = ImageCompressor(out_channel_N=N)
     net.load_state_dict({k: torch.from_numpy(v) for k, v in synth.trained_like_state_dict(N, 1).items()})

@@ -84,6 +84,8 @@ class Step:
         self.enc = net.Encoder.packed()
         self.dec = net.Decoder.packed()
         self.rate = net.bitEstimator.packed()
+        self.g6 = [m.effective_params_x6() for m in (net.Encoder.gdn1, net.Encoder.gdn2,
+                                                      net.Decoder.igdn1, net.Decoder.igdn2)]
 
     def __call__(self, events=None):
         net, N = self.net, self.N
@@ -92,15 +94,17 @@ class Step:
         ev = (lambda i: events[i].record()) if events is not None else (lambda i: None)
         ev(0)
         if kernels.precision() == "x6":
-            hs, _, _ = kernels.conv1_gdn_x6(self.x, w1, net.Encoder.conv1.bias, g1[0], g1[1], N)
+            e1, e2, e3, e4 = self.g6
+            hs, _, _ = kernels.conv1_gdn_x6(self.x, w1, net.Encoder.conv1.bias, e1[0], e1[1], N,
+                                            g6=e1[2])
             ev(1)
-            hs, _, _ = kernels.conv2_gdn_x6(hs, w2, net.Encoder.conv2.bias, g2[0], g2[1])
+            hs, _, _ = kernels.conv2_gdn_x6(hs, w2, net.Encoder.conv2.bias, *e2)
             ev(2)
             y_hat, partial, _, ys = kernels.conv3_quant_rate_x6(hs, w3, self.rate)
             ev(3)
-            hs, _, _ = kernels.deconv_igdn_x6(ys, d1, net.Decoder.deconv1.bias, q1[0], q1[1])
+            hs, _, _ = kernels.deconv_igdn_x6(ys, d1, net.Decoder.deconv1.bias, *e3)
             ev(4)
-            _, h, _ = kernels.deconv_igdn_x6(hs, d2, net.Decoder.deconv2.bias, q2[0], q2[1],
+            _, h, _ = kernels.deconv_igdn_x6(hs, d2, net.Decoder.deconv2.bias, *e4,
                                              want_split=False, want_f32=True)
             ev(5)
         else:

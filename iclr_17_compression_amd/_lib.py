@@ -52,11 +52,13 @@ SIGNATURES = {
     "iclr17_synthesis_deconv3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P]),
     "iclr17_output_partials_per_image": (_I, [_I, _I]),
     "iclr17_split_planes": (_I, [_P, ctypes.c_long, _P, _P]),
-    "iclr17_analysis_conv1_gdn_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
-    "iclr17_analysis_conv2_gdn_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_split_packed": (_I, [_P, _I, _I, _I, _P, _P]),
+    "iclr17_analysis_conv1_gdn_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_analysis_conv2_gdn_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_analysis_conv3_quant_rate_x6": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P,
                                                  _P, _P]),
-    "iclr17_synthesis_deconv_igdn_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_synthesis_deconv_igdn_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
+                                             _P]),
     "iclr17_reduce_partials": (_I, [_P, _I, _I, _P, _P, _D, _P]),
     "iclr17_ms_ssim_workspace_size": (_SZ, [_I, _I, _I]),
     "iclr17_ms_ssim": (_I, [_P, _P, _I, _I, _I, _F, _P, _SZ, _P, _P]),

@@ -96,6 +96,7 @@ struct EngineArgs {
   long in_plane;                    // plane stride (elements)
   unsigned short* out_split;        // [3][B][Hout][Wout][CO] or nullptr
   long out_plane;
+  const unsigned short* ggamma6;    // x6: γ_eff split, [3][CO/8][CO][8] bf16 (plane CO·CO)
 };
 
 struct TileInfo {
@@ -332,15 +333,73 @@ __device__ __forceinline__ void chan_gemm_lds(f4 (&acc)[MT][NT], const float* sX
   }
 }
 
+// x6 channel contraction: acc[m][i] = Σ_j sX[m][j]·Γ[j][i], sX fp32 in LDS (split in VALU, one
+// 8-channel fragment per (mt, 32-deep k-block)), Γ pre-split [3][CO/8][CO][8] bf16 — the
+// B-fragment layout of v_mfma_f32_16x16x32_bf16 — read from L2 (221 KB at CO = 192; there is
+// no LDS left beside the x² tile at two workgroups per CU), one k-block ahead. Entry: the sX
+// writes of every wave are published (caller's barrier).
+template <int CO, int MT, int NT>
+__device__ __forceinline__ void chan_gemm_x6(f4 (&acc)[MT][NT], const float* sX,
+                                             const unsigned short* __restrict__ g6, int wm,
+                                             int ncol0, int lane) {
+  constexpr int XS = CO + 8;
+  constexpr int KB = CO / 32;
+  constexpr long GP = (long)CO * CO;   // plane stride
+  static_assert(KB % 2 == 0, "k-blocks in pairs (ping-pong B registers)");
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
+  const float* xrow = sX + (wm * MT * 16 + (lane & 15)) * XS + 8 * (lane >> 4);
+  const unsigned short* gb = g6 + ((lane >> 4) * CO + ncol0 + (lane & 15)) * 8;
+  u4 b0[3][NT], b1[3][NT];
+  auto load = [&](int kb, u4 (&b)[3][NT]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        b[p][nt] = *(const u4*)(gb + p * GP + (long)kb * 4 * CO * 8 + nt * 128);
+  };
+  auto block = [&](int kb, const u4 (&b)[3][NT]) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      u4 ah, am, al;
+      split8(*(const f4*)(xrow + mt * 16 * XS + kb * 32),
+             *(const f4*)(xrow + mt * 16 * XS + kb * 32 + 4), ah, am, al);
+      const bf8 Ah = __builtin_bit_cast(bf8, ah), Am = __builtin_bit_cast(bf8, am),
+                Al = __builtin_bit_cast(bf8, al);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const bf8 Bh = __builtin_bit_cast(bf8, b[0][nt]), Bm = __builtin_bit_cast(bf8, b[1][nt]),
+                  Bl = __builtin_bit_cast(bf8, b[2][nt]);
+        f4 c = acc[mt][nt];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al, Bh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bl, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bm, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bm, c, 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bh, c, 0, 0, 0);
+      }
+    }
+  };
+  load(0, b0);
+  for (int kb = 0; kb < KB; kb += 2) {
+    load(kb + 1, b1);
+    block(kb, b0);
+    if (kb + 2 < KB) load(kb + 2, b0);
+    block(kb + 1, b1);
+  }
+}
+
 // x (bias already added) in accumulator layout → GDN(x) (or IGDN) left in LDS sX[BM][CO+4].
 // models/GDN.py:83-90: n = conv2d(x², γ, β) = β + Σ_j γ[i][j]·x_j²;  y = x / √n | x·√n.
 // The caller guarantees smem is free on entry; on return every wave has passed a barrier after
 // the last sX write.
-template <int CO, int MT, int NT, bool INVERSE, int R = BM, int T = 256>
+template <int CO, int MT, int NT, bool INVERSE, int R = BM, int T = 256, bool G6 = false>
 __device__ __forceinline__ void gdn_core(const f4 (&x)[MT][NT], float* sX,
                                          const float* __restrict__ gbeta,
                                          const float* __restrict__ gp, int wm, int ncol0,
-                                         int lane) {
+                                         int lane, const unsigned short* g6 = nullptr) {
   constexpr int XS = CO + 8;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
@@ -354,8 +413,13 @@ __device__ __forceinline__ void gdn_core(const f4 (&x)[MT][NT], float* sX,
         sX[row * XS + col] = v * v;
       }
   f4 nacc[MT][NT];
-  chan_gemm_lds<CO, MT, NT, false, T / 64>(nacc, sX, gp, sX + R * XS, wm, ncol0, lane,
-                                           __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+  if constexpr (G6) {
+    __syncthreads();   // x² of every wave published
+    chan_gemm_x6<CO, MT, NT>(nacc, sX, g6, wm, ncol0, lane);
+  } else {
+    chan_gemm_lds<CO, MT, NT, false, T / 64>(nacc, sX, gp, sX + R * XS, wm, ncol0, lane,
+                                             __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+  }
   __syncthreads();  // all reads of x² done
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
@@ -387,11 +451,12 @@ __device__ __forceinline__ void acc_to_lds(const f4 (&v)[MT][NT], float* s, int 
       }
 }
 
-template <int CO, int MT, int NT, bool INVERSE, int R = BM, int T = 256>
+template <int CO, int MT, int NT, bool INVERSE, int R = BM, int T = 256, bool G6 = false>
 __device__ __forceinline__ void gdn_epilogue(f4 (&x)[MT][NT], float* smem, const EngineArgs& a,
                                              const TileInfo& t, int wm, int ncol0, int lane) {
   constexpr int XS = CO + 8;
-  gdn_core<CO, MT, NT, INVERSE, R, T>(x, smem, a.gbeta, a.ggamma, wm, ncol0, lane);
+  gdn_core<CO, MT, NT, INVERSE, R, T, G6>(x, smem, a.gbeta, a.ggamma, wm, ncol0, lane,
+                                          a.ggamma6);
   if (a.out != nullptr) store_tile_rows<CO, R, T>(a, t, smem, XS, a.out, CO, 0);
   if (a.out_split != nullptr) store_tile_rows_split<CO, R, T>(a, t, smem, XS, CO, 0);
   if (a.pre != nullptr) {
@@ -904,7 +969,7 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
       for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[mt][nt][r] += a.bias[ncol0 + nt * 16 + (lane & 15)];
-    gdn_epilogue<CO, MT, NT, EPI == EPI_IGDN>(acc, smem, a, t, wm, ncol0, lane);
+    gdn_epilogue<CO, MT, NT, EPI == EPI_IGDN, BM, 256, X6>(acc, smem, a, t, wm, ncol0, lane);
   } else if constexpr (EPI == EPI_QUANT) {
     quant_epilogue<CO, BN, MT, NT, WN>(acc, smem, a, t, wm, ncol0, lane, wave);
   } else if constexpr (EPI == EPI_OUT3) {
@@ -961,7 +1026,7 @@ constexpr int P1ZERO = P1NI * 256;        // zero slot, after the DMA'd region
 // EPI_GDN: analysis conv1 + bias + GDN1 (forward). EPI_IGDN_BWD: the same contraction is the
 // input gradient of the synthesis deconv3 (its adjoint: conv2d(g_recon, W, stride 4, pad 4)),
 // fused with the IGDN2 backward.
-template <int CO, int EPI>
+template <int CO, int EPI, bool G6 = false>
 __global__ void __launch_bounds__(256) conv1_gdn_kernel(const EngineArgs a) {
   constexpr int WN = 4;
   constexpr int MT = BM / 16;
@@ -1077,7 +1142,7 @@ __global__ void __launch_bounds__(256) conv1_gdn_kernel(const EngineArgs a) {
       for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[mt][nt][r] += a.bias[ncol0 + nt * 16 + (lane & 15)];
-    gdn_epilogue<CO, MT, NT, false>(acc, smem, a, t, wm, ncol0, lane);
+    gdn_epilogue<CO, MT, NT, false, BM, 256, G6>(acc, smem, a, t, wm, ncol0, lane);
   } else {
     static_assert(EPI == EPI_IGDN_BWD, "conv1 kernel epilogues: GDN fwd, IGDN bwd");
     gdn_bwd_epilogue<CO, MT, NT, true>(acc, smem, a, t, wm, ncol0, lane);
@@ -1238,12 +1303,14 @@ struct SplitIO {
   long in_plane = 0;
   unsigned short* out = nullptr;
   long out_plane = 0;
+  const unsigned short* gamma6 = nullptr;   // x6: split γ_eff for the GDN contraction
 };
 
 static void apply_split(EngineArgs& a, const SplitIO* x6) {
   if (x6 == nullptr) return;
   a.in_split = x6->in; a.in_plane = x6->in_plane;
   a.out_split = x6->out; a.out_plane = x6->out_plane;
+  a.ggamma6 = x6->gamma6;
 }
 
 template <int N, int EPI = EPI_GDN>
@@ -1260,6 +1327,12 @@ int launch_conv1(const float* x, int B, int H, int W, const float* wp, const flo
   a.sin = 4; a.sout = 1;
   a.tt.npx = 1; a.tt.nph = 1;
   dim3 grid(a.tiles_x * a.tiles_y * B, 1);
+  if constexpr (EPI == EPI_GDN) {
+    if (a.ggamma6 != nullptr) {
+      hipLaunchKernelGGL((conv1_gdn_kernel<N, EPI, true>), grid, dim3(256), 0, st, a);
+      return check_launch("conv1_gdn");
+    }
+  }
   hipLaunchKernelGGL((conv1_gdn_kernel<N, EPI>), grid, dim3(256), 0, st, a);
   return check_launch(EPI == EPI_GDN ? "conv1_gdn" : "bwd_deconv3_igdn");
 }
@@ -1376,6 +1449,27 @@ __global__ void __launch_bounds__(256) split_planes_kernel(const float* __restri
   }
 }
 
+// packed fp32 operand [taps][K/4][N][4] → split planes [3][taps][K/8][N][8] bf16 (the
+// B-fragment layout of v_mfma_f32_16x16x32_bf16), exact
+__global__ void __launch_bounds__(256) split_packed_kernel(const float* __restrict__ w, int taps,
+                                                           int K, int N,
+                                                           unsigned short* __restrict__ planes) {
+  const long n = (long)taps * (K / 8) * N;   // 8-element groups
+  const long plane = n * 8;
+  for (long g = (long)blockIdx.x * 256 + threadIdx.x; g < n; g += (long)gridDim.x * 256) {
+    const long tk = g / N;
+    const int col = (int)(g - tk * N);
+    const long tap = tk / (K / 8);
+    const int k8 = (int)(tk - tap * (K / 8));
+    const float* src = w + ((tap * (K / 4) + 2 * k8) * N + col) * 4;
+    u4 hi, mi, lo;
+    split8(*(const f4*)src, *(const f4*)(src + (long)N * 4), hi, mi, lo);
+    *(u4*)(planes + g * 8) = hi;
+    *(u4*)(planes + plane + g * 8) = mi;
+    *(u4*)(planes + 2 * plane + g * 8) = lo;
+  }
+}
+
 }  // namespace iclr17
 
 using namespace iclr17;
@@ -1488,10 +1582,21 @@ int iclr17_split_planes(const float* x, long n, uint16_t* planes, void* stream) 
   return check_launch("split_planes");
 }
 
+int iclr17_split_packed(const float* packed, int taps, int K, int N, uint16_t* planes,
+                        void* stream) {
+  ICLR17_REQUIRE(packed && planes && taps > 0 && K > 0 && K % 8 == 0 && N > 0, ICLR17_EINVAL,
+                 "split_packed: bad arguments");
+  const long n = (long)taps * (K / 8) * N;
+  const int blocks = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  hipLaunchKernelGGL(split_packed_kernel, dim3(blocks), dim3(256), 0, S(stream), packed, taps, K,
+                     N, (unsigned short*)planes);
+  return check_launch("split_packed");
+}
+
 int iclr17_analysis_conv1_gdn_x6(const float* x, int B, int H, int W, int N,
                                  const float* w_packed, const float* bias, const float* beta_eff,
-                                 const float* gamma_packed, float* out, uint16_t* out_split,
-                                 float* pre_out, void* stream) {
+                                 const float* gamma_packed, const uint16_t* gamma_split,
+                                 float* out, uint16_t* out_split, float* pre_out, void* stream) {
   int rc = check_dims(B, H, W, N);
   if (rc) return rc;
   ICLR17_REQUIRE(x && w_packed && bias && beta_eff && gamma_packed && (out || out_split),
@@ -1499,17 +1604,19 @@ int iclr17_analysis_conv1_gdn_x6(const float* x, int B, int H, int W, int N,
   SplitIO io;
   io.out = (unsigned short*)out_split;
   io.out_plane = (long)B * (H / 4) * (W / 4) * N;
+  io.gamma6 = (const unsigned short*)gamma_split;
   return N == 192 ? launch_conv1<192>(x, B, H, W, w_packed, bias, beta_eff, gamma_packed, out, pre_out, S(stream), nullptr, &io)
                   : launch_conv1<128>(x, B, H, W, w_packed, bias, beta_eff, gamma_packed, out, pre_out, S(stream), nullptr, &io);
 }
 
 int iclr17_analysis_conv2_gdn_x6(const uint16_t* in_split, int B, int H, int W, int N,
                                  const float* w_packed, const float* bias, const float* beta_eff,
-                                 const float* gamma_packed, float* out, uint16_t* out_split,
-                                 float* pre_out, void* stream) {
+                                 const float* gamma_packed, const uint16_t* gamma_split,
+                                 float* out, uint16_t* out_split, float* pre_out, void* stream) {
   int rc = check_dims(B, H, W, N);
   if (rc) return rc;
-  ICLR17_REQUIRE(in_split && w_packed && bias && beta_eff && gamma_packed && (out || out_split),
+  ICLR17_REQUIRE(in_split && w_packed && bias && beta_eff && gamma_packed && gamma_split &&
+                     (out || out_split),
                  ICLR17_EINVAL, "conv2_gdn_x6: null pointer");
   const int h = H / 4, w = W / 4;
   SplitIO io;
@@ -1517,6 +1624,7 @@ int iclr17_analysis_conv2_gdn_x6(const uint16_t* in_split, int B, int H, int W, 
   io.in_plane = (long)B * h * w * N;
   io.out = (unsigned short*)out_split;
   io.out_plane = (long)B * (h / 2) * (w / 2) * N;
+  io.gamma6 = (const unsigned short*)gamma_split;
   return N == 192 ? launch_conv5<192, EPI_GDN>(nullptr, B, h, w, w_packed, bias, beta_eff, gamma_packed, out, pre_out, 0, nullptr, nullptr, nullptr, nullptr, S(stream), nullptr, &io)
                   : launch_conv5<128, EPI_GDN>(nullptr, B, h, w, w_packed, bias, beta_eff, gamma_packed, out, pre_out, 0, nullptr, nullptr, nullptr, nullptr, S(stream), nullptr, &io);
 }
@@ -1544,17 +1652,20 @@ int iclr17_analysis_conv3_quant_rate_x6(const uint16_t* in_split, int B, int H, 
 
 int iclr17_synthesis_deconv_igdn_x6(const uint16_t* in_split, int B, int h, int w, int N,
                                     const float* w_packed, const float* bias,
-                                    const float* beta_eff, const float* gamma_packed, float* out,
-                                    uint16_t* out_split, float* pre_out, void* stream) {
+                                    const float* beta_eff, const float* gamma_packed,
+                                    const uint16_t* gamma_split, float* out, uint16_t* out_split,
+                                    float* pre_out, void* stream) {
   ICLR17_REQUIRE(B > 0 && h > 0 && w > 0, ICLR17_EINVAL, "deconv_igdn_x6: bad shape");
   ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "channel count N=%d unsupported", N);
-  ICLR17_REQUIRE(in_split && w_packed && bias && beta_eff && gamma_packed && (out || out_split),
+  ICLR17_REQUIRE(in_split && w_packed && bias && beta_eff && gamma_packed && gamma_split &&
+                     (out || out_split),
                  ICLR17_EINVAL, "deconv_igdn_x6: null pointer");
   SplitIO io;
   io.in = (const unsigned short*)in_split;
   io.in_plane = (long)B * h * w * N;
   io.out = (unsigned short*)out_split;
   io.out_plane = (long)B * (2 * h) * (2 * w) * N;
+  io.gamma6 = (const unsigned short*)gamma_split;
   return N == 192 ? launch_deconv5<192>(nullptr, B, h, w, w_packed, bias, beta_eff, gamma_packed, out, pre_out, S(stream), nullptr, &io)
                   : launch_deconv5<128>(nullptr, B, h, w, w_packed, bias, beta_eff, gamma_packed, out, pre_out, S(stream), nullptr, &io);
 }

@@ -231,6 +231,17 @@ def split_planes(x: Tensor) -> Tensor:
     return out
 
 
+def split_packed(packed: Tensor, taps: int, K: int, N: int) -> Tensor:
+    """Packed operand [taps][K/4][N][4] fp32 → split planes [3, taps·K·N] int16 (the x6
+    B-fragment layout); used for the GDN γ (taps = 1, K = N = C)."""
+    _check(packed, "packed operand", packed.dim())
+    if packed.numel() != taps * K * N:
+        raise Iclr17Error(f"iclr17: split_packed: {packed.numel()} != {taps}*{K}*{N}")
+    out = torch.empty(3, taps * K * N, device=packed.device, dtype=torch.int16)
+    call("iclr17_split_packed", _p(packed), taps, K, N, _p(out), _stream(packed))
+    return out
+
+
 def merge_planes(s: Tensor) -> Tensor:
     """Split form → fp32 (hi + mid + lo, exact). Test/debug helper (torch ops)."""
     u = s.to(torch.int32) & 0xFFFF
@@ -239,8 +250,9 @@ def merge_planes(s: Tensor) -> Tensor:
 
 
 def conv1_gdn_x6(x: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Tensor, N: int,
-                 want_f32: bool = False, want_pre: bool = False):
-    """conv1_gdn with the output in split form (+ fp32 / pre-GDN on request)."""
+                 want_f32: bool = False, want_pre: bool = False, g6: Optional[Tensor] = None):
+    """conv1_gdn with the output in split form (+ fp32 / pre-GDN on request); with g6
+    (split_packed of gp) the GDN contraction runs in x6 too."""
     _check(x, "image", 4)
     B, C, H, W = x.shape
     if C != 3:
@@ -252,13 +264,14 @@ def conv1_gdn_x6(x: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Tens
     out = torch.empty(B, H // 4, W // 4, N, device=x.device) if want_f32 else None
     pre = torch.empty(B, H // 4, W // 4, N, device=x.device) if want_pre else None
     call("iclr17_analysis_conv1_gdn_x6", _p(x), B, H, W, N, _p(wp), _p(bias), _p(beta_eff),
-         _p(gp), _p(out), _p(split), _p(pre), _stream(x))
+         _p(gp), _p(g6), _p(out), _p(split), _p(pre), _stream(x))
     return split, out, pre
 
 
 def conv2_gdn_x6(hs: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Tensor,
-                 want_f32: bool = False, want_pre: bool = False):
-    """conv2_gdn on a split-form input; returns (split, fp32 | None, pre | None)."""
+                 g6: Tensor, want_f32: bool = False, want_pre: bool = False):
+    """conv2_gdn on a split-form input (g6: split_packed γ); returns (split, fp32 | None,
+    pre | None)."""
     _check_split(hs, "activation")
     _, B, h4, w4, N = hs.shape
     _check_channels(N)
@@ -268,7 +281,7 @@ def conv2_gdn_x6(hs: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Ten
     out = torch.empty(B, h4 // 2, w4 // 2, N, device=hs.device) if want_f32 else None
     pre = torch.empty(B, h4 // 2, w4 // 2, N, device=hs.device) if want_pre else None
     call("iclr17_analysis_conv2_gdn_x6", _p(hs), B, H, W, N, _p(wp), _p(bias), _p(beta_eff),
-         _p(gp), _p(out), _p(split), _p(pre), _stream(hs))
+         _p(gp), _p(g6), _p(out), _p(split), _p(pre), _stream(hs))
     return split, out, pre
 
 
@@ -299,7 +312,8 @@ def conv3_quant_rate_x6(hs: Tensor, wp: Tensor, rate_packed: Tensor,
 
 
 def deconv_igdn_x6(hs: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Tensor,
-                   want_split: bool = True, want_f32: bool = False, want_pre: bool = False):
+                   g6: Tensor, want_split: bool = True, want_f32: bool = False,
+                   want_pre: bool = False):
     """deconv_igdn on a split-form input; returns (split | None, fp32 | None, pre | None)."""
     _check_split(hs, "activation")
     _, B, hh, ww, N = hs.shape
@@ -311,7 +325,7 @@ def deconv_igdn_x6(hs: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: T
     out = torch.empty(B, 2 * hh, 2 * ww, N, device=hs.device) if want_f32 else None
     pre = torch.empty(B, 2 * hh, 2 * ww, N, device=hs.device) if want_pre else None
     call("iclr17_synthesis_deconv_igdn_x6", _p(hs), B, hh, ww, N, _p(wp), _p(bias), _p(beta_eff),
-         _p(gp), _p(out), _p(split), _p(pre), _stream(hs))
+         _p(gp), _p(g6), _p(out), _p(split), _p(pre), _stream(hs))
     return split, out, pre
 
 

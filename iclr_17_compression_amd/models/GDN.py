@@ -66,6 +66,14 @@ class GDN(nn.Module):
                               lambda: kernels.pack_gdn(self.beta, self.gamma, bb, gb, ped),
                               force=force or self.training)
 
+    def effective_params_x6(self, force: bool = False):
+        """(beta_eff, gamma_packed, gamma split planes) for the x6 inference kernels."""
+        be, gp = self.effective_params(force)
+        C = self.beta.shape[0]
+        g6 = self._pack.get("gdn6", (self.beta, self.gamma),
+                            lambda: kernels.split_packed(gp, 1, C, C), force=force or self.training)
+        return be, gp, g6
+
     def effective_params_bwd(self):
         """(beta_eff, gamma_packed, gamma_packed_transposed) for the backward kernels."""
         bb, gb, ped = self.bounds_f32()

@@ -125,19 +125,25 @@ int iclr17_output_partials_per_image(int H, int W);
  * fp32 accumulation. Activations travel between layers in "split form": three bf16 planes
  * [3][B][h][w][N] (uint16 bf16 bits, plane stride B·h·w·N), written by the producing layer's
  * epilogue. conv1 (3-channel NCHW image) and deconv3 keep exact-f32 products. out / out_split
- * are each nullable, not both. */
+ * are each nullable, not both. The GDN/IGDN channel contraction runs in x6 as well when given
+ * gamma_split (required by conv2/deconv; nullable for conv1: then exact-f32). */
 /* x[n] (n % 8 == 0) → planes[3][n]. */
 int iclr17_split_planes(const float* x, long n, uint16_t* planes, void* stream);
+/* A packed operand [taps][K/4][N][4] fp32 → planes [3][taps][K/8][N][8] (3·taps·K·N uint16). The
+ * x6 GDN/IGDN channel contraction takes gamma_packed split this way (taps = 1, K = N = C):
+ * the gamma_split argument below. */
+int iclr17_split_packed(const float* packed, int taps, int K, int N, uint16_t* planes,
+                        void* stream);
 /* iclr17_analysis_conv1_gdn with the output also (or only) in split form. */
 int iclr17_analysis_conv1_gdn_x6(const float* x, int B, int H, int W, int N,
                                  const float* w_packed, const float* bias, const float* beta_eff,
-                                 const float* gamma_packed, float* out, uint16_t* out_split,
-                                 float* pre_out, void* stream);
+                                 const float* gamma_packed, const uint16_t* gamma_split,
+                                 float* out, uint16_t* out_split, float* pre_out, void* stream);
 /* iclr17_analysis_conv2_gdn on a split-form input. */
 int iclr17_analysis_conv2_gdn_x6(const uint16_t* in_split, int B, int H, int W, int N,
                                  const float* w_packed, const float* bias, const float* beta_eff,
-                                 const float* gamma_packed, float* out, uint16_t* out_split,
-                                 float* pre_out, void* stream);
+                                 const float* gamma_packed, const uint16_t* gamma_split,
+                                 float* out, uint16_t* out_split, float* pre_out, void* stream);
 /* iclr17_analysis_conv3_quant_rate on a split-form input; ŷ also in split form (nullable). */
 int iclr17_analysis_conv3_quant_rate_x6(const uint16_t* in_split, int B, int H, int W, int N,
                                         const float* w_packed, int quant_mode, const float* noise,
@@ -147,8 +153,9 @@ int iclr17_analysis_conv3_quant_rate_x6(const uint16_t* in_split, int B, int H, 
 /* iclr17_synthesis_deconv_igdn on a split-form input. */
 int iclr17_synthesis_deconv_igdn_x6(const uint16_t* in_split, int B, int h, int w, int N,
                                     const float* w_packed, const float* bias,
-                                    const float* beta_eff, const float* gamma_packed, float* out,
-                                    uint16_t* out_split, float* pre_out, void* stream);
+                                    const float* beta_eff, const float* gamma_packed,
+                                    const uint16_t* gamma_split, float* out, uint16_t* out_split,
+                                    float* pre_out, void* stream);
 
 /* testKodak's MS-SSIM (train.py:178 → models/ms_ssim_torch.py:123-196): per-image
  * ms_ssim(x, y, data_range) of NCHW [B,3,H,W] fp32 images, 11-tap σ=1.5 window, 5 levels (each

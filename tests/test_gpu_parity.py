@@ -78,16 +78,18 @@ def test_x6_layers(device, N):
     F = torch.nn.functional
     x = image(11, 2, 64, 96)
     w1, w2, w3, g1, g2 = net.Encoder.packed()
+    e1, e2 = net.Encoder.gdn1.effective_params_x6(), net.Encoder.gdn2.effective_params_x6()
     rate = net.bitEstimator.packed()
     with torch.no_grad():
-        a1s, a1, u1 = kernels.conv1_gdn_x6(x.to(device), w1, net.Encoder.conv1.bias, g1[0], g1[1], N,
-                                           want_f32=True, want_pre=True)
         r_u1 = F.conv2d(x, sd["Encoder.conv1.weight"], sd["Encoder.conv1.bias"], stride=4, padding=4)
         r_a1 = oracle.gdn(r_u1, sd["Encoder.gdn1.beta"], sd["Encoder.gdn1.gamma"], False)
-        assert rel_err(a1, nhwc(r_a1)) < REL and rel_err(u1, nhwc(r_u1)) < REL
-        assert torch.equal(kernels.merge_planes(a1s), a1)
+        for g6 in (None, e1[2]):   # exact-f32 GDN contraction, then the x6 one
+            a1s, a1, u1 = kernels.conv1_gdn_x6(x.to(device), w1, net.Encoder.conv1.bias, g1[0], g1[1], N,
+                                               want_f32=True, want_pre=True, g6=g6)
+            assert rel_err(a1, nhwc(r_a1)) < REL and rel_err(u1, nhwc(r_u1)) < REL
+            assert torch.equal(kernels.merge_planes(a1s), a1)
         a2s, a2, u2 = kernels.conv2_gdn_x6(kernels.split_planes(nhwc(r_a1).contiguous().to(device)), w2,
-                                           net.Encoder.conv2.bias, g2[0], g2[1], want_f32=True, want_pre=True)
+                                           net.Encoder.conv2.bias, *e2, want_f32=True, want_pre=True)
         r_u2 = F.conv2d(r_a1, sd["Encoder.conv2.weight"], sd["Encoder.conv2.bias"], stride=2, padding=2)
         r_a2 = oracle.gdn(r_u2, sd["Encoder.gdn2.beta"], sd["Encoder.gdn2.gamma"], False)
         assert rel_err(u2, nhwc(r_u2)) < REL and rel_err(a2, nhwc(r_a2)) < REL
@@ -100,9 +102,10 @@ def test_x6_layers(device, N):
         check_latents(y_hat.permute(0, 3, 1, 2), y.permute(0, 3, 1, 2), torch.round(r_y), r_y)
         # synthesis
         yq = torch.round(torch.from_numpy(synth.uniform(5, (2, N, 4, 6), -4, 4)))
-        d1, d2, _, q1, q2 = net.Decoder.packed()
+        d1, d2 = net.Decoder.packed()[:2]
+        q1, q2 = net.Decoder.igdn1.effective_params_x6(), net.Decoder.igdn2.effective_params_x6()
         s1s, s1, v1 = kernels.deconv_igdn_x6(kernels.split_planes(nhwc(yq).contiguous().to(device)), d1,
-                                             net.Decoder.deconv1.bias, q1[0], q1[1],
+                                             net.Decoder.deconv1.bias, *q1,
                                              want_f32=True, want_pre=True)
         r_v1 = F.conv_transpose2d(yq, sd["Decoder.deconv1.weight"], sd["Decoder.deconv1.bias"], stride=2, padding=2,
                                   output_padding=1)
@@ -110,7 +113,7 @@ def test_x6_layers(device, N):
         assert rel_err(v1, nhwc(r_v1)) < REL and rel_err(s1, nhwc(r_s1)) < REL
         assert torch.equal(kernels.merge_planes(s1s), s1)
         _, s2, _ = kernels.deconv_igdn_x6(kernels.split_planes(nhwc(r_s1).contiguous().to(device)), d2,
-                                          net.Decoder.deconv2.bias, q2[0], q2[1], want_split=False, want_f32=True)
+                                          net.Decoder.deconv2.bias, *q2, want_split=False, want_f32=True)
         r_s2 = oracle.gdn(F.conv_transpose2d(r_s1, sd["Decoder.deconv2.weight"], sd["Decoder.deconv2.bias"],
                                              stride=2, padding=2, output_padding=1),
                           sd["Decoder.igdn2.beta"], sd["Decoder.igdn2.gamma"], True)

@@ -21,6 +21,8 @@ torch.manual_seed(0)
 a1 = torch.randn(B, 64, 64, N, device=dev) * 0.5
 s1 = torch.randn(B, 32, 32, N, device=dev) * 0.5
 a1s, s1s = kernels.split_planes(a1), kernels.split_planes(s1)
+e2 = net.Encoder.gdn2.effective_params_x6()
+q2x = net.Decoder.igdn2.effective_params_x6()
 assert torch.equal(kernels.merge_planes(a1s), a1), "split not exact"
 
 
@@ -69,13 +71,13 @@ def numerics():
     r2 = ref_conv2(a1[:nb])
     f32 = kernels.conv2_gdn(a1[:nb].contiguous(), w2, net.Encoder.conv2.bias, g2[0], g2[1])
     x6s, x6f, _ = kernels.conv2_gdn_x6(kernels.split_planes(a1[:nb].contiguous()), w2,
-                                       net.Encoder.conv2.bias, g2[0], g2[1], want_f32=True)
+                                       net.Encoder.conv2.bias, *e2, want_f32=True)
     print("conv2_gdn  fp32:", err(f32, r2))
     print("conv2_gdn  x6  :", err(x6f, r2), " split==f32:", torch.equal(kernels.merge_planes(x6s), x6f))
     rd = ref_deconv2(s1[:nb])
     f32 = kernels.deconv_igdn(s1[:nb].contiguous(), d2, net.Decoder.deconv2.bias, q2[0], q2[1])
     _, x6f, _ = kernels.deconv_igdn_x6(kernels.split_planes(s1[:nb].contiguous()), d2,
-                                       net.Decoder.deconv2.bias, q2[0], q2[1], want_split=False,
+                                       net.Decoder.deconv2.bias, *q2x, want_split=False,
                                        want_f32=True)
     print("deconv2_igdn fp32:", err(f32, rd))
     print("deconv2_igdn x6  :", err(x6f, rd))
@@ -86,9 +88,9 @@ def timings():
     fld = 2.0 * B * (32 * 32 * N * N * 25 + 64 * 64 * N * N)
     t = {
         "conv2 fp32": (timeit(lambda: kernels.conv2_gdn(a1, w2, net.Encoder.conv2.bias, g2[0], g2[1])), fl2),
-        "conv2 x6": (timeit(lambda: kernels.conv2_gdn_x6(a1s, w2, net.Encoder.conv2.bias, g2[0], g2[1])), fl2),
+        "conv2 x6": (timeit(lambda: kernels.conv2_gdn_x6(a1s, w2, net.Encoder.conv2.bias, *e2)), fl2),
         "deconv2 fp32": (timeit(lambda: kernels.deconv_igdn(s1, d2, net.Decoder.deconv2.bias, q2[0], q2[1])), fld),
-        "deconv2 x6": (timeit(lambda: kernels.deconv_igdn_x6(s1s, d2, net.Decoder.deconv2.bias, q2[0], q2[1],
+        "deconv2 x6": (timeit(lambda: kernels.deconv_igdn_x6(s1s, d2, net.Decoder.deconv2.bias, *q2x,
                                                              want_split=False, want_f32=True)), fld),
     }
     print(TAG, " ".join(f"{k}={v[0]:.3f}ms({v[1] / v[0] / 1e9:.1f}TF)" for k, v in t.items()), flush=True)

@@ -143,10 +143,10 @@ def run_train(args, net, x, world, dev):
     """C3/C4: fused training step (forward_train + backward + bucketed all-reduce over RCCL +
     ±5 clamp + Adam), λ = 0.01·255² (train_lambda 650.25)."""
     from iclr_17_compression_amd import dist as idist
-    from iclr_17_compression_amd.train import clip_gradient
+    from iclr_17_compression_amd.optim import FusedAdam
     net.train()
     params = list(net.parameters())
-    opt = torch.optim.Adam(params, lr=1e-4)
+    opt = FusedAdam(params, lr=1e-4, grad_clip=5)   # ±5 clamp + Adam in one launch
     lam = 0.01 * 255.0 ** 2
     B, _, S, _ = x.shape
 
@@ -155,7 +155,6 @@ def run_train(args, net, x, world, dev):
         _, mse, bpp = net.forward_train(x)
         (lam * mse + bpp).backward()
         idist.allreduce_grads(params)
-        clip_gradient(params, 5)
         opt.step()
         return bpp
 

@@ -382,6 +382,13 @@ __device__ __forceinline__ void chan_gemm_x6(f4 (&acc)[MT][NT], const float* sX,
       }
     }
   };
+#ifdef ICLR17_G6_SINGLE
+  for (int kb = 0; kb < KB; ++kb) {   // one B register set: fewer VGPRs, loads not overlapped
+    load(kb, b0);
+    block(kb, b0);
+  }
+  (void)b1;
+#else
   load(0, b0);
   for (int kb = 0; kb < KB; kb += 2) {
     load(kb + 1, b1);
@@ -389,6 +396,7 @@ __device__ __forceinline__ void chan_gemm_x6(f4 (&acc)[MT][NT], const float* sX,
     if (kb + 2 < KB) load(kb + 2, b0);
     block(kb + 1, b1);
   }
+#endif
 }
 
 // x (bias already added) in accumulator layout → GDN(x) (or IGDN) left in LDS sX[BM][CO+4].
@@ -1398,7 +1406,11 @@ int launch_deconv5(const float* in, int B, int h, int w, const float* wp, const 
   // Forward: one workgroup per base block running the 4 phases (9/6/6/4 taps) in turn — equal
   // work per workgroup, shared input neighbourhood — when that still fills 2 workgroups per CU.
   const int base_tiles = a.tiles_x * a.tiles_y * B;
+#ifdef ICLR17_NO_PL
+  a.phase_loop = 0;
+#else
   a.phase_loop = (EPI == EPI_IGDN && base_tiles >= 512) ? 1 : 0;
+#endif
   if constexpr (EPI == EPI_IGDN) {
     const bool X6in = a.in_split != nullptr;
     if (a.phase_loop && X6in)

@@ -1,0 +1,67 @@
+"""Fused clamp + Adam — train.py:106-112 (clip_gradient then optimizer.step() of
+torch.optim.Adam(lr), the reference's optimizer, train.py:233) as one HIP launch over every
+parameter tensor (``iclr17_adam_step``).
+
+``FusedAdam`` has torch.optim.Adam's constructor and state layout (``exp_avg``,
+``exp_avg_sq``, ``step``) and the same update order, so checkpoints of its state dict look
+like Adam's. ``grad_clip`` folds train.py's element-wise ±5 clamp into the same pass (the
+clamped gradient is written back, as ``p.grad.data.clamp_`` does).
+"""
+from __future__ import annotations
+
+from typing import Iterable, Optional
+
+import torch
+
+from . import kernels
+from ._lib import Iclr17Error, call
+
+
+class FusedAdam(torch.optim.Optimizer):
+    def __init__(self, params: Iterable, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0, amsgrad: bool = False,
+                 grad_clip: Optional[float] = None):
+        if weight_decay != 0.0 or amsgrad:
+            raise Iclr17Error("iclr17: FusedAdam implements the reference's Adam (no weight decay, "
+                              "no amsgrad)")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps))
+        self.grad_clip = grad_clip
+        self._desc = None
+        self._desc_key = None
+
+    def _descriptors(self, group):
+        ps = [p for p in group["params"] if p.grad is not None]
+        for p in ps:
+            if not p.is_cuda or p.dtype != torch.float32 or not p.is_contiguous():
+                raise Iclr17Error("iclr17: FusedAdam needs contiguous fp32 device parameters")
+            st = self.state[p]
+            if not st:
+                st["step"] = torch.tensor(0.0)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        rows = [(p.data_ptr(), p.grad.data_ptr(), self.state[p]["exp_avg"].data_ptr(),
+                 self.state[p]["exp_avg_sq"].data_ptr(), p.numel()) for p in ps]
+        key = tuple(rows)
+        if key != self._desc_key:   # pointer table on the device, rebuilt only when a buffer moves
+            self._desc = torch.tensor(rows, dtype=torch.int64).to(ps[0].device)
+            self._desc_key = key
+        return ps, max(r[4] for r in rows)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        for group in self.param_groups:
+            if not any(p.grad is not None for p in group["params"]):
+                continue
+            ps, max_n = self._descriptors(group)
+            steps = {int(self.state[p]["step"].item()) for p in ps}
+            if len(steps) != 1:
+                raise Iclr17Error("iclr17: FusedAdam needs one step count per parameter group")
+            t = steps.pop() + 1
+            for p in ps:
+                self.state[p]["step"].fill_(float(t))
+            b1, b2 = group["betas"]
+            clip = float(self.grad_clip) if self.grad_clip else 0.0
+            call("iclr17_adam_step", kernels._p(self._desc), len(ps), max_n, float(group["lr"]),
+                 float(b1), float(b2), float(group["eps"]), t, clip, kernels._stream(ps[0]))
+        return loss

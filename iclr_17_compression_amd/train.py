@@ -29,6 +29,7 @@ import torch
 from . import dist as idist
 from . import synth
 from .model import ImageCompressor, load_model, save_model
+from .optim import FusedAdam
 
 logger = logging.getLogger("ImageCompression")
 
@@ -198,7 +199,8 @@ def main(argv=None):
         test_kodak(net, args.test_dir, device, global_step)
         return 0
     params = list(net.parameters())
-    optimizer = torch.optim.Adam(params, lr=cfg["lr"]["base"])
+    # train.py:233 Adam + train.py:106-111 clamp(±5), fused into one launch (optim.py)
+    optimizer = FusedAdam(params, lr=cfg["lr"]["base"], grad_clip=5)
     per_rank = max(1, cfg["batch_size"] // w)
     stream = ImageDirStream(args.train_dir, 256, per_rank, args.seed + 1000 * r, args.synthetic)
     meters = {k: AverageMeter(cfg["print_freq"]) for k in ("elapsed", "loss", "psnr", "bpp", "mse")}
@@ -219,8 +221,7 @@ def main(argv=None):
         optimizer.zero_grad(set_to_none=True)
         rd_loss.backward()
         idist.allreduce_grads(params)
-        clip_gradient(params, 5)
-        optimizer.step()
+        optimizer.step()   # clamp after the all-reduce (DataParallel's GPU0 clamp), then Adam
         if global_step % cfg["cal_step"] == 0:
             m = mse.item()
             meters["psnr"].update(10 * np.log10(1.0 / m) if m > 0 else 100)

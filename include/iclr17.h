@@ -165,6 +165,14 @@ size_t iclr17_ms_ssim_workspace_size(int B, int H, int W);
 int iclr17_ms_ssim(const float* x, const float* y, int B, int H, int W, float data_range,
                    void* workspace, size_t workspace_bytes, float* out, void* stream);
 
+/* train.py:106-112: element-wise gradient clamp to ±grad_clip (≤ 0: none; written back to the
+ * gradient) fused with one torch.optim.Adam step (no weight decay, no amsgrad) over n_tensors
+ * parameter tensors in one launch. desc: device int64 [n_tensors][5] = {param, grad, exp_avg,
+ * exp_avg_sq, numel} (pointers as integers); step = the 1-based step count after the increment;
+ * max_numel = the largest numel. */
+int iclr17_adam_step(const int64_t* desc, int n_tensors, long max_numel, double lr, double beta1,
+                     double beta2, double eps, long step, float grad_clip, void* stream);
+
 /* Deterministic fixed-order sums: per_image[b] = Σ_t partial[b*T + t] (nullable);
  * *total = (float)(scale · Σ_b per_image[b]) (nullable). model.py:73,78 bits→bpp. */
 int iclr17_reduce_partials(const double* partial, int B, int T, double* per_image, float* total,

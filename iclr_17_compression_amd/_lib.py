@@ -60,6 +60,7 @@ SIGNATURES = {
     "iclr17_synthesis_deconv_igdn_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
                                              _P]),
     "iclr17_reduce_partials": (_I, [_P, _I, _I, _P, _P, _D, _P]),
+    "iclr17_resized_crop_batch": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P]),
     "iclr17_adam_step": (_I, [_P, _I, ctypes.c_long, _D, _D, _D, _D, ctypes.c_long, _F, _P]),
     "iclr17_ms_ssim_workspace_size": (_SZ, [_I, _I, _I]),
     "iclr17_ms_ssim": (_I, [_P, _P, _I, _I, _I, _F, _P, _SZ, _P, _P]),

@@ -11,8 +11,8 @@ Differences from the reference, each a documented defect fix:
   D4  the evaluation directory comes from --test-dir (train.py:159 hard-codes a CLIC path);
   D9  data parallelism is one process per GPU with averaged gradients (DataParallel's gathered
       per-GPU bpp vector made rd_loss non-scalar).
-Data: ``--train-dir`` (PIL decode, random 256 crop, h/v flips: the RandomResizedCrop scale jitter
-of datasets.py:24 is not reproduced) or ``--synthetic`` seeded images.
+Data: ``--train-dir`` (PIL decode on the host; RandomResizedCrop(256), h/v flips and ToTensor
+on the GPU, PIL-exact — data.py) or ``--synthetic`` seeded images.
 """
 from __future__ import annotations
 
@@ -26,6 +26,7 @@ import time
 import numpy as np
 import torch
 
+from . import data
 from . import dist as idist
 from . import synth
 from .model import ImageCompressor, load_model, save_model
@@ -96,15 +97,18 @@ def load_rgb(path):
 
 
 class ImageDirStream:
-    """Random 256×256 crops with h/v flips from a directory (datasets.py:14-37 without the
-    resize jitter), or seeded synthetic images when no directory is given."""
+    """Training batches, datasets.py:14-37: for each image of a directory (sorted *.*), a
+    RandomResizedCrop(256) + random h/v flips + ToTensor, with the pixel work on the GPU
+    (data.resized_crop_batch: PIL-exact resampling from uint8 uploads); or seeded synthetic
+    images when no directory is given."""
 
-    def __init__(self, data_dir, image_size, batch, seed, synthetic=False):
+    def __init__(self, data_dir, image_size, batch, seed, synthetic=False, device=None):
         self.paths = sorted(glob.glob(os.path.join(data_dir, "*.*"))) if data_dir else []
         if not self.paths and not synthetic:
             raise FileNotFoundError(f"no training images under {data_dir!r} (use --synthetic)")
         self.size, self.batch, self.rng = image_size, batch, np.random.default_rng(seed)
         self.synthetic, self.step = synthetic or not self.paths, 0
+        self.device = device
 
     def __iter__(self):
         return self
@@ -114,23 +118,15 @@ class ImageDirStream:
         if self.synthetic:
             u8 = synth.image_u8(10_000 + self.step, self.batch, self.size, self.size)
             return torch.from_numpy(synth.to_unit_float(u8))
-        out = []
+        from PIL import Image
+        imgs, boxes, flips = [], [], []
         for _ in range(self.batch):
-            img = load_rgb(self.paths[self.rng.integers(len(self.paths))])
-            _, H, W = img.shape
-            s = self.size
-            if H < s or W < s:
-                img = torch.nn.functional.interpolate(img[None], size=(max(H, s), max(W, s)),
-                                                      mode="bilinear", align_corners=False)[0]
-                _, H, W = img.shape
-            y, x = self.rng.integers(H - s + 1), self.rng.integers(W - s + 1)
-            crop = img[:, y:y + s, x:x + s]
-            if self.rng.random() < 0.5:
-                crop = crop.flip(2)
-            if self.rng.random() < 0.5:
-                crop = crop.flip(1)
-            out.append(crop)
-        return torch.stack(out)
+            path = self.paths[self.rng.integers(len(self.paths))]
+            img = np.asarray(Image.open(path).convert("RGB"), dtype=np.uint8)
+            imgs.append(img)
+            boxes.append(data.random_resized_crop_params(self.rng, img.shape[0], img.shape[1]))
+            flips.append((bool(self.rng.random() < 0.5), bool(self.rng.random() < 0.5)))
+        return data.resized_crop_batch(imgs, boxes, flips, self.size, self.device)
 
 
 def kodak_images(test_dir):
@@ -202,7 +198,8 @@ def main(argv=None):
     # train.py:233 Adam + train.py:106-111 clamp(±5), fused into one launch (optim.py)
     optimizer = FusedAdam(params, lr=cfg["lr"]["base"], grad_clip=5)
     per_rank = max(1, cfg["batch_size"] // w)
-    stream = ImageDirStream(args.train_dir, 256, per_rank, args.seed + 1000 * r, args.synthetic)
+    stream = ImageDirStream(args.train_dir, 256, per_rank, args.seed + 1000 * r, args.synthetic,
+                            device=device)
     meters = {k: AverageMeter(cfg["print_freq"]) for k in ("elapsed", "loss", "psnr", "bpp", "mse")}
     if args.name and r == 0:
         save_model(net, global_step, save_path)

@@ -165,6 +165,16 @@ size_t iclr17_ms_ssim_workspace_size(int B, int H, int W);
 int iclr17_ms_ssim(const float* x, const float* y, int B, int H, int W, float data_range,
                    void* workspace, size_t workspace_bytes, float* out, void* stream);
 
+/* datasets.py:27-33 training transform on the GPU: per image, PIL-exact bilinear resize of its
+ * crop box to S×S (two passes, 8-bit fixed point), horizontal / vertical flips, /255 → out NCHW
+ * fp32 [B,3,S,S]. src: uint8 HWC images back to back; desc: int64 [B][16] = {src byte offset, H,
+ * W, crop top, left, height, width, flip_h, flip_v, tmp byte offset, x-tap offset, x taps per
+ * output, y-tap offset, y taps per output, 0, 0}; taps: int32 rows [S][2 + k] = {first, count,
+ * k 22-bit taps} per axis (iclr_17_compression_amd/data.py builds them); tmp: Σ crop_h·S·3 bytes;
+ * max_ch: the largest crop height. */
+int iclr17_resized_crop_batch(const uint8_t* src, const int64_t* desc, int B, int S, int max_ch,
+                              const int32_t* taps, uint8_t* tmp, float* out, void* stream);
+
 /* train.py:106-112: element-wise gradient clamp to ±grad_clip (≤ 0: none; written back to the
  * gradient) fused with one torch.optim.Adam step (no weight decay, no amsgrad) over n_tensors
  * parameter tensors in one launch. desc: device int64 [n_tensors][5] = {param, grad, exp_avg,

@@ -21,19 +21,38 @@ hipStream_t S(void* s) { return (hipStream_t)s; }
 
 constexpr int KP = 32;  // pixels per k-step
 
+__device__ __attribute__((aligned(16))) float g_wzero[4] = {0.f, 0.f, 0.f, 0.f};
+
+__device__ __forceinline__ void glds16w(const float* src, float* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+typedef float f16w __attribute__((ext_vector_type(16)));
+
+// GEMM: dW[m][tap, c] = Σ_p G[p][m] · X[p ⊕ tap][c] for one tap and a 64-channel tile c, over one
+// split of the pixels. v_mfma_f32_32x32x2_f32 (exact f32; lane l holds A[m = l&31][k = l>>5] and
+// B[k = l>>5][c = l&31]): a k-step of two pixels needs one element per lane per operand, and 32
+// consecutive lanes read 32 consecutive channels of one LDS pixel row — conflict-free
+// ds_read_b32, the [pixel][channel] tiles need no transpose. Both tiles arrive by LDS-DMA:
+// G [32 px][M] is one contiguous block of the NHWC gradient, X [32 px][64] the tap-shifted rows
+// (zero line outside the image), two stages, one barrier per 32 pixels. 4 waves: wave w owns
+// channels 32(w&1) .. +31 and rows 32·(3 (w>>1)) .. of M (3 tiles of 32×32 at M = 192, 2 at 128).
 template <int M, bool SQUARE>
 __global__ void __launch_bounds__(256) wgrad_k5_kernel(const float* __restrict__ G,
                                                        const float* __restrict__ X, int B, int Ho,
                                                        int Wo, int Hi, int Wi, int C, int ksize,
                                                        int stride, int pad, int nsplit,
                                                        float* __restrict__ part) {
-  constexpr int MT = M / 4 / 16;   // m-tiles per wave (3 for 192, 2 for 128)
-  constexpr int NT = 4;            // 64 columns
-  constexpr int GS = M + 4, XS = 64 + 4;
-  __shared__ __attribute__((aligned(16))) float smem[2 * KP * GS + 2 * KP * XS];
-  float* sG = smem;
-  float* sX = smem + 2 * KP * GS;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int MT = M / 64;                 // 32-row m-tiles per wave
+  constexpr int SG = KP * M, SX = KP * 64;   // floats per stage
+  constexpr int STAGE = SG + SX;
+  constexpr int NGI = SG * 4 / 1024, NXI = SX * 4 / 1024;   // DMA wave-instructions per stage
+  constexpr int NI = NGI + NXI, NI_W = NI / 4;
+  static_assert(NI % 4 == 0, "uniform DMA slots");
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ntap = ksize * ksize;
   const int tap = blockIdx.x % ntap, ct = blockIdx.x / ntap;
   const int kh = tap / ksize, kw = tap % ksize;
@@ -44,101 +63,69 @@ __global__ void __launch_bounds__(256) wgrad_k5_kernel(const float* __restrict__
   const long p1 = p0 + per < P ? p0 + per : P;
   const int nsteps = p1 > p0 ? (int)((p1 - p0 + KP - 1) / KP) : 0;
 
-  constexpr int GL = KP * M / 4 / 256;   // float4 loads of G per thread per step
-  f4 rg[GL], rx[2];
-  auto load = [&](int s) {
+  auto issue = [&](int s, int buf) {
     const long pb = p0 + (long)s * KP;
+    float* st = smem + buf * STAGE;
 #pragma unroll
-    for (int i = 0; i < GL; ++i) {
-      const int idx = tid + 256 * i;
-      const int pr = idx / (M / 4), c4 = idx % (M / 4);
-      const long p = pb + pr;
-      rg[i] = p < p1 ? *(const f4*)(G + p * M + c4 * 4) : f4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int idx = tid + 256 * i;
-      const int pr = idx >> 4, c4 = idx & 15;
-      const long p = pb + pr;
-      f4 v = f4{0.f, 0.f, 0.f, 0.f};
-      if (p < p1) {
-        const int ow = (int)(p % Wo);
-        const long q = p / Wo;
-        const int oh = (int)(q % Ho);
-        const int b = (int)(q / Ho);
-        const int iy = oh * stride - pad + kh, ix = ow * stride - pad + kw;
-        if (iy >= 0 && iy < Hi && ix >= 0 && ix < Wi) {
-          v = *(const f4*)(X + (((long)b * Hi + iy) * Wi + ix) * C + ct * 64 + c4 * 4);
-          if (SQUARE) v = v * v;
+    for (int j = 0; j < NI_W; ++j) {
+      const int i = wave + 4 * j;
+      if (i < NGI) {   // G: contiguous [pb, pb + 32) × M
+        const long e = (long)i * 256 + lane * 4;   // float offset in the tile
+        const long p = pb + e / M;
+        glds16w(p < p1 ? G + pb * M + e : g_wzero, st + i * 256);
+      } else {         // X: 4 pixel rows of 64 channels per instruction
+        const int xi = i - NGI;
+        const int row = xi * 4 + (lane >> 4), piece = lane & 15;
+        const long p = pb + row;
+        const float* src = g_wzero;
+        if (p < p1) {
+          const int ow = (int)(p % Wo);
+          const long q = p / Wo;
+          const int oh = (int)(q % Ho);
+          const int b = (int)(q / Ho);
+          const int iy = oh * stride - pad + kh, ix = ow * stride - pad + kw;
+          if (iy >= 0 && iy < Hi && ix >= 0 && ix < Wi)
+            src = X + (((long)b * Hi + iy) * Wi + ix) * C + ct * 64 + piece * 4;
         }
+        glds16w(src, st + SG + xi * 256);
       }
-      rx[i] = v;
-    }
-  };
-  auto store = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < GL; ++i) {
-      const int idx = tid + 256 * i;
-      *(f4*)(sG + buf * KP * GS + (idx / (M / 4)) * GS + (idx % (M / 4)) * 4) = rg[i];
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int idx = tid + 256 * i;
-      *(f4*)(sX + buf * KP * XS + (idx >> 4) * XS + (idx & 15) * 4) = rx[i];
     }
   };
 
-  f4 acc[MT][NT];
+  f16w acc[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < 16; ++r) acc[mt][r] = 0.f;
+  const int mrow0 = (wave >> 1) * MT * 32;
+  const int aoff = (lane >> 5) * M + mrow0 + (lane & 31);
+  const int boff = (lane >> 5) * 64 + (wave & 1) * 32 + (lane & 31);
 
-  if (nsteps > 0) {
-    load(0);
-    store(0);
-  }
-  __syncthreads();
-  const int m0 = wave * MT * 16;
+  if (nsteps > 0) issue(0, 0);
   for (int s = 0; s < nsteps; ++s) {
-    const int cur = s & 1;
-    if (s + 1 < nsteps) load(s + 1);
-    const float* g = sG + cur * KP * GS;
-    const float* x = sX + cur * KP * XS;
+    __syncthreads();   // stage s landed for every wave; stage (s+1)&1 is free
+    if (s + 1 < nsteps) issue(s + 1, (s + 1) & 1);
+    const float* g = smem + (s & 1) * STAGE + aoff;
+    const float* x = smem + (s & 1) * STAGE + SG + boff;
 #pragma unroll
-    for (int kb = 0; kb < KP / 16; ++kb) {
-      const int pr = kb * 16 + 4 * (lane >> 4);
-      f4 af[MT], bf[NT];
+    for (int k2 = 0; k2 < KP / 2; ++k2) {
+      float bv = x[k2 * 2 * 64];
+      if (SQUARE) bv = bv * bv;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) af[mt][e] = g[(pr + e) * GS + m0 + mt * 16 + (lane & 15)];
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) bf[nt][e] = x[(pr + e) * XS + nt * 16 + (lane & 15)];
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16(af[mt][e], bf[nt][e], acc[mt][nt]);
+        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(g[k2 * 2 * M + mt * 32], bv, acc[mt], 0, 0, 0);
     }
-    if (s + 1 < nsteps) store(cur ^ 1);
-    __syncthreads();
   }
   // part[split][m][c][tap]  (the PyTorch [m][c][kh][kw] layout)
   float* out = part + (long)split * M * C * ntap;
+  const int c = ct * 64 + (wave & 1) * 32 + (lane & 31);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + mt * 16 + 4 * (lane >> 4) + r;
-        const int c = ct * 64 + nt * 16 + (lane & 15);
-        out[((long)m * C + c) * ntap + tap] = acc[mt][nt][r];
-      }
+    for (int r = 0; r < 16; ++r) {
+      const int m = mrow0 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      out[((long)m * C + c) * ntap + tap] = acc[mt][r];
+    }
 }
 
 // conv1 / deconv3 weight gradient: K = 243 = (c, kh, kw) of a 9×9 stride-4 pad-4 window on a
@@ -246,18 +233,25 @@ __global__ void sum_splits_kernel(const float* __restrict__ part, int nsplit, lo
   }
 }
 
-// out[c] = Σ_t part[t][c]: 64 columns per workgroup, T split over 4 lane groups (strided), the 4
-// partial sums combined in order through LDS — fixed order, bitwise reproducible.
-__global__ void sum_rows_kernel(const float* __restrict__ part, int T, int C, float* __restrict__ out) {
+// out[c] = Σ_t part[t][c] in two fixed-order levels (bitwise reproducible): workgroup (column
+// block, split s) sums rows [s·per, (s+1)·per) — 4 lane groups strided, combined in order — into
+// ws[s][c]; then sum_splits adds the splits in order. Enough workgroups to be bandwidth-bound
+// (one workgroup per 64 columns walked thousands of rows serially).
+constexpr int SUM_ROWS_SPLITS = 64;
+
+__global__ void sum_rows_kernel(const float* __restrict__ part, int T, int C, int per,
+                                float* __restrict__ ws) {
   __shared__ float red[4][64];
   const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
+  const int t0 = blockIdx.y * per, t1 = t0 + per < T ? t0 + per : T;
   float s = 0.f;
   if (c < C)
-    for (int t = g; t < T; t += 4) s += part[(long)t * C + c];
+    for (int t = t0 + g; t < t1; t += 4) s += part[(long)t * C + c];
   red[g][cl] = s;
   __syncthreads();
-  if (g == 0 && c < C) out[c] = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
+  if (g == 0 && c < C)
+    ws[(long)blockIdx.y * C + c] = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
 }
 
 // Column sums of a [P][C] row-major matrix (NHWC activations): part[chunk][c].
@@ -287,8 +281,10 @@ __global__ void plane_sum_kernel(const float* __restrict__ A, int C, long HW, fl
 int wgrad9_splits(int ntiles) { return ntiles < 128 ? ntiles : 128; }
 
 int wgrad_splits(long P, int tiles) {
-  // enough workgroups to fill 256 CUs twice, at least ~256 pixels per split
-  int s = (512 + tiles - 1) / tiles;
+  // as many splits as fit ONE round of 512 workgroup slots (256 CUs × 2): a grid just over 512
+  // (75 tiles × 7 = 525) would run a second round for 13 workgroups and double the time;
+  // at least ~256 pixels per split
+  int s = 512 / tiles;
   const long maxs = P / 256 > 1 ? P / 256 : 1;
   if (s > maxs) s = (int)maxs;
   if (s < 1) s = 1;
@@ -302,7 +298,7 @@ using namespace iclr17;
 
 extern "C" {
 
-int iclr17_sum_rows(const float* part, int T, int C, float* out, void* stream);
+int iclr17_sum_rows(const float* part, int T, int C, float* workspace, float* out, void* stream);
 
 size_t iclr17_wgrad_workspace_size(int kind, int B, int Ho, int Wo, int M, int C) {
   const long P = (long)B * Ho * Wo;
@@ -378,11 +374,21 @@ int iclr17_gdn_wgrad(const float* dn, const float* u, long P, int C, float* work
   return check_launch("gdn_wgrad_sum");
 }
 
-// out[c] = Σ_t part[t][c] (fixed order; T rows split over 4 thread groups, combined in order).
-int iclr17_sum_rows(const float* part, int T, int C, float* out, void* stream) {
-  ICLR17_REQUIRE(part && out && T > 0 && C > 0, ICLR17_EINVAL, "sum_rows: bad arguments");
-  hipLaunchKernelGGL(sum_rows_kernel, dim3((C + 63) / 64), dim3(256), 0, S(stream), part, T, C, out);
-  return check_launch("sum_rows");
+size_t iclr17_sum_rows_workspace_size(int C) { return (size_t)SUM_ROWS_SPLITS * C; }
+
+// out[c] = Σ_t part[t][c] (fixed order). workspace: iclr17_sum_rows_workspace_size(C) floats.
+int iclr17_sum_rows(const float* part, int T, int C, float* workspace, float* out, void* stream) {
+  ICLR17_REQUIRE(part && workspace && out && T > 0 && C > 0, ICLR17_EINVAL,
+                 "sum_rows: bad arguments");
+  const int per = (T + SUM_ROWS_SPLITS - 1) / SUM_ROWS_SPLITS;
+  const int ns = (T + per - 1) / per;
+  hipLaunchKernelGGL(sum_rows_kernel, dim3((C + 63) / 64, ns), dim3(256), 0, S(stream), part, T,
+                     C, per, workspace);
+  int rc = check_launch("sum_rows");
+  if (rc) return rc;
+  hipLaunchKernelGGL(sum_splits_kernel, dim3((C + 255) / 256), dim3(256), 0, S(stream), workspace,
+                     ns, (long)C, out);
+  return check_launch("sum_rows_splits");
 }
 
 // Bias gradient of a layer whose output gradient is NHWC [P][C]: db[c] = Σ_p G[p][c].
@@ -394,10 +400,10 @@ int iclr17_bias_grad_nhwc(const float* G, long P, int C, float* workspace, float
   hipLaunchKernelGGL(colsum_kernel, dim3((C + 255) / 256, 1024), dim3(256), 0, st, G, P, C, chunk, workspace);
   int rc = check_launch("bias_grad_nhwc");
   if (rc) return rc;
-  return iclr17_sum_rows(workspace, 1024, C, db, stream);
+  return iclr17_sum_rows(workspace, 1024, C, workspace + 1024L * C, db, stream);
 }
 
-// Bias gradient from an NCHW gradient [B][C][HW] (deconv3 output): workspace B*C floats.
+// Bias gradient from an NCHW gradient [B][C][HW] (deconv3 output): workspace (B + 64)*C floats.
 int iclr17_bias_grad_nchw(const float* G, int B, int C, long HW, float* workspace, float* db,
                           void* stream) {
   ICLR17_REQUIRE(B > 0 && C > 0 && HW > 0 && G && workspace && db, ICLR17_EINVAL, "bias_grad_nchw: bad arguments");
@@ -406,7 +412,7 @@ int iclr17_bias_grad_nchw(const float* G, int B, int C, long HW, float* workspac
   int rc = check_launch("bias_grad_nchw");
   if (rc) return rc;
   // part is [B][C] → sum over b for each c
-  return iclr17_sum_rows(workspace, B, C, db, stream);
+  return iclr17_sum_rows(workspace, B, C, workspace + (long)B * C, db, stream);
 }
 
 }  // extern "C"

@@ -488,7 +488,9 @@ def sum_rows(part: Tensor) -> Tensor:
     """Fixed-order column sums of a [T, C] float32 partial buffer."""
     T, C = part.shape
     out = torch.empty(C, device=part.device, dtype=torch.float32)
-    call("iclr17_sum_rows", _p(part), T, C, _p(out), _stream(part))
+    ws = torch.empty(query("iclr17_sum_rows_workspace_size", C), device=part.device,
+                     dtype=torch.float32)
+    call("iclr17_sum_rows", _p(part), T, C, _p(ws), _p(out), _stream(part))
     return out
 
 
@@ -593,7 +595,7 @@ def gdn_param_grads(dn: Tensor, u: Tensor, dbe: Tensor, beta: Tensor, gamma: Ten
 def bias_grad_nhwc(G: Tensor) -> Tensor:
     C = G.shape[-1]
     P = G.numel() // C
-    ws = torch.empty(1024 * C, device=G.device, dtype=torch.float32)
+    ws = torch.empty((1024 + 64) * C, device=G.device, dtype=torch.float32)
     db = torch.empty(C, device=G.device, dtype=torch.float32)
     call("iclr17_bias_grad_nhwc", _p(G.contiguous()), P, C, _p(ws), _p(db), _stream(G))
     return db
@@ -601,7 +603,7 @@ def bias_grad_nhwc(G: Tensor) -> Tensor:
 
 def bias_grad_nchw(G: Tensor) -> Tensor:
     B, C, H, W = G.shape
-    ws = torch.empty(B * C, device=G.device, dtype=torch.float32)
+    ws = torch.empty((B + 64) * C, device=G.device, dtype=torch.float32)
     db = torch.empty(C, device=G.device, dtype=torch.float32)
     call("iclr17_bias_grad_nchw", _p(G.contiguous()), B, C, H * W, _p(ws), _p(db), _stream(G))
     return db

@@ -248,7 +248,8 @@ int iclr17_bwd_conv_gdn(const float* g_u, int B, int h, int w, int N, const floa
  * gradient and Σ dn is ∂β_eff. kind 0 (bwd_deconv3_igdn with (H/4, W/4), bwd_deconv_igdn with
  * (h, w)), kind 1 (bwd_conv_gdn with (h, w)). Reduce them with iclr17_sum_rows. */
 int iclr17_bwd_tiles(int kind, int h, int w);
-int iclr17_sum_rows(const float* part, int T, int C, float* out, void* stream);
+int iclr17_sum_rows(const float* part, int T, int C, float* workspace, float* out, void* stream);
+size_t iclr17_sum_rows_workspace_size(int C);   /* floats */
 /* Weight gradients in PyTorch layout [m][c][kh][kw] (split-K, fixed-order reduction):
  * k5: G NHWC [B,Ho,Wo,M], X NHWC [B,2Ho,2Wo,C], kind 5 (k5 s2 p2) — conv2/conv3 (G=∂u, X=input)
  *     and deconv1/deconv2 (G=input, X=∂output);
@@ -269,7 +270,7 @@ int iclr17_gdn_param_chain(const float* beta, const float* gamma, const float* d
                            const float* dgamma_eff, int C, float beta_bound, float gamma_bound,
                            float* dbeta, float* dgamma, void* stream);
 /* Bias gradients: Σ over pixels of an NHWC [P][C] or NCHW [B][C][HW] gradient.
- * Workspace: 1024*C floats (NHWC), B*C floats (NCHW). */
+ * Workspace: (1024 + 64)*C floats (NHWC), (B + 64)*C floats (NCHW). */
 int iclr17_bias_grad_nhwc(const float* G, long P, int C, float* workspace, float* db, void* stream);
 int iclr17_bias_grad_nchw(const float* G, int B, int C, long HW, float* workspace, float* db,
                           void* stream);

@@ -184,6 +184,8 @@ def run_train(args, net, x, world, dev):
         "data": "synthetic (splitmix64 uint8/255 images, seeded trained-like weights)",
         "config": {"workload": f"train step, {B} x {S}x{S}x3 crops per GPU, N={args.N}, lambda=0.01",
                    "N": args.N, "batch_per_gpu": B, "global_batch": B * world,
+                   "precision": ("forward x6 (as eval), backward exact-f32" if kernels.precision() == "x6"
+                                 else "exact-f32"),
                    "parallelism": f"dp{world} (RCCL bucketed grad all-reduce)"},
         "roofline": {"bound": "mfma", "kernel": "whole training step", "achieved": round(tflops, 2),
                      "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",

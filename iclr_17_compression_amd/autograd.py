@@ -50,12 +50,20 @@ def needs_grad(x: Optional[Tensor], params: Sequence[Tensor]) -> bool:
 
 # ------------------------------------------------------------------------------ analysis
 def analysis_features_train(enc, x: Tensor):
-    """conv1+GDN1, conv2+GDN2 keeping the pre-activations the backward needs."""
+    """conv1+GDN1, conv2+GDN2 keeping the pre-activations the backward needs. In the x6 mode the
+    kernels also hand conv2 (and conv3) their input in split form; "a2s" is then set."""
     w1, w2, _, g1, g2 = enc.packed()
     N = enc.out_channel_N
+    if kernels.precision() == "x6":
+        e1, e2 = enc.gdn1.effective_params_x6(), enc.gdn2.effective_params_x6()
+        a1s, a1, u1 = kernels.conv1_gdn_x6(x, w1, enc.conv1.bias, e1[0], e1[1], N, want_f32=True,
+                                           want_pre=True, g6=e1[2])
+        a2s, a2, u2 = kernels.conv2_gdn_x6(a1s, w2, enc.conv2.bias, *e2, want_f32=True,
+                                           want_pre=True)
+        return a2, {"x": x, "u1": u1, "a1": a1, "u2": u2, "a2": a2, "a2s": a2s}
     a1, u1 = kernels.conv1_gdn(x, w1, enc.conv1.bias, g1[0], g1[1], N, want_pre=True)
     a2, u2 = kernels.conv2_gdn(a1, w2, enc.conv2.bias, g2[0], g2[1], want_pre=True)
-    return a2, {"x": x, "u1": u1, "a1": a1, "u2": u2, "a2": a2}
+    return a2, {"x": x, "u1": u1, "a1": a1, "u2": u2, "a2": a2, "a2s": None}
 
 
 def analysis_backward(enc, saved: Dict[str, Tensor], g_y: Tensor) -> Dict[str, Tensor]:
@@ -79,10 +87,20 @@ def analysis_backward(enc, saved: Dict[str, Tensor], g_y: Tensor) -> Dict[str, T
 
 
 # ----------------------------------------------------------------------------- synthesis
-def synthesis_forward_train(dec, y_nhwc: Tensor, x_ref: Optional[Tensor] = None):
+def synthesis_forward_train(dec, y_nhwc: Tensor, x_ref: Optional[Tensor] = None,
+                            y_split: Optional[Tensor] = None):
     d1, d2, d3, q1, q2 = dec.packed()
-    s1, v1 = kernels.deconv_igdn(y_nhwc, d1, dec.deconv1.bias, q1[0], q1[1], want_pre=True)
-    s2, v2 = kernels.deconv_igdn(s1, d2, dec.deconv2.bias, q2[0], q2[1], want_pre=True)
+    if kernels.precision() == "x6":
+        if y_split is None:
+            y_split = kernels.split_planes(y_nhwc)
+        e1, e2 = dec.igdn1.effective_params_x6(), dec.igdn2.effective_params_x6()
+        s1s, s1, v1 = kernels.deconv_igdn_x6(y_split, d1, dec.deconv1.bias, *e1, want_f32=True,
+                                             want_pre=True)
+        _, s2, v2 = kernels.deconv_igdn_x6(s1s, d2, dec.deconv2.bias, *e2, want_split=False,
+                                           want_f32=True, want_pre=True)
+    else:
+        s1, v1 = kernels.deconv_igdn(y_nhwc, d1, dec.deconv1.bias, q1[0], q1[1], want_pre=True)
+        s2, v2 = kernels.deconv_igdn(s1, d2, dec.deconv2.bias, q2[0], q2[1], want_pre=True)
     clipped, recon, sse = kernels.deconv3(s2, d3, dec.deconv3.bias, x_ref=x_ref, want_recon=True,
                                           sse_unclipped=x_ref is not None)
     return clipped, recon, sse, {"y": y_nhwc, "v1": v1, "s1": s1, "v2": v2, "s2": s2}
@@ -134,8 +152,13 @@ class CodecTrainFn(torch.autograd.Function):
         a2, saved_a = analysis_features_train(enc, x)
         _, _, w3, _, _ = enc.packed()
         rate = be.packed()
-        y_tilde, bits_part = kernels.conv3_quant_rate(a2, w3, rate, noise)
-        clipped, recon, sse_part, saved_s = synthesis_forward_train(dec, y_tilde, x_ref=x)
+        a2s = saved_a.pop("a2s")
+        if a2s is not None:
+            y_tilde, bits_part, _, y_split = kernels.conv3_quant_rate_x6(a2s, w3, rate, noise)
+        else:
+            (y_tilde, bits_part), y_split = kernels.conv3_quant_rate(a2, w3, rate, noise), None
+        clipped, recon, sse_part, saved_s = synthesis_forward_train(dec, y_tilde, x_ref=x,
+                                                                    y_split=y_split)
         _, bpp = kernels.reduce_partials(bits_part, 1.0 / (B * H * W), per_image=False)
         _, mse = kernels.reduce_partials(sse_part, 1.0 / (B * 3 * H * W), per_image=False)
         ctx.net = net
@@ -174,6 +197,7 @@ class AnalysisFn(torch.autograd.Function):
     def forward(ctx, x, enc, *params):
         ctx.set_materialize_grads(False)
         a2, saved = analysis_features_train(enc, x)
+        saved.pop("a2s")
         _, _, w3, _, _ = enc.packed()
         ctx.enc, ctx.saved = enc, saved
         return kernels.conv3(a2, w3).permute(0, 3, 1, 2)

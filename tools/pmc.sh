@@ -23,3 +23,4 @@ FETCH_SIZE
 WRITE_SIZE
 SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_LDS
 SETS
+exit 0

@@ -17,7 +17,7 @@ import sys
 # bench.py layer name → kernel (B=64 eval at 256², N=192: each name is unique in that run)
 LAYER_KERNELS = {
     "fp32": {
-        "conv1_gdn1": r"conv1_gdn_kernel<192, 0>",
+        "conv1_gdn1": r"conv1_gdn_kernel<192, 0, false>",
         "conv2_gdn2": r"engine_kernel<192, 192, 192, 1, 4, 0, false, false>",
         "conv3_quant_rate": r"engine_kernel<192, 192, 64, 1, 4, 2, false, false>",
         "deconv1_igdn1": r"engine_kernel<192, 192, 192, 1, 4, 1, false, false>",
@@ -25,7 +25,7 @@ LAYER_KERNELS = {
         "deconv3_clamp": r"engine_kernel<192, 48, 48, 4, 1, 3, false, false>",
     },
     "x6": {
-        "conv1_gdn1": r"conv1_gdn_kernel<192, 0>",
+        "conv1_gdn1": r"conv1_gdn_kernel<192, 0, true>",
         "conv2_gdn2": r"engine_kernel<192, 192, 192, 1, 4, 0, false, true>",
         "conv3_quant_rate": r"engine_kernel<192, 192, 64, 1, 4, 2, false, true>",
         "deconv1_igdn1": r"engine_kernel<192, 192, 192, 1, 4, 1, false, true>",

@@ -104,9 +104,9 @@ class Step:
             ev(3)
             hs, _, _ = kernels.deconv_igdn_x6(ys, d1, net.Decoder.deconv1.bias, *e3)
             ev(4)
-            _, h, _ = kernels.deconv_igdn_x6(hs, d2, net.Decoder.deconv2.bias, *e4,
-                                             want_split=False, want_f32=True)
+            hs, _, _ = kernels.deconv_igdn_x6(hs, d2, net.Decoder.deconv2.bias, *e4)
             ev(5)
+            clipped, _, _ = kernels.deconv3_x6(hs, d3, net.Decoder.deconv3.bias)
         else:
             h = kernels.conv1_gdn(self.x, w1, net.Encoder.conv1.bias, g1[0], g1[1], N)
             ev(1)
@@ -118,7 +118,7 @@ class Step:
             ev(4)
             h = kernels.deconv_igdn(h, d2, net.Decoder.deconv2.bias, q2[0], q2[1])
             ev(5)
-        clipped, _, _ = kernels.deconv3(h, d3, net.Decoder.deconv3.bias)
+            clipped, _, _ = kernels.deconv3(h, d3, net.Decoder.deconv3.bias)
         ev(6)
         _, bpp = kernels.reduce_partials(partial, self.scale, per_image=False)
         ev(7)
@@ -401,8 +401,8 @@ def main() -> None:
                    "N": N, "image": f"{S}x{S}x3", "batch_per_gpu": B, "global_batch": B * world,
                    "quant": "round",
                    "precision": ("x6: fp32 operands split exactly into 3 bf16 parts, 6 part products "
-                                 "on v_mfma_f32_16x16x32_bf16, fp32 accumulate (conv1/deconv3/GDN "
-                                 "contractions exact-f32)") if x6 else "fp32 (exact-f32 MFMA products)",
+                                 "on v_mfma_f32_16x16x32_bf16, fp32 accumulate (conv1's "
+                                 "contraction exact-f32)") if x6 else "fp32 (exact-f32 MFMA products)",
                    "parallelism": f"dp{world} (images sharded by rank, no data-path collective)"},
         "roofline": {"bound": "mfma", "kernel": dominant, "achieved": round(achieved, 2),
                      "peak": round(peak, 1), "unit": "TFLOP/s", "peak_basis": peak_note,

@@ -96,13 +96,15 @@ def synthesis_forward_train(dec, y_nhwc: Tensor, x_ref: Optional[Tensor] = None,
         e1, e2 = dec.igdn1.effective_params_x6(), dec.igdn2.effective_params_x6()
         s1s, s1, v1 = kernels.deconv_igdn_x6(y_split, d1, dec.deconv1.bias, *e1, want_f32=True,
                                              want_pre=True)
-        _, s2, v2 = kernels.deconv_igdn_x6(s1s, d2, dec.deconv2.bias, *e2, want_split=False,
-                                           want_f32=True, want_pre=True)
+        s2s, s2, v2 = kernels.deconv_igdn_x6(s1s, d2, dec.deconv2.bias, *e2, want_f32=True,
+                                             want_pre=True)
+        clipped, recon, sse = kernels.deconv3_x6(s2s, d3, dec.deconv3.bias, x_ref=x_ref,
+                                                 want_recon=True, sse_unclipped=x_ref is not None)
     else:
         s1, v1 = kernels.deconv_igdn(y_nhwc, d1, dec.deconv1.bias, q1[0], q1[1], want_pre=True)
         s2, v2 = kernels.deconv_igdn(s1, d2, dec.deconv2.bias, q2[0], q2[1], want_pre=True)
-    clipped, recon, sse = kernels.deconv3(s2, d3, dec.deconv3.bias, x_ref=x_ref, want_recon=True,
-                                          sse_unclipped=x_ref is not None)
+        clipped, recon, sse = kernels.deconv3(s2, d3, dec.deconv3.bias, x_ref=x_ref,
+                                              want_recon=True, sse_unclipped=x_ref is not None)
     return clipped, recon, sse, {"y": y_nhwc, "v1": v1, "s1": s1, "v2": v2, "s2": s2}
 
 

@@ -1020,6 +1020,192 @@ __global__ void __launch_bounds__(256, 2) engine_kernel_occ2(const EngineArgs a)
   engine_body<CI, CO, BN, WM, WN, EPI, PL, X6>(a);
 }
 
+// --------------------------------------------------------------- deconv3, x6 halo kernel
+// synthesis_17.py:23 deconv3 (ConvTranspose2d(N, 3, 9, s4, p4, op3)) + model.py:59 clamp, on the
+// x6 activation format. The all-phase GEMM of the engine (M = base pixels, N = 48 = 3 channels ×
+// 16 output phases, K = 9 taps × CI) with two changes that cut the bytes staged per MFMA:
+//   - a 16×16 base block per workgroup (M = 256; each wave 64 rows = 4 base rows × 16), so one
+//     6 KB weight stage feeds 4× the pixels of the 8×8 engine tile;
+//   - per 32-channel chunk, the 18×18 input patch (the block plus its 3×3 halo) is staged ONCE
+//     in LDS (three bf16 planes, 62 KB) and the 9 taps read shifted windows of it, instead of
+//     DMA-ing each tap's 64 rows again (324 vs 9·256 staged pixels).
+// Patch layout: slot = plane·324 + p (p = r·18 + c), 64 bytes per slot; 16-byte piece g of slot
+// p sits at g ^ 2·((p >> 2) & 1), conflict-free for ds_read_b128 lane groups at every window
+// offset (checked exhaustively). One A stage (single-buffered: the chunk boundary is a
+// barrier-bounded refill the co-resident workgroup covers) + two 6 KB B stages = 73 KB, two
+// workgroups per CU. Epilogue: bias, clamp, 64×64 output block through LDS, per-8×8-quadrant SSE
+// partials in the engine's partial layout (iclr17_output_partials_per_image).
+constexpr int D3_BS = 16;                       // base block side
+constexpr int D3_PS = D3_BS + 2;                // patch side
+constexpr int D3_PPX = D3_PS * D3_PS;           // 324 patch pixels per plane
+constexpr int D3_NAI = (3 * D3_PPX + 15) / 16;  // 61 A wave-instructions per chunk
+constexpr int D3_SA = D3_NAI * 256;             // A stage floats (976 slots × 16)
+constexpr int D3_SB = 32 * 48;                  // B stage floats
+constexpr int D3_LDS = D3_SA + 2 * D3_SB;
+
+template <int CI>
+__global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) {
+  constexpr int KCH = 32, NCH = CI / KCH, NSTEP = 9 * NCH;
+  constexpr int MT = 4, NT = 3;
+  constexpr int AI_W = (D3_NAI + 3) / 4;   // 16 (wave 0..3 takes i = w + 4j, i < 61)
+  static_assert(3 * 64 * 65 <= D3_LDS, "epilogue block fits the stages");
+  __shared__ __attribute__((aligned(16))) float smem[D3_LDS];
+  float* const sA = smem;
+  float* const sB = smem + D3_SA;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int bid = blockIdx.x;
+  const int tx = bid % a.tiles_x;
+  bid /= a.tiles_x;
+  const int ty = bid % a.tiles_y;
+  const int b = bid / a.tiles_y;
+
+  // A DMA sources: per instruction j of this wave, slot q = 16i + lane/4 (plane, patch pixel),
+  // physical piece lane & 3 ← logical piece (lane & 3) ^ swizzle(p). -1: zero line.
+  int asrc[AI_W];
+#pragma unroll
+  for (int j = 0; j < AI_W; ++j) {
+    const int i = wave + 4 * j;
+    const int q = i * 16 + (lane >> 2);
+    const int pl = q / D3_PPX, p = q - pl * D3_PPX;
+    const int r = p / D3_PS, c = p - r * D3_PS;
+    const int iy = ty * D3_BS - 1 + r, ix = tx * D3_BS - 1 + c;
+    const bool ok = i < D3_NAI && pl < 3 && (unsigned)iy < (unsigned)a.Hin &&
+                    (unsigned)ix < (unsigned)a.Win;
+    const int g = (lane & 3) ^ (((p >> 2) & 1) << 1);
+    asrc[j] = ok ? (iy * a.Win + ix) * CI + g * 8 : -1;
+  }
+  const unsigned short* __restrict__ inb = a.in_split + (long)b * a.Hin * a.Win * CI;
+  auto issue_a = [&](int cc) {
+#pragma unroll
+    for (int j = 0; j < AI_W; ++j) {
+      const int i = wave + 4 * j;
+      if (i < D3_NAI) {
+        const int q = i * 16 + (lane >> 2);
+        const int pl = q / D3_PPX;
+        const unsigned short* src = inb + (long)(pl < 3 ? pl : 0) * a.in_plane + asrc[j] + cc * KCH;
+        glds16(asrc[j] >= 0 ? (const float*)src : g_zero16, sA + i * 256);
+      }
+    }
+  };
+  auto issue_b = [&](int s, int buf) {
+    const int cc = s / 9, tap = s - cc * 9;
+    const float* __restrict__ ws = a.w + ((long)tap * CI + cc * KCH) * 48 + lane * 4;
+    glds16(ws + wave * 256, sB + buf * D3_SB + wave * 256);
+    if (wave < 2) glds16(ws + (wave + 4) * 256, sB + buf * D3_SB + (wave + 4) * 256);
+  };
+
+  f4 acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4;
+  const int prow = (4 * wave + 1) * D3_PS + 1 + (lane & 15);   // window origin for mt = 0
+  const int boff = (2 * g * 48 + (lane & 15)) * 4;
+
+  auto compute = [&](int buf, int tap) {
+    const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+    const float* sb = sB + buf * D3_SB + boff;
+    bf8 Bh[NT], Bm[NT], Bl[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      u4 bh, bm, bl;
+      split8(*(const f4*)(sb + nt * 64), *(const f4*)(sb + 48 * 4 + nt * 64), bh, bm, bl);
+      Bh[nt] = __builtin_bit_cast(bf8, bh);
+      Bm[nt] = __builtin_bit_cast(bf8, bm);
+      Bl[nt] = __builtin_bit_cast(bf8, bl);
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int p = prow + (mt + dy) * D3_PS + dx;
+      const unsigned short* sa =
+          (const unsigned short*)(sA + p * 16 + ((g ^ (((p >> 2) & 1) << 1)) * 4));
+      const bf8 Ah = __builtin_bit_cast(bf8, *(const u4*)(sa));
+      const bf8 Am = __builtin_bit_cast(bf8, *(const u4*)(sa + D3_PPX * 32));
+      const bf8 Al = __builtin_bit_cast(bf8, *(const u4*)(sa + 2 * D3_PPX * 32));
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        f4 c = acc[mt][nt];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al, Bh[nt], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bl[nt], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bm[nt], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bh[nt], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bm[nt], c, 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bh[nt], c, 0, 0, 0);
+      }
+    }
+  };
+
+  issue_a(0);
+  issue_b(0, 0);
+  for (int s = 0; s < NSTEP; ++s) {
+    __syncthreads();   // vmcnt(0) + barrier: A (at a chunk start) and B of step s landed
+    const int tap = s - (s / 9) * 9;
+    if (s + 1 < NSTEP && tap != 8) issue_b(s + 1, (s + 1) & 1);
+    compute(s & 1, tap);
+    if (tap == 8 && s + 1 < NSTEP) {
+      __syncthreads();   // every wave is done with this chunk's patch
+      issue_a((s + 1) / 9);
+      issue_b(s + 1, (s + 1) & 1);
+    }
+  }
+  __syncthreads();     // stage reads done before the epilogue reuses LDS
+
+  // epilogue: column n = co·16 + ry·4 + rx of row m = (by, bx) → output (4by + ry, 4bx + rx)
+  constexpr int OS = 4 * D3_BS, SS = OS + 1;
+  float* sO = smem;   // [3][64][65]
+  const int H = a.Hout, W = a.Wout;
+  float sse = 0.f;
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass == 1 && a.recon == nullptr) break;
+    float* dst = pass == 0 ? a.out : a.recon;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int by = 4 * wave + mt, bx = 4 * g + r;
+          const int ph = lane & 15;
+          float v = acc[mt][nt][r] + a.bias[nt];
+          if (pass == 0) v = fminf(fmaxf(v, 0.0f), 1.0f);
+          sO[(nt * OS + by * 4 + (ph >> 2)) * SS + bx * 4 + (ph & 3)] = v;
+        }
+    __syncthreads();
+    // wave w stores output quadrant (qy, qx) = (w >> 1, w & 1): 3 × 32 rows × 8 float4
+    const int qy = wave >> 1, qx = wave & 1;
+    const bool sse_pass = pass == (a.sse_unclipped ? 1 : 0) && a.xref != nullptr;
+    for (int k = lane; k < 3 * 32 * 8; k += 64) {
+      const int c4 = k & 7, row = (k >> 3) & 31, co = k >> 8;
+      const int oyl = qy * 32 + row, oxl = qx * 32 + c4 * 4;
+      const int oy = ty * OS + oyl, ox = tx * OS + oxl;
+      if (oy >= H || ox >= W) continue;
+      const float* sp = sO + (co * OS + oyl) * SS + oxl;
+      const f4 v = f4{sp[0], sp[1], sp[2], sp[3]};
+      const long off = (((long)b * 3 + co) * H + oy) * W + ox;
+      *(f4*)(dst + off) = v;
+      if (sse_pass) {
+        const f4 xr = *(const f4*)(a.xref + off);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = v[e] - xr[e];
+          sse += d * d;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (a.xref != nullptr) {
+    sse = wave_sum(sse);
+    const int ty8 = 2 * ty + (wave >> 1), tx8 = 2 * tx + (wave & 1);
+    const int tiles_x8 = (a.gw + 7) / 8;
+    if (lane == 0 && ty8 * 8 < a.gh && tx8 * 8 < a.gw)
+      a.partial[(long)b * a.partials_per_image + ty8 * tiles_x8 + tx8] = (double)sse;
+  }
+}
+
 // ------------------------------------------------------------------------------ conv1 kernel
 // Conv2d(3, N, 9, stride 4, pad 4) on the NCHW image with GDN fused. The 37×37×3 input patch of
 // an 8×8 output block is staged once in LDS; K = 243 = (c, kh, kw) padded to 256, each A element
@@ -1563,6 +1749,37 @@ int iclr17_synthesis_deconv_igdn(const float* in, int B, int h, int w, int N,
                  "deconv_igdn: null pointer");
   return N == 192 ? launch_deconv5<192>(in, B, h, w, w_packed, bias, beta_eff, gamma_packed, out, pre_out, S(stream))
                   : launch_deconv5<128>(in, B, h, w, w_packed, bias, beta_eff, gamma_packed, out, pre_out, S(stream));
+}
+
+int iclr17_synthesis_deconv3_x6(const uint16_t* in_split, int B, int H, int W, int N,
+                                const float* w_packed, const float* bias, const float* x,
+                                float* clipped, float* recon, double* sse_partial,
+                                int sse_unclipped, void* stream) {
+  int rc = check_dims(B, H, W, N);
+  if (rc) return rc;
+  ICLR17_REQUIRE(in_split && w_packed && bias && clipped, ICLR17_EINVAL,
+                 "deconv3_x6: null pointer");
+  ICLR17_REQUIRE(x == nullptr || sse_partial != nullptr, ICLR17_EINVAL,
+                 "deconv3_x6: sse_partial required with x");
+  ICLR17_REQUIRE(!sse_unclipped || recon != nullptr, ICLR17_EINVAL,
+                 "deconv3_x6: the unclipped SSE needs the recon output");
+  EngineArgs a;
+  memset(&a, 0, sizeof(a));
+  a.sse_unclipped = sse_unclipped;
+  a.in_split = (const unsigned short*)in_split;
+  a.w = w_packed; a.bias = bias; a.out = clipped; a.recon = recon; a.xref = x;
+  a.partial = sse_partial;
+  a.B = B; a.Hin = H / 4; a.Win = W / 4; a.Hout = H; a.Wout = W;
+  a.gh = H / 4; a.gw = W / 4;
+  a.in_plane = (long)B * a.Hin * a.Win * N;
+  a.tiles_y = (a.gh + D3_BS - 1) / D3_BS; a.tiles_x = (a.gw + D3_BS - 1) / D3_BS;
+  a.partials_per_image = ((a.gh + 7) / 8) * ((a.gw + 7) / 8);
+  dim3 grid(a.tiles_x * a.tiles_y * B);
+  if (N == 192)
+    hipLaunchKernelGGL((deconv3_x6_kernel<192>), grid, dim3(256), 0, S(stream), a);
+  else
+    hipLaunchKernelGGL((deconv3_x6_kernel<128>), grid, dim3(256), 0, S(stream), a);
+  return check_launch("deconv3_x6");
 }
 
 int iclr17_output_partials_per_image(int H, int W) {

@@ -376,6 +376,29 @@ def deconv3(h: Tensor, wp: Tensor, bias: Tensor, x_ref: Optional[Tensor] = None,
     return clipped, recon, partial
 
 
+def deconv3_x6(hs: Tensor, wp: Tensor, bias: Tensor, x_ref: Optional[Tensor] = None,
+               want_recon: bool = False, sse_unclipped: bool = False):
+    """deconv3 on a split-form input [3,B,H/4,W/4,N] (the halo-tiled x6 kernel); the same
+    returns as ``deconv3``."""
+    _check_split(hs, "activation")
+    _, B, h4, w4, N = hs.shape
+    _check_channels(N)
+    H, W = 4 * h4, 4 * w4
+    _check_image_dims(H, W)
+    clipped = torch.empty(B, 3, H, W, device=hs.device, dtype=torch.float32)
+    recon = torch.empty_like(clipped) if want_recon else None
+    partial = None
+    if x_ref is not None:
+        _check(x_ref, "reference image", 4)
+        if tuple(x_ref.shape) != (B, 3, H, W):
+            raise Iclr17Error("iclr17: reference image shape mismatch")
+        x_ref = x_ref.contiguous()
+        partial = torch.empty(B, output_partials_per_image(H, W), device=hs.device, dtype=torch.float64)
+    call("iclr17_synthesis_deconv3_x6", _p(hs), B, H, W, N, _p(wp), _p(bias), _p(x_ref),
+         _p(clipped), _p(recon), _p(partial), int(sse_unclipped), _stream(hs))
+    return clipped, recon, partial
+
+
 def reduce_partials(partial: Tensor, scale: float = 1.0, per_image: bool = True):
     """Deterministic per-image sums (float64 [B]) and scale·Σ (float32 0-dim)."""
     _check_f64(partial)

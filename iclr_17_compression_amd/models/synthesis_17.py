@@ -55,13 +55,14 @@ class Synthesis_net_17(nn.Module):
 
     def decode(self, y_nhwc, x_ref=None, want_recon=True, y_split=None):
         """NHWC latent → (clipped NCHW, unclipped NCHW | None, SSE partials | None).
-        With ``y_split`` (the latent in x6 split form) deconv1/deconv2 run in the x6 mode."""
+        With ``y_split`` (the latent in x6 split form) the three layers run in the x6 mode."""
         d1, d2, d3, g1, g2 = self.packed()
         if y_split is not None:
             q1, q2 = self.igdn1.effective_params_x6(), self.igdn2.effective_params_x6()
             hs, _, _ = kernels.deconv_igdn_x6(y_split, d1, self.deconv1.bias, *q1)
-            _, h, _ = kernels.deconv_igdn_x6(hs, d2, self.deconv2.bias, *q2,
-                                             want_split=False, want_f32=True)
+            hs, _, _ = kernels.deconv_igdn_x6(hs, d2, self.deconv2.bias, *q2)
+            return kernels.deconv3_x6(hs, d3, self.deconv3.bias, x_ref=x_ref,
+                                      want_recon=want_recon)
         else:
             h = kernels.deconv_igdn(y_nhwc, d1, self.deconv1.bias, g1[0], g1[1])
             h = kernels.deconv_igdn(h, d2, self.deconv2.bias, g2[0], g2[1])

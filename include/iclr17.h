@@ -124,7 +124,7 @@ int iclr17_output_partials_per_image(int H, int W);
  * mid·hi, hi·lo, mid·mid, lo·hi — the dropped terms are below 2^-24 of the product), with
  * fp32 accumulation. Activations travel between layers in "split form": three bf16 planes
  * [3][B][h][w][N] (uint16 bf16 bits, plane stride B·h·w·N), written by the producing layer's
- * epilogue. conv1 (3-channel NCHW image) and deconv3 keep exact-f32 products. out / out_split
+ * epilogue. conv1 (3-channel NCHW image) keeps exact-f32 products. out / out_split
  * are each nullable, not both. The GDN/IGDN channel contraction runs in x6 as well when given
  * gamma_split (required by conv2/deconv; nullable for conv1: then exact-f32). */
 /* x[n] (n % 8 == 0) → planes[3][n]. */
@@ -156,6 +156,12 @@ int iclr17_synthesis_deconv_igdn_x6(const uint16_t* in_split, int B, int h, int 
                                     const float* beta_eff, const float* gamma_packed,
                                     const uint16_t* gamma_split, float* out, uint16_t* out_split,
                                     float* pre_out, void* stream);
+/* iclr17_synthesis_deconv3 on a split-form input (the same outputs and sse_partial layout:
+ * iclr17_output_partials_per_image(H, W) doubles per image). */
+int iclr17_synthesis_deconv3_x6(const uint16_t* in_split, int B, int H, int W, int N,
+                                const float* w_packed, const float* bias, const float* x,
+                                float* clipped, float* recon, double* sse_partial,
+                                int sse_unclipped, void* stream);
 
 /* testKodak's MS-SSIM (train.py:178 → models/ms_ssim_torch.py:123-196): per-image
  * ms_ssim(x, y, data_range) of NCHW [B,3,H,W] fp32 images, 11-tap σ=1.5 window, 5 levels (each

@@ -120,6 +120,41 @@ def test_x6_layers(device, N):
         assert rel_err(s2, nhwc(r_s2)) < REL
 
 
+@pytest.mark.parametrize("N", [192, 128])
+@pytest.mark.parametrize("shape", [(2, 64, 96), (1, 80, 112), (1, 256, 256)])
+def test_deconv3_x6(device, N, shape):
+    """The halo-tiled x6 deconv3 (16×16 base blocks, partial blocks at 80/112) against the
+    oracle from the oracle's input: clipped / unclipped output and the per-8×8-tile SSE
+    partials (both SSE modes) in the fp32 kernel's layout."""
+    B, H, W = shape
+    net, sd = net_for(N, 1, device), sd_for(N, 1)
+    F = torch.nn.functional
+    d3 = net.Decoder.packed()[2]
+    s2 = torch.from_numpy(synth.normal_like(21, (B, N, H // 4, W // 4), 0.6))
+    x = image(12, B, H, W)
+    with torch.no_grad():
+        r_out = F.conv_transpose2d(s2, sd["Decoder.deconv3.weight"], sd["Decoder.deconv3.bias"],
+                                   stride=4, padding=4, output_padding=3)
+        hs = kernels.split_planes(nhwc(s2).contiguous().to(device))
+        xd = x.to(device)
+        for unclipped in (False, True):
+            clipped, recon, part = kernels.deconv3_x6(hs, d3, net.Decoder.deconv3.bias, x_ref=xd,
+                                                      want_recon=True, sse_unclipped=unclipped)
+            assert rel_err(recon, r_out) < REL
+            assert rel_err(clipped, r_out.clamp(0, 1)) < REL
+            assert part.shape == (B, kernels.output_partials_per_image(H, W))
+            per, _ = kernels.reduce_partials(part)
+            ref = ((r_out if unclipped else r_out.clamp(0, 1)) - x.double()).pow(2).sum((1, 2, 3))
+            assert rel_err(per, ref) < METRIC_REL
+            # tile for tile against the fp32 kernel's partials
+            _, _, part32 = kernels.deconv3(nhwc(s2).contiguous().to(device), d3,
+                                           net.Decoder.deconv3.bias, x_ref=xd, want_recon=True,
+                                           sse_unclipped=unclipped)
+            assert rel_err(part, part32) < 1e-4
+        c2, r2, p2 = kernels.deconv3_x6(hs, d3, net.Decoder.deconv3.bias)
+        assert r2 is None and p2 is None and torch.equal(c2, clipped)
+
+
 # ------------------------------------------------------------------------------------ layers
 @pytest.mark.parametrize("N", [192, 128])
 def test_analysis_layers(device, N):

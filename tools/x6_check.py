@@ -21,6 +21,8 @@ torch.manual_seed(0)
 a1 = torch.randn(B, 64, 64, N, device=dev) * 0.5
 s1 = torch.randn(B, 32, 32, N, device=dev) * 0.5
 a1s, s1s = kernels.split_planes(a1), kernels.split_planes(s1)
+s2 = torch.randn(B, 64, 64, N, device=dev) * 0.3
+s2s = kernels.split_planes(s2)
 e2 = net.Encoder.gdn2.effective_params_x6()
 q2x = net.Decoder.igdn2.effective_params_x6()
 assert torch.equal(kernels.merge_planes(a1s), a1), "split not exact"
@@ -81,17 +83,28 @@ def numerics():
                                        want_f32=True)
     print("deconv2_igdn fp32:", err(f32, rd))
     print("deconv2_igdn x6  :", err(x6f, rd))
+    d = net.Decoder
+    r3 = F.conv_transpose2d(s2[:nb].permute(0, 3, 1, 2).double(), d.deconv3.weight.double(),
+                            d.deconv3.bias.double(), 4, 4, 3)
+    _, f32, _ = kernels.deconv3(s2[:nb].contiguous(), d3, d.deconv3.bias, want_recon=True)
+    _, x6r, _ = kernels.deconv3_x6(kernels.split_planes(s2[:nb].contiguous()), d3, d.deconv3.bias,
+                                   want_recon=True)
+    print("deconv3 fp32:", err(f32, r3))
+    print("deconv3 x6  :", err(x6r, r3))
 
 
 def timings():
     fl2 = 2.0 * B * (32 * 32 * N * N * 25 + 32 * 32 * N * N)
     fld = 2.0 * B * (32 * 32 * N * N * 25 + 64 * 64 * N * N)
+    fl3 = 2.0 * B * 64 * 64 * N * 3 * 81
     t = {
         "conv2 fp32": (timeit(lambda: kernels.conv2_gdn(a1, w2, net.Encoder.conv2.bias, g2[0], g2[1])), fl2),
         "conv2 x6": (timeit(lambda: kernels.conv2_gdn_x6(a1s, w2, net.Encoder.conv2.bias, *e2)), fl2),
         "deconv2 fp32": (timeit(lambda: kernels.deconv_igdn(s1, d2, net.Decoder.deconv2.bias, q2[0], q2[1])), fld),
         "deconv2 x6": (timeit(lambda: kernels.deconv_igdn_x6(s1s, d2, net.Decoder.deconv2.bias, *q2x,
                                                              want_split=False, want_f32=True)), fld),
+        "deconv3 fp32": (timeit(lambda: kernels.deconv3(s2, d3, net.Decoder.deconv3.bias)), fl3),
+        "deconv3 x6": (timeit(lambda: kernels.deconv3_x6(s2s, d3, net.Decoder.deconv3.bias)), fl3),
     }
     print(TAG, " ".join(f"{k}={v[0]:.3f}ms({v[1] / v[0] / 1e9:.1f}TF)" for k, v in t.items()), flush=True)
 

@@ -34,7 +34,9 @@
 namespace iclr17 {
 
 // Diagnostic ablation builds only (tools/ablate.sh, tools/ab.sh): -DICLR17_ABL=mask — 8 skips
-// the engine epilogue, 16 replaces conv1's patch gather by constants, 32 skips conv1's epilogue
+// the engine epilogue, 16 replaces conv1's patch gather by constants, 32 skips conv1's epilogue,
+// 64 / 128 skip the engine's A / B operand DMA after the first two steps, 256 replaces the x6 B
+// split by one pack, 512 makes the x6 A pieces contiguous (all: wrong values, timing only)
 #ifndef ICLR17_ABL
 #define ICLR17_ABL 0
 #endif
@@ -851,13 +853,19 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
     const int dy = (td & 0xff) - 128, dx = ((td >> 8) & 0xff) - 128;
     const int so = (dy * a.Win + dx) * CI + cc * KCH;
     float* sa = smem + buf * STAGE;
+    const bool skip_a = (ICLR17_ABL & 64) && s > 1, skip_b = (ICLR17_ABL & 128) && s > 1;
 #pragma unroll
     for (int j = 0; j < AI_W; ++j) {
+      if (skip_a) break;
       const bool ok = rval[j] && (unsigned)(iy0[j] + dy) < (unsigned)a.Hin &&
                       (unsigned)(ix0[j] + dx) < (unsigned)a.Win;
       const int i = wave * AI_W + j;
       if constexpr (X6) {
         const unsigned short* src = inb6 + (i >> 2) * a.in_plane + pbase[j] + so;
+        if (ICLR17_ABL & 512) {   // within [image start, this lane's valid pixel] of the plane
+          const int e = pbase[j] + so, base = (e & ~511) >= 512 ? (e & ~511) - 512 : 0;
+          src = inb6 + (i >> 2) * a.in_plane + base + (e >= 512 ? lane * 8 : 0);
+        }
         glds16(ok ? (const float*)src : g_zero16, sa + i * 256);
       } else {
         glds16(ok ? inb + pbase[j] + so : g_zero16, sa + i * 256);
@@ -868,6 +876,7 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
 #pragma unroll
     for (int j = 0; j < BI_W; ++j) {
       const int i = wave + 4 * j;
+      if (skip_b) break;
       if (NBI % 4 == 0 || i < NBI) glds16(ws + bsrc[j], sb + i * 256);
     }
   };
@@ -900,7 +909,16 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       u4 bh, bm, bl;
-      split8(*(const f4*)(sb + nt * 64), *(const f4*)(sb + BN * 4 + nt * 64), bh, bm, bl);
+      if (ICLR17_ABL & 256) {
+        const f4 x0 = *(const f4*)(sb + nt * 64), x1 = *(const f4*)(sb + BN * 4 + nt * 64);
+        bh = u4{__builtin_amdgcn_perm(__float_as_uint(x0[1]), __float_as_uint(x0[0]), 0x07060302u),
+                __builtin_amdgcn_perm(__float_as_uint(x0[3]), __float_as_uint(x0[2]), 0x07060302u),
+                __builtin_amdgcn_perm(__float_as_uint(x1[1]), __float_as_uint(x1[0]), 0x07060302u),
+                __builtin_amdgcn_perm(__float_as_uint(x1[3]), __float_as_uint(x1[2]), 0x07060302u)};
+        bm = bh ^ 1u;
+        bl = bh ^ 2u;
+      } else
+        split8(*(const f4*)(sb + nt * 64), *(const f4*)(sb + BN * 4 + nt * 64), bh, bm, bl);
       Bh[nt] = __builtin_bit_cast(bf8, bh);
       Bm[nt] = __builtin_bit_cast(bf8, bm);
       Bl[nt] = __builtin_bit_cast(bf8, bl);

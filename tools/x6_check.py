@@ -23,6 +23,7 @@ s1 = torch.randn(B, 32, 32, N, device=dev) * 0.5
 a1s, s1s = kernels.split_planes(a1), kernels.split_planes(s1)
 s2 = torch.randn(B, 64, 64, N, device=dev) * 0.3
 s2s = kernels.split_planes(s2)
+x0 = torch.rand(B, 3, 256, 256, device=dev)
 e2 = net.Encoder.gdn2.effective_params_x6()
 q2x = net.Decoder.igdn2.effective_params_x6()
 assert torch.equal(kernels.merge_planes(a1s), a1), "split not exact"
@@ -97,7 +98,11 @@ def timings():
     fl2 = 2.0 * B * (32 * 32 * N * N * 25 + 32 * 32 * N * N)
     fld = 2.0 * B * (32 * 32 * N * N * 25 + 64 * 64 * N * N)
     fl3 = 2.0 * B * 64 * 64 * N * 3 * 81
+    fl1 = 2.0 * B * 64 * 64 * (N * 243 + N * N)
+    e1 = net.Encoder.gdn1.effective_params_x6()
     t = {
+        "conv1 x6": (timeit(lambda: kernels.conv1_gdn_x6(x0, w1, net.Encoder.conv1.bias, g1[0], g1[1], N,
+                                                         g6=e1[2])), fl1),
         "conv2 fp32": (timeit(lambda: kernels.conv2_gdn(a1, w2, net.Encoder.conv2.bias, g2[0], g2[1])), fl2),
         "conv2 x6": (timeit(lambda: kernels.conv2_gdn_x6(a1s, w2, net.Encoder.conv2.bias, *e2)), fl2),
         "deconv2 fp32": (timeit(lambda: kernels.deconv_igdn(s1, d2, net.Decoder.deconv2.bias, q2[0], q2[1])), fld),

@@ -255,6 +255,71 @@ def run_kodak(args, dev):
     }
 
 
+def run_codec(args, dev):
+    """§8 f4: the codec with a REAL bitstream. One step = analysis + round (fused kernels) →
+    rANS encode of ŷ (+ stream offsets, pack) → rANS decode → synthesis + clamp; the bitstream
+    stays in HBM. Reports the entropy-coder kernels' own rates and the real vs the estimated
+    (reference model.py:71-78) bits."""
+    N, S, B = args.N, args.size, args.batch
+    net = ImageCompressor(out_channel_N=N)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in synth.trained_like_state_dict(N, 1).items()})
+    net = net.to(dev).eval()
+    x = torch.from_numpy(synth.to_unit_float(synth.image_u8(0, B, S, S))).to(dev)
+    cum = net.bitEstimator.entropy_tables()
+    h = w = S // 16
+    t_enc, t_dec = [], []
+
+    def step(timed=False):
+        q = net.encode_latents(x)
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        e0.record()
+        words, offsets = kernels.rans_encode(q["y_hat"], cum)
+        e1.record()
+        y = kernels.rans_decode(words, offsets, cum, B, h, w, N)
+        e2.record()
+        split = kernels.split_planes(y) if kernels.precision() == "x6" else None
+        clipped, _, _ = net.Decoder.decode(y, want_recon=False, y_split=split)
+        if timed:
+            t_enc.append((e0, e1))
+            t_dec.append((e1, e2))
+        return q, words, y, clipped
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            q, words, y, _ = step(timed=True)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        if not torch.equal(y, q["y_hat"]):
+            raise SystemExit("codec bench: decoded latents differ from the encoded ones")
+        bits, _ = kernels.reduce_partials(q["bits_partial"])
+    enc_ms = sorted(a.elapsed_time(b) for a, b in t_enc)[len(t_enc) // 2]
+    dec_ms = sorted(a.elapsed_time(b) for a, b in t_dec)[len(t_dec) // 2]
+    syms = B * h * w * N
+    real_bits = 16.0 * words.numel() + 32.0 * B * kernels.STREAMS_PER_IMAGE   # + the length header
+    est_bits = float(bits.sum().item())
+    return {
+        "metric": "Mpixels/s encode+decode through a real rANS bitstream (SURVEY 8f row 4)",
+        "value": round(B * S * S * args.steps / elapsed / 1e6, 2), "unit": "Mpix/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32 transforms, u32 rANS state",
+        "data": "synthetic (splitmix64 uint8/255 images, seeded trained-like weights)",
+        "config": {"workload": f"image -> bitstream -> image, {B} x {S}x{S}x3, N={N}",
+                   "precision": kernels.precision(), "K": kernels.ENTROPY_K,
+                   "streams_per_image": kernels.STREAMS_PER_IMAGE},
+        "entropy_coder": {"encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
+                          "encode_Msym_per_s": round(syms / enc_ms / 1e3, 1),
+                          "decode_Msym_per_s": round(syms / dec_ms / 1e3, 1),
+                          "real_bpp": round(real_bits / (B * S * S), 5),
+                          "estimated_bpp": round(est_bits / (B * S * S), 5),
+                          "real_over_estimated": round(real_bits / est_bits, 5)},
+    }
+
+
 def cpu_baseline(N: int, H: int, W: int, budget_s: float) -> dict:
     """The oracle (op-for-op restatement of the reference forward, bit-identical to it on the
     build host) timed on this host's cores on a bounded sample."""
@@ -304,7 +369,7 @@ def main() -> None:
     ap.add_argument("--N", type=int, default=192)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", choices=("eval", "train", "kodak"), default="eval")
+    ap.add_argument("--mode", choices=("eval", "train", "kodak", "codec"), default="eval")
     ap.add_argument("--precision", choices=kernels.PRECISIONS, default=None,
                     help="inference contraction mode (default: ICLR17_PRECISION or x6)")
     args = ap.parse_args()
@@ -319,9 +384,10 @@ def main() -> None:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
-    if args.mode == "kodak":
+    if args.mode in ("kodak", "codec"):
         if rank == 0:
-            print(json.dumps(run_kodak(args, dev)), flush=True)
+            run = run_kodak if args.mode == "kodak" else run_codec
+            print(json.dumps(run(args, dev)), flush=True)
         return
     N, S, B = args.N, args.size, args.batch
     net = ImageCompressor(out_channel_N=N)

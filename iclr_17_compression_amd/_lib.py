@@ -63,6 +63,12 @@ SIGNATURES = {
     "iclr17_reduce_partials": (_I, [_P, _I, _I, _P, _P, _D, _P]),
     "iclr17_resized_crop_batch": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P]),
     "iclr17_adam_step": (_I, [_P, _I, ctypes.c_long, _D, _D, _D, _D, ctypes.c_long, _F, _P]),
+    "iclr17_entropy_tables": (_I, [_P, _I, _I, _P, _P]),
+    "iclr17_rans_capacity": (ctypes.c_long, [_I, _I, _I, _I]),
+    "iclr17_rans_encode": (_I, [_P, _I, _I, _I, _I, _I, _P, _I, _P, ctypes.c_long, _P, _P, _P]),
+    "iclr17_rans_offsets": (_I, [_P, _I, _P, _P]),
+    "iclr17_rans_pack": (_I, [_P, ctypes.c_long, _P, _I, _P, _P]),
+    "iclr17_rans_decode": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P]),
     "iclr17_ms_ssim_workspace_size": (_SZ, [_I, _I, _I]),
     "iclr17_ms_ssim": (_I, [_P, _P, _I, _I, _I, _F, _P, _SZ, _P, _P]),
     "iclr17_gdn": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),

@@ -399,6 +399,78 @@ def deconv3_x6(hs: Tensor, wp: Tensor, bias: Tensor, x_ref: Optional[Tensor] = N
     return clipped, recon, partial
 
 
+# ---------------------------------------------------------------- entropy coding (§8 f4)
+ENTROPY_K = 32            # symbols −K..K per channel (+ escape for larger |ŷ|)
+STREAMS_PER_IMAGE = 1     # rANS streams per image (contiguous channel groups; 64 states each)
+
+
+def entropy_tables(rate_packed: Tensor, N: int, K: int = ENTROPY_K) -> Tensor:
+    """Quantised per-channel CDFs of the factorised model: int32 [N, 2K + 3]."""
+    _check(rate_packed, "rate table")
+    if rate_packed.numel() != 11 * N:
+        raise Iclr17Error(f"iclr17: entropy_tables: rate table is not [11][{N}]")
+    cum = torch.empty(N, 2 * K + 3, device=rate_packed.device, dtype=torch.int32)
+    call("iclr17_entropy_tables", _p(rate_packed), N, K, _p(cum), _stream(rate_packed))
+    return cum
+
+
+def _rans_status(status: Tensor, what: str) -> None:
+    st = int(status.item())
+    if st:
+        why = []
+        if st & 1:
+            why.append("a latent is not integer-valued (or NaN)")
+        if st & 2:
+            why.append("|latent| > 32767")
+        if st & 4:
+            why.append("a stream ran past its words")
+        if st & 8:
+            why.append("a stream did not end in the initial state")
+        raise Iclr17Error(f"iclr17: {what}: " + "; ".join(why))
+
+
+def rans_encode(y_hat: Tensor, cum: Tensor, K: int = ENTROPY_K,
+                streams_per_image: int = STREAMS_PER_IMAGE):
+    """ŷ NHWC [B,h,w,N] → (words int16 [T] (uint16 bit patterns), offsets int64 [B·P + 1]);
+    stream b·P + g holds channels g·N/P .. of image b."""
+    _check(y_hat, "latent", 4)
+    B, h, w, N = y_hat.shape
+    P = streams_per_image
+    cap = query("iclr17_rans_capacity", h, w, N, P)
+    if cap <= 0:
+        raise Iclr17Error(f"iclr17: rans_encode: N={N} not divisible into {P} streams")
+    dev = y_hat.device
+    scratch = torch.empty(B * P * cap, device=dev, dtype=torch.int16)
+    lengths = torch.empty(B * P, device=dev, dtype=torch.int32)
+    status = torch.zeros(1, device=dev, dtype=torch.int32)
+    st = _stream(y_hat)
+    call("iclr17_rans_encode", _p(y_hat.contiguous()), B, h, w, N, P, _p(cum), K, _p(scratch),
+         scratch.numel(), _p(lengths), _p(status), st)
+    offsets = torch.empty(B * P + 1, device=dev, dtype=torch.int64)
+    call("iclr17_rans_offsets", _p(lengths), B * P, _p(offsets), st)
+    total = int(offsets[-1].item())
+    words = torch.empty(max(total, 1), device=dev, dtype=torch.int16)
+    call("iclr17_rans_pack", _p(scratch), cap, _p(offsets), B * P, _p(words), st)
+    _rans_status(status, "rans_encode")
+    return words[:total], offsets
+
+
+def rans_decode(words: Tensor, offsets: Tensor, cum: Tensor, B: int, h: int, w: int, N: int,
+                K: int = ENTROPY_K, streams_per_image: int = STREAMS_PER_IMAGE) -> Tensor:
+    """Inverse of rans_encode → ŷ NHWC fp32 [B,h,w,N]."""
+    P = streams_per_image
+    if offsets.numel() != B * P + 1 or N % P:
+        raise Iclr17Error("iclr17: rans_decode: offsets do not match B x streams_per_image")
+    dev = cum.device
+    y = torch.empty(B, h, w, N, device=dev, dtype=torch.float32)
+    status = torch.zeros(1, device=dev, dtype=torch.int32)
+    words = words.contiguous() if words.numel() else torch.zeros(1, device=dev, dtype=torch.int16)
+    call("iclr17_rans_decode", _p(words), _p(offsets.contiguous()), B, h, w, N, P, _p(cum), K,
+         _p(y), _p(status), _stream(y))
+    _rans_status(status, "rans_decode")
+    return y
+
+
 def reduce_partials(partial: Tensor, scale: float = 1.0, per_image: bool = True):
     """Deterministic per-image sums (float64 [B]) and scale·Σ (float32 0-dim)."""
     _check_f64(partial)

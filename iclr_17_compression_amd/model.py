@@ -63,8 +63,20 @@ class ImageCompressor(nn.Module):
             want_y: bool = False) -> Dict[str, torch.Tensor]:
         """The fused forward. Returns a dict with ``clipped`` (NCHW), ``y_hat`` (NHWC), bits
         partials and, on request, per-image SSE partials (vs x) and the unclipped recon."""
-        kernels._check(x, "image", 4)
         training = self.training if training is None else training
+        x = x.contiguous()
+        q = self.encode_latents(x, noise, training, want_y)
+        y_hat, bits_partial, y_split = q["y_hat"], q["bits_partial"], q["y_split"]
+        clipped, recon, sse_partial = self.Decoder.decode(y_hat, x_ref=x if x_ref_sse else None,
+                                                          want_recon=want_recon, y_split=y_split)
+        return {"clipped": clipped, "y_hat": y_hat, "bits_partial": bits_partial,
+                "sse_partial": sse_partial, "recon": recon, "y": q["y"]}
+
+    def encode_latents(self, x: torch.Tensor, noise: Optional[torch.Tensor] = None,
+                       training: bool = False, want_y: bool = False) -> Dict[str, torch.Tensor]:
+        """The analysis half of ``run``: conv1+GDN → conv2+GDN → conv3+quantise+rate. Returns
+        ``y_hat`` (NHWC), the bits partials, ``y_split`` (x6 split form, or None) and ``y``."""
+        kernels._check(x, "image", 4)
         if training and noise is None:
             noise = self._latent_noise(x)
         if not training:
@@ -84,11 +96,8 @@ class ImageCompressor(nn.Module):
             h = kernels.conv2_gdn(h, w2, self.Encoder.conv2.bias, g2[0], g2[1])
             q = kernels.conv3_quant_rate(h, w3, self.bitEstimator.packed(), noise, want_y=want_y)
             y_split = None
-        y_hat, bits_partial = q[0], q[1]
-        clipped, recon, sse_partial = self.Decoder.decode(y_hat, x_ref=x if x_ref_sse else None,
-                                                          want_recon=want_recon, y_split=y_split)
-        return {"clipped": clipped, "y_hat": y_hat, "bits_partial": bits_partial,
-                "sse_partial": sse_partial, "recon": recon, "y": q[2] if want_y else None}
+        return {"y_hat": q[0], "bits_partial": q[1], "y_split": y_split,
+                "y": q[2] if want_y else None}
 
     def forward(self, input_image, noise: Optional[torch.Tensor] = None):
         """model.py:47-80 → (clipped_recon, ŷ or ỹ, bpp). In training mode with autograd on, the
@@ -119,6 +128,54 @@ class ImageCompressor(nn.Module):
         (clipped_recon, mse of the UNclipped recon (model.py:61), bpp), all differentiable."""
         clipped, _, bpp, mse = self._train_outputs(input_image, noise, list(self.parameters()))
         return clipped, mse, bpp
+
+    # ------------------------------------------------------------- entropy coding (§8 f4)
+    @torch.no_grad()
+    def compress(self, x: torch.Tensor, streams_per_image: int = kernels.STREAMS_PER_IMAGE,
+                 K: int = kernels.ENTROPY_K) -> Dict[str, object]:
+        """Encode images to byte strings: the analysis transform, rounding, then rANS over the
+        factorised BitEstimator (the model the reference uses only to estimate bpp). Per image:
+        P little-endian uint32 stream word counts, then the stream words (uint16 LE).
+        Returns {"strings": [bytes] * B, "shape": (h, w), "streams_per_image": P, "K": K}."""
+        y_hat = self.encode_latents(x)["y_hat"]
+        B, h, w, N = y_hat.shape
+        P = streams_per_image
+        words, offsets = kernels.rans_encode(y_hat, self.bitEstimator.entropy_tables(K), K, P)
+        off = offsets.cpu().numpy()
+        wv = words.cpu().numpy().view("<u2")
+        strings = []
+        for b in range(B):
+            o = off[b * P:(b + 1) * P + 1]
+            strings.append(np.diff(o).astype("<u4").tobytes() + wv[o[0]:o[-1]].tobytes())
+        return {"strings": strings, "shape": (h, w), "streams_per_image": P, "K": K}
+
+    @torch.no_grad()
+    def decompress(self, strings, shape, streams_per_image: int = kernels.STREAMS_PER_IMAGE,
+                   K: int = kernels.ENTROPY_K, device=None) -> Dict[str, torch.Tensor]:
+        """Inverse of ``compress``: byte strings → {"y_hat": NCHW latents, "x_hat": the clipped
+        reconstruction} (bit-identical latents; the synthesis as in ``forward``)."""
+        P, N = streams_per_image, self.out_channel_N
+        h, w = shape
+        device = device or next(self.parameters()).device
+        counts, payload = [], []
+        for sbytes in strings:
+            head = np.frombuffer(sbytes[:4 * P], dtype="<u4")
+            if head.size != P:
+                raise kernels.Iclr17Error("iclr17: decompress: truncated stream header")
+            body = np.frombuffer(sbytes[4 * P:], dtype="<u2")
+            if body.size != int(head.sum()):
+                raise kernels.Iclr17Error("iclr17: decompress: stream lengths do not match the payload")
+            counts.append(head.astype(np.int64))
+            payload.append(body)
+        B = len(strings)
+        off = np.concatenate([[0], np.cumsum(np.concatenate(counts))]).astype(np.int64)
+        words = torch.from_numpy(np.concatenate(payload).view(np.int16).copy()).to(device)
+        offsets = torch.from_numpy(off).to(device)
+        y_hat = kernels.rans_decode(words, offsets, self.bitEstimator.entropy_tables(K), B, h, w, N,
+                                    K, P)
+        split = kernels.split_planes(y_hat) if kernels.precision() == "x6" else None
+        clipped, _, _ = self.Decoder.decode(y_hat, want_recon=False, y_split=split)
+        return {"y_hat": y_hat.permute(0, 3, 1, 2), "x_hat": clipped}
 
     @torch.no_grad()
     def evaluate(self, x: torch.Tensor, want_y: bool = False,

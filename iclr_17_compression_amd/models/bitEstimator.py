@@ -49,6 +49,13 @@ class BitEstimator(nn.Module):
         ps = self.params_in_order()
         return self._pack.get("rate", ps, lambda: kernels.pack_rate(ps), force=force or self.training)
 
+    def entropy_tables(self, K: int = kernels.ENTROPY_K):
+        """Quantised CDFs for the entropy coder (cached like the packed parameters)."""
+        ps = self.params_in_order()
+        return self._pack.get(f"cdf{K}", ps,
+                              lambda: kernels.entropy_tables(self.packed(), self.channel, K),
+                              force=self.training)
+
     def forward(self, x):
         # bitEstimator.py:38-42
         from ..autograd import no_backward

@@ -163,6 +163,37 @@ int iclr17_synthesis_deconv3_x6(const uint16_t* in_split, int B, int H, int W, i
                                 float* clipped, float* recon, double* sse_partial,
                                 int sse_unclipped, void* stream);
 
+/* ---------------------------------------------------------------- entropy coding (§8 f4)
+ * A real bitstream for ŷ with the factorised model the reference only uses to ESTIMATE the rate
+ * (model.py:71-78 / bitEstimator.py). Per channel c, symbols v ∈ [−K, K] plus an escape (the
+ * value then follows as one uniform 16-bit symbol, |v| ≤ 32767); frequencies quantised to 16
+ * bits from F_c(v ± ½) (the rate kernel's own CDF evaluation). Interleaved rANS: 64 32-bit
+ * states per stream (state l owns symbols l, l + 64, …), 16-bit words ordered by lane within
+ * each block of 64 symbols; each image's channels are cut into P contiguous groups ("streams",
+ * N % P == 0), symbols in (channel, row, column) order; one wave per stream. A stream is its 64
+ * final states (128 words) followed by the renormalisation words (oracle/rans_ref.py spells
+ * out the order). */
+/* cum: int32 [N][2K + 3] cumulative frequencies (cum[c][2K + 2] = 65536). */
+int iclr17_entropy_tables(const float* rate_packed, int N, int K, int32_t* cum, void* stream);
+/* Words of per-stream scratch: 128 + 2·(N/P)·h·w (0: bad arguments). */
+long iclr17_rans_capacity(int h, int w, int N, int streams_per_image);
+/* ŷ NHWC [B][h][w][N] (integer-valued fp32) → each stream's words at the END of its scratch
+ * slot s·capacity (s = b·P + group), its word count in lengths[s]. status |= 1 non-integer or
+ * NaN, 2 |v| > 32767 (int32 on the device, caller-zeroed). */
+int iclr17_rans_encode(const float* y_hat, int B, int h, int w, int N, int streams_per_image,
+                       const int32_t* cum, int K, uint16_t* scratch, long scratch_words,
+                       uint32_t* lengths, int32_t* status, void* stream);
+/* offsets[0] = 0, offsets[i + 1] = offsets[i] + lengths[i] (int64 [n + 1]). */
+int iclr17_rans_offsets(const uint32_t* lengths, int n, int64_t* offsets, void* stream);
+/* Concatenate the n streams: words[offsets[s] .. offsets[s + 1]) = stream s. */
+int iclr17_rans_pack(const uint16_t* scratch, long capacity, const int64_t* offsets, int n,
+                     uint16_t* words, void* stream);
+/* Inverse of encode + pack → ŷ NHWC. status |= 4 a stream ran past its words, 8 a stream did
+ * not end in the encoder's initial state with every word consumed (corrupt input). */
+int iclr17_rans_decode(const uint16_t* words, const int64_t* offsets, int B, int h, int w, int N,
+                       int streams_per_image, const int32_t* cum, int K, float* y_hat,
+                       int32_t* status, void* stream);
+
 /* testKodak's MS-SSIM (train.py:178 → models/ms_ssim_torch.py:123-196): per-image
  * ms_ssim(x, y, data_range) of NCHW [B,3,H,W] fp32 images, 11-tap σ=1.5 window, 5 levels (each
  * level must be ≥ 11×11: H, W ≥ 161 or so), the reference's level weights and final product.

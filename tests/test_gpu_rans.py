@@ -1,0 +1,113 @@
+"""Entropy coder on the GPU against the oracle restatement (oracle/rans_ref.py):
+tables from the same factorised model, bitstreams word for word (given the GPU's tables),
+round trips at full size, corrupt-input detection, and compress/decompress through the model.
+The reference has no coder (it only estimates bits, model.py:71-78); the size check ties the
+real bitstream to that estimate."""
+import numpy as np
+import pytest
+import torch
+
+from iclr_17_compression_amd import kernels, synth
+from iclr_17_compression_amd.model import ImageCompressor
+from oracle import codec_ref as oracle
+from oracle import rans_ref
+
+pytestmark = pytest.mark.gpu
+K = kernels.ENTROPY_K
+
+
+def net_for(N, seed, device):
+    net = ImageCompressor(out_channel_N=N)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in synth.trained_like_state_dict(N, seed).items()})
+    return net.to(device).eval()
+
+
+def image(seed, B, H, W):
+    return torch.from_numpy(synth.to_unit_float(synth.image_u8(seed, B, H, W)))
+
+
+@pytest.mark.parametrize("N", [192, 128])
+def test_tables_match_oracle(device, N):
+    net = net_for(N, 1, device)
+    cum = net.bitEstimator.entropy_tables().cpu().numpy()
+    sd = oracle.state_dict_to_torch(synth.trained_like_state_dict(N, 1))
+    ref = rans_ref.tables_from_cdf(rans_ref.boundary_cdf(sd, N, K), K)
+    assert cum.shape == ref.shape
+    assert (cum[:, -1] == 65536).all() and (np.diff(cum, axis=1) >= 1).all()
+    # the CDF is evaluated with the GPU's expf/tanhf vs torch's: a frequency may move by one
+    # where p·(2^16 − 66) lands next to an integer; at most a handful of entries
+    diff = np.abs(cum - ref)
+    assert diff.max() <= 2 and (diff > 0).sum() <= max(4, N // 16)
+
+
+@pytest.mark.parametrize("N,P", [(192, 16), (128, 4), (192, 1)])
+def test_bitstream_matches_oracle(device, N, P):
+    net = net_for(N, 1, device)
+    with torch.no_grad():
+        y_hat = net.run(image(7, 2, 64, 96).to(device), training=False)["y_hat"].clone()
+    y_hat[0, 0, 0, :4] = torch.tensor([K + 1.0, -K - 1.0, 1000.0, -32767.0])   # escapes
+    y_hat[1, 3, 5, N - 1] = 32767.0
+    cum = net.bitEstimator.entropy_tables()
+    words, offsets = kernels.rans_encode(y_hat, cum, K, P)
+    ref_w, ref_o = rans_ref.encode(y_hat.cpu().numpy(), cum.cpu().numpy(), K, P)
+    assert np.array_equal(offsets.cpu().numpy(), ref_o)
+    assert np.array_equal(words.cpu().numpy().view(np.uint16), ref_w)
+    back = kernels.rans_decode(words, offsets, cum, 2, 4, 6, N, K, P)
+    assert torch.equal(back, y_hat)
+
+
+def test_round_trip_full_size(device):
+    """B=16 of 256² (C3-sized latents) plus wide-range values: decode(encode(ŷ)) == ŷ."""
+    N = 192
+    net = net_for(N, 2, device)
+    cum = net.bitEstimator.entropy_tables()
+    y = torch.from_numpy(np.round(synth.normal_like(9, (16, 16, 16, N), 3.0))).to(device)
+    y[3] = torch.from_numpy(np.round(synth.uniform(10, (16, 16, N), -300, 300))).to(device)
+    words, offsets = kernels.rans_encode(y, cum)
+    assert torch.equal(kernels.rans_decode(words, offsets, cum, 16, 16, 16, N), y)
+    z = torch.zeros(2, 16, 16, N, device=device)
+    words, offsets = kernels.rans_encode(z, cum)
+    assert torch.equal(kernels.rans_decode(words, offsets, cum, 2, 16, 16, N), z)
+
+
+def test_bad_input_and_corrupt_streams_fail_loudly(device):
+    N = 128
+    cum = net_for(N, 1, device).bitEstimator.entropy_tables()
+    y = torch.zeros(1, 4, 4, N, device=device)
+    y[0, 1, 1, 3] = 0.5
+    with pytest.raises(kernels.Iclr17Error, match="integer"):
+        kernels.rans_encode(y, cum)
+    y[0, 1, 1, 3] = 40000.0
+    with pytest.raises(kernels.Iclr17Error, match="32767"):
+        kernels.rans_encode(y, cum)
+    y = torch.from_numpy(np.round(synth.normal_like(4, (1, 4, 4, N), 2.0))).to(device)
+    words, offsets = kernels.rans_encode(y, cum)
+    with pytest.raises(kernels.Iclr17Error, match="stream"):
+        kernels.rans_decode(words[:-1], torch.clamp(offsets, max=words.numel() - 1), cum, 1, 4, 4, N)
+
+
+@pytest.mark.parametrize("precision", ["x6", "fp32"])
+def test_compress_decompress(device, precision):
+    old = kernels.precision()
+    kernels.set_precision(precision)
+    try:
+        N = 192
+        net = net_for(N, 1, device)
+        x = image(8, 3, 64, 96).to(device)
+        with torch.no_grad():
+            clipped, y_hat, _ = net(x)
+            ev = net.evaluate(x)
+        enc = net.compress(x)
+        assert len(enc["strings"]) == 3 and enc["shape"] == (4, 6)
+        dec = net.decompress(enc["strings"], enc["shape"])
+        assert torch.equal(dec["y_hat"], y_hat)
+        assert torch.equal(dec["x_hat"], clipped)
+        # real size vs the reference's estimate: the 16-bit frequency tables cost a little,
+        # each stream adds its 64 32-bit final states, each image a 4-byte length per stream
+        P = enc["streams_per_image"]
+        est = ev["bpp"].cpu().numpy() * 64 * 96
+        real = np.array([8 * len(s) for s in enc["strings"]], dtype=np.float64)
+        assert (real >= 0.97 * est).all()
+        assert (real <= 1.03 * est + P * (64 * 32 + 32 + 16)).all()
+    finally:
+        kernels.set_precision(old)

@@ -84,6 +84,7 @@ class Step:
         self.enc = net.Encoder.packed()
         self.dec = net.Decoder.packed()
         self.rate = net.bitEstimator.packed()
+        self.w1x6 = net.Encoder.packed_conv1_x6()
         self.g6 = [m.effective_params_x6() for m in (net.Encoder.gdn1, net.Encoder.gdn2,
                                                       net.Decoder.igdn1, net.Decoder.igdn2)]
 
@@ -95,8 +96,8 @@ class Step:
         ev(0)
         if kernels.precision() == "x6":
             e1, e2, e3, e4 = self.g6
-            hs, _, _ = kernels.conv1_gdn_x6(self.x, w1, net.Encoder.conv1.bias, e1[0], e1[1], N,
-                                            g6=e1[2])
+            hs, _, _ = kernels.conv1x6_gdn(self.x, self.w1x6, net.Encoder.conv1.bias, e1[0], e1[2],
+                                           N)
             ev(1)
             hs, _, _ = kernels.conv2_gdn_x6(hs, w2, net.Encoder.conv2.bias, *e2)
             ev(2)

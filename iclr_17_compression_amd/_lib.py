@@ -27,6 +27,7 @@ ICLR17_W_CONV1 = 0
 ICLR17_W_CONV5 = 1
 ICLR17_W_DECONV5 = 2
 ICLR17_W_DECONV9 = 3
+ICLR17_W_CONV1_X6 = 4
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -55,6 +56,7 @@ SIGNATURES = {
     "iclr17_split_planes": (_I, [_P, ctypes.c_long, _P, _P]),
     "iclr17_split_packed": (_I, [_P, _I, _I, _I, _P, _P]),
     "iclr17_analysis_conv1_gdn_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_analysis_conv1x6_gdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_analysis_conv2_gdn_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_analysis_conv3_quant_rate_x6": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P,
                                                  _P, _P]),

@@ -56,8 +56,8 @@ def analysis_features_train(enc, x: Tensor):
     N = enc.out_channel_N
     if kernels.precision() == "x6":
         e1, e2 = enc.gdn1.effective_params_x6(), enc.gdn2.effective_params_x6()
-        a1s, a1, u1 = kernels.conv1_gdn_x6(x, w1, enc.conv1.bias, e1[0], e1[1], N, want_f32=True,
-                                           want_pre=True, g6=e1[2])
+        a1s, a1, u1 = kernels.conv1x6_gdn(x, enc.packed_conv1_x6(), enc.conv1.bias, e1[0], e1[2],
+                                          N, want_f32=True, want_pre=True)
         a2s, a2, u2 = kernels.conv2_gdn_x6(a1s, w2, enc.conv2.bias, *e2, want_f32=True,
                                            want_pre=True)
         return a2, {"x": x, "u1": u1, "a1": a1, "u2": u2, "a2": a2, "a2s": a2s}

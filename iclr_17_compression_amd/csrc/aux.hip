@@ -26,6 +26,24 @@ __global__ void pack_conv1_kernel(const float* __restrict__ w, float* __restrict
   out[i] = k < 243 ? w[(long)n * 243 + k] : 0.f;
 }
 
+// conv1 [N][3][9][9] → [64 quads][N][4] in the x6 kernel's k order (engine_fp32.hip,
+// conv1_x6_kernel): k' = 8g + e; g < 27: (c, kh) = (g / 9, g % 9), kw = e; g = 27: zero;
+// g ≥ 28: pair (g − 28)·8 + e (< 27, else zero), kw = 8.
+__global__ void pack_conv1_x6_kernel(const float* __restrict__ w, float* __restrict__ out, int N) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 256 * N) return;
+  const int e4 = i & 3, n = (i >> 2) % N, q = (i >> 2) / N;
+  const int k = 4 * q + e4, g = k >> 3, e = k & 7;
+  int src = -1;
+  if (g < 27) {
+    src = g * 9 + e;
+  } else if (g >= 28) {
+    const int p = (g - 28) * 8 + e;
+    if (p < 27) src = p * 9 + 8;
+  }
+  out[i] = src >= 0 ? w[(long)n * 243 + src] : 0.f;
+}
+
 // conv k5 [co][ci][5][5] → [25 taps][ci/4][co][4], tap = kh·5 + kw.
 __global__ void pack_conv5_kernel(const float* __restrict__ w, float* __restrict__ out, int N) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -270,7 +288,8 @@ extern "C" {
 
 size_t iclr17_packed_weight_size(int which, int N) {
   switch (which) {
-    case ICLR17_W_CONV1: return (size_t)256 * N;
+    case ICLR17_W_CONV1:
+    case ICLR17_W_CONV1_X6: return (size_t)256 * N;
     case ICLR17_W_CONV5:
     case ICLR17_W_DECONV5: return (size_t)25 * N * N;
     case ICLR17_W_DECONV9: return (size_t)9 * N * 48;
@@ -287,6 +306,7 @@ int iclr17_pack_weight(int which, const float* w, float* packed, int N, void* st
   hipStream_t st = S(stream);
   switch (which) {
     case ICLR17_W_CONV1: hipLaunchKernelGGL(pack_conv1_kernel, grid, dim3(256), 0, st, w, packed, N); break;
+    case ICLR17_W_CONV1_X6: hipLaunchKernelGGL(pack_conv1_x6_kernel, grid, dim3(256), 0, st, w, packed, N); break;
     case ICLR17_W_CONV5: hipLaunchKernelGGL(pack_conv5_kernel, grid, dim3(256), 0, st, w, packed, N); break;
     case ICLR17_W_DECONV5: {
       TapList tl;

@@ -43,6 +43,18 @@ namespace iclr17 {
 
 constexpr int BM = 64;        // output pixels per tile
 
+#ifndef ICLR17_CONV3_BN
+#define ICLR17_CONV3_BN 96    // conv3 (+ quantiser) output columns per workgroup
+#endif
+#ifndef ICLR17_QSTAGES
+#define ICLR17_QSTAGES 2      // conv3's DMA ring depth (3, 4 measured slower: DESIGN.md §5)
+#endif
+#ifndef ICLR17_PL_MIN
+#define ICLR17_PL_MIN 512     // deconv base tiles from which one workgroup runs all 4 phases
+#endif
+static_assert(ICLR17_QSTAGES >= 2 && ICLR17_QSTAGES <= 4, "conv3 ring depth");
+constexpr int conv3_bn(int N) { return N % ICLR17_CONV3_BN == 0 ? ICLR17_CONV3_BN : 64; }
+
 enum Epi : int {
   EPI_GDN = 0, EPI_IGDN = 1, EPI_QUANT = 2, EPI_OUT3 = 3, EPI_PLAIN = 4,
   EPI_GDN_BWD = 5, EPI_IGDN_BWD = 6, EPI_RATE_BWD = 7
@@ -278,6 +290,17 @@ __device__ __forceinline__ void chan_gemm(f4 (&acc)[MT][NT], const float* sX,
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) g[nt] = gn[nt];
   }
+}
+
+// s_waitcnt vmcnt(N) (exp/lgkm counters untouched) + workgroup barrier; the empty asm statements
+// keep the compiler from moving LDS accesses across it.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_barrier() {
+  static_assert(N >= 0 && N < 64, "vmcnt field");
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 
 // Zero source for glds lanes whose tap falls outside the image (padding).
@@ -787,7 +810,10 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   constexpr int NBI = SB * 4 / 1024;             // B glds wave-instructions per step
   constexpr int AI_W = NAI / 4;                  // per wave
   constexpr int BI_W = (NBI + 3) / 4;
-  constexpr int LDS_A = 2 * STAGE;
+  // DMA ring depth: conv3 (+ quantiser) has a third of conv2's MFMAs per step, too few to hide
+  // an L2-miss DMA issued one step ahead, so it runs NS stages with a counted vmcnt wait.
+  constexpr int NS = (EPI == EPI_QUANT && X6) ? ICLR17_QSTAGES : 2;
+  constexpr int LDS_A = NS * STAGE;
   constexpr int LDS_X = (EPI == EPI_GDN || EPI == EPI_IGDN || EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD)
                             ? BM * (CO + 8) + GSTAGE_FLOATS(CO) : 0;
   constexpr int LDS_O = BM * (BN + 4) + 8;
@@ -798,8 +824,9 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   static_assert(MT * WM * 16 == BM && NT * WN * 16 == BN, "tile shape");
   static_assert(WM * WN == 4, "4 waves");
   static_assert(CI % KCH == 0 && NAI % 4 == 0, "k-step split");
-  static_assert(BN == CO || BN == 64, "B image: whole rows, or one 1 KB piece per quad row");
+  static_assert(BN == CO || BN % 16 == 0, "B image: quad rows of BN columns");
   static_assert((SB * 4) % 1024 == 0, "B image in whole wave-instructions");
+  static_assert(NS == 2 || NBI % 4 == 0, "counted vmcnt: equal DMA count per wave");
   __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -835,7 +862,8 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
 #pragma unroll
   for (int j = 0; j < BI_W; ++j) {
     const int i = wave + 4 * j;
-    bsrc[j] = (BN == CO) ? i * 256 + lane * 4 : (i * CO + t.nb * BN) * 4 + lane * 4;
+    const int o = i * 256 + lane * 4;   // offset in the LDS image [8 quads][BN][4]
+    bsrc[j] = (BN == CO) ? o : ((o / (BN * 4)) * CO + t.nb * BN) * 4 + o % (BN * 4);
   }
 
   int t0 = 0, ntaps = 1;
@@ -971,10 +999,30 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
     for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
 
   issue(0, 0);
-  for (int s = 0; s < nsteps; ++s) {
-    __syncthreads();   // vmcnt(0) + barrier: step s landed for every wave; stage (s+1)&1 is free
-    if (s + 1 < nsteps) issue(s + 1, (s + 1) & 1);
-    compute(s & 1);
+  if constexpr (NS == 2) {
+    for (int s = 0; s < nsteps; ++s) {
+      __syncthreads();   // vmcnt(0) + barrier: step s landed for every wave; stage (s+1)&1 is free
+      if (s + 1 < nsteps) issue(s + 1, (s + 1) & 1);
+      compute(s & 1);
+    }
+  } else {
+    // NS-stage ring: steps s+1 .. s+NS-2 stay in flight while step s is waited for (each wave
+    // issues exactly AI_W + BI_W DMA instructions per step, and nothing else touches vmcnt).
+    constexpr int PER = AI_W + BI_W;
+#pragma unroll
+    for (int j = 1; j < NS - 1; ++j)
+      if (j < nsteps) issue(j, j);
+    int buf = 0;
+    for (int s = 0; s < nsteps; ++s) {
+      const int ahead = nsteps - 1 - s < NS - 2 ? nsteps - 1 - s : NS - 2;   // steps in flight
+      if (ahead >= 2) wait_vmcnt_barrier<2 * PER>();
+      else if (ahead == 1) wait_vmcnt_barrier<PER>();
+      else wait_vmcnt_barrier<0>();
+      // every wave is past compute(s-1): its stage, (s + NS - 1) % NS, is free
+      if (s + NS - 1 < nsteps) issue(s + NS - 1, buf == 0 ? NS - 1 : buf - 1);
+      compute(buf);
+      buf = buf + 1 == NS ? 0 : buf + 1;
+    }
   }
   __syncthreads();     // last stage reads done before the epilogue reuses LDS
   if (ICLR17_ABL & 8) {   // diagnostic: keep the accumulators live, skip the epilogue
@@ -1361,6 +1409,184 @@ __global__ void __launch_bounds__(256) conv1_gdn_kernel(const EngineArgs a) {
   }
 }
 
+// ------------------------------------------------------------------- conv1, x6 contraction
+// conv1 + GDN1 with both contractions in x6 (analysis_17.py:14-17). The 37×37×3 patch arrives
+// by LDS-DMA as before and is then split once into three bf16 planes [3][3·37][40] in LDS, so
+// the main loop does no splitting. K is reordered so that a lane's 8-deep k-group is 8
+// consecutive patch columns of one row: k' = 8g + e with
+//   g < 27      : (c, kh) = (g / 9, g % 9), kw = e           — one 16-byte read per plane
+//   g = 27      : zero weights (the lane reads a valid row; 0 · finite = 0)
+//   g = 28 .. 31: pair (g − 28)·8 + e (zero weights past 26), kw = 8 — gathered element-wise
+// (packing ICLR17_W_CONV1_X6, then iclr17_split_packed). The weights' split planes
+// [3][32][CO][8] are read from L2 one step ahead, like the x6 GDN γ: no B image in LDS, and no
+// barrier in the main loop.
+constexpr int P1U = 3 * P1 * P1RS;        // u16 elements per split plane (4440)
+
+template <int CO>
+__global__ void __launch_bounds__(256) conv1_x6_kernel(const EngineArgs a) {
+  constexpr int WN = 4;
+  constexpr int MT = BM / 16;
+  constexpr int NT = CO / WN / 16;
+  constexpr int S_FLOATS = 3 * P1U / 2;                 // split planes (6660 floats)
+  constexpr int LDS_P = S_FLOATS + P1NI * 256;          // + the fp32 DMA landing area
+  constexpr int LDS_X = BM * (CO + 8);
+  constexpr int LDS_FLOATS = LDS_P > LDS_X ? LDS_P : LDS_X;
+  __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
+  unsigned short* sp = (unsigned short*)smem;
+  float* sr = smem + S_FLOATS;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = 0, wn = wave;
+  const TileInfo t = decode_tile(a);
+  const int ncol0 = wn * (CO / WN);
+  const int H = a.Hin, W = a.Win;
+  const int iy0 = t.ty * 32 - 4, ix0 = t.tx * 32 - 4;
+
+  // Patch by LDS-DMA into the landing area (pieces as in conv1_gdn_kernel).
+#pragma unroll
+  for (int j = 0; j < (P1NI + 3) / 4; ++j) {
+    const int i = wave + 4 * j;
+    if (i < P1NI) {
+      const int pc = i * 64 + lane;
+      const int cr = pc / 10, q = pc - cr * 10;
+      const int c = cr / P1, r = cr - c * P1;
+      const int iy = iy0 + r, ix = ix0 + 4 * q;
+      const bool ok = pc < P1PIECES && iy >= 0 && iy < H && ix >= 0 && ix < W;
+      glds16(ok ? a.in + (((long)t.b * 3 + c) * H + iy) * W + ix : g_zero16, sr + i * 256);
+    }
+  }
+  // Weight planes: lane's B fragment base (k-group lane >> 4, column ncol0 + lane & 15).
+  constexpr long GP = 32L * CO * 8;                     // plane stride (u16)
+  const unsigned short* gb = (const unsigned short*)a.w + ((lane >> 4) * CO + ncol0 + (lane & 15)) * 8;
+  u4 b0[3][NT], b1[3][NT];
+  auto loadb = [&](int s, u4 (&b)[3][NT]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        b[p][nt] = *(const u4*)(gb + p * GP + (long)s * 4 * CO * 8 + nt * 128);
+  };
+  loadb(0, b0);
+  __syncthreads();   // patch landed
+
+  // Split pass: piece pc (4 floats at column 4q of row cr) → 4 bf16 in each plane.
+  for (int pc = tid; pc < P1PIECES; pc += 256) {
+    const f4 x = *(const f4*)(sr + pc * 4);
+    unsigned h[4], m[4], l[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      h[i] = __float_as_uint(x[i]) & 0xffff0000u;
+      const float r = x[i] - __uint_as_float(h[i]);
+      m[i] = __float_as_uint(r) & 0xffff0000u;
+      l[i] = __float_as_uint(r - __uint_as_float(m[i]));
+    }
+    const int o = pc * 4;   // u16 offset (row stride 40 = 10 pieces)
+    *(uint2*)(sp + o) = uint2{__builtin_amdgcn_perm(h[1], h[0], 0x07060302u),
+                              __builtin_amdgcn_perm(h[3], h[2], 0x07060302u)};
+    *(uint2*)(sp + P1U + o) = uint2{__builtin_amdgcn_perm(m[1], m[0], 0x07060302u),
+                                    __builtin_amdgcn_perm(m[3], m[2], 0x07060302u)};
+    *(uint2*)(sp + 2 * P1U + o) = uint2{__builtin_amdgcn_perm(l[1], l[0], 0x07060302u),
+                                        __builtin_amdgcn_perm(l[3], l[2], 0x07060302u)};
+  }
+  __syncthreads();   // planes published
+
+  f4 acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
+
+  // Pixel part of a lane's patch offset, per mt: output pixel (my, mx) → row 4·my, column 4·mx.
+  int pix[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int m = mt * 16 + (lane & 15);
+    pix[mt] = (m >> 3) * 4 * P1RS + (m & 7) * 4;
+  }
+  const int kg = lane >> 4;
+  auto pair_off = [](int p) { return ((p / 9) * P1 + p % 9) * P1RS; };
+
+  auto mfma6 = [&](int mt, const bf8& Ah, const bf8& Am, const bf8& Al, const u4 (&b)[3][NT]) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const bf8 Bh = __builtin_bit_cast(bf8, b[0][nt]), Bm = __builtin_bit_cast(bf8, b[1][nt]),
+                Bl = __builtin_bit_cast(bf8, b[2][nt]);
+      f4 c = acc[mt][nt];
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al, Bh, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bl, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bm, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bh, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bm, c, 0, 0, 0);
+      acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bh, c, 0, 0, 0);
+    }
+  };
+  // Steps 0..6: 8 consecutive columns of one patch row per lane (two 8-byte reads per plane).
+  auto step_rows = [&](int s, const u4 (&b)[3][NT]) {
+    const int g = 4 * s + kg;
+    const int po = pair_off(g < 27 ? g : 26);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const unsigned short* e = sp + po + pix[mt];
+      u4 v[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const uint2 lo2 = *(const uint2*)(e + p * P1U), hi2 = *(const uint2*)(e + p * P1U + 4);
+        v[p] = u4{lo2.x, lo2.y, hi2.x, hi2.y};
+      }
+      mfma6(mt, __builtin_bit_cast(bf8, v[0]), __builtin_bit_cast(bf8, v[1]),
+            __builtin_bit_cast(bf8, v[2]), b);
+    }
+  };
+  // Step 7: column kw = 8 of pairs 8·kg + e (e = 0..7), gathered element-wise.
+  auto step_col8 = [&](const u4 (&b)[3][NT]) {
+    int po[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int p = 8 * kg + e;
+      po[e] = pair_off(p < 27 ? p : 26) + 8;
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      u4 v[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const unsigned lo = sp[p * P1U + po[2 * i] + pix[mt]];
+          const unsigned hi = sp[p * P1U + po[2 * i + 1] + pix[mt]];
+          v[p][i] = lo | (hi << 16);
+        }
+      mfma6(mt, __builtin_bit_cast(bf8, v[0]), __builtin_bit_cast(bf8, v[1]),
+            __builtin_bit_cast(bf8, v[2]), b);
+    }
+  };
+  loadb(1, b1);
+  step_rows(0, b0);
+  loadb(2, b0);
+  step_rows(1, b1);
+  loadb(3, b1);
+  step_rows(2, b0);
+  loadb(4, b0);
+  step_rows(3, b1);
+  loadb(5, b1);
+  step_rows(4, b0);
+  loadb(6, b0);
+  step_rows(5, b1);
+  loadb(7, b1);
+  step_rows(6, b0);
+  step_col8(b1);
+
+  __syncthreads();  // patch reads done before the epilogue reuses LDS
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[mt][nt][r] += a.bias[ncol0 + nt * 16 + (lane & 15)];
+  gdn_epilogue<CO, MT, NT, false, BM, 256, true>(acc, smem, a, t, wm, ncol0, lane);
+}
+
 // --------------------------------------------------------------------- stand-alone GDN / IGDN
 // GDN.forward (models/GDN.py:64-94) on a [B,C,H,W] tensor stored NCHW or NHWC: 64 pixels of one
 // image per workgroup (linear pixel order), all C channels, the same fused core as the layers.
@@ -1566,14 +1792,17 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
   fill_conv5_taps(a.tt);
   a.qmode = qmode; a.noise = noise; a.rate = rate; a.yhat = yhat; a.partial = partial;
   if constexpr (EPI == EPI_QUANT) {
-    constexpr int BN = 64;
+    // Column split of conv3: 96 columns (2×2 waves) at N = 192 — B=64 gives 512 workgroups, one
+    // round of slots, and 20 % fewer operand bytes per MAC than 64-column tiles.
+    constexpr int BN = conv3_bn(N);
+    constexpr int WN = (BN / 16) % 4 == 0 ? 4 : 2, WM = 4 / WN;
     a.partials_per_image = a.tiles_x * a.tiles_y * (N / BN);
     dim3 grid(a.tiles_x * a.tiles_y * B, N / BN);
     if (X6in)
-      hipLaunchKernelGGL((engine_kernel<N, N, BN, 1, 4, EPI_QUANT, false, true>), grid, dim3(256),
-                         0, st, a);
+      hipLaunchKernelGGL((engine_kernel<N, N, BN, WM, WN, EPI_QUANT, false, true>), grid,
+                         dim3(256), 0, st, a);
     else
-      hipLaunchKernelGGL((engine_kernel<N, N, BN, 1, 4, EPI_QUANT>), grid, dim3(256), 0, st, a);
+      hipLaunchKernelGGL((engine_kernel<N, N, BN, WM, WN, EPI_QUANT>), grid, dim3(256), 0, st, a);
     return check_launch("conv3_quant_rate");
   } else if constexpr (EPI == EPI_PLAIN || EPI == EPI_RATE_BWD) {
     constexpr int BN = 64;
@@ -1613,7 +1842,7 @@ int launch_deconv5(const float* in, int B, int h, int w, const float* wp, const 
 #ifdef ICLR17_NO_PL
   a.phase_loop = 0;
 #else
-  a.phase_loop = (EPI == EPI_IGDN && base_tiles >= 512) ? 1 : 0;
+  a.phase_loop = (EPI == EPI_IGDN && base_tiles >= ICLR17_PL_MIN) ? 1 : 0;
 #endif
   if constexpr (EPI == EPI_IGDN) {
     const bool X6in = a.in_split != nullptr;
@@ -1729,7 +1958,7 @@ int iclr17_analysis_conv2_gdn(const float* in, int B, int H, int W, int N, const
 
 int iclr17_rate_partials_per_image(int H, int W, int N) {
   const int gh = H / 16, gw = W / 16;
-  return ((gh + 7) / 8) * ((gw + 7) / 8) * (N / 64);
+  return ((gh + 7) / 8) * ((gw + 7) / 8) * (N / conv3_bn(N));
 }
 
 int iclr17_analysis_conv3_quant_rate(const float* in, int B, int H, int W, int N,
@@ -1854,6 +2083,33 @@ int iclr17_analysis_conv1_gdn_x6(const float* x, int B, int H, int W, int N,
   io.gamma6 = (const unsigned short*)gamma_split;
   return N == 192 ? launch_conv1<192>(x, B, H, W, w_packed, bias, beta_eff, gamma_packed, out, pre_out, S(stream), nullptr, &io)
                   : launch_conv1<128>(x, B, H, W, w_packed, bias, beta_eff, gamma_packed, out, pre_out, S(stream), nullptr, &io);
+}
+
+int iclr17_analysis_conv1x6_gdn(const float* x, int B, int H, int W, int N,
+                                const uint16_t* w_split, const float* bias, const float* beta_eff,
+                                const uint16_t* gamma_split, float* out, uint16_t* out_split,
+                                float* pre_out, void* stream) {
+  int rc = check_dims(B, H, W, N);
+  if (rc) return rc;
+  ICLR17_REQUIRE(x && w_split && bias && beta_eff && gamma_split && (out || out_split),
+                 ICLR17_EINVAL, "conv1x6_gdn: null pointer");
+  EngineArgs a;
+  memset(&a, 0, sizeof(a));
+  a.in = x; a.w = (const float*)w_split; a.bias = bias; a.gbeta = beta_eff;
+  a.out = out; a.pre = pre_out;
+  a.out_split = (unsigned short*)out_split;
+  a.out_plane = (long)B * (H / 4) * (W / 4) * N;
+  a.ggamma6 = (const unsigned short*)gamma_split;
+  a.B = B; a.Hin = H; a.Win = W; a.Hout = H / 4; a.Wout = W / 4;
+  a.gh = H / 4; a.gw = W / 4; a.tiles_y = (a.gh + 7) / 8; a.tiles_x = (a.gw + 7) / 8;
+  a.sin = 4; a.sout = 1;
+  a.tt.npx = 1; a.tt.nph = 1;
+  dim3 grid(a.tiles_x * a.tiles_y * B, 1);
+  if (N == 192)
+    hipLaunchKernelGGL(conv1_x6_kernel<192>, grid, dim3(256), 0, S(stream), a);
+  else
+    hipLaunchKernelGGL(conv1_x6_kernel<128>, grid, dim3(256), 0, S(stream), a);
+  return check_launch("conv1x6_gdn");
 }
 
 int iclr17_analysis_conv2_gdn_x6(const uint16_t* in_split, int B, int H, int W, int N,

@@ -268,6 +268,32 @@ def conv1_gdn_x6(x: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Tens
     return split, out, pre
 
 
+def conv1x6_gdn(x: Tensor, w_split: Tensor, bias: Tensor, beta_eff: Tensor, g6: Tensor, N: int,
+                want_f32: bool = False, want_pre: bool = False):
+    """analysis_17.py:14-17 with both contractions in x6 (w_split: ``pack_conv1_x6``).
+    Returns (split, fp32 | None, pre | None) like ``conv1_gdn_x6``."""
+    _check(x, "image", 4)
+    B, C, H, W = x.shape
+    if C != 3:
+        raise Iclr17Error(f"iclr17: the analysis transform takes 3-channel images (got {C})")
+    _check_image_dims(H, W)
+    _check_channels(N)
+    if w_split.dtype != torch.int16 or w_split.numel() != 3 * 256 * N:
+        raise Iclr17Error("iclr17: conv1x6_gdn needs the split ICLR17_W_CONV1_X6 packing")
+    x = x.contiguous()
+    split = torch.empty(3, B, H // 4, W // 4, N, device=x.device, dtype=torch.int16)
+    out = torch.empty(B, H // 4, W // 4, N, device=x.device) if want_f32 else None
+    pre = torch.empty(B, H // 4, W // 4, N, device=x.device) if want_pre else None
+    call("iclr17_analysis_conv1x6_gdn", _p(x), B, H, W, N, _p(w_split), _p(bias), _p(beta_eff),
+         _p(g6), _p(out), _p(split), _p(pre), _stream(x))
+    return split, out, pre
+
+
+def pack_conv1_x6(w: Tensor, N: int) -> Tensor:
+    """conv1 weight [N,3,9,9] → the split planes conv1x6_gdn reads ([3, 256·N] int16)."""
+    return split_packed(pack_weight(_lib.ICLR17_W_CONV1_X6, w, N), 1, 256, N)
+
+
 def conv2_gdn_x6(hs: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Tensor,
                  g6: Tensor, want_f32: bool = False, want_pre: bool = False):
     """conv2_gdn on a split-form input (g6: split_packed γ); returns (split, fp32 | None,

@@ -87,7 +87,8 @@ class ImageCompressor(nn.Module):
         if kernels.precision() == "x6":
             e1 = self.Encoder.gdn1.effective_params_x6()
             e2 = self.Encoder.gdn2.effective_params_x6()
-            hs, _, _ = kernels.conv1_gdn_x6(x, w1, self.Encoder.conv1.bias, e1[0], e1[1], N, g6=e1[2])
+            hs, _, _ = kernels.conv1x6_gdn(x, self.Encoder.packed_conv1_x6(), self.Encoder.conv1.bias,
+                                           e1[0], e1[2], N)
             hs, _, _ = kernels.conv2_gdn_x6(hs, w2, self.Encoder.conv2.bias, *e2)
             q = kernels.conv3_quant_rate_x6(hs, w3, self.bitEstimator.packed(), noise, want_y=want_y)
             y_split = q[3]

@@ -48,6 +48,13 @@ class Analysis_net_17(nn.Module):
         g2 = self.gdn2.effective_params(force)
         return w1, w2, w3, g1, g2
 
+    def packed_conv1_x6(self, force: bool = False):
+        """conv1's weights in the x6 kernel's split layout (kernels.pack_conv1_x6), cached."""
+        N = self.out_channel_N
+        return self._pack.get("w1x6", (self.conv1.weight,),
+                              lambda: kernels.pack_conv1_x6(self.conv1.weight, N),
+                              force or self.training)
+
     def features(self, x):
         """conv1+gdn1 → conv2+gdn2 as NHWC (the input of conv3); no autograd."""
         w1, w2, _, g1, g2 = self.packed()

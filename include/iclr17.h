@@ -49,6 +49,7 @@ extern "C" {
 #define ICLR17_W_CONV5 1   /* Analysis conv2/conv3 [N,N,5,5] analysis_17.py:18,22 */
 #define ICLR17_W_DECONV5 2 /* Synthesis deconv1/deconv2 [N,N,5,5] synthesis_17.py:15,19 */
 #define ICLR17_W_DECONV9 3 /* Synthesis deconv3 [N,3,9,9] synthesis_17.py:23 */
+#define ICLR17_W_CONV1_X6 4 /* Analysis conv1 in the k order of iclr17_analysis_conv1x6_gdn */
 
 int iclr17_version(void);
 /* Copies the calling thread's last error message (NUL-terminated); returns its length. */
@@ -139,6 +140,14 @@ int iclr17_analysis_conv1_gdn_x6(const float* x, int B, int H, int W, int N,
                                  const float* w_packed, const float* bias, const float* beta_eff,
                                  const float* gamma_packed, const uint16_t* gamma_split,
                                  float* out, uint16_t* out_split, float* pre_out, void* stream);
+/* analysis_17.py:14-17,33 with BOTH contractions in x6 (conv1's patch contraction too): the
+ * weights are packed with ICLR17_W_CONV1_X6 and split by iclr17_split_packed(taps = 1, K = 256,
+ * N) into w_split [3][32][N][8]; gamma_split as above. out / out_split / pre_out as
+ * iclr17_analysis_conv1_gdn_x6. */
+int iclr17_analysis_conv1x6_gdn(const float* x, int B, int H, int W, int N,
+                                const uint16_t* w_split, const float* bias, const float* beta_eff,
+                                const uint16_t* gamma_split, float* out, uint16_t* out_split,
+                                float* pre_out, void* stream);
 /* iclr17_analysis_conv2_gdn on a split-form input. */
 int iclr17_analysis_conv2_gdn_x6(const uint16_t* in_split, int B, int H, int W, int N,
                                  const float* w_packed, const float* bias, const float* beta_eff,

@@ -122,6 +122,25 @@ def test_x6_layers(device, N):
 
 @pytest.mark.parametrize("N", [192, 128])
 @pytest.mark.parametrize("shape", [(2, 64, 96), (1, 80, 112), (1, 256, 256)])
+def test_conv1x6(device, N, shape):
+    """conv1 + GDN1 with both contractions in x6 (reordered K, split patch in LDS, weight planes
+    from L2) against the oracle; partial 8×8 tiles at 80×112."""
+    net, sd = net_for(N, 1, device), sd_for(N, 1)
+    F = torch.nn.functional
+    x = image(12, *shape)
+    e1 = net.Encoder.gdn1.effective_params_x6()
+    with torch.no_grad():
+        r_u1 = F.conv2d(x, sd["Encoder.conv1.weight"], sd["Encoder.conv1.bias"], stride=4, padding=4)
+        r_a1 = oracle.gdn(r_u1, sd["Encoder.gdn1.beta"], sd["Encoder.gdn1.gamma"], False)
+        a1s, a1, u1 = kernels.conv1x6_gdn(x.to(device), net.Encoder.packed_conv1_x6(),
+                                          net.Encoder.conv1.bias, e1[0], e1[2], N,
+                                          want_f32=True, want_pre=True)
+    assert rel_err(u1, nhwc(r_u1)) < REL and rel_err(a1, nhwc(r_a1)) < REL
+    assert torch.equal(kernels.merge_planes(a1s), a1)
+
+
+@pytest.mark.parametrize("N", [192, 128])
+@pytest.mark.parametrize("shape", [(2, 64, 96), (1, 80, 112), (1, 256, 256)])
 def test_deconv3_x6(device, N, shape):
     """The halo-tiled x6 deconv3 (16×16 base blocks, partial blocks at 80/112) against the
     oracle from the oracle's input: clipped / unclipped output and the per-8×8-tile SSE

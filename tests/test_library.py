@@ -34,7 +34,9 @@ def test_version_and_size_queries():
     assert _lib.query("iclr17_packed_weight_size", _lib.ICLR17_W_CONV5, 192) == 25 * 192 * 192
     assert _lib.query("iclr17_packed_weight_size", _lib.ICLR17_W_CONV1, 128) == 256 * 128
     assert _lib.query("iclr17_packed_weight_size", _lib.ICLR17_W_DECONV9, 192) == 9 * 192 * 48
-    assert _lib.query("iclr17_rate_partials_per_image", 256, 256, 192) == 4 * 3
+    assert _lib.query("iclr17_packed_weight_size", _lib.ICLR17_W_CONV1_X6, 192) == 256 * 192
+    assert _lib.query("iclr17_rate_partials_per_image", 256, 256, 192) == 4 * 2   # 96-column tiles
+    assert _lib.query("iclr17_rate_partials_per_image", 256, 256, 128) == 4 * 2   # 64-column tiles
     assert _lib.query("iclr17_output_partials_per_image", 256, 256) == 64
     assert _lib.query("iclr17_rate_bits_partials", 192, 16, 16) == 12
 

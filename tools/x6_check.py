@@ -100,9 +100,11 @@ def timings():
     fl3 = 2.0 * B * 64 * 64 * N * 3 * 81
     fl1 = 2.0 * B * 64 * 64 * (N * 243 + N * N)
     e1 = net.Encoder.gdn1.effective_params_x6()
+    w1x6 = net.Encoder.packed_conv1_x6()
     t = {
         "conv1 x6": (timeit(lambda: kernels.conv1_gdn_x6(x0, w1, net.Encoder.conv1.bias, g1[0], g1[1], N,
                                                          g6=e1[2])), fl1),
+        "conv1 x6x6": (timeit(lambda: kernels.conv1x6_gdn(x0, w1x6, net.Encoder.conv1.bias, e1[0], e1[2], N)), fl1),
         "conv2 fp32": (timeit(lambda: kernels.conv2_gdn(a1, w2, net.Encoder.conv2.bias, g2[0], g2[1])), fl2),
         "conv2 x6": (timeit(lambda: kernels.conv2_gdn_x6(a1s, w2, net.Encoder.conv2.bias, *e2)), fl2),
         "deconv2 fp32": (timeit(lambda: kernels.deconv_igdn(s1, d2, net.Decoder.deconv2.bias, q2[0], q2[1])), fld),

@@ -66,17 +66,27 @@ def analysis_features_train(enc, x: Tensor):
     return a2, {"x": x, "u1": u1, "a1": a1, "u2": u2, "a2": a2, "a2s": None}
 
 
-def analysis_backward(enc, saved: Dict[str, Tensor], g_y: Tensor) -> Dict[str, Tensor]:
-    """∂L/∂y (NHWC) → parameter gradients of Analysis_net_17 (analysis_17.py:14-39)."""
+def analysis_backward(enc, saved: Dict[str, Tensor], g_y: Tensor,
+                      g_y_split: Optional[Tensor] = None) -> Dict[str, Tensor]:
+    """∂L/∂y (NHWC) → parameter gradients of Analysis_net_17 (analysis_17.py:14-39). In the x6
+    mode the input-gradient contractions run on split-form gradients (g_y_split, or split here)."""
     bb1, gb1, _ = enc.gdn1.bounds_f32()
     bb2, gb2, _ = enc.gdn2.bounds_f32()
     w3t = kernels.pack_weight(_lib.ICLR17_W_DECONV5, enc.conv3.weight, enc.out_channel_N)
     w2t = kernels.pack_weight(_lib.ICLR17_W_DECONV5, enc.conv2.weight, enc.out_channel_N)
     p2 = enc.gdn2.effective_params_bwd()
     p1 = enc.gdn1.effective_params_bwd()
-    g_u2, dn2, db2, dbe2 = kernels.bwd_conv_gdn(g_y, w3t, saved["u2"], *p2)
-    dW3 = kernels.wgrad_k5(g_y, saved["a2"])
-    g_u1, dn1, db1, dbe1 = kernels.bwd_conv_gdn(g_u2, w2t, saved["u1"], *p1)
+    if kernels.precision() == "x6":
+        if g_y_split is None:
+            g_y_split = kernels.split_planes(g_y)
+        g_u2, dn2, db2, dbe2, g_u2s = kernels.bwd_conv_gdn(g_y, w3t, saved["u2"], *p2,
+                                                           g_split=g_y_split, want_split=True)
+        dW3 = kernels.wgrad_k5(g_y, saved["a2"])
+        g_u1, dn1, db1, dbe1 = kernels.bwd_conv_gdn(g_u2, w2t, saved["u1"], *p1, g_split=g_u2s)
+    else:
+        g_u2, dn2, db2, dbe2 = kernels.bwd_conv_gdn(g_y, w3t, saved["u2"], *p2)
+        dW3 = kernels.wgrad_k5(g_y, saved["a2"])
+        g_u1, dn1, db1, dbe1 = kernels.bwd_conv_gdn(g_u2, w2t, saved["u1"], *p1)
     dW2 = kernels.wgrad_k5(g_u2, saved["a1"])
     dW1 = kernels.wgrad_k9(g_u1, saved["x"])
     dbeta2, dgamma2 = kernels.gdn_param_grads(dn2, saved["u2"], dbe2, enc.gdn2.beta, enc.gdn2.gamma, bb2, gb2)
@@ -109,33 +119,51 @@ def synthesis_forward_train(dec, y_nhwc: Tensor, x_ref: Optional[Tensor] = None,
 
 
 def synthesis_backward(dec, saved: Dict[str, Tensor], g_recon: Tensor, g_bpp: Optional[Tensor] = None,
-                       rate_packed: Optional[Tensor] = None, count: float = 0.0):
+                       rate_packed: Optional[Tensor] = None, count: float = 0.0,
+                       want_split: bool = False):
     """∂L/∂recon (NCHW) → (∂L/∂ỹ NHWC incl. the rate term when g_bpp is given, parameter
-    gradients of Synthesis_net_17, rate-parameter partials)."""
+    gradients of Synthesis_net_17, rate-parameter partials[, ∂L/∂ỹ in split form (x6 mode,
+    else None)]). In the x6 mode the input-gradient contractions run in x6, each kernel handing
+    the next its gradient in split form."""
+    x6 = kernels.precision() == "x6"
     N = dec.out_channel_N
     bq1, gq1, _ = dec.igdn1.bounds_f32()
     bq2, gq2, _ = dec.igdn2.bounds_f32()
-    d3c = kernels.pack_weight(_lib.ICLR17_W_CONV1, dec.deconv3.weight, N)
+    d3c = None if x6 else kernels.pack_weight(_lib.ICLR17_W_CONV1, dec.deconv3.weight, N)
+    d3x = kernels.pack_conv1_x6(dec.deconv3.weight, N) if x6 else None
     d2c = kernels.pack_weight(_lib.ICLR17_W_CONV5, dec.deconv2.weight, N)
     d1c = kernels.pack_weight(_lib.ICLR17_W_CONV5, dec.deconv1.weight, N)
     q2 = dec.igdn2.effective_params_bwd()
     q1 = dec.igdn1.effective_params_bwd()
-    g_v2, dnq2, dbd2, dbeq2 = kernels.bwd_deconv3_igdn(g_recon, d3c, saved["v2"], *q2)
-    dWd3 = kernels.wgrad_k9(saved["s2"], g_recon)
-    dbd3 = kernels.bias_grad_nchw(g_recon)
-    g_v1, dnq1, dbd1, dbeq1 = kernels.bwd_deconv_igdn(g_v2, d2c, saved["v1"], *q1)
-    dWd2 = kernels.wgrad_k5(saved["s1"], g_v2)
     y = saved["y"]
     B, h, w, _ = y.shape
-    g_y, rpart = kernels.bwd_deconv_rate(g_v1, d1c, y if g_bpp is not None else None, rate_packed,
-                                         g_bpp, count, h, w)
+    g_ys = None
+    if x6:
+        g_v2, dnq2, dbd2, dbeq2, g_v2s = kernels.bwd_deconv3_igdn(g_recon, None, saved["v2"], *q2,
+                                                                  w_split=d3x, want_split=True)
+        dWd3 = kernels.wgrad_k9(saved["s2"], g_recon)
+        dbd3 = kernels.bias_grad_nchw(g_recon)
+        g_v1, dnq1, dbd1, dbeq1, g_v1s = kernels.bwd_deconv_igdn(g_v2, d2c, saved["v1"], *q1,
+                                                                 g_split=g_v2s, want_split=True)
+        dWd2 = kernels.wgrad_k5(saved["s1"], g_v2)
+        r = kernels.bwd_deconv_rate(g_v1, d1c, y if g_bpp is not None else None, rate_packed,
+                                    g_bpp, count, h, w, g_split=g_v1s, want_split=want_split)
+        g_y, rpart, g_ys = r if want_split else (*r, None)
+    else:
+        g_v2, dnq2, dbd2, dbeq2 = kernels.bwd_deconv3_igdn(g_recon, d3c, saved["v2"], *q2)
+        dWd3 = kernels.wgrad_k9(saved["s2"], g_recon)
+        dbd3 = kernels.bias_grad_nchw(g_recon)
+        g_v1, dnq1, dbd1, dbeq1 = kernels.bwd_deconv_igdn(g_v2, d2c, saved["v1"], *q1)
+        dWd2 = kernels.wgrad_k5(saved["s1"], g_v2)
+        g_y, rpart = kernels.bwd_deconv_rate(g_v1, d1c, y if g_bpp is not None else None,
+                                             rate_packed, g_bpp, count, h, w)
     dWd1 = kernels.wgrad_k5(y, g_v1)
     dbq2, dgq2 = kernels.gdn_param_grads(dnq2, saved["v2"], dbeq2, dec.igdn2.beta, dec.igdn2.gamma, bq2, gq2)
     dbq1, dgq1 = kernels.gdn_param_grads(dnq1, saved["v1"], dbeq1, dec.igdn1.beta, dec.igdn1.gamma, bq1, gq1)
     grads = {"deconv1.weight": dWd1, "deconv1.bias": dbd1, "igdn1.beta": dbq1, "igdn1.gamma": dgq1,
              "deconv2.weight": dWd2, "deconv2.bias": dbd2, "igdn2.beta": dbq2, "igdn2.gamma": dgq2,
              "deconv3.weight": dWd3, "deconv3.bias": dbd3}
-    return g_y, grads, rpart
+    return (g_y, grads, rpart, g_ys) if want_split else (g_y, grads, rpart)
 
 
 def _ordered(module, prefix: str, grads: Dict[str, Tensor]) -> List[Optional[Tensor]]:
@@ -177,10 +205,11 @@ class CodecTrainFn(torch.autograd.Function):
             g_recon = torch.zeros_like(ctx.recon)
         else:
             g_recon = kernels.grad_recon(ctx.recon, ctx.x, g_mse, g_clipped)
-        g_y, gs, rpart = synthesis_backward(dec, ctx.saved_s, g_recon, g_bpp, ctx.rate, ctx.count)
+        g_y, gs, rpart, g_ys = synthesis_backward(dec, ctx.saved_s, g_recon, g_bpp, ctx.rate,
+                                                  ctx.count, want_split=g_ytilde is None)
         if g_ytilde is not None:
             g_y = g_y + g_ytilde.permute(0, 2, 3, 1)
-        ga = analysis_backward(enc, ctx.saved_a, g_y.contiguous())
+        ga = analysis_backward(enc, ctx.saved_a, g_y.contiguous(), g_ys)
         rg = kernels.rate_param_grads(rpart, be.params_in_order()) if g_bpp is not None else [None] * 11
         grads += _ordered(enc, "Encoder.", ga)
         grads += _ordered(dec, "Decoder.", gs)

@@ -557,6 +557,7 @@ __device__ __forceinline__ void gdn_bwd_epilogue(f4 (&g)[MT][NT], float* smem, c
       }
   __syncthreads();
   store_tile_rows<CO>(a, t, sX, XS, a.out, CO, 0);
+  if (a.out_split != nullptr) store_tile_rows_split<CO>(a, t, sX, XS, CO, 0);   // x6 consumer
   if (a.colsum_out != nullptr) tile_colsum<CO>(a, t, sX, XS, a.colsum_out);
 }
 
@@ -640,6 +641,7 @@ __device__ __forceinline__ void rate_bwd_epilogue(f4 (&acc)[MT][NT], float* smem
       }
   __syncthreads();
   store_tile_rows<BN>(a, t, sO, OS, a.out, CO, cbase);
+  if (a.out_split != nullptr) store_tile_rows_split<BN>(a, t, sO, OS, CO, cbase);
   if (rate) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
@@ -1422,14 +1424,14 @@ __global__ void __launch_bounds__(256) conv1_gdn_kernel(const EngineArgs a) {
 // barrier in the main loop.
 constexpr int P1U = 3 * P1 * P1RS;        // u16 elements per split plane (4440)
 
-template <int CO>
+template <int CO, int EPI>
 __global__ void __launch_bounds__(256) conv1_x6_kernel(const EngineArgs a) {
   constexpr int WN = 4;
   constexpr int MT = BM / 16;
   constexpr int NT = CO / WN / 16;
   constexpr int S_FLOATS = 3 * P1U / 2;                 // split planes (6660 floats)
   constexpr int LDS_P = S_FLOATS + P1NI * 256;          // + the fp32 DMA landing area
-  constexpr int LDS_X = BM * (CO + 8);
+  constexpr int LDS_X = BM * (CO + 8) + (EPI == EPI_IGDN_BWD ? GSTAGE_FLOATS(CO) : 0);
   constexpr int LDS_FLOATS = LDS_P > LDS_X ? LDS_P : LDS_X;
   __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
   unsigned short* sp = (unsigned short*)smem;
@@ -1578,13 +1580,18 @@ __global__ void __launch_bounds__(256) conv1_x6_kernel(const EngineArgs a) {
   step_col8(b1);
 
   __syncthreads();  // patch reads done before the epilogue reuses LDS
+  if constexpr (EPI == EPI_GDN) {
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
+      for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[mt][nt][r] += a.bias[ncol0 + nt * 16 + (lane & 15)];
-  gdn_epilogue<CO, MT, NT, false, BM, 256, true>(acc, smem, a, t, wm, ncol0, lane);
+        for (int r = 0; r < 4; ++r) acc[mt][nt][r] += a.bias[ncol0 + nt * 16 + (lane & 15)];
+    gdn_epilogue<CO, MT, NT, false, BM, 256, true>(acc, smem, a, t, wm, ncol0, lane);
+  } else {
+    static_assert(EPI == EPI_IGDN_BWD, "conv1 x6 epilogues: GDN fwd, IGDN bwd");
+    gdn_bwd_epilogue<CO, MT, NT, true>(acc, smem, a, t, wm, ncol0, lane);
+  }
 }
 
 // --------------------------------------------------------------------- stand-alone GDN / IGDN
@@ -1770,6 +1777,13 @@ int launch_conv1(const float* x, int B, int H, int W, const float* wp, const flo
       hipLaunchKernelGGL((conv1_gdn_kernel<N, EPI, true>), grid, dim3(256), 0, st, a);
       return check_launch("conv1_gdn");
     }
+  } else {
+    if (a.in_split != nullptr) {   // bwd: a.w = the split ICLR17_W_CONV1_X6 planes (x6 contraction)
+      a.w = (const float*)a.in_split;
+      a.in_split = nullptr;
+      hipLaunchKernelGGL((conv1_x6_kernel<N, EPI>), grid, dim3(256), 0, st, a);
+      return check_launch("bwd_deconv3_igdn_x6");
+    }
   }
   hipLaunchKernelGGL((conv1_gdn_kernel<N, EPI>), grid, dim3(256), 0, st, a);
   return check_launch(EPI == EPI_GDN ? "conv1_gdn" : "bwd_deconv3_igdn");
@@ -1807,15 +1821,19 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
   } else if constexpr (EPI == EPI_PLAIN || EPI == EPI_RATE_BWD) {
     constexpr int BN = 64;
     dim3 grid(a.tiles_x * a.tiles_y * B, N / BN);
-    hipLaunchKernelGGL((engine_kernel<N, N, BN, 1, 4, EPI>), grid, dim3(256), 0, st, a);
+    if (EPI == EPI_RATE_BWD && X6in)
+      hipLaunchKernelGGL((engine_kernel<N, N, BN, 1, 4, EPI, false, true>), grid, dim3(256), 0,
+                         st, a);
+    else
+      hipLaunchKernelGGL((engine_kernel<N, N, BN, 1, 4, EPI>), grid, dim3(256), 0, st, a);
     return check_launch(EPI == EPI_PLAIN ? "conv3" : "bwd_deconv1_rate");
   } else {
     dim3 grid(a.tiles_x * a.tiles_y * B, 1);
-    if constexpr (EPI == EPI_GDN) {
+    if constexpr (EPI == EPI_GDN || EPI == EPI_IGDN_BWD) {
       if (X6in) {
         hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI, false, true>), grid, dim3(256), 0,
                            st, a);
-        return check_launch("conv2_gdn");
+        return check_launch(EPI == EPI_GDN ? "conv2_gdn" : "bwd_deconv_igdn");
       }
     }
     hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI>), grid, dim3(256), 0, st, a);
@@ -1856,6 +1874,12 @@ int launch_deconv5(const float* in, int B, int h, int w, const float* wp, const 
       hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI, false, true>), dim3(base_tiles * 4),
                          dim3(256), 0, st, a);
     if (a.phase_loop || X6in) return check_launch("deconv_igdn");
+  } else {
+    if (a.in_split != nullptr) {
+      hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI, false, true>), dim3(base_tiles * 4),
+                         dim3(256), 0, st, a);
+      return check_launch("bwd_conv_gdn");
+    }
   }
     hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI>), dim3(base_tiles * 4), dim3(256), 0,
                        st, a);
@@ -2106,9 +2130,9 @@ int iclr17_analysis_conv1x6_gdn(const float* x, int B, int H, int W, int N,
   a.tt.npx = 1; a.tt.nph = 1;
   dim3 grid(a.tiles_x * a.tiles_y * B, 1);
   if (N == 192)
-    hipLaunchKernelGGL(conv1_x6_kernel<192>, grid, dim3(256), 0, S(stream), a);
+    hipLaunchKernelGGL((conv1_x6_kernel<192, EPI_GDN>), grid, dim3(256), 0, S(stream), a);
   else
-    hipLaunchKernelGGL(conv1_x6_kernel<128>, grid, dim3(256), 0, S(stream), a);
+    hipLaunchKernelGGL((conv1_x6_kernel<128, EPI_GDN>), grid, dim3(256), 0, S(stream), a);
   return check_launch("conv1x6_gdn");
 }
 
@@ -2183,33 +2207,45 @@ static EngineArgs bwd_args(const float* saved, const float* gammaT, float* tout)
 }
 
 int iclr17_bwd_deconv3_igdn(const float* g_recon, int B, int H, int W, int N,
-                            const float* w_packed, const float* v_saved, const float* beta_eff,
-                            const float* gamma_packed, const float* gamma_packed_t, float* g_v,
+                            const float* w_packed, const uint16_t* w_split, const float* v_saved,
+                            const float* beta_eff, const float* gamma_packed,
+                            const float* gamma_packed_t, float* g_v, uint16_t* g_v_split,
                             float* dn, float* colsum_gv, float* colsum_dn, void* stream) {
   int rc = check_dims(B, H, W, N);
   if (rc) return rc;
-  ICLR17_REQUIRE(g_recon && w_packed && v_saved && beta_eff && gamma_packed && gamma_packed_t &&
-                     g_v && dn, ICLR17_EINVAL, "bwd_deconv3_igdn: null pointer");
+  ICLR17_REQUIRE(g_recon && (w_packed || w_split) && v_saved && beta_eff && gamma_packed &&
+                     gamma_packed_t && g_v && dn, ICLR17_EINVAL, "bwd_deconv3_igdn: null pointer");
   EngineArgs b = bwd_args(v_saved, gamma_packed_t, dn);
   b.colsum_out = colsum_gv;
   b.colsum_t = colsum_dn;
-  return N == 192 ? launch_conv1<192, EPI_IGDN_BWD>(g_recon, B, H, W, w_packed, nullptr, beta_eff, gamma_packed, g_v, nullptr, S(stream), &b)
-                  : launch_conv1<128, EPI_IGDN_BWD>(g_recon, B, H, W, w_packed, nullptr, beta_eff, gamma_packed, g_v, nullptr, S(stream), &b);
+  SplitIO io;
+  io.in = (const unsigned short*)w_split;   // x6: the conv1_x6 kernel reads these weight planes
+  io.out = (unsigned short*)g_v_split;
+  io.out_plane = (long)B * (H / 4) * (W / 4) * N;
+  return N == 192 ? launch_conv1<192, EPI_IGDN_BWD>(g_recon, B, H, W, w_packed, nullptr, beta_eff, gamma_packed, g_v, nullptr, S(stream), &b, &io)
+                  : launch_conv1<128, EPI_IGDN_BWD>(g_recon, B, H, W, w_packed, nullptr, beta_eff, gamma_packed, g_v, nullptr, S(stream), &b, &io);
 }
 
-int iclr17_bwd_deconv_igdn(const float* g_v, int B, int h, int w, int N, const float* w_packed,
-                           const float* v_prev, const float* beta_eff, const float* gamma_packed,
-                           const float* gamma_packed_t, float* g_v_prev, float* dn,
-                           float* colsum_gv, float* colsum_dn, void* stream) {
+int iclr17_bwd_deconv_igdn(const float* g_v, const uint16_t* g_v_split, int B, int h, int w,
+                           int N, const float* w_packed, const float* v_prev,
+                           const float* beta_eff, const float* gamma_packed,
+                           const float* gamma_packed_t, float* g_v_prev, uint16_t* g_v_prev_split,
+                           float* dn, float* colsum_gv, float* colsum_dn, void* stream) {
   ICLR17_REQUIRE(B > 0 && h > 0 && w > 0, ICLR17_EINVAL, "bwd_deconv_igdn: bad shape");
   ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "channel count N=%d unsupported", N);
-  ICLR17_REQUIRE(g_v && w_packed && v_prev && beta_eff && gamma_packed && gamma_packed_t &&
-                     g_v_prev && dn, ICLR17_EINVAL, "bwd_deconv_igdn: null pointer");
+  ICLR17_REQUIRE((g_v || g_v_split) && w_packed && v_prev && beta_eff && gamma_packed &&
+                     gamma_packed_t && g_v_prev && dn, ICLR17_EINVAL,
+                 "bwd_deconv_igdn: null pointer");
   EngineArgs b = bwd_args(v_prev, gamma_packed_t, dn);
   b.colsum_out = colsum_gv;
   b.colsum_t = colsum_dn;
-  return N == 192 ? launch_conv5<192, EPI_IGDN_BWD>(g_v, B, 2 * h, 2 * w, w_packed, nullptr, beta_eff, gamma_packed, g_v_prev, nullptr, 0, nullptr, nullptr, nullptr, nullptr, S(stream), &b)
-                  : launch_conv5<128, EPI_IGDN_BWD>(g_v, B, 2 * h, 2 * w, w_packed, nullptr, beta_eff, gamma_packed, g_v_prev, nullptr, 0, nullptr, nullptr, nullptr, nullptr, S(stream), &b);
+  SplitIO io;
+  io.in = (const unsigned short*)g_v_split;
+  io.in_plane = (long)B * 2 * h * 2 * w * N;
+  io.out = (unsigned short*)g_v_prev_split;
+  io.out_plane = (long)B * h * w * N;
+  return N == 192 ? launch_conv5<192, EPI_IGDN_BWD>(g_v, B, 2 * h, 2 * w, w_packed, nullptr, beta_eff, gamma_packed, g_v_prev, nullptr, 0, nullptr, nullptr, nullptr, nullptr, S(stream), &b, &io)
+                  : launch_conv5<128, EPI_IGDN_BWD>(g_v, B, 2 * h, 2 * w, w_packed, nullptr, beta_eff, gamma_packed, g_v_prev, nullptr, 0, nullptr, nullptr, nullptr, nullptr, S(stream), &b, &io);
 }
 
 int iclr17_rate_bwd_partials(int h, int w) { return ((h + 7) / 8) * ((w + 7) / 8); }
@@ -2222,35 +2258,48 @@ int iclr17_bwd_tiles(int kind, int h, int w) {
   return kind == 1 ? 4 * t : t;
 }
 
-int iclr17_bwd_deconv_rate(const float* g_v, int B, int h, int w, int N, const float* w_packed,
-                           const float* y_tilde, const float* rate_packed, const float* g_bpp,
-                           float count, float* g_y, float* rate_partial, void* stream) {
+int iclr17_bwd_deconv_rate(const float* g_v, const uint16_t* g_v_split, int B, int h, int w,
+                           int N, const float* w_packed, const float* y_tilde,
+                           const float* rate_packed, const float* g_bpp, float count, float* g_y,
+                           uint16_t* g_y_split, float* rate_partial, void* stream) {
   ICLR17_REQUIRE(B > 0 && h > 0 && w > 0, ICLR17_EINVAL, "bwd_deconv_rate: bad shape");
   ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "channel count N=%d unsupported", N);
-  ICLR17_REQUIRE(g_v && w_packed && g_y, ICLR17_EINVAL, "bwd_deconv_rate: null pointer");
+  ICLR17_REQUIRE((g_v || g_v_split) && w_packed && g_y, ICLR17_EINVAL,
+                 "bwd_deconv_rate: null pointer");
   ICLR17_REQUIRE(g_bpp == nullptr || (y_tilde && rate_packed && rate_partial && count > 0),
                  ICLR17_EINVAL, "bwd_deconv_rate: rate term needs y_tilde, rate params, partials");
   EngineArgs b = bwd_args(y_tilde, nullptr, nullptr);
   b.gscale = g_bpp;
   b.count = count;
   b.rpart = rate_partial;
-  return N == 192 ? launch_conv5<192, EPI_RATE_BWD>(g_v, B, 2 * h, 2 * w, w_packed, nullptr, nullptr, nullptr, g_y, nullptr, 0, nullptr, rate_packed, nullptr, nullptr, S(stream), &b)
-                  : launch_conv5<128, EPI_RATE_BWD>(g_v, B, 2 * h, 2 * w, w_packed, nullptr, nullptr, nullptr, g_y, nullptr, 0, nullptr, rate_packed, nullptr, nullptr, S(stream), &b);
+  SplitIO io;
+  io.in = (const unsigned short*)g_v_split;
+  io.in_plane = (long)B * 2 * h * 2 * w * N;
+  io.out = (unsigned short*)g_y_split;
+  io.out_plane = (long)B * h * w * N;
+  return N == 192 ? launch_conv5<192, EPI_RATE_BWD>(g_v, B, 2 * h, 2 * w, w_packed, nullptr, nullptr, nullptr, g_y, nullptr, 0, nullptr, rate_packed, nullptr, nullptr, S(stream), &b, &io)
+                  : launch_conv5<128, EPI_RATE_BWD>(g_v, B, 2 * h, 2 * w, w_packed, nullptr, nullptr, nullptr, g_y, nullptr, 0, nullptr, rate_packed, nullptr, nullptr, S(stream), &b, &io);
 }
 
-int iclr17_bwd_conv_gdn(const float* g_u, int B, int h, int w, int N, const float* w_packed,
-                        const float* u_prev, const float* beta_eff, const float* gamma_packed,
-                        const float* gamma_packed_t, float* g_u_prev, float* dn,
-                        float* colsum_gu, float* colsum_dn, void* stream) {
+int iclr17_bwd_conv_gdn(const float* g_u, const uint16_t* g_u_split, int B, int h, int w, int N,
+                        const float* w_packed, const float* u_prev, const float* beta_eff,
+                        const float* gamma_packed, const float* gamma_packed_t, float* g_u_prev,
+                        uint16_t* g_u_prev_split, float* dn, float* colsum_gu, float* colsum_dn,
+                        void* stream) {
   ICLR17_REQUIRE(B > 0 && h > 0 && w > 0, ICLR17_EINVAL, "bwd_conv_gdn: bad shape");
   ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "channel count N=%d unsupported", N);
-  ICLR17_REQUIRE(g_u && w_packed && u_prev && beta_eff && gamma_packed && gamma_packed_t &&
-                     g_u_prev && dn, ICLR17_EINVAL, "bwd_conv_gdn: null pointer");
+  ICLR17_REQUIRE((g_u || g_u_split) && w_packed && u_prev && beta_eff && gamma_packed &&
+                     gamma_packed_t && g_u_prev && dn, ICLR17_EINVAL, "bwd_conv_gdn: null pointer");
   EngineArgs b = bwd_args(u_prev, gamma_packed_t, dn);
   b.colsum_out = colsum_gu;
   b.colsum_t = colsum_dn;
-  return N == 192 ? launch_deconv5<192, EPI_GDN_BWD>(g_u, B, h, w, w_packed, nullptr, beta_eff, gamma_packed, g_u_prev, nullptr, S(stream), &b)
-                  : launch_deconv5<128, EPI_GDN_BWD>(g_u, B, h, w, w_packed, nullptr, beta_eff, gamma_packed, g_u_prev, nullptr, S(stream), &b);
+  SplitIO io;
+  io.in = (const unsigned short*)g_u_split;
+  io.in_plane = (long)B * h * w * N;
+  io.out = (unsigned short*)g_u_prev_split;
+  io.out_plane = (long)B * 2 * h * 2 * w * N;
+  return N == 192 ? launch_deconv5<192, EPI_GDN_BWD>(g_u, B, h, w, w_packed, nullptr, beta_eff, gamma_packed, g_u_prev, nullptr, S(stream), &b, &io)
+                  : launch_deconv5<128, EPI_GDN_BWD>(g_u, B, h, w, w_packed, nullptr, beta_eff, gamma_packed, g_u_prev, nullptr, S(stream), &b, &io);
 }
 
 int iclr17_gdn(const float* x, int B, int C, int H, int W, int layout, int inverse,

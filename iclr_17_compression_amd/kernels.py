@@ -615,62 +615,88 @@ def sum_rows(part: Tensor) -> Tensor:
     return out
 
 
-def bwd_deconv3_igdn(g_recon: Tensor, wp_conv1form: Tensor, v_saved: Tensor, beta_eff: Tensor,
-                     gp: Tensor, gpt: Tensor):
+def _split_like(t: Tensor) -> Tensor:
+    return torch.empty((3,) + tuple(t.shape), device=t.device, dtype=torch.int16)
+
+
+def bwd_deconv3_igdn(g_recon: Tensor, wp_conv1form: Optional[Tensor], v_saved: Tensor,
+                     beta_eff: Tensor, gp: Tensor, gpt: Tensor, w_split: Optional[Tensor] = None,
+                     want_split: bool = False):
     """deconv3 input-gradient fused with IGDN2 backward →
-    (g_v2 NHWC, dn NHWC, Σ g_v2 = ∂bias of deconv2, Σ dn = ∂β_eff of IGDN2)."""
+    (g_v2 NHWC, dn NHWC, Σ g_v2 = ∂bias of deconv2, Σ dn = ∂β_eff of IGDN2[, g_v2 split]).
+    w_split (``pack_conv1_x6`` of the deconv3 weight) runs the contraction in x6."""
     B, _, H, W = g_recon.shape
     N = v_saved.shape[3]
     g_v = torch.empty_like(v_saved)
     dn = torch.empty_like(v_saved)
+    sp = _split_like(v_saved) if want_split else None
     cs_g, cs_d = _colsum_buffers(v_saved, 0, H // 4, W // 4)
     call("iclr17_bwd_deconv3_igdn", _p(g_recon.contiguous()), B, H, W, N, _p(wp_conv1form),
-         _p(v_saved), _p(beta_eff), _p(gp), _p(gpt), _p(g_v), _p(dn), _p(cs_g), _p(cs_d),
-         _stream(g_recon))
-    return g_v, dn, sum_rows(cs_g), sum_rows(cs_d)
+         _p(w_split), _p(v_saved), _p(beta_eff), _p(gp), _p(gpt), _p(g_v), _p(sp), _p(dn),
+         _p(cs_g), _p(cs_d), _stream(g_recon))
+    out = (g_v, dn, sum_rows(cs_g), sum_rows(cs_d))
+    return out + (sp,) if want_split else out
 
 
-def bwd_deconv_igdn(g_v: Tensor, wp_conv5form: Tensor, v_prev: Tensor, beta_eff: Tensor, gp: Tensor,
-                    gpt: Tensor):
+def bwd_deconv_igdn(g_v: Optional[Tensor], wp_conv5form: Tensor, v_prev: Tensor, beta_eff: Tensor,
+                    gp: Tensor, gpt: Tensor, g_split: Optional[Tensor] = None,
+                    want_split: bool = False):
     """deconv2 input-gradient fused with IGDN1 backward →
-    (g_v1 NHWC, dn NHWC, Σ g_v1 = ∂bias of deconv1, Σ dn = ∂β_eff of IGDN1)."""
+    (g_v1 NHWC, dn NHWC, Σ g_v1 = ∂bias of deconv1, Σ dn = ∂β_eff of IGDN1[, g_v1 split]).
+    g_split (g_v in split form) runs the contraction in x6."""
     B, h, w, N = v_prev.shape
     g_prev = torch.empty_like(v_prev)
     dn = torch.empty_like(v_prev)
+    sp = _split_like(v_prev) if want_split else None
     cs_g, cs_d = _colsum_buffers(v_prev, 0, h, w)
-    call("iclr17_bwd_deconv_igdn", _p(g_v.contiguous()), B, h, w, N, _p(wp_conv5form), _p(v_prev),
-         _p(beta_eff), _p(gp), _p(gpt), _p(g_prev), _p(dn), _p(cs_g), _p(cs_d), _stream(g_v))
-    return g_prev, dn, sum_rows(cs_g), sum_rows(cs_d)
+    gin = g_v.contiguous() if g_split is None else None
+    call("iclr17_bwd_deconv_igdn", _p(gin), _p(g_split), B, h, w, N, _p(wp_conv5form), _p(v_prev),
+         _p(beta_eff), _p(gp), _p(gpt), _p(g_prev), _p(sp), _p(dn), _p(cs_g), _p(cs_d),
+         _stream(v_prev))
+    out = (g_prev, dn, sum_rows(cs_g), sum_rows(cs_d))
+    return out + (sp,) if want_split else out
 
 
-def bwd_deconv_rate(g_v1: Tensor, wp_conv5form: Tensor, y_tilde: Optional[Tensor],
+def bwd_deconv_rate(g_v1: Optional[Tensor], wp_conv5form: Tensor, y_tilde: Optional[Tensor],
                     rate_packed: Optional[Tensor], g_bpp: Optional[Tensor], count: float,
-                    h: int, w: int):
-    """deconv1 input-gradient (+ rate backward when g_bpp is given) → (g_y NHWC, rate partials)."""
-    B, _, _, N = g_v1.shape
-    g_y = torch.empty(B, h, w, N, device=g_v1.device, dtype=torch.float32)
+                    h: int, w: int, g_split: Optional[Tensor] = None, want_split: bool = False):
+    """deconv1 input-gradient (+ rate backward when g_bpp is given) →
+    (g_y NHWC, rate partials[, g_y split]). g_split (g_v1 in split form) runs x6."""
+    ref = g_v1 if g_split is None else g_split[0]
+    B, _, _, N = ref.shape
+    g_y = torch.empty(B, h, w, N, device=ref.device, dtype=torch.float32)
+    sp = _split_like(g_y) if want_split else None
     part = None
     gb = None
     if g_bpp is not None:
         T = query("iclr17_rate_bwd_partials", h, w)
-        part = torch.empty(B * T, 11, N, device=g_v1.device, dtype=torch.float32)
+        part = torch.empty(B * T, 11, N, device=ref.device, dtype=torch.float32)
         gb = g_bpp.detach().reshape(()).contiguous()
-    call("iclr17_bwd_deconv_rate", _p(g_v1.contiguous()), B, h, w, N, _p(wp_conv5form), _p(y_tilde),
-         _p(rate_packed), _p(gb), ctypes.c_float(count), _p(g_y), _p(part), _stream(g_v1))
-    return g_y, part
+    gin = g_v1.contiguous() if g_split is None else None
+    call("iclr17_bwd_deconv_rate", _p(gin), _p(g_split), B, h, w, N, _p(wp_conv5form),
+         _p(y_tilde), _p(rate_packed), _p(gb), ctypes.c_float(count), _p(g_y), _p(sp), _p(part),
+         _stream(ref))
+    return (g_y, part, sp) if want_split else (g_y, part)
 
 
-def bwd_conv_gdn(g_u: Tensor, wp_deconv5form: Tensor, u_prev: Tensor, beta_eff: Tensor, gp: Tensor,
-                 gpt: Tensor):
+def bwd_conv_gdn(g_u: Optional[Tensor], wp_deconv5form: Tensor, u_prev: Tensor, beta_eff: Tensor,
+                 gp: Tensor, gpt: Tensor, g_split: Optional[Tensor] = None,
+                 want_split: bool = False):
     """conv3/conv2 input-gradient fused with GDN2/GDN1 backward →
-    (g_u_prev NHWC, dn NHWC, Σ g_u_prev = ∂bias of the previous conv, Σ dn = ∂β_eff)."""
-    B, h, w, N = g_u.shape
+    (g_u_prev NHWC, dn NHWC, Σ g_u_prev = ∂bias of the previous conv, Σ dn = ∂β_eff
+    [, g_u_prev split]). g_split (g_u in split form) runs the contraction in x6."""
+    ref = g_u if g_split is None else g_split[0]
+    B, h, w, N = ref.shape
     g_prev = torch.empty_like(u_prev)
     dn = torch.empty_like(u_prev)
-    cs_g, cs_d = _colsum_buffers(g_u, 1, h, w)
-    call("iclr17_bwd_conv_gdn", _p(g_u.contiguous()), B, h, w, N, _p(wp_deconv5form), _p(u_prev),
-         _p(beta_eff), _p(gp), _p(gpt), _p(g_prev), _p(dn), _p(cs_g), _p(cs_d), _stream(g_u))
-    return g_prev, dn, sum_rows(cs_g), sum_rows(cs_d)
+    sp = _split_like(u_prev) if want_split else None
+    cs_g, cs_d = _colsum_buffers(u_prev, 1, h, w)
+    gin = g_u.contiguous() if g_split is None else None
+    call("iclr17_bwd_conv_gdn", _p(gin), _p(g_split), B, h, w, N, _p(wp_deconv5form), _p(u_prev),
+         _p(beta_eff), _p(gp), _p(gpt), _p(g_prev), _p(sp), _p(dn), _p(cs_g), _p(cs_d),
+         _stream(u_prev))
+    out = (g_prev, dn, sum_rows(cs_g), sum_rows(cs_d))
+    return out + (sp,) if want_split else out
 
 
 def wgrad_k5(G: Tensor, X: Tensor) -> Tensor:

@@ -31,8 +31,18 @@ def make(N, seed, device):
     return net.to(device).train(), oracle.state_dict_to_torch(sd)
 
 
+@pytest.fixture(params=["x6", "fp32"])
+def precision(request):
+    """x6: the input-gradient contractions run in x6 on split-form gradients; fp32: exact f32."""
+    from iclr_17_compression_amd import kernels
+    old = kernels.precision()
+    kernels.set_precision(request.param)
+    yield request.param
+    kernels.set_precision(old)
+
+
 @pytest.mark.parametrize("N,B,H,W", [(192, 2, 64, 64), (128, 2, 48, 80)])
-def test_train_step_all_grads(device, N, B, H, W):
+def test_train_step_all_grads(device, precision, N, B, H, W):
     net, sd = make(N, 2, device)
     x = torch.from_numpy(synth.to_unit_float(synth.image_u8(3, B, H, W)))
     noise = torch.from_numpy(synth.uniform(4, (B, N, H // 16, W // 16), -0.5, 0.5))

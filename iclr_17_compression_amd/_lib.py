@@ -79,11 +79,11 @@ SIGNATURES = {
     "iclr17_rate_bits": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "iclr17_rate_bits_partials": (_I, [_I, _I, _I]),
     "iclr17_grad_recon": (_I, [_P, _P, _P, _P, _I64, _P, _P]),
-    "iclr17_bwd_deconv3_igdn": (_I, [_P, _I, _I, _I, _I] + [_P] * 12),
-    "iclr17_bwd_deconv_igdn": (_I, [_P, _P, _I, _I, _I, _I] + [_P] * 11),
+    "iclr17_bwd_deconv3_igdn": (_I, [_P, _I, _I, _I, _I] + [_P] * 14),
+    "iclr17_bwd_deconv_igdn": (_I, [_P, _P, _I, _I, _I, _I] + [_P] * 13),
     "iclr17_bwd_deconv_rate": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _F, _P, _P, _P, _P]),
     "iclr17_rate_bwd_partials": (_I, [_I, _I]),
-    "iclr17_bwd_conv_gdn": (_I, [_P, _P, _I, _I, _I, _I] + [_P] * 11),
+    "iclr17_bwd_conv_gdn": (_I, [_P, _P, _I, _I, _I, _I] + [_P] * 13),
     "iclr17_bwd_tiles": (_I, [_I, _I, _I]),
     "iclr17_sum_rows": (_I, [_P, _I, _I, _P, _P, _P]),
     "iclr17_sum_rows_workspace_size": (_SZ, [_I]),

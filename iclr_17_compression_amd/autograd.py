@@ -74,15 +74,19 @@ def analysis_backward(enc, saved: Dict[str, Tensor], g_y: Tensor,
     bb2, gb2, _ = enc.gdn2.bounds_f32()
     w3t = kernels.pack_weight(_lib.ICLR17_W_DECONV5, enc.conv3.weight, enc.out_channel_N)
     w2t = kernels.pack_weight(_lib.ICLR17_W_DECONV5, enc.conv2.weight, enc.out_channel_N)
-    p2 = enc.gdn2.effective_params_bwd()
-    p1 = enc.gdn1.effective_params_bwd()
+    x6 = kernels.precision() == "x6"
+    p2 = None if x6 else enc.gdn2.effective_params_bwd()
+    p1 = None if x6 else enc.gdn1.effective_params_bwd()
     if kernels.precision() == "x6":
         if g_y_split is None:
             g_y_split = kernels.split_planes(g_y)
-        g_u2, dn2, db2, dbe2, g_u2s = kernels.bwd_conv_gdn(g_y, w3t, saved["u2"], *p2,
-                                                           g_split=g_y_split, want_split=True)
+        x2, x1 = enc.gdn2.effective_params_bwd_x6(), enc.gdn1.effective_params_bwd_x6()
+        g_u2, dn2, db2, dbe2, g_u2s = kernels.bwd_conv_gdn(g_y, w3t, saved["u2"], *x2[:3],
+                                                           g_split=g_y_split, want_split=True,
+                                                           g6=x2[3], g6t=x2[4])
         dW3 = kernels.wgrad_k5(g_y, saved["a2"])
-        g_u1, dn1, db1, dbe1 = kernels.bwd_conv_gdn(g_u2, w2t, saved["u1"], *p1, g_split=g_u2s)
+        g_u1, dn1, db1, dbe1 = kernels.bwd_conv_gdn(g_u2, w2t, saved["u1"], *x1[:3], g_split=g_u2s,
+                                                    g6=x1[3], g6t=x1[4])
     else:
         g_u2, dn2, db2, dbe2 = kernels.bwd_conv_gdn(g_y, w3t, saved["u2"], *p2)
         dW3 = kernels.wgrad_k5(g_y, saved["a2"])
@@ -133,18 +137,20 @@ def synthesis_backward(dec, saved: Dict[str, Tensor], g_recon: Tensor, g_bpp: Op
     d3x = kernels.pack_conv1_x6(dec.deconv3.weight, N) if x6 else None
     d2c = kernels.pack_weight(_lib.ICLR17_W_CONV5, dec.deconv2.weight, N)
     d1c = kernels.pack_weight(_lib.ICLR17_W_CONV5, dec.deconv1.weight, N)
-    q2 = dec.igdn2.effective_params_bwd()
-    q1 = dec.igdn1.effective_params_bwd()
+    q2 = dec.igdn2.effective_params_bwd_x6() if x6 else dec.igdn2.effective_params_bwd()
+    q1 = dec.igdn1.effective_params_bwd_x6() if x6 else dec.igdn1.effective_params_bwd()
     y = saved["y"]
     B, h, w, _ = y.shape
     g_ys = None
     if x6:
-        g_v2, dnq2, dbd2, dbeq2, g_v2s = kernels.bwd_deconv3_igdn(g_recon, None, saved["v2"], *q2,
-                                                                  w_split=d3x, want_split=True)
+        g_v2, dnq2, dbd2, dbeq2, g_v2s = kernels.bwd_deconv3_igdn(g_recon, None, saved["v2"], *q2[:3],
+                                                                  w_split=d3x, want_split=True,
+                                                                  g6=q2[3], g6t=q2[4])
         dWd3 = kernels.wgrad_k9(saved["s2"], g_recon)
         dbd3 = kernels.bias_grad_nchw(g_recon)
-        g_v1, dnq1, dbd1, dbeq1, g_v1s = kernels.bwd_deconv_igdn(g_v2, d2c, saved["v1"], *q1,
-                                                                 g_split=g_v2s, want_split=True)
+        g_v1, dnq1, dbd1, dbeq1, g_v1s = kernels.bwd_deconv_igdn(g_v2, d2c, saved["v1"], *q1[:3],
+                                                                 g_split=g_v2s, want_split=True,
+                                                                 g6=q1[3], g6t=q1[4])
         dWd2 = kernels.wgrad_k5(saved["s1"], g_v2)
         r = kernels.bwd_deconv_rate(g_v1, d1c, y if g_bpp is not None else None, rate_packed,
                                     g_bpp, count, h, w, g_split=g_v1s, want_split=want_split)

@@ -111,6 +111,7 @@ struct EngineArgs {
   unsigned short* out_split;        // [3][B][Hout][Wout][CO] or nullptr
   long out_plane;
   const unsigned short* ggamma6;    // x6: γ_eff split, [3][CO/8][CO][8] bf16 (plane CO·CO)
+  const unsigned short* ggammaT6;   // x6 backward: the transposed packing of γ_eff, split
 };
 
 struct TileInfo {
@@ -363,7 +364,7 @@ __device__ __forceinline__ void chan_gemm_lds(f4 (&acc)[MT][NT], const float* sX
 // B-fragment layout of v_mfma_f32_16x16x32_bf16 — read from L2 (221 KB at CO = 192; there is
 // no LDS left beside the x² tile at two workgroups per CU), one k-block ahead. Entry: the sX
 // writes of every wave are published (caller's barrier).
-template <int CO, int MT, int NT>
+template <int CO, int MT, int NT, bool SQ = false>
 __device__ __forceinline__ void chan_gemm_x6(f4 (&acc)[MT][NT], const float* sX,
                                              const unsigned short* __restrict__ g6, int wm,
                                              int ncol0, int lane) {
@@ -389,8 +390,13 @@ __device__ __forceinline__ void chan_gemm_x6(f4 (&acc)[MT][NT], const float* sX,
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       u4 ah, am, al;
-      split8(*(const f4*)(xrow + mt * 16 * XS + kb * 32),
-             *(const f4*)(xrow + mt * 16 * XS + kb * 32 + 4), ah, am, al);
+      f4 x0 = *(const f4*)(xrow + mt * 16 * XS + kb * 32);
+      f4 x1 = *(const f4*)(xrow + mt * 16 * XS + kb * 32 + 4);
+      if (SQ) {   // u² rounded to fp32 first, as the fp32 contraction (and conv2d(x², γ)) does
+        x0 = x0 * x0;
+        x1 = x1 * x1;
+      }
+      split8(x0, x1, ah, am, al);
       const bf8 Ah = __builtin_bit_cast(bf8, ah), Am = __builtin_bit_cast(bf8, am),
                 Al = __builtin_bit_cast(bf8, al);
 #pragma unroll
@@ -516,7 +522,12 @@ __device__ __forceinline__ void gdn_bwd_epilogue(f4 (&g)[MT][NT], float* smem, c
   const int wave = threadIdx.x >> 6;
   load_tile_rows<CO>(a, t, a.saved, sX, XS, CO, 0);   // u, kept in LDS through GEMM 1
   f4 acc2[MT][NT];
-  chan_gemm_lds<CO, MT, NT, true>(acc2, sX, a.ggamma, sG, wm, ncol0, lane, wave);  // Σ_j γ[i][j] u_j²
+  if (a.ggamma6 != nullptr) {   // x6: γ and γᵀ pre-split, from L2 (no LDS stages)
+    __syncthreads();            // u tile published
+    chan_gemm_x6<CO, MT, NT, true>(acc2, sX, a.ggamma6, wm, ncol0, lane);
+  } else {
+    chan_gemm_lds<CO, MT, NT, true>(acc2, sX, a.ggamma, sG, wm, ncol0, lane, wave);  // Σ_j γ[i][j] u_j²
+  }
   __syncthreads();
   f4 u[MT][NT];
 #pragma unroll
@@ -542,7 +553,12 @@ __device__ __forceinline__ void gdn_bwd_epilogue(f4 (&g)[MT][NT], float* smem, c
         u[mt][nt][r] = uu;
         sX[idx] = dn;
       }
-  chan_gemm_lds<CO, MT, NT>(acc2, sX, a.ggammaT, sG, wm, ncol0, lane, wave);  // w_j = Σ_i γ[i][j] dn_i
+  if (a.ggammaT6 != nullptr) {
+    __syncthreads();            // dn tile published
+    chan_gemm_x6<CO, MT, NT>(acc2, sX, a.ggammaT6, wm, ncol0, lane);
+  } else {
+    chan_gemm_lds<CO, MT, NT>(acc2, sX, a.ggammaT, sG, wm, ncol0, lane, wave);  // w_j = Σ_i γ[i][j] dn_i
+  }
   store_tile_rows<CO>(a, t, sX, XS, a.tout, CO, 0);
   if (a.colsum_t != nullptr) tile_colsum<CO>(a, t, sX, XS, a.colsum_t);
   __syncthreads();
@@ -1749,6 +1765,7 @@ struct SplitIO {
   unsigned short* out = nullptr;
   long out_plane = 0;
   const unsigned short* gamma6 = nullptr;   // x6: split γ_eff for the GDN contraction
+  const unsigned short* gammaT6 = nullptr;  // x6 backward: split transposed γ_eff
 };
 
 static void apply_split(EngineArgs& a, const SplitIO* x6) {
@@ -1756,6 +1773,7 @@ static void apply_split(EngineArgs& a, const SplitIO* x6) {
   a.in_split = x6->in; a.in_plane = x6->in_plane;
   a.out_split = x6->out; a.out_plane = x6->out_plane;
   a.ggamma6 = x6->gamma6;
+  a.ggammaT6 = x6->gammaT6;
 }
 
 template <int N, int EPI = EPI_GDN>
@@ -2209,7 +2227,8 @@ static EngineArgs bwd_args(const float* saved, const float* gammaT, float* tout)
 int iclr17_bwd_deconv3_igdn(const float* g_recon, int B, int H, int W, int N,
                             const float* w_packed, const uint16_t* w_split, const float* v_saved,
                             const float* beta_eff, const float* gamma_packed,
-                            const float* gamma_packed_t, float* g_v, uint16_t* g_v_split,
+                            const float* gamma_packed_t,
+                            const uint16_t* gamma_split, const uint16_t* gamma_t_split, float* g_v, uint16_t* g_v_split,
                             float* dn, float* colsum_gv, float* colsum_dn, void* stream) {
   int rc = check_dims(B, H, W, N);
   if (rc) return rc;
@@ -2219,6 +2238,8 @@ int iclr17_bwd_deconv3_igdn(const float* g_recon, int B, int H, int W, int N,
   b.colsum_out = colsum_gv;
   b.colsum_t = colsum_dn;
   SplitIO io;
+  io.gamma6 = (const unsigned short*)gamma_split;
+  io.gammaT6 = (const unsigned short*)gamma_t_split;
   io.in = (const unsigned short*)w_split;   // x6: the conv1_x6 kernel reads these weight planes
   io.out = (unsigned short*)g_v_split;
   io.out_plane = (long)B * (H / 4) * (W / 4) * N;
@@ -2229,7 +2250,8 @@ int iclr17_bwd_deconv3_igdn(const float* g_recon, int B, int H, int W, int N,
 int iclr17_bwd_deconv_igdn(const float* g_v, const uint16_t* g_v_split, int B, int h, int w,
                            int N, const float* w_packed, const float* v_prev,
                            const float* beta_eff, const float* gamma_packed,
-                           const float* gamma_packed_t, float* g_v_prev, uint16_t* g_v_prev_split,
+                           const float* gamma_packed_t,
+                            const uint16_t* gamma_split, const uint16_t* gamma_t_split, float* g_v_prev, uint16_t* g_v_prev_split,
                            float* dn, float* colsum_gv, float* colsum_dn, void* stream) {
   ICLR17_REQUIRE(B > 0 && h > 0 && w > 0, ICLR17_EINVAL, "bwd_deconv_igdn: bad shape");
   ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "channel count N=%d unsupported", N);
@@ -2240,6 +2262,8 @@ int iclr17_bwd_deconv_igdn(const float* g_v, const uint16_t* g_v_split, int B, i
   b.colsum_out = colsum_gv;
   b.colsum_t = colsum_dn;
   SplitIO io;
+  io.gamma6 = (const unsigned short*)gamma_split;
+  io.gammaT6 = (const unsigned short*)gamma_t_split;
   io.in = (const unsigned short*)g_v_split;
   io.in_plane = (long)B * 2 * h * 2 * w * N;
   io.out = (unsigned short*)g_v_prev_split;
@@ -2283,7 +2307,8 @@ int iclr17_bwd_deconv_rate(const float* g_v, const uint16_t* g_v_split, int B, i
 
 int iclr17_bwd_conv_gdn(const float* g_u, const uint16_t* g_u_split, int B, int h, int w, int N,
                         const float* w_packed, const float* u_prev, const float* beta_eff,
-                        const float* gamma_packed, const float* gamma_packed_t, float* g_u_prev,
+                        const float* gamma_packed, const float* gamma_packed_t,
+                            const uint16_t* gamma_split, const uint16_t* gamma_t_split, float* g_u_prev,
                         uint16_t* g_u_prev_split, float* dn, float* colsum_gu, float* colsum_dn,
                         void* stream) {
   ICLR17_REQUIRE(B > 0 && h > 0 && w > 0, ICLR17_EINVAL, "bwd_conv_gdn: bad shape");
@@ -2294,6 +2319,8 @@ int iclr17_bwd_conv_gdn(const float* g_u, const uint16_t* g_u_split, int B, int 
   b.colsum_out = colsum_gu;
   b.colsum_t = colsum_dn;
   SplitIO io;
+  io.gamma6 = (const unsigned short*)gamma_split;
+  io.gammaT6 = (const unsigned short*)gamma_t_split;
   io.in = (const unsigned short*)g_u_split;
   io.in_plane = (long)B * h * w * N;
   io.out = (unsigned short*)g_u_prev_split;

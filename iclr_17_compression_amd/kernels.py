@@ -621,7 +621,8 @@ def _split_like(t: Tensor) -> Tensor:
 
 def bwd_deconv3_igdn(g_recon: Tensor, wp_conv1form: Optional[Tensor], v_saved: Tensor,
                      beta_eff: Tensor, gp: Tensor, gpt: Tensor, w_split: Optional[Tensor] = None,
-                     want_split: bool = False):
+                     want_split: bool = False, g6: Optional[Tensor] = None,
+                     g6t: Optional[Tensor] = None):
     """deconv3 input-gradient fused with IGDN2 backward →
     (g_v2 NHWC, dn NHWC, Σ g_v2 = ∂bias of deconv2, Σ dn = ∂β_eff of IGDN2[, g_v2 split]).
     w_split (``pack_conv1_x6`` of the deconv3 weight) runs the contraction in x6."""
@@ -632,7 +633,8 @@ def bwd_deconv3_igdn(g_recon: Tensor, wp_conv1form: Optional[Tensor], v_saved: T
     sp = _split_like(v_saved) if want_split else None
     cs_g, cs_d = _colsum_buffers(v_saved, 0, H // 4, W // 4)
     call("iclr17_bwd_deconv3_igdn", _p(g_recon.contiguous()), B, H, W, N, _p(wp_conv1form),
-         _p(w_split), _p(v_saved), _p(beta_eff), _p(gp), _p(gpt), _p(g_v), _p(sp), _p(dn),
+         _p(w_split), _p(v_saved), _p(beta_eff), _p(gp), _p(gpt), _p(g6), _p(g6t), _p(g_v),
+         _p(sp), _p(dn),
          _p(cs_g), _p(cs_d), _stream(g_recon))
     out = (g_v, dn, sum_rows(cs_g), sum_rows(cs_d))
     return out + (sp,) if want_split else out
@@ -640,7 +642,8 @@ def bwd_deconv3_igdn(g_recon: Tensor, wp_conv1form: Optional[Tensor], v_saved: T
 
 def bwd_deconv_igdn(g_v: Optional[Tensor], wp_conv5form: Tensor, v_prev: Tensor, beta_eff: Tensor,
                     gp: Tensor, gpt: Tensor, g_split: Optional[Tensor] = None,
-                    want_split: bool = False):
+                    want_split: bool = False, g6: Optional[Tensor] = None,
+                    g6t: Optional[Tensor] = None):
     """deconv2 input-gradient fused with IGDN1 backward →
     (g_v1 NHWC, dn NHWC, Σ g_v1 = ∂bias of deconv1, Σ dn = ∂β_eff of IGDN1[, g_v1 split]).
     g_split (g_v in split form) runs the contraction in x6."""
@@ -651,7 +654,7 @@ def bwd_deconv_igdn(g_v: Optional[Tensor], wp_conv5form: Tensor, v_prev: Tensor,
     cs_g, cs_d = _colsum_buffers(v_prev, 0, h, w)
     gin = g_v.contiguous() if g_split is None else None
     call("iclr17_bwd_deconv_igdn", _p(gin), _p(g_split), B, h, w, N, _p(wp_conv5form), _p(v_prev),
-         _p(beta_eff), _p(gp), _p(gpt), _p(g_prev), _p(sp), _p(dn), _p(cs_g), _p(cs_d),
+         _p(beta_eff), _p(gp), _p(gpt), _p(g6), _p(g6t), _p(g_prev), _p(sp), _p(dn), _p(cs_g), _p(cs_d),
          _stream(v_prev))
     out = (g_prev, dn, sum_rows(cs_g), sum_rows(cs_d))
     return out + (sp,) if want_split else out
@@ -681,7 +684,8 @@ def bwd_deconv_rate(g_v1: Optional[Tensor], wp_conv5form: Tensor, y_tilde: Optio
 
 def bwd_conv_gdn(g_u: Optional[Tensor], wp_deconv5form: Tensor, u_prev: Tensor, beta_eff: Tensor,
                  gp: Tensor, gpt: Tensor, g_split: Optional[Tensor] = None,
-                 want_split: bool = False):
+                 want_split: bool = False, g6: Optional[Tensor] = None,
+                 g6t: Optional[Tensor] = None):
     """conv3/conv2 input-gradient fused with GDN2/GDN1 backward →
     (g_u_prev NHWC, dn NHWC, Σ g_u_prev = ∂bias of the previous conv, Σ dn = ∂β_eff
     [, g_u_prev split]). g_split (g_u in split form) runs the contraction in x6."""
@@ -693,7 +697,7 @@ def bwd_conv_gdn(g_u: Optional[Tensor], wp_deconv5form: Tensor, u_prev: Tensor, 
     cs_g, cs_d = _colsum_buffers(u_prev, 1, h, w)
     gin = g_u.contiguous() if g_split is None else None
     call("iclr17_bwd_conv_gdn", _p(gin), _p(g_split), B, h, w, N, _p(wp_deconv5form), _p(u_prev),
-         _p(beta_eff), _p(gp), _p(gpt), _p(g_prev), _p(sp), _p(dn), _p(cs_g), _p(cs_d),
+         _p(beta_eff), _p(gp), _p(gpt), _p(g6), _p(g6t), _p(g_prev), _p(sp), _p(dn), _p(cs_g), _p(cs_d),
          _stream(u_prev))
     out = (g_prev, dn, sum_rows(cs_g), sum_rows(cs_d))
     return out + (sp,) if want_split else out

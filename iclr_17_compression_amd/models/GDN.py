@@ -79,6 +79,13 @@ class GDN(nn.Module):
         bb, gb, ped = self.bounds_f32()
         return kernels.pack_gdn(self.beta, self.gamma, bb, gb, ped, transposed=True)
 
+    def effective_params_bwd_x6(self):
+        """effective_params_bwd plus γ and γᵀ split for the x6 backward contractions:
+        (beta_eff, gamma_packed, gamma_packed_t, gamma_split, gamma_t_split)."""
+        be, gp, gpt = self.effective_params_bwd()
+        C = self.beta.shape[0]
+        return be, gp, gpt, kernels.split_packed(gp, 1, C, C), kernels.split_packed(gpt, 1, C, C)
+
     def forward(self, inputs):
         unfold = inputs.dim() == 5
         if unfold:  # GDN.py:65-69

@@ -268,14 +268,16 @@ int iclr17_grad_recon(const float* recon, const float* x, const float* g_mse, co
 int iclr17_bwd_deconv3_igdn(const float* g_recon, int B, int H, int W, int N,
                             const float* w_packed, const uint16_t* w_split, const float* v_saved,
                             const float* beta_eff, const float* gamma_packed,
-                            const float* gamma_packed_t, float* g_v, uint16_t* g_v_split,
+                            const float* gamma_packed_t,
+                            const uint16_t* gamma_split, const uint16_t* gamma_t_split, float* g_v, uint16_t* g_v_split,
                             float* dn, float* colsum_gv, float* colsum_dn, void* stream);
 /* synthesis_17.py:19-22 / :18 backward: g_v_prev = IGDNᵀ(conv2d(g_v, Wd, s2, p2)).
  * g_v NHWC [B,2h,2w,N]; v_prev = the previous deconv's pre-IGDN output NHWC [B,h,w,N]. */
 int iclr17_bwd_deconv_igdn(const float* g_v, const uint16_t* g_v_split, int B, int h, int w,
                            int N, const float* w_packed, const float* v_prev,
                            const float* beta_eff, const float* gamma_packed,
-                           const float* gamma_packed_t, float* g_v_prev, uint16_t* g_v_prev_split,
+                           const float* gamma_packed_t,
+                            const uint16_t* gamma_split, const uint16_t* gamma_t_split, float* g_v_prev, uint16_t* g_v_prev_split,
                            float* dn, float* colsum_gv, float* colsum_dn, void* stream);
 /* synthesis_17.py:15 backward + model.py:71-78 rate backward:
  * g_y = conv2d(g_v1, Wd1, s2, p2) + (*g_bpp / count)·∂bits/∂ỹ; per-tile rate parameter partials
@@ -290,7 +292,8 @@ int iclr17_rate_bwd_partials(int h, int w);
  * u_prev = the previous conv's pre-GDN output NHWC [B,2h,2w,N]. */
 int iclr17_bwd_conv_gdn(const float* g_u, const uint16_t* g_u_split, int B, int h, int w, int N,
                         const float* w_packed, const float* u_prev, const float* beta_eff,
-                        const float* gamma_packed, const float* gamma_packed_t, float* g_u_prev,
+                        const float* gamma_packed, const float* gamma_packed_t,
+                            const uint16_t* gamma_split, const uint16_t* gamma_t_split, float* g_u_prev,
                         uint16_t* g_u_prev_split, float* dn, float* colsum_gu, float* colsum_dn,
                         void* stream);
 /* x6 backward: the four GDN/rate backward kernels above take their incoming gradient in split
@@ -299,7 +302,8 @@ int iclr17_bwd_conv_gdn(const float* g_u, const uint16_t* g_u_split, int B, int 
  * may be NULL — and additionally write their outgoing gradient in split form when
  * *_prev_split / g_y_split / g_v_split is non-NULL. bwd_deconv3_igdn runs x6 when w_split (the
  * deconv3 weight packed ICLR17_W_CONV1_X6 and split by iclr17_split_packed(1, 256, N)) is
- * non-NULL; w_packed may then be NULL. */
+ * non-NULL; w_packed may then be NULL. gamma_split / gamma_t_split (nullable: iclr17_split_packed
+ * of gamma_packed and gamma_packed_t) run the two GDN-backward channel contractions in x6. */
 /* The three GDN-backward kernels above also emit (nullable) per-workgroup column sums of their
  * two outputs, [B * iclr17_bwd_tiles(kind, h, w)][N] floats: Σ ∂u is the preceding layer's bias
  * gradient and Σ dn is ∂β_eff. kind 0 (bwd_deconv3_igdn with (H/4, W/4), bwd_deconv_igdn with

@@ -48,6 +48,12 @@ def needs_grad(x: Optional[Tensor], params: Sequence[Tensor]) -> bool:
                                         any(p.requires_grad for p in params))
 
 
+def _split_of(saved: Dict[str, Tensor], key: str) -> Tensor:
+    """The split form of a saved activation (kept from the x6 forward, or split now)."""
+    s = saved.get(key + "s")
+    return s if s is not None else kernels.split_planes(saved[key])
+
+
 # ------------------------------------------------------------------------------ analysis
 def analysis_features_train(enc, x: Tensor):
     """conv1+GDN1, conv2+GDN2 keeping the pre-activations the backward needs. In the x6 mode the
@@ -60,10 +66,10 @@ def analysis_features_train(enc, x: Tensor):
                                           N, want_f32=True, want_pre=True)
         a2s, a2, u2 = kernels.conv2_gdn_x6(a1s, w2, enc.conv2.bias, *e2, want_f32=True,
                                            want_pre=True)
-        return a2, {"x": x, "u1": u1, "a1": a1, "u2": u2, "a2": a2, "a2s": a2s}
+        return a2, {"x": x, "u1": u1, "a1": a1, "u2": u2, "a2": a2, "a2s": a2s, "a1s": a1s}
     a1, u1 = kernels.conv1_gdn(x, w1, enc.conv1.bias, g1[0], g1[1], N, want_pre=True)
     a2, u2 = kernels.conv2_gdn(a1, w2, enc.conv2.bias, g2[0], g2[1], want_pre=True)
-    return a2, {"x": x, "u1": u1, "a1": a1, "u2": u2, "a2": a2, "a2s": None}
+    return a2, {"x": x, "u1": u1, "a1": a1, "u2": u2, "a2": a2, "a2s": None, "a1s": None}
 
 
 def analysis_backward(enc, saved: Dict[str, Tensor], g_y: Tensor,
@@ -84,14 +90,15 @@ def analysis_backward(enc, saved: Dict[str, Tensor], g_y: Tensor,
         g_u2, dn2, db2, dbe2, g_u2s = kernels.bwd_conv_gdn(g_y, w3t, saved["u2"], *x2[:3],
                                                            g_split=g_y_split, want_split=True,
                                                            g6=x2[3], g6t=x2[4])
-        dW3 = kernels.wgrad_k5(g_y, saved["a2"])
+        dW3 = kernels.wgrad_k5_x6(g_y_split, _split_of(saved, "a2"))
         g_u1, dn1, db1, dbe1 = kernels.bwd_conv_gdn(g_u2, w2t, saved["u1"], *x1[:3], g_split=g_u2s,
                                                     g6=x1[3], g6t=x1[4])
+        dW2 = kernels.wgrad_k5_x6(g_u2s, _split_of(saved, "a1"))
     else:
         g_u2, dn2, db2, dbe2 = kernels.bwd_conv_gdn(g_y, w3t, saved["u2"], *p2)
         dW3 = kernels.wgrad_k5(g_y, saved["a2"])
         g_u1, dn1, db1, dbe1 = kernels.bwd_conv_gdn(g_u2, w2t, saved["u1"], *p1)
-    dW2 = kernels.wgrad_k5(g_u2, saved["a1"])
+        dW2 = kernels.wgrad_k5(g_u2, saved["a1"])
     dW1 = kernels.wgrad_k9(g_u1, saved["x"])
     dbeta2, dgamma2 = kernels.gdn_param_grads(dn2, saved["u2"], dbe2, enc.gdn2.beta, enc.gdn2.gamma, bb2, gb2)
     dbeta1, dgamma1 = kernels.gdn_param_grads(dn1, saved["u1"], dbe1, enc.gdn1.beta, enc.gdn1.gamma, bb1, gb1)
@@ -114,11 +121,13 @@ def synthesis_forward_train(dec, y_nhwc: Tensor, x_ref: Optional[Tensor] = None,
                                              want_pre=True)
         clipped, recon, sse = kernels.deconv3_x6(s2s, d3, dec.deconv3.bias, x_ref=x_ref,
                                                  want_recon=True, sse_unclipped=x_ref is not None)
-    else:
-        s1, v1 = kernels.deconv_igdn(y_nhwc, d1, dec.deconv1.bias, q1[0], q1[1], want_pre=True)
-        s2, v2 = kernels.deconv_igdn(s1, d2, dec.deconv2.bias, q2[0], q2[1], want_pre=True)
-        clipped, recon, sse = kernels.deconv3(s2, d3, dec.deconv3.bias, x_ref=x_ref,
-                                              want_recon=True, sse_unclipped=x_ref is not None)
+        # the split forms of y and s1 are the x6 weight-gradient operands
+        return clipped, recon, sse, {"y": y_nhwc, "v1": v1, "s1": s1, "v2": v2, "s2": s2,
+                                     "ys": y_split, "s1s": s1s}
+    s1, v1 = kernels.deconv_igdn(y_nhwc, d1, dec.deconv1.bias, q1[0], q1[1], want_pre=True)
+    s2, v2 = kernels.deconv_igdn(s1, d2, dec.deconv2.bias, q2[0], q2[1], want_pre=True)
+    clipped, recon, sse = kernels.deconv3(s2, d3, dec.deconv3.bias, x_ref=x_ref,
+                                          want_recon=True, sse_unclipped=x_ref is not None)
     return clipped, recon, sse, {"y": y_nhwc, "v1": v1, "s1": s1, "v2": v2, "s2": s2}
 
 
@@ -151,10 +160,12 @@ def synthesis_backward(dec, saved: Dict[str, Tensor], g_recon: Tensor, g_bpp: Op
         g_v1, dnq1, dbd1, dbeq1, g_v1s = kernels.bwd_deconv_igdn(g_v2, d2c, saved["v1"], *q1[:3],
                                                                  g_split=g_v2s, want_split=True,
                                                                  g6=q1[3], g6t=q1[4])
-        dWd2 = kernels.wgrad_k5(saved["s1"], g_v2)
+        dWd2 = kernels.wgrad_k5_x6(_split_of(saved, "s1"), g_v2s)
         r = kernels.bwd_deconv_rate(g_v1, d1c, y if g_bpp is not None else None, rate_packed,
                                     g_bpp, count, h, w, g_split=g_v1s, want_split=want_split)
         g_y, rpart, g_ys = r if want_split else (*r, None)
+        dWd1 = kernels.wgrad_k5_x6(saved.get("ys") if saved.get("ys") is not None
+                                   else kernels.split_planes(y), g_v1s)
     else:
         g_v2, dnq2, dbd2, dbeq2 = kernels.bwd_deconv3_igdn(g_recon, d3c, saved["v2"], *q2)
         dWd3 = kernels.wgrad_k9(saved["s2"], g_recon)
@@ -163,7 +174,7 @@ def synthesis_backward(dec, saved: Dict[str, Tensor], g_recon: Tensor, g_bpp: Op
         dWd2 = kernels.wgrad_k5(saved["s1"], g_v2)
         g_y, rpart = kernels.bwd_deconv_rate(g_v1, d1c, y if g_bpp is not None else None,
                                              rate_packed, g_bpp, count, h, w)
-    dWd1 = kernels.wgrad_k5(y, g_v1)
+        dWd1 = kernels.wgrad_k5(y, g_v1)
     dbq2, dgq2 = kernels.gdn_param_grads(dnq2, saved["v2"], dbeq2, dec.igdn2.beta, dec.igdn2.gamma, bq2, gq2)
     dbq1, dgq1 = kernels.gdn_param_grads(dnq1, saved["v1"], dbeq1, dec.igdn1.beta, dec.igdn1.gamma, bq1, gq1)
     grads = {"deconv1.weight": dWd1, "deconv1.bias": dbd1, "igdn1.beta": dbq1, "igdn1.gamma": dgq1,
@@ -188,7 +199,7 @@ class CodecTrainFn(torch.autograd.Function):
         a2, saved_a = analysis_features_train(enc, x)
         _, _, w3, _, _ = enc.packed()
         rate = be.packed()
-        a2s = saved_a.pop("a2s")
+        a2s = saved_a.get("a2s")
         if a2s is not None:
             y_tilde, bits_part, _, y_split = kernels.conv3_quant_rate_x6(a2s, w3, rate, noise)
         else:
@@ -233,8 +244,7 @@ class AnalysisFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, enc, *params):
         ctx.set_materialize_grads(False)
-        a2, saved = analysis_features_train(enc, x)
-        saved.pop("a2s")
+        a2, saved = analysis_features_train(enc, x)   # a2s stays: conv3's x6 weight gradient
         _, _, w3, _, _ = enc.packed()
         ctx.enc, ctx.saved = enc, saved
         return kernels.conv3(a2, w3).permute(0, 3, 1, 2)

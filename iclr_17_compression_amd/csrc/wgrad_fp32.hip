@@ -128,6 +128,212 @@ __global__ void __launch_bounds__(256) wgrad_k5_kernel(const float* __restrict__
     }
 }
 
+// The same weight gradient in the bf16x6 scheme, from split-form operands (three bf16 planes, the
+// x6 activation format: G = ∂u or a synthesis activation, X = a layer input or ∂v). GEMM as above
+// but on v_mfma_f32_16x16x32_bf16 with K = 32 pixels per step: a workgroup owns one tap, MB rows
+// of M and 64 columns of C; 2×2 waves of (MB/2) × 32. Both tiles arrive by LDS-DMA as
+// [pixel][channel] bf16 rows (per plane), and the k-strided MFMA operands (8 consecutive pixels of
+// one channel) come out of ds_read_b64_tr_b16: a 16-lane group reads 4 pixel rows × 16 channels and
+// lane i receives channel i of the 4 rows — two reads make the 8-deep k-group. Six part products
+// (lo·hi, hi·lo, mid·mid, mid·hi, hi·mid, hi·hi) per 16×16 tile, fp32 accumulation. Partials land
+// in the same [split][m][c][tap] layout as wgrad_k5_kernel.
+typedef short s4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint2 tr16(const unsigned short* lds) {
+  const s4v v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)lds);
+  return __builtin_bit_cast(uint2, v);
+}
+
+template <int M, int CB, int WM, int WN>
+__global__ void __launch_bounds__(512) wgrad_k5_x6_kernel(const unsigned short* __restrict__ G6,
+                                                          long pg, const unsigned short* __restrict__ X6,
+                                                          long pxs, int B, int Ho, int Wo, int Hi,
+                                                          int Wi, int C, int nsplit,
+                                                          float* __restrict__ part) {
+  constexpr int NW = WM * WN;                        // 8 waves
+  constexpr int MT = M / WM / 16, NT = CB / WN / 16; // 16×16 tiles per wave
+  constexpr int GPL = KP * M, XPL = KP * CB;         // u16 per plane image
+  constexpr int STAGE = 3 * GPL + 3 * XPL;           // u16 per stage
+  constexpr int GPR = M / 8, XPR = CB / 8;           // 16-byte pieces per pixel row
+  constexpr int NGI = KP * GPR / 64, NXI = KP * XPR / 64;   // DMA wave-instructions per plane
+  constexpr int NI = 3 * NGI + 3 * NXI;
+  constexpr int NI_W = NI / NW;
+  static_assert(NW == 8 && MT * WM * 16 == M && NT * WN * 16 == CB, "tile shape");
+  static_assert(KP * GPR % 64 == 0 && KP * XPR % 64 == 0 && NI % NW == 0, "whole DMA slots");
+  static_assert(M == CB && (M == 192 || M == 128), "square layers, 384- or 256-byte rows");
+  __shared__ __attribute__((aligned(16))) unsigned short smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  // XCD-aware order: the hardware deals workgroup ids round-robin to the 8 XCDs (id % 8), so
+  // logical workgroup xcd·(n/8) + id/8 puts each split's consecutive tap workgroups on one XCD —
+  // they all read the same G chunk and overlapping X rows, which then hit that XCD's L2.
+  const int nwg = gridDim.x;                  // padded to a multiple of 8
+  const int L = (blockIdx.x % 8) * (nwg / 8) + blockIdx.x / 8;
+  const int tiles = 25 * (C / CB);
+  if (L >= tiles * nsplit) return;            // padding workgroups (before any barrier)
+  const int tile = L % tiles;
+  const int tap = tile % 25, ct = tile / 25;
+  // LDS images are XOR-swizzled by 16-byte piece: piece k of pixel row r sits at k ^ swz(r). A
+  // transposed read's 32-lane half touches rows {q, 8 + q} (+4), two pieces each; swz gives them
+  // disjoint bank windows (384-byte rows: the row parity already splits the 64 banks in two).
+  auto swz = [](int r) {
+    return M == 192 ? 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1))
+                    : 2 * ((r & 3) | (((r >> 3) & 1) << 2));
+  };
+  const int kh = tap / 5, kw = tap % 5;
+  const int split = L / tiles;
+  const long P = (long)B * Ho * Wo;
+  const long per = ((P + nsplit - 1) / nsplit + KP - 1) / KP * KP;
+  const long p0 = split * per;
+  const long p1 = p0 + per < P ? p0 + per : P;
+  const int nsteps = p1 > p0 ? (int)((p1 - p0 + KP - 1) / KP) : 0;
+
+  // DMA slot j of this wave: instruction i = wave + NW·j, a fixed plane and 16-byte piece column.
+  // G slots: a contiguous [pixel][M] row, 32-bit offset advanced by KP·M per step. X slots: the
+  // tap-shifted source pixel of output pixel p, tracked incrementally as (b, oh, ow); the 32-bit
+  // element offset moves by 2·KP·C while the step stays in the output row, else is recomputed.
+  int pj[NI_W], off[NI_W], ow_[NI_W], oh_[NI_W], b_[NI_W];
+  auto xoff = [&](int j) {
+    const int iy = oh_[j] * 2 - 2 + kh, ix = ow_[j] * 2 - 2 + kw;
+    return ((b_[j] * Hi + iy) * Wi + ix) * C;
+  };
+#pragma unroll
+  for (int j = 0; j < NI_W; ++j) {
+    const int i = wave + NW * j;
+    const bool isg = i < 3 * NGI;
+    const int pc = (isg ? (i % NGI) : ((i - 3 * NGI) % NXI)) * 64 + lane;
+    const int prow = isg ? pc / GPR : pc / XPR;
+    const int piece = (isg ? pc % GPR : pc % XPR) ^ swz(prow);
+    const long p = p0 + prow;
+    pj[j] = (int)p;
+    ow_[j] = (int)(p % Wo);
+    const long qq = p / Wo;
+    oh_[j] = (int)(qq % Ho);
+    b_[j] = (int)(qq / Ho);
+    off[j] = isg ? (int)p * M + piece * 8 : ct * CB + piece * 8;   // X: the channel part only
+  }
+  const int p1i = (int)p1;
+  int xo[NI_W];
+#pragma unroll
+  for (int j = 0; j < NI_W; ++j) xo[j] = xoff(j);
+  auto issue = [&](int buf) {
+    unsigned short* st = smem + buf * STAGE;
+#pragma unroll
+    for (int j = 0; j < NI_W; ++j) {
+      const int i = wave + NW * j;
+      const void* src = g_wzero;
+      unsigned short* dst;
+      if (i < 3 * NGI) {
+        const int pl = i / NGI, ii = i % NGI;
+        if (pj[j] < p1i) src = G6 + pl * pg + off[j];
+        dst = st + pl * GPL + ii * 512;
+      } else {
+        const int pl = (i - 3 * NGI) / NXI, ii = (i - 3 * NGI) % NXI;
+        const int iy = oh_[j] * 2 - 2 + kh, ix = ow_[j] * 2 - 2 + kw;
+        if (pj[j] < p1i && (unsigned)iy < (unsigned)Hi && (unsigned)ix < (unsigned)Wi)
+          src = X6 + pl * pxs + xo[j] + off[j];
+        dst = st + 3 * GPL + pl * XPL + ii * 512;
+      }
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
+  auto advance = [&]() {   // every slot's pixel moves on by KP
+#pragma unroll
+    for (int j = 0; j < NI_W; ++j) {
+      const int i = wave + NW * j;
+      pj[j] += KP;
+      if (i < 3 * NGI) {
+        off[j] += KP * M;
+      } else {
+        ow_[j] += KP;
+        if (ow_[j] < Wo) {
+          xo[j] += 2 * KP * C;
+        } else {
+          do {
+            ow_[j] -= Wo;
+            if (++oh_[j] == Ho) { oh_[j] = 0; ++b_[j]; }
+          } while (ow_[j] >= Wo);
+          xo[j] = xoff(j);
+        }
+      }
+    }
+  };
+
+  f4 acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
+  // transposed-read lane addresses: group g = lane >> 4 takes pixel rows 8g .. 8g+7 (two reads of
+  // 4); lane 4q + p of the group addresses row q, channels 4p .. 4p+3.
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const int fr = swz(8 * g + q);   // = swz(8g + q + 4): the row swizzle ignores bit 2
+  int aoff[MT], boff[NT];          // u16 offsets within a plane image (second read: + 4 rows)
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int ch = wm * (M / WM) + mt * 16 + 4 * pp;
+    aoff[mt] = (8 * g + q) * M + (((ch >> 3) ^ fr) << 3) + (ch & 7);
+  }
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int ch = wn * (CB / WN) + nt * 16 + 4 * pp;
+    boff[nt] = (8 * g + q) * CB + (((ch >> 3) ^ fr) << 3) + (ch & 7);
+  }
+
+  if (nsteps > 0) issue(0);
+  for (int s = 0; s < nsteps; ++s) {
+    __syncthreads();   // stage s landed for every wave; stage (s+1)&1 is free
+    if (s + 1 < nsteps) {
+      advance();
+      issue((s + 1) & 1);
+    }
+    const unsigned short* st = smem + (s & 1) * STAGE;
+    bf8 Bf[3][NT];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const unsigned short* b = st + 3 * GPL + pl * XPL + boff[nt];
+        const uint2 lo = tr16(b), hi = tr16(b + 4 * CB);
+        Bf[pl][nt] = __builtin_bit_cast(bf8, u4{lo.x, lo.y, hi.x, hi.y});
+      }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      bf8 Af[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+        const unsigned short* a = st + pl * GPL + aoff[mt];
+        const uint2 lo = tr16(a), hi = tr16(a + 4 * M);
+        Af[pl] = __builtin_bit_cast(bf8, u4{lo.x, lo.y, hi.x, hi.y});
+      }
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        f4 c = acc[mt][nt];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af[2], Bf[0][nt], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af[0], Bf[2][nt], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af[1], Bf[1][nt], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af[1], Bf[0][nt], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af[0], Bf[1][nt], c, 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af[0], Bf[0][nt], c, 0, 0, 0);
+      }
+    }
+  }
+  // part[split][m][c][tap]: lane holds rows 4(lane >> 4) + r, column lane & 15 of each tile
+  float* out = part + (long)split * M * C * 25;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = wm * (M / WM) + mt * 16 + 4 * (lane >> 4) + r;
+        const int c = ct * CB + wn * (CB / WN) + nt * 16 + (lane & 15);
+        out[((long)m * C + c) * 25 + tap] = acc[mt][nt][r];
+      }
+}
+
 // conv1 / deconv3 weight gradient: K = 243 = (c, kh, kw) of a 9×9 stride-4 pad-4 window on a
 // 3-channel NCHW image X; pixels iterate over 8×8 output tiles whose 37×37×3 input patch is
 // staged in LDS (as in the conv1 forward kernel).
@@ -278,6 +484,14 @@ __global__ void plane_sum_kernel(const float* __restrict__ A, int C, long HW, fl
   if (threadIdx.x == 0) part[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
 }
 
+// x6 wgrad: a workgroup owns all M rows and 192 | 128 columns (C % that == 0), one per CU
+int wgrad6_cb(int C) { return C % 192 == 0 ? 192 : 128; }
+int wgrad6_splits(long P, int tiles) {   // one round of 256 workgroup slots (1 per CU)
+  int s = 256 / tiles;
+  const long maxs = P / 256 > 1 ? P / 256 : 1;
+  if (s > maxs) s = (int)maxs;
+  return s < 1 ? 1 : s;
+}
 int wgrad9_splits(int ntiles) { return ntiles < 128 ? ntiles : 128; }
 
 int wgrad_splits(long P, int tiles) {
@@ -303,6 +517,7 @@ int iclr17_sum_rows(const float* part, int T, int C, float* workspace, float* ou
 size_t iclr17_wgrad_workspace_size(int kind, int B, int Ho, int Wo, int M, int C) {
   const long P = (long)B * Ho * Wo;
   if (kind == 9) return (size_t)wgrad9_splits(B * ((Wo + 7) / 8) * ((Ho + 7) / 8)) * M * 243;
+  if (kind == 6) return (size_t)wgrad6_splits(P, 25 * (C / wgrad6_cb(C))) * M * C * 25;
   const int ntap = kind == 1 ? 1 : 25;
   const int tiles = ntap * (C / 64);
   return (size_t)wgrad_splits(P, tiles) * M * C * ntap;
@@ -330,6 +545,31 @@ int iclr17_wgrad_k5(const float* G, const float* X, int B, int Ho, int Wo, int M
   return check_launch("wgrad_k5_sum");
 }
 
+int iclr17_wgrad_k5_x6(const uint16_t* G_split, const uint16_t* X_split, int B, int Ho, int Wo,
+                       int M, int C, float* workspace, float* dW, void* stream) {
+  ICLR17_REQUIRE(B > 0 && Ho > 0 && Wo > 0, ICLR17_EINVAL, "wgrad_k5_x6: bad shape");
+  ICLR17_REQUIRE((M == 128 || M == 192) && C % 64 == 0 && C > 0, ICLR17_EUNSUPPORTED,
+                 "wgrad_k5_x6: M=%d C=%d unsupported", M, C);
+  ICLR17_REQUIRE(G_split && X_split && workspace && dW, ICLR17_EINVAL, "wgrad_k5_x6: null pointer");
+  const long P = (long)B * Ho * Wo;
+  ICLR17_REQUIRE(M == C, ICLR17_EUNSUPPORTED, "wgrad_k5_x6: M=%d C=%d (square layers only)", M, C);
+  const int tiles = 25 * (C / wgrad6_cb(C));
+  const int ns = wgrad6_splits(P, tiles);
+  const long pg = P * M, pxs = (long)B * 4 * Ho * Wo * C;
+  hipStream_t st = S(stream);
+  dim3 grid((tiles * ns + 7) / 8 * 8);   // 1-D, padded to whole XCD rounds (see the kernel)
+  const unsigned short* g6 = (const unsigned short*)G_split;
+  const unsigned short* x6 = (const unsigned short*)X_split;
+  if (M == 192)
+    hipLaunchKernelGGL((wgrad_k5_x6_kernel<192, 192, 2, 4>), grid, dim3(512), 0, st, g6, pg, x6, pxs, B, Ho, Wo, 2 * Ho, 2 * Wo, C, ns, workspace);
+  else
+    hipLaunchKernelGGL((wgrad_k5_x6_kernel<128, 128, 2, 4>), grid, dim3(512), 0, st, g6, pg, x6, pxs, B, Ho, Wo, 2 * Ho, 2 * Wo, C, ns, workspace);
+  int rc = check_launch("wgrad_k5_x6");
+  if (rc) return rc;
+  const long n = (long)M * C * 25;
+  hipLaunchKernelGGL(sum_splits_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, workspace, ns, n, dW);
+  return check_launch("wgrad_k5_x6_sum");
+}
 int iclr17_wgrad_k9(const float* G, const float* X, int B, int Ho, int Wo, int M,
                     float* workspace, float* dW, void* stream) {
   ICLR17_REQUIRE(B > 0 && Ho > 0 && Wo > 0, ICLR17_EINVAL, "wgrad_k9: bad shape");

@@ -715,6 +715,22 @@ def wgrad_k5(G: Tensor, X: Tensor) -> Tensor:
     return dW
 
 
+def wgrad_k5_x6(G_split: Tensor, X_split: Tensor) -> Tensor:
+    """wgrad_k5 in x6 from split-form operands (G_split [3,B,Ho,Wo,M], X_split [3,B,2Ho,2Wo,C])."""
+    _check_split(G_split, "wgrad G")
+    _check_split(X_split, "wgrad X")
+    _, B, Ho, Wo, M = G_split.shape
+    C = X_split.shape[4]
+    if tuple(X_split.shape[1:4]) != (B, 2 * Ho, 2 * Wo):
+        raise Iclr17Error(f"iclr17: wgrad_k5_x6: X {tuple(X_split.shape)} vs G {tuple(G_split.shape)}")
+    ws = torch.empty(query("iclr17_wgrad_workspace_size", 6, B, Ho, Wo, M, C), device=G_split.device,
+                     dtype=torch.float32)
+    dW = torch.empty(M, C, 5, 5, device=G_split.device, dtype=torch.float32)
+    call("iclr17_wgrad_k5_x6", _p(G_split), _p(X_split), B, Ho, Wo, M, C, _p(ws), _p(dW),
+         _stream(G_split))
+    return dW
+
+
 def wgrad_k9(G: Tensor, X: Tensor) -> Tensor:
     """dW [M][3][9][9] = Σ G[b,o,m] · X[b,c,4o−4+k] (G NHWC [B,Ho,Wo,M], X NCHW [B,3,4Ho,4Wo])."""
     B, Ho, Wo, M = G.shape

@@ -319,6 +319,11 @@ size_t iclr17_sum_rows_workspace_size(int C);   /* floats */
 size_t iclr17_wgrad_workspace_size(int kind, int B, int Ho, int Wo, int M, int C);
 int iclr17_wgrad_k5(const float* G, const float* X, int B, int Ho, int Wo, int M, int C,
                     float* workspace, float* dW, void* stream);
+/* wgrad_k5 in the bf16x6 scheme from split-form operands: G_split [3][B][Ho][Wo][M], X_split
+ * [3][B][2Ho][2Wo][C] (the x6 activation format); workspace: iclr17_wgrad_workspace_size(6, ...)
+ * floats. */
+int iclr17_wgrad_k5_x6(const uint16_t* G_split, const uint16_t* X_split, int B, int Ho, int Wo,
+                       int M, int C, float* workspace, float* dW, void* stream);
 int iclr17_wgrad_k9(const float* G, const float* X, int B, int Ho, int Wo, int M,
                     float* workspace, float* dW, void* stream);
 /* GDN.py:83 weight gradient: dgamma_eff[i][j] = Σ_p dn[p][i]·u[p][j]² (dβ_eff = Σ_p dn comes

@@ -130,3 +130,17 @@ def test_backward_is_deterministic(device):
         grads.append({k: p.grad.clone() for k, p in net.named_parameters()})
     for k in grads[0]:
         assert torch.equal(grads[0][k], grads[1][k]), k
+
+
+@pytest.mark.parametrize("M,C,B,Ho,Wo", [(192, 192, 2, 16, 16), (192, 192, 3, 8, 12), (128, 128, 2, 32, 32)])
+def test_wgrad_k5_x6_matches_fp32(device, M, C, B, Ho, Wo):
+    """The x6 weight gradient (split-form operands, ds_read_b64_tr_b16 fragments) against the
+    exact-f32 wgrad_k5 on the same values: the split is exact, so only rounding differs.
+    Partial last k-step (B·Ho·Wo not a multiple of 32 per split) at 3×8×12."""
+    from iclr_17_compression_amd import kernels
+    G = torch.from_numpy(synth.normal_like(21, (B, Ho, Wo, M), 1.0)).to(device)
+    X = torch.from_numpy(synth.normal_like(22, (B, 2 * Ho, 2 * Wo, C), 1.0)).to(device)
+    ref = kernels.wgrad_k5(G, X)
+    got = kernels.wgrad_k5_x6(kernels.split_planes(G), kernels.split_planes(X))
+    torch.cuda.synchronize()
+    assert grad_err(got, ref) < 1e-5

@@ -23,6 +23,7 @@ rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit 1; fi
 step bench 600 python bench.py || exit 1
 step bench_train 600 python bench.py --mode train --batch 32 --steps 10 --warmup 3 || exit 1
 step bench_kodak 600 python bench.py --mode kodak --steps 5 --warmup 2 || exit 1
+step bench_2048 600 python bench.py --no-cpu-baseline --size 2048 --batch 8 --steps 10 --warmup 3 || exit 1
 cd /tmp
 step prof_eval 600 rocprofv3 --kernel-trace --stats -d "$O/prof_eval" -o run --output-format csv -- \
   python "$R/bench.py" --no-cpu-baseline --steps 10 --warmup 3 || exit 1

@@ -25,9 +25,9 @@ LAYER_KERNELS = {
         "deconv3_clamp": r"engine_kernel<192, 48, 48, 4, 1, 3, false, false>",
     },
     "x6": {
-        "conv1_gdn1": r"conv1_gdn_kernel<192, 0, true>",
+        "conv1_gdn1": r"conv1_x6_kernel<192, 0>",
         "conv2_gdn2": r"engine_kernel<192, 192, 192, 1, 4, 0, false, true>",
-        "conv3_quant_rate": r"engine_kernel<192, 192, 64, 1, 4, 2, false, true>",
+        "conv3_quant_rate": r"engine_kernel<192, 192, 96, 2, 2, 2, false, true>",
         "deconv1_igdn1": r"engine_kernel<192, 192, 192, 1, 4, 1, false, true>",
         "deconv2_igdn2": r"engine_kernel_occ2<192, 192, 192, 1, 4, 1, true, true>",
         "deconv3_clamp": r"deconv3_x6_kernel<192>",

@@ -74,6 +74,10 @@ SIGNATURES = {
     "iclr17_ms_ssim_workspace_size": (_SZ, [_I, _I, _I]),
     "iclr17_ms_ssim": (_I, [_P, _P, _I, _I, _I, _F, _P, _SZ, _P, _P]),
     "iclr17_gdn": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "iclr17_gdn_bwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_bitest_bwd_chunks": (_I, [_I64, _I]),
+    "iclr17_bit_estimator_bwd": (_I, [_P, _P, _I64, _I, _I64, _P, _P, _P, _P]),
+    "iclr17_bitparm_bwd": (_I, [_P, _P, _I64, _I, _I64, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_bit_estimator": (_I, [_P, _I64, _I, _I64, _P, _P, _P]),
     "iclr17_bitparm": (_I, [_P, _I64, _I, _I64, _P, _P, _P, _P, _P]),
     "iclr17_rate_bits": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P]),

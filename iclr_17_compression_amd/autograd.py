@@ -38,9 +38,73 @@ def no_backward(out: Tensor, name: str, params: Sequence[Tensor], x: Tensor):
 
 
 def gdn_apply(x: Tensor, module) -> Tensor:
+    if needs_grad(x, (module.beta, module.gamma)):
+        return GDNFn.apply(x, module, module.beta, module.gamma)
     beta_eff, gp = module.effective_params()
-    out = kernels.gdn(x, beta_eff, gp, module.inverse)
-    return no_backward(out, "GDN", (module.beta, module.gamma), x)
+    return kernels.gdn(x, beta_eff, gp, module.inverse)
+
+
+class GDNFn(torch.autograd.Function):
+    """Stand-alone GDN / IGDN (GDN.py:64-94) with its autograd: ∂x from the fused backward
+    kernel, ∂β / ∂γ through GDN.py:73-79 (LowerBound's gradient rule included)."""
+
+    @staticmethod
+    def forward(ctx, x, module, beta, gamma):
+        beta_eff, gp = module.effective_params()
+        ctx.module = module
+        ctx.save_for_backward(x)
+        return kernels.gdn(x, beta_eff, gp, module.inverse)
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        m = ctx.module
+        be, gp, gpt = m.effective_params_bwd()
+        dx, dn, u = kernels.gdn_backward(x, g, be, gp, gpt, m.inverse)
+        bb, gb, _ = m.bounds_f32()
+        dbeta, dgamma = kernels.gdn_param_grads(dn, u, kernels.bias_grad_nhwc(dn), m.beta, m.gamma,
+                                                bb, gb)
+        return dx, None, dbeta.view_as(m.beta), dgamma.view_as(m.gamma)
+
+
+class BitEstimatorFn(torch.autograd.Function):
+    """BitEstimator.forward (bitEstimator.py:38-42) with its autograd."""
+
+    @staticmethod
+    def forward(ctx, x, module, *params):
+        ctx.module = module
+        ctx.save_for_backward(x)
+        return kernels.bit_estimator(x, module.packed(), module.channel)
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        m = ctx.module
+        dx, part = kernels.bit_estimator_backward(x, g, m.packed(), m.channel)
+        grads = kernels.rate_param_grads(part, m.params_in_order())
+        return (dx.view_as(x), None, *[gr.view_as(p) for gr, p in zip(grads, m.params_in_order())])
+
+
+class BitparmFn(torch.autograd.Function):
+    """One Bitparm layer (bitEstimator.py:20-25) with its autograd."""
+
+    @staticmethod
+    def forward(ctx, x, module, *params):
+        ctx.module = module
+        ctx.save_for_backward(x)
+        return kernels.bitparm(x, module.h, module.b, module.a)
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        m = ctx.module
+        dx, part = kernels.bitparm_backward(x, g, m.h, m.b, m.a)
+        if m.a is not None:   # slots 0-2 of the rate table: (h, b, a) as BitEstimator's f1
+            grads = kernels.rate_param_grads(part, [m.h, m.b, m.a] * 3 + [m.h, m.b])[:3]
+        else:                 # slots 9-10: the final layer's (h, b)
+            grads = kernels.rate_param_grads(part, [m.h, m.b, m.h] * 3 + [m.h, m.b])[9:]
+        ps = [p for p in (m.h, m.b, m.a) if p is not None]
+        return (dx.view_as(x), None, *[gr.view_as(p) for gr, p in zip(grads, ps)])
 
 
 def needs_grad(x: Optional[Tensor], params: Sequence[Tensor]) -> bool:

@@ -153,6 +153,89 @@ __global__ void bitparm_kernel(const float* __restrict__ x, int64_t n, int C, in
   }
 }
 
+// Autograd of the stand-alone BitEstimator / Bitparm forward (bitEstimator.py:20-42) for an
+// upstream gradient g = ∂L/∂out, op for op as rate_bwd_element (engine_fp32.hip) does for the
+// rate term. rp is the packed [11][C] table (softplus(h_k), b_k, tanh(a_k) for k = 1..3 at
+// slots 3k-3.., softplus(h4), b4 at 9, 10). MODE 0: the 4-layer BitEstimator; 1: one non-final
+// Bitparm (slots 0-2); 2: the final Bitparm (slots 9, 10). One workgroup per (channel, chunk of
+// that channel's elements): ∂x per element, and the 11 per-channel parameter partials summed in
+// a fixed order into partial[chunk][11][C] (iclr17_rate_param_grad turns them into ∂h, ∂b, ∂a).
+template <int MODE>
+__global__ void __launch_bounds__(256) bitest_bwd_kernel(const float* __restrict__ x,
+                                                         const float* __restrict__ g, int64_t E,
+                                                         int C, int64_t inner,
+                                                         const float* __restrict__ rp,
+                                                         float* __restrict__ dx, int64_t per,
+                                                         float* __restrict__ partial) {
+  __shared__ float red[4][11];
+  const int c = blockIdx.x, chunk = blockIdx.y;
+  const int64_t e0 = (int64_t)chunk * per;
+  const int64_t e1 = e0 + per < E ? e0 + per : E;
+  constexpr int K0 = MODE == 1 ? 0 : (MODE == 2 ? 3 : 0);   // first non-final layer
+  constexpr int K1 = MODE == 1 ? 1 : (MODE == 2 ? 0 : 3);   // non-final layers
+  constexpr bool FINAL = MODE != 1;
+  float pg[11];
+#pragma unroll
+  for (int k = 0; k < 11; ++k) pg[k] = 0.f;
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += 256) {
+    const int64_t i = (e / inner) * C * inner + (int64_t)c * inner + e % inner;
+    float v = x[i];
+    float xs[4], Ts[3];
+#pragma unroll
+    for (int k = 0; k < K1; ++k) {
+      xs[k] = v;
+      const float t = v * rp[(3 * (K0 + k)) * C + c] + rp[(3 * (K0 + k) + 1) * C + c];
+      const float T = tanhf(t);
+      v = t + T * rp[(3 * (K0 + k) + 2) * C + c];
+      Ts[k] = T;
+    }
+    float gx = g[i];
+    if (FINAL) {
+      xs[3] = v;
+      const float F = 1.0f / (1.0f + expf(-(v * rp[9 * C + c] + rp[10 * C + c])));
+      const float gt4 = (gx * (1.0f - F)) * F;              // sigmoid backward
+      pg[10] += gt4;                                        // b4
+      pg[9] += gt4 * xs[3];                                 // softplus(h4)
+      gx = gt4 * rp[9 * C + c];
+    }
+#pragma unroll
+    for (int k = K1 - 1; k >= 0; --k) {
+      const int s3 = 3 * (K0 + k);
+      const float T = Ts[k];
+      const float gT = gx * rp[(s3 + 2) * C + c];
+      pg[s3 + 2] += gx * T;                                 // tanh(a_k)
+      const float gt = gx + gT * (1.0f - T * T);            // tanh backward
+      pg[s3 + 1] += gt;                                     // b_k
+      pg[s3] += gt * xs[k];                                 // softplus(h_k)
+      gx = gt * rp[s3 * C + c];
+    }
+    dx[i] = gx;
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 11; ++k) {
+    const float v = wave_sum(pg[k]);
+    if (lane == 0) red[wave][k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 11) {
+    const int k = threadIdx.x;
+    partial[((int64_t)chunk * 11 + k) * C + c] = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
+  }
+}
+
+// One Bitparm's parameters into the packed [11][C] slots its MODE reads (zeros elsewhere).
+__global__ void pack_bitparm_kernel(const float* __restrict__ h, const float* __restrict__ b,
+                                    const float* __restrict__ a, float* __restrict__ rp, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  for (int k = 0; k < 11; ++k) rp[k * C + c] = 0.f;
+  const int s = a != nullptr ? 0 : 9;
+  rp[s * C + c] = softplus_ref(h[c]);
+  rp[(s + 1) * C + c] = b[c];
+  if (a != nullptr) rp[2 * C + c] = tanhf(a[c]);
+}
+
 __global__ void softplus_tanh_kernel(const float* __restrict__ h, const float* __restrict__ a,
                                      float* __restrict__ sp, float* __restrict__ ta, int C) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -374,6 +457,51 @@ int iclr17_bitparm(const float* x, int64_t n, int C, int64_t inner, const float*
   hipLaunchKernelGGL(bitparm_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, n, C, inner, sp,
                      b, ta, out);
   return check_launch("bitparm");
+}
+
+int iclr17_bitest_bwd_chunks(int64_t n, int C) {
+  const int64_t E = C > 0 ? n / C : 0;   // elements per channel
+  const int64_t per = 16384;
+  int64_t t = (E + per - 1) / per;
+  return (int)(t < 1 ? 1 : t);
+}
+
+static int bitest_bwd_launch(int mode, const float* x, const float* g, int64_t n, int C,
+                             int64_t inner, const float* rp, float* dx, float* partial,
+                             hipStream_t st) {
+  const int T = iclr17_bitest_bwd_chunks(n, C);
+  const int64_t E = n / C;
+  const int64_t per = (E + T - 1) / T;
+  const dim3 grid(C, T);
+  if (mode == 0)
+    hipLaunchKernelGGL(bitest_bwd_kernel<0>, grid, dim3(256), 0, st, x, g, E, C, inner, rp, dx, per, partial);
+  else if (mode == 1)
+    hipLaunchKernelGGL(bitest_bwd_kernel<1>, grid, dim3(256), 0, st, x, g, E, C, inner, rp, dx, per, partial);
+  else
+    hipLaunchKernelGGL(bitest_bwd_kernel<2>, grid, dim3(256), 0, st, x, g, E, C, inner, rp, dx, per, partial);
+  return check_launch("bit_estimator_bwd");
+}
+
+int iclr17_bit_estimator_bwd(const float* x, const float* g, int64_t n, int C, int64_t inner,
+                             const float* rate_packed, float* dx, float* partial, void* stream) {
+  ICLR17_REQUIRE(n > 0 && C > 0 && inner > 0 && n % C == 0, ICLR17_EINVAL,
+                 "bit_estimator_bwd: bad shape");
+  ICLR17_REQUIRE(x && g && rate_packed && dx && partial, ICLR17_EINVAL,
+                 "bit_estimator_bwd: null pointer");
+  return bitest_bwd_launch(0, x, g, n, C, inner, rate_packed, dx, partial, S(stream));
+}
+
+int iclr17_bitparm_bwd(const float* x, const float* g, int64_t n, int C, int64_t inner,
+                       const float* h, const float* b, const float* a, float* work, float* dx,
+                       float* partial, void* stream) {
+  ICLR17_REQUIRE(n > 0 && C > 0 && inner > 0 && n % C == 0, ICLR17_EINVAL, "bitparm_bwd: bad shape");
+  ICLR17_REQUIRE(x && g && h && b && work && dx && partial, ICLR17_EINVAL,
+                 "bitparm_bwd: null pointer");
+  hipStream_t st = S(stream);
+  hipLaunchKernelGGL(pack_bitparm_kernel, dim3((C + 255) / 256), dim3(256), 0, st, h, b, a, work, C);
+  int rc = check_launch("bitparm_bwd_pack");
+  if (rc) return rc;
+  return bitest_bwd_launch(a != nullptr ? 1 : 2, x, g, n, C, inner, work, dx, partial, st);
 }
 
 int iclr17_rate_bits_partials(int C, int h, int w) {

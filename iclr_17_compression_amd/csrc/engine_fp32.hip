@@ -1661,6 +1661,114 @@ __global__ void __launch_bounds__(256) gdn_kernel(const float* __restrict__ x, i
   }
 }
 
+// ------------------------------------------------------------ stand-alone GDN / IGDN backward
+// Autograd of GDN.forward (models/GDN.py:64-94) for the stand-alone module: from x (= u) and
+// g = ∂L/∂y, the same op-for-op chain as gdn_bwd_epilogue — n = β + γ·u², s = √n,
+//   GDN : ∂u = g/s + 2u·(γᵀ dn),  dn = ((−g·u)/(s·s)) / (2s)
+//   IGDN: ∂u = g·s + 2u·(γᵀ dn),  dn = (g·u) / (2s)
+// — on 64 pixels of one image per workgroup (linear pixel order, ragged last tile). Writes ∂x in
+// the input's layout, dn NHWC [B·HW][C] (for dβ = Σ dn and dγ = Σ dn ⊗ u²) and, for an NCHW
+// input, u NHWC (the operand of the γ gradient).
+template <int C, bool INVERSE, int LAYOUT>
+__global__ void __launch_bounds__(256) gdn_bwd_kernel(const float* __restrict__ x,
+                                                      const float* __restrict__ gy, int HW,
+                                                      const float* __restrict__ beta,
+                                                      const float* __restrict__ gp,
+                                                      const float* __restrict__ gpt, float* dx,
+                                                      float* dn_out, float* u_out) {
+  constexpr int XS = C + 8;
+  constexpr int WN = 4, MT = 4, NT = C / WN / 16;
+  __shared__ __attribute__((aligned(16))) float smem[BM * XS + GSTAGE_FLOATS(C)];
+  float* sX = smem;
+  float* sG = smem + BM * XS;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles = (HW + BM - 1) / BM;
+  const int b = blockIdx.x / tiles, p0 = (blockIdx.x % tiles) * BM;
+  const int np = HW - p0 < BM ? HW - p0 : BM;
+  const int ncol0 = wave * (C / WN);
+  auto gidx = [&](int pl, int c) -> long {   // element (pixel p0 + pl, channel c) of x / g / ∂x
+    return LAYOUT == ICLR17_LAYOUT_NCHW ? ((long)b * C + c) * HW + p0 + pl
+                                        : ((long)b * HW + p0 + pl) * C + c;
+  };
+  for (int idx = tid; idx < BM * C; idx += 256) {
+    const int pl = LAYOUT == ICLR17_LAYOUT_NCHW ? idx % BM : idx / C;
+    const int c = LAYOUT == ICLR17_LAYOUT_NCHW ? idx / BM : idx % C;
+    sX[pl * XS + c] = pl < np ? x[gidx(pl, c)] : 0.f;
+  }
+  f4 g[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int pl = mt * 16 + 4 * (lane >> 4) + r, c = ncol0 + nt * 16 + (lane & 15);
+        g[mt][nt][r] = pl < np ? gy[gidx(pl, c)] : 0.f;
+      }
+  f4 acc2[MT][NT];
+  chan_gemm_lds<C, MT, NT, true>(acc2, sX, gp, sG, 0, ncol0, lane, wave);   // Σ_j γ[i][j] u_j²
+  __syncthreads();
+  f4 u[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = ncol0 + nt * 16 + (lane & 15);
+        const int i = (mt * 16 + 4 * (lane >> 4) + r) * XS + col;
+        const float uu = sX[i];
+        const float sq = sqrtf(acc2[mt][nt][r] + beta[col]);
+        const float gg = g[mt][nt][r];
+        float dn;
+        if (INVERSE) {
+          g[mt][nt][r] = gg * sq;
+          dn = (gg * uu) / (2.0f * sq);
+        } else {
+          g[mt][nt][r] = gg / sq;
+          dn = ((-gg * uu) / (sq * sq)) / (2.0f * sq);
+        }
+        u[mt][nt][r] = uu;
+        sX[i] = dn;
+      }
+  chan_gemm_lds<C, MT, NT>(acc2, sX, gpt, sG, 0, ncol0, lane, wave);   // w_j = Σ_i γ[i][j] dn_i
+  for (int idx = tid; idx < np * (C / 4); idx += 256) {   // dn rows (NHWC)
+    const int pl = idx / (C / 4), c4 = idx % (C / 4);
+    *(f4*)(dn_out + ((long)b * HW + p0 + pl) * C + c4 * 4) = *(const f4*)(sX + pl * XS + c4 * 4);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = (mt * 16 + 4 * (lane >> 4) + r) * XS + ncol0 + nt * 16 + (lane & 15);
+        sX[i] = g[mt][nt][r] + acc2[mt][nt][r] * (2.0f * u[mt][nt][r]);
+      }
+  __syncthreads();
+  for (int idx = tid; idx < BM * C; idx += 256) {
+    const int pl = LAYOUT == ICLR17_LAYOUT_NCHW ? idx % BM : idx / C;
+    const int c = LAYOUT == ICLR17_LAYOUT_NCHW ? idx / BM : idx % C;
+    if (pl < np) dx[gidx(pl, c)] = sX[pl * XS + c];
+  }
+  if (u_out != nullptr) {
+    __syncthreads();
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          sX[(mt * 16 + 4 * (lane >> 4) + r) * XS + ncol0 + nt * 16 + (lane & 15)] = u[mt][nt][r];
+    __syncthreads();
+    for (int idx = tid; idx < np * (C / 4); idx += 256) {
+      const int pl = idx / (C / 4), c4 = idx % (C / 4);
+      *(f4*)(u_out + ((long)b * HW + p0 + pl) * C + c4 * 4) = *(const f4*)(sX + pl * XS + c4 * 4);
+    }
+  }
+}
+
 // ====================================================================================== host
 namespace {
 
@@ -2327,6 +2435,33 @@ int iclr17_bwd_conv_gdn(const float* g_u, const uint16_t* g_u_split, int B, int 
   io.out_plane = (long)B * 2 * h * 2 * w * N;
   return N == 192 ? launch_deconv5<192, EPI_GDN_BWD>(g_u, B, h, w, w_packed, nullptr, beta_eff, gamma_packed, g_u_prev, nullptr, S(stream), &b, &io)
                   : launch_deconv5<128, EPI_GDN_BWD>(g_u, B, h, w, w_packed, nullptr, beta_eff, gamma_packed, g_u_prev, nullptr, S(stream), &b, &io);
+}
+
+int iclr17_gdn_bwd(const float* x, const float* g, int B, int C, int H, int W, int layout,
+                   int inverse, const float* beta_eff, const float* gamma_packed,
+                   const float* gamma_packed_t, float* dx, float* dn, float* u_nhwc,
+                   void* stream) {
+  ICLR17_REQUIRE(B > 0 && H > 0 && W > 0, ICLR17_EINVAL, "gdn_bwd: bad shape");
+  ICLR17_REQUIRE(C == 128 || C == 192, ICLR17_EUNSUPPORTED, "gdn_bwd: C=%d unsupported (128, 192)", C);
+  ICLR17_REQUIRE(layout == ICLR17_LAYOUT_NCHW || layout == ICLR17_LAYOUT_NHWC, ICLR17_EINVAL,
+                 "gdn_bwd: bad layout %d", layout);
+  ICLR17_REQUIRE(x && g && beta_eff && gamma_packed && gamma_packed_t && dx && dn, ICLR17_EINVAL,
+                 "gdn_bwd: null pointer");
+  const int HW = H * W;
+  dim3 grid(B * ((HW + BM - 1) / BM));
+  hipStream_t st = S(stream);
+#define ICLR17_GDNB_LAUNCH(CC, INV, LAY)                                                        \
+  hipLaunchKernelGGL((gdn_bwd_kernel<CC, INV, LAY>), grid, dim3(256), 0, st, x, g, HW, beta_eff, \
+                     gamma_packed, gamma_packed_t, dx, dn, u_nhwc)
+  if (C == 192) {
+    if (inverse) { if (layout == ICLR17_LAYOUT_NCHW) ICLR17_GDNB_LAUNCH(192, true, 0); else ICLR17_GDNB_LAUNCH(192, true, 1); }
+    else { if (layout == ICLR17_LAYOUT_NCHW) ICLR17_GDNB_LAUNCH(192, false, 0); else ICLR17_GDNB_LAUNCH(192, false, 1); }
+  } else {
+    if (inverse) { if (layout == ICLR17_LAYOUT_NCHW) ICLR17_GDNB_LAUNCH(128, true, 0); else ICLR17_GDNB_LAUNCH(128, true, 1); }
+    else { if (layout == ICLR17_LAYOUT_NCHW) ICLR17_GDNB_LAUNCH(128, false, 0); else ICLR17_GDNB_LAUNCH(128, false, 1); }
+  }
+#undef ICLR17_GDNB_LAUNCH
+  return check_launch("gdn_bwd");
 }
 
 int iclr17_gdn(const float* x, int B, int C, int H, int W, int layout, int inverse,

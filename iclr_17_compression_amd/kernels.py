@@ -570,6 +570,68 @@ def bitparm(x: Tensor, h: Tensor, b: Tensor, a: Optional[Tensor]) -> Tensor:
     return out
 
 
+def gdn_backward(x: Tensor, g: Tensor, beta_eff: Tensor, gp: Tensor, gpt: Tensor, inverse: bool):
+    """Autograd of ``gdn`` (GDN.py:64-94) → (∂x in x's layout, dn NHWC [P, C], u NHWC [P, C])."""
+    _check(x, "input", 4)
+    B, C, H, W = x.shape
+    _check_channels(C)
+    if x.is_contiguous():
+        layout, src = _lib.ICLR17_LAYOUT_NCHW, x
+    elif x.is_contiguous(memory_format=torch.channels_last):
+        layout, src = _lib.ICLR17_LAYOUT_NHWC, x
+    else:
+        layout, src = _lib.ICLR17_LAYOUT_NCHW, x.contiguous()
+    mf = torch.channels_last if layout == _lib.ICLR17_LAYOUT_NHWC else torch.contiguous_format
+    gs = g.contiguous(memory_format=mf)
+    dx = torch.empty_like(src, memory_format=mf)
+    P = B * H * W
+    dn = torch.empty(P, C, device=x.device, dtype=torch.float32)
+    u = torch.empty(P, C, device=x.device, dtype=torch.float32) if layout == _lib.ICLR17_LAYOUT_NCHW else None
+    call("iclr17_gdn_bwd", _p(src), _p(gs), B, C, H, W, layout, int(bool(inverse)), _p(beta_eff),
+         _p(gp), _p(gpt), _p(dx), _p(dn), _p(u), _stream(x))
+    if u is None:   # NHWC input: x itself is the [P, C] operand
+        u = src.permute(0, 2, 3, 1).reshape(P, C)
+    return dx, dn, u
+
+
+def _like_layout(g: Tensor, src: Tensor) -> Tensor:
+    """g in src's memory layout (contiguous, or channels-last for a channels-last 4-D src)."""
+    if src.dim() == 4 and not src.is_contiguous():
+        return g.contiguous(memory_format=torch.channels_last)
+    return g.contiguous()
+
+
+def _bitest_partials(x: Tensor, C: int) -> Tensor:
+    T = query("iclr17_bitest_bwd_chunks", x.numel(), C)
+    return torch.empty(T, 11, C, device=x.device, dtype=torch.float32)
+
+
+def bit_estimator_backward(x: Tensor, g: Tensor, rate_packed: Tensor, C: int):
+    """Autograd of ``bit_estimator`` → (∂x, parameter partials [T, 11, C] for rate_param_grads)."""
+    src, inner = _layout_inner(x)
+    gs = _like_layout(g, src)
+    dx = torch.empty_like(src)
+    part = _bitest_partials(src, C)
+    call("iclr17_bit_estimator_bwd", _p(src), _p(gs), src.numel(), C, inner, _p(rate_packed),
+         _p(dx), _p(part), _stream(x))
+    return dx, part
+
+
+def bitparm_backward(x: Tensor, g: Tensor, h: Tensor, b: Tensor, a: Optional[Tensor]):
+    """Autograd of ``bitparm`` → (∂x, parameter partials [T, 11, C]: slots 0-2, or 9-10 final)."""
+    C = h.numel()
+    src, inner = _layout_inner(x)
+    gs = _like_layout(g, src)
+    dx = torch.empty_like(src)
+    part = _bitest_partials(src, C)
+    work = torch.empty(11 * C, device=x.device, dtype=torch.float32)
+    hc, bc = h.detach().reshape(-1).contiguous(), b.detach().reshape(-1).contiguous()
+    ac = a.detach().reshape(-1).contiguous() if a is not None else None
+    call("iclr17_bitparm_bwd", _p(src), _p(gs), src.numel(), C, inner, _p(hc), _p(bc), _p(ac),
+         _p(work), _p(dx), _p(part), _stream(x))
+    return dx, part
+
+
 def rate_bits(z: Tensor, rate_packed: Tensor) -> Tensor:
     """model.py:71-73 on a 4-D latent: per-image Σ bits partials [B, T] (float64)."""
     _check(z, "latent", 4)

@@ -25,9 +25,11 @@ class Bitparm(nn.Module):
 
     def forward(self, x):
         # bitEstimator.py:20-25
-        from ..autograd import no_backward
-        return no_backward(kernels.bitparm(x, self.h, self.b, self.a), "Bitparm",
-                           [p for p in (self.h, self.b, self.a) if p is not None], x)
+        from ..autograd import BitparmFn, needs_grad
+        ps = [p for p in (self.h, self.b, self.a) if p is not None]
+        if needs_grad(x, ps):
+            return BitparmFn.apply(x, self, *ps)
+        return kernels.bitparm(x, self.h, self.b, self.a)
 
 
 class BitEstimator(nn.Module):
@@ -58,6 +60,7 @@ class BitEstimator(nn.Module):
 
     def forward(self, x):
         # bitEstimator.py:38-42
-        from ..autograd import no_backward
-        return no_backward(kernels.bit_estimator(x, self.packed(), self.channel), "BitEstimator",
-                           self.params_in_order(), x)
+        from ..autograd import BitEstimatorFn, needs_grad
+        if needs_grad(x, self.params_in_order()):
+            return BitEstimatorFn.apply(x, self, *self.params_in_order())
+        return kernels.bit_estimator(x, self.packed(), self.channel)

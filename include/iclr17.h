@@ -235,6 +235,25 @@ int iclr17_reduce_partials(const double* partial, int B, int T, double* per_imag
                            double scale, void* stream);
 
 /* ------------------------------------------------------------------ stand-alone modules */
+/* GDN.py:64-94 backward of the stand-alone module (autograd of gdn(x)): from x and g = ∂L/∂y
+ * (both in `layout`), writes ∂x (same layout), dn = ∂L/∂n NHWC [B·H·W][C] and, when u_nhwc is
+ * non-NULL, x as NHWC [B·H·W][C]. Parameter gradients: ∂β_eff = Σ_p dn (iclr17_bias_grad_nhwc),
+ * ∂γ_eff = iclr17_gdn_wgrad(dn, u), then iclr17_gdn_param_chain. */
+int iclr17_gdn_bwd(const float* x, const float* g, int B, int C, int H, int W, int layout,
+                   int inverse, const float* beta_eff, const float* gamma_packed,
+                   const float* gamma_packed_t, float* dx, float* dn, float* u_nhwc,
+                   void* stream);
+/* bitEstimator.py:20-42 backward of the stand-alone modules for an upstream gradient g (same
+ * shape as x; channel of flat element i is (i / inner) % C): ∂x, and per-channel parameter
+ * partials partial[iclr17_bitest_bwd_chunks(n, C)][11][C] in the rate-table slots (reduce and
+ * chain to ∂h, ∂b, ∂a with iclr17_rate_param_grad). bitparm_bwd: one Bitparm (a == NULL: the
+ * final layer, slots 9-10; else slots 0-2); work: 11·C floats. */
+int iclr17_bitest_bwd_chunks(int64_t n, int C);
+int iclr17_bit_estimator_bwd(const float* x, const float* g, int64_t n, int C, int64_t inner,
+                             const float* rate_packed, float* dx, float* partial, void* stream);
+int iclr17_bitparm_bwd(const float* x, const float* g, int64_t n, int C, int64_t inner,
+                       const float* h, const float* b, const float* a, float* work, float* dx,
+                       float* partial, void* stream);
 /* GDN.forward (GDN.py:64-94) on a [B,C,H,W] tensor in NCHW or NHWC memory layout. */
 int iclr17_gdn(const float* x, int B, int C, int H, int W, int layout, int inverse,
                const float* beta_eff, const float* gamma_packed, float* y, void* stream);

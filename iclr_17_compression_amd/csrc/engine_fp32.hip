@@ -529,7 +529,6 @@ __device__ __forceinline__ void gdn_bwd_epilogue(f4 (&g)[MT][NT], float* smem, c
     chan_gemm_lds<CO, MT, NT, true>(acc2, sX, a.ggamma, sG, wm, ncol0, lane, wave);  // Σ_j γ[i][j] u_j²
   }
   __syncthreads();
-  f4 u[MT][NT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -550,7 +549,6 @@ __device__ __forceinline__ void gdn_bwd_epilogue(f4 (&g)[MT][NT], float* smem, c
           g[mt][nt][r] = gg / sq;
           dn = ((-gg * uu) / (sq * sq)) / (2.0f * sq);
         }
-        u[mt][nt][r] = uu;
         sX[idx] = dn;
       }
   if (a.ggammaT6 != nullptr) {
@@ -562,15 +560,21 @@ __device__ __forceinline__ void gdn_bwd_epilogue(f4 (&g)[MT][NT], float* smem, c
   store_tile_rows<CO>(a, t, sX, XS, a.tout, CO, 0);
   if (a.colsum_t != nullptr) tile_colsum<CO>(a, t, sX, XS, a.colsum_t);
   __syncthreads();
+  // u again, from HBM/L2 rather than held in 48 VGPRs through both contractions (that kept
+  // the kernel at one wave per SIMD)
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
+    for (int r = 0; r < 4; ++r) {
+      const int row = wm * MT * 16 + mt * 16 + 4 * (lane >> 4) + r;
+      const long p = out_pixel(a, t, row);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int idx = (wm * MT * 16 + mt * 16 + 4 * (lane >> 4) + r) * XS + ncol0 + nt * 16 + (lane & 15);
-        sX[idx] = g[mt][nt][r] + acc2[mt][nt][r] * (2.0f * u[mt][nt][r]);
+      for (int nt = 0; nt < NT; ++nt) {
+        const int col = ncol0 + nt * 16 + (lane & 15);
+        const float uu = p < 0 ? 0.f : a.saved[p * CO + col];
+        sX[row * XS + col] = g[mt][nt][r] + acc2[mt][nt][r] * (2.0f * uu);
       }
+    }
   __syncthreads();
   store_tile_rows<CO>(a, t, sX, XS, a.out, CO, 0);
   if (a.out_split != nullptr) store_tile_rows_split<CO>(a, t, sX, XS, CO, 0);   // x6 consumer
@@ -1441,7 +1445,7 @@ __global__ void __launch_bounds__(256) conv1_gdn_kernel(const EngineArgs a) {
 constexpr int P1U = 3 * P1 * P1RS;        // u16 elements per split plane (4440)
 
 template <int CO, int EPI>
-__global__ void __launch_bounds__(256) conv1_x6_kernel(const EngineArgs a) {
+__global__ void __launch_bounds__(256, 2) conv1_x6_kernel(const EngineArgs a) {
   constexpr int WN = 4;
   constexpr int MT = BM / 16;
   constexpr int NT = CO / WN / 16;
@@ -1955,11 +1959,17 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
     return check_launch(EPI == EPI_PLAIN ? "conv3" : "bwd_deconv1_rate");
   } else {
     dim3 grid(a.tiles_x * a.tiles_y * B, 1);
-    if constexpr (EPI == EPI_GDN || EPI == EPI_IGDN_BWD) {
+    if constexpr (EPI == EPI_GDN) {
       if (X6in) {
         hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI, false, true>), grid, dim3(256), 0,
                            st, a);
-        return check_launch(EPI == EPI_GDN ? "conv2_gdn" : "bwd_deconv_igdn");
+        return check_launch("conv2_gdn");
+      }
+    } else if constexpr (EPI == EPI_IGDN_BWD) {
+      if (X6in) {   // held to 256 VGPRs: two waves per SIMD
+        hipLaunchKernelGGL((engine_kernel_occ2<N, N, N, 1, 4, EPI, false, true>), grid, dim3(256),
+                           0, st, a);
+        return check_launch("bwd_deconv_igdn");
       }
     }
     hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI>), grid, dim3(256), 0, st, a);
@@ -2001,9 +2011,9 @@ int launch_deconv5(const float* in, int B, int h, int w, const float* wp, const 
                          dim3(256), 0, st, a);
     if (a.phase_loop || X6in) return check_launch("deconv_igdn");
   } else {
-    if (a.in_split != nullptr) {
-      hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI, false, true>), dim3(base_tiles * 4),
-                         dim3(256), 0, st, a);
+    if (a.in_split != nullptr) {   // held to 256 VGPRs: two waves per SIMD
+      hipLaunchKernelGGL((engine_kernel_occ2<N, N, N, 1, 4, EPI, false, true>),
+                         dim3(base_tiles * 4), dim3(256), 0, st, a);
       return check_launch("bwd_conv_gdn");
     }
   }

@@ -472,16 +472,25 @@ __global__ void colsum_kernel(const float* __restrict__ A, long P, int C, int ch
   part[(long)blockIdx.y * C + c] = s;
 }
 
-// Per-channel sums of an NCHW tensor [B][C][HW]: part[b][c] (one workgroup per (b, c)).
-__global__ void plane_sum_kernel(const float* __restrict__ A, int C, long HW, float* __restrict__ part) {
+// Per-channel sums of an NCHW tensor [B][C][HW] over fixed PLANE_CHUNK-element chunks of each
+// plane: part[b·K + k][c], K = ⌈HW / PLANE_CHUNK⌉ (one workgroup per (b, c, k)); summed over the
+// B·K rows by iclr17_sum_rows in a fixed order.
+constexpr long PLANE_CHUNK = 4096;
+__global__ void plane_sum_kernel(const float* __restrict__ A, int C, long HW, int K,
+                                 float* __restrict__ part) {
   __shared__ float red[4];
-  const long base = (long)blockIdx.x * HW;
+  const int bc = blockIdx.x, k = blockIdx.y;
+  const long base = (long)bc * HW;
+  const long lo = k * PLANE_CHUNK, hi = lo + PLANE_CHUNK < HW ? lo + PLANE_CHUNK : HW;
   float s = 0.f;
-  for (long i = threadIdx.x; i < HW; i += 256) s += A[base + i];
+  for (long i = lo + threadIdx.x; i < hi; i += 256) s += A[base + i];
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) part[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+  if (threadIdx.x == 0) {
+    const int b = bc / C, c = bc % C;
+    part[((long)b * K + k) * C + c] = ((red[0] + red[1]) + red[2]) + red[3];
+  }
 }
 
 // x6 wgrad: a workgroup owns all M rows and 192 | 128 columns (C % that == 0), one per CU
@@ -648,11 +657,12 @@ int iclr17_bias_grad_nchw(const float* G, int B, int C, long HW, float* workspac
                           void* stream) {
   ICLR17_REQUIRE(B > 0 && C > 0 && HW > 0 && G && workspace && db, ICLR17_EINVAL, "bias_grad_nchw: bad arguments");
   hipStream_t st = S(stream);
-  hipLaunchKernelGGL(plane_sum_kernel, dim3(B * C), dim3(256), 0, st, G, C, HW, workspace);
+  const int K = (int)((HW + PLANE_CHUNK - 1) / PLANE_CHUNK);
+  hipLaunchKernelGGL(plane_sum_kernel, dim3(B * C, K), dim3(256), 0, st, G, C, HW, K, workspace);
   int rc = check_launch("bias_grad_nchw");
   if (rc) return rc;
-  // part is [B][C] → sum over b for each c
-  return iclr17_sum_rows(workspace, B, C, workspace + (long)B * C, db, stream);
+  // part is [B·K][C] → sum over the rows for each c
+  return iclr17_sum_rows(workspace, B * K, C, workspace + (long)B * K * C, db, stream);
 }
 
 }  // extern "C"

@@ -832,7 +832,7 @@ def bias_grad_nhwc(G: Tensor) -> Tensor:
 
 def bias_grad_nchw(G: Tensor) -> Tensor:
     B, C, H, W = G.shape
-    ws = torch.empty((B + 64) * C, device=G.device, dtype=torch.float32)
+    ws = torch.empty((B * ((H * W + 4095) // 4096) + 64) * C, device=G.device, dtype=torch.float32)
     db = torch.empty(C, device=G.device, dtype=torch.float32)
     call("iclr17_bias_grad_nchw", _p(G.contiguous()), B, C, H * W, _p(ws), _p(db), _stream(G))
     return db

@@ -355,7 +355,7 @@ int iclr17_gdn_param_chain(const float* beta, const float* gamma, const float* d
                            const float* dgamma_eff, int C, float beta_bound, float gamma_bound,
                            float* dbeta, float* dgamma, void* stream);
 /* Bias gradients: Σ over pixels of an NHWC [P][C] or NCHW [B][C][HW] gradient.
- * Workspace: (1024 + 64)*C floats (NHWC), (B + 64)*C floats (NCHW). */
+ * Workspace: (1024 + 64)*C floats (NHWC), (B·⌈HW/4096⌉ + 64)*C floats (NCHW). */
 int iclr17_bias_grad_nhwc(const float* G, long P, int C, float* workspace, float* db, void* stream);
 int iclr17_bias_grad_nchw(const float* G, int B, int C, long HW, float* workspace, float* db,
                           void* stream);

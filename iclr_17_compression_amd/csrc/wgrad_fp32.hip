@@ -434,7 +434,15 @@ __global__ void sum_splits_kernel(const float* __restrict__ part, int nsplit, lo
                                   float* __restrict__ out) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     float s = 0.f;
-    for (int k = 0; k < nsplit; ++k) s += part[(long)k * n + i];
+    int k = 0;
+    for (; k + 8 <= nsplit; k += 8) {   // 8 loads in flight, added in split order
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = part[(long)(k + j) * n + i];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[j];
+    }
+    for (; k < nsplit; ++k) s += part[(long)k * n + i];
     out[i] = s;
   }
 }

@@ -402,3 +402,31 @@ def test_errors_are_loud(device):
         net(torch.rand(1, 3, 40, 64, device=device))
     with pytest.raises(_lib.Iclr17Error, match="float32"):
         net(torch.rand(1, 3, 64, 64, device=device, dtype=torch.float64))
+
+
+def test_c5_2048_full_size_properties(device):
+    """C5's full image size (2048×2048, N=192), through properties that do not need a CPU
+    reference of that size: the x6 and exact-f32 modes agree (latents bit for bit except at
+    near-ties of the fp32 y, bpp / PSNR within 1e-5 relative); an image's results do not depend on
+    its batch; compress → decompress returns the latents and reconstruction bit for bit."""
+    net = net_for(192, 1, device)
+    x = image(41, 2, 2048, 2048).to(device)
+    old = kernels.precision()
+    try:
+        kernels.set_precision("fp32")
+        ev32 = net.evaluate(x[:1], want_y=True)
+        kernels.set_precision("x6")
+        ev6 = net.evaluate(x[:1], want_y=True)
+        ev6b = net.evaluate(x)                         # the same image inside a batch of two
+        enc = net.compress(x[:1])
+        dec = net.decompress(enc["strings"], enc["shape"])
+    finally:
+        kernels.set_precision(old)
+    n = check_latents(ev6["y_hat"], ev6["y"], ev32["y_hat"].cpu(), ev32["y"].cpu())
+    print("x6 vs fp32 near-tie flips at 2048²:", n)
+    assert ev6["bpp"].item() == pytest.approx(ev32["bpp"].item(), rel=METRIC_REL)
+    assert ev6["psnr"].item() == pytest.approx(ev32["psnr"].item(), rel=METRIC_REL)
+    for k in ("y_hat", "bpp", "clipped"):
+        assert torch.equal(ev6b[k][0], ev6[k][0]), k
+    assert torch.equal(dec["y_hat"].cpu(), ev6["y_hat"].cpu())
+    assert torch.equal(dec["x_hat"].cpu(), ev6["clipped"].cpu())

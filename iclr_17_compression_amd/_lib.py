@@ -94,6 +94,7 @@ SIGNATURES = {
     "iclr17_wgrad_workspace_size": (_SZ, [_I, _I, _I, _I, _I, _I]),
     "iclr17_wgrad_k5": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "iclr17_wgrad_k5_x6": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "iclr17_wgrad_k9_x6": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P]),
     "iclr17_wgrad_k9": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P]),
     "iclr17_gdn_wgrad_workspace_size": (_SZ, [ctypes.c_long, _I]),
     "iclr17_gdn_wgrad": (_I, [_P, _P, ctypes.c_long, _I, _P, _P, _P]),

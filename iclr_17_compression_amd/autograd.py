@@ -155,15 +155,17 @@ def analysis_backward(enc, saved: Dict[str, Tensor], g_y: Tensor,
                                                            g_split=g_y_split, want_split=True,
                                                            g6=x2[3], g6t=x2[4])
         dW3 = kernels.wgrad_k5_x6(g_y_split, _split_of(saved, "a2"))
-        g_u1, dn1, db1, dbe1 = kernels.bwd_conv_gdn(g_u2, w2t, saved["u1"], *x1[:3], g_split=g_u2s,
-                                                    g6=x1[3], g6t=x1[4])
+        g_u1, dn1, db1, dbe1, g_u1s = kernels.bwd_conv_gdn(g_u2, w2t, saved["u1"], *x1[:3],
+                                                           g_split=g_u2s, want_split=True,
+                                                           g6=x1[3], g6t=x1[4])
         dW2 = kernels.wgrad_k5_x6(g_u2s, _split_of(saved, "a1"))
+        dW1 = kernels.wgrad_k9_x6(g_u1s, saved["x"])
     else:
         g_u2, dn2, db2, dbe2 = kernels.bwd_conv_gdn(g_y, w3t, saved["u2"], *p2)
         dW3 = kernels.wgrad_k5(g_y, saved["a2"])
         g_u1, dn1, db1, dbe1 = kernels.bwd_conv_gdn(g_u2, w2t, saved["u1"], *p1)
         dW2 = kernels.wgrad_k5(g_u2, saved["a1"])
-    dW1 = kernels.wgrad_k9(g_u1, saved["x"])
+        dW1 = kernels.wgrad_k9(g_u1, saved["x"])
     dbeta2, dgamma2 = kernels.gdn_param_grads(dn2, saved["u2"], dbe2, enc.gdn2.beta, enc.gdn2.gamma, bb2, gb2)
     dbeta1, dgamma1 = kernels.gdn_param_grads(dn1, saved["u1"], dbe1, enc.gdn1.beta, enc.gdn1.gamma, bb1, gb1)
     return {"conv1.weight": dW1, "conv1.bias": db1, "gdn1.beta": dbeta1, "gdn1.gamma": dgamma1,
@@ -187,7 +189,7 @@ def synthesis_forward_train(dec, y_nhwc: Tensor, x_ref: Optional[Tensor] = None,
                                                  want_recon=True, sse_unclipped=x_ref is not None)
         # the split forms of y and s1 are the x6 weight-gradient operands
         return clipped, recon, sse, {"y": y_nhwc, "v1": v1, "s1": s1, "v2": v2, "s2": s2,
-                                     "ys": y_split, "s1s": s1s}
+                                     "ys": y_split, "s1s": s1s, "s2s": s2s}
     s1, v1 = kernels.deconv_igdn(y_nhwc, d1, dec.deconv1.bias, q1[0], q1[1], want_pre=True)
     s2, v2 = kernels.deconv_igdn(s1, d2, dec.deconv2.bias, q2[0], q2[1], want_pre=True)
     clipped, recon, sse = kernels.deconv3(s2, d3, dec.deconv3.bias, x_ref=x_ref,
@@ -219,7 +221,7 @@ def synthesis_backward(dec, saved: Dict[str, Tensor], g_recon: Tensor, g_bpp: Op
         g_v2, dnq2, dbd2, dbeq2, g_v2s = kernels.bwd_deconv3_igdn(g_recon, None, saved["v2"], *q2[:3],
                                                                   w_split=d3x, want_split=True,
                                                                   g6=q2[3], g6t=q2[4])
-        dWd3 = kernels.wgrad_k9(saved["s2"], g_recon)
+        dWd3 = kernels.wgrad_k9_x6(_split_of(saved, "s2"), g_recon)
         dbd3 = kernels.bias_grad_nchw(g_recon)
         g_v1, dnq1, dbd1, dbeq1, g_v1s = kernels.bwd_deconv_igdn(g_v2, d2c, saved["v1"], *q1[:3],
                                                                  g_split=g_v2s, want_split=True,

@@ -174,27 +174,6 @@ __device__ __forceinline__ void load_tile_rows(const EngineArgs& a, const TileIn
   }
 }
 
-// Exact three-way bf16 split of 8 floats: x = hi + mid + lo, each part a bf16 (truncation
-// split: hi = the top 8 significand bits, mid the next 8, lo the last 8, all exact in fp32).
-// Packed as bf16x8 fragments (u4 = 8 × 16 bits).
-__device__ __forceinline__ void split8(const f4& x0, const f4& x1, u4& hi, u4& mi, u4& lo) {
-  const float x[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-  unsigned h[8], m[8], l[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    h[i] = __float_as_uint(x[i]) & 0xffff0000u;
-    const float r = x[i] - __uint_as_float(h[i]);
-    m[i] = __float_as_uint(r) & 0xffff0000u;
-    l[i] = __float_as_uint(r - __uint_as_float(m[i]));
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    hi[i] = __builtin_amdgcn_perm(h[2 * i + 1], h[2 * i], 0x07060302u);
-    mi[i] = __builtin_amdgcn_perm(m[2 * i + 1], m[2 * i], 0x07060302u);
-    lo[i] = __builtin_amdgcn_perm(l[2 * i + 1], l[2 * i], 0x07060302u);
-  }
-}
-
 // Store a [BM][BN] LDS tile (row stride ld) as the three bf16 planes of the x6 activation
 // format (rows of CO channels, columns col0 ..), 8 channels (16 bytes per plane) per lane.
 template <int BN, int R = BM, int T = 256>

@@ -144,8 +144,8 @@ __device__ __forceinline__ uint2 tr16(const unsigned short* lds) {
   return __builtin_bit_cast(uint2, v);
 }
 
-template <int M, int CB, int WM, int WN>
-__global__ void __launch_bounds__(512) wgrad_k5_x6_kernel(const unsigned short* __restrict__ G6,
+template <int M, int CB, int WM, int WN, int KS>
+__global__ void __launch_bounds__(512) wgrad_x6_kernel(const unsigned short* __restrict__ G6,
                                                           long pg, const unsigned short* __restrict__ X6,
                                                           long pxs, int B, int Ho, int Wo, int Hi,
                                                           int Wi, int C, int nsplit,
@@ -157,10 +157,12 @@ __global__ void __launch_bounds__(512) wgrad_k5_x6_kernel(const unsigned short* 
   constexpr int GPR = M / 8, XPR = CB / 8;           // 16-byte pieces per pixel row
   constexpr int NGI = KP * GPR / 64, NXI = KP * XPR / 64;   // DMA wave-instructions per plane
   constexpr int NI = 3 * NGI + 3 * NXI;
-  constexpr int NI_W = NI / NW;
+  constexpr int NI_W = (NI + NW - 1) / NW;
+  constexpr int TAPS = KS * KS, STRIDE = KS == 5 ? 2 : 1, PAD = KS / 2;
+  static_assert(KS == 5 || KS == 1, "k5 s2 p2, or 1×1");
   static_assert(NW == 8 && MT * WM * 16 == M && NT * WN * 16 == CB, "tile shape");
-  static_assert(KP * GPR % 64 == 0 && KP * XPR % 64 == 0 && NI % NW == 0, "whole DMA slots");
-  static_assert(M == CB && (M == 192 || M == 128), "square layers, 384- or 256-byte rows");
+  static_assert(KP * GPR % 64 == 0 && KP * XPR % 64 == 0, "whole DMA instructions");
+  static_assert((M == 192 || M == 128) && (CB == 192 || CB == 128), "384- or 256-byte rows");
   __shared__ __attribute__((aligned(16))) unsigned short smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -170,18 +172,20 @@ __global__ void __launch_bounds__(512) wgrad_k5_x6_kernel(const unsigned short* 
   // they all read the same G chunk and overlapping X rows, which then hit that XCD's L2.
   const int nwg = gridDim.x;                  // padded to a multiple of 8
   const int L = (blockIdx.x % 8) * (nwg / 8) + blockIdx.x / 8;
-  const int tiles = 25 * (C / CB);
+  const int tiles = TAPS * (C / CB);
   if (L >= tiles * nsplit) return;            // padding workgroups (before any barrier)
   const int tile = L % tiles;
-  const int tap = tile % 25, ct = tile / 25;
+  const int tap = tile % TAPS, ct = tile / TAPS;
   // LDS images are XOR-swizzled by 16-byte piece: piece k of pixel row r sits at k ^ swz(r). A
   // transposed read's 32-lane half touches rows {q, 8 + q} (+4), two pieces each; swz gives them
   // disjoint bank windows (384-byte rows: the row parity already splits the 64 banks in two).
-  auto swz = [](int r) {
-    return M == 192 ? 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1))
-                    : 2 * ((r & 3) | (((r >> 3) & 1) << 2));
+  auto swz_rows = [](int r, int row_elems) {
+    return row_elems == 192 ? 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1))
+                            : 2 * ((r & 3) | (((r >> 3) & 1) << 2));
   };
-  const int kh = tap / 5, kw = tap % 5;
+  auto swzg = [&](int r) { return swz_rows(r, M); };
+  auto swzx = [&](int r) { return swz_rows(r, CB); };
+  const int kh = tap / KS, kw = tap % KS;
   const int split = L / tiles;
   const long P = (long)B * Ho * Wo;
   const long per = ((P + nsplit - 1) / nsplit + KP - 1) / KP * KP;
@@ -195,7 +199,7 @@ __global__ void __launch_bounds__(512) wgrad_k5_x6_kernel(const unsigned short* 
   // element offset moves by 2·KP·C while the step stays in the output row, else is recomputed.
   int pj[NI_W], off[NI_W], ow_[NI_W], oh_[NI_W], b_[NI_W];
   auto xoff = [&](int j) {
-    const int iy = oh_[j] * 2 - 2 + kh, ix = ow_[j] * 2 - 2 + kw;
+    const int iy = oh_[j] * STRIDE - PAD + kh, ix = ow_[j] * STRIDE - PAD + kw;
     return ((b_[j] * Hi + iy) * Wi + ix) * C;
   };
 #pragma unroll
@@ -204,7 +208,7 @@ __global__ void __launch_bounds__(512) wgrad_k5_x6_kernel(const unsigned short* 
     const bool isg = i < 3 * NGI;
     const int pc = (isg ? (i % NGI) : ((i - 3 * NGI) % NXI)) * 64 + lane;
     const int prow = isg ? pc / GPR : pc / XPR;
-    const int piece = (isg ? pc % GPR : pc % XPR) ^ swz(prow);
+    const int piece = isg ? (pc % GPR) ^ swzg(prow) : (pc % XPR) ^ swzx(prow);
     const long p = p0 + prow;
     pj[j] = (int)p;
     ow_[j] = (int)(p % Wo);
@@ -222,6 +226,7 @@ __global__ void __launch_bounds__(512) wgrad_k5_x6_kernel(const unsigned short* 
 #pragma unroll
     for (int j = 0; j < NI_W; ++j) {
       const int i = wave + NW * j;
+      if (NI % NW != 0 && i >= NI) break;   // wave-uniform
       const void* src = g_wzero;
       unsigned short* dst;
       if (i < 3 * NGI) {
@@ -230,7 +235,7 @@ __global__ void __launch_bounds__(512) wgrad_k5_x6_kernel(const unsigned short* 
         dst = st + pl * GPL + ii * 512;
       } else {
         const int pl = (i - 3 * NGI) / NXI, ii = (i - 3 * NGI) % NXI;
-        const int iy = oh_[j] * 2 - 2 + kh, ix = ow_[j] * 2 - 2 + kw;
+        const int iy = oh_[j] * STRIDE - PAD + kh, ix = ow_[j] * STRIDE - PAD + kw;
         if (pj[j] < p1i && (unsigned)iy < (unsigned)Hi && (unsigned)ix < (unsigned)Wi)
           src = X6 + pl * pxs + xo[j] + off[j];
         dst = st + 3 * GPL + pl * XPL + ii * 512;
@@ -249,7 +254,7 @@ __global__ void __launch_bounds__(512) wgrad_k5_x6_kernel(const unsigned short* 
       } else {
         ow_[j] += KP;
         if (ow_[j] < Wo) {
-          xo[j] += 2 * KP * C;
+          xo[j] += STRIDE * KP * C;
         } else {
           do {
             ow_[j] -= Wo;
@@ -269,17 +274,17 @@ __global__ void __launch_bounds__(512) wgrad_k5_x6_kernel(const unsigned short* 
   // transposed-read lane addresses: group g = lane >> 4 takes pixel rows 8g .. 8g+7 (two reads of
   // 4); lane 4q + p of the group addresses row q, channels 4p .. 4p+3.
   const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
-  const int fr = swz(8 * g + q);   // = swz(8g + q + 4): the row swizzle ignores bit 2
+  const int frg = swzg(8 * g + q), frx = swzx(8 * g + q);   // both ignore row bit 2 (+4 rows)
   int aoff[MT], boff[NT];          // u16 offsets within a plane image (second read: + 4 rows)
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int ch = wm * (M / WM) + mt * 16 + 4 * pp;
-    aoff[mt] = (8 * g + q) * M + (((ch >> 3) ^ fr) << 3) + (ch & 7);
+    aoff[mt] = (8 * g + q) * M + (((ch >> 3) ^ frg) << 3) + (ch & 7);
   }
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
     const int ch = wn * (CB / WN) + nt * 16 + 4 * pp;
-    boff[nt] = (8 * g + q) * CB + (((ch >> 3) ^ fr) << 3) + (ch & 7);
+    boff[nt] = (8 * g + q) * CB + (((ch >> 3) ^ frx) << 3) + (ch & 7);
   }
 
   if (nsteps > 0) issue(0);
@@ -321,7 +326,7 @@ __global__ void __launch_bounds__(512) wgrad_k5_x6_kernel(const unsigned short* 
     }
   }
   // part[split][m][c][tap]: lane holds rows 4(lane >> 4) + r, column lane & 15 of each tile
-  float* out = part + (long)split * M * C * 25;
+  float* out = part + (long)split * M * C * TAPS;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -330,8 +335,63 @@ __global__ void __launch_bounds__(512) wgrad_k5_x6_kernel(const unsigned short* 
       for (int r = 0; r < 4; ++r) {
         const int m = wm * (M / WM) + mt * 16 + 4 * (lane >> 4) + r;
         const int c = ct * CB + wn * (CB / WN) + nt * 16 + (lane & 15);
-        out[((long)m * C + c) * 25 + tap] = acc[mt][nt][r];
+        out[((long)m * C + c) * TAPS + tap] = acc[mt][nt][r];
       }
+}
+
+// k9 s4 p4 weight gradient in x6 as a 1×1 one: the 243 (c, kh, kw) window values of every
+// output pixel, split, as the X operand [3][P][256] (k = c·81 + kh·9 + kw, the PyTorch
+// [M][3][9][9] order; k ≥ 243 zero) — im2col of a 3-channel NCHW image, 8 k per thread.
+__global__ void im2col9_split_kernel(const float* __restrict__ X, int B, int Ho, int Wo,
+                                     unsigned short* __restrict__ planes) {
+  const long P = (long)B * Ho * Wo;
+  const long n = P * 32;
+  const int H = Ho * 4, W = Wo * 4;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (long)gridDim.x * blockDim.x) {
+    const long p = t >> 5;
+    const int kg = (int)(t & 31);
+    const int ox = (int)(p % Wo), oy = (int)((p / Wo) % Ho), b = (int)(p / ((long)Wo * Ho));
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = kg * 8 + e;
+      float x = 0.f;
+      if (k < 243) {
+        const int c = k / 81, kh = (k % 81) / 9, kw = k % 9;
+        const int iy = oy * 4 - 4 + kh, ix = ox * 4 - 4 + kw;
+        if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+          x = X[(((long)b * 3 + c) * H + iy) * W + ix];
+      }
+      v[e] = x;
+    }
+    u4 hi, mi, lo;
+    split8(f4{v[0], v[1], v[2], v[3]}, f4{v[4], v[5], v[6], v[7]}, hi, mi, lo);
+    unsigned short* d = planes + p * 256 + kg * 8;
+    *(u4*)d = hi;
+    *(u4*)(d + P * 256) = mi;
+    *(u4*)(d + 2 * P * 256) = lo;
+  }
+}
+
+// Σ over splits of part[s][m][256] → dW[m][243] (fixed split order, 8 loads in flight).
+__global__ void sum_splits_k9_kernel(const float* __restrict__ part, int nsplit, int M,
+                                     float* __restrict__ out) {
+  const long n = (long)M * 243;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long src = (i / 243) * 256 + i % 243;
+    const long stride = (long)M * 256;
+    float s = 0.f;
+    int k = 0;
+    for (; k + 8 <= nsplit; k += 8) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = part[(long)(k + j) * stride + src];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[j];
+    }
+    for (; k < nsplit; ++k) s += part[(long)k * stride + src];
+    out[i] = s;
+  }
 }
 
 // conv1 / deconv3 weight gradient: K = 243 = (c, kh, kw) of a 9×9 stride-4 pad-4 window on a
@@ -535,6 +595,8 @@ size_t iclr17_wgrad_workspace_size(int kind, int B, int Ho, int Wo, int M, int C
   const long P = (long)B * Ho * Wo;
   if (kind == 9) return (size_t)wgrad9_splits(B * ((Wo + 7) / 8) * ((Ho + 7) / 8)) * M * 243;
   if (kind == 6) return (size_t)wgrad6_splits(P, 25 * (C / wgrad6_cb(C))) * M * C * 25;
+  if (kind == 7)   // k9 x6: partials [ns][M][256] + the split im2col [3][P][256] (u16)
+    return (size_t)wgrad6_splits(P, 2) * M * 256 + (size_t)P * 256 * 3 / 2;
   const int ntap = kind == 1 ? 1 : 25;
   const int tiles = ntap * (C / 64);
   return (size_t)wgrad_splits(P, tiles) * M * C * ntap;
@@ -578,14 +640,42 @@ int iclr17_wgrad_k5_x6(const uint16_t* G_split, const uint16_t* X_split, int B, 
   const unsigned short* g6 = (const unsigned short*)G_split;
   const unsigned short* x6 = (const unsigned short*)X_split;
   if (M == 192)
-    hipLaunchKernelGGL((wgrad_k5_x6_kernel<192, 192, 2, 4>), grid, dim3(512), 0, st, g6, pg, x6, pxs, B, Ho, Wo, 2 * Ho, 2 * Wo, C, ns, workspace);
+    hipLaunchKernelGGL((wgrad_x6_kernel<192, 192, 2, 4, 5>), grid, dim3(512), 0, st, g6, pg, x6, pxs, B, Ho, Wo, 2 * Ho, 2 * Wo, C, ns, workspace);
   else
-    hipLaunchKernelGGL((wgrad_k5_x6_kernel<128, 128, 2, 4>), grid, dim3(512), 0, st, g6, pg, x6, pxs, B, Ho, Wo, 2 * Ho, 2 * Wo, C, ns, workspace);
+    hipLaunchKernelGGL((wgrad_x6_kernel<128, 128, 2, 4, 5>), grid, dim3(512), 0, st, g6, pg, x6, pxs, B, Ho, Wo, 2 * Ho, 2 * Wo, C, ns, workspace);
   int rc = check_launch("wgrad_k5_x6");
   if (rc) return rc;
   const long n = (long)M * C * 25;
   hipLaunchKernelGGL(sum_splits_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, workspace, ns, n, dW);
   return check_launch("wgrad_k5_x6_sum");
+}
+int iclr17_wgrad_k9_x6(const uint16_t* G_split, const float* X, int B, int Ho, int Wo, int M,
+                       float* workspace, float* dW, void* stream) {
+  ICLR17_REQUIRE(B > 0 && Ho > 0 && Wo > 0, ICLR17_EINVAL, "wgrad_k9_x6: bad shape");
+  ICLR17_REQUIRE(M == 128 || M == 192, ICLR17_EUNSUPPORTED, "wgrad_k9_x6: M=%d unsupported", M);
+  ICLR17_REQUIRE(G_split && X && workspace && dW, ICLR17_EINVAL, "wgrad_k9_x6: null pointer");
+  const long P = (long)B * Ho * Wo;
+  const int tiles = 2;   // 256 columns (243 used) in two 128-column tiles
+  const int ns = wgrad6_splits(P, tiles);
+  float* part = workspace;
+  unsigned short* cols = (unsigned short*)(workspace + (long)ns * M * 256);
+  hipStream_t st = S(stream);
+  const long nt = P * 32;
+  hipLaunchKernelGGL(im2col9_split_kernel, dim3((unsigned)((nt + 255) / 256 < 65536 ? (nt + 255) / 256 : 65536)),
+                     dim3(256), 0, st, X, B, Ho, Wo, cols);
+  int rc = check_launch("wgrad_k9_x6_im2col");
+  if (rc) return rc;
+  dim3 grid((tiles * ns + 7) / 8 * 8);
+  const unsigned short* g6 = (const unsigned short*)G_split;
+  if (M == 192)
+    hipLaunchKernelGGL((wgrad_x6_kernel<192, 128, 2, 4, 1>), grid, dim3(512), 0, st, g6, P * M, cols, P * 256, B, Ho, Wo, Ho, Wo, 256, ns, part);
+  else
+    hipLaunchKernelGGL((wgrad_x6_kernel<128, 128, 2, 4, 1>), grid, dim3(512), 0, st, g6, P * M, cols, P * 256, B, Ho, Wo, Ho, Wo, 256, ns, part);
+  rc = check_launch("wgrad_k9_x6");
+  if (rc) return rc;
+  const long n = (long)M * 243;
+  hipLaunchKernelGGL(sum_splits_k9_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, ns, M, dW);
+  return check_launch("wgrad_k9_x6_sum");
 }
 int iclr17_wgrad_k9(const float* G, const float* X, int B, int Ho, int Wo, int M,
                     float* workspace, float* dW, void* stream) {

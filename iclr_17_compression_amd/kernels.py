@@ -793,6 +793,21 @@ def wgrad_k5_x6(G_split: Tensor, X_split: Tensor) -> Tensor:
     return dW
 
 
+def wgrad_k9_x6(G_split: Tensor, X: Tensor) -> Tensor:
+    """wgrad_k9 in x6: G_split [3,B,Ho,Wo,M] split form, X NCHW fp32 [B,3,4Ho,4Wo]."""
+    _check_split(G_split, "wgrad G")
+    _check(X, "wgrad X", 4)
+    _, B, Ho, Wo, M = G_split.shape
+    if tuple(X.shape) != (B, 3, 4 * Ho, 4 * Wo):
+        raise Iclr17Error(f"iclr17: wgrad_k9_x6: X {tuple(X.shape)} vs G {tuple(G_split.shape)}")
+    ws = torch.empty(query("iclr17_wgrad_workspace_size", 7, B, Ho, Wo, M, 3), device=X.device,
+                     dtype=torch.float32)
+    dW = torch.empty(M, 3, 9, 9, device=X.device, dtype=torch.float32)
+    call("iclr17_wgrad_k9_x6", _p(G_split), _p(X.contiguous()), B, Ho, Wo, M, _p(ws), _p(dW),
+         _stream(X))
+    return dW
+
+
 def wgrad_k9(G: Tensor, X: Tensor) -> Tensor:
     """dW [M][3][9][9] = Σ G[b,o,m] · X[b,c,4o−4+k] (G NHWC [B,Ho,Wo,M], X NCHW [B,3,4Ho,4Wo])."""
     B, Ho, Wo, M = G.shape

@@ -343,6 +343,11 @@ int iclr17_wgrad_k5(const float* G, const float* X, int B, int Ho, int Wo, int M
  * floats. */
 int iclr17_wgrad_k5_x6(const uint16_t* G_split, const uint16_t* X_split, int B, int Ho, int Wo,
                        int M, int C, float* workspace, float* dW, void* stream);
+/* wgrad_k9 in the bf16x6 scheme: G_split [3][B][Ho][Wo][M] (split form), X NCHW fp32 [B,3,4Ho,4Wo];
+ * the 243-wide window of every output pixel is formed split (im2col, inside the workspace) and
+ * contracted as a 1×1 weight gradient. workspace: iclr17_wgrad_workspace_size(7, ...) floats. */
+int iclr17_wgrad_k9_x6(const uint16_t* G_split, const float* X, int B, int Ho, int Wo, int M,
+                       float* workspace, float* dW, void* stream);
 int iclr17_wgrad_k9(const float* G, const float* X, int B, int Ho, int Wo, int M,
                     float* workspace, float* dW, void* stream);
 /* GDN.py:83 weight gradient: dgamma_eff[i][j] = Σ_p dn[p][i]·u[p][j]² (dβ_eff = Σ_p dn comes

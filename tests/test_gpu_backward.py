@@ -208,3 +208,16 @@ def test_standalone_bit_estimator_backward(device, channels_last):
     assert grad_err(xd.grad, xr.grad) < 1e-4
     for name, prm in be.named_parameters():
         assert grad_err(prm.grad, p["bitEstimator." + name].grad) < 1e-4, name
+
+
+@pytest.mark.parametrize("M,B,Ho,Wo", [(192, 2, 16, 16), (128, 1, 8, 12), (192, 3, 20, 12)])
+def test_wgrad_k9_x6_matches_fp32(device, M, B, Ho, Wo):
+    """The x6 conv1/deconv3 weight gradient (split im2col + 1×1 x6 GEMM, tr_b16 fragments)
+    against the exact-f32 wgrad_k9 on the same values, incl. ragged last k-steps."""
+    from iclr_17_compression_amd import kernels
+    G = torch.from_numpy(synth.normal_like(23, (B, Ho, Wo, M), 1.0)).to(device)
+    X = torch.from_numpy(synth.uniform(24, (B, 3, 4 * Ho, 4 * Wo), 0.0, 1.0)).to(device)
+    ref = kernels.wgrad_k9(G, X)
+    got = kernels.wgrad_k9_x6(kernels.split_planes(G), X)
+    torch.cuda.synchronize()
+    assert grad_err(got, ref) < 1e-5

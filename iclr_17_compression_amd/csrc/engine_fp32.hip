@@ -49,6 +49,9 @@ constexpr int BM = 64;        // output pixels per tile
 #ifndef ICLR17_QSTAGES
 #define ICLR17_QSTAGES 2      // conv3's DMA ring depth (3, 4 measured slower: DESIGN.md §5)
 #endif
+#ifndef ICLR17_W8
+#define ICLR17_W8 0           // x6 GDN / IGDN layers on 128-pixel tiles, 8 waves (engine_kernel_w8)
+#endif
 #ifndef ICLR17_PL_MIN
 #define ICLR17_PL_MIN 512     // deconv base tiles from which one workgroup runs all 4 phases
 #endif
@@ -798,33 +801,37 @@ __device__ __forceinline__ void out3_epilogue(f4 (&acc)[MT][NT], float* smem, co
 // columns in VALU. One 32-deep step = per 16×16 tile six v_mfma_f32_16x16x32_bf16:
 // lo·hi + hi·lo + mid·mid + mid·hi + hi·mid + hi·hi (the dropped mid·lo, lo·mid, lo·lo terms are
 // below 2^-24 of the product), accumulated in fp32.
-template <int CI, int CO, int BN, int WM, int WN, int EPI, bool PL, bool X6>
+template <int CI, int CO, int BN, int WM, int WN, int EPI, bool PL, bool X6, int BMT = BM>
 __device__ __forceinline__ void engine_body(const EngineArgs& a) {
-  constexpr int MT = BM / WM / 16;
+  constexpr int NWV = WM * WN;                   // waves (4, or 8 for the 128-row tiles)
+  constexpr int MT = BMT / WM / 16;
   constexpr int NT = BN / WN / 16;
   constexpr int KCH = 32;                        // input channels per k-step
   constexpr int NCH = CI / KCH;
-  constexpr int SA = X6 ? 3 * BM * KCH / 2 : BM * KCH;   // A image floats per stage
+  constexpr int SA = X6 ? 3 * BMT * KCH / 2 : BMT * KCH;   // A image floats per stage
   constexpr int SB = KCH * BN;                   // B image floats per stage
   constexpr int STAGE = SA + SB;
   constexpr int NAI = SA * 4 / 1024;             // A glds wave-instructions per step (8 | 12)
   constexpr int NBI = SB * 4 / 1024;             // B glds wave-instructions per step
-  constexpr int AI_W = NAI / 4;                  // per wave
-  constexpr int BI_W = (NBI + 3) / 4;
+  constexpr int AI_W = NAI / NWV;                // per wave
+  constexpr int BI_W = (NBI + NWV - 1) / NWV;
+  constexpr int API = BMT / 16;                  // x6: A wave-instructions per plane (16 rows each)
   // DMA ring depth: conv3 (+ quantiser) has a third of conv2's MFMAs per step, too few to hide
   // an L2-miss DMA issued one step ahead, so it runs NS stages with a counted vmcnt wait.
   constexpr int NS = (EPI == EPI_QUANT && X6) ? ICLR17_QSTAGES : 2;
   constexpr int LDS_A = NS * STAGE;
   constexpr int LDS_X = (EPI == EPI_GDN || EPI == EPI_IGDN || EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD)
-                            ? BM * (CO + 8) + GSTAGE_FLOATS(CO) : 0;
-  constexpr int LDS_O = BM * (BN + 4) + 8;
+                            ? BMT * (CO + 8) + GSTAGE_FLOATS(CO) : 0;
+  constexpr int LDS_O = BMT * (BN + 4) + 8;
   constexpr int LDS_3 = 3 * 32 * 33 + 8;
   constexpr int L1 = LDS_A > LDS_X ? LDS_A : LDS_X;
   constexpr int L2 = LDS_O > LDS_3 ? LDS_O : LDS_3;
   constexpr int LDS_FLOATS = L1 > L2 ? L1 : L2;
-  static_assert(MT * WM * 16 == BM && NT * WN * 16 == BN, "tile shape");
-  static_assert(WM * WN == 4, "4 waves");
-  static_assert(CI % KCH == 0 && NAI % 4 == 0, "k-step split");
+  static_assert(MT * WM * 16 == BMT && NT * WN * 16 == BN, "tile shape");
+  static_assert(BMT == BM || (X6 && (EPI == EPI_GDN || EPI == EPI_IGDN) && NWV == 8),
+                "128-row tiles: the x6 GDN / IGDN layers on 8 waves");
+  static_assert(NWV == 4 || NWV == 8, "4 or 8 waves");
+  static_assert(CI % KCH == 0 && NAI % NWV == 0, "k-step split");
   static_assert(BN == CO || BN % 16 == 0, "B image: quad rows of BN columns");
   static_assert((SB * 4) % 1024 == 0, "B image in whole wave-instructions");
   static_assert(NS == 2 || NBI % 4 == 0, "counted vmcnt: equal DMA count per wave");
@@ -833,7 +840,7 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (scalar branches)
   const int wm = wave / WN, wn = wave % WN;
-  TileInfo t = decode_tile(a);
+  TileInfo t = decode_tile<BMT / 8>(a);
   const int ph_first = t.py * a.tt.npx + t.px;
   const int ph_end = PL ? a.tt.nph : ph_first + 1;   // PL: the phase loop (a.phase_loop = 1)
   const int ncol0 = t.nb * BN + wn * (BN / WN);
@@ -847,9 +854,9 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
 #pragma unroll
   for (int j = 0; j < AI_W; ++j) {
     const int i = wave * AI_W + j;
-    const int row = X6 ? 16 * (i & 3) + (lane >> 2) : i * 8 + (lane >> 3);
+    const int row = X6 ? 16 * (i % API) + (lane >> 2) : i * 8 + (lane >> 3);
     const int c = X6 ? (lane & 3) ^ ((row >> 1) & 3) : (lane & 7) ^ (row & 7);
-    const int gy = t.ty * 8 + (row >> 3), gx = t.tx * 8 + (row & 7);
+    const int gy = t.ty * (BMT / 8) + (row >> 3), gx = t.tx * 8 + (row & 7);
     rval[j] = gy < a.gh && gx < a.gw;
     iy0[j] = gy * a.sin;
     ix0[j] = gx * a.sin;
@@ -862,7 +869,7 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   int bsrc[BI_W];
 #pragma unroll
   for (int j = 0; j < BI_W; ++j) {
-    const int i = wave + 4 * j;
+    const int i = wave + NWV * j;
     const int o = i * 256 + lane * 4;   // offset in the LDS image [8 quads][BN][4]
     bsrc[j] = (BN == CO) ? o : ((o / (BN * 4)) * CO + t.nb * BN) * 4 + o % (BN * 4);
   }
@@ -890,10 +897,10 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
                       (unsigned)(ix0[j] + dx) < (unsigned)a.Win;
       const int i = wave * AI_W + j;
       if constexpr (X6) {
-        const unsigned short* src = inb6 + (i >> 2) * a.in_plane + pbase[j] + so;
+        const unsigned short* src = inb6 + (i / API) * a.in_plane + pbase[j] + so;
         if (ICLR17_ABL & 512) {   // within [image start, this lane's valid pixel] of the plane
           const int e = pbase[j] + so, base = (e & ~511) >= 512 ? (e & ~511) - 512 : 0;
-          src = inb6 + (i >> 2) * a.in_plane + base + (e >= 512 ? lane * 8 : 0);
+          src = inb6 + (i / API) * a.in_plane + base + (e >= 512 ? lane * 8 : 0);
         }
         glds16(ok ? (const float*)src : g_zero16, sa + i * 256);
       } else {
@@ -904,9 +911,9 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
     float* sb = sa + SA;
 #pragma unroll
     for (int j = 0; j < BI_W; ++j) {
-      const int i = wave + 4 * j;
+      const int i = wave + NWV * j;
       if (skip_b) break;
-      if (NBI % 4 == 0 || i < NBI) glds16(ws + bsrc[j], sb + i * 256);
+      if (NBI % NWV == 0 || i < NBI) glds16(ws + bsrc[j], sb + i * 256);
     }
   };
 
@@ -955,8 +962,8 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const bf8 Ah = __builtin_bit_cast(bf8, *(const u4*)(sa + aoff6[mt]));
-      const bf8 Am = __builtin_bit_cast(bf8, *(const u4*)(sa + BM * KCH + aoff6[mt]));
-      const bf8 Al = __builtin_bit_cast(bf8, *(const u4*)(sa + 2 * BM * KCH + aoff6[mt]));
+      const bf8 Am = __builtin_bit_cast(bf8, *(const u4*)(sa + BMT * KCH + aoff6[mt]));
+      const bf8 Al = __builtin_bit_cast(bf8, *(const u4*)(sa + 2 * BMT * KCH + aoff6[mt]));
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         f4 c = acc[mt][nt];
@@ -1044,7 +1051,7 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
       for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[mt][nt][r] += a.bias[ncol0 + nt * 16 + (lane & 15)];
-    gdn_epilogue<CO, MT, NT, EPI == EPI_IGDN, BM, 256, X6>(acc, smem, a, t, wm, ncol0, lane);
+    gdn_epilogue<CO, MT, NT, EPI == EPI_IGDN, BMT, NWV * 64, X6>(acc, smem, a, t, wm, ncol0, lane);
   } else if constexpr (EPI == EPI_QUANT) {
     quant_epilogue<CO, BN, MT, NT, WN>(acc, smem, a, t, wm, ncol0, lane, wave);
   } else if constexpr (EPI == EPI_OUT3) {
@@ -1078,6 +1085,14 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
 template <int CI, int CO, int BN, int WM, int WN, int EPI, bool PL = false, bool X6 = false>
 __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
   engine_body<CI, CO, BN, WM, WN, EPI, PL, X6>(a);
+}
+
+// 128-pixel tiles (16×8 base pixels) on 8 waves (2 × 4), one workgroup per CU at two waves per
+// SIMD: the weight slice of a k-step feeds twice the pixels, so a CU moves 48 KB per step for the
+// work two 64-pixel workgroups did with 72 KB. The x6 GDN / IGDN layers (ICLR17_W8).
+template <int CI, int CO, int EPI, bool PL>
+__global__ void __launch_bounds__(512) engine_kernel_w8(const EngineArgs a) {
+  engine_body<CI, CO, CO, 2, 4, EPI, PL, true, 128>(a);
 }
 
 // The same kernel held to 256 VGPRs (2 waves per SIMD) where the compiler would otherwise just
@@ -1939,6 +1954,12 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
   } else {
     dim3 grid(a.tiles_x * a.tiles_y * B, 1);
     if constexpr (EPI == EPI_GDN) {
+      if (X6in && ICLR17_W8) {   // 128-pixel tiles on 8 waves
+        a.tiles_y = (a.gh + 15) / 16;
+        hipLaunchKernelGGL((engine_kernel_w8<N, N, EPI, false>), dim3(a.tiles_x * a.tiles_y * B),
+                           dim3(512), 0, st, a);
+        return check_launch("conv2_gdn");
+      }
       if (X6in) {
         hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI, false, true>), grid, dim3(256), 0,
                            st, a);
@@ -1979,6 +2000,16 @@ int launch_deconv5(const float* in, int B, int h, int w, const float* wp, const 
 #endif
   if constexpr (EPI == EPI_IGDN) {
     const bool X6in = a.in_split != nullptr;
+    if (X6in && ICLR17_W8) {   // 128-pixel tiles on 8 waves (phase loop when the grid is large)
+      a.tiles_y = (h + 15) / 16;
+      const int bt = a.tiles_x * a.tiles_y * B;
+      a.phase_loop = bt >= ICLR17_PL_MIN / 2 ? 1 : 0;
+      if (a.phase_loop)
+        hipLaunchKernelGGL((engine_kernel_w8<N, N, EPI, true>), dim3(bt), dim3(512), 0, st, a);
+      else
+        hipLaunchKernelGGL((engine_kernel_w8<N, N, EPI, false>), dim3(bt * 4), dim3(512), 0, st, a);
+      return check_launch("deconv_igdn");
+    }
     if (a.phase_loop && X6in)
       hipLaunchKernelGGL((engine_kernel_occ2<N, N, N, 1, 4, EPI, true, true>), dim3(base_tiles),
                          dim3(256), 0, st, a);

@@ -49,6 +49,9 @@ constexpr int BM = 64;        // output pixels per tile
 #ifndef ICLR17_QSTAGES
 #define ICLR17_QSTAGES 2      // conv3's DMA ring depth (3, 4 measured slower: DESIGN.md §5)
 #endif
+#ifndef ICLR17_PHASE_MAJOR
+#define ICLR17_PHASE_MAJOR 1  // deconv phases dispatched phase-major (longest first)
+#endif
 #ifndef ICLR17_W8
 #define ICLR17_W8 0           // x6 GDN / IGDN layers on 128-pixel tiles, 8 waves (engine_kernel_w8)
 #endif
@@ -127,12 +130,23 @@ __device__ __forceinline__ TileInfo decode_tile(const EngineArgs& a) {
   TileInfo t;
   t.th = TH;
   int bid = blockIdx.x;
+#if ICLR17_PHASE_MAJOR
+  // stride phases in dispatch order 0..3 (9, 6, 6, 4 taps): longest workgroups first
+  const int per_ph = a.tiles_x * a.tiles_y * a.B;
+  const int phm = a.phase_loop ? 0 : bid / per_ph;
+  if (!a.phase_loop) bid -= phm * per_ph;
+#endif
   t.tx = bid % a.tiles_x;
   bid /= a.tiles_x;
   t.ty = bid % a.tiles_y;
   bid /= a.tiles_y;
+#if ICLR17_PHASE_MAJOR
+  const int ph = phm;
+  t.b = bid;
+#else
   const int ph = a.phase_loop ? 0 : bid % a.tt.nph;
   t.b = a.phase_loop ? bid : bid / a.tt.nph;
+#endif
   t.py = ph / a.tt.npx;
   t.px = ph % a.tt.npx;
   t.nb = blockIdx.y;

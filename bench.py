@@ -487,7 +487,7 @@ def main() -> None:
         "layers": layers,
         "bpp_last": round(bpp.item(), 6),
     }
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:   # the CPU leg: N=1 only
         result["cpu_baseline"] = cpu_baseline(N, S, S, args.cpu_budget)
     if rank == 0:
         print(json.dumps(result), flush=True)

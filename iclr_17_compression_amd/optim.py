@@ -42,8 +42,26 @@ class FusedAdam(torch.optim.Optimizer):
         rows = [(p.data_ptr(), p.grad.data_ptr(), self.state[p]["exp_avg"].data_ptr(),
                  self.state[p]["exp_avg_sq"].data_ptr(), p.numel()) for p in ps]
         key = tuple(rows)
-        if key != self._desc_key:   # pointer table on the device, rebuilt only when a buffer moves
-            self._desc = torch.tensor(rows, dtype=torch.int64).to(ps[0].device)
+        if key != self._desc_key:   # pointer table on the device, rewritten when a buffer moves
+            # (with zero_grad(set_to_none=True) the gradients are new tensors every step). The
+            # table goes up by a non-blocking copy from one of two pinned host buffers, so the
+            # host never waits for the device here; a buffer is refilled only after the copy
+            # that last read it has completed (its event).
+            n = len(rows)
+            if self._desc is None or self._desc.shape[0] != n:
+                self._desc = torch.empty((n, 5), dtype=torch.int64, device=ps[0].device)
+                self._host = [torch.empty((n, 5), dtype=torch.int64, pin_memory=True)
+                              for _ in range(2)]
+                self._host_ev = [None, None]
+                self._slot = 0
+            slot, self._slot = self._slot, self._slot ^ 1
+            if self._host_ev[slot] is not None:
+                self._host_ev[slot].synchronize()
+            self._host[slot].copy_(torch.tensor(rows, dtype=torch.int64))
+            self._desc.copy_(self._host[slot], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(ps[0].device))
+            self._host_ev[slot] = ev
             self._desc_key = key
         return ps, max(r[4] for r in rows)
 

@@ -51,7 +51,7 @@ SIGNATURES = {
     "iclr17_rate_partials_per_image": (_I, [_I, _I, _I]),
     "iclr17_synthesis_deconv_igdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_synthesis_deconv3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P]),
-    "iclr17_synthesis_deconv3_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P]),
+    "iclr17_synthesis_deconv3_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "iclr17_output_partials_per_image": (_I, [_I, _I]),
     "iclr17_split_planes": (_I, [_P, ctypes.c_long, _P, _P]),
     "iclr17_split_packed": (_I, [_P, _I, _I, _I, _P, _P]),

@@ -1139,7 +1139,7 @@ constexpr int D3_SA = D3_NAI * 256;             // A stage floats (976 slots × 
 constexpr int D3_SB = 32 * 48;                  // B stage floats
 constexpr int D3_LDS = D3_SA + 2 * D3_SB;
 
-template <int CI>
+template <int CI, bool PRE = false>
 __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) {
   constexpr int KCH = 32, NCH = CI / KCH, NSTEP = 9 * NCH;
   constexpr int MT = 4, NT = 3;
@@ -1234,6 +1234,76 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
     }
   };
 
+  if constexpr (PRE) {
+    // Pre-split weights [3][9][CI/8][48][8] (the 16x16x32 B-fragment layout) read from L2 one
+    // step ahead: no B stage, no per-step split (the four waves no longer split the same B), and
+    // barriers only at chunk boundaries.
+    constexpr long WPL = 9L * CI * 48;   // plane stride (u16)
+    const unsigned short* gb = (const unsigned short*)a.w + ((lane >> 4) * 48 + (lane & 15)) * 8;
+    typedef const __attribute__((address_space(1))) u4* gu4p;   // global: no flat disambiguation
+    auto loadb = [&](int s, u4 (&bb)[3][NT]) {
+      const int cc = s / 9, tap = s - cc * 9;
+      const unsigned short* src = gb + ((long)tap * (CI / 8) + cc * 4) * 48 * 8;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) bb[pl][nt] = *(gu4p)(src + pl * WPL + nt * 128);
+    };
+    typedef const __attribute__((address_space(3))) u4* lu4p;
+    const __attribute__((address_space(3))) float* sA3 =
+        (const __attribute__((address_space(3))) float*)sA;
+    auto compute_pre = [&](const u4 (&bb)[3][NT], int tap) {
+      const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int p = prow + (mt + dy) * D3_PS + dx;
+        const int o = p * 16 + ((g ^ (((p >> 2) & 1) << 1)) * 4);   // floats
+        const bf8 Ah = __builtin_bit_cast(bf8, *(lu4p)(sA3 + o));
+        const bf8 Am = __builtin_bit_cast(bf8, *(lu4p)(sA3 + o + D3_PPX * 16));
+        const bf8 Al = __builtin_bit_cast(bf8, *(lu4p)(sA3 + o + 2 * D3_PPX * 16));
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const bf8 Bh = __builtin_bit_cast(bf8, bb[0][nt]), Bm = __builtin_bit_cast(bf8, bb[1][nt]),
+                    Bl = __builtin_bit_cast(bf8, bb[2][nt]);
+          f4 c = acc[mt][nt];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al, Bh, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bl, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bm, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bh, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bm, c, 0, 0, 0);
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bh, c, 0, 0, 0);
+        }
+      }
+    };
+    u4 b0[3][NT], b1[3][NT];
+    issue_a(0);
+    loadb(0, b0);
+    for (int cc = 0; cc < NCH; ++cc) {
+      __syncthreads();   // this chunk's patch landed
+      // ping-pong B registers, one step ahead (written out: the register sets stay in VGPRs)
+      const int s0 = cc * 9;
+      const bool more = cc + 1 < NCH;
+      loadb(s0 + 1, b1); compute_pre(b0, 0);
+      loadb(s0 + 2, b0); compute_pre(b1, 1);
+      loadb(s0 + 3, b1); compute_pre(b0, 2);
+      loadb(s0 + 4, b0); compute_pre(b1, 3);
+      loadb(s0 + 5, b1); compute_pre(b0, 4);
+      loadb(s0 + 6, b0); compute_pre(b1, 5);
+      loadb(s0 + 7, b1); compute_pre(b0, 6);
+      loadb(s0 + 8, b0); compute_pre(b1, 7);
+      if (more) loadb(s0 + 9, b1);
+      compute_pre(b0, 8);
+      // tap 8 used b0; b1 holds the next chunk's tap 0
+      if (more) {
+        __syncthreads();   // every wave is done with this chunk's patch
+        issue_a(cc + 1);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) b0[pl][nt] = b1[pl][nt];
+      }
+    }
+  } else {
   issue_a(0);
   issue_b(0, 0);
   for (int s = 0; s < NSTEP; ++s) {
@@ -1246,6 +1316,7 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
       issue_a((s + 1) / 9);
       issue_b(s + 1, (s + 1) & 1);
     }
+  }
   }
   __syncthreads();     // stage reads done before the epilogue reuses LDS
 
@@ -2183,12 +2254,12 @@ int iclr17_synthesis_deconv_igdn(const float* in, int B, int h, int w, int N,
 }
 
 int iclr17_synthesis_deconv3_x6(const uint16_t* in_split, int B, int H, int W, int N,
-                                const float* w_packed, const float* bias, const float* x,
-                                float* clipped, float* recon, double* sse_partial,
-                                int sse_unclipped, void* stream) {
+                                const float* w_packed, const uint16_t* w_split, const float* bias,
+                                const float* x, float* clipped, float* recon,
+                                double* sse_partial, int sse_unclipped, void* stream) {
   int rc = check_dims(B, H, W, N);
   if (rc) return rc;
-  ICLR17_REQUIRE(in_split && w_packed && bias && clipped, ICLR17_EINVAL,
+  ICLR17_REQUIRE(in_split && (w_packed || w_split) && bias && clipped, ICLR17_EINVAL,
                  "deconv3_x6: null pointer");
   ICLR17_REQUIRE(x == nullptr || sse_partial != nullptr, ICLR17_EINVAL,
                  "deconv3_x6: sse_partial required with x");
@@ -2206,6 +2277,14 @@ int iclr17_synthesis_deconv3_x6(const uint16_t* in_split, int B, int H, int W, i
   a.tiles_y = (a.gh + D3_BS - 1) / D3_BS; a.tiles_x = (a.gw + D3_BS - 1) / D3_BS;
   a.partials_per_image = ((a.gh + 7) / 8) * ((a.gw + 7) / 8);
   dim3 grid(a.tiles_x * a.tiles_y * B);
+  if (w_split != nullptr) {   // pre-split weights read from L2 (no B stage, no in-loop split)
+    a.w = (const float*)w_split;
+    if (N == 192)
+      hipLaunchKernelGGL((deconv3_x6_kernel<192, true>), grid, dim3(256), 0, S(stream), a);
+    else
+      hipLaunchKernelGGL((deconv3_x6_kernel<128, true>), grid, dim3(256), 0, S(stream), a);
+    return check_launch("deconv3_x6");
+  }
   if (N == 192)
     hipLaunchKernelGGL((deconv3_x6_kernel<192>), grid, dim3(256), 0, S(stream), a);
   else

@@ -402,10 +402,13 @@ def deconv3(h: Tensor, wp: Tensor, bias: Tensor, x_ref: Optional[Tensor] = None,
     return clipped, recon, partial
 
 
-def deconv3_x6(hs: Tensor, wp: Tensor, bias: Tensor, x_ref: Optional[Tensor] = None,
-               want_recon: bool = False, sse_unclipped: bool = False):
+def deconv3_x6(hs: Tensor, wp: Optional[Tensor], bias: Tensor, x_ref: Optional[Tensor] = None,
+               want_recon: bool = False, sse_unclipped: bool = False,
+               w_split: Optional[Tensor] = None):
     """deconv3 on a split-form input [3,B,H/4,W/4,N] (the halo-tiled x6 kernel); the same
-    returns as ``deconv3``."""
+    returns as ``deconv3``. ``w_split`` (``split_deconv3``) lets the kernel read pre-split weight
+    fragments from L2 instead of splitting the packed weights in its loop: bit-identical, but
+    measured 7 % slower (VGPR pressure), so the model does not use it."""
     _check_split(hs, "activation")
     _, B, h4, w4, N = hs.shape
     _check_channels(N)
@@ -420,9 +423,14 @@ def deconv3_x6(hs: Tensor, wp: Tensor, bias: Tensor, x_ref: Optional[Tensor] = N
             raise Iclr17Error("iclr17: reference image shape mismatch")
         x_ref = x_ref.contiguous()
         partial = torch.empty(B, output_partials_per_image(H, W), device=hs.device, dtype=torch.float64)
-    call("iclr17_synthesis_deconv3_x6", _p(hs), B, H, W, N, _p(wp), _p(bias), _p(x_ref),
-         _p(clipped), _p(recon), _p(partial), int(sse_unclipped), _stream(hs))
+    call("iclr17_synthesis_deconv3_x6", _p(hs), B, H, W, N, _p(wp), _p(w_split), _p(bias),
+         _p(x_ref), _p(clipped), _p(recon), _p(partial), int(sse_unclipped), _stream(hs))
     return clipped, recon, partial
+
+
+def split_deconv3(wp: Tensor, N: int) -> Tensor:
+    """The deconv3 all-phase packing [9][N/4][48][4] → split planes for deconv3_x6's w_split."""
+    return split_packed(wp, 9, N, 48)
 
 
 # ---------------------------------------------------------------- entropy coding (§8 f4)

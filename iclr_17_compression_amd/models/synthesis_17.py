@@ -47,6 +47,13 @@ class Synthesis_net_17(nn.Module):
                             lambda: kernels.pack_weight(_lib.ICLR17_W_DECONV9, self.deconv3.weight, N), f)
         return d1, d2, d3, self.igdn1.effective_params(force), self.igdn2.effective_params(force)
 
+    def packed_deconv3_x6(self, force: bool = False):
+        """deconv3's packed weights split for the x6 kernel (kernels.split_deconv3), cached."""
+        N = self.out_channel_N
+        return self._pack.get("d3x6", (self.deconv3.weight,),
+                              lambda: kernels.split_deconv3(self.packed(force)[2], N),
+                              force or self.training)
+
     @staticmethod
     def to_nhwc(y):
         """NCHW-shaped latent (any memory format) → contiguous NHWC [B, h, w, N] (no copy when

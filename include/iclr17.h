@@ -166,11 +166,13 @@ int iclr17_synthesis_deconv_igdn_x6(const uint16_t* in_split, int B, int h, int 
                                     const uint16_t* gamma_split, float* out, uint16_t* out_split,
                                     float* pre_out, void* stream);
 /* iclr17_synthesis_deconv3 on a split-form input (the same outputs and sse_partial layout:
- * iclr17_output_partials_per_image(H, W) doubles per image). */
+ * iclr17_output_partials_per_image(H, W) doubles per image). w_split (nullable: then w_packed,
+ * split in the loop) is w_packed split by iclr17_split_packed(taps = 9, K = N, N = 48): the
+ * kernel then reads the weight fragments from L2 and splits nothing. */
 int iclr17_synthesis_deconv3_x6(const uint16_t* in_split, int B, int H, int W, int N,
-                                const float* w_packed, const float* bias, const float* x,
-                                float* clipped, float* recon, double* sse_partial,
-                                int sse_unclipped, void* stream);
+                                const float* w_packed, const uint16_t* w_split, const float* bias,
+                                const float* x, float* clipped, float* recon,
+                                double* sse_partial, int sse_unclipped, void* stream);
 
 /* ---------------------------------------------------------------- entropy coding (§8 f4)
  * A real bitstream for ŷ with the factorised model the reference only uses to ESTIMATE the rate

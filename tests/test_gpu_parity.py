@@ -172,6 +172,10 @@ def test_deconv3_x6(device, N, shape):
             assert rel_err(part, part32) < 1e-4
         c2, r2, p2 = kernels.deconv3_x6(hs, d3, net.Decoder.deconv3.bias)
         assert r2 is None and p2 is None and torch.equal(c2, clipped)
+        # pre-split weights read from L2: the same split values and product order, bit for bit
+        c3, r3, p3 = kernels.deconv3_x6(hs, d3, net.Decoder.deconv3.bias, x_ref=xd, want_recon=True,
+                                        sse_unclipped=True, w_split=net.Decoder.packed_deconv3_x6())
+        assert torch.equal(c3, clipped) and torch.equal(r3, recon) and torch.equal(p3, part)
 
 
 # ------------------------------------------------------------------------------------ layers

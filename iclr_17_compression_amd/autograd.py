@@ -5,7 +5,9 @@
   reference autograd graph of ``rd_loss.backward()`` (train.py:105) as fused kernels.
 * ``AnalysisFn`` / ``SynthesisFn`` — Encoder / Decoder used on their own (NewTests-style
   callers, train_decoder_new.py:66-105 trains a Decoder alone).
-* Where a backward kernel is not wired yet (stand-alone GDN / BitEstimator modules), outputs
+* ``GDNFn`` / ``BitEstimatorFn`` / ``BitparmFn`` — the stand-alone modules with their own
+  backward kernels.
+* Where no backward is wired (ImageCompressor.forward in eval mode with autograd on), outputs
   carry a grad_fn that raises instead of silently producing wrong gradients.
 """
 from __future__ import annotations

@@ -49,6 +49,9 @@ constexpr int BM = 64;        // output pixels per tile
 #ifndef ICLR17_QSTAGES
 #define ICLR17_QSTAGES 2      // conv3's DMA ring depth (3, 4 measured slower: DESIGN.md §5)
 #endif
+#ifndef ICLR17_GDN_PLANES
+#define ICLR17_GDN_PLANES 1   // x6 GDN contraction: x² split once into LDS planes (not per wave)
+#endif
 #ifndef ICLR17_PHASE_MAJOR
 #define ICLR17_PHASE_MAJOR 1  // deconv phases dispatched phase-major (longest first)
 #endif
@@ -426,16 +429,102 @@ __device__ __forceinline__ void chan_gemm_x6(f4 (&acc)[MT][NT], const float* sX,
 #endif
 }
 
+// The same x6 contraction with the A operand already split in LDS: three bf16 planes
+// [3][R][CO+8] (u16), written once by the producing waves, so no wave splits rows in VALU (with
+// one wave row every wave used to split the whole x² tile for itself).
+template <int CO, int MT, int NT, int R>
+__device__ __forceinline__ void chan_gemm_x6p(f4 (&acc)[MT][NT], const unsigned short* sP,
+                                              const unsigned short* __restrict__ g6, int wm,
+                                              int ncol0, int lane) {
+  constexpr int PS = CO + 8;
+  constexpr int KB = CO / 32;
+  constexpr long GP = (long)CO * CO;
+  static_assert(KB % 2 == 0, "k-blocks in pairs (ping-pong B registers)");
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
+  const unsigned short* arow = sP + (wm * MT * 16 + (lane & 15)) * PS + 8 * (lane >> 4);
+  const unsigned short* gb = g6 + ((lane >> 4) * CO + ncol0 + (lane & 15)) * 8;
+  u4 b0[3][NT], b1[3][NT];
+  auto load = [&](int kb, u4 (&b)[3][NT]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        b[p][nt] = *(const u4*)(gb + p * GP + (long)kb * 4 * CO * 8 + nt * 128);
+  };
+  auto block = [&](int kb, const u4 (&b)[3][NT]) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const unsigned short* a = arow + mt * 16 * PS + kb * 32;
+      const bf8 Ah = __builtin_bit_cast(bf8, *(const u4*)(a));
+      const bf8 Am = __builtin_bit_cast(bf8, *(const u4*)(a + R * PS));
+      const bf8 Al = __builtin_bit_cast(bf8, *(const u4*)(a + 2 * R * PS));
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const bf8 Bh = __builtin_bit_cast(bf8, b[0][nt]), Bm = __builtin_bit_cast(bf8, b[1][nt]),
+                  Bl = __builtin_bit_cast(bf8, b[2][nt]);
+        f4 c = acc[mt][nt];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al, Bh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bl, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bm, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bm, c, 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bh, c, 0, 0, 0);
+      }
+    }
+  };
+  load(0, b0);
+  for (int kb = 0; kb < KB; kb += 2) {
+    load(kb + 1, b1);
+    block(kb, b0);
+    if (kb + 2 < KB) load(kb + 2, b0);
+    block(kb + 1, b1);
+  }
+}
+
+// LDS floats the GDN core needs for an R-row tile (fp32 x² tile + γ stages, or, for the x6
+// contraction, the three split planes of x²).
+constexpr int gdn_lds_floats(int R, int CO, bool G6, bool GPL = ICLR17_GDN_PLANES) {
+  return G6 && GPL ? (3 * R * (CO + 8) + 1) / 2 : R * (CO + 8) + GSTAGE_FLOATS(CO);
+}
+
 // x (bias already added) in accumulator layout → GDN(x) (or IGDN) left in LDS sX[BM][CO+4].
 // models/GDN.py:83-90: n = conv2d(x², γ, β) = β + Σ_j γ[i][j]·x_j²;  y = x / √n | x·√n.
 // The caller guarantees smem is free on entry; on return every wave has passed a barrier after
 // the last sX write.
-template <int CO, int MT, int NT, bool INVERSE, int R = BM, int T = 256, bool G6 = false>
+template <int CO, int MT, int NT, bool INVERSE, int R = BM, int T = 256, bool G6 = false,
+          bool GPL = ICLR17_GDN_PLANES>
 __device__ __forceinline__ void gdn_core(const f4 (&x)[MT][NT], float* sX,
                                          const float* __restrict__ gbeta,
                                          const float* __restrict__ gp, int wm, int ncol0,
                                          int lane, const unsigned short* g6 = nullptr) {
   constexpr int XS = CO + 8;
+  f4 nacc[MT][NT];
+  if constexpr (G6 && GPL) {
+    // x² (rounded to fp32, as conv2d(x², γ) sees it) split once into three bf16 planes
+    unsigned short* sP = (unsigned short*)sX;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * MT * 16 + mt * 16 + 4 * (lane >> 4) + r;
+          const int col = ncol0 + nt * 16 + (lane & 15);
+          const float v = x[mt][nt][r] * x[mt][nt][r];
+          const unsigned h = __float_as_uint(v) & 0xffff0000u;
+          const float rr = v - __uint_as_float(h);
+          const unsigned m = __float_as_uint(rr) & 0xffff0000u;
+          const unsigned l = __float_as_uint(rr - __uint_as_float(m));
+          sP[row * XS + col] = (unsigned short)(h >> 16);
+          sP[(R + row) * XS + col] = (unsigned short)(m >> 16);
+          sP[(2 * R + row) * XS + col] = (unsigned short)(l >> 16);
+        }
+    __syncthreads();   // planes of every wave published
+    chan_gemm_x6p<CO, MT, NT, R>(nacc, sP, g6, wm, ncol0, lane);
+  } else {
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -447,8 +536,9 @@ __device__ __forceinline__ void gdn_core(const f4 (&x)[MT][NT], float* sX,
         const float v = x[mt][nt][r];
         sX[row * XS + col] = v * v;
       }
-  f4 nacc[MT][NT];
-  if constexpr (G6) {
+  }
+  if constexpr (G6 && GPL) {
+  } else if constexpr (G6) {
     __syncthreads();   // x² of every wave published
     chan_gemm_x6<CO, MT, NT>(nacc, sX, g6, wm, ncol0, lane);
   } else {
@@ -486,12 +576,13 @@ __device__ __forceinline__ void acc_to_lds(const f4 (&v)[MT][NT], float* s, int 
       }
 }
 
-template <int CO, int MT, int NT, bool INVERSE, int R = BM, int T = 256, bool G6 = false>
+template <int CO, int MT, int NT, bool INVERSE, int R = BM, int T = 256, bool G6 = false,
+          bool GPL = ICLR17_GDN_PLANES>
 __device__ __forceinline__ void gdn_epilogue(f4 (&x)[MT][NT], float* smem, const EngineArgs& a,
                                              const TileInfo& t, int wm, int ncol0, int lane) {
   constexpr int XS = CO + 8;
-  gdn_core<CO, MT, NT, INVERSE, R, T, G6>(x, smem, a.gbeta, a.ggamma, wm, ncol0, lane,
-                                          a.ggamma6);
+  gdn_core<CO, MT, NT, INVERSE, R, T, G6, GPL>(x, smem, a.gbeta, a.ggamma, wm, ncol0, lane,
+                                               a.ggamma6);
   if (a.out != nullptr) store_tile_rows<CO, R, T>(a, t, smem, XS, a.out, CO, 0);
   if (a.out_split != nullptr) store_tile_rows_split<CO, R, T>(a, t, smem, XS, CO, 0);
   if (a.pre != nullptr) {
@@ -834,8 +925,12 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   // an L2-miss DMA issued one step ahead, so it runs NS stages with a counted vmcnt wait.
   constexpr int NS = (EPI == EPI_QUANT && X6) ? ICLR17_QSTAGES : 2;
   constexpr int LDS_A = NS * STAGE;
-  constexpr int LDS_X = (EPI == EPI_GDN || EPI == EPI_IGDN || EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD)
-                            ? BMT * (CO + 8) + GSTAGE_FLOATS(CO) : 0;
+  constexpr int LDS_XF = BMT * (CO + 8) + GSTAGE_FLOATS(CO);
+  // x6 GDN planes, except in the phase-loop instance (held to 256 VGPRs: the planes path spills)
+  constexpr bool GPL = ICLR17_GDN_PLANES && !PL;
+  constexpr int LDS_XP = gdn_lds_floats(BMT, CO, X6, GPL);
+  constexpr int LDS_X = (EPI == EPI_GDN || EPI == EPI_IGDN) ? (LDS_XF > LDS_XP ? LDS_XF : LDS_XP)
+                        : (EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD) ? LDS_XF : 0;
   constexpr int LDS_O = BMT * (BN + 4) + 8;
   constexpr int LDS_3 = 3 * 32 * 33 + 8;
   constexpr int L1 = LDS_A > LDS_X ? LDS_A : LDS_X;
@@ -1065,7 +1160,8 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
       for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[mt][nt][r] += a.bias[ncol0 + nt * 16 + (lane & 15)];
-    gdn_epilogue<CO, MT, NT, EPI == EPI_IGDN, BMT, NWV * 64, X6>(acc, smem, a, t, wm, ncol0, lane);
+    gdn_epilogue<CO, MT, NT, EPI == EPI_IGDN, BMT, NWV * 64, X6, GPL>(acc, smem, a, t, wm, ncol0,
+                                                                     lane);
   } else if constexpr (EPI == EPI_QUANT) {
     quant_epilogue<CO, BN, MT, NT, WN>(acc, smem, a, t, wm, ncol0, lane, wave);
   } else if constexpr (EPI == EPI_OUT3) {
@@ -1394,7 +1490,8 @@ __global__ void __launch_bounds__(256) conv1_gdn_kernel(const EngineArgs a) {
   constexpr int NT = CO / WN / 16;
   constexpr int LDS_PB = P1ZERO + 4 + 256 + 64;   // patch + zero slot + k/m tables
   constexpr int LDS_P = LDS_PB + 2 * 32 * CO;                        // + two B stages
-  constexpr int LDS_X = BM * (CO + 8) + GSTAGE_FLOATS(CO);
+  constexpr int LDS_X = gdn_lds_floats(BM, CO, G6) > BM * (CO + 8) + GSTAGE_FLOATS(CO)
+                            ? gdn_lds_floats(BM, CO, G6) : BM * (CO + 8) + GSTAGE_FLOATS(CO);
   constexpr int LDS_FLOATS = LDS_P > LDS_X ? LDS_P : LDS_X;
   __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
   int* ktab = (int*)(smem + P1ZERO + 4);
@@ -1530,7 +1627,9 @@ __global__ void __launch_bounds__(256, 2) conv1_x6_kernel(const EngineArgs a) {
   constexpr int NT = CO / WN / 16;
   constexpr int S_FLOATS = 3 * P1U / 2;                 // split planes (6660 floats)
   constexpr int LDS_P = S_FLOATS + P1NI * 256;          // + the fp32 DMA landing area
-  constexpr int LDS_X = BM * (CO + 8) + (EPI == EPI_IGDN_BWD ? GSTAGE_FLOATS(CO) : 0);
+  constexpr int LDS_X = EPI == EPI_IGDN_BWD ? BM * (CO + 8) + GSTAGE_FLOATS(CO)
+                                            : gdn_lds_floats(BM, CO, true) > BM * (CO + 8)
+                                                  ? gdn_lds_floats(BM, CO, true) : BM * (CO + 8);
   constexpr int LDS_FLOATS = LDS_P > LDS_X ? LDS_P : LDS_X;
   __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
   unsigned short* sp = (unsigned short*)smem;

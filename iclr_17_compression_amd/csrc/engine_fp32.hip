@@ -52,6 +52,9 @@ constexpr int BM = 64;        // output pixels per tile
 #ifndef ICLR17_GDN_PLANES
 #define ICLR17_GDN_PLANES 1   // x6 GDN contraction: x² split once into LDS planes (not per wave)
 #endif
+#ifndef ICLR17_PL_PLANES
+#define ICLR17_PL_PLANES 0    // the planes path in the phase-loop deconv too (single B set)
+#endif
 #ifndef ICLR17_PHASE_MAJOR
 #define ICLR17_PHASE_MAJOR 1  // deconv phases dispatched phase-major (longest first)
 #endif
@@ -432,7 +435,7 @@ __device__ __forceinline__ void chan_gemm_x6(f4 (&acc)[MT][NT], const float* sX,
 // The same x6 contraction with the A operand already split in LDS: three bf16 planes
 // [3][R][CO+8] (u16), written once by the producing waves, so no wave splits rows in VALU (with
 // one wave row every wave used to split the whole x² tile for itself).
-template <int CO, int MT, int NT, int R>
+template <int CO, int MT, int NT, int R, bool SINGLE_B = false>
 __device__ __forceinline__ void chan_gemm_x6p(f4 (&acc)[MT][NT], const unsigned short* sP,
                                               const unsigned short* __restrict__ g6, int wm,
                                               int ncol0, int lane) {
@@ -475,12 +478,20 @@ __device__ __forceinline__ void chan_gemm_x6p(f4 (&acc)[MT][NT], const unsigned 
       }
     }
   };
-  load(0, b0);
-  for (int kb = 0; kb < KB; kb += 2) {
-    load(kb + 1, b1);
-    block(kb, b0);
-    if (kb + 2 < KB) load(kb + 2, b0);
-    block(kb + 1, b1);
+  if constexpr (SINGLE_B) {   // one B register set (the 256-VGPR phase-loop instance)
+    for (int kb = 0; kb < KB; ++kb) {
+      load(kb, b0);
+      block(kb, b0);
+    }
+    (void)b1;
+  } else {
+    load(0, b0);
+    for (int kb = 0; kb < KB; kb += 2) {
+      load(kb + 1, b1);
+      block(kb, b0);
+      if (kb + 2 < KB) load(kb + 2, b0);
+      block(kb + 1, b1);
+    }
   }
 }
 
@@ -495,7 +506,7 @@ constexpr int gdn_lds_floats(int R, int CO, bool G6, bool GPL = ICLR17_GDN_PLANE
 // The caller guarantees smem is free on entry; on return every wave has passed a barrier after
 // the last sX write.
 template <int CO, int MT, int NT, bool INVERSE, int R = BM, int T = 256, bool G6 = false,
-          bool GPL = ICLR17_GDN_PLANES>
+          bool GPL = ICLR17_GDN_PLANES, bool SINGLE_B = false>
 __device__ __forceinline__ void gdn_core(const f4 (&x)[MT][NT], float* sX,
                                          const float* __restrict__ gbeta,
                                          const float* __restrict__ gp, int wm, int ncol0,
@@ -523,7 +534,7 @@ __device__ __forceinline__ void gdn_core(const f4 (&x)[MT][NT], float* sX,
           sP[(2 * R + row) * XS + col] = (unsigned short)(l >> 16);
         }
     __syncthreads();   // planes of every wave published
-    chan_gemm_x6p<CO, MT, NT, R>(nacc, sP, g6, wm, ncol0, lane);
+    chan_gemm_x6p<CO, MT, NT, R, SINGLE_B>(nacc, sP, g6, wm, ncol0, lane);
   } else {
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
@@ -577,12 +588,12 @@ __device__ __forceinline__ void acc_to_lds(const f4 (&v)[MT][NT], float* s, int 
 }
 
 template <int CO, int MT, int NT, bool INVERSE, int R = BM, int T = 256, bool G6 = false,
-          bool GPL = ICLR17_GDN_PLANES>
+          bool GPL = ICLR17_GDN_PLANES, bool SINGLE_B = false>
 __device__ __forceinline__ void gdn_epilogue(f4 (&x)[MT][NT], float* smem, const EngineArgs& a,
                                              const TileInfo& t, int wm, int ncol0, int lane) {
   constexpr int XS = CO + 8;
-  gdn_core<CO, MT, NT, INVERSE, R, T, G6, GPL>(x, smem, a.gbeta, a.ggamma, wm, ncol0, lane,
-                                               a.ggamma6);
+  gdn_core<CO, MT, NT, INVERSE, R, T, G6, GPL, SINGLE_B>(x, smem, a.gbeta, a.ggamma, wm, ncol0,
+                                                         lane, a.ggamma6);
   if (a.out != nullptr) store_tile_rows<CO, R, T>(a, t, smem, XS, a.out, CO, 0);
   if (a.out_split != nullptr) store_tile_rows_split<CO, R, T>(a, t, smem, XS, CO, 0);
   if (a.pre != nullptr) {
@@ -927,7 +938,7 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   constexpr int LDS_A = NS * STAGE;
   constexpr int LDS_XF = BMT * (CO + 8) + GSTAGE_FLOATS(CO);
   // x6 GDN planes, except in the phase-loop instance (held to 256 VGPRs: the planes path spills)
-  constexpr bool GPL = ICLR17_GDN_PLANES && !PL;
+  constexpr bool GPL = ICLR17_GDN_PLANES && (!PL || ICLR17_PL_PLANES);
   constexpr int LDS_XP = gdn_lds_floats(BMT, CO, X6, GPL);
   constexpr int LDS_X = (EPI == EPI_GDN || EPI == EPI_IGDN) ? (LDS_XF > LDS_XP ? LDS_XF : LDS_XP)
                         : (EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD) ? LDS_XF : 0;
@@ -1160,8 +1171,8 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
       for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[mt][nt][r] += a.bias[ncol0 + nt * 16 + (lane & 15)];
-    gdn_epilogue<CO, MT, NT, EPI == EPI_IGDN, BMT, NWV * 64, X6, GPL>(acc, smem, a, t, wm, ncol0,
-                                                                     lane);
+    gdn_epilogue<CO, MT, NT, EPI == EPI_IGDN, BMT, NWV * 64, X6, GPL, PL>(acc, smem, a, t, wm,
+                                                                         ncol0, lane);
   } else if constexpr (EPI == EPI_QUANT) {
     quant_epilogue<CO, BN, MT, NT, WN>(acc, smem, a, t, wm, ncol0, lane, wave);
   } else if constexpr (EPI == EPI_OUT3) {

@@ -29,6 +29,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace iclr17 {
@@ -1249,6 +1251,28 @@ constexpr int D3_SA = D3_NAI * 256;             // A stage floats (976 slots × 
 constexpr int D3_SB = 32 * 48;                  // B stage floats
 constexpr int D3_LDS = D3_SA + 2 * D3_SB;
 
+// Column order of the in-loop-split path: logical column j (tile j / 16, lane j % 16) reads packed
+// column co·16 + ry·4 + rx, taking first the 12 columns with ry = 0, then the 9 with rx = 0 < ry,
+// then the rest, each (ry, rx, co)-lexicographic. A tap with dy = −1 feeds only phase ry = 0 and
+// one with dx = −1 only rx = 0 (the packed weights are zero elsewhere), so with this order the
+// three dy = −1 taps need tile 0 alone and the two other dx = −1 taps tiles 0–1: 19 tile-taps
+// per chunk instead of 27. The skipped products are exact zeros, so results are unchanged.
+#ifndef ICLR17_D3_SKIP
+#define ICLR17_D3_SKIP 1
+#endif
+__device__ __forceinline__ int d3_col(int j) {
+  int ry, rx, co;
+  if (j < 12) {          // ry = 0
+    ry = 0; rx = j / 3; co = j % 3;
+  } else if (j < 21) {   // rx = 0 < ry
+    ry = 1 + (j - 12) / 3; rx = 0; co = (j - 12) % 3;
+  } else {
+    const int k = j - 21;
+    ry = 1 + k / 9; rx = 1 + (k / 3) % 3; co = k % 3;
+  }
+  return co * 16 + ry * 4 + rx;
+}
+
 template <int CI, bool PRE = false>
 __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) {
   constexpr int KCH = 32, NCH = CI / KCH, NSTEP = 9 * NCH;
@@ -1309,16 +1333,20 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
     for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
   const int g = lane >> 4;
   const int prow = (4 * wave + 1) * D3_PS + 1 + (lane & 15);   // window origin for mt = 0
-  const int boff = (2 * g * 48 + (lane & 15)) * 4;
-
-  auto compute = [&](int buf, int tap) {
-    const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
-    const float* sb = sB + buf * D3_SB + boff;
-    bf8 Bh[NT], Bm[NT], Bl[NT];
+  int pcol[NT];   // packed column of this lane in tile nt
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
+  for (int nt = 0; nt < NT; ++nt)
+    pcol[nt] = PRE || !ICLR17_D3_SKIP ? nt * 16 + (lane & 15) : d3_col(nt * 16 + (lane & 15));
+
+  auto compute = [&](int buf, int tap, auto ntt) {
+    constexpr int NTT = decltype(ntt)::value;   // tiles this tap touches
+    const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+    const float* sb = sB + buf * D3_SB + 2 * g * 48 * 4;
+    bf8 Bh[NTT], Bm[NTT], Bl[NTT];
+#pragma unroll
+    for (int nt = 0; nt < NTT; ++nt) {
       u4 bh, bm, bl;
-      split8(*(const f4*)(sb + nt * 64), *(const f4*)(sb + 48 * 4 + nt * 64), bh, bm, bl);
+      split8(*(const f4*)(sb + pcol[nt] * 4), *(const f4*)(sb + 48 * 4 + pcol[nt] * 4), bh, bm, bl);
       Bh[nt] = __builtin_bit_cast(bf8, bh);
       Bm[nt] = __builtin_bit_cast(bf8, bm);
       Bl[nt] = __builtin_bit_cast(bf8, bl);
@@ -1332,7 +1360,7 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
       const bf8 Am = __builtin_bit_cast(bf8, *(const u4*)(sa + D3_PPX * 32));
       const bf8 Al = __builtin_bit_cast(bf8, *(const u4*)(sa + 2 * D3_PPX * 32));
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
+      for (int nt = 0; nt < NTT; ++nt) {
         f4 c = acc[mt][nt];
         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al, Bh[nt], c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bl[nt], c, 0, 0, 0);
@@ -1420,7 +1448,12 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
     __syncthreads();   // vmcnt(0) + barrier: A (at a chunk start) and B of step s landed
     const int tap = s - (s / 9) * 9;
     if (s + 1 < NSTEP && tap != 8) issue_b(s + 1, (s + 1) & 1);
-    compute(s & 1, tap);
+    if (ICLR17_D3_SKIP && tap < 3)
+      compute(s & 1, tap, std::integral_constant<int, 1>{});
+    else if (ICLR17_D3_SKIP && (tap == 3 || tap == 6))
+      compute(s & 1, tap, std::integral_constant<int, 2>{});
+    else
+      compute(s & 1, tap, std::integral_constant<int, 3>{});
     if (tap == 8 && s + 1 < NSTEP) {
       __syncthreads();   // every wave is done with this chunk's patch
       issue_a((s + 1) / 9);
@@ -1445,10 +1478,10 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int by = 4 * wave + mt, bx = 4 * g + r;
-          const int ph = lane & 15;
-          float v = acc[mt][nt][r] + a.bias[nt];
+          const int co = pcol[nt] >> 4, ph = pcol[nt] & 15;
+          float v = acc[mt][nt][r] + a.bias[co];
           if (pass == 0) v = fminf(fmaxf(v, 0.0f), 1.0f);
-          sO[(nt * OS + by * 4 + (ph >> 2)) * SS + bx * 4 + (ph & 3)] = v;
+          sO[(co * OS + by * 4 + (ph >> 2)) * SS + bx * 4 + (ph & 3)] = v;
         }
     __syncthreads();
     // wave w stores output quadrant (qy, qx) = (w >> 1, w & 1): 3 × 32 rows × 8 float4

@@ -16,7 +16,7 @@ from typing import Dict, List, Optional, Sequence
 
 import torch
 
-from . import _lib, kernels
+from . import kernels
 
 Tensor = torch.Tensor
 
@@ -144,8 +144,7 @@ def analysis_backward(enc, saved: Dict[str, Tensor], g_y: Tensor,
     mode the input-gradient contractions run on split-form gradients (g_y_split, or split here)."""
     bb1, gb1, _ = enc.gdn1.bounds_f32()
     bb2, gb2, _ = enc.gdn2.bounds_f32()
-    w3t = kernels.pack_weight(_lib.ICLR17_W_DECONV5, enc.conv3.weight, enc.out_channel_N)
-    w2t = kernels.pack_weight(_lib.ICLR17_W_DECONV5, enc.conv2.weight, enc.out_channel_N)
+    w3t, w2t = enc.packed_bwd()
     x6 = kernels.precision() == "x6"
     p2 = None if x6 else enc.gdn2.effective_params_bwd()
     p1 = None if x6 else enc.gdn1.effective_params_bwd()
@@ -210,10 +209,8 @@ def synthesis_backward(dec, saved: Dict[str, Tensor], g_recon: Tensor, g_bpp: Op
     N = dec.out_channel_N
     bq1, gq1, _ = dec.igdn1.bounds_f32()
     bq2, gq2, _ = dec.igdn2.bounds_f32()
-    d3c = None if x6 else kernels.pack_weight(_lib.ICLR17_W_CONV1, dec.deconv3.weight, N)
-    d3x = kernels.pack_conv1_x6(dec.deconv3.weight, N) if x6 else None
-    d2c = kernels.pack_weight(_lib.ICLR17_W_CONV5, dec.deconv2.weight, N)
-    d1c = kernels.pack_weight(_lib.ICLR17_W_CONV5, dec.deconv1.weight, N)
+    d3p, d2c, d1c = dec.packed_bwd(x6)
+    d3c, d3x = (None, d3p) if x6 else (d3p, None)
     q2 = dec.igdn2.effective_params_bwd_x6() if x6 else dec.igdn2.effective_params_bwd()
     q1 = dec.igdn1.effective_params_bwd_x6() if x6 else dec.igdn1.effective_params_bwd()
     y = saved["y"]

@@ -59,32 +59,40 @@ class GDN(nn.Module):
         return (float(np.float32(self.beta_bound)), float(np.float32(self.gamma_bound)),
                 float(np.float32(self.pedestal)))
 
-    def effective_params(self, force: bool = False):
-        """(beta_eff [C], gamma_packed [C*C]) on the parameters' device."""
+    def _packed_all(self, force: bool = False):
+        """(beta_eff, gamma_packed, gamma_packed_transposed), one packing launch, cached until
+        beta or gamma change (their version counters move on every in-place update)."""
         bb, gb, ped = self.bounds_f32()
         return self._pack.get("gdn", (self.beta, self.gamma),
-                              lambda: kernels.pack_gdn(self.beta, self.gamma, bb, gb, ped),
-                              force=force or self.training)
+                              lambda: kernels.pack_gdn(self.beta, self.gamma, bb, gb, ped,
+                                                       transposed=True), force=force)
+
+    def effective_params(self, force: bool = False):
+        """(beta_eff [C], gamma_packed [C*C]) on the parameters' device."""
+        be, gp, _ = self._packed_all(force)
+        return be, gp
 
     def effective_params_x6(self, force: bool = False):
         """(beta_eff, gamma_packed, gamma split planes) for the x6 inference kernels."""
         be, gp = self.effective_params(force)
         C = self.beta.shape[0]
         g6 = self._pack.get("gdn6", (self.beta, self.gamma),
-                            lambda: kernels.split_packed(gp, 1, C, C), force=force or self.training)
+                            lambda: kernels.split_packed(gp, 1, C, C), force=force)
         return be, gp, g6
 
     def effective_params_bwd(self):
         """(beta_eff, gamma_packed, gamma_packed_transposed) for the backward kernels."""
-        bb, gb, ped = self.bounds_f32()
-        return kernels.pack_gdn(self.beta, self.gamma, bb, gb, ped, transposed=True)
+        return self._packed_all()
 
     def effective_params_bwd_x6(self):
         """effective_params_bwd plus γ and γᵀ split for the x6 backward contractions:
         (beta_eff, gamma_packed, gamma_packed_t, gamma_split, gamma_t_split)."""
-        be, gp, gpt = self.effective_params_bwd()
+        be, gp, gpt = self._packed_all()
         C = self.beta.shape[0]
-        return be, gp, gpt, kernels.split_packed(gp, 1, C, C), kernels.split_packed(gpt, 1, C, C)
+        g6 = self.effective_params_x6()[2]
+        g6t = self._pack.get("gdn6t", (self.beta, self.gamma),
+                             lambda: kernels.split_packed(gpt, 1, C, C))
+        return be, gp, gpt, g6, g6t
 
     def forward(self, inputs):
         unfold = inputs.dim() == 5

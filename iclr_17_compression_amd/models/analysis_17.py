@@ -37,7 +37,7 @@ class Analysis_net_17(nn.Module):
         self._pack = PackCache()
 
     def packed(self, force: bool = False):
-        N, f = self.out_channel_N, force or self.training
+        N, f = self.out_channel_N, force
         w1 = self._pack.get("w1", (self.conv1.weight,),
                             lambda: kernels.pack_weight(_lib.ICLR17_W_CONV1, self.conv1.weight, N), f)
         w2 = self._pack.get("w2", (self.conv2.weight,),
@@ -53,7 +53,17 @@ class Analysis_net_17(nn.Module):
         N = self.out_channel_N
         return self._pack.get("w1x6", (self.conv1.weight,),
                               lambda: kernels.pack_conv1_x6(self.conv1.weight, N),
-                              force or self.training)
+                              force)
+
+    def packed_bwd(self):
+        """conv3 / conv2 weights packed as the transposed convolutions of their input gradients
+        (the engine's deconv layout), cached until the weights change."""
+        N = self.out_channel_N
+        w3t = self._pack.get("w3t", (self.conv3.weight,),
+                             lambda: kernels.pack_weight(_lib.ICLR17_W_DECONV5, self.conv3.weight, N))
+        w2t = self._pack.get("w2t", (self.conv2.weight,),
+                             lambda: kernels.pack_weight(_lib.ICLR17_W_DECONV5, self.conv2.weight, N))
+        return w3t, w2t
 
     def features(self, x):
         """conv1+gdn1 → conv2+gdn2 as NHWC (the input of conv3); no autograd."""

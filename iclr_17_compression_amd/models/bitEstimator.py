@@ -49,14 +49,14 @@ class BitEstimator(nn.Module):
     def packed(self, force: bool = False):
         """Per-channel table [11][C]: softplus(h_k), b_k, tanh(a_k) (k=1..3), softplus(h4), b4."""
         ps = self.params_in_order()
-        return self._pack.get("rate", ps, lambda: kernels.pack_rate(ps), force=force or self.training)
+        return self._pack.get("rate", ps, lambda: kernels.pack_rate(ps), force=force)
 
     def entropy_tables(self, K: int = kernels.ENTROPY_K):
         """Quantised CDFs for the entropy coder (cached like the packed parameters)."""
         ps = self.params_in_order()
         return self._pack.get(f"cdf{K}", ps,
                               lambda: kernels.entropy_tables(self.packed(), self.channel, K),
-                              force=self.training)
+                              )
 
     def forward(self, x):
         # bitEstimator.py:38-42

@@ -38,7 +38,7 @@ class Synthesis_net_17(nn.Module):
         self._pack = PackCache()
 
     def packed(self, force: bool = False):
-        N, f = self.out_channel_N, force or self.training
+        N, f = self.out_channel_N, force
         d1 = self._pack.get("d1", (self.deconv1.weight,),
                             lambda: kernels.pack_weight(_lib.ICLR17_W_DECONV5, self.deconv1.weight, N), f)
         d2 = self._pack.get("d2", (self.deconv2.weight,),
@@ -52,7 +52,24 @@ class Synthesis_net_17(nn.Module):
         N = self.out_channel_N
         return self._pack.get("d3x6", (self.deconv3.weight,),
                               lambda: kernels.split_deconv3(self.packed(force)[2], N),
-                              force or self.training)
+                              force)
+
+    def packed_bwd(self, x6: bool):
+        """The deconv weights packed as the convolutions of their input gradients: (deconv3 in
+        the conv1 layout — x6 split form when ``x6`` —, deconv2, deconv1 in the conv5 layout),
+        cached until the weights change."""
+        N = self.out_channel_N
+        if x6:
+            d3 = self._pack.get("d3cx6", (self.deconv3.weight,),
+                                lambda: kernels.pack_conv1_x6(self.deconv3.weight, N))
+        else:
+            d3 = self._pack.get("d3c", (self.deconv3.weight,),
+                                lambda: kernels.pack_weight(_lib.ICLR17_W_CONV1, self.deconv3.weight, N))
+        d2c = self._pack.get("d2c", (self.deconv2.weight,),
+                             lambda: kernels.pack_weight(_lib.ICLR17_W_CONV5, self.deconv2.weight, N))
+        d1c = self._pack.get("d1c", (self.deconv1.weight,),
+                             lambda: kernels.pack_weight(_lib.ICLR17_W_CONV5, self.deconv1.weight, N))
+        return d3, d2c, d1c
 
     @staticmethod
     def to_nhwc(y):

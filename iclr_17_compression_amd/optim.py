@@ -82,4 +82,7 @@ class FusedAdam(torch.optim.Optimizer):
             clip = float(self.grad_clip) if self.grad_clip else 0.0
             call("iclr17_adam_step", kernels._p(self._desc), len(ps), max_n, float(group["lr"]),
                  float(b1), float(b2), float(group["eps"]), t, clip, kernels._stream(ps[0]))
+            # the kernel updated the parameters through raw pointers: move their version
+            # counters as an in-place op would, so version-keyed caches (packed weights) refresh
+            torch.autograd.graph.increment_version(ps)
         return loss

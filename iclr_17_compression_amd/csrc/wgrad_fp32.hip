@@ -31,7 +31,8 @@ __device__ __forceinline__ void glds16w(const float* src, float* lds_wave_base) 
 typedef float f16w __attribute__((ext_vector_type(16)));
 
 // GEMM: dW[m][tap, c] = Σ_p G[p][m] · X[p ⊕ tap][c] for one tap and a 64-channel tile c, over one
-// split of the pixels. v_mfma_f32_32x32x2_f32 (exact f32; lane l holds A[m = l&31][k = l>>5] and
+// split of the pixels (SQUARE: the GDN γ gradient, a 1×1 tap over X², pixel p = row p of X).
+// v_mfma_f32_32x32x2_f32 (exact f32; lane l holds A[m = l&31][k = l>>5] and
 // B[k = l>>5][c = l&31]): a k-step of two pixels needs one element per lane per operand, and 32
 // consecutive lanes read 32 consecutive channels of one LDS pixel row — conflict-free
 // ds_read_b32, the [pixel][channel] tiles need no transpose. Both tiles arrive by LDS-DMA:
@@ -78,7 +79,9 @@ __global__ void __launch_bounds__(256) wgrad_k5_kernel(const float* __restrict__
         const int row = xi * 4 + (lane >> 4), piece = lane & 15;
         const long p = pb + row;
         const float* src = g_wzero;
-        if (p < p1) {
+        if (SQUARE) {   // the GDN 1×1 case: pixel p is row p of X, no spatial mapping
+          if (p < p1) src = X + p * C + ct * 64 + piece * 4;
+        } else if (p < p1) {
           const int ow = (int)(p % Wo);
           const long q = p / Wo;
           const int oh = (int)(q % Ho);

@@ -35,7 +35,7 @@ if [ -n "${VARIANTS:-}" ]; then
     for v in $VARIANTS; do
       n=${v%%:*}
       ICLR17_LIB=/tmp/ab_$n/libiclr17.so step ab_${n}_$r 300 python bench.py --no-cpu-baseline ${BENCH_ARGS:-} || exit 1
-      python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], {k: v['ms'] for k, v in d['layers'].items()})" "$O/ab_${n}_$r.log" $n | tee -a "$O/ab.txt"
+      python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], {k: v['ms'] for k, v in d.get('layers', {}).items()})" "$O/ab_${n}_$r.log" $n | tee -a "$O/ab.txt"
     done
   done
 fi

@@ -270,18 +270,27 @@ __global__ void rate_bits_kernel(const float* __restrict__ z, int C, int HW, int
   }
 }
 
-__global__ void reduce_partials_kernel(const double* __restrict__ partial, int B, int T,
-                                       double* per_image, float* total, double scale) {
+// Per-image sums of T partials, then their total. One workgroup of 16 waves: wave w reduces
+// images w, w + 16, … (lane-strided sums, then a fixed butterfly), thread 0 adds the images in
+// order. Fixed order throughout: bitwise reproducible for a given (B, T).
+__global__ void __launch_bounds__(1024) reduce_partials_kernel(const double* __restrict__ partial,
+                                                               int B, int T, double* per_image,
+                                                               float* total, double scale) {
   __shared__ double img[1024];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double acc = 0.0;
   for (int b0 = 0; b0 < B; b0 += 1024) {
     const int nb = B - b0 < 1024 ? B - b0 : 1024;
-    for (int b = threadIdx.x; b < nb; b += blockDim.x) {
-      double s = 0.0;
+    for (int b = wave; b < nb; b += 16) {
       const double* p = partial + (long)(b0 + b) * T;
-      for (int t = 0; t < T; ++t) s += p[t];
-      img[b] = s;
-      if (per_image) per_image[b0 + b] = s;
+      double s = 0.0;
+      for (int t = lane; t < T; t += 64) s += p[t];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+      if (lane == 0) {
+        img[b] = s;
+        if (per_image) per_image[b0 + b] = s;
+      }
     }
     __syncthreads();
     if (threadIdx.x == 0)
@@ -524,7 +533,7 @@ int iclr17_rate_bits(const float* z, int B, int C, int h, int w, int layout,
 int iclr17_reduce_partials(const double* partial, int B, int T, double* per_image, float* total,
                            double scale, void* stream) {
   ICLR17_REQUIRE(partial && B > 0 && T > 0, ICLR17_EINVAL, "reduce_partials: bad arguments");
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(256), 0, S(stream), partial, B, T,
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(1024), 0, S(stream), partial, B, T,
                      per_image, total, scale);
   return check_launch("reduce_partials");
 }

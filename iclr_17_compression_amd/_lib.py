@@ -98,6 +98,8 @@ SIGNATURES = {
     "iclr17_wgrad_k9": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P]),
     "iclr17_gdn_wgrad_workspace_size": (_SZ, [ctypes.c_long, _I]),
     "iclr17_gdn_wgrad": (_I, [_P, _P, ctypes.c_long, _I, _P, _P, _P]),
+    "iclr17_gdn_wgrad_x6_workspace_size": (_SZ, [ctypes.c_long, _I]),
+    "iclr17_gdn_wgrad_x6": (_I, [_P, _P, ctypes.c_long, _I, _P, _P, _P]),
     "iclr17_gdn_param_chain": (_I, [_P, _P, _P, _P, _I, _F, _F, _P, _P, _P]),
     "iclr17_bias_grad_nhwc": (_I, [_P, ctypes.c_long, _I, _P, _P, _P]),
     "iclr17_bias_grad_nchw": (_I, [_P, _I, _I, ctypes.c_long, _P, _P, _P]),

@@ -342,6 +342,188 @@ __global__ void __launch_bounds__(512) wgrad_x6_kernel(const unsigned short* __r
       }
 }
 
+// GDN.py:83 γ gradient in x6: dγ_eff[i][j] = Σ_p dn[p][i] · u[p][j]², straight from the fp32
+// tensors. The tiles, LDS images and MFMA loop are wgrad_x6_kernel's (M = CB = C, one tap), but
+// the workgroup stages the operands itself: each thread loads its fp32 pieces of the next step
+// into registers while the current step computes, squares u, splits both into the three bf16
+// planes and writes them to the idle LDS buffer — no split copies of dn and u² in HBM, which
+// would cost more traffic than the x6 contraction saves. One workgroup per pixel split.
+__device__ __forceinline__ int swz6(int r, int row_elems) {
+  return row_elems == 192 ? 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1))
+                          : 2 * ((r & 3) | (((r >> 3) & 1) << 2));
+}
+
+__device__ __forceinline__ void split4(const f4& x, uint2& hi, uint2& mi, uint2& lo) {
+  unsigned h[4], m[4], l[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    h[i] = __float_as_uint(x[i]) & 0xffff0000u;
+    const float r = x[i] - __uint_as_float(h[i]);
+    m[i] = __float_as_uint(r) & 0xffff0000u;
+    l[i] = __float_as_uint(r - __uint_as_float(m[i]));
+  }
+  hi = uint2{__builtin_amdgcn_perm(h[1], h[0], 0x07060302u), __builtin_amdgcn_perm(h[3], h[2], 0x07060302u)};
+  mi = uint2{__builtin_amdgcn_perm(m[1], m[0], 0x07060302u), __builtin_amdgcn_perm(m[3], m[2], 0x07060302u)};
+  lo = uint2{__builtin_amdgcn_perm(l[1], l[0], 0x07060302u), __builtin_amdgcn_perm(l[3], l[2], 0x07060302u)};
+}
+
+#ifndef ICLR17_GDN6_PF2
+#define ICLR17_GDN6_PF2 0   // 1: dn loads two steps ahead (6 VGPRs spill at C = 192)
+#endif
+template <int C>
+__global__ void __launch_bounds__(512) gdn_wgrad_x6_kernel(const float* __restrict__ G,
+                                                             const float* __restrict__ X, long P,
+                                                             int nsplit, float* __restrict__ part) {
+  constexpr int WM = 2, WN = 4, MT = C / WM / 16, NT = C / WN / 16;
+  constexpr int PL = KP * C;            // u16 per plane image
+  constexpr int STAGE = 6 * PL;         // three G planes, then three X planes
+  constexpr int R4 = C / 4;             // float4 pieces per pixel row
+  constexpr int NV = KP * R4 / 512;     // pieces per thread per operand per step
+  static_assert(C == 192 || C == 128, "C");
+  static_assert(KP * R4 % 512 == 0, "whole pieces per thread");
+  __shared__ __attribute__((aligned(16))) unsigned short smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int split = blockIdx.x;
+  const long per = ((P + nsplit - 1) / nsplit + KP - 1) / KP * KP;
+  const long p0 = split * per;
+  const long p1 = p0 + per < P ? p0 + per : P;
+  const int nsteps = p1 > p0 ? (int)((p1 - p0 + KP - 1) / KP) : 0;
+
+  int prow[NV], gofs[NV], wofs[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int e = tid + 512 * v;
+    const int r = e / R4, ch = (e % R4) * 4;
+    prow[v] = r;
+    gofs[v] = r * C + ch;
+    wofs[v] = r * C + (((ch >> 3) ^ swz6(r, C)) << 3) + (ch & 7);
+  }
+  // dn pieces run two steps ahead (two register sets), u pieces one step
+  f4 rga[NV], rgb[NV], rx[NV];
+  auto load_one = [&](const float* base, int s, f4 (&r)[NV]) {
+    const long pb = p0 + (long)s * KP;
+    const float* b = base + pb * C;
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+      r[v] = pb + prow[v] < p1 ? *(const f4*)(b + gofs[v]) : f4{0.f, 0.f, 0.f, 0.f};
+  };
+  auto convert = [&](int buf, const f4 (&rg)[NV], const f4 (&ru)[NV]) {
+    unsigned short* st = smem + buf * STAGE;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      uint2 h, m, l;
+      split4(rg[v], h, m, l);
+      *(uint2*)(st + wofs[v]) = h;
+      *(uint2*)(st + PL + wofs[v]) = m;
+      *(uint2*)(st + 2 * PL + wofs[v]) = l;
+      const f4 sq = ru[v] * ru[v];   // u², rounded as the fp32 reference's x ** 2
+      split4(sq, h, m, l);
+      *(uint2*)(st + 3 * PL + wofs[v]) = h;
+      *(uint2*)(st + 4 * PL + wofs[v]) = m;
+      *(uint2*)(st + 5 * PL + wofs[v]) = l;
+    }
+  };
+
+  f4 acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const int fr = swz6(8 * g + q, C);
+  int aoff[MT], boff[NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int ch = wm * (C / WM) + mt * 16 + 4 * pp;
+    aoff[mt] = (8 * g + q) * C + (((ch >> 3) ^ fr) << 3) + (ch & 7);
+  }
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int ch = wn * (C / WN) + nt * 16 + 4 * pp;
+    boff[nt] = (8 * g + q) * C + (((ch >> 3) ^ fr) << 3) + (ch & 7);
+  }
+
+  auto compute = [&](int buf) {
+    const unsigned short* st = smem + buf * STAGE;
+    bf8 Bf[3][NT];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const unsigned short* b = st + (3 + pl) * PL + boff[nt];
+        const uint2 lo = tr16(b), hi = tr16(b + 4 * C);
+        Bf[pl][nt] = __builtin_bit_cast(bf8, u4{lo.x, lo.y, hi.x, hi.y});
+      }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      bf8 Af[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+        const unsigned short* a = st + pl * PL + aoff[mt];
+        const uint2 lo = tr16(a), hi = tr16(a + 4 * C);
+        Af[pl] = __builtin_bit_cast(bf8, u4{lo.x, lo.y, hi.x, hi.y});
+      }
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        f4 c = acc[mt][nt];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af[2], Bf[0][nt], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af[0], Bf[2][nt], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af[1], Bf[1][nt], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af[1], Bf[0][nt], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af[0], Bf[1][nt], c, 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af[0], Bf[0][nt], c, 0, 0, 0);
+      }
+    }
+  };
+
+  // step s computes LDS buffer s & 1; set a holds even steps, set b odd ones
+  if (nsteps > 0) {
+    load_one(G, 0, rga);
+    load_one(X, 0, rx);
+    convert(0, rga, rx);
+  }
+#if !ICLR17_GDN6_PF2
+  for (int s = 0; s < nsteps; ++s) {
+    __syncthreads();   // buffer s & 1 holds step s; the other one is no longer read
+    if (s + 1 < nsteps) {
+      load_one(G, s + 1, rga);
+      load_one(X, s + 1, rx);
+    }
+    compute(s & 1);
+    if (s + 1 < nsteps) convert((s + 1) & 1, rga, rx);
+  }
+  (void)rgb;
+#else
+  if (nsteps > 1) load_one(G, 1, rgb);
+  for (int s = 0; s < nsteps; s += 2) {
+    __syncthreads();   // buffer 0 holds step s; buffer 1 no longer read
+    if (s + 1 < nsteps) load_one(X, s + 1, rx);
+    if (s + 2 < nsteps) load_one(G, s + 2, rga);
+    compute(0);
+    if (s + 1 >= nsteps) break;
+    convert(1, rgb, rx);
+    __syncthreads();   // buffer 1 holds step s + 1; buffer 0 no longer read
+    if (s + 2 < nsteps) load_one(X, s + 2, rx);
+    if (s + 3 < nsteps) load_one(G, s + 3, rgb);
+    compute(1);
+    if (s + 2 < nsteps) convert(0, rga, rx);
+  }
+#endif
+  float* out = part + (long)split * C * C;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = wm * (C / WM) + mt * 16 + 4 * (lane >> 4) + r;
+        const int c = wn * (C / WN) + nt * 16 + (lane & 15);
+        out[(long)m * C + c] = acc[mt][nt][r];
+      }
+}
+
 // k9 s4 p4 weight gradient in x6 as a 1×1 one: the 243 (c, kh, kw) window values of every
 // output pixel, split, as the X operand [3][P][256] (k = c·81 + kh·9 + kw, the PyTorch
 // [M][3][9][9] order; k ≥ 243 zero) — im2col of a 3-channel NCHW image, 8 k per thread.
@@ -573,6 +755,10 @@ int wgrad6_splits(long P, int tiles) {   // one round of 256 workgroup slots (1 
   return s < 1 ? 1 : s;
 }
 int wgrad9_splits(int ntiles) { return ntiles < 128 ? ntiles : 128; }
+int gdn6_splits(long P) {   // one workgroup per CU, at least 4 steps of 32 pixels each
+  const long s = P / 128;
+  return s > 256 ? 256 : s < 1 ? 1 : (int)s;
+}
 
 int wgrad_splits(long P, int tiles) {
   // as many splits as fit ONE round of 512 workgroup slots (256 CUs × 2): a grid just over 512
@@ -722,6 +908,28 @@ int iclr17_gdn_wgrad(const float* dn, const float* u, long P, int C, float* work
   const long n = (long)C * C;
   hipLaunchKernelGGL(sum_splits_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, workspace, ns, n, dgamma_eff);
   return check_launch("gdn_wgrad_sum");
+}
+
+size_t iclr17_gdn_wgrad_x6_workspace_size(long P, int C) {
+  return (size_t)gdn6_splits(P) * C * C;
+}
+
+// iclr17_gdn_wgrad in the x6 scheme (fp32 dn and u in, split by the kernel).
+int iclr17_gdn_wgrad_x6(const float* dn, const float* u, long P, int C, float* workspace,
+                        float* dgamma_eff, void* stream) {
+  ICLR17_REQUIRE(P > 0 && (C == 128 || C == 192), ICLR17_EUNSUPPORTED, "gdn_wgrad_x6: C=%d", C);
+  ICLR17_REQUIRE(dn && u && workspace && dgamma_eff, ICLR17_EINVAL, "gdn_wgrad_x6: null pointer");
+  const int ns = gdn6_splits(P);
+  hipStream_t st = S(stream);
+  if (C == 192)
+    hipLaunchKernelGGL(gdn_wgrad_x6_kernel<192>, dim3(ns), dim3(512), 0, st, dn, u, P, ns, workspace);
+  else
+    hipLaunchKernelGGL(gdn_wgrad_x6_kernel<128>, dim3(ns), dim3(512), 0, st, dn, u, P, ns, workspace);
+  int rc = check_launch("gdn_wgrad_x6");
+  if (rc) return rc;
+  const long n = (long)C * C;
+  hipLaunchKernelGGL(sum_splits_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, workspace, ns, n, dgamma_eff);
+  return check_launch("gdn_wgrad_x6_sum");
 }
 
 size_t iclr17_sum_rows_workspace_size(int C) { return (size_t)SUM_ROWS_SPLITS * C; }

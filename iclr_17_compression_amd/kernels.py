@@ -827,15 +827,26 @@ def wgrad_k9(G: Tensor, X: Tensor) -> Tensor:
     return dW
 
 
+def gdn_wgrad(dn: Tensor, u: Tensor, x6: Optional[bool] = None) -> Tensor:
+    """dγ_eff [C, C] = Σ_p dn[p] ⊗ u[p]² (GDN.py:83); x6 (default: the build's precision) or
+    exact f32."""
+    C = dn.shape[-1]
+    P = dn.numel() // C
+    if x6 is None:
+        x6 = precision() == "x6"
+    name = "iclr17_gdn_wgrad_x6" if x6 else "iclr17_gdn_wgrad"
+    ws = torch.empty(query(name + "_workspace_size", P, C), device=dn.device, dtype=torch.float32)
+    dge = torch.empty(C, C, device=dn.device, dtype=torch.float32)
+    call(name, _p(dn.contiguous()), _p(u.contiguous()), P, C, _p(ws), _p(dge), _stream(dn))
+    return dge
+
+
 def gdn_param_grads(dn: Tensor, u: Tensor, dbe: Tensor, beta: Tensor, gamma: Tensor,
                     beta_bound: float = DEFAULT_BETA_BOUND, gamma_bound: float = DEFAULT_GAMMA_BOUND):
     """GDN parameter gradients (dβ, dγ) in the raw-parameter space (through GDN.py:73-79);
     dbe = ∂β_eff (Σ dn, from the backward kernel's column sums)."""
     C = dn.shape[-1]
-    P = dn.numel() // C
-    ws = torch.empty(query("iclr17_gdn_wgrad_workspace_size", P, C), device=dn.device, dtype=torch.float32)
-    dge = torch.empty(C, C, device=dn.device, dtype=torch.float32)
-    call("iclr17_gdn_wgrad", _p(dn.contiguous()), _p(u.contiguous()), P, C, _p(ws), _p(dge), _stream(dn))
+    dge = gdn_wgrad(dn, u)
     db = torch.empty_like(dbe)
     dg = torch.empty_like(dge)
     call("iclr17_gdn_param_chain", _p(beta.detach().contiguous()), _p(gamma.detach().contiguous()),

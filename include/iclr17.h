@@ -357,6 +357,11 @@ int iclr17_wgrad_k9(const float* G, const float* X, int B, int Ho, int Wo, int M
 size_t iclr17_gdn_wgrad_workspace_size(long P, int C);
 int iclr17_gdn_wgrad(const float* dn, const float* u, long P, int C, float* workspace,
                      float* dgamma_eff, void* stream);
+/* The same gradient in the x6 scheme: dn and u² split into three bf16 parts inside the kernel,
+ * six part products per MAC on the bf16 MFMA, fp32 accumulation. */
+size_t iclr17_gdn_wgrad_x6_workspace_size(long P, int C);
+int iclr17_gdn_wgrad_x6(const float* dn, const float* u, long P, int C, float* workspace,
+                        float* dgamma_eff, void* stream);
 /* GDN.py:10-24,73-79 chain: dβ = LowerBoundᵀ(dβ_eff · 2·max(β, bβ)), same for γ. */
 int iclr17_gdn_param_chain(const float* beta, const float* gamma, const float* dbeta_eff,
                            const float* dgamma_eff, int C, float beta_bound, float gamma_bound,

@@ -221,3 +221,21 @@ def test_wgrad_k9_x6_matches_fp32(device, M, B, Ho, Wo):
     got = kernels.wgrad_k9_x6(kernels.split_planes(G), X)
     torch.cuda.synchronize()
     assert grad_err(got, ref) < 1e-5
+
+
+@pytest.mark.parametrize("C,P", [(192, 131072), (192, 1000 + 17), (128, 4096 + 5), (192, 40)])
+def test_gdn_wgrad_x6_matches_fp32(device, C, P):
+    """The x6 GDN γ gradient (dn and u² split inside the kernel) against the exact-f32 kernel and a
+    float64 reference on the same values: full-size GDN1 pixels, ragged last steps, fewer pixels
+    than one split."""
+    from iclr_17_compression_amd import kernels
+    dn = torch.from_numpy(synth.normal_like(25, (P, C), 1.0))
+    u = torch.from_numpy(synth.normal_like(26, (P, C), 1.0))
+    ref64 = dn.double().t() @ (u.float() * u.float()).double()
+    dd, ud = dn.to(device), u.to(device)
+    got = kernels.gdn_wgrad(dd, ud, x6=True)
+    f32 = kernels.gdn_wgrad(dd, ud, x6=False)
+    torch.cuda.synchronize()
+    assert grad_err(got, ref64.float()) < 1e-5
+    assert grad_err(got, f32) < 1e-5
+    assert torch.equal(kernels.gdn_wgrad(dd, ud, x6=True), got)   # deterministic

@@ -228,8 +228,8 @@ def run_kodak(args, dev):
     land = torch.cat([imgs[i] for i in range(24) if i not in KODAK_PORTRAIT]).to(dev)
     port = torch.cat([imgs[i] for i in KODAK_PORTRAIT]).to(dev)
 
-    def step():
-        return net.evaluate(land, want_msssim=True), net.evaluate(port, want_msssim=True)
+    def step():   # the two orientations on concurrent streams (ImageCompressor.evaluate_many)
+        return tuple(net.evaluate_many([land, port], want_msssim=True))
 
     with torch.no_grad():
         for _ in range(args.warmup):

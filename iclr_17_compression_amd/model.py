@@ -200,3 +200,47 @@ class ImageCompressor(nn.Module):
             res["ms_ssim"] = ms
             res["ms_ssim_db"] = -10 * (torch.log(1 - ms) / math.log(10))
         return res
+
+    def _warm_packs(self) -> None:
+        """Build (or refresh) every derived parameter layout ``run`` reads in eval mode, on the
+        current stream."""
+        self.Encoder.packed()
+        self.Decoder.packed()
+        self.bitEstimator.packed()
+        if kernels.precision() == "x6":
+            self.Encoder.packed_conv1_x6()
+            for g in (self.Encoder.gdn1, self.Encoder.gdn2, self.Decoder.igdn1, self.Decoder.igdn2):
+                g.effective_params_x6()
+
+    def evaluate_many(self, batches, want_y: bool = False,
+                      want_msssim: bool = False):
+        """``evaluate`` of several batches (e.g. Kodak's landscape and portrait images, which
+        cannot share one batch) on concurrent HIP streams: the first on the current stream, each
+        other on a side stream, so one batch's partly filled last round of workgroups in every
+        layer overlaps the other's work. Same kernels and inputs per batch, so the results are
+        bitwise those of sequential ``evaluate`` calls."""
+        batches = list(batches)
+        if len(batches) <= 1 or not batches[0].is_cuda:
+            return [self.evaluate(b, want_y=want_y, want_msssim=want_msssim) for b in batches]
+        cur = torch.cuda.current_stream(batches[0].device)
+        streams = getattr(self, "_side_streams", [])
+        while len(streams) < len(batches) - 1:
+            streams.append(torch.cuda.Stream(device=batches[0].device))
+        self._side_streams = streams
+        self._warm_packs()   # packs are written on cur before any side stream reads them
+        outs = [None] * len(batches)
+        for i, b in enumerate(batches):
+            if i == 0:
+                continue
+            s = streams[i - 1]
+            s.wait_stream(cur)
+            b.record_stream(s)
+            with torch.cuda.stream(s):
+                outs[i] = self.evaluate(b, want_y=want_y, want_msssim=want_msssim)
+        outs[0] = self.evaluate(batches[0], want_y=want_y, want_msssim=want_msssim)
+        for i in range(1, len(batches)):
+            cur.wait_stream(streams[i - 1])
+            for t in outs[i].values():
+                if isinstance(t, torch.Tensor):
+                    t.record_stream(cur)
+        return outs

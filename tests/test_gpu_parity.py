@@ -376,6 +376,21 @@ def test_determinism_and_batch_independence(device, precision):
         assert torch.equal(evi["clipped"][0], ev1["clipped"][i])
 
 
+def test_evaluate_many_matches_sequential(device, precision):
+    """evaluate_many (batches of different shapes on concurrent streams, as the Kodak bench runs
+    landscape and portrait images) gives bitwise the sequential evaluate() results."""
+    net = net_for(192, 1, device)
+    land = image(31, 2, 192, 256).to(device)   # MS-SSIM's 5 levels need ≥ 176 px per side
+    port = image(32, 1, 256, 192).to(device)
+    seq = [net.evaluate(b, want_msssim=True) for b in (land, port)]
+    for _ in range(2):
+        many = net.evaluate_many([land, port], want_msssim=True)
+        torch.cuda.synchronize()
+        for a, b in zip(many, seq):
+            for k in ("clipped", "y_hat", "bpp", "mse", "psnr", "ms_ssim"):
+                assert torch.equal(a[k], b[k]), k
+
+
 def test_ms_ssim_vs_reference_fixture(device, golden_dir):
     """GPU MS-SSIM against the reference's values on the G6 pairs (incl. odd pyramid levels and
     B = 2). The fp32 filter sums run in another order than oneDNN's, so the bar is 1e-5 rel."""

@@ -28,6 +28,9 @@ ICLR17_W_CONV5 = 1
 ICLR17_W_DECONV5 = 2
 ICLR17_W_DECONV9 = 3
 ICLR17_W_CONV1_X6 = 4
+ICLR17_PACK_GDN = 16
+ICLR17_PACK_RATE = 17
+ICLR17_PACK_SPLIT = 18
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -44,6 +47,7 @@ SIGNATURES = {
     "iclr17_pack_weight": (_I, [_I, _P, _P, _I, _P]),
     "iclr17_pack_gdn": (_I, [_P, _P, _P, _P, _P, _I, _F, _F, _F, _P]),
     "iclr17_pack_rate": (_I, [_P] * 12 + [_I, _P]),
+    "iclr17_pack_batch": (_I, [_P, _I, _P, _P]),
     "iclr17_analysis_conv1_gdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_analysis_conv2_gdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_analysis_conv3_quant_rate": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P]),

@@ -17,22 +17,20 @@ struct TapList {
   int kw[25];
 };
 
+// Element i of each packed layout (a pure index map of the reference tensor, so a batch of
+// packs can run in one launch: pack_batch_kernel below).
 // conv1 [N][3][9][9] → [64 quads][N][4], k = c·81 + kh·9 + kw, k ≥ 243 zero.
-__global__ void pack_conv1_kernel(const float* __restrict__ w, float* __restrict__ out, int N) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 256 * N) return;
-  const int e = i & 3, n = (i >> 2) % N, q = (i >> 2) / N;
+__device__ __forceinline__ float pk_conv1(const float* __restrict__ w, int N, long i) {
+  const int e = i & 3, n = (int)((i >> 2) % N), q = (int)((i >> 2) / N);
   const int k = 4 * q + e;
-  out[i] = k < 243 ? w[(long)n * 243 + k] : 0.f;
+  return k < 243 ? w[(long)n * 243 + k] : 0.f;
 }
 
 // conv1 [N][3][9][9] → [64 quads][N][4] in the x6 kernel's k order (engine_fp32.hip,
 // conv1_x6_kernel): k' = 8g + e; g < 27: (c, kh) = (g / 9, g % 9), kw = e; g = 27: zero;
 // g ≥ 28: pair (g − 28)·8 + e (< 27, else zero), kw = 8.
-__global__ void pack_conv1_x6_kernel(const float* __restrict__ w, float* __restrict__ out, int N) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 256 * N) return;
-  const int e4 = i & 3, n = (i >> 2) % N, q = (i >> 2) / N;
+__device__ __forceinline__ float pk_conv1_x6(const float* __restrict__ w, int N, long i) {
+  const int e4 = i & 3, n = (int)((i >> 2) % N), q = (int)((i >> 2) / N);
   const int k = 4 * q + e4, g = k >> 3, e = k & 7;
   int src = -1;
   if (g < 27) {
@@ -41,61 +39,51 @@ __global__ void pack_conv1_x6_kernel(const float* __restrict__ w, float* __restr
     const int p = (g - 28) * 8 + e;
     if (p < 27) src = p * 9 + 8;
   }
-  out[i] = src >= 0 ? w[(long)n * 243 + src] : 0.f;
+  return src >= 0 ? w[(long)n * 243 + src] : 0.f;
 }
 
 // conv k5 [co][ci][5][5] → [25 taps][ci/4][co][4], tap = kh·5 + kw.
-__global__ void pack_conv5_kernel(const float* __restrict__ w, float* __restrict__ out, int N) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long total = 25L * N * N;
-  if (i >= total) return;
+__device__ __forceinline__ float pk_conv5(const float* __restrict__ w, int N, long i) {
   const int e = i & 3;
-  const int co = (i >> 2) % N;
+  const int co = (int)((i >> 2) % N);
   const long r = (i >> 2) / N;
-  const int q = r % (N / 4), tap = r / (N / 4);
+  const int q = (int)(r % (N / 4)), tap = (int)(r / (N / 4));
   const int ci = 4 * q + e;
-  out[i] = w[((long)co * N + ci) * 25 + tap];
+  return w[((long)co * N + ci) * 25 + tap];
 }
 
 // deconv k5 [ci][co][5][5] → phase-major taps [25][ci/4][co][4].
-__global__ void pack_deconv5_kernel(const float* __restrict__ w, float* __restrict__ out, int N,
-                                    TapList tl) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long total = 25L * N * N;
-  if (i >= total) return;
+__device__ __forceinline__ float pk_deconv5(const float* __restrict__ w, int N, const TapList& tl,
+                                            long i) {
   const int e = i & 3;
-  const int co = (i >> 2) % N;
+  const int co = (int)((i >> 2) % N);
   const long r = (i >> 2) / N;
-  const int q = r % (N / 4), tap = r / (N / 4);
+  const int q = (int)(r % (N / 4)), tap = (int)(r / (N / 4));
   const int ci = 4 * q + e;
-  out[i] = w[((long)ci * N + co) * 25 + tl.kh[tap] * 5 + tl.kw[tap]];
+  return w[((long)ci * N + co) * 25 + tl.kh[tap] * 5 + tl.kw[tap]];
 }
 
 // deconv3 [ci][3][9][9] → all-phase [9 neighbours][ci/4][48][4]; column n = co·16 + ry·4 + rx,
 // neighbour (dy, dx) ∈ {-1,0,1}², kernel tap k = r + 4 − 4d (zero outside 0..8).
-__global__ void pack_deconv9_kernel(const float* __restrict__ w, float* __restrict__ out, int N) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long total = 9L * N * 48;
-  if (i >= total) return;
+__device__ __forceinline__ float pk_deconv9(const float* __restrict__ w, int N, long i) {
   const int e = i & 3;
-  const int n = (i >> 2) % 48;
+  const int n = (int)((i >> 2) % 48);
   const long r = (i >> 2) / 48;
-  const int q = r % (N / 4), nb = r / (N / 4);
+  const int q = (int)(r % (N / 4)), nb = (int)(r / (N / 4));
   const int ci = 4 * q + e;
   const int co = n >> 4, ry = (n >> 2) & 3, rx = n & 3;
   const int dy = nb / 3 - 1, dx = nb % 3 - 1;
   const int kh = ry + 4 - 4 * dy, kw = rx + 4 - 4 * dx;
   float v = 0.f;
   if (kh >= 0 && kh < 9 && kw >= 0 && kw < 9) v = w[(((long)ci * 3 + co) * 9 + kh) * 9 + kw];
-  out[i] = v;
+  return v;
 }
 
 // models/GDN.py:73-79 reparametrisation; gamma packed [C/4][C][4] (packed[q][i][e] = γ[i][4q+e]).
-__global__ void pack_gdn_kernel(const float* __restrict__ beta, const float* __restrict__ gamma,
-                                float* __restrict__ beta_eff, float* __restrict__ gp,
-                                float* __restrict__ gpt, int C, float bbound, float gbound,
-                                float ped) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void pk_gdn(const float* __restrict__ beta, const float* __restrict__ gamma,
+                                       float* __restrict__ beta_eff, float* __restrict__ gp,
+                                       float* __restrict__ gpt, int C, float bbound, float gbound,
+                                       float ped, int i) {
   if (i < C) {
     const float m = fmaxf(beta[i], bbound);
     beta_eff[i] = m * m - ped;
@@ -111,6 +99,39 @@ __global__ void pack_gdn_kernel(const float* __restrict__ beta, const float* __r
   }
 }
 
+__global__ void pack_conv1_kernel(const float* __restrict__ w, float* __restrict__ out, int N) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < 256 * N) out[i] = pk_conv1(w, N, i);
+}
+
+__global__ void pack_conv1_x6_kernel(const float* __restrict__ w, float* __restrict__ out, int N) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < 256 * N) out[i] = pk_conv1_x6(w, N, i);
+}
+
+__global__ void pack_conv5_kernel(const float* __restrict__ w, float* __restrict__ out, int N) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < 25L * N * N) out[i] = pk_conv5(w, N, i);
+}
+
+__global__ void pack_deconv5_kernel(const float* __restrict__ w, float* __restrict__ out, int N,
+                                    TapList tl) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < 25L * N * N) out[i] = pk_deconv5(w, N, tl, i);
+}
+
+__global__ void pack_deconv9_kernel(const float* __restrict__ w, float* __restrict__ out, int N) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < 9L * N * 48) out[i] = pk_deconv9(w, N, i);
+}
+
+__global__ void pack_gdn_kernel(const float* __restrict__ beta, const float* __restrict__ gamma,
+                                float* __restrict__ beta_eff, float* __restrict__ gp,
+                                float* __restrict__ gpt, int C, float bbound, float gbound,
+                                float ped) {
+  pk_gdn(beta, gamma, beta_eff, gp, gpt, C, bbound, gbound, ped, blockIdx.x * blockDim.x + threadIdx.x);
+}
+
 struct RatePtrs {
   const float* p[11];  // h1 b1 a1 h2 b2 a2 h3 b3 a3 h4 b4
 };
@@ -120,9 +141,7 @@ __device__ __forceinline__ float softplus_ref(float x) {
   return x > 20.f ? x : log1pf(expf(x));
 }
 
-__global__ void pack_rate_kernel(RatePtrs rp, float* __restrict__ out, int C) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+__device__ __forceinline__ void pk_rate(const RatePtrs& rp, float* __restrict__ out, int C, int c) {
   for (int k = 0; k < 3; ++k) {
     out[(3 * k + 0) * C + c] = softplus_ref(rp.p[3 * k + 0][c]);
     out[(3 * k + 1) * C + c] = rp.p[3 * k + 1][c];
@@ -130,6 +149,58 @@ __global__ void pack_rate_kernel(RatePtrs rp, float* __restrict__ out, int C) {
   }
   out[9 * C + c] = softplus_ref(rp.p[9][c]);
   out[10 * C + c] = rp.p[10][c];
+}
+
+__global__ void pack_rate_kernel(RatePtrs rp, float* __restrict__ out, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < C) pk_rate(rp, out, C, c);
+}
+
+// A batch of packing jobs in one launch (iclr17_pack_batch): job j owns the global thread range
+// [begin[j], begin[j+1]) (block-aligned, so a workgroup serves one job); thread i of a job
+// computes element i of its layout — or, for a split job, one 8-element group of
+// iclr17_split_packed.
+constexpr int PACK_MAXJ = 20;
+struct PackJob {
+  int kind, N, taps, K;
+  const float* src0;
+  const float* src1;
+  void* dst0;
+  void* dst1;
+  void* dst2;
+  float f0, f1, f2;
+  long count;
+};
+struct PackBatch {
+  int n;
+  long begin[PACK_MAXJ + 1];
+  PackJob job[PACK_MAXJ];
+  TapList tl;
+  RatePtrs rp;
+};
+
+__global__ void __launch_bounds__(256) pack_batch_kernel(const PackBatch b) {
+  const long gi = (long)blockIdx.x * 256 + threadIdx.x;
+  int j = 0;
+  while (j + 1 < b.n && gi >= b.begin[j + 1]) ++j;
+  const PackJob& J = b.job[j];
+  const long i = gi - b.begin[j];
+  if (i >= J.count) return;
+  float* out = (float*)J.dst0;
+  switch (J.kind) {
+    case ICLR17_W_CONV1: out[i] = pk_conv1(J.src0, J.N, i); break;
+    case ICLR17_W_CONV1_X6: out[i] = pk_conv1_x6(J.src0, J.N, i); break;
+    case ICLR17_W_CONV5: out[i] = pk_conv5(J.src0, J.N, i); break;
+    case ICLR17_W_DECONV5: out[i] = pk_deconv5(J.src0, J.N, b.tl, i); break;
+    case ICLR17_W_DECONV9: out[i] = pk_deconv9(J.src0, J.N, i); break;
+    case ICLR17_PACK_GDN:
+      pk_gdn(J.src0, J.src1, out, (float*)J.dst1, (float*)J.dst2, J.N, J.f0, J.f1, J.f2, (int)i);
+      break;
+    case ICLR17_PACK_RATE: pk_rate(b.rp, out, J.N, (int)i); break;
+    case ICLR17_PACK_SPLIT:
+      split_packed_group(J.src0, J.K, J.N, J.count * 8, (unsigned short*)J.dst0, i);
+      break;
+  }
 }
 
 __global__ void bit_estimator_kernel(const float* __restrict__ x, int64_t n, int C, int64_t inner,
@@ -389,6 +460,17 @@ size_t iclr17_packed_weight_size(int which, int N) {
   }
 }
 
+static int deconv5_taps(TapList* tl) {
+  int n = 0;
+  for (int ry = 0; ry < 2; ++ry)
+    for (int rx = 0; rx < 2; ++rx) {
+      int c = 0;
+      deconv_phase_taps(5, 2, 2, ry, rx, tl->kh + n, tl->kw + n, &c);
+      n += c;
+    }
+  return n;
+}
+
 int iclr17_pack_weight(int which, const float* w, float* packed, int N, void* stream) {
   ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "pack_weight: N=%d unsupported", N);
   ICLR17_REQUIRE(w && packed, ICLR17_EINVAL, "pack_weight: null pointer");
@@ -402,13 +484,7 @@ int iclr17_pack_weight(int which, const float* w, float* packed, int N, void* st
     case ICLR17_W_CONV5: hipLaunchKernelGGL(pack_conv5_kernel, grid, dim3(256), 0, st, w, packed, N); break;
     case ICLR17_W_DECONV5: {
       TapList tl;
-      int n = 0;
-      for (int ry = 0; ry < 2; ++ry)
-        for (int rx = 0; rx < 2; ++rx) {
-          int c = 0;
-          deconv_phase_taps(5, 2, 2, ry, rx, tl.kh + n, tl.kw + n, &c);
-          n += c;
-        }
+      const int n = deconv5_taps(&tl);
       ICLR17_REQUIRE(n == 25, ICLR17_EINVAL, "pack_weight: deconv tap count %d", n);
       hipLaunchKernelGGL(pack_deconv5_kernel, grid, dim3(256), 0, st, w, packed, N, tl);
       break;
@@ -416,6 +492,90 @@ int iclr17_pack_weight(int which, const float* w, float* packed, int N, void* st
     case ICLR17_W_DECONV9: hipLaunchKernelGGL(pack_deconv9_kernel, grid, dim3(256), 0, st, w, packed, N); break;
   }
   return check_launch("pack_weight");
+}
+
+// The packs of a parameter update in two launches: every non-split job, then the splits (which
+// may read packs made by the first). Jobs are checked like the single-pack entry points.
+int iclr17_pack_batch(const iclr17_pack_job* jobs, int n, const float* const* rate_params,
+                      void* stream) {
+  ICLR17_REQUIRE(jobs && n >= 0, ICLR17_EINVAL, "pack_batch: bad arguments");
+  hipStream_t st = S(stream);
+  PackBatch b;
+  memset(&b, 0, sizeof(b));
+  ICLR17_REQUIRE(deconv5_taps(&b.tl) == 25, ICLR17_EINVAL, "pack_batch: deconv tap count");
+  if (rate_params)
+    for (int k = 0; k < 11; ++k) {
+      ICLR17_REQUIRE(rate_params[k], ICLR17_EINVAL, "pack_batch: null rate parameter %d", k);
+      b.rp.p[k] = rate_params[k];
+    }
+  int rate_jobs = 0;
+  for (int phase = 0; phase < 2; ++phase) {
+    b.n = 0;
+    long total = 0;
+    auto flush = [&]() -> int {
+      if (b.n == 0) return 0;
+      b.begin[b.n] = total;
+      hipLaunchKernelGGL(pack_batch_kernel, dim3((unsigned)(total / 256)), dim3(256), 0, st, b);
+      b.n = 0;
+      total = 0;
+      return check_launch("pack_batch");
+    };
+    for (int j = 0; j < n; ++j) {
+      const iclr17_pack_job& q = jobs[j];
+      if ((q.kind == ICLR17_PACK_SPLIT) != (phase == 1)) continue;
+      PackJob J;
+      memset(&J, 0, sizeof(J));
+      J.kind = q.kind;
+      J.N = q.N;
+      J.taps = q.taps;
+      J.K = q.K;
+      J.src0 = q.src0;
+      J.src1 = q.src1;
+      J.dst0 = q.dst0;
+      J.dst1 = q.dst1;
+      J.dst2 = q.dst2;
+      J.f0 = q.f0;
+      J.f1 = q.f1;
+      J.f2 = q.f2;
+      switch (q.kind) {
+        case ICLR17_W_CONV1: case ICLR17_W_CONV1_X6: case ICLR17_W_CONV5: case ICLR17_W_DECONV5:
+        case ICLR17_W_DECONV9:
+          ICLR17_REQUIRE(q.N == 128 || q.N == 192, ICLR17_EUNSUPPORTED, "pack_batch: N=%d", q.N);
+          ICLR17_REQUIRE(q.src0 && q.dst0, ICLR17_EINVAL, "pack_batch: null weight pointer (job %d)", j);
+          J.count = (long)iclr17_packed_weight_size(q.kind, q.N);
+          break;
+        case ICLR17_PACK_GDN:
+          ICLR17_REQUIRE(q.N > 0 && q.N % 4 == 0, ICLR17_EINVAL, "pack_batch: GDN C=%d", q.N);
+          ICLR17_REQUIRE(q.src0 && q.src1 && q.dst0 && q.dst1, ICLR17_EINVAL,
+                         "pack_batch: null GDN pointer (job %d)", j);
+          J.count = (long)q.N * q.N;
+          break;
+        case ICLR17_PACK_RATE:
+          ICLR17_REQUIRE(rate_params && q.dst0 && q.N > 0 && ++rate_jobs == 1, ICLR17_EINVAL,
+                         "pack_batch: one rate job, with rate_params");
+          J.count = q.N;
+          break;
+        case ICLR17_PACK_SPLIT:
+          ICLR17_REQUIRE(q.src0 && q.dst0 && q.taps > 0 && q.K > 0 && q.K % 8 == 0 && q.N > 0,
+                         ICLR17_EINVAL, "pack_batch: bad split job %d", j);
+          J.count = (long)q.taps * (q.K / 8) * q.N;
+          break;
+        default:
+          ICLR17_REQUIRE(false, ICLR17_EINVAL, "pack_batch: unknown job kind %d", q.kind);
+      }
+      if (b.n == PACK_MAXJ) {
+        const int rc = flush();
+        if (rc) return rc;
+      }
+      b.job[b.n] = J;
+      b.begin[b.n] = total;
+      total += (J.count + 255) / 256 * 256;
+      ++b.n;
+    }
+    const int rc = flush();
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 int iclr17_pack_gdn(const float* beta, const float* gamma, float* beta_eff, float* gamma_packed,

@@ -87,6 +87,23 @@ __device__ __forceinline__ void split8(const f4& x0, const f4& x1, u4& hi, u4& m
   }
 }
 
+// Group g (8 consecutive k of one column) of a packed operand [taps][K/4][N][4] fp32 → planes
+// [3][taps][K/8][N][8] (plane = taps·K·N uint16): iclr17_split_packed.
+__device__ __forceinline__ void split_packed_group(const float* __restrict__ w, int K, int N,
+                                                   long plane, unsigned short* __restrict__ planes,
+                                                   long g) {
+  const long tk = g / N;
+  const int col = (int)(g - tk * N);
+  const long tap = tk / (K / 8);
+  const int k8 = (int)(tk - tap * (K / 8));
+  const float* src = w + ((tap * (K / 4) + 2 * k8) * N + col) * 4;
+  u4 hi, mi, lo;
+  split8(*(const f4*)src, *(const f4*)(src + (long)N * 4), hi, mi, lo);
+  *(u4*)(planes + g * 8) = hi;
+  *(u4*)(planes + plane + g * 8) = mi;
+  *(u4*)(planes + 2 * plane + g * 8) = lo;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);

@@ -2301,19 +2301,8 @@ __global__ void __launch_bounds__(256) split_packed_kernel(const float* __restri
                                                            int K, int N,
                                                            unsigned short* __restrict__ planes) {
   const long n = (long)taps * (K / 8) * N;   // 8-element groups
-  const long plane = n * 8;
-  for (long g = (long)blockIdx.x * 256 + threadIdx.x; g < n; g += (long)gridDim.x * 256) {
-    const long tk = g / N;
-    const int col = (int)(g - tk * N);
-    const long tap = tk / (K / 8);
-    const int k8 = (int)(tk - tap * (K / 8));
-    const float* src = w + ((tap * (K / 4) + 2 * k8) * N + col) * 4;
-    u4 hi, mi, lo;
-    split8(*(const f4*)src, *(const f4*)(src + (long)N * 4), hi, mi, lo);
-    *(u4*)(planes + g * 8) = hi;
-    *(u4*)(planes + plane + g * 8) = mi;
-    *(u4*)(planes + 2 * plane + g * 8) = lo;
-  }
+  for (long g = (long)blockIdx.x * 256 + threadIdx.x; g < n; g += (long)gridDim.x * 256)
+    split_packed_group(w, K, N, n * 8, planes, g);
 }
 
 }  // namespace iclr17

@@ -10,6 +10,7 @@ are packed into kernel layouts by the ``pack_*`` helpers (derived caches).
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 from typing import Optional, Sequence, Tuple
@@ -61,11 +62,56 @@ def _check_channels(N: int) -> None:
 
 
 # ------------------------------------------------------------------------------ packing
+class _PackJob(ctypes.Structure):
+    """iclr17_pack_job (include/iclr17.h)."""
+    _fields_ = [("kind", ctypes.c_int), ("N", ctypes.c_int), ("taps", ctypes.c_int),
+                ("K", ctypes.c_int), ("src0", ctypes.c_void_p), ("src1", ctypes.c_void_p),
+                ("dst0", ctypes.c_void_p), ("dst1", ctypes.c_void_p), ("dst2", ctypes.c_void_p),
+                ("f0", ctypes.c_float), ("f1", ctypes.c_float), ("f2", ctypes.c_float)]
+
+
+_deferred: Optional[list] = None   # queued pack jobs inside batched_packs()
+
+
+def _ptr(t: Optional[Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+@contextlib.contextmanager
+def batched_packs():
+    """Inside the block, pack_weight / pack_gdn / pack_rate / split_packed allocate their
+    outputs and queue the work; on exit it runs as one iclr17_pack_batch (two launches instead of
+    one per pack). Nothing may read the outputs inside the block. Re-entrant (inner blocks join
+    the outer batch)."""
+    global _deferred
+    if _deferred is not None:
+        yield
+        return
+    _deferred = []
+    try:
+        yield
+        jobs = _deferred
+    finally:
+        _deferred = None
+    if not jobs:
+        return
+    arr = (_PackJob * len(jobs))(*[j[0] for j in jobs])
+    rate = [j[2] for j in jobs if j[2] is not None]
+    rate_arr = (ctypes.c_void_p * 11)(*rate[0]) if rate else None
+    call("iclr17_pack_batch", ctypes.cast(arr, ctypes.c_void_p), len(jobs),
+         None if rate_arr is None else ctypes.cast(rate_arr, ctypes.c_void_p), jobs[0][3])
+    del jobs   # sources stay alive until here; the stream orders their reuse after the launch
+
+
 def pack_weight(which: int, w: Tensor, N: int) -> Tensor:
     _check(w, "weight", 4)
     w = w.detach().contiguous()
     size = query("iclr17_packed_weight_size", which, N)
     out = torch.empty(size, device=w.device, dtype=torch.float32)
+    if _deferred is not None:
+        _deferred.append((_PackJob(which, N, 0, 0, _ptr(w), None, _ptr(out), None, None),
+                          (w, out), None, _stream(w)))
+        return out
     call("iclr17_pack_weight", which, _p(w), _p(out), N, _stream(w))
     return out
 
@@ -84,6 +130,11 @@ def pack_gdn(beta: Tensor, gamma: Tensor, beta_bound: float = DEFAULT_BETA_BOUND
     beta_eff = torch.empty(C, device=beta.device, dtype=torch.float32)
     gp = torch.empty(C * C, device=beta.device, dtype=torch.float32)
     gpt = torch.empty(C * C, device=beta.device, dtype=torch.float32) if transposed else None
+    if _deferred is not None:
+        _deferred.append((_PackJob(_lib.ICLR17_PACK_GDN, C, 0, 0, _ptr(beta), _ptr(gamma),
+                                   _ptr(beta_eff), _ptr(gp), _ptr(gpt), beta_bound, gamma_bound,
+                                   pedestal), (beta, gamma, beta_eff, gp, gpt), None, _stream(beta)))
+        return (beta_eff, gp, gpt) if transposed else (beta_eff, gp)
     call("iclr17_pack_gdn", _p(beta), _p(gamma), _p(beta_eff), _p(gp), _p(gpt), C,
          ctypes.c_float(beta_bound), ctypes.c_float(gamma_bound), ctypes.c_float(pedestal),
          _stream(beta))
@@ -99,6 +150,12 @@ def pack_rate(params: Sequence[Tensor]) -> Tensor:
         _check(p, f"rate param {i}")
     C = ps[0].numel()
     out = torch.empty(11 * C, device=ps[0].device, dtype=torch.float32)
+    if _deferred is not None:
+        if any(j[2] is not None for j in _deferred):
+            raise Iclr17Error("iclr17: one rate pack per batched_packs() block")
+        _deferred.append((_PackJob(_lib.ICLR17_PACK_RATE, C, 0, 0, None, None, _ptr(out), None, None),
+                          (ps, out), [p.data_ptr() for p in ps], _stream(ps[0])))
+        return out
     call("iclr17_pack_rate", *[_p(p) for p in ps], _p(out), C, _stream(ps[0]))
     return out
 
@@ -238,6 +295,10 @@ def split_packed(packed: Tensor, taps: int, K: int, N: int) -> Tensor:
     if packed.numel() != taps * K * N:
         raise Iclr17Error(f"iclr17: split_packed: {packed.numel()} != {taps}*{K}*{N}")
     out = torch.empty(3, taps * K * N, device=packed.device, dtype=torch.int16)
+    if _deferred is not None:
+        _deferred.append((_PackJob(_lib.ICLR17_PACK_SPLIT, N, taps, K, _ptr(packed), None,
+                                   _ptr(out), None, None), (packed, out), None, _stream(packed)))
+        return out
     call("iclr17_split_packed", _p(packed), taps, K, N, _p(out), _stream(packed))
     return out
 

@@ -122,6 +122,7 @@ class ImageCompressor(nn.Module):
             raise kernels.Iclr17Error("iclr17: gradients w.r.t. the input image are not implemented")
         if noise is None:
             noise = self._latent_noise(x)
+        self._warm_packs(backward=True)   # one batched pack per parameter update
         return CodecTrainFn.apply(x.contiguous(), noise.contiguous(), self, *params)
 
     def forward_train(self, input_image, noise: Optional[torch.Tensor] = None):
@@ -201,16 +202,28 @@ class ImageCompressor(nn.Module):
             res["ms_ssim_db"] = -10 * (torch.log(1 - ms) / math.log(10))
         return res
 
-    def _warm_packs(self) -> None:
-        """Build (or refresh) every derived parameter layout ``run`` reads in eval mode, on the
-        current stream."""
-        self.Encoder.packed()
-        self.Decoder.packed()
-        self.bitEstimator.packed()
-        if kernels.precision() == "x6":
-            self.Encoder.packed_conv1_x6()
-            for g in (self.Encoder.gdn1, self.Encoder.gdn2, self.Decoder.igdn1, self.Decoder.igdn2):
-                g.effective_params_x6()
+    def _warm_packs(self, backward: bool = False) -> None:
+        """Build (or refresh) every derived parameter layout ``run`` reads (with ``backward``
+        also those of the training backward) on the current stream, the stale ones as one
+        batched packing launch pair (kernels.batched_packs)."""
+        x6 = kernels.precision() == "x6"
+        gdns = (self.Encoder.gdn1, self.Encoder.gdn2, self.Decoder.igdn1, self.Decoder.igdn2)
+        with kernels.batched_packs():
+            self.Encoder.packed()
+            self.Decoder.packed()
+            self.bitEstimator.packed()
+            if x6:
+                self.Encoder.packed_conv1_x6()
+                for g in gdns:
+                    g.effective_params_x6()
+            if backward:
+                self.Encoder.packed_bwd()
+                self.Decoder.packed_bwd(x6)
+                for g in gdns:
+                    if x6:
+                        g.effective_params_bwd_x6()
+                    else:
+                        g.effective_params_bwd()
 
     def evaluate_many(self, batches, want_y: bool = False,
                       want_msssim: bool = False):

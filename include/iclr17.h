@@ -77,6 +77,30 @@ int iclr17_pack_rate(const float* h1, const float* b1, const float* a1, const fl
                      const float* a3, const float* h4, const float* b4, float* packed, int C,
                      void* stream);
 
+/* A batch of packs in two launches (all non-split jobs, then the splits, which may read packs
+ * made by the first launch): the derived layouts of a training step's parameter update without
+ * ~25 separate small launches. kind: an ICLR17_W_* weight layout (src0 = w, dst0 = packed, N),
+ * ICLR17_PACK_GDN (src0 = beta, src1 = gamma, dst0/1/2 = beta_eff, gamma_packed,
+ * gamma_packed_t (nullable), N = C, f0/f1/f2 = beta_bound, gamma_bound, pedestal: as
+ * iclr17_pack_gdn), ICLR17_PACK_RATE (dst0 = packed, N = C; the 11 parameters in rate_params,
+ * as iclr17_pack_rate; at most one rate job per call) or ICLR17_PACK_SPLIT (src0 = packed,
+ * dst0 = planes (uint16), taps, K, N: as iclr17_split_packed). Results are bitwise those of
+ * the single-pack entry points. */
+#define ICLR17_PACK_GDN 16
+#define ICLR17_PACK_RATE 17
+#define ICLR17_PACK_SPLIT 18
+typedef struct iclr17_pack_job {
+  int kind, N, taps, K;
+  const float* src0;
+  const float* src1;
+  void* dst0;
+  void* dst1;
+  void* dst2;
+  float f0, f1, f2;
+} iclr17_pack_job;
+int iclr17_pack_batch(const iclr17_pack_job* jobs, int n, const float* const* rate_params,
+                      void* stream);
+
 /* ------------------------------------------------------------------ fused codec layers
  * Shapes: B images, input image H×W (multiples of 16), N channels.
  * pre_out (nullable) receives the layer's pre-GDN / pre-IGDN activation (needed only by

@@ -449,3 +449,33 @@ def test_c5_2048_full_size_properties(device):
         assert torch.equal(ev6b[k][0], ev6[k][0]), k
     assert torch.equal(dec["y_hat"].cpu(), ev6["y_hat"].cpu())
     assert torch.equal(dec["x_hat"].cpu(), ev6["clipped"].cpu())
+
+
+def test_batched_packs_match_single(device):
+    """kernels.batched_packs (iclr17_pack_batch: every layout of a parameter update in two
+    launches, more than one launch's worth of jobs) gives bitwise the single-pack results."""
+    net = net_for(192, 1, device)
+    enc, dec, be = net.Encoder, net.Decoder, net.bitEstimator
+    g = enc.gdn1
+
+    def all_packs():
+        out = []
+        for _ in range(4):   # 22 first-phase jobs: more than one launch of the batch kernel
+            out += [kernels.pack_weight(_lib.ICLR17_W_CONV1, enc.conv1.weight, 192),
+                    kernels.pack_weight(_lib.ICLR17_W_CONV5, enc.conv2.weight, 192),
+                    kernels.pack_weight(_lib.ICLR17_W_DECONV5, dec.deconv1.weight, 192),
+                    kernels.pack_weight(_lib.ICLR17_W_DECONV9, dec.deconv3.weight, 192),
+                    kernels.pack_conv1_x6(enc.conv1.weight, 192)]
+        bb, gb, ped = g.bounds_f32()
+        be_, gp, gpt = kernels.pack_gdn(g.beta, g.gamma, bb, gb, ped, transposed=True)
+        out += [be_, gp, gpt, kernels.split_packed(gp, 1, 192, 192), kernels.split_packed(gpt, 1, 192, 192),
+                kernels.pack_rate(be.params_in_order())]
+        return out
+
+    single = all_packs()
+    with kernels.batched_packs():
+        batched = all_packs()
+    torch.cuda.synchronize()
+    assert len(single) == len(batched)
+    for a, b in zip(single, batched):
+        assert torch.equal(a, b)

@@ -188,8 +188,8 @@ def run_train(args, net, x, world, dev):
         "data": "synthetic (splitmix64 uint8/255 images, seeded trained-like weights)",
         "config": {"workload": f"train step, {B} x {S}x{S}x3 crops per GPU, N={args.N}, lambda=0.01",
                    "N": args.N, "batch_per_gpu": B, "global_batch": B * world,
-                   "precision": ("x6: forward, input gradients and k5 weight gradients; exact-f32 "
-                                 "conv1/deconv3 weight gradients and GDN parameter gradients"
+                   "precision": ("x6: forward, input gradients, weight gradients and GDN γ "
+                                 "gradients (bias/β/rate-parameter sums and Adam in fp32)"
                                  if kernels.precision() == "x6" else "exact-f32"),
                    "parallelism": f"dp{world} (RCCL bucketed grad all-reduce)"},
         "roofline": {"bound": "mfma", "kernel": "whole training step", "achieved": round(tflops, 2),

@@ -48,6 +48,9 @@ constexpr int BM = 64;        // output pixels per tile
 #ifndef ICLR17_CONV3_BN
 #define ICLR17_CONV3_BN 96    // conv3 (+ quantiser) output columns per workgroup
 #endif
+#ifndef ICLR17_W3SPLIT
+#define ICLR17_W3SPLIT 1      // conv3 x6 honours caller-provided pre-split weights (0: ignore)
+#endif
 #ifndef ICLR17_QSTAGES
 #define ICLR17_QSTAGES 2      // conv3's DMA ring depth (3, 4 measured slower: DESIGN.md §5)
 #endif
@@ -129,6 +132,7 @@ struct EngineArgs {
   long out_plane;
   const unsigned short* ggamma6;    // x6: γ_eff split, [3][CO/8][CO][8] bf16 (plane CO·CO)
   const unsigned short* ggammaT6;   // x6 backward: the transposed packing of γ_eff, split
+  const unsigned short* w6;         // x6 conv3: weights pre-split, [3][25][CI/8][CO][8] bf16
 };
 
 struct TileInfo {
@@ -922,7 +926,8 @@ __device__ __forceinline__ void out3_epilogue(f4 (&acc)[MT][NT], float* smem, co
 // columns in VALU. One 32-deep step = per 16×16 tile six v_mfma_f32_16x16x32_bf16:
 // lo·hi + hi·lo + mid·mid + mid·hi + hi·mid + hi·hi (the dropped mid·lo, lo·mid, lo·lo terms are
 // below 2^-24 of the product), accumulated in fp32.
-template <int CI, int CO, int BN, int WM, int WN, int EPI, bool PL, bool X6, int BMT = BM>
+template <int CI, int CO, int BN, int WM, int WN, int EPI, bool PL, bool X6, int BMT = BM,
+          bool BS = false>
 __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   constexpr int NWV = WM * WN;                   // waves (4, or 8 for the 128-row tiles)
   constexpr int MT = BMT / WM / 16;
@@ -930,7 +935,10 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   constexpr int KCH = 32;                        // input channels per k-step
   constexpr int NCH = CI / KCH;
   constexpr int SA = X6 ? 3 * BMT * KCH / 2 : BMT * KCH;   // A image floats per stage
-  constexpr int SB = KCH * BN;                   // B image floats per stage
+  // B image floats per stage: fp32 [8 quads][BN][4], or (BS: weights pre-split, x6) the three
+  // bf16 planes [3][4 k-groups][BN][8] — 1.5× the bytes, no split VALU in the loop
+  constexpr int SB = BS ? 3 * KCH * BN / 2 : KCH * BN;
+  static_assert(!BS || (X6 && EPI == EPI_QUANT), "pre-split B: the x6 conv3 kernel");
   constexpr int STAGE = SA + SB;
   constexpr int NAI = SA * 4 / 1024;             // A glds wave-instructions per step (8 | 12)
   constexpr int NBI = SB * 4 / 1024;             // B glds wave-instructions per step
@@ -995,8 +1003,15 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
 #pragma unroll
   for (int j = 0; j < BI_W; ++j) {
     const int i = wave + NWV * j;
-    const int o = i * 256 + lane * 4;   // offset in the LDS image [8 quads][BN][4]
-    bsrc[j] = (BN == CO) ? o : ((o / (BN * 4)) * CO + t.nb * BN) * 4 + o % (BN * 4);
+    if constexpr (BS) {   // u16 offset: LDS image [3][4][BN][8] ← planes [3][25][CI/8][CO][8]
+      const int o = i * 512 + lane * 8;
+      const int pl = o / (4 * BN * 8), r = o - pl * (4 * BN * 8);
+      const int k8 = r / (BN * 8), co8 = r - k8 * (BN * 8);
+      bsrc[j] = pl * (25 * CI * CO) + (k8 * CO + t.nb * BN) * 8 + co8;
+    } else {
+      const int o = i * 256 + lane * 4;   // offset in the LDS image [8 quads][BN][4]
+      bsrc[j] = (BN == CO) ? o : ((o / (BN * 4)) * CO + t.nb * BN) * 4 + o % (BN * 4);
+    }
   }
 
   int t0 = 0, ntaps = 1;
@@ -1032,13 +1047,22 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
         glds16(ok ? inb + pbase[j] + so : g_zero16, sa + i * 256);
       }
     }
-    const float* __restrict__ ws = a.w + ((long)tap * CI + cc * KCH) * CO;   // uniform base
     float* sb = sa + SA;
+    if constexpr (BS) {
+      const unsigned short* __restrict__ ws6 = a.w6 + ((long)tap * (CI / 8) + cc * 4) * CO * 8;
 #pragma unroll
-    for (int j = 0; j < BI_W; ++j) {
-      const int i = wave + NWV * j;
-      if (skip_b) break;
-      if (NBI % NWV == 0 || i < NBI) glds16(ws + bsrc[j], sb + i * 256);
+      for (int j = 0; j < BI_W; ++j) {
+        const int i = wave + NWV * j;
+        if (NBI % NWV == 0 || i < NBI) glds16((const float*)(ws6 + bsrc[j]), sb + i * 256);
+      }
+    } else {
+      const float* __restrict__ ws = a.w + ((long)tap * CI + cc * KCH) * CO;   // uniform base
+#pragma unroll
+      for (int j = 0; j < BI_W; ++j) {
+        const int i = wave + NWV * j;
+        if (skip_b) break;
+        if (NBI % NWV == 0 || i < NBI) glds16(ws + bsrc[j], sb + i * 256);
+      }
     }
   };
 
@@ -1070,7 +1094,13 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       u4 bh, bm, bl;
-      if (ICLR17_ABL & 256) {
+      if constexpr (BS) {   // the fragments as stored: k-group lane >> 4, column of lane & 15
+        const unsigned short* b6 = (const unsigned short*)(smem + buf * STAGE + SA) +
+                                   ((lane >> 4) * BN + wn * (BN / WN) + nt * 16 + (lane & 15)) * 8;
+        bh = *(const u4*)b6;
+        bm = *(const u4*)(b6 + 4 * BN * 8);
+        bl = *(const u4*)(b6 + 8 * BN * 8);
+      } else if (ICLR17_ABL & 256) {
         const f4 x0 = *(const f4*)(sb + nt * 64), x1 = *(const f4*)(sb + BN * 4 + nt * 64);
         bh = u4{__builtin_amdgcn_perm(__float_as_uint(x0[1]), __float_as_uint(x0[0]), 0x07060302u),
                 __builtin_amdgcn_perm(__float_as_uint(x0[3]), __float_as_uint(x0[2]), 0x07060302u),
@@ -1208,9 +1238,10 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   }  // phase loop
 }
 
-template <int CI, int CO, int BN, int WM, int WN, int EPI, bool PL = false, bool X6 = false>
+template <int CI, int CO, int BN, int WM, int WN, int EPI, bool PL = false, bool X6 = false,
+          bool BS = false>
 __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
-  engine_body<CI, CO, BN, WM, WN, EPI, PL, X6>(a);
+  engine_body<CI, CO, BN, WM, WN, EPI, PL, X6, BM, BS>(a);
 }
 
 // 128-pixel tiles (16×8 base pixels) on 8 waves (2 × 4), one workgroup per CU at two waves per
@@ -2103,6 +2134,7 @@ struct SplitIO {
   long out_plane = 0;
   const unsigned short* gamma6 = nullptr;   // x6: split γ_eff for the GDN contraction
   const unsigned short* gammaT6 = nullptr;  // x6 backward: split transposed γ_eff
+  const unsigned short* w6 = nullptr;       // x6 conv3: pre-split weights
 };
 
 static void apply_split(EngineArgs& a, const SplitIO* x6) {
@@ -2111,6 +2143,7 @@ static void apply_split(EngineArgs& a, const SplitIO* x6) {
   a.out_split = x6->out; a.out_plane = x6->out_plane;
   a.ggamma6 = x6->gamma6;
   a.ggammaT6 = x6->gammaT6;
+  a.w6 = x6->w6;
 }
 
 template <int N, int EPI = EPI_GDN>
@@ -2167,7 +2200,10 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
     constexpr int WN = (BN / 16) % 4 == 0 ? 4 : 2, WM = 4 / WN;
     a.partials_per_image = a.tiles_x * a.tiles_y * (N / BN);
     dim3 grid(a.tiles_x * a.tiles_y * B, N / BN);
-    if (X6in)
+    if (X6in && a.w6 != nullptr && ICLR17_W3SPLIT)
+      hipLaunchKernelGGL((engine_kernel<N, N, BN, WM, WN, EPI_QUANT, false, true, true>), grid,
+                         dim3(256), 0, st, a);
+    else if (X6in)
       hipLaunchKernelGGL((engine_kernel<N, N, BN, WM, WN, EPI_QUANT, false, true>), grid,
                          dim3(256), 0, st, a);
     else
@@ -2531,14 +2567,15 @@ int iclr17_analysis_conv2_gdn_x6(const uint16_t* in_split, int B, int H, int W, 
 }
 
 int iclr17_analysis_conv3_quant_rate_x6(const uint16_t* in_split, int B, int H, int W, int N,
-                                        const float* w_packed, int quant_mode, const float* noise,
+                                        const float* w_packed, const uint16_t* w_split,
+                                        int quant_mode, const float* noise,
                                         const float* rate_packed, float* y_out, float* y_hat,
                                         uint16_t* y_hat_split, double* bits_partial,
                                         void* stream) {
   int rc = check_dims(B, H, W, N);
   if (rc) return rc;
-  ICLR17_REQUIRE(in_split && w_packed && rate_packed && y_hat && bits_partial, ICLR17_EINVAL,
-                 "conv3_quant_rate_x6: null pointer");
+  ICLR17_REQUIRE(in_split && (w_packed || w_split) && rate_packed && y_hat && bits_partial,
+                 ICLR17_EINVAL, "conv3_quant_rate_x6: null pointer");
   ICLR17_REQUIRE(quant_mode == ICLR17_QUANT_ROUND || (quant_mode == ICLR17_QUANT_NOISE && noise),
                  ICLR17_EINVAL, "conv3_quant_rate_x6: bad quant mode %d / missing noise", quant_mode);
   const int h = H / 8, w = W / 8;
@@ -2547,6 +2584,7 @@ int iclr17_analysis_conv3_quant_rate_x6(const uint16_t* in_split, int B, int H, 
   io.in_plane = (long)B * h * w * N;
   io.out = (unsigned short*)y_hat_split;
   io.out_plane = (long)B * (h / 2) * (w / 2) * N;
+  io.w6 = (const unsigned short*)w_split;
   return N == 192 ? launch_conv5<192, EPI_QUANT>(nullptr, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io)
                   : launch_conv5<128, EPI_QUANT>(nullptr, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io);
 }

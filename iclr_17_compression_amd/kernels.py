@@ -372,10 +372,12 @@ def conv2_gdn_x6(hs: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Ten
     return split, out, pre
 
 
-def conv3_quant_rate_x6(hs: Tensor, wp: Tensor, rate_packed: Tensor,
-                        noise: Optional[Tensor] = None, want_y: bool = False):
+def conv3_quant_rate_x6(hs: Tensor, wp: Optional[Tensor], rate_packed: Tensor,
+                        noise: Optional[Tensor] = None, want_y: bool = False,
+                        w_split: Optional[Tensor] = None):
     """conv3_quant_rate on a split-form input. Returns (y_hat, bits_partial, y | None,
-    y_hat_split)."""
+    y_hat_split). ``w_split`` (``split_conv5``) lets the kernel stage pre-split weight planes
+    instead of splitting ``wp`` in the loop (bitwise the same result)."""
     _check_split(hs, "activation")
     _, B, h8, w8, N = hs.shape
     _check_channels(N)
@@ -393,9 +395,19 @@ def conv3_quant_rate_x6(hs: Tensor, wp: Tensor, rate_packed: Tensor,
     y = torch.empty_like(y_hat) if want_y else None
     T = rate_partials_per_image(H, W, N)
     partial = torch.empty(B, T, device=hs.device, dtype=torch.float64)
-    call("iclr17_analysis_conv3_quant_rate_x6", _p(hs), B, H, W, N, _p(wp), mode, _p(noise),
+    if wp is None and w_split is None:
+        raise Iclr17Error("iclr17: conv3_quant_rate_x6 needs wp or w_split")
+    if w_split is not None and (w_split.dtype != torch.int16 or w_split.numel() != 3 * 25 * N * N):
+        raise Iclr17Error(f"iclr17: conv3 w_split must be int16 [3, 25*{N}*{N}] (split_conv5)")
+    call("iclr17_analysis_conv3_quant_rate_x6", _p(hs), B, H, W, N, _p(wp), _p(w_split), mode,
+         _p(noise),
          _p(rate_packed), _p(y), _p(y_hat), _p(y_hat_split), _p(partial), _stream(hs))
     return y_hat, partial, y, y_hat_split
+
+
+def split_conv5(wp: Tensor, N: int) -> Tensor:
+    """The conv5 packing [25][N/4][N][4] → split planes for conv3_quant_rate_x6's w_split."""
+    return split_packed(wp, 25, N, N)
 
 
 def deconv_igdn_x6(hs: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Tensor,

@@ -55,6 +55,13 @@ class Analysis_net_17(nn.Module):
                               lambda: kernels.pack_conv1_x6(self.conv1.weight, N),
                               force)
 
+    def packed_conv3_x6(self, force: bool = False):
+        """conv3's packed weights split for the x6 kernel (kernels.split_conv5), cached."""
+        N = self.out_channel_N
+        return self._pack.get("w3x6", (self.conv3.weight,),
+                              lambda: kernels.split_conv5(self.packed(force)[2], N),
+                              force)
+
     def packed_bwd(self):
         """conv3 / conv2 weights packed as the transposed convolutions of their input gradients
         (the engine's deconv layout), cached until the weights change."""

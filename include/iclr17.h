@@ -177,9 +177,13 @@ int iclr17_analysis_conv2_gdn_x6(const uint16_t* in_split, int B, int H, int W, 
                                  const float* w_packed, const float* bias, const float* beta_eff,
                                  const float* gamma_packed, const uint16_t* gamma_split,
                                  float* out, uint16_t* out_split, float* pre_out, void* stream);
-/* iclr17_analysis_conv3_quant_rate on a split-form input; ŷ also in split form (nullable). */
+/* iclr17_analysis_conv3_quant_rate on a split-form input; ŷ also in split form (nullable).
+ * w_split (nullable: then w_packed, split in the loop) is w_packed split by
+ * iclr17_split_packed(taps = 25, K = N, N = N): the kernel then stages the weight planes as
+ * they are and splits nothing. One of w_packed / w_split must be non-NULL. */
 int iclr17_analysis_conv3_quant_rate_x6(const uint16_t* in_split, int B, int H, int W, int N,
-                                        const float* w_packed, int quant_mode, const float* noise,
+                                        const float* w_packed, const uint16_t* w_split,
+                                        int quant_mode, const float* noise,
                                         const float* rate_packed, float* y_out, float* y_hat,
                                         uint16_t* y_hat_split, double* bits_partial,
                                         void* stream);

@@ -77,6 +77,8 @@ SIGNATURES = {
     "iclr17_rans_decode": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P]),
     "iclr17_ms_ssim_workspace_size": (_SZ, [_I, _I, _I]),
     "iclr17_ms_ssim": (_I, [_P, _P, _I, _I, _I, _F, _P, _SZ, _P, _P]),
+    "iclr17_ssim_workspace_size": (_SZ, [_I, _I, _I]),
+    "iclr17_ssim": (_I, [_P, _P, _I, _I, _I, _F, _P, _SZ, _P, _P, _P]),
     "iclr17_gdn": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "iclr17_gdn_bwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_bitest_bwd_chunks": (_I, [_I64, _I]),

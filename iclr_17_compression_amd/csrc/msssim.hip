@@ -238,9 +238,40 @@ __global__ void __launch_bounds__(256) msssim_finish_kernel(const double* __rest
   }
 }
 
-int level_plan(int H, int W, Level* lv, int B, long* pyr_floats, long* partial_doubles) {
+// Single-scale SSIM (ms_ssim_torch.py:86-120 → _ssim :36-83 with size_average=False, full=True):
+// per image the means of the ssim and cs maps over C·Ho·Wo, the same fixed-order sums as above.
+__global__ void __launch_bounds__(256) ssim_finish_kernel(const double* __restrict__ partial,
+                                                          long tiles3, double count,
+                                                          float* __restrict__ out_ssim,
+                                                          float* __restrict__ out_cs) {
+  __shared__ double red[2][256];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const double* p = partial + 2 * (long)b * tiles3;
+  double a = 0.0, c = 0.0;
+  for (long t = tid; t < tiles3; t += 256) {
+    a += p[2 * t];
+    c += p[2 * t + 1];
+  }
+  red[0][tid] = a;
+  red[1][tid] = c;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) {
+      red[0][tid] += red[0][tid + s];
+      red[1][tid] += red[1][tid + s];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    out_ssim[b] = (float)(red[0][0] / count);
+    if (out_cs) out_cs[b] = (float)(red[1][0] / count);
+  }
+}
+
+int level_plan(int H, int W, Level* lv, int B, long* pyr_floats, long* partial_doubles,
+               int levels = LEVELS) {
   long off = 0, part = 0;
-  for (int l = 0; l < LEVELS; ++l) {
+  for (int l = 0; l < levels; ++l) {
     if (H < WIN || W < WIN) return -1;
     lv[l].H = H;
     lv[l].W = W;
@@ -313,6 +344,36 @@ int iclr17_ms_ssim(const float* x, const float* y, int B, int H, int W, float da
   }
   hipLaunchKernelGGL(msssim_finish_kernel, dim3(B), dim3(256), 0, st, partial, fp, B, means, out);
   return check_launch("ms_ssim");
+}
+
+size_t iclr17_ssim_workspace_size(int B, int H, int W) {
+  Level lv[1];
+  long pyr = 0, part = 0;
+  if (B <= 0 || level_plan(H, W, lv, B, &pyr, &part, 1) != 0) return 0;
+  return (size_t)part * 8 + 256;
+}
+
+int iclr17_ssim(const float* x, const float* y, int B, int H, int W, float data_range,
+                void* workspace, size_t workspace_bytes, float* out_ssim, float* out_cs,
+                void* stream) {
+  ICLR17_REQUIRE(x && y && workspace && out_ssim && B > 0, ICLR17_EINVAL, "ssim: null pointer");
+  ICLR17_REQUIRE(B <= 10000 && H <= 65535 * 2, ICLR17_EINVAL, "ssim: B=%d H=%d exceed the grid", B, H);
+  Level lv[1];
+  long pyr = 0, part = 0;
+  ICLR17_REQUIRE(level_plan(H, W, lv, B, &pyr, &part, 1) == 0, ICLR17_EINVAL,
+                 "ssim: %dx%d is smaller than the 11-tap window", H, W);
+  ICLR17_REQUIRE(workspace_bytes >= iclr17_ssim_workspace_size(B, H, W), ICLR17_EINVAL,
+                 "ssim: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  double* partial = (double*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
+  const float c1 = (0.01f * data_range) * (0.01f * data_range);
+  const float c2 = (0.03f * data_range) * (0.03f * data_range);
+  const int Ho = H - WIN + 1, Wo = W - WIN + 1;
+  dim3 grid((Wo + TOW - 1) / TOW, (Ho + TOH - 1) / TOH, B * 3);
+  hipLaunchKernelGGL(ssim_level_kernel, grid, dim3(256), 0, st, x, y, H, W, c1, c2, partial);
+  hipLaunchKernelGGL(ssim_finish_kernel, dim3(B), dim3(256), 0, st, partial, 3L * lv[0].tiles,
+                     3.0 * Ho * Wo, out_ssim, out_cs);
+  return check_launch("ssim");
 }
 
 }  // extern "C"

@@ -447,6 +447,26 @@ def ms_ssim(x: Tensor, y: Tensor, data_range: float = 1.0) -> Tensor:
     return out
 
 
+def ssim(x: Tensor, y: Tensor, data_range: float = 1.0):
+    """Per-image single-scale SSIM and cs means ([B], [B]) of NCHW fp32 batches
+    (models/ms_ssim_torch.py:36-83 with size_average=False, full=True), on the GPU."""
+    _check(x, "image", 4)
+    _check(y, "image", 4)
+    if x.shape != y.shape or x.shape[1] != 3:
+        raise Iclr17Error(f"iclr17: ssim needs two [B,3,H,W] batches of one shape "
+                          f"(got {tuple(x.shape)} and {tuple(y.shape)})")
+    B, _, H, W = x.shape
+    nbytes = query("iclr17_ssim_workspace_size", B, H, W)
+    if nbytes == 0:
+        raise Iclr17Error(f"iclr17: ssim: {H}x{W} is smaller than the 11-tap window")
+    ws = torch.empty(nbytes, device=x.device, dtype=torch.uint8)
+    s = torch.empty(B, device=x.device, dtype=torch.float32)
+    cs = torch.empty(B, device=x.device, dtype=torch.float32)
+    call("iclr17_ssim", _p(x.contiguous()), _p(y.contiguous()), B, H, W, float(data_range),
+         _p(ws), nbytes, _p(s), _p(cs), _stream(x))
+    return s, cs
+
+
 def output_partials_per_image(H: int, W: int) -> int:
     return query("iclr17_output_partials_per_image", H, W)
 

@@ -241,6 +241,15 @@ size_t iclr17_ms_ssim_workspace_size(int B, int H, int W);
 int iclr17_ms_ssim(const float* x, const float* y, int B, int H, int W, float data_range,
                    void* workspace, size_t workspace_bytes, float* out, void* stream);
 
+/* Single-scale SSIM, models/ms_ssim_torch.py:86-120 (ssim → _ssim :36-83, size_average=False,
+ * full=True): per image the means over C·Ho·Wo of the ssim map (out_ssim [B]) and the cs map
+ * (out_cs [B], may be null) of NCHW [B,3,H,W] fp32 images, 11-tap σ=1.5 window, H, W ≥ 11.
+ * workspace: iclr17_ssim_workspace_size(B,H,W) bytes (0 = shape unsupported). */
+size_t iclr17_ssim_workspace_size(int B, int H, int W);
+int iclr17_ssim(const float* x, const float* y, int B, int H, int W, float data_range,
+                void* workspace, size_t workspace_bytes, float* out_ssim, float* out_cs,
+                void* stream);
+
 /* datasets.py:27-33 training transform on the GPU: per image, PIL-exact bilinear resize of its
  * crop box to S×S (two passes, 8-bit fixed point), horizontal / vertical flips, /255 → out NCHW
  * fp32 [B,3,S,S]. src: uint8 HWC images back to back; desc: int64 [B][16] = {src byte offset, H,

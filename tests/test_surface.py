@@ -64,3 +64,39 @@ def test_checkpoint_roundtrip(tmp_path):
     assert load_model(other, str(tmp_path / "iter_7.pth.tar")) == 0
     for k, v in other.state_dict().items():
         assert torch.equal(v, sd[k])
+
+
+def test_star_imports_give_train_py_names():
+    """train.py:3 does `from model import *` and then uses ImageCompressor, save_model,
+    load_model, np, torch, logging and ms_ssim (train.py:26,117,178) without importing them;
+    `from models import *` yields the reference's models/__init__.py:1-9 names."""
+    ns = {}
+    exec("from iclr_17_compression_amd.model import *", ns)
+    for name in ("ImageCompressor", "save_model", "load_model", "np", "torch", "logging",
+                 "ms_ssim", "ssim", "GDN", "BitEstimator", "Analysis_net_17", "Synthesis_net_17"):
+        assert name in ns, name
+    ns = {}
+    exec("from iclr_17_compression_amd.models import *", ns)
+    for name in ("GDN", "BitEstimator", "Analysis_net_17", "Synthesis_net_17", "ms_ssim", "ssim"):
+        assert name in ns, name
+
+
+def test_ms_ssim_argument_checks_and_no_cpu_fallback():
+    """The reference's ValueError checks (ms_ssim_torch.py:140-150) come first; CPU tensors go to
+    the GPU kernels, so on a host without a GPU the call fails loudly instead of computing on CPU."""
+    from iclr_17_compression_amd._lib import Iclr17Error
+    from iclr_17_compression_amd.models import ms_ssim, ssim
+    x = torch.rand(1, 3, 176, 176)
+    with pytest.raises(ValueError, match="4-d"):
+        ms_ssim(x[0], x[0], data_range=1.0)
+    with pytest.raises(ValueError, match="same dimensions"):
+        ms_ssim(x, x[:, :, :170], data_range=1.0)
+    with pytest.raises(ValueError, match="odd"):
+        ssim(x, x, win_size=10)
+    with pytest.raises(Iclr17Error, match="default window"):
+        ms_ssim(x, x, win_sigma=2.0)
+    with pytest.raises(Iclr17Error, match="weights"):
+        ms_ssim(x, x, weights=[0.5, 0.5])
+    if not torch.cuda.is_available():
+        with pytest.raises(Iclr17Error, match="no CPU implementation"):
+            ms_ssim(x, x, data_range=1.0, size_average=True)

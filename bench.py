@@ -85,9 +85,12 @@ class Step:
         self.enc = net.Encoder.packed()
         self.dec = net.Decoder.packed()
         self.rate = net.bitEstimator.packed()
+        gdns = (net.Encoder.gdn1, net.Encoder.gdn2, net.Decoder.igdn1, net.Decoder.igdn2)
         self.w1x6 = net.Encoder.packed_conv1_x6()
-        self.g6 = [m.effective_params_x6() for m in (net.Encoder.gdn1, net.Encoder.gdn2,
-                                                      net.Decoder.igdn1, net.Decoder.igdn2)]
+        self.g6 = [m.effective_params_x6() for m in gdns]
+        self.ebf = net.Encoder.packed_bf16()
+        self.dbf = net.Decoder.packed_bf16()
+        self.gbf = [m.effective_params_bf16() for m in gdns]
 
     def __call__(self, events=None):
         net, N = self.net, self.N
@@ -95,7 +98,20 @@ class Step:
         d1, d2, d3, q1, q2 = self.dec
         ev = (lambda i: events[i].record()) if events is not None else (lambda i: None)
         ev(0)
-        if kernels.precision() == "x6":
+        if kernels.precision() == "bf16":
+            (w1b, w2b, w3b), (d1b, d2b), (e1, e2, e3, e4) = self.ebf, self.dbf, self.gbf
+            h = kernels.conv1_gdn_bf16(self.x, w1b, net.Encoder.conv1.bias, *e1, N)
+            ev(1)
+            h = kernels.conv2_gdn_bf16(h, w2b, net.Encoder.conv2.bias, *e2)
+            ev(2)
+            y_hat, partial, _, ybf = kernels.conv3_quant_rate_bf16(h, w3b, self.rate)
+            ev(3)
+            h = kernels.deconv_igdn_bf16(ybf, d1b, net.Decoder.deconv1.bias, *e3)
+            ev(4)
+            h = kernels.deconv_igdn_bf16(h, d2b, net.Decoder.deconv2.bias, *e4)
+            ev(5)
+            clipped, _, _ = kernels.deconv3_bf16(h, d3, net.Decoder.deconv3.bias)
+        elif kernels.precision() == "x6":
             e1, e2, e3, e4 = self.g6
             hs, _, _ = kernels.conv1x6_gdn(self.x, self.w1x6, net.Encoder.conv1.bias, e1[0], e1[2],
                                            N)
@@ -452,11 +468,15 @@ def main() -> None:
                   "gbs": round(bytes_[k] * B / (per_layer_ms[k] * 1e-3) / 1e9, 1) if bytes_[k] else None}
               for k in LAYERS}
     total_flops = sum(flops.values()) * B
-    x6 = kernels.precision() == "x6"
-    traffic, traffic_src = pmc_traffic(dominant, N, S, B, kernels.precision())
-    peak = X6_PEAK_TFLOPS if (x6 and dominant in X6_LAYERS) else FP32_MFMA_PEAK_TFLOPS
-    peak_note = ("bf16 dense MFMA peak / 6 (bf16x6: six bf16 part products per fp32 MAC)"
-                 if peak == X6_PEAK_TFLOPS else "fp32 MFMA dense peak (exact-f32 products)")
+    prec = kernels.precision()
+    x6 = prec == "x6"
+    traffic, traffic_src = pmc_traffic(dominant, N, S, B, prec)
+    if prec == "bf16":
+        peak, peak_note = BF16_MFMA_PEAK_TFLOPS, "bf16 dense MFMA peak (one bf16 product per MAC)"
+    elif x6 and dominant in X6_LAYERS:
+        peak, peak_note = X6_PEAK_TFLOPS, "bf16 dense MFMA peak / 6 (bf16x6: six bf16 part products per fp32 MAC)"
+    else:
+        peak, peak_note = FP32_MFMA_PEAK_TFLOPS, "fp32 MFMA dense peak (exact-f32 products)"
     result = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -468,14 +488,16 @@ def main() -> None:
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "bf16" if prec == "bf16" else "f32",
         "data": "synthetic (splitmix64 uint8/255 images, seeded trained-like weights)",
         "config": {"workload": f"eval encode+decode (round quantiser + rate), {B} x {S}x{S}x3 images per GPU, N={N}",
                    "N": N, "image": f"{S}x{S}x3", "batch_per_gpu": B, "global_batch": B * world,
                    "quant": "round",
                    "precision": ("x6: fp32 operands split exactly into 3 bf16 parts, 6 part products "
                                  "on v_mfma_f32_16x16x32_bf16, fp32 accumulate (every contraction)")
-                                if x6 else "fp32 (exact-f32 MFMA products)",
+                                if x6 else ("bf16: bf16 activations and weights, one bf16 product "
+                                            "per MAC, fp32 accumulate and epilogues" if prec == "bf16"
+                                            else "fp32 (exact-f32 MFMA products)"),
                    "parallelism": f"dp{world} (images sharded by rank, no data-path collective)"},
         "roofline": {"bound": "mfma", "kernel": dominant, "achieved": round(achieved, 2),
                      "peak": round(peak, 1), "unit": "TFLOP/s", "peak_basis": peak_note,

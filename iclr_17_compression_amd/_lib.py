@@ -31,6 +31,8 @@ ICLR17_W_CONV1_X6 = 4
 ICLR17_PACK_GDN = 16
 ICLR17_PACK_RATE = 17
 ICLR17_PACK_SPLIT = 18
+ICLR17_BF_CONV5 = 32
+ICLR17_BF_DECONV5 = 33
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -55,14 +57,14 @@ SIGNATURES = {
     "iclr17_rate_partials_per_image": (_I, [_I, _I, _I]),
     "iclr17_synthesis_deconv_igdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_synthesis_deconv3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P]),
-    "iclr17_synthesis_deconv3_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
+    "iclr17_synthesis_deconv3_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P]),
     "iclr17_output_partials_per_image": (_I, [_I, _I]),
     "iclr17_split_planes": (_I, [_P, ctypes.c_long, _P, _P]),
     "iclr17_split_packed": (_I, [_P, _I, _I, _I, _P, _P]),
     "iclr17_analysis_conv1_gdn_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_analysis_conv1x6_gdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_analysis_conv2_gdn_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
-    "iclr17_analysis_conv3_quant_rate_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _P, _P, _P, _P,
+    "iclr17_analysis_conv3_quant_rate_x6": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P,
                                                  _P, _P, _P]),
     "iclr17_synthesis_deconv_igdn_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
                                              _P]),
@@ -110,6 +112,17 @@ SIGNATURES = {
     "iclr17_bias_grad_nhwc": (_I, [_P, ctypes.c_long, _I, _P, _P, _P]),
     "iclr17_bias_grad_nchw": (_I, [_P, _I, _I, ctypes.c_long, _P, _P, _P]),
     "iclr17_rate_param_grad": (_I, [_P, _I, _I] + [_P] * 7 + [_P] * 11 + [_P]),
+    # bf16 throughput mode (csrc/engine_bf16.hip)
+    "iclr17_bf16_weight_size": (_SZ, [_I, _I]),
+    "iclr17_pack_bf16": (_I, [_I, _P, _P, _I, _P]),
+    "iclr17_round_packed": (_I, [_P, _I, _I, _I, _P, _P]),
+    "iclr17_to_bf16": (_I, [_P, ctypes.c_long, _P, _P]),
+    "iclr17_analysis_conv1_gdn_bf16": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
+    "iclr17_analysis_conv2_gdn_bf16": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
+    "iclr17_bf16_rate_partials_per_image": (_I, [_I, _I, _I]),
+    "iclr17_analysis_conv3_quant_rate_bf16": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_synthesis_deconv_igdn_bf16": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
+    "iclr17_synthesis_deconv3_bf16": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P]),
 }
 
 

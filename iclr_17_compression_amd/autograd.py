@@ -126,7 +126,7 @@ def analysis_features_train(enc, x: Tensor):
     kernels also hand conv2 (and conv3) their input in split form; "a2s" is then set."""
     w1, w2, _, g1, g2 = enc.packed()
     N = enc.out_channel_N
-    if kernels.precision() == "x6":
+    if kernels.precision() != "fp32":
         e1, e2 = enc.gdn1.effective_params_x6(), enc.gdn2.effective_params_x6()
         a1s, a1, u1 = kernels.conv1x6_gdn(x, enc.packed_conv1_x6(), enc.conv1.bias, e1[0], e1[2],
                                           N, want_f32=True, want_pre=True)
@@ -145,10 +145,10 @@ def analysis_backward(enc, saved: Dict[str, Tensor], g_y: Tensor,
     bb1, gb1, _ = enc.gdn1.bounds_f32()
     bb2, gb2, _ = enc.gdn2.bounds_f32()
     w3t, w2t = enc.packed_bwd()
-    x6 = kernels.precision() == "x6"
+    x6 = kernels.precision() != "fp32"
     p2 = None if x6 else enc.gdn2.effective_params_bwd()
     p1 = None if x6 else enc.gdn1.effective_params_bwd()
-    if kernels.precision() == "x6":
+    if kernels.precision() != "fp32":
         if g_y_split is None:
             g_y_split = kernels.split_planes(g_y)
         x2, x1 = enc.gdn2.effective_params_bwd_x6(), enc.gdn1.effective_params_bwd_x6()
@@ -178,7 +178,7 @@ def analysis_backward(enc, saved: Dict[str, Tensor], g_y: Tensor,
 def synthesis_forward_train(dec, y_nhwc: Tensor, x_ref: Optional[Tensor] = None,
                             y_split: Optional[Tensor] = None):
     d1, d2, d3, q1, q2 = dec.packed()
-    if kernels.precision() == "x6":
+    if kernels.precision() != "fp32":
         if y_split is None:
             y_split = kernels.split_planes(y_nhwc)
         e1, e2 = dec.igdn1.effective_params_x6(), dec.igdn2.effective_params_x6()
@@ -205,7 +205,7 @@ def synthesis_backward(dec, saved: Dict[str, Tensor], g_recon: Tensor, g_bpp: Op
     gradients of Synthesis_net_17, rate-parameter partials[, ∂L/∂ỹ in split form (x6 mode,
     else None)]). In the x6 mode the input-gradient contractions run in x6, each kernel handing
     the next its gradient in split form."""
-    x6 = kernels.precision() == "x6"
+    x6 = kernels.precision() != "fp32"
     N = dec.out_channel_N
     bq1, gq1, _ = dec.igdn1.bounds_f32()
     bq2, gq2, _ = dec.igdn2.bounds_f32()

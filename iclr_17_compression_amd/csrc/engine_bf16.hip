@@ -1,0 +1,804 @@
+// bf16 throughput mode of the Ballé-2017 codec forward on gfx950.
+//
+// Activations between layers are bf16 NHWC ([B][h][w][N], round-to-nearest-even from fp32), the
+// weights and the GDN γ are bf16, every contraction is ONE v_mfma_f32_16x16x32_bf16 product per
+// MAC with fp32 accumulation, and the epilogues (bias, GDN/IGDN normalisation, quantiser, rate,
+// clamp) run in fp32. This is the mode the north_star's "≥ 40 % of the bf16 MFMA peak" bar is
+// quoted on; the parity modes (exact-f32 and x6) stay the default.
+//
+// The k5 engine (conv2, conv3 + quantiser + rate, deconv1, deconv2), analysis_17.py:18-23 and
+// synthesis_17.py:15-22:
+//   * Tile: TH × 16 output pixels of the base grid (conv: the output grid; deconv: one stride
+//     phase of the input grid) × NB output channels per workgroup of WM × WN waves. MFMA
+//     orientation C[channel][pixel]: A = weights (16 channels × 8 k per lane), B = pixels (one
+//     pixel's 8 consecutive input channels per lane), so a lane's accumulator holds 4
+//     consecutive channels of one pixel and the epilogue stores 8 bytes per lane.
+//   * Input: per 16-channel chunk the halo patch of the tile (conv: (2·TH+3) × 35 pixels, stored
+//     as even / odd column planes so a stride-2 tap reads consecutive 32-byte pixel slots; deconv:
+//     (TH+2) × 18) is staged ONCE by LDS-DMA and every tap reads a shifted window of it — 4.8×
+//     (conv) / 1.3× (deconv) the tile's pixels instead of 25× / 6.25×. Double buffered: chunk
+//     c+1's patch streams in during chunk c's steps. Fragment reads are conflict-free (a 16-lane
+//     group reads 16 consecutive pixel slots, the two 16-byte halves in alternate slots).
+//   * K order: one k32 step = two taps × the chunk's 16 channels (lane groups 0/1: tap 2s,
+//     channel halves; 2/3: tap 2s+1); an odd tap count is padded with a zero-weight tap.
+//   * Weights: the step's [4 k-groups][NB][8] bf16 slice (12 KB at NB = 192) by LDS-DMA into a
+//     two-stage ring, one barrier per step.
+//   * Epilogues: GDN / IGDN (x² → bf16 tile in LDS, the channel contraction n = γ·x² on the same
+//     MFMA with γ bf16 from L2, then x/√(β+n) or x·√(β+n) in fp32), and the quantiser + rate of
+//     conv3 (round half-to-even, the factorised CDF twice, −log₂, per-workgroup bit sums).
+#include <string.h>
+
+#include "common.h"
+
+namespace iclr17 {
+namespace bfm {
+
+typedef unsigned short u16;
+typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+
+enum BEpi : int { BE_GDN = 0, BE_IGDN = 1, BE_QUANT = 2 };
+enum BMode : int { BM_CONV = 0, BM_DECONV = 1 };
+
+__device__ __forceinline__ unsigned pack_bf2(float a, float b) {
+  const bf2 v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(unsigned, v);
+}
+
+__device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+__device__ __attribute__((aligned(16))) unsigned g_zero16[4] = {0u, 0u, 0u, 0u};
+
+__device__ __forceinline__ f4 mfma_bf16(const u4& a, const u4& b, const f4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, a),
+                                                 __builtin_bit_cast(bf8, b), c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void vm_barrier() {
+  // every LDS-DMA of this wave landed (vmcnt(0)), then the workgroup barrier
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt((0 & 15) | (7 << 4) | (15 << 8));
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+struct K5Args {
+  const u16* in;        // bf16 NHWC [B][Hin][Win][CI]
+  const u16* w;         // packed bf16 weights (iclr17_pack_bf16 ICLR17_BF_CONV5 / _DECONV5)
+  const float* bias;    // [CO] or null
+  const float* beta;    // GDN: β_eff [CO]
+  const u16* gamma;     // GDN: γ_eff bf16 in the A-fragment layout [CO/8][CO][8]
+  u16* out;             // bf16 NHWC [B][Hout][Wout][CO]
+  float* out_f32;       // QUANT: ŷ fp32 NHWC
+  float* y_f32;         // QUANT: y (before rounding) fp32 NHWC, or null
+  const float* rate;    // QUANT: packed rate table [11][CO]
+  double* partial;      // QUANT: bit sums [B][ppi]
+  int ppi;              // QUANT: partials per image
+  int B, Hin, Win, Hout, Wout;
+  int gh, gw;           // base grid (conv: output grid; deconv: input grid)
+  int tiles_x, tiles_y;
+};
+
+// ---------------------------------------------------------------------- tap geometry
+// conv (k5 s2 p2): tap t = 5·ky + kx reads patch row 2·r + ky, column 2·m + kx.
+// deconv (k5 s2 p2 op1), stride phase (py, px): output (2g + p) sums k ≡ p (mod 2), input
+// g + (p + 2 − k)/2, i.e. offsets d ∈ {1, 0, −1} (p = 0: k = 0, 2, 4) or {1, 0} (p = 1: k = 1, 3).
+template <int MODE, int PH>
+struct Taps {
+  static constexpr int NY = MODE == BM_CONV ? 5 : ((PH >> 1) == 0 ? 3 : 2);
+  static constexpr int NX = MODE == BM_CONV ? 5 : ((PH & 1) == 0 ? 3 : 2);
+  static constexpr int T = NY * NX;
+  static constexpr int S = (T + 1) / 2;   // k32 steps per chunk
+  __host__ __device__ static constexpr int ky(int t) {
+    return MODE == BM_CONV ? t / 5 : ((PH >> 1) == 0 ? 2 * (t / NX) : 2 * (t / NX) + 1);
+  }
+  __host__ __device__ static constexpr int kx(int t) {
+    return MODE == BM_CONV ? t % 5 : ((PH & 1) == 0 ? 2 * (t % NX) : 2 * (t % NX) + 1);
+  }
+};
+
+template <int MODE, int TH>
+struct Patch {
+  // conv: rows 2·TH+3, each row two column planes (even / odd) of 18 slots of 32 bytes
+  // deconv: rows TH+2, 18 slots of 32 bytes
+  static constexpr int ROWS = MODE == BM_CONV ? 2 * TH + 3 : TH + 2;
+  static constexpr int ROWB = MODE == BM_CONV ? 2 * 18 * 32 : 18 * 32;
+  static constexpr int BYTES = ROWS * ROWB;
+  static constexpr int NQI = (BYTES + 1023) / 1024;   // LDS-DMA wave-instructions per chunk
+  static constexpr int BUF = NQI * 1024;               // buffer bytes (tail slots load zeros)
+  // byte offset of (patch row pr, patch column pc) for lane half h
+  __host__ __device__ static constexpr int off(int pr, int pc) {
+    return MODE == BM_CONV ? pr * ROWB + (pc & 1) * 18 * 32 + (pc >> 1) * 32 : pr * ROWB + pc * 32;
+  }
+  // tap offset relative to tile pixel (r, m) = (0, 0)
+  template <int PH>
+  __host__ __device__ static constexpr int tap_off(int t) {
+    using TP = Taps<MODE, PH>;
+    if (t >= TP::T) return 0;   // the zero-weight pad tap reads any valid slot
+    if (MODE == BM_CONV) return off(TP::ky(t), TP::kx(t));
+    const int dy = ((PH >> 1) + 2 - TP::ky(t)) / 2, dx = ((PH & 1) + 2 - TP::kx(t)) / 2;
+    return off(dy + 1, dx + 1);
+  }
+};
+
+// ------------------------------------------------------------------------- GDN epilogue
+// GDN / IGDN (models/GDN.py:64-94) on a C[channel][pixel] accumulator tile: acc[nt][mt][j] is
+// channel ncol + nt·16 + 4·(lane >> 4) + j of tile pixel pix0 + mt·16 + (lane & 15). Adds the
+// bias, writes x² as bf16 into an LDS tile [R pixels][CO] (row stride CO·2 + 32 bytes: the
+// 16-lane fragment reads hit distinct banks), contracts it with γ_eff (bf16 A fragments from L2,
+// one 16-channel block at a time), forms x/√(β+n) or x·√(β+n) in fp32 and stores the bf16 rows
+// through the same tile, 16 bytes per lane. Entry: LDS free (caller's barrier).
+template <int CO, int MT, int NT, int NTHR, bool INV, class PixFn>
+__device__ __forceinline__ void gdn_epilogue_bf16(f4 (&acc)[NT][MT], unsigned char* sq,
+                                                  const float* __restrict__ bias,
+                                                  const float* __restrict__ beta,
+                                                  const u16* __restrict__ gamma, u16* out, int R,
+                                                  int pix0, int ncol, PixFn out_pixel) {
+  typedef const __attribute__((address_space(3))) u4* lu4p;
+  constexpr int RS = CO * 2 + 32;
+  const int tid = threadIdx.x, lane = tid & 63, kg = lane >> 4;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int ch = ncol + nt * 16 + 4 * kg;
+    const f4 bv = bias ? *(const f4*)(bias + ch) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      acc[nt][mt] += bv;
+      const f4 v = acc[nt][mt];
+      const int p = pix0 + mt * 16 + (lane & 15);
+      *(uint2*)(sq + p * RS + ch * 2) = uint2{pack_bf2(v[0] * v[0], v[1] * v[1]),
+                                              pack_bf2(v[2] * v[2], v[3] * v[3])};
+    }
+  }
+  __syncthreads();
+  // n[i][p] = Σ_j γ[i][j]·x²[j][p]: A = γ (rows i), B = x² (k = j)
+  const u16* gb = gamma + (kg * CO + ncol + (lane & 15)) * 8;
+  const unsigned char* xb = sq + (pix0 + (lane & 15)) * RS + kg * 16;
+  constexpr int KB = CO / 32;
+  u4 gnext = *(const u4*)gb;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    f4 nacc[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) nacc[mt] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      const u4 gc = gnext;
+      const int nn = kb + 1 < KB ? nt : nt + 1, kn = kb + 1 < KB ? kb + 1 : 0;
+      if (nn < NT) gnext = *(const u4*)(gb + (long)kn * 4 * CO * 8 + nn * 128);
+      u4 xs[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) xs[mt] = *(lu4p)(xb + mt * 16 * RS + kb * 64);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) nacc[mt] = mfma_bf16(gc, xs[mt], nacc[mt]);
+    }
+    const int ch = ncol + nt * 16 + 4 * kg;
+    const f4 be = *(const f4*)(beta + ch);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float s = sqrtf(nacc[mt][j] + be[j]);
+        acc[nt][mt][j] = INV ? acc[nt][mt][j] * s : acc[nt][mt][j] / s;
+      }
+  }
+  __syncthreads();   // x² reads done: the tile is rewritten with the output
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int ch = ncol + nt * 16 + 4 * kg;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const f4 y = acc[nt][mt];
+      const int p = pix0 + mt * 16 + (lane & 15);
+      *(uint2*)(sq + p * RS + ch * 2) = uint2{pack_bf2(y[0], y[1]), pack_bf2(y[2], y[3])};
+    }
+  }
+  __syncthreads();
+  constexpr int PCS = CO * 2 / 16;   // 16-byte pieces per pixel row
+  for (int idx = tid; idx < R * PCS; idx += NTHR) {
+    const int p = idx / PCS, pc = idx - p * PCS;
+    const long o = out_pixel(p);
+    if (o < 0) continue;
+    *(u4*)(out + o * CO + pc * 8) = *(lu4p)(sq + p * RS + pc * 16);
+  }
+}
+
+// ------------------------------------------------------------------------------ kernel
+template <int MODE, int TH, int NB, int WM, int WN, int CO, int CI, int EPI>
+struct K5 {
+  static constexpr int NW = WM * WN, NT_ = NW * 64;
+  static constexpr int MT = TH / WM;            // 16-pixel tile rows per wave
+  static constexpr int NT = NB / WN / 16;       // 16-channel blocks per wave
+  static constexpr int R = TH * 16;             // pixels per tile
+  static constexpr int NCH = CI / 16;           // 16-channel chunks
+  static constexpr int SB = 4 * NB * 16;        // weight stage bytes
+  static constexpr int NBI = SB / 1024;         // weight DMA wave-instructions per step
+  using P = Patch<MODE, TH>;
+  static constexpr int RS = CO * 2 + 32;        // epilogue tile row stride (bytes): conflict-free
+  static constexpr int MAIN_LDS = 2 * P::BUF + 2 * SB;
+  static constexpr int EPI_LDS = EPI == BE_QUANT ? 64 : R * RS;
+  static constexpr int LDS = MAIN_LDS > EPI_LDS ? MAIN_LDS : EPI_LDS;
+  static_assert(TH % WM == 0 && NB % (WN * 16) == 0 && SB % 1024 == 0, "tile shape");
+  static_assert(EPI == BE_QUANT || NB == CO, "GDN needs every channel of a pixel in the tile");
+};
+
+template <int MODE, int TH, int NB, int WM, int WN, int CO, int CI, int EPI, int PH>
+__device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, int b, int ty, int tx,
+                                        int nb) {
+  using KK = K5<MODE, TH, NB, WM, WN, CO, CI, EPI>;
+  using P = typename KK::P;
+  using TP = Taps<MODE, PH>;
+  constexpr int MT = KK::MT, NT = KK::NT, NW = KK::NW, S = TP::S, NCH = KK::NCH;
+  constexpr int SB = KK::SB, NBI = KK::NBI;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int kg = lane >> 4, half = kg & 1, hi = kg >> 1;
+  unsigned char* const sP = smem;                    // two patch buffers
+  unsigned char* const sB = smem + 2 * P::BUF;       // two weight stages
+
+  // ---- patch DMA sources: per instruction j of this wave, slot q = 64·i + lane (16 bytes)
+  constexpr int QW = (P::NQI + NW - 1) / NW;
+  int qsrc[QW];
+  const long img = (long)b * a.Hin * a.Win;
+  const int iy0 = MODE == BM_CONV ? 2 * ty * TH - 2 : ty * TH - 1;
+  const int ix0 = MODE == BM_CONV ? 2 * tx * 16 - 2 : tx * 16 - 1;
+#pragma unroll
+  for (int j = 0; j < QW; ++j) {
+    const int i = wave + NW * j;
+    const int q = i * 64 + lane;
+    const int byte = q * 16;
+    const int pr = byte / P::ROWB, rem = byte - pr * P::ROWB;
+    int pc, h;
+    bool ok;
+    if (MODE == BM_CONV) {
+      const int par = rem / (18 * 32), r2 = rem - par * 18 * 32;
+      const int idx = r2 / 32;
+      h = (r2 / 16) & 1;
+      pc = 2 * idx + par;
+      ok = pc < 35;
+    } else {
+      pc = rem / 32;
+      h = (rem / 16) & 1;
+      ok = true;
+    }
+    const int iy = iy0 + pr, ix = ix0 + pc;
+    ok = ok && i < P::NQI && pr < P::ROWS && (unsigned)iy < (unsigned)a.Hin &&
+         (unsigned)ix < (unsigned)a.Win;
+    qsrc[j] = ok ? (int)(((long)iy * a.Win + ix) * CI + 8 * h) : -1;
+  }
+  const u16* __restrict__ inb = a.in + img * CI;
+  auto issue_patch_part = [&](int c, int j) {
+    const int i = wave + NW * j;
+    if (i < P::NQI) {
+      const void* src = qsrc[j] >= 0 ? (const void*)(inb + qsrc[j] + c * 16) : (const void*)g_zero16;
+      glds16(src, sP + (c & 1) * P::BUF + i * 1024);
+    }
+  };
+  // ---- weight DMA: stage slot q = 64·i + lane → (k-group, column) of the workgroup's slice
+  const long wstep = 4L * CO * 8;                     // u16 per (chunk, step) of the packing
+  constexpr int BW = (NBI + NW - 1) / NW;
+  int wsrc[BW];
+#pragma unroll
+  for (int j = 0; j < BW; ++j) {
+    const int i = wave + NW * j;
+    const int q = i * 64 + lane;
+    const int g = q / NB, col = q - g * NB;
+    wsrc[j] = (g * CO + nb * NB + col) * 8;
+  }
+  // packed weights of this phase: [NCH][S][4][CO][8]
+  const u16* __restrict__ wph = a.w;
+  if (MODE == BM_DECONV) {
+    long off = 0;
+#pragma unroll
+    for (int p = 0; p < PH; ++p) {
+      const int ny = (p >> 1) == 0 ? 3 : 2, nx = (p & 1) == 0 ? 3 : 2;
+      off += (long)NCH * ((ny * nx + 1) / 2) * wstep;
+    }
+    wph += off;
+  }
+  auto issue_w = [&](int gstep) {   // gstep = c·S + s
+    const u16* src = wph + (long)gstep * wstep;
+    unsigned char* dst = sB + (gstep & 1) * SB;
+#pragma unroll
+    for (int j = 0; j < BW; ++j) {
+      const int i = wave + NW * j;
+      if (NBI % NW == 0 || i < NBI) glds16(src + wsrc[j], dst + i * 1024);
+    }
+  };
+
+  // ---- per-lane fragment addresses
+  // B (pixels): lane pixel (tile row wm·MT + mt, column lane & 15), channel half `half`
+  const int prow0 = (MODE == BM_CONV ? 2 : 1) * (wm * MT);
+  const int pbase = P::off(prow0, MODE == BM_CONV ? 2 * (lane & 15) : (lane & 15)) + 16 * half;
+  constexpr int MT_STRIDE = (MODE == BM_CONV ? 2 : 1) * P::ROWB;
+  // A (weights): stage [4][NB][8]: lane (k-group kg, column ncol + nt·16 + lane & 15)
+  const int ncol = wn * (NB / WN);
+  const int abase = (kg * NB + ncol + (lane & 15)) * 16;
+
+  f4 acc[NT][MT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = f4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: chunk 0's patch and step 0's weights
+#pragma unroll
+  for (int j = 0; j < QW; ++j) issue_patch_part(0, j);
+  issue_w(0);
+
+  typedef const __attribute__((address_space(3))) u4* lu4p;
+  for (int c = 0; c < NCH; ++c) {
+    const unsigned char* pbuf = sP + (c & 1) * P::BUF + pbase;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int g = c * S + s;
+      vm_barrier();   // step g's weights (and at s = 0 chunk c's patch) landed; stage (g+1)&1 free
+      if (g + 1 < NCH * S) issue_w(g + 1);
+      if (c + 1 < NCH) {   // chunk c+1's patch, spread over this chunk's first steps
+#pragma unroll
+        for (int j = 0; j < QW; ++j)
+          if (j % (S > 1 ? S - 1 : 1) == s) issue_patch_part(c + 1, j);
+      }
+      // tap pair (2s, 2s+1): lanes 0-31 the first, 32-63 the second
+      const int t0 = P::template tap_off<PH>(2 * s), t1 = P::template tap_off<PH>(2 * s + 1);
+      const unsigned char* pb = pbuf + t0 + hi * (t1 - t0);
+      const unsigned char* wb = sB + (g & 1) * SB + abase;
+      u4 wa[NT], px[MT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) wa[nt] = *(lu4p)(wb + nt * 256);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) px[mt] = *(lu4p)(pb + mt * MT_STRIDE);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = mfma_bf16(wa[nt], px[mt], acc[nt][mt]);
+    }
+  }
+  __syncthreads();   // every wave is done with the stages before the epilogue reuses LDS
+
+  // ---- epilogue. acc[nt][mt][j]: channel ncol + nt·16 + 4·kg + j, tile pixel p(mt) =
+  // (wm·MT + mt)·16 + (lane & 15)
+  auto out_pixel = [&](int p) -> long {   // NHWC pixel index, or -1 outside the grid
+    const int gy = ty * TH + (p >> 4), gx = tx * 16 + (p & 15);
+    if (gy >= a.gh || gx >= a.gw) return -1;
+    if (MODE == BM_CONV) return ((long)b * a.Hout + gy) * a.Wout + gx;
+    return ((long)b * a.Hout + 2 * gy + (PH >> 1)) * a.Wout + 2 * gx + (PH & 1);
+  };
+  if constexpr (EPI == BE_GDN || EPI == BE_IGDN) {
+    gdn_epilogue_bf16<CO, MT, NT, KK::NT_, EPI == BE_IGDN>(acc, smem, a.bias, a.beta, a.gamma, a.out,
+                                                          KK::R, wm * MT * 16, ncol, out_pixel);
+  } else {
+    static_assert(EPI == BE_QUANT, "epilogue");
+    // conv3 + model.py:56 round (half to even) + model.py:71-73 rate, per element
+    float bits = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int ch = nb * NB + ncol + nt * 16 + 4 * kg;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int p = (wm * MT + mt) * 16 + (lane & 15);
+        const long o = out_pixel(p);
+        if (o < 0) continue;
+        const f4 y = acc[nt][mt];
+        f4 q;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          q[j] = rintf(y[j]);
+          bits += element_bits(q[j], a.rate, CO, ch + j);
+        }
+        if (a.y_f32) *(f4*)(a.y_f32 + o * CO + ch) = y;
+        *(f4*)(a.out_f32 + o * CO + ch) = q;
+        *(uint2*)(a.out + o * CO + ch) = uint2{pack_bf2(q[0], q[1]), pack_bf2(q[2], q[3])};
+      }
+    }
+    bits = wave_sum(bits);
+    float* red = (float*)smem;
+    if (lane == 0) red[wave] = bits;
+    __syncthreads();
+    if (tid == 0) {
+      double s = 0.0;
+      for (int w = 0; w < NW; ++w) s += (double)red[w];
+      const int tile = ty * a.tiles_x + tx;
+      a.partial[(long)b * a.ppi + tile * (CO / NB) + nb] = s;
+    }
+  }
+}
+
+template <int MODE, int TH, int NB, int WM, int WN, int CO, int CI, int EPI>
+__global__ void __launch_bounds__(WM * WN * 64)
+k5_bf16_kernel(const K5Args a) {
+  using KK = K5<MODE, TH, NB, WM, WN, CO, CI, EPI>;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[KK::LDS];
+  int bid = blockIdx.x;
+  const int per_ph = a.tiles_x * a.tiles_y * a.B;
+  const int ph = MODE == BM_DECONV ? bid / per_ph : 0;   // phases dispatched phase-major
+  bid -= ph * per_ph;
+  const int tx = bid % a.tiles_x;
+  bid /= a.tiles_x;
+  const int ty = bid % a.tiles_y;
+  const int b = bid / a.tiles_y;
+  const int nb = blockIdx.y;
+  if constexpr (MODE == BM_CONV) {
+    k5_body<MODE, TH, NB, WM, WN, CO, CI, EPI, 0>(a, smem, b, ty, tx, nb);
+  } else {
+    switch (ph) {   // wave-uniform: the tap lists are compile-time per phase
+      case 0: k5_body<MODE, TH, NB, WM, WN, CO, CI, EPI, 0>(a, smem, b, ty, tx, nb); break;
+      case 1: k5_body<MODE, TH, NB, WM, WN, CO, CI, EPI, 1>(a, smem, b, ty, tx, nb); break;
+      case 2: k5_body<MODE, TH, NB, WM, WN, CO, CI, EPI, 2>(a, smem, b, ty, tx, nb); break;
+      default: k5_body<MODE, TH, NB, WM, WN, CO, CI, EPI, 3>(a, smem, b, ty, tx, nb); break;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ conv1
+// analysis_17.py:14-17 conv1 (3→N, k9 s4 p4) + GDN1 in bf16. An 8×8 output block per
+// workgroup (4 waves, each all 64 pixels × N/4 channels). The 37×37×3 input patch lands in LDS
+// by LDS-DMA as fp32 and is rounded once into one bf16 plane [3·37][40]. K = 243 is reordered
+// (ICLR17_W_CONV1_X6 packing): k-group g = 4s + (lane >> 4) is 8 consecutive patch columns of
+// one (channel, kernel row) pair for g < 27, zero for g = 27, and for g = 28..31 the kw = 8
+// column of 8 pairs gathered element-wise. The weight fragments [32][N][8] bf16 come from L2
+// one step ahead (no LDS stage, no barrier in the 8-step loop).
+constexpr int C1P = 37;                       // patch side: 8·4 + 9 − 4
+constexpr int C1RS = 40;                      // row stride (elements): 10 16-byte fp32 pieces
+constexpr int C1PIECES = 3 * C1P * 10;        // fp32 16-byte pieces of the patch (1110)
+constexpr int C1NI = (C1PIECES + 63) / 64;    // LDS-DMA wave-instructions (18)
+constexpr int C1U = 3 * C1P * C1RS;           // u16 elements of the bf16 plane (4440)
+
+template <int CO>
+struct C1 {
+  static constexpr int LAND = C1NI * 1024;            // fp32 landing area (bytes)
+  static constexpr int PLANE = C1U * 2;                // bf16 plane (bytes)
+  static constexpr int MAIN = LAND + PLANE;
+  static constexpr int EPI = 64 * (CO * 2 + 32);
+  static constexpr int LDS = MAIN > EPI ? MAIN : EPI;
+};
+
+template <int CO>
+__global__ void __launch_bounds__(256, 2) conv1_bf16_kernel(const float* __restrict__ x, int H,
+                                                            int W, const u16* __restrict__ wbf,
+                                                            const float* __restrict__ bias,
+                                                            const float* __restrict__ beta,
+                                                            const u16* __restrict__ gamma,
+                                                            u16* __restrict__ out, int tiles_x,
+                                                            int tiles_y) {
+  constexpr int MT = 4, NT = CO / 4 / 16;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[C1<CO>::LDS];
+  float* sr = (float*)smem;                                // fp32 landing area
+  u16* sp = (u16*)(smem + C1<CO>::LAND);                   // bf16 plane
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int bid = blockIdx.x;
+  const int tx = bid % tiles_x;
+  bid /= tiles_x;
+  const int ty = bid % tiles_y;
+  const int b = bid / tiles_y;
+  const int ncol = wave * (CO / 4);
+  const int iy0 = ty * 32 - 4, ix0 = tx * 32 - 4;
+  // patch by LDS-DMA: piece (c, r, q) = columns 4q .. 4q+3 of patch row r of channel c; the
+  // patch origin ix0 ≡ 0 (mod 4) and W ≡ 0 (mod 16): a piece is wholly in or out of the image
+#pragma unroll
+  for (int j = 0; j < (C1NI + 3) / 4; ++j) {
+    const int i = wave + 4 * j;
+    if (i < C1NI) {
+      const int pc = i * 64 + lane;
+      const int cr = pc / 10, q = pc - cr * 10;
+      const int c = cr / C1P, r = cr - c * C1P;
+      const int iy = iy0 + r, ix = ix0 + 4 * q;
+      const bool ok = pc < C1PIECES && iy >= 0 && iy < H && ix >= 0 && ix < W;
+      glds16(ok ? (const void*)(x + (((long)b * 3 + c) * H + iy) * W + ix) : (const void*)g_zero16,
+             sr + i * 256);
+    }
+  }
+  // weight fragments: lane (k-group lane >> 4, channel ncol + nt·16 + lane & 15)
+  const u16* gb = wbf + ((lane >> 4) * CO + ncol + (lane & 15)) * 8;
+  u4 w0[NT], w1[NT];
+  auto loadw = [&](int s, u4 (&w)[NT]) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) w[nt] = *(const u4*)(gb + (long)s * 4 * CO * 8 + nt * 128);
+  };
+  loadw(0, w0);
+  vm_barrier();   // patch landed
+  for (int pc = tid; pc < C1PIECES; pc += 256) {   // round once into the bf16 plane
+    const f4 v = *(const f4*)(sr + pc * 4);
+    *(uint2*)(sp + pc * 4) = uint2{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+  }
+  __syncthreads();
+
+  f4 acc[NT][MT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = f4{0.f, 0.f, 0.f, 0.f};
+  int pix[MT];   // output pixel (my, mx) → patch row 4·my, column 4·mx
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int m = mt * 16 + (lane & 15);
+    pix[mt] = (m >> 3) * 4 * C1RS + (m & 7) * 4;
+  }
+  const int kg = lane >> 4;
+  auto pair_off = [](int p) { return ((p / 9) * C1P + p % 9) * C1RS; };
+  auto mfma_all = [&](int mt, const u4& px, const u4 (&w)[NT]) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[nt][mt] = mfma_bf16(w[nt], px, acc[nt][mt]);
+  };
+  auto step_rows = [&](int s, const u4 (&w)[NT]) {
+    const int g = 4 * s + kg;
+    const int po = pair_off(g < 27 ? g : 26);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const u16* e = sp + po + pix[mt];
+      const uint2 lo2 = *(const uint2*)e, hi2 = *(const uint2*)(e + 4);
+      mfma_all(mt, u4{lo2.x, lo2.y, hi2.x, hi2.y}, w);
+    }
+  };
+  auto step_col8 = [&](const u4 (&w)[NT]) {
+    int po[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int p = 8 * kg + e;
+      po[e] = pair_off(p < 27 ? p : 26) + 8;
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      u4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const unsigned lo = sp[po[2 * i] + pix[mt]], hi = sp[po[2 * i + 1] + pix[mt]];
+        v[i] = lo | (hi << 16);
+      }
+      mfma_all(mt, v, w);
+    }
+  };
+  loadw(1, w1); step_rows(0, w0);
+  loadw(2, w0); step_rows(1, w1);
+  loadw(3, w1); step_rows(2, w0);
+  loadw(4, w0); step_rows(3, w1);
+  loadw(5, w1); step_rows(4, w0);
+  loadw(6, w0); step_rows(5, w1);
+  loadw(7, w1); step_rows(6, w0);
+  step_col8(w1);
+  __syncthreads();   // plane reads done before the epilogue reuses LDS
+  const int Ho = H / 4, Wo = W / 4;
+  auto out_pixel = [&](int p) -> long {
+    const int oy = ty * 8 + (p >> 3), ox = tx * 8 + (p & 7);
+    if (oy >= Ho || ox >= Wo) return -1;
+    return ((long)b * Ho + oy) * Wo + ox;
+  };
+  gdn_epilogue_bf16<CO, MT, NT, 256, false>(acc, smem, bias, beta, gamma, out, 64, 0, ncol,
+                                            out_pixel);
+}
+
+// ------------------------------------------------------------------------------ packing
+// conv (ICLR17_BF_CONV5), W[co][ci][5][5] → [CI/16][S=13][4][CO][8]: k-group kg of step s is tap
+// 2s + (kg >> 1), channels 16c + 8·(kg & 1) + e; tap 25 (the pad) is zero.
+// deconv (ICLR17_BF_DECONV5), W[ci][co][5][5] → the four phases back to back, phase p:
+// [CI/16][S_p][4][CO][8] with the phase's taps in Taps<BM_DECONV, p> order.
+__global__ void __launch_bounds__(256) pack_k5_bf16_kernel(const float* __restrict__ w, int N,
+                                                           int deconv, u16* __restrict__ out,
+                                                           long total) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int e = (int)(i & 7);
+    long r = i >> 3;
+    const int co = (int)(r % N);
+    r /= N;
+    const int kg = (int)(r & 3);
+    r >>= 2;
+    const int nch = N / 16;
+    int ph = 0, ny = 5, nx = 5, S = 13;
+    if (deconv) {   // phase blocks of nch·S_p·4·N·8
+      for (ph = 0; ph < 4; ++ph) {
+        ny = (ph >> 1) == 0 ? 3 : 2;
+        nx = (ph & 1) == 0 ? 3 : 2;
+        S = (ny * nx + 1) / 2;
+        if (r < (long)nch * S) break;
+        r -= (long)nch * S;
+      }
+    }
+    const int c = (int)(r / S), s = (int)(r % S);
+    const int t = 2 * s + (kg >> 1);
+    const int ci = 16 * c + 8 * (kg & 1) + e;
+    float v = 0.f;
+    if (t < ny * nx) {
+      int ky, kx;
+      if (!deconv) {
+        ky = t / 5;
+        kx = t % 5;
+      } else {
+        ky = (ph >> 1) == 0 ? 2 * (t / nx) : 2 * (t / nx) + 1;
+        kx = (ph & 1) == 0 ? 2 * (t % nx) : 2 * (t % nx) + 1;
+      }
+      v = deconv ? w[(((long)ci * N + co) * 5 + ky) * 5 + kx] : w[(((long)co * N + ci) * 5 + ky) * 5 + kx];
+    }
+    out[i] = __builtin_bit_cast(u16, (__bf16)v);
+  }
+}
+
+// packed fp32 operand [taps][K/4][N][4] → bf16 (round to nearest even) [taps][K/8][N][8]:
+// the 16x16x32 fragment layout (conv1's reordered weights, the GDN γ)
+__global__ void __launch_bounds__(256) round_packed_kernel(const float* __restrict__ w, int K, int N,
+                                                           long groups, u16* __restrict__ out) {
+  for (long g = (long)blockIdx.x * 256 + threadIdx.x; g < groups; g += (long)gridDim.x * 256) {
+    const long tk = g / N;
+    const int col = (int)(g - tk * N);
+    const long tap = tk / (K / 8);
+    const int k8 = (int)(tk - tap * (K / 8));
+    const float* src = w + ((tap * (K / 4) + 2 * k8) * N + col) * 4;
+    const f4 lo = *(const f4*)src, hi = *(const f4*)(src + (long)N * 4);
+    *(u4*)(out + g * 8) = u4{pack_bf2(lo[0], lo[1]), pack_bf2(lo[2], lo[3]), pack_bf2(hi[0], hi[1]),
+                             pack_bf2(hi[2], hi[3])};
+  }
+}
+
+// fp32 → bf16 (round to nearest even), 8 per thread
+__global__ void __launch_bounds__(256) to_bf16_kernel(const float* __restrict__ x, long n8,
+                                                      u16* __restrict__ out) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    const f4 a = *(const f4*)(x + 8 * i), b = *(const f4*)(x + 8 * i + 4);
+    *(u4*)(out + 8 * i) = u4{pack_bf2(a[0], a[1]), pack_bf2(a[2], a[3]), pack_bf2(b[0], b[1]),
+                             pack_bf2(b[2], b[3])};
+  }
+}
+
+// ------------------------------------------------------------------------------ launchers
+template <int N>
+int launch_conv2(const K5Args& a0, hipStream_t st) {
+  K5Args a = a0;
+  a.tiles_y = (a.gh + 15) / 16;
+  a.tiles_x = (a.gw + 15) / 16;
+  hipLaunchKernelGGL((k5_bf16_kernel<BM_CONV, 16, N, 4, 2, N, N, BE_GDN>),
+                     dim3(a.tiles_x * a.tiles_y * a.B, 1), dim3(512), 0, st, a);
+  return check_launch("conv2_gdn_bf16");
+}
+
+template <int N>
+int launch_conv3(const K5Args& a0, hipStream_t st) {
+  K5Args a = a0;
+  a.tiles_y = (a.gh + 7) / 8;
+  a.tiles_x = (a.gw + 15) / 16;
+  constexpr int NB = N / 2;
+  a.ppi = a.tiles_x * a.tiles_y * 2;
+  hipLaunchKernelGGL((k5_bf16_kernel<BM_CONV, 8, NB, 2, 2, N, N, BE_QUANT>),
+                     dim3(a.tiles_x * a.tiles_y * a.B, 2), dim3(256), 0, st, a);
+  return check_launch("conv3_quant_rate_bf16");
+}
+
+template <int N, int TH>
+int launch_deconv(const K5Args& a0, hipStream_t st) {
+  K5Args a = a0;
+  a.tiles_y = (a.gh + TH - 1) / TH;
+  a.tiles_x = (a.gw + 15) / 16;
+  constexpr int WM = TH == 16 ? 4 : 2, WN = 8 / WM;
+  hipLaunchKernelGGL((k5_bf16_kernel<BM_DECONV, TH, N, WM, WN, N, N, BE_IGDN>),
+                     dim3(a.tiles_x * a.tiles_y * a.B * 4, 1), dim3(512), 0, st, a);
+  return check_launch("deconv_igdn_bf16");
+}
+
+}  // namespace bfm
+}  // namespace iclr17
+
+using namespace iclr17;
+using namespace iclr17::bfm;
+
+extern "C" {
+
+size_t iclr17_bf16_weight_size(int which, int N) {
+  if (N != 128 && N != 192) return 0;
+  switch (which) {
+    case ICLR17_BF_CONV5: return (size_t)(N / 16) * 13 * 4 * N * 8;
+    case ICLR17_BF_DECONV5: return (size_t)(N / 16) * (5 + 3 + 3 + 2) * 4 * N * 8;
+    default: return 0;
+  }
+}
+
+int iclr17_pack_bf16(int which, const float* w, uint16_t* out, int N, void* stream) {
+  const size_t total = iclr17_bf16_weight_size(which, N);
+  ICLR17_REQUIRE(total > 0, ICLR17_EUNSUPPORTED, "pack_bf16: kind %d, N=%d unsupported", which, N);
+  ICLR17_REQUIRE(w && out, ICLR17_EINVAL, "pack_bf16: null pointer");
+  const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+  hipLaunchKernelGGL(pack_k5_bf16_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, N,
+                     which == ICLR17_BF_DECONV5 ? 1 : 0, out, (long)total);
+  return check_launch("pack_bf16");
+}
+
+int iclr17_round_packed(const float* packed, int taps, int K, int N, uint16_t* out, void* stream) {
+  ICLR17_REQUIRE(packed && out && taps > 0 && K % 8 == 0 && N > 0, ICLR17_EINVAL,
+                 "round_packed: bad arguments");
+  const long groups = (long)taps * (K / 8) * N;
+  const int blocks = (int)((groups + 255) / 256 < 4096 ? (groups + 255) / 256 : 4096);
+  hipLaunchKernelGGL(round_packed_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, packed,
+                     K, N, groups, out);
+  return check_launch("round_packed");
+}
+
+int iclr17_to_bf16(const float* x, long n, uint16_t* out, void* stream) {
+  ICLR17_REQUIRE(x && out && n >= 0 && n % 8 == 0, ICLR17_EINVAL,
+                 "to_bf16: null pointer or n (%ld) not a multiple of 8", n);
+  if (n == 0) return ICLR17_OK;
+  const long n8 = n / 8;
+  const int blocks = (int)((n8 + 255) / 256 < 8192 ? (n8 + 255) / 256 : 8192);
+  hipLaunchKernelGGL(to_bf16_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, n8, out);
+  return check_launch("to_bf16");
+}
+
+int iclr17_analysis_conv1_gdn_bf16(const float* x, int B, int H, int W, int N,
+                                   const uint16_t* w_bf16, const float* bias,
+                                   const float* beta_eff, const uint16_t* gamma_bf16,
+                                   uint16_t* out, void* stream) {
+  ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "conv1_gdn_bf16: N=%d", N);
+  ICLR17_REQUIRE(x && w_bf16 && bias && beta_eff && gamma_bf16 && out && B > 0 && H > 0 && W > 0 &&
+                     H % 16 == 0 && W % 16 == 0,
+                 ICLR17_EINVAL, "conv1_gdn_bf16: bad arguments (H, W multiples of 16)");
+  const int tiles_y = (H / 4 + 7) / 8, tiles_x = (W / 4 + 7) / 8;
+  const dim3 grid(tiles_x * tiles_y * B);
+  hipStream_t st = (hipStream_t)stream;
+  if (N == 192)
+    hipLaunchKernelGGL(conv1_bf16_kernel<192>, grid, dim3(256), 0, st, x, H, W, w_bf16, bias,
+                       beta_eff, gamma_bf16, out, tiles_x, tiles_y);
+  else
+    hipLaunchKernelGGL(conv1_bf16_kernel<128>, grid, dim3(256), 0, st, x, H, W, w_bf16, bias,
+                       beta_eff, gamma_bf16, out, tiles_x, tiles_y);
+  return check_launch("conv1_gdn_bf16");
+}
+
+int iclr17_analysis_conv2_gdn_bf16(const uint16_t* in, int B, int H, int W, int N,
+                                   const uint16_t* w_bf16, const float* bias, const float* beta_eff,
+                                   const uint16_t* gamma_bf16, uint16_t* out, void* stream) {
+  ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "conv2_gdn_bf16: N=%d", N);
+  ICLR17_REQUIRE(in && w_bf16 && bias && beta_eff && gamma_bf16 && out && B > 0 && H % 16 == 0 &&
+                     W % 16 == 0 && H > 0 && W > 0,
+                 ICLR17_EINVAL, "conv2_gdn_bf16: bad arguments (H, W multiples of 16)");
+  K5Args a;
+  memset(&a, 0, sizeof(a));
+  a.in = in; a.w = w_bf16; a.bias = bias; a.beta = beta_eff; a.gamma = gamma_bf16; a.out = out;
+  a.B = B; a.Hin = H / 4; a.Win = W / 4; a.Hout = H / 8; a.Wout = W / 8;
+  a.gh = a.Hout; a.gw = a.Wout;
+  hipStream_t st = (hipStream_t)stream;
+  return N == 192 ? launch_conv2<192>(a, st) : launch_conv2<128>(a, st);
+}
+
+int iclr17_bf16_rate_partials_per_image(int H, int W, int N) {
+  (void)N;
+  return ((H / 16 + 7) / 8) * ((W / 16 + 15) / 16) * 2;
+}
+
+int iclr17_analysis_conv3_quant_rate_bf16(const uint16_t* in, int B, int H, int W, int N,
+                                          const uint16_t* w_bf16, const float* rate_packed,
+                                          float* y_out, float* y_hat, uint16_t* y_hat_bf16,
+                                          double* bits_partial, void* stream) {
+  ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "conv3_quant_rate_bf16: N=%d", N);
+  ICLR17_REQUIRE(in && w_bf16 && rate_packed && y_hat && y_hat_bf16 && bits_partial && B > 0 &&
+                     H % 16 == 0 && W % 16 == 0 && H > 0 && W > 0,
+                 ICLR17_EINVAL, "conv3_quant_rate_bf16: bad arguments");
+  K5Args a;
+  memset(&a, 0, sizeof(a));
+  a.in = in; a.w = w_bf16; a.rate = rate_packed; a.y_f32 = y_out; a.out_f32 = y_hat;
+  a.out = y_hat_bf16; a.partial = bits_partial;
+  a.B = B; a.Hin = H / 8; a.Win = W / 8; a.Hout = H / 16; a.Wout = W / 16;
+  a.gh = a.Hout; a.gw = a.Wout;
+  hipStream_t st = (hipStream_t)stream;
+  return N == 192 ? launch_conv3<192>(a, st) : launch_conv3<128>(a, st);
+}
+
+int iclr17_synthesis_deconv_igdn_bf16(const uint16_t* in, int B, int h, int w, int N,
+                                      const uint16_t* w_bf16, const float* bias,
+                                      const float* beta_eff, const uint16_t* gamma_bf16,
+                                      uint16_t* out, void* stream) {
+  ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "deconv_igdn_bf16: N=%d", N);
+  ICLR17_REQUIRE(in && w_bf16 && bias && beta_eff && gamma_bf16 && out && B > 0 && h > 0 && w > 0,
+                 ICLR17_EINVAL, "deconv_igdn_bf16: bad arguments");
+  K5Args a;
+  memset(&a, 0, sizeof(a));
+  a.in = in; a.w = w_bf16; a.bias = bias; a.beta = beta_eff; a.gamma = gamma_bf16; a.out = out;
+  a.B = B; a.Hin = h; a.Win = w; a.Hout = 2 * h; a.Wout = 2 * w;
+  a.gh = h; a.gw = w;
+  hipStream_t st = (hipStream_t)stream;
+  // 16-row tiles where the grid stays ≥ 2 rounds of workgroups (deconv2), 8 rows otherwise
+  const bool big = (long)((h + 15) / 16) * ((w + 15) / 16) * B * 4 >= 512;
+  if (N == 192) return big ? launch_deconv<192, 16>(a, st) : launch_deconv<192, 8>(a, st);
+  return big ? launch_deconv<128, 16>(a, st) : launch_deconv<128, 8>(a, st);
+}
+
+}  // extern "C"

@@ -48,9 +48,6 @@ constexpr int BM = 64;        // output pixels per tile
 #ifndef ICLR17_CONV3_BN
 #define ICLR17_CONV3_BN 96    // conv3 (+ quantiser) output columns per workgroup
 #endif
-#ifndef ICLR17_W3SPLIT
-#define ICLR17_W3SPLIT 1      // conv3 x6 honours caller-provided pre-split weights (0: ignore)
-#endif
 #ifndef ICLR17_QSTAGES
 #define ICLR17_QSTAGES 2      // conv3's DMA ring depth (3, 4 measured slower: DESIGN.md §5)
 #endif
@@ -132,7 +129,6 @@ struct EngineArgs {
   long out_plane;
   const unsigned short* ggamma6;    // x6: γ_eff split, [3][CO/8][CO][8] bf16 (plane CO·CO)
   const unsigned short* ggammaT6;   // x6 backward: the transposed packing of γ_eff, split
-  const unsigned short* w6;         // x6 conv3: weights pre-split, [3][25][CI/8][CO][8] bf16
 };
 
 struct TileInfo {
@@ -926,8 +922,7 @@ __device__ __forceinline__ void out3_epilogue(f4 (&acc)[MT][NT], float* smem, co
 // columns in VALU. One 32-deep step = per 16×16 tile six v_mfma_f32_16x16x32_bf16:
 // lo·hi + hi·lo + mid·mid + mid·hi + hi·mid + hi·hi (the dropped mid·lo, lo·mid, lo·lo terms are
 // below 2^-24 of the product), accumulated in fp32.
-template <int CI, int CO, int BN, int WM, int WN, int EPI, bool PL, bool X6, int BMT = BM,
-          bool BS = false>
+template <int CI, int CO, int BN, int WM, int WN, int EPI, bool PL, bool X6, int BMT = BM>
 __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   constexpr int NWV = WM * WN;                   // waves (4, or 8 for the 128-row tiles)
   constexpr int MT = BMT / WM / 16;
@@ -935,10 +930,7 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   constexpr int KCH = 32;                        // input channels per k-step
   constexpr int NCH = CI / KCH;
   constexpr int SA = X6 ? 3 * BMT * KCH / 2 : BMT * KCH;   // A image floats per stage
-  // B image floats per stage: fp32 [8 quads][BN][4], or (BS: weights pre-split, x6) the three
-  // bf16 planes [3][4 k-groups][BN][8] — 1.5× the bytes, no split VALU in the loop
-  constexpr int SB = BS ? 3 * KCH * BN / 2 : KCH * BN;
-  static_assert(!BS || (X6 && EPI == EPI_QUANT), "pre-split B: the x6 conv3 kernel");
+  constexpr int SB = KCH * BN;                   // B image floats per stage: [8 quads][BN][4]
   constexpr int STAGE = SA + SB;
   constexpr int NAI = SA * 4 / 1024;             // A glds wave-instructions per step (8 | 12)
   constexpr int NBI = SB * 4 / 1024;             // B glds wave-instructions per step
@@ -1003,15 +995,8 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
 #pragma unroll
   for (int j = 0; j < BI_W; ++j) {
     const int i = wave + NWV * j;
-    if constexpr (BS) {   // u16 offset: LDS image [3][4][BN][8] ← planes [3][25][CI/8][CO][8]
-      const int o = i * 512 + lane * 8;
-      const int pl = o / (4 * BN * 8), r = o - pl * (4 * BN * 8);
-      const int k8 = r / (BN * 8), co8 = r - k8 * (BN * 8);
-      bsrc[j] = pl * (25 * CI * CO) + (k8 * CO + t.nb * BN) * 8 + co8;
-    } else {
-      const int o = i * 256 + lane * 4;   // offset in the LDS image [8 quads][BN][4]
-      bsrc[j] = (BN == CO) ? o : ((o / (BN * 4)) * CO + t.nb * BN) * 4 + o % (BN * 4);
-    }
+    const int o = i * 256 + lane * 4;   // offset in the LDS image [8 quads][BN][4]
+    bsrc[j] = (BN == CO) ? o : ((o / (BN * 4)) * CO + t.nb * BN) * 4 + o % (BN * 4);
   }
 
   int t0 = 0, ntaps = 1;
@@ -1048,21 +1033,12 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
       }
     }
     float* sb = sa + SA;
-    if constexpr (BS) {
-      const unsigned short* __restrict__ ws6 = a.w6 + ((long)tap * (CI / 8) + cc * 4) * CO * 8;
+    const float* __restrict__ ws = a.w + ((long)tap * CI + cc * KCH) * CO;   // uniform base
 #pragma unroll
-      for (int j = 0; j < BI_W; ++j) {
-        const int i = wave + NWV * j;
-        if (NBI % NWV == 0 || i < NBI) glds16((const float*)(ws6 + bsrc[j]), sb + i * 256);
-      }
-    } else {
-      const float* __restrict__ ws = a.w + ((long)tap * CI + cc * KCH) * CO;   // uniform base
-#pragma unroll
-      for (int j = 0; j < BI_W; ++j) {
-        const int i = wave + NWV * j;
-        if (skip_b) break;
-        if (NBI % NWV == 0 || i < NBI) glds16(ws + bsrc[j], sb + i * 256);
-      }
+    for (int j = 0; j < BI_W; ++j) {
+      const int i = wave + NWV * j;
+      if (skip_b) break;
+      if (NBI % NWV == 0 || i < NBI) glds16(ws + bsrc[j], sb + i * 256);
     }
   };
 
@@ -1094,13 +1070,7 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       u4 bh, bm, bl;
-      if constexpr (BS) {   // the fragments as stored: k-group lane >> 4, column of lane & 15
-        const unsigned short* b6 = (const unsigned short*)(smem + buf * STAGE + SA) +
-                                   ((lane >> 4) * BN + wn * (BN / WN) + nt * 16 + (lane & 15)) * 8;
-        bh = *(const u4*)b6;
-        bm = *(const u4*)(b6 + 4 * BN * 8);
-        bl = *(const u4*)(b6 + 8 * BN * 8);
-      } else if (ICLR17_ABL & 256) {
+      if (ICLR17_ABL & 256) {
         const f4 x0 = *(const f4*)(sb + nt * 64), x1 = *(const f4*)(sb + BN * 4 + nt * 64);
         bh = u4{__builtin_amdgcn_perm(__float_as_uint(x0[1]), __float_as_uint(x0[0]), 0x07060302u),
                 __builtin_amdgcn_perm(__float_as_uint(x0[3]), __float_as_uint(x0[2]), 0x07060302u),
@@ -1238,10 +1208,9 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   }  // phase loop
 }
 
-template <int CI, int CO, int BN, int WM, int WN, int EPI, bool PL = false, bool X6 = false,
-          bool BS = false>
+template <int CI, int CO, int BN, int WM, int WN, int EPI, bool PL = false, bool X6 = false>
 __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
-  engine_body<CI, CO, BN, WM, WN, EPI, PL, X6, BM, BS>(a);
+  engine_body<CI, CO, BN, WM, WN, EPI, PL, X6, BM>(a);
 }
 
 // 128-pixel tiles (16×8 base pixels) on 8 waves (2 × 4), one workgroup per CU at two waves per
@@ -1304,11 +1273,15 @@ __device__ __forceinline__ int d3_col(int j) {
   return co * 16 + ry * 4 + rx;
 }
 
-template <int CI, bool PRE = false>
+// BF: the bf16 throughput mode (engine_bf16.hip) — the input is ONE bf16 plane (bf16 NHWC), the
+// weights are rounded to bf16 in the loop and each MAC is one bf16 product.
+template <int CI, bool BF = false>
 __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) {
   constexpr int KCH = 32, NCH = CI / KCH, NSTEP = 9 * NCH;
   constexpr int MT = 4, NT = 3;
-  constexpr int AI_W = (D3_NAI + 3) / 4;   // 16 (wave 0..3 takes i = w + 4j, i < 61)
+  constexpr int NPL = BF ? 1 : 3;                         // input planes
+  constexpr int NAI = (NPL * D3_PPX + 15) / 16;           // A wave-instructions per chunk
+  constexpr int AI_W = (NAI + 3) / 4;   // x6: 16 (wave 0..3 takes i = w + 4j, i < 61)
   static_assert(3 * 64 * 65 <= D3_LDS, "epilogue block fits the stages");
   __shared__ __attribute__((aligned(16))) float smem[D3_LDS];
   float* const sA = smem;
@@ -1332,7 +1305,7 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
     const int pl = q / D3_PPX, p = q - pl * D3_PPX;
     const int r = p / D3_PS, c = p - r * D3_PS;
     const int iy = ty * D3_BS - 1 + r, ix = tx * D3_BS - 1 + c;
-    const bool ok = i < D3_NAI && pl < 3 && (unsigned)iy < (unsigned)a.Hin &&
+    const bool ok = i < NAI && pl < NPL && (unsigned)iy < (unsigned)a.Hin &&
                     (unsigned)ix < (unsigned)a.Win;
     const int g = (lane & 3) ^ (((p >> 2) & 1) << 1);
     asrc[j] = ok ? (iy * a.Win + ix) * CI + g * 8 : -1;
@@ -1342,10 +1315,10 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
 #pragma unroll
     for (int j = 0; j < AI_W; ++j) {
       const int i = wave + 4 * j;
-      if (i < D3_NAI) {
+      if (i < NAI) {
         const int q = i * 16 + (lane >> 2);
         const int pl = q / D3_PPX;
-        const unsigned short* src = inb + (long)(pl < 3 ? pl : 0) * a.in_plane + asrc[j] + cc * KCH;
+        const unsigned short* src = inb + (long)(pl < NPL ? pl : 0) * a.in_plane + asrc[j] + cc * KCH;
         glds16(asrc[j] >= 0 ? (const float*)src : g_zero16, sA + i * 256);
       }
     }
@@ -1367,12 +1340,32 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
   int pcol[NT];   // packed column of this lane in tile nt
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
-    pcol[nt] = PRE || !ICLR17_D3_SKIP ? nt * 16 + (lane & 15) : d3_col(nt * 16 + (lane & 15));
+    pcol[nt] = !ICLR17_D3_SKIP ? nt * 16 + (lane & 15) : d3_col(nt * 16 + (lane & 15));
 
   auto compute = [&](int buf, int tap, auto ntt) {
     constexpr int NTT = decltype(ntt)::value;   // tiles this tap touches
     const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
     const float* sb = sB + buf * D3_SB + 2 * g * 48 * 4;
+    if constexpr (BF) {   // one bf16 product: weights rounded to nearest even, the bf16 plane
+      bf8 Bb[NTT];
+#pragma unroll
+      for (int nt = 0; nt < NTT; ++nt) {
+        const f4 w0 = *(const f4*)(sb + pcol[nt] * 4), w1 = *(const f4*)(sb + 48 * 4 + pcol[nt] * 4);
+        Bb[nt] = bf8{(__bf16)w0[0], (__bf16)w0[1], (__bf16)w0[2], (__bf16)w0[3],
+                     (__bf16)w1[0], (__bf16)w1[1], (__bf16)w1[2], (__bf16)w1[3]};
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int p = prow + (mt + dy) * D3_PS + dx;
+        const unsigned short* sa =
+            (const unsigned short*)(sA + p * 16 + ((g ^ (((p >> 2) & 1) << 1)) * 4));
+        const bf8 Ab = __builtin_bit_cast(bf8, *(const u4*)(sa));
+#pragma unroll
+        for (int nt = 0; nt < NTT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ab, Bb[nt], acc[mt][nt], 0, 0, 0);
+      }
+      return;
+    }
     bf8 Bh[NTT], Bm[NTT], Bl[NTT];
 #pragma unroll
     for (int nt = 0; nt < NTT; ++nt) {
@@ -1403,76 +1396,6 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
     }
   };
 
-  if constexpr (PRE) {
-    // Pre-split weights [3][9][CI/8][48][8] (the 16x16x32 B-fragment layout) read from L2 one
-    // step ahead: no B stage, no per-step split (the four waves no longer split the same B), and
-    // barriers only at chunk boundaries.
-    constexpr long WPL = 9L * CI * 48;   // plane stride (u16)
-    const unsigned short* gb = (const unsigned short*)a.w + ((lane >> 4) * 48 + (lane & 15)) * 8;
-    typedef const __attribute__((address_space(1))) u4* gu4p;   // global: no flat disambiguation
-    auto loadb = [&](int s, u4 (&bb)[3][NT]) {
-      const int cc = s / 9, tap = s - cc * 9;
-      const unsigned short* src = gb + ((long)tap * (CI / 8) + cc * 4) * 48 * 8;
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) bb[pl][nt] = *(gu4p)(src + pl * WPL + nt * 128);
-    };
-    typedef const __attribute__((address_space(3))) u4* lu4p;
-    const __attribute__((address_space(3))) float* sA3 =
-        (const __attribute__((address_space(3))) float*)sA;
-    auto compute_pre = [&](const u4 (&bb)[3][NT], int tap) {
-      const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const int p = prow + (mt + dy) * D3_PS + dx;
-        const int o = p * 16 + ((g ^ (((p >> 2) & 1) << 1)) * 4);   // floats
-        const bf8 Ah = __builtin_bit_cast(bf8, *(lu4p)(sA3 + o));
-        const bf8 Am = __builtin_bit_cast(bf8, *(lu4p)(sA3 + o + D3_PPX * 16));
-        const bf8 Al = __builtin_bit_cast(bf8, *(lu4p)(sA3 + o + 2 * D3_PPX * 16));
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-          const bf8 Bh = __builtin_bit_cast(bf8, bb[0][nt]), Bm = __builtin_bit_cast(bf8, bb[1][nt]),
-                    Bl = __builtin_bit_cast(bf8, bb[2][nt]);
-          f4 c = acc[mt][nt];
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al, Bh, c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bl, c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bm, c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bh, c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bm, c, 0, 0, 0);
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bh, c, 0, 0, 0);
-        }
-      }
-    };
-    u4 b0[3][NT], b1[3][NT];
-    issue_a(0);
-    loadb(0, b0);
-    for (int cc = 0; cc < NCH; ++cc) {
-      __syncthreads();   // this chunk's patch landed
-      // ping-pong B registers, one step ahead (written out: the register sets stay in VGPRs)
-      const int s0 = cc * 9;
-      const bool more = cc + 1 < NCH;
-      loadb(s0 + 1, b1); compute_pre(b0, 0);
-      loadb(s0 + 2, b0); compute_pre(b1, 1);
-      loadb(s0 + 3, b1); compute_pre(b0, 2);
-      loadb(s0 + 4, b0); compute_pre(b1, 3);
-      loadb(s0 + 5, b1); compute_pre(b0, 4);
-      loadb(s0 + 6, b0); compute_pre(b1, 5);
-      loadb(s0 + 7, b1); compute_pre(b0, 6);
-      loadb(s0 + 8, b0); compute_pre(b1, 7);
-      if (more) loadb(s0 + 9, b1);
-      compute_pre(b0, 8);
-      // tap 8 used b0; b1 holds the next chunk's tap 0
-      if (more) {
-        __syncthreads();   // every wave is done with this chunk's patch
-        issue_a(cc + 1);
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-          for (int nt = 0; nt < NT; ++nt) b0[pl][nt] = b1[pl][nt];
-      }
-    }
-  } else {
   issue_a(0);
   issue_b(0, 0);
   for (int s = 0; s < NSTEP; ++s) {
@@ -1490,7 +1413,6 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
       issue_a((s + 1) / 9);
       issue_b(s + 1, (s + 1) & 1);
     }
-  }
   }
   __syncthreads();     // stage reads done before the epilogue reuses LDS
 
@@ -2134,7 +2056,6 @@ struct SplitIO {
   long out_plane = 0;
   const unsigned short* gamma6 = nullptr;   // x6: split γ_eff for the GDN contraction
   const unsigned short* gammaT6 = nullptr;  // x6 backward: split transposed γ_eff
-  const unsigned short* w6 = nullptr;       // x6 conv3: pre-split weights
 };
 
 static void apply_split(EngineArgs& a, const SplitIO* x6) {
@@ -2143,7 +2064,6 @@ static void apply_split(EngineArgs& a, const SplitIO* x6) {
   a.out_split = x6->out; a.out_plane = x6->out_plane;
   a.ggamma6 = x6->gamma6;
   a.ggammaT6 = x6->gammaT6;
-  a.w6 = x6->w6;
 }
 
 template <int N, int EPI = EPI_GDN>
@@ -2200,10 +2120,7 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
     constexpr int WN = (BN / 16) % 4 == 0 ? 4 : 2, WM = 4 / WN;
     a.partials_per_image = a.tiles_x * a.tiles_y * (N / BN);
     dim3 grid(a.tiles_x * a.tiles_y * B, N / BN);
-    if (X6in && a.w6 != nullptr && ICLR17_W3SPLIT)
-      hipLaunchKernelGGL((engine_kernel<N, N, BN, WM, WN, EPI_QUANT, false, true, true>), grid,
-                         dim3(256), 0, st, a);
-    else if (X6in)
+    if (X6in)
       hipLaunchKernelGGL((engine_kernel<N, N, BN, WM, WN, EPI_QUANT, false, true>), grid,
                          dim3(256), 0, st, a);
     else
@@ -2424,22 +2341,21 @@ int iclr17_synthesis_deconv_igdn(const float* in, int B, int h, int w, int N,
                   : launch_deconv5<128>(in, B, h, w, w_packed, bias, beta_eff, gamma_packed, out, pre_out, S(stream));
 }
 
-int iclr17_synthesis_deconv3_x6(const uint16_t* in_split, int B, int H, int W, int N,
-                                const float* w_packed, const uint16_t* w_split, const float* bias,
-                                const float* x, float* clipped, float* recon,
-                                double* sse_partial, int sse_unclipped, void* stream) {
+static int launch_deconv3_halo(const uint16_t* in, int B, int H, int W, int N, const float* w_packed,
+                               const float* bias, const float* x, float* clipped, float* recon,
+                               double* sse_partial, int sse_unclipped, void* stream, bool bf) {
+  const char* what = bf ? "deconv3_bf16" : "deconv3_x6";
   int rc = check_dims(B, H, W, N);
   if (rc) return rc;
-  ICLR17_REQUIRE(in_split && (w_packed || w_split) && bias && clipped, ICLR17_EINVAL,
-                 "deconv3_x6: null pointer");
+  ICLR17_REQUIRE(in && w_packed && bias && clipped, ICLR17_EINVAL, "%s: null pointer", what);
   ICLR17_REQUIRE(x == nullptr || sse_partial != nullptr, ICLR17_EINVAL,
-                 "deconv3_x6: sse_partial required with x");
+                 "%s: sse_partial required with x", what);
   ICLR17_REQUIRE(!sse_unclipped || recon != nullptr, ICLR17_EINVAL,
-                 "deconv3_x6: the unclipped SSE needs the recon output");
+                 "%s: the unclipped SSE needs the recon output", what);
   EngineArgs a;
   memset(&a, 0, sizeof(a));
   a.sse_unclipped = sse_unclipped;
-  a.in_split = (const unsigned short*)in_split;
+  a.in_split = (const unsigned short*)in;
   a.w = w_packed; a.bias = bias; a.out = clipped; a.recon = recon; a.xref = x;
   a.partial = sse_partial;
   a.B = B; a.Hin = H / 4; a.Win = W / 4; a.Hout = H; a.Wout = W;
@@ -2448,19 +2364,34 @@ int iclr17_synthesis_deconv3_x6(const uint16_t* in_split, int B, int H, int W, i
   a.tiles_y = (a.gh + D3_BS - 1) / D3_BS; a.tiles_x = (a.gw + D3_BS - 1) / D3_BS;
   a.partials_per_image = ((a.gh + 7) / 8) * ((a.gw + 7) / 8);
   dim3 grid(a.tiles_x * a.tiles_y * B);
-  if (w_split != nullptr) {   // pre-split weights read from L2 (no B stage, no in-loop split)
-    a.w = (const float*)w_split;
+  if (bf) {
     if (N == 192)
       hipLaunchKernelGGL((deconv3_x6_kernel<192, true>), grid, dim3(256), 0, S(stream), a);
     else
       hipLaunchKernelGGL((deconv3_x6_kernel<128, true>), grid, dim3(256), 0, S(stream), a);
-    return check_launch("deconv3_x6");
+  } else {
+    if (N == 192)
+      hipLaunchKernelGGL((deconv3_x6_kernel<192>), grid, dim3(256), 0, S(stream), a);
+    else
+      hipLaunchKernelGGL((deconv3_x6_kernel<128>), grid, dim3(256), 0, S(stream), a);
   }
-  if (N == 192)
-    hipLaunchKernelGGL((deconv3_x6_kernel<192>), grid, dim3(256), 0, S(stream), a);
-  else
-    hipLaunchKernelGGL((deconv3_x6_kernel<128>), grid, dim3(256), 0, S(stream), a);
-  return check_launch("deconv3_x6");
+  return check_launch(what);
+}
+
+int iclr17_synthesis_deconv3_x6(const uint16_t* in_split, int B, int H, int W, int N,
+                                const float* w_packed, const float* bias, const float* x,
+                                float* clipped, float* recon, double* sse_partial,
+                                int sse_unclipped, void* stream) {
+  return launch_deconv3_halo(in_split, B, H, W, N, w_packed, bias, x, clipped, recon, sse_partial,
+                             sse_unclipped, stream, false);
+}
+
+int iclr17_synthesis_deconv3_bf16(const uint16_t* in, int B, int H, int W, int N,
+                                  const float* w_packed, const float* bias, const float* x_ref,
+                                  float* clipped, float* recon, double* sse_partial,
+                                  int sse_unclipped, void* stream) {
+  return launch_deconv3_halo(in, B, H, W, N, w_packed, bias, x_ref, clipped, recon, sse_partial,
+                             sse_unclipped, stream, true);
 }
 
 int iclr17_output_partials_per_image(int H, int W) {
@@ -2567,14 +2498,13 @@ int iclr17_analysis_conv2_gdn_x6(const uint16_t* in_split, int B, int H, int W, 
 }
 
 int iclr17_analysis_conv3_quant_rate_x6(const uint16_t* in_split, int B, int H, int W, int N,
-                                        const float* w_packed, const uint16_t* w_split,
-                                        int quant_mode, const float* noise,
+                                        const float* w_packed, int quant_mode, const float* noise,
                                         const float* rate_packed, float* y_out, float* y_hat,
                                         uint16_t* y_hat_split, double* bits_partial,
                                         void* stream) {
   int rc = check_dims(B, H, W, N);
   if (rc) return rc;
-  ICLR17_REQUIRE(in_split && (w_packed || w_split) && rate_packed && y_hat && bits_partial,
+  ICLR17_REQUIRE(in_split && w_packed && rate_packed && y_hat && bits_partial,
                  ICLR17_EINVAL, "conv3_quant_rate_x6: null pointer");
   ICLR17_REQUIRE(quant_mode == ICLR17_QUANT_ROUND || (quant_mode == ICLR17_QUANT_NOISE && noise),
                  ICLR17_EINVAL, "conv3_quant_rate_x6: bad quant mode %d / missing noise", quant_mode);
@@ -2584,7 +2514,6 @@ int iclr17_analysis_conv3_quant_rate_x6(const uint16_t* in_split, int B, int H, 
   io.in_plane = (long)B * h * w * N;
   io.out = (unsigned short*)y_hat_split;
   io.out_plane = (long)B * (h / 2) * (w / 2) * N;
-  io.w6 = (const unsigned short*)w_split;
   return N == 192 ? launch_conv5<192, EPI_QUANT>(nullptr, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io)
                   : launch_conv5<128, EPI_QUANT>(nullptr, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io);
 }

@@ -249,13 +249,15 @@ def deconv_igdn(h: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Tenso
 
 
 # ------------------------------------------------------------- x6 (bf16x6) precision mode
-PRECISIONS = ("x6", "fp32")
+PRECISIONS = ("x6", "fp32", "bf16")
 _precision = os.environ.get("ICLR17_PRECISION", "x6")
 
 
 def precision() -> str:
     """Inference contraction mode: "x6" (bf16x6 split products on the bf16 MFMA, fp32-accurate;
-    default) or "fp32" (exact-f32 MFMA products). Training kernels are fp32 in both."""
+    default), "fp32" (exact-f32 MFMA products) or "bf16" (the throughput mode: bf16 activations
+    and weights, one bf16 product per MAC, fp32 accumulation — no parity claim). Training runs
+    the x6 kernels in the x6 and bf16 modes and exact f32 in the fp32 mode."""
     if _precision not in PRECISIONS:
         raise Iclr17Error(f"iclr17: ICLR17_PRECISION must be one of {PRECISIONS} (got {_precision!r})")
     return _precision
@@ -372,12 +374,10 @@ def conv2_gdn_x6(hs: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Ten
     return split, out, pre
 
 
-def conv3_quant_rate_x6(hs: Tensor, wp: Optional[Tensor], rate_packed: Tensor,
-                        noise: Optional[Tensor] = None, want_y: bool = False,
-                        w_split: Optional[Tensor] = None):
+def conv3_quant_rate_x6(hs: Tensor, wp: Tensor, rate_packed: Tensor,
+                        noise: Optional[Tensor] = None, want_y: bool = False):
     """conv3_quant_rate on a split-form input. Returns (y_hat, bits_partial, y | None,
-    y_hat_split). ``w_split`` (``split_conv5``) lets the kernel stage pre-split weight planes
-    instead of splitting ``wp`` in the loop (bitwise the same result)."""
+    y_hat_split)."""
     _check_split(hs, "activation")
     _, B, h8, w8, N = hs.shape
     _check_channels(N)
@@ -395,19 +395,9 @@ def conv3_quant_rate_x6(hs: Tensor, wp: Optional[Tensor], rate_packed: Tensor,
     y = torch.empty_like(y_hat) if want_y else None
     T = rate_partials_per_image(H, W, N)
     partial = torch.empty(B, T, device=hs.device, dtype=torch.float64)
-    if wp is None and w_split is None:
-        raise Iclr17Error("iclr17: conv3_quant_rate_x6 needs wp or w_split")
-    if w_split is not None and (w_split.dtype != torch.int16 or w_split.numel() != 3 * 25 * N * N):
-        raise Iclr17Error(f"iclr17: conv3 w_split must be int16 [3, 25*{N}*{N}] (split_conv5)")
-    call("iclr17_analysis_conv3_quant_rate_x6", _p(hs), B, H, W, N, _p(wp), _p(w_split), mode,
-         _p(noise),
+    call("iclr17_analysis_conv3_quant_rate_x6", _p(hs), B, H, W, N, _p(wp), mode, _p(noise),
          _p(rate_packed), _p(y), _p(y_hat), _p(y_hat_split), _p(partial), _stream(hs))
     return y_hat, partial, y, y_hat_split
-
-
-def split_conv5(wp: Tensor, N: int) -> Tensor:
-    """The conv5 packing [25][N/4][N][4] → split planes for conv3_quant_rate_x6's w_split."""
-    return split_packed(wp, 25, N, N)
 
 
 def deconv_igdn_x6(hs: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Tensor,
@@ -495,15 +485,17 @@ def deconv3(h: Tensor, wp: Tensor, bias: Tensor, x_ref: Optional[Tensor] = None,
     return clipped, recon, partial
 
 
-def deconv3_x6(hs: Tensor, wp: Optional[Tensor], bias: Tensor, x_ref: Optional[Tensor] = None,
-               want_recon: bool = False, sse_unclipped: bool = False,
-               w_split: Optional[Tensor] = None):
+def deconv3_x6(hs: Tensor, wp: Tensor, bias: Tensor, x_ref: Optional[Tensor] = None,
+               want_recon: bool = False, sse_unclipped: bool = False):
     """deconv3 on a split-form input [3,B,H/4,W/4,N] (the halo-tiled x6 kernel); the same
-    returns as ``deconv3``. ``w_split`` (``split_deconv3``) lets the kernel read pre-split weight
-    fragments from L2 instead of splitting the packed weights in its loop: bit-identical, but
-    measured 7 % slower (VGPR pressure), so the model does not use it."""
+    returns as ``deconv3``."""
     _check_split(hs, "activation")
     _, B, h4, w4, N = hs.shape
+    return _deconv3_halo("iclr17_synthesis_deconv3_x6", hs, B, h4, w4, N, wp, bias, x_ref,
+                         want_recon, sse_unclipped)
+
+
+def _deconv3_halo(fn, hs, B, h4, w4, N, wp, bias, x_ref, want_recon, sse_unclipped):
     _check_channels(N)
     H, W = 4 * h4, 4 * w4
     _check_image_dims(H, W)
@@ -516,14 +508,126 @@ def deconv3_x6(hs: Tensor, wp: Optional[Tensor], bias: Tensor, x_ref: Optional[T
             raise Iclr17Error("iclr17: reference image shape mismatch")
         x_ref = x_ref.contiguous()
         partial = torch.empty(B, output_partials_per_image(H, W), device=hs.device, dtype=torch.float64)
-    call("iclr17_synthesis_deconv3_x6", _p(hs), B, H, W, N, _p(wp), _p(w_split), _p(bias),
-         _p(x_ref), _p(clipped), _p(recon), _p(partial), int(sse_unclipped), _stream(hs))
+    call(fn, _p(hs), B, H, W, N, _p(wp), _p(bias), _p(x_ref), _p(clipped), _p(recon),
+         _p(partial), int(sse_unclipped), _stream(hs))
     return clipped, recon, partial
 
 
-def split_deconv3(wp: Tensor, N: int) -> Tensor:
-    """The deconv3 all-phase packing [9][N/4][48][4] → split planes for deconv3_x6's w_split."""
-    return split_packed(wp, 9, N, 48)
+# ------------------------------------------------------------ bf16 throughput precision mode
+# A bf16 activation is an int16 tensor [B, h, w, N] holding the bf16 bit patterns (round to
+# nearest even) of an NHWC activation; the bf16 kernels (csrc/engine_bf16.hip) read and write it.
+def _check_bf16(t: Tensor, what: str):
+    if not isinstance(t, Tensor) or t.dtype != torch.int16 or t.dim() != 4:
+        raise Iclr17Error(f"iclr17: {what} must be a bf16-pattern int16 NHWC tensor [B,h,w,N]")
+    if not t.is_cuda:
+        raise Iclr17Error(f"iclr17: {what} must be a device tensor (there is no CPU path)")
+    if not t.is_contiguous():
+        raise Iclr17Error(f"iclr17: {what} must be contiguous")
+
+
+def to_bf16(x: Tensor) -> Tensor:
+    """fp32 → bf16 bit patterns (int16, same shape), round to nearest even."""
+    _check(x, "tensor", x.dim())
+    x = x.contiguous()
+    out = torch.empty(x.shape, device=x.device, dtype=torch.int16)
+    if x.numel() % 8:
+        raise Iclr17Error("iclr17: to_bf16 needs a multiple of 8 elements")
+    call("iclr17_to_bf16", _p(x), x.numel(), _p(out), _stream(x))
+    return out
+
+
+def from_bf16(t: Tensor) -> Tensor:
+    """bf16 bit patterns (int16) → fp32 (exact; torch ops, a test/debug helper)."""
+    return ((t.to(torch.int32) & 0xFFFF) << 16).view(torch.float32)
+
+
+def pack_bf16(which: int, w: Tensor, N: int) -> Tensor:
+    """k5 weights → the bf16 engine's step layout (ICLR17_BF_CONV5 / ICLR17_BF_DECONV5)."""
+    _check(w, "weight", 4)
+    size = query("iclr17_bf16_weight_size", which, N)
+    if size == 0:
+        raise Iclr17Error(f"iclr17: pack_bf16: kind {which}, N={N} unsupported")
+    out = torch.empty(size, device=w.device, dtype=torch.int16)
+    call("iclr17_pack_bf16", which, _p(w.detach().contiguous()), _p(out), N, _stream(w))
+    return out
+
+
+def round_packed(packed: Tensor, taps: int, K: int, N: int) -> Tensor:
+    """Packed fp32 [taps][K/4][N][4] → bf16 fragments [taps][K/8][N][8] (round to nearest even)."""
+    _check(packed, "packed operand", packed.dim())
+    if packed.numel() != taps * K * N:
+        raise Iclr17Error(f"iclr17: round_packed: {packed.numel()} != {taps}*{K}*{N}")
+    out = torch.empty(taps * K * N, device=packed.device, dtype=torch.int16)
+    call("iclr17_round_packed", _p(packed), taps, K, N, _p(out), _stream(packed))
+    return out
+
+
+def conv1_gdn_bf16(x: Tensor, w_bf: Tensor, bias: Tensor, beta_eff: Tensor, g_bf: Tensor,
+                   N: int) -> Tensor:
+    """analysis_17.py:14-17 in bf16: x NCHW fp32 → bf16 NHWC [B,H/4,W/4,N]. w_bf: round_packed
+    of the ICLR17_W_CONV1_X6 packing (1, 256, N); g_bf: round_packed of γ's gp (1, N, N)."""
+    _check(x, "image", 4)
+    B, C, H, W = x.shape
+    if C != 3:
+        raise Iclr17Error(f"iclr17: the analysis transform takes 3-channel images (got {C})")
+    _check_image_dims(H, W)
+    _check_channels(N)
+    out = torch.empty(B, H // 4, W // 4, N, device=x.device, dtype=torch.int16)
+    call("iclr17_analysis_conv1_gdn_bf16", _p(x.contiguous()), B, H, W, N, _p(w_bf), _p(bias),
+         _p(beta_eff), _p(g_bf), _p(out), _stream(x))
+    return out
+
+
+def conv2_gdn_bf16(h: Tensor, w_bf: Tensor, bias: Tensor, beta_eff: Tensor, g_bf: Tensor) -> Tensor:
+    """analysis_17.py:18-21 in bf16: bf16 NHWC [B,H/4,W/4,N] → [B,H/8,W/8,N]."""
+    _check_bf16(h, "activation")
+    B, h4, w4, N = h.shape
+    _check_channels(N)
+    H, W = 4 * h4, 4 * w4
+    _check_image_dims(H, W)
+    out = torch.empty(B, h4 // 2, w4 // 2, N, device=h.device, dtype=torch.int16)
+    call("iclr17_analysis_conv2_gdn_bf16", _p(h), B, H, W, N, _p(w_bf), _p(bias), _p(beta_eff),
+         _p(g_bf), _p(out), _stream(h))
+    return out
+
+
+def conv3_quant_rate_bf16(h: Tensor, w_bf: Tensor, rate_packed: Tensor, want_y: bool = False):
+    """analysis_17.py:22 + model.py:56,71-73 (round mode) in bf16 → (ŷ fp32 NHWC, bits partials
+    [B,T] float64, y fp32 | None, ŷ bf16 NHWC)."""
+    _check_bf16(h, "activation")
+    B, h8, w8, N = h.shape
+    _check_channels(N)
+    H, W = 8 * h8, 8 * w8
+    _check_image_dims(H, W)
+    y_hat = torch.empty(B, h8 // 2, w8 // 2, N, device=h.device, dtype=torch.float32)
+    y_hat_bf = torch.empty(B, h8 // 2, w8 // 2, N, device=h.device, dtype=torch.int16)
+    y = torch.empty_like(y_hat) if want_y else None
+    T = query("iclr17_bf16_rate_partials_per_image", H, W, N)
+    partial = torch.empty(B, T, device=h.device, dtype=torch.float64)
+    call("iclr17_analysis_conv3_quant_rate_bf16", _p(h), B, H, W, N, _p(w_bf), _p(rate_packed),
+         _p(y), _p(y_hat), _p(y_hat_bf), _p(partial), _stream(h))
+    return y_hat, partial, y, y_hat_bf
+
+
+def deconv_igdn_bf16(h: Tensor, w_bf: Tensor, bias: Tensor, beta_eff: Tensor, g_bf: Tensor) -> Tensor:
+    """synthesis_17.py:15-22 in bf16: bf16 NHWC [B,h,w,N] → [B,2h,2w,N]."""
+    _check_bf16(h, "activation")
+    B, hh, ww, N = h.shape
+    _check_channels(N)
+    out = torch.empty(B, 2 * hh, 2 * ww, N, device=h.device, dtype=torch.int16)
+    call("iclr17_synthesis_deconv_igdn_bf16", _p(h), B, hh, ww, N, _p(w_bf), _p(bias),
+         _p(beta_eff), _p(g_bf), _p(out), _stream(h))
+    return out
+
+
+def deconv3_bf16(h: Tensor, wp: Tensor, bias: Tensor, x_ref: Optional[Tensor] = None,
+                 want_recon: bool = False, sse_unclipped: bool = False):
+    """synthesis_17.py:23-25 + model.py:59 in bf16: bf16 NHWC [B,H/4,W/4,N] → the ``deconv3``
+    returns (wp: the fp32 ICLR17_W_DECONV9 packing, rounded to bf16 in the kernel)."""
+    _check_bf16(h, "activation")
+    B, h4, w4, N = h.shape
+    return _deconv3_halo("iclr17_synthesis_deconv3_bf16", h, B, h4, w4, N, wp, bias, x_ref,
+                         want_recon, sse_unclipped)
 
 
 # ---------------------------------------------------------------- entropy coding (§8 f4)
@@ -926,7 +1030,7 @@ def gdn_wgrad(dn: Tensor, u: Tensor, x6: Optional[bool] = None) -> Tensor:
     C = dn.shape[-1]
     P = dn.numel() // C
     if x6 is None:
-        x6 = precision() == "x6"
+        x6 = precision() != "fp32"
     name = "iclr17_gdn_wgrad_x6" if x6 else "iclr17_gdn_wgrad"
     ws = torch.empty(query(name + "_workspace_size", P, C), device=dn.device, dtype=torch.float32)
     dge = torch.empty(C, C, device=dn.device, dtype=torch.float32)

@@ -68,7 +68,8 @@ class ImageCompressor(nn.Module):
         q = self.encode_latents(x, noise, training, want_y)
         y_hat, bits_partial, y_split = q["y_hat"], q["bits_partial"], q["y_split"]
         clipped, recon, sse_partial = self.Decoder.decode(y_hat, x_ref=x if x_ref_sse else None,
-                                                          want_recon=want_recon, y_split=y_split)
+                                                          want_recon=want_recon, y_split=y_split,
+                                                          y_bf16=q.get("y_bf16"))
         return {"clipped": clipped, "y_hat": y_hat, "bits_partial": bits_partial,
                 "sse_partial": sse_partial, "recon": recon, "y": q["y"]}
 
@@ -84,7 +85,17 @@ class ImageCompressor(nn.Module):
         x = x.contiguous()
         w1, w2, w3, g1, g2 = self.Encoder.packed()
         N = self.out_channel_N
-        if kernels.precision() == "x6":
+        if kernels.precision() == "bf16" and noise is None:
+            # the throughput mode: bf16 activations and weights, one bf16 product per MAC
+            w1b, w2b, w3b = self.Encoder.packed_bf16()
+            e1 = self.Encoder.gdn1.effective_params_bf16()
+            e2 = self.Encoder.gdn2.effective_params_bf16()
+            h = kernels.conv1_gdn_bf16(x, w1b, self.Encoder.conv1.bias, *e1, N)
+            h = kernels.conv2_gdn_bf16(h, w2b, self.Encoder.conv2.bias, *e2)
+            y_hat, bits, y, ybf = kernels.conv3_quant_rate_bf16(h, w3b, self.bitEstimator.packed(),
+                                                                want_y=want_y)
+            return {"y_hat": y_hat, "bits_partial": bits, "y_split": None, "y_bf16": ybf, "y": y}
+        if kernels.precision() != "fp32":
             e1 = self.Encoder.gdn1.effective_params_x6()
             e2 = self.Encoder.gdn2.effective_params_x6()
             hs, _, _ = kernels.conv1x6_gdn(x, self.Encoder.packed_conv1_x6(), self.Encoder.conv1.bias,
@@ -176,7 +187,8 @@ class ImageCompressor(nn.Module):
         y_hat = kernels.rans_decode(words, offsets, self.bitEstimator.entropy_tables(K), B, h, w, N,
                                     K, P)
         split = kernels.split_planes(y_hat) if kernels.precision() == "x6" else None
-        clipped, _, _ = self.Decoder.decode(y_hat, want_recon=False, y_split=split)
+        ybf = kernels.to_bf16(y_hat) if kernels.precision() == "bf16" else None
+        clipped, _, _ = self.Decoder.decode(y_hat, want_recon=False, y_split=split, y_bf16=ybf)
         return {"y_hat": y_hat.permute(0, 3, 1, 2), "x_hat": clipped}
 
     @torch.no_grad()
@@ -206,8 +218,13 @@ class ImageCompressor(nn.Module):
         """Build (or refresh) every derived parameter layout ``run`` reads (with ``backward``
         also those of the training backward) on the current stream, the stale ones as one
         batched packing launch pair (kernels.batched_packs)."""
-        x6 = kernels.precision() == "x6"
+        x6 = kernels.precision() != "fp32"
         gdns = (self.Encoder.gdn1, self.Encoder.gdn2, self.Decoder.igdn1, self.Decoder.igdn2)
+        if kernels.precision() == "bf16" and not backward:
+            self.Encoder.packed_bf16()
+            self.Decoder.packed_bf16()
+            for g in gdns:
+                g.effective_params_bf16()
         with kernels.batched_packs():
             self.Encoder.packed()
             self.Decoder.packed()

@@ -80,6 +80,15 @@ class GDN(nn.Module):
                             lambda: kernels.split_packed(gp, 1, C, C), force=force)
         return be, gp, g6
 
+    def effective_params_bf16(self, force: bool = False):
+        """(beta_eff, γ_eff rounded to bf16 in the 16x16x32 fragment layout) for the bf16
+        throughput kernels."""
+        be, gp = self.effective_params(force)
+        C = self.beta.shape[0]
+        gb = self._pack.get("gdnbf", (self.beta, self.gamma),
+                            lambda: kernels.round_packed(gp, 1, C, C), force=force)
+        return be, gb
+
     def effective_params_bwd(self):
         """(beta_eff, gamma_packed, gamma_packed_transposed) for the backward kernels."""
         return self._packed_all()

@@ -55,12 +55,19 @@ class Analysis_net_17(nn.Module):
                               lambda: kernels.pack_conv1_x6(self.conv1.weight, N),
                               force)
 
-    def packed_conv3_x6(self, force: bool = False):
-        """conv3's packed weights split for the x6 kernel (kernels.split_conv5), cached."""
-        N = self.out_channel_N
-        return self._pack.get("w3x6", (self.conv3.weight,),
-                              lambda: kernels.split_conv5(self.packed(force)[2], N),
-                              force)
+    def packed_bf16(self, force: bool = False):
+        """The bf16 throughput-mode weights (conv1 in the reordered-K fragment layout, conv2 and
+        conv3 in the bf16 engine's step layout), cached until the weights change."""
+        N, f = self.out_channel_N, force
+        w1 = self._pack.get("w1bf", (self.conv1.weight,),
+                            lambda: kernels.round_packed(
+                                kernels.pack_weight(_lib.ICLR17_W_CONV1_X6, self.conv1.weight, N),
+                                1, 256, N), f)
+        w2 = self._pack.get("w2bf", (self.conv2.weight,),
+                            lambda: kernels.pack_bf16(_lib.ICLR17_BF_CONV5, self.conv2.weight, N), f)
+        w3 = self._pack.get("w3bf", (self.conv3.weight,),
+                            lambda: kernels.pack_bf16(_lib.ICLR17_BF_CONV5, self.conv3.weight, N), f)
+        return w1, w2, w3
 
     def packed_bwd(self):
         """conv3 / conv2 weights packed as the transposed convolutions of their input gradients
@@ -87,4 +94,12 @@ class Analysis_net_17(nn.Module):
                 raise kernels.Iclr17Error("iclr17: gradients w.r.t. the input image are not implemented")
             return AnalysisFn.apply(x.contiguous(), self, *params)
         _, _, w3, _, _ = self.packed()
+        if kernels.precision() == "bf16":
+            w1b, w2b, w3b = self.packed_bf16()
+            e1, e2 = self.gdn1.effective_params_bf16(), self.gdn2.effective_params_bf16()
+            h = kernels.conv1_gdn_bf16(x.contiguous(), w1b, self.conv1.bias, *e1, self.out_channel_N)
+            h = kernels.conv2_gdn_bf16(h, w2b, self.conv2.bias, *e2)
+            be = torch.zeros(11 * self.out_channel_N, device=x.device)   # rate unused: y only
+            y = kernels.conv3_quant_rate_bf16(h, w3b, be, want_y=True)[2]
+            return y.permute(0, 3, 1, 2)
         return kernels.conv3(self.features(x), w3).permute(0, 3, 1, 2)

@@ -47,12 +47,14 @@ class Synthesis_net_17(nn.Module):
                             lambda: kernels.pack_weight(_lib.ICLR17_W_DECONV9, self.deconv3.weight, N), f)
         return d1, d2, d3, self.igdn1.effective_params(force), self.igdn2.effective_params(force)
 
-    def packed_deconv3_x6(self, force: bool = False):
-        """deconv3's packed weights split for the x6 kernel (kernels.split_deconv3), cached."""
-        N = self.out_channel_N
-        return self._pack.get("d3x6", (self.deconv3.weight,),
-                              lambda: kernels.split_deconv3(self.packed(force)[2], N),
-                              force)
+    def packed_bf16(self, force: bool = False):
+        """deconv1 / deconv2 in the bf16 engine's step layout (4 stride phases), cached."""
+        N, f = self.out_channel_N, force
+        d1 = self._pack.get("d1bf", (self.deconv1.weight,),
+                            lambda: kernels.pack_bf16(_lib.ICLR17_BF_DECONV5, self.deconv1.weight, N), f)
+        d2 = self._pack.get("d2bf", (self.deconv2.weight,),
+                            lambda: kernels.pack_bf16(_lib.ICLR17_BF_DECONV5, self.deconv2.weight, N), f)
+        return d1, d2
 
     def packed_bwd(self, x6: bool):
         """The deconv weights packed as the convolutions of their input gradients: (deconv3 in
@@ -77,10 +79,17 @@ class Synthesis_net_17(nn.Module):
         the latent is already channels-last, e.g. the Encoder's own output)."""
         return y.permute(0, 2, 3, 1).contiguous()
 
-    def decode(self, y_nhwc, x_ref=None, want_recon=True, y_split=None):
+    def decode(self, y_nhwc, x_ref=None, want_recon=True, y_split=None, y_bf16=None):
         """NHWC latent → (clipped NCHW, unclipped NCHW | None, SSE partials | None).
-        With ``y_split`` (the latent in x6 split form) the three layers run in the x6 mode."""
+        With ``y_split`` (the latent in x6 split form) the three layers run in the x6 mode, with
+        ``y_bf16`` (bf16 bit patterns) in the bf16 throughput mode."""
         d1, d2, d3, g1, g2 = self.packed()
+        if y_bf16 is not None:
+            b1, b2 = self.packed_bf16()
+            q1, q2 = self.igdn1.effective_params_bf16(), self.igdn2.effective_params_bf16()
+            h = kernels.deconv_igdn_bf16(y_bf16, b1, self.deconv1.bias, *q1)
+            h = kernels.deconv_igdn_bf16(h, b2, self.deconv2.bias, *q2)
+            return kernels.deconv3_bf16(h, d3, self.deconv3.bias, x_ref=x_ref, want_recon=want_recon)
         if y_split is not None:
             q1, q2 = self.igdn1.effective_params_x6(), self.igdn2.effective_params_x6()
             hs, _, _ = kernels.deconv_igdn_x6(y_split, d1, self.deconv1.bias, *q1)
@@ -102,5 +111,6 @@ class Synthesis_net_17(nn.Module):
             return SynthesisFn.apply(x, self, *params)
         y = self.to_nhwc(x)
         split = kernels.split_planes(y) if kernels.precision() == "x6" else None
-        _, recon, _ = self.decode(y, want_recon=True, y_split=split)
+        ybf = kernels.to_bf16(y) if kernels.precision() == "bf16" else None
+        _, recon, _ = self.decode(y, want_recon=True, y_split=split, y_bf16=ybf)
         return recon

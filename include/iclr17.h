@@ -178,12 +178,9 @@ int iclr17_analysis_conv2_gdn_x6(const uint16_t* in_split, int B, int H, int W, 
                                  const float* gamma_packed, const uint16_t* gamma_split,
                                  float* out, uint16_t* out_split, float* pre_out, void* stream);
 /* iclr17_analysis_conv3_quant_rate on a split-form input; ŷ also in split form (nullable).
- * w_split (nullable: then w_packed, split in the loop) is w_packed split by
- * iclr17_split_packed(taps = 25, K = N, N = N): the kernel then stages the weight planes as
- * they are and splits nothing. One of w_packed / w_split must be non-NULL. */
+ * The packed fp32 weights are split in the loop. */
 int iclr17_analysis_conv3_quant_rate_x6(const uint16_t* in_split, int B, int H, int W, int N,
-                                        const float* w_packed, const uint16_t* w_split,
-                                        int quant_mode, const float* noise,
+                                        const float* w_packed, int quant_mode, const float* noise,
                                         const float* rate_packed, float* y_out, float* y_hat,
                                         uint16_t* y_hat_split, double* bits_partial,
                                         void* stream);
@@ -194,13 +191,12 @@ int iclr17_synthesis_deconv_igdn_x6(const uint16_t* in_split, int B, int h, int 
                                     const uint16_t* gamma_split, float* out, uint16_t* out_split,
                                     float* pre_out, void* stream);
 /* iclr17_synthesis_deconv3 on a split-form input (the same outputs and sse_partial layout:
- * iclr17_output_partials_per_image(H, W) doubles per image). w_split (nullable: then w_packed,
- * split in the loop) is w_packed split by iclr17_split_packed(taps = 9, K = N, N = 48): the
- * kernel then reads the weight fragments from L2 and splits nothing. */
+ * iclr17_output_partials_per_image(H, W) doubles per image); the packed fp32 weights are split
+ * in the loop. */
 int iclr17_synthesis_deconv3_x6(const uint16_t* in_split, int B, int H, int W, int N,
-                                const float* w_packed, const uint16_t* w_split, const float* bias,
-                                const float* x, float* clipped, float* recon,
-                                double* sse_partial, int sse_unclipped, void* stream);
+                                const float* w_packed, const float* bias, const float* x,
+                                float* clipped, float* recon, double* sse_partial,
+                                int sse_unclipped, void* stream);
 
 /* ---------------------------------------------------------------- entropy coding (§8 f4)
  * A real bitstream for ŷ with the factorised model the reference only uses to ESTIMATE the rate
@@ -414,6 +410,49 @@ int iclr17_rate_param_grad(const float* partial, int T, int C, const float* h1, 
                            const float* h4, float* dh1, float* db1, float* da1, float* dh2,
                            float* db2, float* da2, float* dh3, float* db3, float* da3, float* dh4,
                            float* db4, void* stream);
+
+/* ------------------------------------------------------------------ bf16 throughput mode
+ * The codec forward with bf16 activations (NHWC [B][h][w][N], round to nearest even), bf16
+ * weights and γ, ONE v_mfma_f32_16x16x32_bf16 product per MAC with fp32 accumulation, fp32
+ * epilogues (csrc/engine_bf16.hip). Same layers and arguments as the fp32 / x6 entry points
+ * above; no bit-identity claim (flip rate, Δbpp and ΔPSNR are reported instead).
+ * Weight layouts: iclr17_pack_bf16 (k5 layers), iclr17_round_packed of the fp32 packings
+ * (conv1: ICLR17_W_CONV1_X6 with taps 1, K 256; GDN γ: iclr17_pack_gdn's gp with taps 1, K = N). */
+#define ICLR17_BF_CONV5 32   /* conv2/conv3 W[co][ci][5][5] → [N/16][13][4][N][8] bf16 */
+#define ICLR17_BF_DECONV5 33 /* deconv1/2 W[ci][co][5][5] → 4 phases [N/16][S_p][4][N][8] bf16 */
+size_t iclr17_bf16_weight_size(int which, int N);   /* uint16 elements; 0 = unsupported */
+int iclr17_pack_bf16(int which, const float* w, uint16_t* out, int N, void* stream);
+/* packed fp32 [taps][K/4][N][4] → bf16 [taps][K/8][N][8] (round to nearest even) */
+int iclr17_round_packed(const float* packed, int taps, int K, int N, uint16_t* out, void* stream);
+/* fp32 → bf16 (round to nearest even), n a multiple of 8 */
+int iclr17_to_bf16(const float* x, long n, uint16_t* out, void* stream);
+/* analysis_17.py:14-17 conv1 + GDN1: x NCHW fp32 → out bf16 NHWC [B,H/4,W/4,N] */
+int iclr17_analysis_conv1_gdn_bf16(const float* x, int B, int H, int W, int N,
+                                   const uint16_t* w_bf16, const float* bias,
+                                   const float* beta_eff, const uint16_t* gamma_bf16,
+                                   uint16_t* out, void* stream);
+/* analysis_17.py:18-21 conv2 + GDN2: bf16 NHWC [B,H/4,W/4,N] → bf16 NHWC [B,H/8,W/8,N] */
+int iclr17_analysis_conv2_gdn_bf16(const uint16_t* in, int B, int H, int W, int N,
+                                   const uint16_t* w_bf16, const float* bias, const float* beta_eff,
+                                   const uint16_t* gamma_bf16, uint16_t* out, void* stream);
+/* analysis_17.py:22 + model.py:56,71-73 (round mode): → ŷ fp32 NHWC, ŷ bf16 NHWC, optional y
+ * fp32 NHWC, bit partials [B][iclr17_bf16_rate_partials_per_image] (float64) */
+int iclr17_bf16_rate_partials_per_image(int H, int W, int N);
+int iclr17_analysis_conv3_quant_rate_bf16(const uint16_t* in, int B, int H, int W, int N,
+                                          const uint16_t* w_bf16, const float* rate_packed,
+                                          float* y_out, float* y_hat, uint16_t* y_hat_bf16,
+                                          double* bits_partial, void* stream);
+/* synthesis_17.py:15-22 deconv + IGDN: bf16 NHWC [B,h,w,N] → bf16 NHWC [B,2h,2w,N] */
+int iclr17_synthesis_deconv_igdn_bf16(const uint16_t* in, int B, int h, int w, int N,
+                                      const uint16_t* w_bf16, const float* bias,
+                                      const float* beta_eff, const uint16_t* gamma_bf16,
+                                      uint16_t* out, void* stream);
+/* synthesis_17.py:23-25 deconv3 + model.py:59 clamp: bf16 NHWC [B,H/4,W/4,N] → clipped NCHW
+ * fp32 (+ unclipped, + SSE partials as iclr17_synthesis_deconv3) */
+int iclr17_synthesis_deconv3_bf16(const uint16_t* in, int B, int H, int W, int N,
+                                  const float* w_packed, const float* bias, const float* x_ref,
+                                  float* clipped, float* recon, double* sse_partial,
+                                  int sse_unclipped, void* stream);
 
 #ifdef __cplusplus
 }

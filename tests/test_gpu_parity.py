@@ -100,13 +100,6 @@ def test_x6_layers(device, N):
         assert rel_err(y, nhwc(r_y)) < REL
         assert torch.equal(kernels.merge_planes(y_hat_s), y_hat)
         check_latents(y_hat.permute(0, 3, 1, 2), y.permute(0, 3, 1, 2), torch.round(r_y), r_y)
-        # pre-split weight planes (split_conv5) stage the same operands: bitwise the same outputs
-        a2_in = kernels.split_planes(nhwc(r_a2).contiguous().to(device))
-        yb_hat, bits_b, yb, yb_hat_s = kernels.conv3_quant_rate_x6(
-            a2_in, None, rate, want_y=True, w_split=kernels.split_conv5(w3, N))
-        _, bits_a, _, _ = kernels.conv3_quant_rate_x6(a2_in, w3, rate, want_y=True)
-        assert torch.equal(yb, y) and torch.equal(yb_hat, y_hat) and torch.equal(yb_hat_s, y_hat_s)
-        assert torch.equal(bits_b, bits_a)
         # synthesis
         yq = torch.round(torch.from_numpy(synth.uniform(5, (2, N, 4, 6), -4, 4)))
         d1, d2 = net.Decoder.packed()[:2]
@@ -179,10 +172,6 @@ def test_deconv3_x6(device, N, shape):
             assert rel_err(part, part32) < 1e-4
         c2, r2, p2 = kernels.deconv3_x6(hs, d3, net.Decoder.deconv3.bias)
         assert r2 is None and p2 is None and torch.equal(c2, clipped)
-        # pre-split weights read from L2: the same split values and product order, bit for bit
-        c3, r3, p3 = kernels.deconv3_x6(hs, d3, net.Decoder.deconv3.bias, x_ref=xd, want_recon=True,
-                                        sse_unclipped=True, w_split=net.Decoder.packed_deconv3_x6())
-        assert torch.equal(c3, clipped) and torch.equal(r3, recon) and torch.equal(p3, part)
 
 
 # ------------------------------------------------------------------------------------ layers

@@ -91,6 +91,7 @@ class Step:
         self.ebf = net.Encoder.packed_bf16()
         self.dbf = net.Decoder.packed_bf16()
         self.gbf = [m.effective_params_bf16() for m in gdns]
+        self.rtab = net.bitEstimator.rate_table()
 
     def __call__(self, events=None):
         net, N = self.net, self.N
@@ -104,7 +105,7 @@ class Step:
             ev(1)
             h = kernels.conv2_gdn_bf16(h, w2b, net.Encoder.conv2.bias, *e2)
             ev(2)
-            y_hat, partial, _, ybf = kernels.conv3_quant_rate_bf16(h, w3b, self.rate)
+            y_hat, partial, _, ybf = kernels.conv3_quant_rate_bf16(h, w3b, self.rate, self.rtab)
             ev(3)
             h = kernels.deconv_igdn_bf16(ybf, d1b, net.Decoder.deconv1.bias, *e3)
             ev(4)

@@ -120,7 +120,9 @@ SIGNATURES = {
     "iclr17_analysis_conv1_gdn_bf16": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "iclr17_analysis_conv2_gdn_bf16": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "iclr17_bf16_rate_partials_per_image": (_I, [_I, _I, _I]),
-    "iclr17_analysis_conv3_quant_rate_bf16": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_rate_table_size": (_SZ, [_I]),
+    "iclr17_rate_table": (_I, [_P, _I, _P, _P]),
+    "iclr17_analysis_conv3_quant_rate_bf16": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_synthesis_deconv_igdn_bf16": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "iclr17_synthesis_deconv3_bf16": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P]),
 }

@@ -33,6 +33,13 @@
 namespace iclr17 {
 namespace bfm {
 
+// Diagnostic ablation builds only (tools/bf16_ab.sh): -DICLR17_BFABL=mask — 1 weight DMA, 2 patch
+// DMA replaced by sink loads, 4 no main-loop barrier, 8 fragment reads hoisted out of the step
+// loop, 16 no GDN epilogue (all: wrong values, timing only)
+#ifndef ICLR17_BFABL
+#define ICLR17_BFABL 0
+#endif
+
 typedef unsigned short u16;
 typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
 
@@ -56,6 +63,16 @@ __device__ __forceinline__ f4 mfma_bf16(const u4& a, const u4& b, const f4& c) {
                                                  __builtin_bit_cast(bf8, b), c, 0, 0, 0);
 }
 
+// s_waitcnt vmcnt(N) (lgkm / exp untouched) + workgroup barrier
+template <int N>
+__device__ __forceinline__ void wait_vm_barrier() {
+  static_assert(N >= 0 && N < 64, "vmcnt field");
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 __device__ __forceinline__ void vm_barrier() {
   // every LDS-DMA of this wave landed (vmcnt(0)), then the workgroup barrier
   asm volatile("" ::: "memory");
@@ -74,6 +91,7 @@ struct K5Args {
   float* out_f32;       // QUANT: ŷ fp32 NHWC
   float* y_f32;         // QUANT: y (before rounding) fp32 NHWC, or null
   const float* rate;    // QUANT: packed rate table [11][CO]
+  const float* rtab;    // QUANT: element_bits(v, c) for integer v ∈ [−RT_K, RT_K] ([CO][2·RT_K+1])
   double* partial;      // QUANT: bit sums [B][ppi]
   int ppi;              // QUANT: partials per image
   int B, Hin, Win, Hout, Wout;
@@ -123,13 +141,36 @@ struct Patch {
   }
 };
 
+// ------------------------------------------------------------------------- rate table
+// element_bits(v, c) (model.py:71-73 per element) for the integer latents v ∈ [−RT_K, RT_K] of
+// each channel: the round-mode quantiser epilogue looks them up instead of evaluating the
+// 4-layer factorised CDF twice (tanh ×3, sigmoid, log) per element.
+constexpr int RT_K = 32, RT_W = 2 * RT_K + 1;
+
+__global__ void __launch_bounds__(256) rate_table_kernel(const float* __restrict__ rate, int C,
+                                                         float* __restrict__ table) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= C * RT_W) return;
+  const int c = i / RT_W, v = i - c * RT_W - RT_K;
+  table[i] = element_bits((float)v, rate, C, c);
+}
+
 // ------------------------------------------------------------------------- GDN epilogue
 // GDN / IGDN (models/GDN.py:64-94) on a C[channel][pixel] accumulator tile: acc[nt][mt][j] is
 // channel ncol + nt·16 + 4·(lane >> 4) + j of tile pixel pix0 + mt·16 + (lane & 15). Adds the
 // bias, writes x² as bf16 into an LDS tile [R pixels][CO] (row stride CO·2 + 32 bytes: the
-// 16-lane fragment reads hit distinct banks), contracts it with γ_eff (bf16 A fragments from L2,
-// one 16-channel block at a time), forms x/√(β+n) or x·√(β+n) in fp32 and stores the bf16 rows
-// through the same tile, 16 bytes per lane. Entry: LDS free (caller's barrier).
+// 16-lane fragment reads hit distinct banks; the 8-byte writes are 4-way), contracts it
+// with γ_eff (bf16 A fragments from L2, a whole 16-channel block's fragments one block ahead),
+// forms x·rsqrt(β+n) or x·sqrt(β+n) in fp32 and stores the bf16 rows through the same tile,
+// 16 bytes per lane. Entry: LDS free (caller's barrier).
+template <int CO>
+__device__ __forceinline__ int epi_off(int p, int ch) {   // byte offset of (pixel, channel)
+  return p * (CO * 2 + 32) + ch * 2;
+}
+
+template <int CO>
+constexpr int epi_tile_bytes(int R) { return R * (CO * 2 + 32); }
+
 template <int CO, int MT, int NT, int NTHR, bool INV, class PixFn>
 __device__ __forceinline__ void gdn_epilogue_bf16(f4 (&acc)[NT][MT], unsigned char* sq,
                                                   const float* __restrict__ bias,
@@ -137,8 +178,10 @@ __device__ __forceinline__ void gdn_epilogue_bf16(f4 (&acc)[NT][MT], unsigned ch
                                                   const u16* __restrict__ gamma, u16* out, int R,
                                                   int pix0, int ncol, PixFn out_pixel) {
   typedef const __attribute__((address_space(3))) u4* lu4p;
-  constexpr int RS = CO * 2 + 32;
   const int tid = threadIdx.x, lane = tid & 63, kg = lane >> 4;
+  constexpr int KB = CO / 32;
+  // γ fragments: k-groups 4·kb + kg, rows ncol + nt·16 + lane & 15
+  const u16* gb = gamma + (kg * CO + ncol + (lane & 15)) * 8;
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
     const int ch = ncol + nt * 16 + 4 * kg;
@@ -148,16 +191,17 @@ __device__ __forceinline__ void gdn_epilogue_bf16(f4 (&acc)[NT][MT], unsigned ch
       acc[nt][mt] += bv;
       const f4 v = acc[nt][mt];
       const int p = pix0 + mt * 16 + (lane & 15);
-      *(uint2*)(sq + p * RS + ch * 2) = uint2{pack_bf2(v[0] * v[0], v[1] * v[1]),
-                                              pack_bf2(v[2] * v[2], v[3] * v[3])};
+      *(uint2*)(sq + epi_off<CO>(p, ch)) = uint2{pack_bf2(v[0] * v[0], v[1] * v[1]),
+                                                 pack_bf2(v[2] * v[2], v[3] * v[3])};
     }
   }
+  u4 gf[KB];
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) gf[kb] = *(const u4*)(gb + (long)kb * 4 * CO * 8);
   __syncthreads();
-  // n[i][p] = Σ_j γ[i][j]·x²[j][p]: A = γ (rows i), B = x² (k = j)
-  const u16* gb = gamma + (kg * CO + ncol + (lane & 15)) * 8;
-  const unsigned char* xb = sq + (pix0 + (lane & 15)) * RS + kg * 16;
-  constexpr int KB = CO / 32;
-  u4 gnext = *(const u4*)gb;
+  // n[i][p] = Σ_j γ[i][j]·x²[j][p]: A = γ (rows i), B = x² (k = j); γ fragment kb of block nt+1
+  // is loaded into the register fragment kb of block nt frees (about KB iterations ahead)
+  const int pl = pix0 + (lane & 15);
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
     f4 nacc[MT];
@@ -165,12 +209,11 @@ __device__ __forceinline__ void gdn_epilogue_bf16(f4 (&acc)[NT][MT], unsigned ch
     for (int mt = 0; mt < MT; ++mt) nacc[mt] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) {
-      const u4 gc = gnext;
-      const int nn = kb + 1 < KB ? nt : nt + 1, kn = kb + 1 < KB ? kb + 1 : 0;
-      if (nn < NT) gnext = *(const u4*)(gb + (long)kn * 4 * CO * 8 + nn * 128);
       u4 xs[MT];
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) xs[mt] = *(lu4p)(xb + mt * 16 * RS + kb * 64);
+      for (int mt = 0; mt < MT; ++mt) xs[mt] = *(lu4p)(sq + epi_off<CO>(pl + mt * 16, 32 * kb + 8 * kg));
+      const u4 gc = gf[kb];
+      if (nt + 1 < NT) gf[kb] = *(const u4*)(gb + (long)kb * 4 * CO * 8 + (nt + 1) * 128);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) nacc[mt] = mfma_bf16(gc, xs[mt], nacc[mt]);
     }
@@ -180,8 +223,8 @@ __device__ __forceinline__ void gdn_epilogue_bf16(f4 (&acc)[NT][MT], unsigned ch
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float s = sqrtf(nacc[mt][j] + be[j]);
-        acc[nt][mt][j] = INV ? acc[nt][mt][j] * s : acc[nt][mt][j] / s;
+        const float n = nacc[mt][j] + be[j];
+        acc[nt][mt][j] *= INV ? __builtin_amdgcn_sqrtf(n) : __builtin_amdgcn_rsqf(n);
       }
   }
   __syncthreads();   // x² reads done: the tile is rewritten with the output
@@ -192,7 +235,7 @@ __device__ __forceinline__ void gdn_epilogue_bf16(f4 (&acc)[NT][MT], unsigned ch
     for (int mt = 0; mt < MT; ++mt) {
       const f4 y = acc[nt][mt];
       const int p = pix0 + mt * 16 + (lane & 15);
-      *(uint2*)(sq + p * RS + ch * 2) = uint2{pack_bf2(y[0], y[1]), pack_bf2(y[2], y[3])};
+      *(uint2*)(sq + epi_off<CO>(p, ch)) = uint2{pack_bf2(y[0], y[1]), pack_bf2(y[2], y[3])};
     }
   }
   __syncthreads();
@@ -201,7 +244,7 @@ __device__ __forceinline__ void gdn_epilogue_bf16(f4 (&acc)[NT][MT], unsigned ch
     const int p = idx / PCS, pc = idx - p * PCS;
     const long o = out_pixel(p);
     if (o < 0) continue;
-    *(u4*)(out + o * CO + pc * 8) = *(lu4p)(sq + p * RS + pc * 16);
+    *(u4*)(out + o * CO + pc * 8) = *(lu4p)(sq + epi_off<CO>(p, pc * 8));
   }
 }
 
@@ -216,9 +259,9 @@ struct K5 {
   static constexpr int SB = 4 * NB * 16;        // weight stage bytes
   static constexpr int NBI = SB / 1024;         // weight DMA wave-instructions per step
   using P = Patch<MODE, TH>;
-  static constexpr int RS = CO * 2 + 32;        // epilogue tile row stride (bytes): conflict-free
-  static constexpr int MAIN_LDS = 2 * P::BUF + 2 * SB;
-  static constexpr int EPI_LDS = EPI == BE_QUANT ? 64 : R * RS;
+  static constexpr int NST = 3;                 // weight stages (ring)
+  static constexpr int MAIN_LDS = 2 * P::BUF + NST * SB + 1024;
+  static constexpr int EPI_LDS = EPI == BE_QUANT ? 64 : epi_tile_bytes<CO>(R);
   static constexpr int LDS = MAIN_LDS > EPI_LDS ? MAIN_LDS : EPI_LDS;
   static_assert(TH % WM == 0 && NB % (WN * 16) == 0 && SB % 1024 == 0, "tile shape");
   static_assert(EPI == BE_QUANT || NB == CO, "GDN needs every channel of a pixel in the tile");
@@ -236,28 +279,32 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int kg = lane >> 4, half = kg & 1, hi = kg >> 1;
-  unsigned char* const sP = smem;                    // two patch buffers
-  unsigned char* const sB = smem + 2 * P::BUF;       // two weight stages
-
-  // ---- patch DMA sources: per instruction j of this wave, slot q = 64·i + lane (16 bytes)
-  constexpr int QW = (P::NQI + NW - 1) / NW;
-  int qsrc[QW];
+  // LDS-DMA schedule. Every step every wave issues exactly K DMA instructions (weights of step
+  // g+2 into a three-stage ring, pieces of the next chunk's patch, 1 KB sink loads as padding),
+  // so a counted `s_waitcnt vmcnt(K)` before the step's barrier retires everything but the
+  // previous step's group: the weights of step g (issued two steps earlier) and, at a chunk
+  // start, the whole patch (its pieces go out in the previous chunk's steps 0 .. S-2).
+  constexpr int NST = KK::NST, SI = S - 1;
+  constexpr int PS = (P::NQI + SI - 1) / SI;          // patch pieces per issuing step
+  constexpr int K = (NBI + PS + NW - 1) / NW;         // DMA instructions per wave per step
+  constexpr int GS = NCH * S;                         // steps
+  unsigned char* const sP = smem;                     // two patch buffers
+  unsigned char* const sB = smem + 2 * P::BUF;        // NST weight stages
+  unsigned char* const sD = sB + NST * SB;            // 1 KB sink of the padding loads
   const long img = (long)b * a.Hin * a.Win;
   const int iy0 = MODE == BM_CONV ? 2 * ty * TH - 2 : ty * TH - 1;
   const int ix0 = MODE == BM_CONV ? 2 * tx * 16 - 2 : tx * 16 - 1;
-#pragma unroll
-  for (int j = 0; j < QW; ++j) {
-    const int i = wave + NW * j;
-    const int q = i * 64 + lane;
-    const int byte = q * 16;
+  const u16* __restrict__ inb = a.in + img * CI;
+  // patch piece (wave-instruction) `piece`: this lane's 16-byte slot → source u16 offset or -1
+  auto piece_src = [&](int piece) -> int {
+    const int byte = (piece * 64 + lane) * 16;
     const int pr = byte / P::ROWB, rem = byte - pr * P::ROWB;
     int pc, h;
     bool ok;
     if (MODE == BM_CONV) {
       const int par = rem / (18 * 32), r2 = rem - par * 18 * 32;
-      const int idx = r2 / 32;
       h = (r2 / 16) & 1;
-      pc = 2 * idx + par;
+      pc = 2 * (r2 / 32) + par;
       ok = pc < 35;
     } else {
       pc = rem / 32;
@@ -265,28 +312,22 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
       ok = true;
     }
     const int iy = iy0 + pr, ix = ix0 + pc;
-    ok = ok && i < P::NQI && pr < P::ROWS && (unsigned)iy < (unsigned)a.Hin &&
-         (unsigned)ix < (unsigned)a.Win;
-    qsrc[j] = ok ? (int)(((long)iy * a.Win + ix) * CI + 8 * h) : -1;
-  }
-  const u16* __restrict__ inb = a.in + img * CI;
-  auto issue_patch_part = [&](int c, int j) {
-    const int i = wave + NW * j;
-    if (i < P::NQI) {
-      const void* src = qsrc[j] >= 0 ? (const void*)(inb + qsrc[j] + c * 16) : (const void*)g_zero16;
-      glds16(src, sP + (c & 1) * P::BUF + i * 1024);
-    }
+    ok = ok && pr < P::ROWS && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
+    return ok ? (iy * a.Win + ix) * CI + 8 * h : -1;
   };
-  // ---- weight DMA: stage slot q = 64·i + lane → (k-group, column) of the workgroup's slice
+  auto issue_piece = [&](int c, int piece) {
+    const int src = piece_src(piece);
+    glds16(src >= 0 ? (const void*)(inb + src + c * 16) : (const void*)g_zero16,
+           sP + (c & 1) * P::BUF + piece * 1024);
+  };
+  // weight slots: slot k·NW + wave < NBI of a group copies 1 KB of the step's [4][NB][8] slice
   const long wstep = 4L * CO * 8;                     // u16 per (chunk, step) of the packing
-  constexpr int BW = (NBI + NW - 1) / NW;
-  int wsrc[BW];
+  int wsrc[K];
 #pragma unroll
-  for (int j = 0; j < BW; ++j) {
-    const int i = wave + NW * j;
-    const int q = i * 64 + lane;
+  for (int k = 0; k < K; ++k) {
+    const int q = (k * NW + wave) * 64 + lane;
     const int g = q / NB, col = q - g * NB;
-    wsrc[j] = (g * CO + nb * NB + col) * 8;
+    wsrc[k] = (g * CO + nb * NB + col) * 8;
   }
   // packed weights of this phase: [NCH][S][4][CO][8]
   const u16* __restrict__ wph = a.w;
@@ -299,14 +340,12 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
     }
     wph += off;
   }
-  auto issue_w = [&](int gstep) {   // gstep = c·S + s
-    const u16* src = wph + (long)gstep * wstep;
-    unsigned char* dst = sB + (gstep & 1) * SB;
-#pragma unroll
-    for (int j = 0; j < BW; ++j) {
-      const int i = wave + NW * j;
-      if (NBI % NW == 0 || i < NBI) glds16(src + wsrc[j], dst + i * 1024);
-    }
+  auto issue_w = [&](int k, int wg) {   // weight slot k of step wg (a sink load past the end)
+    const int slot = k * NW + wave;
+    if (wg < GS && (!(ICLR17_BFABL & 1) || wg < 2))
+      glds16(wph + (long)wg * wstep + wsrc[k], sB + (wg % NST) * SB + slot * 1024);
+    else
+      glds16(g_zero16, sD);
   };
 
   // ---- per-lane fragment addresses
@@ -324,33 +363,56 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = f4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: chunk 0's patch and step 0's weights
+  // prologue: chunk 0's patch and step 0's weights (any count per wave), then step 1's weights
+  // as a full K-group
+  for (int piece = wave; piece < P::NQI; piece += NW) issue_piece(0, piece);
 #pragma unroll
-  for (int j = 0; j < QW; ++j) issue_patch_part(0, j);
-  issue_w(0);
+  for (int k = 0; k < K; ++k)
+    if (k * NW + wave < NBI) issue_w(k, 0);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    if (k * NW + wave < NBI) issue_w(k, 1);
+    else glds16(g_zero16, sD);
+  }
 
   typedef const __attribute__((address_space(3))) u4* lu4p;
+  int stage = 0;   // g % NST
   for (int c = 0; c < NCH; ++c) {
     const unsigned char* pbuf = sP + (c & 1) * P::BUF + pbase;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       const int g = c * S + s;
-      vm_barrier();   // step g's weights (and at s = 0 chunk c's patch) landed; stage (g+1)&1 free
-      if (g + 1 < NCH * S) issue_w(g + 1);
-      if (c + 1 < NCH) {   // chunk c+1's patch, spread over this chunk's first steps
+      if (!(ICLR17_BFABL & 4))
+        wait_vm_barrier<K>();   // all but the previous step's group landed: weights of step g and,
+                                // at s = 0, chunk c's patch; stage (g+2) % NST is free
 #pragma unroll
-        for (int j = 0; j < QW; ++j)
-          if (j % (S > 1 ? S - 1 : 1) == s) issue_patch_part(c + 1, j);
+      for (int k = 0; k < K; ++k) {
+        const int slot = k * NW + wave;
+        if (slot < NBI) {
+          issue_w(k, g + 2);
+        } else {
+          const int piece = s * PS + slot - NBI;
+          if (s < SI && c + 1 < NCH && piece < P::NQI && !(ICLR17_BFABL & 2)) issue_piece(c + 1, piece);
+          else glds16(g_zero16, sD);
+        }
       }
       // tap pair (2s, 2s+1): lanes 0-31 the first, 32-63 the second
       const int t0 = P::template tap_off<PH>(2 * s), t1 = P::template tap_off<PH>(2 * s + 1);
       const unsigned char* pb = pbuf + t0 + hi * (t1 - t0);
-      const unsigned char* wb = sB + (g & 1) * SB + abase;
+      const unsigned char* wb = sB + stage * SB + abase;
+      stage = stage == NST - 1 ? 0 : stage + 1;
       u4 wa[NT], px[MT];
+      if (!(ICLR17_BFABL & 8) || g == 0) {
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) wa[nt] = *(lu4p)(wb + nt * 256);
+        for (int nt = 0; nt < NT; ++nt) wa[nt] = *(lu4p)(wb + nt * 256);
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) px[mt] = *(lu4p)(pb + mt * MT_STRIDE);
+        for (int mt = 0; mt < MT; ++mt) px[mt] = *(lu4p)(pb + mt * MT_STRIDE);
+      } else {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) wa[nt] = u4{(unsigned)g, 1u, 2u, (unsigned)nt};
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) px[mt] = u4{(unsigned)s, 3u, (unsigned)mt, 4u};
+      }
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -367,6 +429,15 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
     if (MODE == BM_CONV) return ((long)b * a.Hout + gy) * a.Wout + gx;
     return ((long)b * a.Hout + 2 * gy + (PH >> 1)) * a.Wout + 2 * gx + (PH & 1);
   };
+  if ((ICLR17_BFABL & 16) && EPI != BE_QUANT) {
+    float sum = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) sum += acc[nt][mt][0] + acc[nt][mt][3];
+    if (sum == 12345.f) a.out[0] = 1;
+    return;
+  }
   if constexpr (EPI == BE_GDN || EPI == BE_IGDN) {
     gdn_epilogue_bf16<CO, MT, NT, KK::NT_, EPI == BE_IGDN>(acc, smem, a.bias, a.beta, a.gamma, a.out,
                                                           KK::R, wm * MT * 16, ncol, out_pixel);
@@ -387,7 +458,9 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           q[j] = rintf(y[j]);
-          bits += element_bits(q[j], a.rate, CO, ch + j);
+          // integer latents: the per-channel table of the same element_bits (bit-identical)
+          bits += fabsf(q[j]) <= (float)RT_K ? a.rtab[(ch + j) * RT_W + (int)q[j] + RT_K]
+                                             : element_bits(q[j], a.rate, CO, ch + j);
         }
         if (a.y_f32) *(f4*)(a.y_f32 + o * CO + ch) = y;
         *(f4*)(a.out_f32 + o * CO + ch) = q;
@@ -452,7 +525,7 @@ struct C1 {
   static constexpr int LAND = C1NI * 1024;            // fp32 landing area (bytes)
   static constexpr int PLANE = C1U * 2;                // bf16 plane (bytes)
   static constexpr int MAIN = LAND + PLANE;
-  static constexpr int EPI = 64 * (CO * 2 + 32);
+  static constexpr int EPI = epi_tile_bytes<CO>(64);
   static constexpr int LDS = MAIN > EPI ? MAIN : EPI;
 };
 
@@ -764,17 +837,27 @@ int iclr17_bf16_rate_partials_per_image(int H, int W, int N) {
   return ((H / 16 + 7) / 8) * ((W / 16 + 15) / 16) * 2;
 }
 
+size_t iclr17_rate_table_size(int N) { return (size_t)N * RT_W; }
+
+int iclr17_rate_table(const float* rate_packed, int N, float* table, void* stream) {
+  ICLR17_REQUIRE(rate_packed && table && N > 0, ICLR17_EINVAL, "rate_table: bad arguments");
+  hipLaunchKernelGGL(rate_table_kernel, dim3((N * RT_W + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, rate_packed, N, table);
+  return check_launch("rate_table");
+}
+
 int iclr17_analysis_conv3_quant_rate_bf16(const uint16_t* in, int B, int H, int W, int N,
                                           const uint16_t* w_bf16, const float* rate_packed,
-                                          float* y_out, float* y_hat, uint16_t* y_hat_bf16,
-                                          double* bits_partial, void* stream) {
+                                          const float* rate_table, float* y_out, float* y_hat,
+                                          uint16_t* y_hat_bf16, double* bits_partial,
+                                          void* stream) {
   ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "conv3_quant_rate_bf16: N=%d", N);
-  ICLR17_REQUIRE(in && w_bf16 && rate_packed && y_hat && y_hat_bf16 && bits_partial && B > 0 &&
+  ICLR17_REQUIRE(in && w_bf16 && rate_packed && rate_table && y_hat && y_hat_bf16 && bits_partial && B > 0 &&
                      H % 16 == 0 && W % 16 == 0 && H > 0 && W > 0,
                  ICLR17_EINVAL, "conv3_quant_rate_bf16: bad arguments");
   K5Args a;
   memset(&a, 0, sizeof(a));
-  a.in = in; a.w = w_bf16; a.rate = rate_packed; a.y_f32 = y_out; a.out_f32 = y_hat;
+  a.in = in; a.w = w_bf16; a.rate = rate_packed; a.rtab = rate_table; a.y_f32 = y_out; a.out_f32 = y_hat;
   a.out = y_hat_bf16; a.partial = bits_partial;
   a.B = B; a.Hin = H / 8; a.Win = W / 8; a.Hout = H / 16; a.Wout = W / 16;
   a.gh = a.Hout; a.gw = a.Wout;

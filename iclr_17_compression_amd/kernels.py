@@ -591,9 +591,21 @@ def conv2_gdn_bf16(h: Tensor, w_bf: Tensor, bias: Tensor, beta_eff: Tensor, g_bf
     return out
 
 
-def conv3_quant_rate_bf16(h: Tensor, w_bf: Tensor, rate_packed: Tensor, want_y: bool = False):
+def rate_table(rate_packed: Tensor, N: int) -> Tensor:
+    """element_bits(v, c) for the integer latents v ∈ [−32, 32]: float32 [N, 65]."""
+    _check(rate_packed, "rate table")
+    if rate_packed.numel() != 11 * N:
+        raise Iclr17Error(f"iclr17: rate_table: packed rate parameters are not [11][{N}]")
+    out = torch.empty(N, 65, device=rate_packed.device, dtype=torch.float32)
+    call("iclr17_rate_table", _p(rate_packed), N, _p(out), _stream(rate_packed))
+    return out
+
+
+def conv3_quant_rate_bf16(h: Tensor, w_bf: Tensor, rate_packed: Tensor, rtab: Optional[Tensor] = None,
+                          want_y: bool = False):
     """analysis_17.py:22 + model.py:56,71-73 (round mode) in bf16 → (ŷ fp32 NHWC, bits partials
-    [B,T] float64, y fp32 | None, ŷ bf16 NHWC)."""
+    [B,T] float64, y fp32 | None, ŷ bf16 NHWC). rtab: ``rate_table`` of rate_packed (made here
+    when not given)."""
     _check_bf16(h, "activation")
     B, h8, w8, N = h.shape
     _check_channels(N)
@@ -604,8 +616,10 @@ def conv3_quant_rate_bf16(h: Tensor, w_bf: Tensor, rate_packed: Tensor, want_y: 
     y = torch.empty_like(y_hat) if want_y else None
     T = query("iclr17_bf16_rate_partials_per_image", H, W, N)
     partial = torch.empty(B, T, device=h.device, dtype=torch.float64)
+    if rtab is None:
+        rtab = rate_table(rate_packed, N)
     call("iclr17_analysis_conv3_quant_rate_bf16", _p(h), B, H, W, N, _p(w_bf), _p(rate_packed),
-         _p(y), _p(y_hat), _p(y_hat_bf), _p(partial), _stream(h))
+         _p(rtab), _p(y), _p(y_hat), _p(y_hat_bf), _p(partial), _stream(h))
     return y_hat, partial, y, y_hat_bf
 
 

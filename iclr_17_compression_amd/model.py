@@ -93,6 +93,7 @@ class ImageCompressor(nn.Module):
             h = kernels.conv1_gdn_bf16(x, w1b, self.Encoder.conv1.bias, *e1, N)
             h = kernels.conv2_gdn_bf16(h, w2b, self.Encoder.conv2.bias, *e2)
             y_hat, bits, y, ybf = kernels.conv3_quant_rate_bf16(h, w3b, self.bitEstimator.packed(),
+                                                                self.bitEstimator.rate_table(),
                                                                 want_y=want_y)
             return {"y_hat": y_hat, "bits_partial": bits, "y_split": None, "y_bf16": ybf, "y": y}
         if kernels.precision() != "fp32":
@@ -223,6 +224,7 @@ class ImageCompressor(nn.Module):
         if kernels.precision() == "bf16" and not backward:
             self.Encoder.packed_bf16()
             self.Decoder.packed_bf16()
+            self.bitEstimator.rate_table()
             for g in gdns:
                 g.effective_params_bf16()
         with kernels.batched_packs():

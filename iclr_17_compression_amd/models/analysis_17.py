@@ -99,7 +99,8 @@ class Analysis_net_17(nn.Module):
             e1, e2 = self.gdn1.effective_params_bf16(), self.gdn2.effective_params_bf16()
             h = kernels.conv1_gdn_bf16(x.contiguous(), w1b, self.conv1.bias, *e1, self.out_channel_N)
             h = kernels.conv2_gdn_bf16(h, w2b, self.conv2.bias, *e2)
-            be = torch.zeros(11 * self.out_channel_N, device=x.device)   # rate unused: y only
-            y = kernels.conv3_quant_rate_bf16(h, w3b, be, want_y=True)[2]
+            z = torch.zeros(11 * self.out_channel_N, device=x.device)   # rate unused: y only
+            y = kernels.conv3_quant_rate_bf16(h, w3b, z, torch.zeros(self.out_channel_N, 65, device=x.device),
+                                              want_y=True)[2]
             return y.permute(0, 3, 1, 2)
         return kernels.conv3(self.features(x), w3).permute(0, 3, 1, 2)

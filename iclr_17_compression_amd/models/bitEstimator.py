@@ -51,6 +51,13 @@ class BitEstimator(nn.Module):
         ps = self.params_in_order()
         return self._pack.get("rate", ps, lambda: kernels.pack_rate(ps), force=force)
 
+    def rate_table(self, force: bool = False):
+        """element_bits for the integer latents −32..32 per channel ([C, 65]; the round-mode
+        quantiser epilogue looks them up), cached like the packed parameters."""
+        ps = self.params_in_order()
+        return self._pack.get("rtab", ps, lambda: kernels.rate_table(self.packed(force), self.channel),
+                              force=force)
+
     def entropy_tables(self, K: int = kernels.ENTROPY_K):
         """Quantised CDFs for the entropy coder (cached like the packed parameters)."""
         ps = self.params_in_order()

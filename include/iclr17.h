@@ -435,13 +435,20 @@ int iclr17_analysis_conv1_gdn_bf16(const float* x, int B, int H, int W, int N,
 int iclr17_analysis_conv2_gdn_bf16(const uint16_t* in, int B, int H, int W, int N,
                                    const uint16_t* w_bf16, const float* bias, const float* beta_eff,
                                    const uint16_t* gamma_bf16, uint16_t* out, void* stream);
+/* model.py:71-73 per element for the integer latents v ∈ [−32, 32] of each channel:
+ * table[c][v + 32] = clamp(−log2(F_c(v+½) − F_c(v−½) + 1e-10), 0, 50) from the packed rate
+ * parameters (iclr17_pack_rate); iclr17_rate_table_size(N) floats. */
+size_t iclr17_rate_table_size(int N);
+int iclr17_rate_table(const float* rate_packed, int N, float* table, void* stream);
 /* analysis_17.py:22 + model.py:56,71-73 (round mode): → ŷ fp32 NHWC, ŷ bf16 NHWC, optional y
- * fp32 NHWC, bit partials [B][iclr17_bf16_rate_partials_per_image] (float64) */
+ * fp32 NHWC, bit partials [B][iclr17_bf16_rate_partials_per_image] (float64); rate_table from
+ * iclr17_rate_table of the same rate_packed (|ŷ| > 32 evaluates the model directly). */
 int iclr17_bf16_rate_partials_per_image(int H, int W, int N);
 int iclr17_analysis_conv3_quant_rate_bf16(const uint16_t* in, int B, int H, int W, int N,
                                           const uint16_t* w_bf16, const float* rate_packed,
-                                          float* y_out, float* y_hat, uint16_t* y_hat_bf16,
-                                          double* bits_partial, void* stream);
+                                          const float* rate_table, float* y_out, float* y_hat,
+                                          uint16_t* y_hat_bf16, double* bits_partial,
+                                          void* stream);
 /* synthesis_17.py:15-22 deconv + IGDN: bf16 NHWC [B,h,w,N] → bf16 NHWC [B,2h,2w,N] */
 int iclr17_synthesis_deconv_igdn_bf16(const uint16_t* in, int B, int h, int w, int N,
                                       const uint16_t* w_bf16, const float* bias,

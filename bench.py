@@ -119,7 +119,7 @@ class Step:
             ev(1)
             hs, _, _ = kernels.conv2_gdn_x6(hs, w2, net.Encoder.conv2.bias, *e2)
             ev(2)
-            y_hat, partial, _, ys = kernels.conv3_quant_rate_x6(hs, w3, self.rate)
+            y_hat, partial, _, ys = kernels.conv3_quant_rate_x6(hs, w3, self.rate, rtab=self.rtab)
             ev(3)
             hs, _, _ = kernels.deconv_igdn_x6(ys, d1, net.Decoder.deconv1.bias, *e3)
             ev(4)
@@ -131,7 +131,7 @@ class Step:
             ev(1)
             h = kernels.conv2_gdn(h, w2, net.Encoder.conv2.bias, g2[0], g2[1])
             ev(2)
-            y_hat, partial = kernels.conv3_quant_rate(h, w3, self.rate)
+            y_hat, partial = kernels.conv3_quant_rate(h, w3, self.rate, rtab=self.rtab)
             ev(3)
             h = kernels.deconv_igdn(y_hat, d1, net.Decoder.deconv1.bias, q1[0], q1[1])
             ev(4)

@@ -52,7 +52,7 @@ SIGNATURES = {
     "iclr17_pack_batch": (_I, [_P, _I, _P, _P]),
     "iclr17_analysis_conv1_gdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_analysis_conv2_gdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
-    "iclr17_analysis_conv3_quant_rate": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P]),
+    "iclr17_analysis_conv3_quant_rate": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_analysis_conv3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P]),
     "iclr17_rate_partials_per_image": (_I, [_I, _I, _I]),
     "iclr17_synthesis_deconv_igdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
@@ -65,7 +65,7 @@ SIGNATURES = {
     "iclr17_analysis_conv1x6_gdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_analysis_conv2_gdn_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_analysis_conv3_quant_rate_x6": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P,
-                                                 _P, _P, _P]),
+                                                 _P, _P, _P, _P]),
     "iclr17_synthesis_deconv_igdn_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
                                              _P]),
     "iclr17_reduce_partials": (_I, [_P, _I, _I, _P, _P, _D, _P]),

@@ -104,6 +104,7 @@ struct EngineArgs {
   int qmode;
   const float* noise;   // NCHW [B][CO][Hout][Wout]
   const float* rate;    // packed [11][CO]
+  const float* rtab;    // round mode, nullable: element_bits of the integer latents −32..32 [CO][65]
   float* yhat;          // NHWC
   double* partial;      // per-tile partial sums
   int partials_per_image;
@@ -808,7 +809,11 @@ __device__ __forceinline__ void quant_epilogue(f4 (&acc)[MT][NT], float* smem, c
           const float u = ok ? a.noise[(((long)t.b * CO + col) * a.Hout + gy) * a.Wout + gx] : 0.f;
           yh = y + u;
         }
-        if (ok) bits += element_bits(yh, a.rate, CO, col);
+        if (ok) {   // integer latents: the per-channel table of the same element_bits
+          bits += (a.rtab != nullptr && a.qmode == ICLR17_QUANT_ROUND && fabsf(yh) <= 32.f)
+                      ? a.rtab[col * 65 + (int)yh + 32]
+                      : element_bits(yh, a.rate, CO, col);
+        }
         sO[row * OS + lcol] = yh;
       }
   __syncthreads();
@@ -2101,7 +2106,8 @@ template <int N, int EPI>
 int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, const float* bias,
                  const float* beta, const float* gamma, float* out, float* pre, int qmode,
                  const float* noise, const float* rate, float* yhat, double* partial,
-                 hipStream_t st, const EngineArgs* bwd = nullptr, const SplitIO* x6 = nullptr) {
+                 hipStream_t st, const EngineArgs* bwd = nullptr, const SplitIO* x6 = nullptr,
+                 const float* rtab = nullptr) {
   EngineArgs a;
   memset(&a, 0, sizeof(a));
   if (bwd) a = *bwd;
@@ -2112,7 +2118,7 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
   a.gh = a.Hout; a.gw = a.Wout; a.tiles_y = (a.gh + 7) / 8; a.tiles_x = (a.gw + 7) / 8;
   a.sin = 2; a.sout = 1;
   fill_conv5_taps(a.tt);
-  a.qmode = qmode; a.noise = noise; a.rate = rate; a.yhat = yhat; a.partial = partial;
+  a.qmode = qmode; a.noise = noise; a.rate = rate; a.rtab = rtab; a.yhat = yhat; a.partial = partial;
   if constexpr (EPI == EPI_QUANT) {
     // Column split of conv3: 96 columns (2×2 waves) at N = 192 — B=64 gives 512 workgroups, one
     // round of slots, and 20 % fewer operand bytes per MAC than 64-column tiles.
@@ -2306,8 +2312,9 @@ int iclr17_rate_partials_per_image(int H, int W, int N) {
 
 int iclr17_analysis_conv3_quant_rate(const float* in, int B, int H, int W, int N,
                                      const float* w_packed, int quant_mode, const float* noise,
-                                     const float* rate_packed, float* y_out, float* y_hat,
-                                     double* bits_partial, void* stream) {
+                                     const float* rate_packed, const float* rate_table,
+                                     float* y_out, float* y_hat, double* bits_partial,
+                                     void* stream) {
   int rc = check_dims(B, H, W, N);
   if (rc) return rc;
   ICLR17_REQUIRE(in && w_packed && rate_packed && y_hat && bits_partial, ICLR17_EINVAL,
@@ -2315,8 +2322,8 @@ int iclr17_analysis_conv3_quant_rate(const float* in, int B, int H, int W, int N
   ICLR17_REQUIRE(quant_mode == ICLR17_QUANT_ROUND || (quant_mode == ICLR17_QUANT_NOISE && noise),
                  ICLR17_EINVAL, "conv3_quant_rate: bad quant mode %d / missing noise", quant_mode);
   const int h = H / 8, w = W / 8;
-  return N == 192 ? launch_conv5<192, EPI_QUANT>(in, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream))
-                  : launch_conv5<128, EPI_QUANT>(in, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream));
+  return N == 192 ? launch_conv5<192, EPI_QUANT>(in, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, nullptr, rate_table)
+                  : launch_conv5<128, EPI_QUANT>(in, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, nullptr, rate_table);
 }
 
 int iclr17_analysis_conv3(const float* in, int B, int H, int W, int N, const float* w_packed,
@@ -2499,9 +2506,9 @@ int iclr17_analysis_conv2_gdn_x6(const uint16_t* in_split, int B, int H, int W, 
 
 int iclr17_analysis_conv3_quant_rate_x6(const uint16_t* in_split, int B, int H, int W, int N,
                                         const float* w_packed, int quant_mode, const float* noise,
-                                        const float* rate_packed, float* y_out, float* y_hat,
-                                        uint16_t* y_hat_split, double* bits_partial,
-                                        void* stream) {
+                                        const float* rate_packed, const float* rate_table,
+                                        float* y_out, float* y_hat, uint16_t* y_hat_split,
+                                        double* bits_partial, void* stream) {
   int rc = check_dims(B, H, W, N);
   if (rc) return rc;
   ICLR17_REQUIRE(in_split && w_packed && rate_packed && y_hat && bits_partial,
@@ -2514,8 +2521,8 @@ int iclr17_analysis_conv3_quant_rate_x6(const uint16_t* in_split, int B, int H, 
   io.in_plane = (long)B * h * w * N;
   io.out = (unsigned short*)y_hat_split;
   io.out_plane = (long)B * (h / 2) * (w / 2) * N;
-  return N == 192 ? launch_conv5<192, EPI_QUANT>(nullptr, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io)
-                  : launch_conv5<128, EPI_QUANT>(nullptr, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io);
+  return N == 192 ? launch_conv5<192, EPI_QUANT>(nullptr, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io, rate_table)
+                  : launch_conv5<128, EPI_QUANT>(nullptr, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io, rate_table);
 }
 
 int iclr17_synthesis_deconv_igdn_x6(const uint16_t* in_split, int B, int h, int w, int N,

@@ -210,10 +210,11 @@ def rate_partials_per_image(H: int, W: int, N: int) -> int:
 
 
 def conv3_quant_rate(h: Tensor, wp: Tensor, rate_packed: Tensor, noise: Optional[Tensor] = None,
-                     want_y: bool = False):
+                     want_y: bool = False, rtab: Optional[Tensor] = None):
     """analysis_17.py:22 + model.py:48-56,71-73. Returns (y_hat NHWC, bits_partial [B,T], y?).
 
-    noise (training) is NCHW [B,N,H/16,W/16], the shape model.py:48 draws."""
+    noise (training) is NCHW [B,N,H/16,W/16], the shape model.py:48 draws. rtab (``rate_table``
+    of rate_packed, round mode): bits of the integer latents by lookup."""
     _check(h, "activation", 4)
     B, h8, w8, N = h.shape
     _check_channels(N)
@@ -231,7 +232,7 @@ def conv3_quant_rate(h: Tensor, wp: Tensor, rate_packed: Tensor, noise: Optional
     T = rate_partials_per_image(H, W, N)
     partial = torch.empty(B, T, device=h.device, dtype=torch.float64)
     call("iclr17_analysis_conv3_quant_rate", _p(h.contiguous()), B, H, W, N, _p(wp), mode,
-         _p(noise), _p(rate_packed), _p(y), _p(y_hat), _p(partial), _stream(h))
+         _p(noise), _p(rate_packed), _p(rtab), _p(y), _p(y_hat), _p(partial), _stream(h))
     return (y_hat, partial, y) if want_y else (y_hat, partial)
 
 
@@ -375,9 +376,10 @@ def conv2_gdn_x6(hs: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Ten
 
 
 def conv3_quant_rate_x6(hs: Tensor, wp: Tensor, rate_packed: Tensor,
-                        noise: Optional[Tensor] = None, want_y: bool = False):
+                        noise: Optional[Tensor] = None, want_y: bool = False,
+                        rtab: Optional[Tensor] = None):
     """conv3_quant_rate on a split-form input. Returns (y_hat, bits_partial, y | None,
-    y_hat_split)."""
+    y_hat_split). rtab as ``conv3_quant_rate``."""
     _check_split(hs, "activation")
     _, B, h8, w8, N = hs.shape
     _check_channels(N)
@@ -396,7 +398,7 @@ def conv3_quant_rate_x6(hs: Tensor, wp: Tensor, rate_packed: Tensor,
     T = rate_partials_per_image(H, W, N)
     partial = torch.empty(B, T, device=hs.device, dtype=torch.float64)
     call("iclr17_analysis_conv3_quant_rate_x6", _p(hs), B, H, W, N, _p(wp), mode, _p(noise),
-         _p(rate_packed), _p(y), _p(y_hat), _p(y_hat_split), _p(partial), _stream(hs))
+         _p(rate_packed), _p(rtab), _p(y), _p(y_hat), _p(y_hat_split), _p(partial), _stream(hs))
     return y_hat, partial, y, y_hat_split
 
 

@@ -102,12 +102,16 @@ class ImageCompressor(nn.Module):
             hs, _, _ = kernels.conv1x6_gdn(x, self.Encoder.packed_conv1_x6(), self.Encoder.conv1.bias,
                                            e1[0], e1[2], N)
             hs, _, _ = kernels.conv2_gdn_x6(hs, w2, self.Encoder.conv2.bias, *e2)
-            q = kernels.conv3_quant_rate_x6(hs, w3, self.bitEstimator.packed(), noise, want_y=want_y)
+            rt = self.bitEstimator.rate_table() if noise is None else None
+            q = kernels.conv3_quant_rate_x6(hs, w3, self.bitEstimator.packed(), noise, want_y=want_y,
+                                            rtab=rt)
             y_split = q[3]
         else:
             h = kernels.conv1_gdn(x, w1, self.Encoder.conv1.bias, g1[0], g1[1], N)
             h = kernels.conv2_gdn(h, w2, self.Encoder.conv2.bias, g2[0], g2[1])
-            q = kernels.conv3_quant_rate(h, w3, self.bitEstimator.packed(), noise, want_y=want_y)
+            rt = self.bitEstimator.rate_table() if noise is None else None
+            q = kernels.conv3_quant_rate(h, w3, self.bitEstimator.packed(), noise, want_y=want_y,
+                                         rtab=rt)
             y_split = None
         return {"y_hat": q[0], "bits_partial": q[1], "y_split": y_split,
                 "y": q[2] if want_y else None}
@@ -221,12 +225,6 @@ class ImageCompressor(nn.Module):
         batched packing launch pair (kernels.batched_packs)."""
         x6 = kernels.precision() != "fp32"
         gdns = (self.Encoder.gdn1, self.Encoder.gdn2, self.Decoder.igdn1, self.Decoder.igdn2)
-        if kernels.precision() == "bf16" and not backward:
-            self.Encoder.packed_bf16()
-            self.Decoder.packed_bf16()
-            self.bitEstimator.rate_table()
-            for g in gdns:
-                g.effective_params_bf16()
         with kernels.batched_packs():
             self.Encoder.packed()
             self.Decoder.packed()
@@ -243,6 +241,13 @@ class ImageCompressor(nn.Module):
                         g.effective_params_bwd_x6()
                     else:
                         g.effective_params_bwd()
+        if not backward:   # eval: the rate table of the round quantiser (+ the bf16 layouts)
+            self.bitEstimator.rate_table()
+            if kernels.precision() == "bf16":
+                self.Encoder.packed_bf16()
+                self.Decoder.packed_bf16()
+                for g in gdns:
+                    g.effective_params_bf16()
 
     def evaluate_many(self, batches, want_y: bool = False,
                       want_msssim: bool = False):

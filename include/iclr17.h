@@ -117,11 +117,14 @@ int iclr17_analysis_conv2_gdn(const float* in, int B, int H, int W, int N, const
 /* analysis_17.py:22,35 + model.py:48-56,71-73 : y = conv3(h) (no bias); ŷ = round(y) or y+noise;
  * per-element rate bits summed per tile. in NHWC [B,H/8,W/8,N]; y_out, y_hat NHWC
  * [B,H/16,W/16,N] (y_out nullable); noise NCHW [B,N,H/16,W/16] (QUANT_NOISE only);
- * bits_partial[B * iclr17_rate_partials_per_image(H,W,N)] doubles. */
+ * bits_partial[B * iclr17_rate_partials_per_image(H,W,N)] doubles. rate_table (nullable;
+ * iclr17_rate_table of rate_packed): in round mode the bits of |ŷ| ≤ 32 are looked up instead
+ * of evaluating the factorised model (the same fp32 function, so the same values). */
 int iclr17_analysis_conv3_quant_rate(const float* in, int B, int H, int W, int N,
                                      const float* w_packed, int quant_mode, const float* noise,
-                                     const float* rate_packed, float* y_out, float* y_hat,
-                                     double* bits_partial, void* stream);
+                                     const float* rate_packed, const float* rate_table,
+                                     float* y_out, float* y_hat, double* bits_partial,
+                                     void* stream);
 int iclr17_rate_partials_per_image(int H, int W, int N);
 /* analysis_17.py:22,35 alone (Analysis_net_17.forward without the quantiser): y NHWC. */
 int iclr17_analysis_conv3(const float* in, int B, int H, int W, int N, const float* w_packed,
@@ -181,9 +184,9 @@ int iclr17_analysis_conv2_gdn_x6(const uint16_t* in_split, int B, int H, int W, 
  * The packed fp32 weights are split in the loop. */
 int iclr17_analysis_conv3_quant_rate_x6(const uint16_t* in_split, int B, int H, int W, int N,
                                         const float* w_packed, int quant_mode, const float* noise,
-                                        const float* rate_packed, float* y_out, float* y_hat,
-                                        uint16_t* y_hat_split, double* bits_partial,
-                                        void* stream);
+                                        const float* rate_packed, const float* rate_table,
+                                        float* y_out, float* y_hat, uint16_t* y_hat_split,
+                                        double* bits_partial, void* stream);
 /* iclr17_synthesis_deconv_igdn on a split-form input. */
 int iclr17_synthesis_deconv_igdn_x6(const uint16_t* in_split, int B, int h, int w, int N,
                                     const float* w_packed, const float* bias,

@@ -239,8 +239,9 @@ def test_rate_table_matches_element_bits(device):
     v = torch.arange(-32, 33, dtype=torch.float32).view(1, 1, 1, 65).expand(1, N, 1, 65).contiguous()
     ref = oracle.element_bits(v, sd)[0, :, 0, :]
     assert tab.shape == (N, 65)
-    # p = F(v+½) − F(v−½) cancels in fp32 far in the tails: there the device's and torch-CPU's
-    # ulp-level CDF differences dominate, so the 1e-5 bar applies where bits < 16 (p > 1.5e-5)
-    core = ref < 16
-    assert torch.allclose(tab[core], ref[core], rtol=1e-5, atol=1e-6)
-    assert torch.allclose(tab, ref, rtol=1e-2)
+    # p = F(v+½) − F(v−½) cancels in fp32: ulp-level differences δF between the device's and
+    # torch-CPU's CDFs move bits by ≈ δF / (p ln 2) = δF · 2^bits / ln 2; bound δF by 8 ulps of 1
+    tol = 1e-5 * ref + 8 * 2.0 ** -24 * torch.exp2(ref) / 0.6931
+    err = (tab - ref).abs()
+    print(f"rate table: max |Δbits| {err.max().item():.3e}, max |Δ|/tol {(err / tol).max().item():.3f}")
+    assert bool((err <= tol).all())

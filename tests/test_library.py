@@ -53,8 +53,8 @@ def test_argument_validation_without_gpu():
         _lib.call("iclr17_synthesis_deconv3", None, 1, 256, 256, 192, *[None] * 6, 0, None)
     with pytest.raises(_lib.Iclr17Error, match="quant mode"):
         _lib.call("iclr17_analysis_conv3_quant_rate", ctypes.c_void_p(16), 1, 256, 256, 192,
-                  ctypes.c_void_p(16), 1, None, ctypes.c_void_p(16), None, ctypes.c_void_p(16),
-                  ctypes.c_void_p(16), None)
+                  ctypes.c_void_p(16), 1, None, ctypes.c_void_p(16), None, None,
+                  ctypes.c_void_p(16), ctypes.c_void_p(16), None)
     assert "quant mode" in _lib.last_error()
 
 

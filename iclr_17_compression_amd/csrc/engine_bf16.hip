@@ -259,7 +259,7 @@ struct K5 {
   static constexpr int SB = 4 * NB * 16;        // weight stage bytes
   static constexpr int NBI = SB / 1024;         // weight DMA wave-instructions per step
   using P = Patch<MODE, TH>;
-  static constexpr int NST = 3;                 // weight stages (ring)
+  static constexpr int NST = 4;                 // weight stages (ring)
   static constexpr int MAIN_LDS = 2 * P::BUF + NST * SB + 1024;
   static constexpr int EPI_LDS = EPI == BE_QUANT ? 64 : epi_tile_bytes<CO>(R);
   static constexpr int LDS = MAIN_LDS > EPI_LDS ? MAIN_LDS : EPI_LDS;
@@ -280,11 +280,13 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
   const int wm = wave / WN, wn = wave % WN;
   const int kg = lane >> 4, half = kg & 1, hi = kg >> 1;
   // LDS-DMA schedule. Every step every wave issues exactly K DMA instructions (weights of step
-  // g+2 into a three-stage ring, pieces of the next chunk's patch, 1 KB sink loads as padding),
-  // so a counted `s_waitcnt vmcnt(K)` before the step's barrier retires everything but the
-  // previous step's group: the weights of step g (issued two steps earlier) and, at a chunk
-  // start, the whole patch (its pieces go out in the previous chunk's steps 0 .. S-2).
-  constexpr int NST = KK::NST, SI = S - 1;
+  // g+F+1 into a four-stage ring, pieces of the next chunk's patch, 1 KB sink loads as padding),
+  // so a counted `s_waitcnt vmcnt(F·K)` before the step's barrier retires everything but the
+  // last F steps' groups: the weights of step g and, at a chunk start, the whole patch (its
+  // pieces go out in the previous chunk's steps 0 .. S-F-1). F = 2 groups stay in flight where
+  // a chunk has ≥ 4 steps, else 1.
+  constexpr int NST = KK::NST, F = S >= 4 ? 2 : 1, SI = S - F;
+  static_assert(NST >= F + 2, "ring depth");
   constexpr int PS = (P::NQI + SI - 1) / SI;          // patch pieces per issuing step
   constexpr int K = (NBI + PS + NW - 1) / NW;         // DMA instructions per wave per step
   constexpr int GS = NCH * S;                         // steps
@@ -315,10 +317,11 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
     ok = ok && pr < P::ROWS && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
     return ok ? (iy * a.Win + ix) * CI + 8 * h : -1;
   };
-  auto issue_piece = [&](int c, int piece) {
-    const int src = piece_src(piece);
-    glds16(src >= 0 ? (const void*)(inb + src + c * 16) : (const void*)g_zero16,
-           sP + (c & 1) * P::BUF + piece * 1024);
+  // patch piece of chunk c1 (valid) or a sink load (not valid: same instruction count)
+  auto issue_piece = [&](int c1, int piece, bool valid) {
+    const int src = piece_src(valid ? piece : 0);
+    glds16(src >= 0 && valid ? (const void*)(inb + src + c1 * 16) : (const void*)g_zero16,
+           valid ? sP + (c1 & 1) * P::BUF + piece * 1024 : sD);
   };
   // weight slots: slot k·NW + wave < NBI of a group copies 1 KB of the step's [4][NB][8] slice
   const long wstep = 4L * CO * 8;                     // u16 per (chunk, step) of the packing
@@ -340,12 +343,12 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
     }
     wph += off;
   }
-  auto issue_w = [&](int k, int wg) {   // weight slot k of step wg (a sink load past the end)
+  // weight slot k of step wg; past the last step a load of the last step into the sink
+  auto issue_w = [&](int k, int wg) {
     const int slot = k * NW + wave;
-    if (wg < GS && (!(ICLR17_BFABL & 1) || wg < 2))
-      glds16(wph + (long)wg * wstep + wsrc[k], sB + (wg % NST) * SB + slot * 1024);
-    else
-      glds16(g_zero16, sD);
+    const bool ok = wg < GS && (!(ICLR17_BFABL & 1) || wg < 2);
+    glds16(wph + (long)(wg < GS ? wg : GS - 1) * wstep + wsrc[k],
+           ok ? sB + (wg & (NST - 1)) * SB + slot * 1024 : sD);
   };
 
   // ---- per-lane fragment addresses
@@ -363,16 +366,22 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = f4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: chunk 0's patch and step 0's weights (any count per wave), then step 1's weights
-  // as a full K-group
-  for (int piece = wave; piece < P::NQI; piece += NW) issue_piece(0, piece);
+  // prologue: chunk 0's patch and the weights of steps 0 .. F-1 (any count per wave), then
+  // step F's weights as a full K-group, so the loop's first wait leaves exactly F groups
+  for (int piece = wave; piece < P::NQI; piece += NW) issue_piece(0, piece, true);
 #pragma unroll
-  for (int k = 0; k < K; ++k)
-    if (k * NW + wave < NBI) issue_w(k, 0);
+  for (int f = 0; f < F; ++f)
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (k * NW + wave < NBI) issue_w(k, f);
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    if (k * NW + wave < NBI) issue_w(k, 1);
+    if (k * NW + wave < NBI) issue_w(k, F);
     else glds16(g_zero16, sD);
+  }
+  if constexpr (F == 2) {   // one more full group: the first wait keeps two in flight
+#pragma unroll
+    for (int k = 0; k < K; ++k) glds16(g_zero16, sD);
   }
 
   typedef const __attribute__((address_space(3))) u4* lu4p;
@@ -383,24 +392,25 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
     for (int s = 0; s < S; ++s) {
       const int g = c * S + s;
       if (!(ICLR17_BFABL & 4))
-        wait_vm_barrier<K>();   // all but the previous step's group landed: weights of step g and,
-                                // at s = 0, chunk c's patch; stage (g+2) % NST is free
+        wait_vm_barrier<F * K>();   // all but the last F groups landed: weights of step g and,
+                                    // at s = 0, chunk c's patch; stage (g+F+1) % NST is free
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const int slot = k * NW + wave;
-        if (slot < NBI) {
-          issue_w(k, g + 2);
-        } else {
+        if ((k + 1) * NW <= NBI || slot < NBI) {
+          issue_w(k, g + F + 1);
+        } else if (s < SI) {
           const int piece = s * PS + slot - NBI;
-          if (s < SI && c + 1 < NCH && piece < P::NQI && !(ICLR17_BFABL & 2)) issue_piece(c + 1, piece);
-          else glds16(g_zero16, sD);
+          issue_piece(c + 1, piece, c + 1 < NCH && piece < P::NQI && !(ICLR17_BFABL & 2));
+        } else {
+          glds16(g_zero16, sD);
         }
       }
       // tap pair (2s, 2s+1): lanes 0-31 the first, 32-63 the second
       const int t0 = P::template tap_off<PH>(2 * s), t1 = P::template tap_off<PH>(2 * s + 1);
       const unsigned char* pb = pbuf + t0 + hi * (t1 - t0);
       const unsigned char* wb = sB + stage * SB + abase;
-      stage = stage == NST - 1 ? 0 : stage + 1;
+      stage = (stage + 1) & (NST - 1);
       u4 wa[NT], px[MT];
       if (!(ICLR17_BFABL & 8) || g == 0) {
 #pragma unroll

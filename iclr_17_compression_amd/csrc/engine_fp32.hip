@@ -35,42 +35,10 @@
 
 namespace iclr17 {
 
-// Diagnostic ablation builds only (tools/ablate.sh, tools/ab.sh): -DICLR17_ABL=mask — 8 skips
-// the engine epilogue, 16 replaces conv1's patch gather by constants, 32 skips conv1's epilogue,
-// 64 / 128 skip the engine's A / B operand DMA after the first two steps, 256 replaces the x6 B
-// split by one pack, 512 makes the x6 A pieces contiguous (all: wrong values, timing only)
-#ifndef ICLR17_ABL
-#define ICLR17_ABL 0
-#endif
-
 constexpr int BM = 64;        // output pixels per tile
 
-#ifndef ICLR17_CONV3_BN
-#define ICLR17_CONV3_BN 96    // conv3 (+ quantiser) output columns per workgroup
-#endif
-#ifndef ICLR17_QSTAGES
-#define ICLR17_QSTAGES 2      // conv3's DMA ring depth (3, 4 measured slower: DESIGN.md §5)
-#endif
-#ifndef ICLR17_GDN_PLANES
-#define ICLR17_GDN_PLANES 1   // x6 GDN contraction: x² split once into LDS planes (not per wave)
-#endif
-#ifndef ICLR17_PL_PLANES
-#define ICLR17_PL_PLANES 0    // the planes path in the phase-loop deconv too (single B set)
-#endif
-#ifndef ICLR17_PHASE_MAJOR
-#define ICLR17_PHASE_MAJOR 1  // deconv phases dispatched phase-major (longest first)
-#endif
-#ifndef ICLR17_W8
-#define ICLR17_W8 0           // x6 GDN / IGDN layers on 128-pixel tiles, 8 waves (engine_kernel_w8)
-#endif
-#ifndef ICLR17_PL_MIN
-// deconv base tiles from which one workgroup runs all 4 phases (the phase loop). Off since the
-// phase-major dispatch and the LDS-plane GDN contraction: the per-phase workgroups are then
-// 1.5 % faster on deconv2 (512 enables it again).
-#define ICLR17_PL_MIN (1 << 30)
-#endif
-static_assert(ICLR17_QSTAGES >= 2 && ICLR17_QSTAGES <= 4, "conv3 ring depth");
-constexpr int conv3_bn(int N) { return N % ICLR17_CONV3_BN == 0 ? ICLR17_CONV3_BN : 64; }
+// conv3 (+ quantiser) output columns per workgroup: 96 at N = 192, 64 at N = 128
+constexpr int conv3_bn(int N) { return N % 96 == 0 ? 96 : 64; }
 
 enum Epi : int {
   EPI_GDN = 0, EPI_IGDN = 1, EPI_QUANT = 2, EPI_OUT3 = 3, EPI_PLAIN = 4,
@@ -122,7 +90,6 @@ struct EngineArgs {
   float* rpart;         // rate bwd: per-tile parameter partials [tiles][11][CO]
   float* colsum_out;    // GDN bwd: per-tile column sums of ∂u (the conv bias gradient) [tiles][CO]
   float* colsum_t;      // GDN bwd: per-tile column sums of dn (∂β_eff) [tiles][CO]
-  int phase_loop;       // 1: a workgroup runs every stride phase of its base block in turn
   // x6 mode: activations as three bf16 planes (hi, mid, lo; x = hi + mid + lo exactly)
   const unsigned short* in_split;   // [3][B][Hin][Win][CI]
   long in_plane;                    // plane stride (elements)
@@ -142,23 +109,15 @@ __device__ __forceinline__ TileInfo decode_tile(const EngineArgs& a) {
   TileInfo t;
   t.th = TH;
   int bid = blockIdx.x;
-#if ICLR17_PHASE_MAJOR
   // stride phases in dispatch order 0..3 (9, 6, 6, 4 taps): longest workgroups first
   const int per_ph = a.tiles_x * a.tiles_y * a.B;
-  const int phm = a.phase_loop ? 0 : bid / per_ph;
-  if (!a.phase_loop) bid -= phm * per_ph;
-#endif
+  const int ph = bid / per_ph;
+  bid -= ph * per_ph;
   t.tx = bid % a.tiles_x;
   bid /= a.tiles_x;
   t.ty = bid % a.tiles_y;
   bid /= a.tiles_y;
-#if ICLR17_PHASE_MAJOR
-  const int ph = phm;
   t.b = bid;
-#else
-  const int ph = a.phase_loop ? 0 : bid % a.tt.nph;
-  t.b = a.phase_loop ? bid : bid / a.tt.nph;
-#endif
   t.py = ph / a.tt.npx;
   t.px = ph % a.tt.npx;
   t.nb = blockIdx.y;
@@ -421,13 +380,6 @@ __device__ __forceinline__ void chan_gemm_x6(f4 (&acc)[MT][NT], const float* sX,
       }
     }
   };
-#ifdef ICLR17_G6_SINGLE
-  for (int kb = 0; kb < KB; ++kb) {   // one B register set: fewer VGPRs, loads not overlapped
-    load(kb, b0);
-    block(kb, b0);
-  }
-  (void)b1;
-#else
   load(0, b0);
   for (int kb = 0; kb < KB; kb += 2) {
     load(kb + 1, b1);
@@ -435,13 +387,12 @@ __device__ __forceinline__ void chan_gemm_x6(f4 (&acc)[MT][NT], const float* sX,
     if (kb + 2 < KB) load(kb + 2, b0);
     block(kb + 1, b1);
   }
-#endif
 }
 
 // The same x6 contraction with the A operand already split in LDS: three bf16 planes
 // [3][R][CO+8] (u16), written once by the producing waves, so no wave splits rows in VALU (with
 // one wave row every wave used to split the whole x² tile for itself).
-template <int CO, int MT, int NT, int R, bool SINGLE_B = false>
+template <int CO, int MT, int NT, int R>
 __device__ __forceinline__ void chan_gemm_x6p(f4 (&acc)[MT][NT], const unsigned short* sP,
                                               const unsigned short* __restrict__ g6, int wm,
                                               int ncol0, int lane) {
@@ -484,42 +435,33 @@ __device__ __forceinline__ void chan_gemm_x6p(f4 (&acc)[MT][NT], const unsigned 
       }
     }
   };
-  if constexpr (SINGLE_B) {   // one B register set (the 256-VGPR phase-loop instance)
-    for (int kb = 0; kb < KB; ++kb) {
-      load(kb, b0);
-      block(kb, b0);
-    }
-    (void)b1;
-  } else {
-    load(0, b0);
-    for (int kb = 0; kb < KB; kb += 2) {
-      load(kb + 1, b1);
-      block(kb, b0);
-      if (kb + 2 < KB) load(kb + 2, b0);
-      block(kb + 1, b1);
-    }
+  load(0, b0);
+  for (int kb = 0; kb < KB; kb += 2) {
+    load(kb + 1, b1);
+    block(kb, b0);
+    if (kb + 2 < KB) load(kb + 2, b0);
+    block(kb + 1, b1);
   }
 }
 
 // LDS floats the GDN core needs for an R-row tile (fp32 x² tile + γ stages, or, for the x6
 // contraction, the three split planes of x²).
-constexpr int gdn_lds_floats(int R, int CO, bool G6, bool GPL = ICLR17_GDN_PLANES) {
-  return G6 && GPL ? (3 * R * (CO + 8) + 1) / 2 : R * (CO + 8) + GSTAGE_FLOATS(CO);
+constexpr int gdn_lds_floats(int R, int CO, bool G6) {
+  return G6 ? (3 * R * (CO + 8) + 1) / 2 : R * (CO + 8) + GSTAGE_FLOATS(CO);
 }
 
 // x (bias already added) in accumulator layout → GDN(x) (or IGDN) left in LDS sX[BM][CO+4].
 // models/GDN.py:83-90: n = conv2d(x², γ, β) = β + Σ_j γ[i][j]·x_j²;  y = x / √n | x·√n.
 // The caller guarantees smem is free on entry; on return every wave has passed a barrier after
 // the last sX write.
-template <int CO, int MT, int NT, bool INVERSE, int R = BM, int T = 256, bool G6 = false,
-          bool GPL = ICLR17_GDN_PLANES, bool SINGLE_B = false>
+template <int CO, int MT, int NT, bool INVERSE, int R = BM, int T = 256, bool G6 = false>
 __device__ __forceinline__ void gdn_core(const f4 (&x)[MT][NT], float* sX,
                                          const float* __restrict__ gbeta,
                                          const float* __restrict__ gp, int wm, int ncol0,
                                          int lane, const unsigned short* g6 = nullptr) {
   constexpr int XS = CO + 8;
   f4 nacc[MT][NT];
-  if constexpr (G6 && GPL) {
+  if constexpr (G6) {
     // x² (rounded to fp32, as conv2d(x², γ) sees it) split once into three bf16 planes
     unsigned short* sP = (unsigned short*)sX;
 #pragma unroll
@@ -540,7 +482,7 @@ __device__ __forceinline__ void gdn_core(const f4 (&x)[MT][NT], float* sX,
           sP[(2 * R + row) * XS + col] = (unsigned short)(l >> 16);
         }
     __syncthreads();   // planes of every wave published
-    chan_gemm_x6p<CO, MT, NT, R, SINGLE_B>(nacc, sP, g6, wm, ncol0, lane);
+    chan_gemm_x6p<CO, MT, NT, R>(nacc, sP, g6, wm, ncol0, lane);
   } else {
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
@@ -553,12 +495,6 @@ __device__ __forceinline__ void gdn_core(const f4 (&x)[MT][NT], float* sX,
         const float v = x[mt][nt][r];
         sX[row * XS + col] = v * v;
       }
-  }
-  if constexpr (G6 && GPL) {
-  } else if constexpr (G6) {
-    __syncthreads();   // x² of every wave published
-    chan_gemm_x6<CO, MT, NT>(nacc, sX, g6, wm, ncol0, lane);
-  } else {
     chan_gemm_lds<CO, MT, NT, false, T / 64>(nacc, sX, gp, sX + R * XS, wm, ncol0, lane,
                                              __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
   }
@@ -593,13 +529,12 @@ __device__ __forceinline__ void acc_to_lds(const f4 (&v)[MT][NT], float* s, int 
       }
 }
 
-template <int CO, int MT, int NT, bool INVERSE, int R = BM, int T = 256, bool G6 = false,
-          bool GPL = ICLR17_GDN_PLANES, bool SINGLE_B = false>
+template <int CO, int MT, int NT, bool INVERSE, int R = BM, int T = 256, bool G6 = false>
 __device__ __forceinline__ void gdn_epilogue(f4 (&x)[MT][NT], float* smem, const EngineArgs& a,
                                              const TileInfo& t, int wm, int ncol0, int lane) {
   constexpr int XS = CO + 8;
-  gdn_core<CO, MT, NT, INVERSE, R, T, G6, GPL, SINGLE_B>(x, smem, a.gbeta, a.ggamma, wm, ncol0,
-                                                         lane, a.ggamma6);
+  gdn_core<CO, MT, NT, INVERSE, R, T, G6>(x, smem, a.gbeta, a.ggamma, wm, ncol0, lane,
+                                          a.ggamma6);
   if (a.out != nullptr) store_tile_rows<CO, R, T>(a, t, smem, XS, a.out, CO, 0);
   if (a.out_split != nullptr) store_tile_rows_split<CO, R, T>(a, t, smem, XS, CO, 0);
   if (a.pre != nullptr) {
@@ -927,7 +862,7 @@ __device__ __forceinline__ void out3_epilogue(f4 (&acc)[MT][NT], float* smem, co
 // columns in VALU. One 32-deep step = per 16×16 tile six v_mfma_f32_16x16x32_bf16:
 // lo·hi + hi·lo + mid·mid + mid·hi + hi·mid + hi·hi (the dropped mid·lo, lo·mid, lo·lo terms are
 // below 2^-24 of the product), accumulated in fp32.
-template <int CI, int CO, int BN, int WM, int WN, int EPI, bool PL, bool X6, int BMT = BM>
+template <int CI, int CO, int BN, int WM, int WN, int EPI, bool X6, int BMT = BM>
 __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   constexpr int NWV = WM * WN;                   // waves (4, or 8 for the 128-row tiles)
   constexpr int MT = BMT / WM / 16;
@@ -944,12 +879,9 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   constexpr int API = BMT / 16;                  // x6: A wave-instructions per plane (16 rows each)
   // DMA ring depth: conv3 (+ quantiser) has a third of conv2's MFMAs per step, too few to hide
   // an L2-miss DMA issued one step ahead, so it runs NS stages with a counted vmcnt wait.
-  constexpr int NS = (EPI == EPI_QUANT && X6) ? ICLR17_QSTAGES : 2;
-  constexpr int LDS_A = NS * STAGE;
+  constexpr int LDS_A = 2 * STAGE;   // two-stage ring (3, 4 stages measured slower: DESIGN.md §5)
   constexpr int LDS_XF = BMT * (CO + 8) + GSTAGE_FLOATS(CO);
-  // x6 GDN planes, except in the phase-loop instance (held to 256 VGPRs: the planes path spills)
-  constexpr bool GPL = ICLR17_GDN_PLANES && (!PL || ICLR17_PL_PLANES);
-  constexpr int LDS_XP = gdn_lds_floats(BMT, CO, X6, GPL);
+  constexpr int LDS_XP = gdn_lds_floats(BMT, CO, X6);
   constexpr int LDS_X = (EPI == EPI_GDN || EPI == EPI_IGDN) ? (LDS_XF > LDS_XP ? LDS_XF : LDS_XP)
                         : (EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD) ? LDS_XF : 0;
   constexpr int LDS_O = BMT * (BN + 4) + 8;
@@ -964,15 +896,13 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   static_assert(CI % KCH == 0 && NAI % NWV == 0, "k-step split");
   static_assert(BN == CO || BN % 16 == 0, "B image: quad rows of BN columns");
   static_assert((SB * 4) % 1024 == 0, "B image in whole wave-instructions");
-  static_assert(NS == 2 || NBI % 4 == 0, "counted vmcnt: equal DMA count per wave");
   __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (scalar branches)
   const int wm = wave / WN, wn = wave % WN;
   TileInfo t = decode_tile<BMT / 8>(a);
-  const int ph_first = t.py * a.tt.npx + t.px;
-  const int ph_end = PL ? a.tt.nph : ph_first + 1;   // PL: the phase loop (a.phase_loop = 1)
+  const int ph = t.py * a.tt.npx + t.px;
   const int ncol0 = t.nb * BN + wn * (BN / WN);
 
   // A DMA. fp32: wave-instruction i covers rows 8i .. 8i+7; lane → (row, physical chunk
@@ -1005,33 +935,23 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   }
 
   int t0 = 0, ntaps = 1;
-  // Step order: tap-major (the 6 channel chunks of a tap in a row). Chunk-major order
-  // (-DICLR17_CHUNKMAJOR) keeps a workgroup's input footprint to one chunk and cuts the HBM
-  // refetch 3-5x, but measured 3-6 % slower on the same box: these layers are
-  // bound by MFMA issue, and the Infinity Cache absorbs the L2 misses.
+  // Step order: tap-major (the 6 channel chunks of a tap in a row). Chunk-major order keeps a
+  // workgroup's input footprint to one chunk and cuts the HBM refetch 3-5x, but measured 3-6 %
+  // slower on the same box: these layers are bound by MFMA issue, and the
+  // Infinity Cache absorbs the L2 misses.
   auto issue = [&](int s, int buf) {
-#ifdef ICLR17_CHUNKMAJOR
-    const int cc = s / ntaps, tap = t0 + s - cc * ntaps;
-#else
     const int tap = t0 + s / NCH, cc = s - (s / NCH) * NCH;
-#endif
     const int td = a.tt.dydx[tap];
     const int dy = (td & 0xff) - 128, dx = ((td >> 8) & 0xff) - 128;
     const int so = (dy * a.Win + dx) * CI + cc * KCH;
     float* sa = smem + buf * STAGE;
-    const bool skip_a = (ICLR17_ABL & 64) && s > 1, skip_b = (ICLR17_ABL & 128) && s > 1;
 #pragma unroll
     for (int j = 0; j < AI_W; ++j) {
-      if (skip_a) break;
       const bool ok = rval[j] && (unsigned)(iy0[j] + dy) < (unsigned)a.Hin &&
                       (unsigned)(ix0[j] + dx) < (unsigned)a.Win;
       const int i = wave * AI_W + j;
       if constexpr (X6) {
         const unsigned short* src = inb6 + (i / API) * a.in_plane + pbase[j] + so;
-        if (ICLR17_ABL & 512) {   // within [image start, this lane's valid pixel] of the plane
-          const int e = pbase[j] + so, base = (e & ~511) >= 512 ? (e & ~511) - 512 : 0;
-          src = inb6 + (i / API) * a.in_plane + base + (e >= 512 ? lane * 8 : 0);
-        }
         glds16(ok ? (const float*)src : g_zero16, sa + i * 256);
       } else {
         glds16(ok ? inb + pbase[j] + so : g_zero16, sa + i * 256);
@@ -1042,7 +962,6 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
 #pragma unroll
     for (int j = 0; j < BI_W; ++j) {
       const int i = wave + NWV * j;
-      if (skip_b) break;
       if (NBI % NWV == 0 || i < NBI) glds16(ws + bsrc[j], sb + i * 256);
     }
   };
@@ -1075,16 +994,7 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       u4 bh, bm, bl;
-      if (ICLR17_ABL & 256) {
-        const f4 x0 = *(const f4*)(sb + nt * 64), x1 = *(const f4*)(sb + BN * 4 + nt * 64);
-        bh = u4{__builtin_amdgcn_perm(__float_as_uint(x0[1]), __float_as_uint(x0[0]), 0x07060302u),
-                __builtin_amdgcn_perm(__float_as_uint(x0[3]), __float_as_uint(x0[2]), 0x07060302u),
-                __builtin_amdgcn_perm(__float_as_uint(x1[1]), __float_as_uint(x1[0]), 0x07060302u),
-                __builtin_amdgcn_perm(__float_as_uint(x1[3]), __float_as_uint(x1[2]), 0x07060302u)};
-        bm = bh ^ 1u;
-        bl = bh ^ 2u;
-      } else
-        split8(*(const f4*)(sb + nt * 64), *(const f4*)(sb + BN * 4 + nt * 64), bh, bm, bl);
+      split8(*(const f4*)(sb + nt * 64), *(const f4*)(sb + BN * 4 + nt * 64), bh, bm, bl);
       Bh[nt] = __builtin_bit_cast(bf8, bh);
       Bm[nt] = __builtin_bit_cast(bf8, bm);
       Bl[nt] = __builtin_bit_cast(bf8, bl);
@@ -1125,9 +1035,6 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
     }
   };
 
-  for (int ph = ph_first; ph < ph_end; ++ph) {
-  t.py = ph / a.tt.npx;
-  t.px = ph - t.py * a.tt.npx;
   t0 = a.tt.begin[ph];
   ntaps = a.tt.begin[ph + 1] - t0;
   const int nsteps = ntaps * NCH;
@@ -1137,41 +1044,12 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
     for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
 
   issue(0, 0);
-  if constexpr (NS == 2) {
-    for (int s = 0; s < nsteps; ++s) {
-      __syncthreads();   // vmcnt(0) + barrier: step s landed for every wave; stage (s+1)&1 is free
-      if (s + 1 < nsteps) issue(s + 1, (s + 1) & 1);
-      compute(s & 1);
-    }
-  } else {
-    // NS-stage ring: steps s+1 .. s+NS-2 stay in flight while step s is waited for (each wave
-    // issues exactly AI_W + BI_W DMA instructions per step, and nothing else touches vmcnt).
-    constexpr int PER = AI_W + BI_W;
-#pragma unroll
-    for (int j = 1; j < NS - 1; ++j)
-      if (j < nsteps) issue(j, j);
-    int buf = 0;
-    for (int s = 0; s < nsteps; ++s) {
-      const int ahead = nsteps - 1 - s < NS - 2 ? nsteps - 1 - s : NS - 2;   // steps in flight
-      if (ahead >= 2) wait_vmcnt_barrier<2 * PER>();
-      else if (ahead == 1) wait_vmcnt_barrier<PER>();
-      else wait_vmcnt_barrier<0>();
-      // every wave is past compute(s-1): its stage, (s + NS - 1) % NS, is free
-      if (s + NS - 1 < nsteps) issue(s + NS - 1, buf == 0 ? NS - 1 : buf - 1);
-      compute(buf);
-      buf = buf + 1 == NS ? 0 : buf + 1;
-    }
+  for (int s = 0; s < nsteps; ++s) {
+    __syncthreads();   // vmcnt(0) + barrier: step s landed for every wave; stage (s+1)&1 is free
+    if (s + 1 < nsteps) issue(s + 1, (s + 1) & 1);
+    compute(s & 1);
   }
   __syncthreads();     // last stage reads done before the epilogue reuses LDS
-  if (ICLR17_ABL & 8) {   // diagnostic: keep the accumulators live, skip the epilogue
-    float sum = 0.f;
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) sum += acc[mt][nt][0] + acc[mt][nt][1] + acc[mt][nt][2] + acc[mt][nt][3];
-    if (sum == 12345.f) a.out[0] = sum;
-    continue;
-  }
 
   if constexpr (EPI == EPI_GDN || EPI == EPI_IGDN) {
     static_assert(BN == CO, "GDN fusion needs every channel of a pixel in the workgroup");
@@ -1181,8 +1059,8 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
       for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[mt][nt][r] += a.bias[ncol0 + nt * 16 + (lane & 15)];
-    gdn_epilogue<CO, MT, NT, EPI == EPI_IGDN, BMT, NWV * 64, X6, GPL, PL>(acc, smem, a, t, wm,
-                                                                         ncol0, lane);
+    gdn_epilogue<CO, MT, NT, EPI == EPI_IGDN, BMT, NWV * 64, X6>(acc, smem, a, t, wm, ncol0,
+                                                                lane);
   } else if constexpr (EPI == EPI_QUANT) {
     quant_epilogue<CO, BN, MT, NT, WN>(acc, smem, a, t, wm, ncol0, lane, wave);
   } else if constexpr (EPI == EPI_OUT3) {
@@ -1209,28 +1087,18 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
     __syncthreads();
     store_tile_rows<BN>(a, t, smem, OS, a.out, CO, t.nb * BN);
   }
-  if (ph + 1 < ph_end) __syncthreads();   // epilogue LDS reads done before the next phase's DMA
-  }  // phase loop
 }
 
-template <int CI, int CO, int BN, int WM, int WN, int EPI, bool PL = false, bool X6 = false>
+template <int CI, int CO, int BN, int WM, int WN, int EPI, bool X6 = false>
 __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
-  engine_body<CI, CO, BN, WM, WN, EPI, PL, X6, BM>(a);
-}
-
-// 128-pixel tiles (16×8 base pixels) on 8 waves (2 × 4), one workgroup per CU at two waves per
-// SIMD: the weight slice of a k-step feeds twice the pixels, so a CU moves 48 KB per step for the
-// work two 64-pixel workgroups did with 72 KB. The x6 GDN / IGDN layers (ICLR17_W8).
-template <int CI, int CO, int EPI, bool PL>
-__global__ void __launch_bounds__(512) engine_kernel_w8(const EngineArgs a) {
-  engine_body<CI, CO, CO, 2, 4, EPI, PL, true, 128>(a);
+  engine_body<CI, CO, BN, WM, WN, EPI, X6, BM>(a);
 }
 
 // The same kernel held to 256 VGPRs (2 waves per SIMD) where the compiler would otherwise just
-// exceed it (the phase-loop x6 IGDN instance).
-template <int CI, int CO, int BN, int WM, int WN, int EPI, bool PL = false, bool X6 = false>
+// exceed it (the x6 GDN / IGDN backward instances).
+template <int CI, int CO, int BN, int WM, int WN, int EPI, bool X6 = false>
 __global__ void __launch_bounds__(256, 2) engine_kernel_occ2(const EngineArgs a) {
-  engine_body<CI, CO, BN, WM, WN, EPI, PL, X6>(a);
+  engine_body<CI, CO, BN, WM, WN, EPI, X6>(a);
 }
 
 // --------------------------------------------------------------- deconv3, x6 halo kernel
@@ -1262,9 +1130,6 @@ constexpr int D3_LDS = D3_SA + 2 * D3_SB;
 // one with dx = −1 only rx = 0 (the packed weights are zero elsewhere), so with this order the
 // three dy = −1 taps need tile 0 alone and the two other dx = −1 taps tiles 0–1: 19 tile-taps
 // per chunk instead of 27. The skipped products are exact zeros, so results are unchanged.
-#ifndef ICLR17_D3_SKIP
-#define ICLR17_D3_SKIP 1
-#endif
 __device__ __forceinline__ int d3_col(int j) {
   int ry, rx, co;
   if (j < 12) {          // ry = 0
@@ -1345,7 +1210,7 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
   int pcol[NT];   // packed column of this lane in tile nt
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
-    pcol[nt] = !ICLR17_D3_SKIP ? nt * 16 + (lane & 15) : d3_col(nt * 16 + (lane & 15));
+    pcol[nt] = d3_col(nt * 16 + (lane & 15));
 
   auto compute = [&](int buf, int tap, auto ntt) {
     constexpr int NTT = decltype(ntt)::value;   // tiles this tap touches
@@ -1407,9 +1272,9 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
     __syncthreads();   // vmcnt(0) + barrier: A (at a chunk start) and B of step s landed
     const int tap = s - (s / 9) * 9;
     if (s + 1 < NSTEP && tap != 8) issue_b(s + 1, (s + 1) & 1);
-    if (ICLR17_D3_SKIP && tap < 3)
+    if (tap < 3)
       compute(s & 1, tap, std::integral_constant<int, 1>{});
-    else if (ICLR17_D3_SKIP && (tap == 3 || tap == 6))
+    else if (tap == 3 || tap == 6)
       compute(s & 1, tap, std::integral_constant<int, 2>{});
     else
       compute(s & 1, tap, std::integral_constant<int, 3>{});
@@ -1583,21 +1448,12 @@ __global__ void __launch_bounds__(256) conv1_gdn_kernel(const EngineArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int o = ko[e] == P1ZERO ? P1ZERO : ko[e] + moff[mt];
-          af[mt][e] = (ICLR17_ABL & 16) ? (float)(o + e) : smem[o];
+          af[mt][e] = smem[o];
         }
       mfma_block<MT, NT>(acc, af, bf);
     }
   }
   __syncthreads();  // patch reads done before the epilogue reuses LDS
-  if (ICLR17_ABL & 32) {   // diagnostic: skip the epilogue
-    float sum = 0.f;
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) sum += acc[mt][nt][0] + acc[mt][nt][1] + acc[mt][nt][2] + acc[mt][nt][3];
-    if (sum == 12345.f) a.out[0] = sum;
-    return;
-  }
   if constexpr (EPI == EPI_GDN) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
@@ -2127,7 +1983,7 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
     a.partials_per_image = a.tiles_x * a.tiles_y * (N / BN);
     dim3 grid(a.tiles_x * a.tiles_y * B, N / BN);
     if (X6in)
-      hipLaunchKernelGGL((engine_kernel<N, N, BN, WM, WN, EPI_QUANT, false, true>), grid,
+      hipLaunchKernelGGL((engine_kernel<N, N, BN, WM, WN, EPI_QUANT, true>), grid,
                          dim3(256), 0, st, a);
     else
       hipLaunchKernelGGL((engine_kernel<N, N, BN, WM, WN, EPI_QUANT>), grid, dim3(256), 0, st, a);
@@ -2136,7 +1992,7 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
     constexpr int BN = 64;
     dim3 grid(a.tiles_x * a.tiles_y * B, N / BN);
     if (EPI == EPI_RATE_BWD && X6in)
-      hipLaunchKernelGGL((engine_kernel<N, N, BN, 1, 4, EPI, false, true>), grid, dim3(256), 0,
+      hipLaunchKernelGGL((engine_kernel<N, N, BN, 1, 4, EPI, true>), grid, dim3(256), 0,
                          st, a);
     else
       hipLaunchKernelGGL((engine_kernel<N, N, BN, 1, 4, EPI>), grid, dim3(256), 0, st, a);
@@ -2144,20 +2000,14 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
   } else {
     dim3 grid(a.tiles_x * a.tiles_y * B, 1);
     if constexpr (EPI == EPI_GDN) {
-      if (X6in && ICLR17_W8) {   // 128-pixel tiles on 8 waves
-        a.tiles_y = (a.gh + 15) / 16;
-        hipLaunchKernelGGL((engine_kernel_w8<N, N, EPI, false>), dim3(a.tiles_x * a.tiles_y * B),
-                           dim3(512), 0, st, a);
-        return check_launch("conv2_gdn");
-      }
       if (X6in) {
-        hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI, false, true>), grid, dim3(256), 0,
+        hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI, true>), grid, dim3(256), 0,
                            st, a);
         return check_launch("conv2_gdn");
       }
     } else if constexpr (EPI == EPI_IGDN_BWD) {
       if (X6in) {   // held to 256 VGPRs: two waves per SIMD
-        hipLaunchKernelGGL((engine_kernel_occ2<N, N, N, 1, 4, EPI, false, true>), grid, dim3(256),
+        hipLaunchKernelGGL((engine_kernel_occ2<N, N, N, 1, 4, EPI, true>), grid, dim3(256),
                            0, st, a);
         return check_launch("bwd_deconv_igdn");
       }
@@ -2180,39 +2030,17 @@ int launch_deconv5(const float* in, int B, int h, int w, const float* wp, const 
   a.gh = h; a.gw = w; a.tiles_y = (h + 7) / 8; a.tiles_x = (w + 7) / 8;
   a.sin = 1; a.sout = 2;
   fill_deconv_taps(a.tt, 5, 2, 2);
-  // Forward: one workgroup per base block running the 4 phases (9/6/6/4 taps) in turn — equal
-  // work per workgroup, shared input neighbourhood — when that still fills 2 workgroups per CU.
+  // one workgroup per (base tile, stride phase), phase-major: the 9-tap phase first
   const int base_tiles = a.tiles_x * a.tiles_y * B;
-#ifdef ICLR17_NO_PL
-  a.phase_loop = 0;
-#else
-  a.phase_loop = (EPI == EPI_IGDN && base_tiles >= ICLR17_PL_MIN) ? 1 : 0;
-#endif
   if constexpr (EPI == EPI_IGDN) {
-    const bool X6in = a.in_split != nullptr;
-    if (X6in && ICLR17_W8) {   // 128-pixel tiles on 8 waves (phase loop when the grid is large)
-      a.tiles_y = (h + 15) / 16;
-      const int bt = a.tiles_x * a.tiles_y * B;
-      a.phase_loop = bt >= ICLR17_PL_MIN / 2 ? 1 : 0;
-      if (a.phase_loop)
-        hipLaunchKernelGGL((engine_kernel_w8<N, N, EPI, true>), dim3(bt), dim3(512), 0, st, a);
-      else
-        hipLaunchKernelGGL((engine_kernel_w8<N, N, EPI, false>), dim3(bt * 4), dim3(512), 0, st, a);
+    if (a.in_split != nullptr) {
+      hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI, true>), dim3(base_tiles * 4),
+                         dim3(256), 0, st, a);
       return check_launch("deconv_igdn");
     }
-    if (a.phase_loop && X6in)
-      hipLaunchKernelGGL((engine_kernel_occ2<N, N, N, 1, 4, EPI, true, true>), dim3(base_tiles),
-                         dim3(256), 0, st, a);
-    else if (a.phase_loop)
-      hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI, true>), dim3(base_tiles), dim3(256),
-                         0, st, a);
-    else if (X6in)
-      hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI, false, true>), dim3(base_tiles * 4),
-                         dim3(256), 0, st, a);
-    if (a.phase_loop || X6in) return check_launch("deconv_igdn");
   } else {
     if (a.in_split != nullptr) {   // held to 256 VGPRs: two waves per SIMD
-      hipLaunchKernelGGL((engine_kernel_occ2<N, N, N, 1, 4, EPI, false, true>),
+      hipLaunchKernelGGL((engine_kernel_occ2<N, N, N, 1, 4, EPI, true>),
                          dim3(base_tiles * 4), dim3(256), 0, st, a);
       return check_launch("bwd_conv_gdn");
     }

@@ -367,9 +367,6 @@ __device__ __forceinline__ void split4(const f4& x, uint2& hi, uint2& mi, uint2&
   lo = uint2{__builtin_amdgcn_perm(l[1], l[0], 0x07060302u), __builtin_amdgcn_perm(l[3], l[2], 0x07060302u)};
 }
 
-#ifndef ICLR17_GDN6_PF2
-#define ICLR17_GDN6_PF2 0   // 1: dn loads two steps ahead (6 VGPRs spill at C = 192)
-#endif
 template <int C>
 __global__ void __launch_bounds__(512) gdn_wgrad_x6_kernel(const float* __restrict__ G,
                                                              const float* __restrict__ X, long P,
@@ -401,7 +398,7 @@ __global__ void __launch_bounds__(512) gdn_wgrad_x6_kernel(const float* __restri
     wofs[v] = r * C + (((ch >> 3) ^ swz6(r, C)) << 3) + (ch & 7);
   }
   // dn pieces run two steps ahead (two register sets), u pieces one step
-  f4 rga[NV], rgb[NV], rx[NV];
+  f4 rga[NV], rx[NV];
   auto load_one = [&](const float* base, int s, f4 (&r)[NV]) {
     const long pb = p0 + (long)s * KP;
     const float* b = base + pb * C;
@@ -484,7 +481,6 @@ __global__ void __launch_bounds__(512) gdn_wgrad_x6_kernel(const float* __restri
     load_one(X, 0, rx);
     convert(0, rga, rx);
   }
-#if !ICLR17_GDN6_PF2
   for (int s = 0; s < nsteps; ++s) {
     __syncthreads();   // buffer s & 1 holds step s; the other one is no longer read
     if (s + 1 < nsteps) {
@@ -494,23 +490,6 @@ __global__ void __launch_bounds__(512) gdn_wgrad_x6_kernel(const float* __restri
     compute(s & 1);
     if (s + 1 < nsteps) convert((s + 1) & 1, rga, rx);
   }
-  (void)rgb;
-#else
-  if (nsteps > 1) load_one(G, 1, rgb);
-  for (int s = 0; s < nsteps; s += 2) {
-    __syncthreads();   // buffer 0 holds step s; buffer 1 no longer read
-    if (s + 1 < nsteps) load_one(X, s + 1, rx);
-    if (s + 2 < nsteps) load_one(G, s + 2, rga);
-    compute(0);
-    if (s + 1 >= nsteps) break;
-    convert(1, rgb, rx);
-    __syncthreads();   // buffer 1 holds step s + 1; buffer 0 no longer read
-    if (s + 2 < nsteps) load_one(X, s + 2, rx);
-    if (s + 3 < nsteps) load_one(G, s + 3, rgb);
-    compute(1);
-    if (s + 2 < nsteps) convert(0, rga, rx);
-  }
-#endif
   float* out = part + (long)split * C * C;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)

@@ -139,6 +139,7 @@ class Step:
             ev(5)
             clipped, _, _ = kernels.deconv3(h, d3, net.Decoder.deconv3.bias)
         ev(6)
+        self.last_partial = partial
         _, bpp = kernels.reduce_partials(partial, self.scale, per_image=False)
         ev(7)
         return clipped, y_hat, bpp
@@ -344,11 +345,20 @@ def run_codec(args, dev):
     }
 
 
+def cpu_threads() -> tuple:
+    """(threads used, cores in this process's affinity mask): every affinity core, unless the
+    box's CPU share is pinned by OMP_NUM_THREADS (16 on the GPU pool, whose affinity mask shows
+    the whole machine)."""
+    aff = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return (min(aff, int(omp)) if omp.isdigit() and int(omp) > 0 else aff), aff
+
+
 def cpu_baseline(N: int, H: int, W: int, budget_s: float) -> dict:
     """The oracle (op-for-op restatement of the reference forward, bit-identical to it on the
     build host) timed on this host's cores on a bounded sample."""
     from oracle import codec_ref as oracle
-    cores = min(16, len(os.sched_getaffinity(0)))
+    cores, aff = cpu_threads()
     torch.set_num_threads(cores)
     sd = oracle.state_dict_to_torch(synth.trained_like_state_dict(N, 1))
     B = 4
@@ -363,24 +373,136 @@ def cpu_baseline(N: int, H: int, W: int, budget_s: float) -> dict:
                 break
         dt = time.perf_counter() - t0
     return {"value": round(n * B * H * W / dt / 1e6, 4), "unit": "Mpix/s", "cores": cores,
-            "kind": "port",
-            "sample": f"{n} x eval forward of B={B} {H}x{W} images, N={N}, fp32 torch CPU "
-                      f"({dt:.1f} s, {platform.processor() or platform.machine()})"}
+            "affinity_cores": aff, "kind": "port",
+            "sample": f"{n} x eval forward of B={B} {H}x{W} images, N={N}, fp32 torch CPU, "
+                      f"{cores} threads ({dt:.1f} s, {platform.processor() or platform.machine()})"}
+
+
+def cpu_baseline_train(N: int, S: int, budget_s: float) -> dict:
+    """The training step of the reference on the CPU: the oracle's rd_loss (model.py:47-80 with
+    the uniform-noise quantiser, λ·MSE + bpp) forward + autograd backward + torch Adam with the
+    ±5 gradient clamp (train.py:115-120), timed on a bounded sample of B=2 crops."""
+    from oracle import codec_ref as oracle
+    cores, aff = cpu_threads()
+    torch.set_num_threads(cores)
+    sd = oracle.state_dict_to_torch(synth.trained_like_state_dict(N, 2))
+    params = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    opt = torch.optim.Adam(list(params.values()), lr=1e-4)
+    B = 2
+    x = torch.from_numpy(synth.to_unit_float(synth.image_u8(98, B, S, S)))
+    lam = 0.01 * 255.0 ** 2
+
+    def step(i):
+        noise = torch.from_numpy(synth.uniform(500 + i, (B, N, S // 16, S // 16), -0.5, 0.5))
+        opt.zero_grad(set_to_none=True)
+        loss, _, _ = oracle.rd_loss(x, params, noise, lam)
+        loss.backward()
+        for p in params.values():
+            p.grad.clamp_(-5, 5)
+        opt.step()
+
+    step(0)   # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        step(n + 1)
+        n += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(n * B * S * S / dt / 1e6, 5), "unit": "Mpix/s", "cores": cores,
+            "affinity_cores": aff, "kind": "port",
+            "sample": f"{n} x train step (fwd + autograd bwd + Adam) of B={B} {S}x{S} crops, "
+                      f"N={N}, fp32 torch CPU, {cores} threads ({dt:.1f} s)"}
+
+
+def lib_sha() -> str:
+    import hashlib
+    from iclr_17_compression_amd import _lib
+    return hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest()[:16]
 
 
 def pmc_traffic(layer: str, N: int, S: int, B: int, prec: str):
-    """HBM bytes per launch of `layer` from the newest committed PMC summary
-    (profiles/*_traffic.json, made by tools/pmc.sh + tools/pmc_summary.py on the B=64 256² N=192
-    eval workload — counters cannot be collected inside this process). None for other shapes."""
-    if (N, S, B) != (192, 256, 64):
-        return None, None
-    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
-                                          "*_traffic.json")))
+    """HBM bytes per launch of `layer` from a committed PMC summary (profiles/*_traffic.json, made
+    by tools/profile_round.sh — counters cannot be collected inside this process). Only a summary
+    of THIS library build (SHA-256 of the loaded libiclr17.so), this precision and this workload
+    counts; otherwise (None, reason)."""
+    sha = lib_sha()
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")))
+    seen = []
     for f in reversed(files):
         d = json.load(open(f))
-        if d.get("precision", "fp32") == prec and layer in d.get("layers", {}):
-            return d["layers"][layer]["traffic_bytes"], f"profiles/{os.path.basename(f)} (build {d.get('build')})"
-    return None, None
+        if d.get("precision") != prec or d.get("workload") != {"N": N, "S": S, "B": B}:
+            continue
+        seen.append(f"{os.path.basename(f)}@{d.get('lib_sha256')}")
+        e = d.get("layers", {}).get(layer, {})
+        if d.get("lib_sha256") == sha and "traffic_bytes" in e:
+            return e["traffic_bytes"], (f"profiles/{os.path.basename(f)} (lib {sha}, kernel "
+                                        f"{e.get('kernel')}, trace mean {e.get('mean_ms', 0):.4f} ms)")
+    why = (f"no PMC summary of this build (lib {sha}) for {prec} {layer} at N={N} S={S} B={B}"
+           + (f"; summaries of other builds: {', '.join(seen[:3])}" if seen else ""))
+    return None, why
+
+
+def time_eval(net, x, args, world, dev) -> dict:
+    """W warm-up steps, then K timed steps between barrier + synchronize brackets, then a second
+    pass of K steps with HIP-event brackets per layer on the launching stream (outside the
+    wall-clock region, so the brackets cannot perturb it). Elapsed is the max over ranks."""
+    step = Step(net, x)
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(8)] for _ in range(args.steps)]
+        for i in range(args.steps):
+            clipped, y_hat, bpp = step(evs[i])
+        torch.cuda.synchronize()
+        B, _, H, W = x.shape
+        bits, _ = kernels.reduce_partials(step.last_partial)
+    per_layer_ms = {name: float(np.mean([evs[i][j].elapsed_time(evs[i][j + 1]) for i in range(args.steps)]))
+                    for j, name in enumerate(LAYERS)}
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return {"elapsed": t.item(), "per_layer_ms": per_layer_ms, "bpp": bpp, "clipped": clipped,
+            "y_hat": y_hat, "bpp_img": (bits / (H * W)).double()}
+
+
+def roofline(per_layer_ms: dict, prec: str, N: int, S: int, B: int):
+    """(dominant layer, per-layer table, roofline object) of one eval pass."""
+    flops, bytes_ = layer_flops(N, S, S), layer_bytes(N, S, S)
+    dominant = max(LAYERS, key=lambda k: per_layer_ms[k])
+    achieved = flops[dominant] * B / (per_layer_ms[dominant] * 1e-3) / 1e12
+    layers = {k: {"ms": round(per_layer_ms[k], 4),
+                  "tflops": round(flops[k] * B / (per_layer_ms[k] * 1e-3) / 1e12, 2) if flops[k] else None,
+                  "gbs": round(bytes_[k] * B / (per_layer_ms[k] * 1e-3) / 1e9, 1) if bytes_[k] else None}
+              for k in LAYERS}
+    if prec == "bf16":
+        peak, note = BF16_MFMA_PEAK_TFLOPS, "bf16 dense MFMA peak (one bf16 product per MAC)"
+    elif prec == "x6" and dominant in X6_LAYERS:
+        peak, note = X6_PEAK_TFLOPS, "bf16 dense MFMA peak / 6 (bf16x6: six bf16 part products per fp32 MAC)"
+    else:
+        peak, note = FP32_MFMA_PEAK_TFLOPS, "fp32 MFMA dense peak (exact-f32 products)"
+    for k in LAYERS:
+        if flops[k]:
+            layers[k]["frac"] = round(flops[k] * B / (per_layer_ms[k] * 1e-3) / 1e12 / peak, 4)
+    traffic, src = pmc_traffic(dominant, N, S, B, prec)
+    roof = {"bound": "mfma", "kernel": dominant, "achieved": round(achieved, 2), "peak": round(peak, 1),
+            "unit": "TFLOP/s", "peak_basis": note, "frac": round(achieved / peak, 4),
+            "traffic": traffic, "traffic_source": src if traffic is not None else None}
+    if traffic is None:
+        roof["traffic_null_reason"] = src
+    return dominant, layers, roof
 
 
 def main() -> None:
@@ -393,6 +515,8 @@ def main() -> None:
     ap.add_argument("--N", type=int, default=192)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-bf16-leg", action="store_true",
+                    help="x6 eval: skip the bf16 throughput-mode leg reported as bf16_mode")
     ap.add_argument("--mode", choices=("eval", "train", "kodak", "codec"), default="eval")
     ap.add_argument("--precision", choices=kernels.PRECISIONS, default=None,
                     help="inference contraction mode (default: ICLR17_PRECISION or x6)")
@@ -421,63 +545,24 @@ def main() -> None:
     x = torch.from_numpy(synth.to_unit_float(synth.image_u8(1000 + rank, B, S, S))).to(dev)
     if args.mode == "train":
         result = run_train(args, net, x, world, dev)
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:   # the CPU leg: N=1 only
+            result["cpu_baseline"] = cpu_baseline_train(N, S, args.cpu_budget)
         if rank == 0:
             print(json.dumps(result), flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
-    step = Step(net, x)
-
-    with torch.no_grad():
-        for _ in range(args.warmup):
-            step()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        elapsed = time.perf_counter() - t0
-        # per-kernel durations: HIP events on the launching stream, a second pass of the same
-        # K steps (kept out of the wall-clock region so the brackets cannot perturb it)
-        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(8)] for _ in range(args.steps)]
-        for i in range(args.steps):
-            _, _, bpp = step(evs[i])
-        torch.cuda.synchronize()
-    per_layer_ms = {name: float(np.mean([evs[i][j].elapsed_time(evs[i][j + 1]) for i in range(args.steps)]))
-                    for j, name in enumerate(LAYERS)}
-
-    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = t.item()
+    prec = kernels.precision()
+    r = time_eval(net, x, args, world, dev)
+    elapsed, per_layer_ms, bpp = r["elapsed"], r["per_layer_ms"], r["bpp"]
     pixels = world * B * S * S * args.steps
     value = pixels / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
-
+    x6 = prec == "x6"
     flops = layer_flops(N, S, S)
     bytes_ = layer_bytes(N, S, S)
-    dominant = max(LAYERS, key=lambda k: per_layer_ms[k])
-    achieved = flops[dominant] * B / (per_layer_ms[dominant] * 1e-3) / 1e12
-    layers = {k: {"ms": round(per_layer_ms[k], 4),
-                  "tflops": round(flops[k] * B / (per_layer_ms[k] * 1e-3) / 1e12, 2) if flops[k] else None,
-                  "gbs": round(bytes_[k] * B / (per_layer_ms[k] * 1e-3) / 1e9, 1) if bytes_[k] else None}
-              for k in LAYERS}
+    dominant, layers, roof = roofline(per_layer_ms, prec, N, S, B)
     total_flops = sum(flops.values()) * B
-    prec = kernels.precision()
-    x6 = prec == "x6"
-    traffic, traffic_src = pmc_traffic(dominant, N, S, B, prec)
-    if prec == "bf16":
-        peak, peak_note = BF16_MFMA_PEAK_TFLOPS, "bf16 dense MFMA peak (one bf16 product per MAC)"
-    elif x6 and dominant in X6_LAYERS:
-        peak, peak_note = X6_PEAK_TFLOPS, "bf16 dense MFMA peak / 6 (bf16x6: six bf16 part products per fp32 MAC)"
-    else:
-        peak, peak_note = FP32_MFMA_PEAK_TFLOPS, "fp32 MFMA dense peak (exact-f32 products)"
     result = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -500,16 +585,36 @@ def main() -> None:
                                             "per MAC, fp32 accumulate and epilogues" if prec == "bf16"
                                             else "fp32 (exact-f32 MFMA products)"),
                    "parallelism": f"dp{world} (images sharded by rank, no data-path collective)"},
-        "roofline": {"bound": "mfma", "kernel": dominant, "achieved": round(achieved, 2),
-                     "peak": round(peak, 1), "unit": "TFLOP/s", "peak_basis": peak_note,
-                     "frac": round(achieved / peak, 4), "traffic": traffic,
-                     "traffic_source": traffic_src,
-                     "algorithmic_bytes_per_launch": bytes_[dominant] * B,
+        "roofline": {**roof, "algorithmic_bytes_per_launch": bytes_[dominant] * B,
                      "flop_per_launch": flops[dominant] * B,
                      "whole_step_tflops": round(total_flops / (ms_per_step * 1e-3) / 1e12, 2)},
         "layers": layers,
         "bpp_last": round(bpp.item(), 6),
     }
+    if x6 and world == 1 and not args.no_bf16_leg:
+        # the bf16 throughput mode on the same batch: rate, roofline, and its deviation from the
+        # x6 (fp32-exact) results — latent flips, Δbpp, ΔPSNR
+        kernels.set_precision("bf16")
+        try:
+            rb = time_eval(net, x, args, world, dev)
+        finally:
+            kernels.set_precision(prec)
+        dom_b, layers_b, roof_b = roofline(rb["per_layer_ms"], "bf16", N, S, B)
+        flips = int((rb["y_hat"] != r["y_hat"]).sum().item())
+
+        def psnr(c):
+            return (10 * torch.log10(1.0 / ((c - x) ** 2).mean(dim=(1, 2, 3)))).double()
+        result["bf16_mode"] = {
+            "value": round(pixels / rb["elapsed"] / 1e6, 2), "unit": "Mpix/s",
+            "ms_per_step": round(rb["elapsed"] / args.steps * 1e3, 4), "dtype": "bf16",
+            "roofline": {k: roof_b[k] for k in ("kernel", "achieved", "peak", "frac", "traffic",
+                                                  "traffic_source", "traffic_null_reason")
+                         if k in roof_b},
+            "layers": layers_b,
+            "vs_x6": {"latent_flip_rate": flips / r["y_hat"].numel(),
+                      "max_abs_dbpp_per_image": float((rb["bpp_img"] - r["bpp_img"]).abs().max()),
+                      "max_abs_dpsnr_db_per_image": float((psnr(rb["clipped"]) - psnr(r["clipped"])).abs().max())},
+        }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:   # the CPU leg: N=1 only
         result["cpu_baseline"] = cpu_baseline(N, S, S, args.cpu_budget)
     if rank == 0:

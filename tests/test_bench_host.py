@@ -1,0 +1,58 @@
+"""Host logic of bench.py (no GPU): the roofline's HBM traffic is taken only from a PMC summary of
+the library build that runs (tools/profile_round.sh stamps the SHA-256 of libiclr17.so), for the
+same precision and workload; anything else gives traffic = null with the reason. And the CPU
+baseline's thread count."""
+import json
+import os
+import sys
+
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+
+def _write(tmp_path, name, sha, prec="x6", workload=None, layer="deconv2_igdn2"):
+    d = tmp_path / "profiles"
+    d.mkdir(exist_ok=True)
+    (d / name).write_text(json.dumps({
+        "lib_sha256": sha, "precision": prec,
+        "workload": workload or {"N": 192, "S": 256, "B": 64},
+        "layers": {layer: {"kernel": "k", "traffic_bytes": 123.0, "mean_ms": 0.1}}}))
+
+
+def test_traffic_only_from_this_build(tmp_path, monkeypatch):
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    sha = bench.lib_sha()
+    _write(tmp_path, "r01_traffic.json", "0" * 16)
+    t, why = bench.pmc_traffic("deconv2_igdn2", 192, 256, 64, "x6")
+    assert t is None and sha in why and "r01_traffic.json" in why
+    _write(tmp_path, "r02_traffic.json", sha)
+    t, src = bench.pmc_traffic("deconv2_igdn2", 192, 256, 64, "x6")
+    assert t == 123.0 and "r02_traffic.json" in src
+    # another precision, workload or layer of the same build does not count
+    assert bench.pmc_traffic("deconv2_igdn2", 192, 256, 64, "bf16")[0] is None
+    assert bench.pmc_traffic("deconv2_igdn2", 192, 256, 32, "x6")[0] is None
+    assert bench.pmc_traffic("conv2_gdn2", 192, 256, 64, "x6")[0] is None
+
+
+def test_cpu_threads(monkeypatch):
+    aff = len(os.sched_getaffinity(0))
+    monkeypatch.delenv("OMP_NUM_THREADS", raising=False)
+    assert bench.cpu_threads() == (aff, aff)
+    monkeypatch.setenv("OMP_NUM_THREADS", "1")
+    assert bench.cpu_threads() == (1, aff)
+
+
+@pytest.mark.parametrize("prec,kernel_peak", [("bf16", bench.BF16_MFMA_PEAK_TFLOPS),
+                                              ("x6", bench.X6_PEAK_TFLOPS)])
+def test_roofline_object(prec, kernel_peak, tmp_path, monkeypatch):
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))   # no PMC summaries
+    ms = {k: 0.1 for k in bench.LAYERS}
+    ms["deconv2_igdn2"] = 0.2
+    dom, layers, roof = bench.roofline(ms, prec, 192, 256, 64)
+    assert dom == "deconv2_igdn2" and roof["peak"] == round(kernel_peak, 1)
+    flops = bench.layer_flops(192, 256, 256)["deconv2_igdn2"] * 64
+    assert roof["achieved"] == pytest.approx(flops / 0.2e-3 / 1e12, rel=1e-3)
+    assert roof["frac"] == pytest.approx(roof["achieved"] / kernel_peak, rel=1e-3)
+    assert roof["traffic"] is None and roof["traffic_null_reason"]

@@ -170,11 +170,43 @@ def run_train(args, net, x, world, dev):
     lam = 0.01 * 255.0 ** 2
     B, _, S, _ = x.shape
 
+    reducer = idist.GradAllReducer(params).attach(net)   # all-reduce overlapped with backward
+    loader, data_info = None, None
+    if args.train_dir:   # the data path inside the timed region: decode pool → GPU transform
+        from iclr_17_compression_amd import data
+        paths = make_train_dir(args.train_dir, idist.rank())
+        loader = data.TrainLoader(paths, B, S, 7, dev, idist.rank(), world,
+                                  workers=args.workers, prefetch=args.prefetch,
+                                  cache=not args.stream_data)
+        data_info = {"images": len(paths), "workers": args.workers, "prefetch": args.prefetch,
+                     "source": ("decoded images resident in HBM (decoded once), crop/resample "
+                                "on the GPU" if loader.store is not None else
+                                "streamed: worker decode + crop, pinned upload, GPU resample")}
+        # the loader alone (no training consuming it): one epoch after a warm-up epoch
+        for _ in loader.epoch(0):
+            pass
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        n = 0
+        for xb in loader.epoch(1):
+            n += xb.shape[0]
+        torch.cuda.synchronize()
+        data_info["loader_crops_per_s"] = round(n / (time.perf_counter() - t0), 1)
+        print(f"data path alone: {data_info['loader_crops_per_s']} crops/s", file=sys.stderr, flush=True)
+
+        def batches():
+            e = 2
+            while True:
+                yield from loader.epoch(e)
+                e += 1
+        it = batches()
+
     def step():
+        xb = next(it) if loader is not None else x
         opt.zero_grad(set_to_none=True)
-        _, mse, bpp = net.forward_train(x)
+        _, mse, bpp = net.forward_train(xb)
         (lam * mse + bpp).backward()
-        idist.allreduce_grads(params)
+        reducer.finish()
         opt.step()
         return bpp
 
@@ -193,6 +225,9 @@ def run_train(args, net, x, world, dev):
     torch.cuda.synchronize()
     elapsed = idist.max_over_ranks(time.perf_counter() - t0, dev)
     ms = elapsed / args.steps * 1e3
+    if loader is not None:
+        loader.close()
+        data_info["step_crops_per_s"] = round(B * args.steps / elapsed, 1)
     flops = train_flops(args.N, S, S) * B
     tflops = flops / (ms * 1e-3) / 1e12
     x6t = kernels.precision() == "x6"
@@ -209,7 +244,7 @@ def run_train(args, net, x, world, dev):
                    "precision": ("x6: forward, input gradients, weight gradients and GDN γ "
                                  "gradients (bias/β/rate-parameter sums and Adam in fp32)"
                                  if kernels.precision() == "x6" else "exact-f32"),
-                   "parallelism": f"dp{world} (RCCL bucketed grad all-reduce)"},
+                   "parallelism": f"dp{world} (RCCL bucketed grad all-reduce overlapped with the backward)"},
         "roofline": {"bound": "mfma", "kernel": "whole training step", "achieved": round(tflops, 2),
                      "peak": round(tpeak, 1), "unit": "TFLOP/s",
                      "peak_basis": ("bf16 dense MFMA peak / 6 (most of the step runs x6)" if x6t
@@ -217,7 +252,39 @@ def run_train(args, net, x, world, dev):
                      "frac": round(tflops / tpeak, 4), "traffic": None,
                      "flop_per_step": flops},
         "bpp_last": round(bpp.item(), 6),
+        **({"data_path": data_info} if data_info else {}),
     }
+
+
+def make_train_dir(spec: str, rank: int):
+    """--train-dir: a directory of images, or "png:N" / "jpg:N" — N synthetic photos (768×512 and
+    512×768, shifted and flipped variants of 16 smooth synthetic images) encoded by PIL into a
+    temporary directory once per rank."""
+    kind, _, n = spec.partition(":")
+    if kind not in ("png", "jpg") or not n.isdigit():
+        return sorted(glob.glob(os.path.join(spec, "*.*")))
+    import tempfile
+    from PIL import Image
+    n = int(n)
+    d = os.path.join(tempfile.gettempdir(), f"iclr17_bench_{kind}_{n}_{rank}")
+    os.makedirs(d, exist_ok=True)
+    base = {}
+    paths = []
+    for i in range(n):
+        p = os.path.join(d, f"img{i:04d}.{kind}")
+        if not os.path.exists(p):
+            portrait = i % 4 == 0
+            k = (i % 16, portrait)
+            if k not in base:
+                H, W = (768, 512) if portrait else (512, 768)
+                base[k] = synth.smooth_image_u8(5000 + i % 16, H, W).transpose(1, 2, 0)
+            img = np.roll(base[k], (37 * i) % 251, axis=1)
+            img = np.ascontiguousarray(img[::-1] if (i // 16) % 2 else img)
+            Image.fromarray(img).save(p, **({"compress_level": 1} if kind == "png" else {"quality": 95}))
+        paths.append(p)
+        if i % 64 == 63:
+            print(f"make_train_dir: {i + 1}/{n}", file=sys.stderr, flush=True)
+    return paths
 
 
 KODAK_PORTRAIT = (3, 8, 9, 16, 17, 18)   # kodim04/09/10/17/18/19: 512 wide x 768 tall
@@ -515,12 +582,21 @@ def main() -> None:
     ap.add_argument("--N", type=int, default=192)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--train-dir", default="",
+                    help='train mode: images for the data path in the timed step ("png:N": N synthetic PNGs)')
+    ap.add_argument("--workers", type=int, default=8)
+    ap.add_argument("--stream-data", action="store_true",
+                    help="train-dir: decode every epoch instead of keeping decoded images in HBM")
+    ap.add_argument("--prefetch", type=int, default=4)
     ap.add_argument("--no-bf16-leg", action="store_true",
                     help="x6 eval: skip the bf16 throughput-mode leg reported as bf16_mode")
     ap.add_argument("--mode", choices=("eval", "train", "kodak", "codec"), default="eval")
     ap.add_argument("--precision", choices=kernels.PRECISIONS, default=None,
                     help="inference contraction mode (default: ICLR17_PRECISION or x6)")
     args = ap.parse_args()
+    if os.environ.get("ICLR17_HANG_DUMP"):   # diagnostic: periodic stack dumps to stderr
+        import faulthandler
+        faulthandler.dump_traceback_later(int(os.environ["ICLR17_HANG_DUMP"]), repeat=True)
     if args.precision:
         kernels.set_precision(args.precision)
 

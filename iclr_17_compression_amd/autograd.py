@@ -289,6 +289,10 @@ class CodecTrainFn(torch.autograd.Function):
             g_recon = kernels.grad_recon(ctx.recon, ctx.x, g_mse, g_clipped)
         g_y, gs, rpart, g_ys = synthesis_backward(dec, ctx.saved_s, g_recon, g_bpp, ctx.rate,
                                                   ctx.count, want_split=g_ytilde is None)
+        red = getattr(net, "_grad_reducer", None)
+        red = red if red is not None and red.active else None
+        if red is not None:   # the synthesis gradients all-reduce during the analysis backward
+            red.launch(list(dec.parameters()), _ordered(dec, "", gs))
         if g_ytilde is not None:
             g_y = g_y + g_ytilde.permute(0, 2, 3, 1)
         ga = analysis_backward(enc, ctx.saved_a, g_y.contiguous(), g_ys)
@@ -299,6 +303,9 @@ class CodecTrainFn(torch.autograd.Function):
         order = ["f1.h", "f1.b", "f1.a", "f2.h", "f2.b", "f2.a", "f3.h", "f3.b", "f3.a", "f4.h", "f4.b"]
         rmap = dict(zip(order, rg))
         grads += [rmap[n] for n in names]
+        if red is not None:
+            red.launch(list(enc.parameters()) + list(be.parameters()),
+                       _ordered(enc, "", ga) + [rmap[n] for n in names])
         ctx.saved_a = ctx.saved_s = ctx.recon = None
         return (None, None, None, *grads)
 

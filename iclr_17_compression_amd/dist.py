@@ -10,7 +10,7 @@
 from __future__ import annotations
 
 import os
-from typing import List, Sequence
+from typing import List, Optional, Sequence
 
 import torch
 import torch.distributed as dist
@@ -101,6 +101,69 @@ def allreduce_grads(params: Sequence[Tensor], bucket_mb: float = 4.0) -> None:
             n = p.numel()
             p.grad.copy_(flat[off:off + n].view_as(p.grad))
             off += n
+
+
+class GradAllReducer:
+    """Gradient averaging overlapped with the backward (the reference's DataParallel gradient
+    reduction, train.py:228, as one process per GPU).
+
+    The fused training backward (autograd.CodecTrainFn) produces the synthesis gradients first
+    and the analysis ones last. Attached to a model, it hands each group of parameter gradients
+    to ``launch`` as soon as that group is computed: the gradients are packed into one flat
+    buffer (≤ bucket_mb per bucket) on the compute stream and all-reduced asynchronously — RCCL
+    runs on its own stream — while the compute stream goes on with the rest of the backward.
+    ``finish`` makes the compute stream wait for every reduction and writes the averages into
+    ``p.grad``, before the clamp + Adam launch.
+
+    Usage per step (grads must start as None: set_to_none zero_grad)::
+
+        opt.zero_grad(set_to_none=True); loss.backward(); reducer.finish(); opt.step()
+    """
+
+    def __init__(self, params: Sequence[Tensor], bucket_mb: float = 4.0):
+        self.params = list(params)
+        self.bucket_bytes = int(bucket_mb * 2 ** 20)
+        self.pending = []        # (work, flat, params)
+        self.launched = set()
+
+    def attach(self, net) -> "GradAllReducer":
+        net._grad_reducer = self
+        return self
+
+    @property
+    def active(self) -> bool:
+        return world() > 1
+
+    def launch(self, params: Sequence[Tensor], grads: Sequence[Optional[Tensor]]) -> None:
+        """All-reduce (sum, async) these parameters' freshly computed gradients."""
+        pairs = [(p, g) for p, g in zip(params, grads) if g is not None and id(p) not in self.launched]
+        for bucket in bucketize([g for _, g in pairs], self.bucket_bytes):
+            ids = {id(g) for g in bucket}
+            ps = [p for p, g in pairs if id(g) in ids]
+            flat = torch.cat([g.reshape(-1) for g in bucket])
+            work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, async_op=True)
+            self.pending.append((work, flat, ps))
+            self.launched.update(id(p) for p in ps)
+
+    def finish(self) -> None:
+        """Wait for the reductions (stream-ordered) and set p.grad = the rank average. Gradients
+        no backward launched (parameters outside the fused backward) are reduced here."""
+        w = world()
+        if w == 1:
+            return
+        rest = [p for p in self.params if p.grad is not None and id(p) not in self.launched]
+        if rest:
+            self.launch(rest, [p.grad for p in rest])
+        for work, flat, ps in self.pending:
+            work.wait()
+            flat.mul_(1.0 / w)
+            off = 0
+            for p in ps:
+                n = p.numel()
+                p.grad.copy_(flat[off:off + n].view_as(p.grad))
+                off += n
+        self.pending.clear()
+        self.launched.clear()
 
 
 def max_over_ranks(value: float, device) -> float:

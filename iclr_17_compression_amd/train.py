@@ -11,8 +11,10 @@ Differences from the reference, each a documented defect fix:
   D4  the evaluation directory comes from --test-dir (train.py:159 hard-codes a CLIC path);
   D9  data parallelism is one process per GPU with averaged gradients (DataParallel's gathered
       per-GPU bpp vector made rd_loss non-scalar).
-Data: ``--train-dir`` (PIL decode on the host; RandomResizedCrop(256), h/v flips and ToTensor
-on the GPU, PIL-exact — data.py) or ``--synthetic`` seeded images.
+Data: ``--train-dir`` (data.TrainLoader: shuffled epochs, PIL decode + crop in worker
+processes, resampling / flips / ToTensor on the GPU, PIL-exact, one batch ahead on a side
+stream) or ``--synthetic`` seeded images. Epoch loop, per-epoch learning rate, "Epoch N" log
+field and saves every 25 epochs as train.py:84-154, 249-260.
 """
 from __future__ import annotations
 
@@ -96,37 +98,25 @@ def load_rgb(path):
     return torch.from_numpy(img).permute(2, 0, 1).float().div(255.0)   # ToTensor semantics
 
 
-class ImageDirStream:
-    """Training batches, datasets.py:14-37: for each image of a directory (sorted *.*), a
-    RandomResizedCrop(256) + random h/v flips + ToTensor, with the pixel work on the GPU
-    (data.resized_crop_batch: PIL-exact resampling from uint8 uploads); or seeded synthetic
-    images when no directory is given."""
+class SyntheticLoader:
+    """Seeded synthetic epochs with TrainLoader's interface (``--synthetic``, no image files):
+    ``images`` per epoch, each rank its own images."""
 
-    def __init__(self, data_dir, image_size, batch, seed, synthetic=False, device=None):
-        self.paths = sorted(glob.glob(os.path.join(data_dir, "*.*"))) if data_dir else []
-        if not self.paths and not synthetic:
-            raise FileNotFoundError(f"no training images under {data_dir!r} (use --synthetic)")
-        self.size, self.batch, self.rng = image_size, batch, np.random.default_rng(seed)
-        self.synthetic, self.step = synthetic or not self.paths, 0
-        self.device = device
+    def __init__(self, batch, size, seed, device, rank=0, world=1, images=256):
+        self.batch, self.size, self.seed, self.device = batch, size, seed, device
+        self.rank, self.world, self.images = rank, world, images
 
-    def __iter__(self):
-        return self
+    def steps_per_epoch(self):
+        return max(1, self.images // (self.batch * self.world))
 
-    def __next__(self):
-        self.step += 1
-        if self.synthetic:
-            u8 = synth.image_u8(10_000 + self.step, self.batch, self.size, self.size)
-            return torch.from_numpy(synth.to_unit_float(u8))
-        from PIL import Image
-        imgs, boxes, flips = [], [], []
-        for _ in range(self.batch):
-            path = self.paths[self.rng.integers(len(self.paths))]
-            img = np.asarray(Image.open(path).convert("RGB"), dtype=np.uint8)
-            imgs.append(img)
-            boxes.append(data.random_resized_crop_params(self.rng, img.shape[0], img.shape[1]))
-            flips.append((bool(self.rng.random() < 0.5), bool(self.rng.random() < 0.5)))
-        return data.resized_crop_batch(imgs, boxes, flips, self.size, self.device)
+    def epoch(self, epoch):
+        for s in range(self.steps_per_epoch()):
+            u8 = synth.image_u8(10_000 + (self.seed * 1000 + epoch) * 4096 + s * self.world + self.rank,
+                                self.batch, self.size, self.size)
+            yield torch.from_numpy(synth.to_unit_float(u8)).to(self.device, non_blocking=True)
+
+    def close(self):
+        pass
 
 
 def kodak_images(test_dir):
@@ -168,6 +158,8 @@ def main(argv=None):
     ap.add_argument("--test-dir", default="")
     ap.add_argument("--synthetic", action="store_true")
     ap.add_argument("--max-steps", type=int, default=0, help="stop after this many steps (0: tot_step)")
+    ap.add_argument("--workers", type=int, default=4, help="image decode processes")
+    ap.add_argument("--prefetch", type=int, default=4, help="batches decoded ahead")
     args = ap.parse_args(argv)
 
     device = idist.init_from_env("nccl")
@@ -197,27 +189,57 @@ def main(argv=None):
     params = list(net.parameters())
     # train.py:233 Adam + train.py:106-111 clamp(±5), fused into one launch (optim.py)
     optimizer = FusedAdam(params, lr=cfg["lr"]["base"], grad_clip=5)
+    reducer = idist.GradAllReducer(params).attach(net)   # all-reduce overlapped with backward
     per_rank = max(1, cfg["batch_size"] // w)
-    stream = ImageDirStream(args.train_dir, 256, per_rank, args.seed + 1000 * r, args.synthetic,
-                            device=device)
-    meters = {k: AverageMeter(cfg["print_freq"]) for k in ("elapsed", "loss", "psnr", "bpp", "mse")}
-    if args.name and r == 0:
-        save_model(net, global_step, save_path)
+    if args.synthetic or not args.train_dir:
+        if not args.synthetic:
+            raise FileNotFoundError("no --train-dir given (use --synthetic for seeded images)")
+        loader = SyntheticLoader(per_rank, 256, args.seed, device, r, w)
+    else:
+        paths = sorted(glob.glob(os.path.join(args.train_dir, "*.*")))   # datasets.py:19
+        loader = data.TrainLoader(paths, per_rank, 256, args.seed, device, r, w,
+                                  workers=args.workers, prefetch=args.prefetch)
     tot = args.max_steps or cfg["tot_step"]
     lam = cfg["train_lambda"]
+    if args.name and r == 0:
+        save_model(net, global_step, save_path)                        # train.py:250
+    steps_epoch = global_step // loader.steps_per_epoch()              # train.py:249
+    try:
+        for epoch in range(steps_epoch, cfg["tot_epoch"]):             # train.py:252-260
+            lr = learning_rate(cfg, global_step)                       # once per epoch, as :253
+            for g in optimizer.param_groups:
+                g["lr"] = lr
+            if global_step > tot:
+                if args.name and r == 0:
+                    save_model(net, global_step, save_path)
+                break
+            global_step = train_epoch(net, loader, optimizer, reducer, cfg, lam, lr, epoch,
+                                      global_step, tot, args, device)
+            if epoch % 25 == 0 and args.name and r == 0:
+                save_model(net, global_step, save_path)
+            if args.max_steps and global_step >= args.max_steps:
+                break
+    finally:
+        loader.close()
+    if args.name and r == 0:
+        save_model(net, global_step, save_path)
+    return 0
+
+
+def train_epoch(net, loader, optimizer, reducer, cfg, lam, lr, epoch, global_step, tot, args,
+                device):
+    """train(), train.py:84-154: one pass over the loader's epoch."""
+    logger.info("Epoch {} begin".format(epoch))
     net.train()
-    while global_step < tot:
-        lr = learning_rate(cfg, global_step)
-        for g in optimizer.param_groups:
-            g["lr"] = lr
+    meters = {k: AverageMeter(cfg["print_freq"]) for k in ("elapsed", "loss", "psnr", "bpp", "mse")}
+    for x in loader.epoch(epoch):
         t0 = time.time()
-        x = next(stream).to(device, non_blocking=True)
         global_step += 1
         clipped, mse, bpp = net.forward_train(x)
         rd_loss = lam * mse + bpp
         optimizer.zero_grad(set_to_none=True)
         rd_loss.backward()
-        idist.allreduce_grads(params)
+        reducer.finish()   # the all-reduces overlapped the backward (dist.GradAllReducer)
         optimizer.step()   # clamp after the all-reduce (DataParallel's GPU0 clamp), then Adam
         if global_step % cfg["cal_step"] == 0:
             m = mse.item()
@@ -230,6 +252,7 @@ def main(argv=None):
             M = meters
             logger.info(" | ".join([
                 f"Step [{global_step}/{tot}={global_step / tot * 100.0:.2f}%]",
+                f"Epoch {epoch}",
                 f"Time {M['elapsed'].val:.3f} ({M['elapsed'].avg:.3f})",
                 f"Lr {lr}",
                 f"Total Loss {M['loss'].val:.3f} ({M['loss'].avg:.3f})",
@@ -239,9 +262,9 @@ def main(argv=None):
         if global_step % cfg["save_model_freq"] == 0 and args.test_dir:
             test_kodak(net, args.test_dir, device, global_step)      # train.py:150-152 (D8)
             net.train()
-    if args.name and r == 0:
-        save_model(net, global_step, save_path)
-    return 0
+        if args.max_steps and global_step >= args.max_steps:
+            break
+    return global_step
 
 
 if __name__ == "__main__":

@@ -38,6 +38,21 @@ def _worker(r, w, port, q):
             expect = (i + 1) * (1 + w) / 2.0
             assert torch.allclose(p.grad, torch.full(p.shape, expect))
         assert idist.max_over_ranks(float(r), "cpu") == float(w - 1)
+        # the overlapped reducer: groups launched as a backward would (decoder first), one
+        # parameter left for finish(), a bucket size that splits groups
+        ps = [torch.nn.Parameter(torch.zeros(s)) for s in (40, 3000, 9, 700, 5)]
+        for i, p in enumerate(ps):
+            p.grad = torch.full(p.shape, float(r + 1) * (i + 2)) + torch.arange(p.numel()) * r
+        red = idist.GradAllReducer(ps, bucket_mb=0.005)
+        assert red.active
+        red.launch(ps[2:4], [p.grad for p in ps[2:4]])
+        red.launch(ps[0:2], [p.grad for p in ps[0:2]])
+        red.launch(ps[2:3], [ps[2].grad])   # already in flight: not reduced twice
+        red.finish()
+        for i, p in enumerate(ps):
+            expect = (i + 2) * (1 + w) / 2.0 + torch.arange(p.numel()) * (w - 1) / 2.0
+            assert torch.allclose(p.grad, expect), i
+        assert not red.pending and not red.launched
         q.put((r, "ok"))
     except Exception as e:  # pragma: no cover - reported to the parent
         q.put((r, repr(e)))

@@ -99,3 +99,23 @@ def test_g5_ms_ssim(golden_dir):
         synth.smooth_image_u8(meta["image_seed_base"] + row["index"], row["height"], row["width"])))[None]
     clipped = oracle.codec_forward(x, sd)[0]
     assert oracle.ms_ssim(clipped, x, 1.0).item() == row["ms_ssim"]
+
+
+def g8_state_dict(golden_dir):
+    d = np.load(os.path.join(golden_dir, "g8_weights_n128.npz"))
+    return {k: torch.from_numpy(d[k].astype(np.float32)) for k in d.files}
+
+
+def test_g8_operating_point(golden_dir):
+    """The trained N=128 operating point (PSNR ≈ 28 dB, bpp ≈ 0.21): the oracle reproduces the
+    reference's bpp, PSNR and MS-SSIM of two Kodak-synth images bit for bit."""
+    meta = json.load(open(os.path.join(golden_dir, "g8_kodak24_synth_n128_trained.json")))
+    sd = g8_state_dict(golden_dir)
+    for row in meta["images"][:2]:
+        x = torch.from_numpy(synth.to_unit_float(
+            synth.smooth_image_u8(meta["image_seed_base"] + row["index"], row["height"], row["width"])))[None]
+        clipped, y_hat, bpp, _, _ = oracle.codec_forward(x, sd)
+        assert bpp.item() == row["bpp"]
+        assert oracle.psnr(clipped, x).item() == row["psnr"]
+        assert oracle.ms_ssim(clipped, x, 1.0).item() == row["ms_ssim"]
+        assert 25.0 <= row["psnr"] and row["bpp"] < 1.0 and row["ms_ssim"] > 0.9

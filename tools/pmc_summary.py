@@ -42,10 +42,10 @@ LAYER_KERNELS = {
     },
     "bf16": {
         "conv1_gdn1": (r"conv1_bf16_kernel<192>", None),
-        "conv2_gdn2": (r"k5_bf16_kernel<0, 16, 192, 4, 2, 192, 192, 0>", None),
-        "conv3_quant_rate": (r"k5_bf16_kernel<0, 8, 96, 2, 2, 192, 192, 2>", None),
-        "deconv1_igdn1": (r"k5_bf16_kernel<1, 8, 192, 2, 4, 192, 192, 1>", None),
-        "deconv2_igdn2": (r"k5_bf16_kernel<1, 16, 192, 4, 2, 192, 192, 1>", None),
+        "conv2_gdn2": (r"k5_bf16_kernel<0, 16, 192, 192, 192, 0>", None),
+        "conv3_quant_rate": (r"k5_bf16_kernel<0, 8, 96, 192, 192, 2>", None),
+        "deconv1_igdn1": (r"k5_bf16_kernel<1, 8, 192, 192, 192, 1>", None),
+        "deconv2_igdn2": (r"k5_bf16_kernel<1, 16, 192, 192, 192, 1>", None),
         "deconv3_clamp": (r"deconv3_x6_kernel<192, true>", None),
     },
 }

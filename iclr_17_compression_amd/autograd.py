@@ -138,8 +138,19 @@ def analysis_features_train(enc, x: Tensor):
     return a2, {"x": x, "u1": u1, "a1": a1, "u2": u2, "a2": a2, "a2s": None, "a1s": None}
 
 
+def conv1_input_grad(enc, g_u1: Tensor) -> Tensor:
+    """∂L/∂x of conv1 (analysis_17.py:32, k9 s4 p4): the transposed convolution of ∂L/∂u1
+    (NHWC) with conv1's own weights — the shape and arithmetic of deconv3 (k9 s4 p4 op3, N → 3),
+    so it runs on the exact-f32 deconv3 kernel with conv1.weight in deconv3's packing, a zero
+    bias and the unclipped output."""
+    w = enc.packed_conv1_t()
+    zero = torch.zeros(3, device=g_u1.device, dtype=torch.float32)
+    _, dx, _ = kernels.deconv3(g_u1.contiguous(), w, zero, want_recon=True)
+    return dx
+
+
 def analysis_backward(enc, saved: Dict[str, Tensor], g_y: Tensor,
-                      g_y_split: Optional[Tensor] = None) -> Dict[str, Tensor]:
+                      g_y_split: Optional[Tensor] = None, want_dx: bool = False) -> Dict[str, Tensor]:
     """∂L/∂y (NHWC) → parameter gradients of Analysis_net_17 (analysis_17.py:14-39). In the x6
     mode the input-gradient contractions run on split-form gradients (g_y_split, or split here)."""
     bb1, gb1, _ = enc.gdn1.bounds_f32()
@@ -169,9 +180,12 @@ def analysis_backward(enc, saved: Dict[str, Tensor], g_y: Tensor,
         dW1 = kernels.wgrad_k9(g_u1, saved["x"])
     dbeta2, dgamma2 = kernels.gdn_param_grads(dn2, saved["u2"], dbe2, enc.gdn2.beta, enc.gdn2.gamma, bb2, gb2)
     dbeta1, dgamma1 = kernels.gdn_param_grads(dn1, saved["u1"], dbe1, enc.gdn1.beta, enc.gdn1.gamma, bb1, gb1)
-    return {"conv1.weight": dW1, "conv1.bias": db1, "gdn1.beta": dbeta1, "gdn1.gamma": dgamma1,
-            "conv2.weight": dW2, "conv2.bias": db2, "gdn2.beta": dbeta2, "gdn2.gamma": dgamma2,
-            "conv3.weight": dW3}
+    grads = {"conv1.weight": dW1, "conv1.bias": db1, "gdn1.beta": dbeta1, "gdn1.gamma": dgamma1,
+             "conv2.weight": dW2, "conv2.bias": db2, "gdn2.beta": dbeta2, "gdn2.gamma": dgamma2,
+             "conv3.weight": dW3}
+    if want_dx:
+        grads["x"] = conv1_input_grad(enc, g_u1)
+    return grads
 
 
 # ----------------------------------------------------------------------------- synthesis
@@ -295,7 +309,8 @@ class CodecTrainFn(torch.autograd.Function):
             red.launch(list(dec.parameters()), _ordered(dec, "", gs))
         if g_ytilde is not None:
             g_y = g_y + g_ytilde.permute(0, 2, 3, 1)
-        ga = analysis_backward(enc, ctx.saved_a, g_y.contiguous(), g_ys)
+        want_dx = ctx.needs_input_grad[0]
+        ga = analysis_backward(enc, ctx.saved_a, g_y.contiguous(), g_ys, want_dx=want_dx)
         rg = kernels.rate_param_grads(rpart, be.params_in_order()) if g_bpp is not None else [None] * 11
         grads += _ordered(enc, "Encoder.", ga)
         grads += _ordered(dec, "Decoder.", gs)
@@ -306,8 +321,11 @@ class CodecTrainFn(torch.autograd.Function):
         if red is not None:
             red.launch(list(enc.parameters()) + list(be.parameters()),
                        _ordered(enc, "", ga) + [rmap[n] for n in names])
+        dx = ga.get("x")
+        if dx is not None and g_mse is not None:   # the loss's own x: ∂mse/∂x = −∂mse/∂recon
+            dx = dx - kernels.grad_recon(ctx.recon, ctx.x, g_mse, None)
         ctx.saved_a = ctx.saved_s = ctx.recon = None
-        return (None, None, None, *grads)
+        return (dx, None, None, *grads)
 
 
 class AnalysisFn(torch.autograd.Function):
@@ -325,9 +343,10 @@ class AnalysisFn(torch.autograd.Function):
     def backward(ctx, g_y):
         if g_y is None:
             return (None, None) + (None,) * len(list(ctx.enc.parameters()))
-        ga = analysis_backward(ctx.enc, ctx.saved, g_y.permute(0, 2, 3, 1).contiguous())
+        ga = analysis_backward(ctx.enc, ctx.saved, g_y.permute(0, 2, 3, 1).contiguous(),
+                               want_dx=ctx.needs_input_grad[0])
         ctx.saved = None
-        return (None, None, *_ordered(ctx.enc, "", ga))
+        return (ga.get("x"), None, *_ordered(ctx.enc, "", ga))
 
 
 class SynthesisFn(torch.autograd.Function):

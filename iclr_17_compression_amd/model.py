@@ -125,17 +125,35 @@ class ImageCompressor(nn.Module):
             clipped, y_tilde, bpp, _ = self._train_outputs(input_image, noise, params)
             return clipped, y_tilde, bpp
         B, _, H, W = input_image.shape
+        if not self.training and needs_grad(input_image, params):
+            return self._eval_autograd(input_image)
         out = self.run(input_image, noise=noise)
         _, bpp = kernels.reduce_partials(out["bits_partial"], scale=1.0 / (B * H * W), per_image=False)
         y_hat = out["y_hat"].permute(0, 3, 1, 2)
-        clipped = no_backward(out["clipped"], "ImageCompressor (eval mode)", params, input_image)
+        clipped = no_backward(out["clipped"], "ImageCompressor (training mode, no grad)", params,
+                              input_image)
+        return clipped, y_hat, bpp
+
+    def _eval_autograd(self, x):
+        """model.py:47-80 in eval mode with autograd on. torch.round (model.py:56) has a zero
+        gradient, so nothing flows back into the encoder or the image; the reconstruction is
+        differentiable in the synthesis parameters (the fused synthesis forward/backward,
+        autograd.SynthesisFn) and the rate in the BitEstimator parameters (model.py:71-78 on
+        the module's autograd kernels). The encoder's parameters and the image get no gradient
+        where torch would give zeros."""
+        B, _, H, W = x.shape
+        with torch.no_grad():
+            y_hat = self.encode_latents(x)["y_hat"].permute(0, 3, 1, 2)
+        recon = self.Decoder(y_hat)
+        clipped = recon.clamp(0., 1.)                                        # model.py:59
+        prob = self.bitEstimator(y_hat + 0.5) - self.bitEstimator(y_hat - 0.5)   # model.py:71-72
+        total_bits = torch.sum(torch.clamp(-1.0 * torch.log(prob + 1e-10) / math.log(2.0), 0, 50))
+        bpp = total_bits / (B * H * W)                                       # model.py:76-78
         return clipped, y_hat, bpp
 
     def _train_outputs(self, x, noise, params):
         from .autograd import CodecTrainFn
         kernels._check(x, "image", 4)
-        if x.requires_grad:
-            raise kernels.Iclr17Error("iclr17: gradients w.r.t. the input image are not implemented")
         if noise is None:
             noise = self._latent_noise(x)
         self._warm_packs(backward=True)   # one batched pack per parameter update

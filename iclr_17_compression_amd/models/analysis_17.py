@@ -79,6 +79,13 @@ class Analysis_net_17(nn.Module):
                              lambda: kernels.pack_weight(_lib.ICLR17_W_DECONV5, self.conv2.weight, N))
         return w3t, w2t
 
+    def packed_conv1_t(self):
+        """conv1.weight in deconv3's packing: the transposed convolution of conv1's input
+        gradient (autograd.conv1_input_grad), cached until the weight changes."""
+        return self._pack.get("w1t", (self.conv1.weight,),
+                              lambda: kernels.pack_weight(_lib.ICLR17_W_DECONV9, self.conv1.weight,
+                                                          self.out_channel_N))
+
     def features(self, x):
         """conv1+gdn1 → conv2+gdn2 as NHWC (the input of conv3); no autograd."""
         w1, w2, _, g1, g2 = self.packed()
@@ -90,8 +97,6 @@ class Analysis_net_17(nn.Module):
         kernels._check(x, "image", 4)
         params = list(self.parameters())
         if needs_grad(x, params):
-            if x.requires_grad:
-                raise kernels.Iclr17Error("iclr17: gradients w.r.t. the input image are not implemented")
             return AnalysisFn.apply(x.contiguous(), self, *params)
         _, _, w3, _, _ = self.packed()
         if kernels.precision() == "bf16":

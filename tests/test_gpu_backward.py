@@ -239,3 +239,71 @@ def test_gdn_wgrad_x6_matches_fp32(device, C, P):
     assert grad_err(got, ref64.float()) < 1e-5
     assert grad_err(got, f32) < 1e-5
     assert torch.equal(kernels.gdn_wgrad(dd, ud, x6=True), got)   # deterministic
+
+
+@pytest.mark.parametrize("N,B,H,W", [(192, 2, 64, 64), (128, 1, 48, 80)])
+def test_input_image_gradient_train_step(device, precision, N, B, H, W):
+    """∂(λ·MSE + bpp)/∂x through the fused training step (the reference's autograd through
+    analysis_17.py:32-39 and the loss): conv1's input gradient on the deconv3 kernel with
+    conv1's weights, against the oracle's autograd; the parameter gradients are unchanged."""
+    net, sd = make(N, 2, device)
+    x = torch.from_numpy(synth.to_unit_float(synth.image_u8(7, B, H, W)))
+    noise = torch.from_numpy(synth.uniform(8, (B, N, H // 16, W // 16), -0.5, 0.5))
+    xg = x.to(device).requires_grad_(True)
+    _, mse, bpp = net.forward_train(xg, noise=noise.to(device))
+    net.zero_grad()
+    (LAM * mse + bpp).backward()
+    xr = x.clone().requires_grad_(True)
+    sdp = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    r_loss, _, _ = oracle.rd_loss(xr, sdp, noise, LAM)
+    r_loss.backward()
+    assert grad_err(xg.grad, xr.grad) < GRAD_REL, grad_err(xg.grad, xr.grad)
+    errs = {k: grad_err(p.grad, sdp[k].grad) for k, p in net.named_parameters()}
+    assert max(errs.values()) < GRAD_REL, errs
+
+
+def test_analysis_module_input_gradient(device):
+    """Analysis_net_17 alone (analysis_17.py:32-39) with x.requires_grad: ∂(Σ y·g)/∂x and the
+    parameter gradients against the oracle's autograd."""
+    N, B, H, W = 192, 2, 64, 48
+    net, sd = make(N, 3, device)
+    x = torch.from_numpy(synth.to_unit_float(synth.image_u8(9, B, H, W)))
+    gy = torch.from_numpy(synth.normal_like(10, (B, N, H // 16, W // 16), 1.0))
+    xg = x.to(device).requires_grad_(True)
+    y = net.Encoder(xg)
+    net.zero_grad()
+    (y * gy.to(device)).sum().backward()
+    xr = x.clone().requires_grad_(True)
+    sdp = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    (oracle.analysis(xr, sdp) * gy).sum().backward()
+    assert grad_err(xg.grad, xr.grad) < GRAD_REL
+    for k, p in net.Encoder.named_parameters():
+        assert grad_err(p.grad, sdp["Encoder." + k].grad) < GRAD_REL, k
+
+
+def test_eval_mode_autograd(device):
+    """ImageCompressor.forward in eval mode with autograd on (model.py:47-80 with torch.round):
+    the outputs equal the fused eval path's, and a loss on (clipped, bpp) back-propagates into
+    the synthesis and BitEstimator parameters as the oracle's autograd does; round's zero
+    gradient leaves the encoder without one."""
+    N, B, H, W = 192, 2, 64, 64
+    net, sd = make(N, 2, device)
+    net.eval()
+    x = torch.from_numpy(synth.to_unit_float(synth.image_u8(11, B, H, W)))
+    clipped, y_hat, bpp = net(x.to(device))
+    with torch.no_grad():
+        c0, yh0, b0 = net(x.to(device))
+    assert torch.equal(y_hat, yh0)
+    assert grad_err(clipped, c0) < 2e-5 and bpp.item() == pytest.approx(b0.item(), rel=1e-5)
+    net.zero_grad()
+    (LAM * torch.mean((clipped - x.to(device)) ** 2) + bpp).backward()
+    sdp = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    r_clipped, r_yhat, r_bpp, _, _ = oracle.codec_forward(x, sdp, training=False)
+    (LAM * torch.mean((r_clipped - x) ** 2) + r_bpp).backward()
+    assert torch.equal(y_hat.cpu(), r_yhat)
+    for k, p in net.named_parameters():
+        ref = sdp[k].grad
+        if k.startswith("Encoder."):
+            assert p.grad is None and (ref is None or ref.abs().max() == 0), k
+            continue
+        assert grad_err(p.grad, ref) < GRAD_REL, (k, grad_err(p.grad, ref))

@@ -1193,11 +1193,20 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
       }
     }
   };
+  // B DMA: the stage [k-quad][48][4] holds logical column j (the d3_col order the fragment
+  // reads walk) at slot j, so a 16-lane group reads 16 consecutive 16-byte slots (conflict-free);
+  // each lane fetches the packed column d3_col(j) of its slot.
+  int bsrc[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q = (wave + 4 * k) * 64 + lane, kq = q / 48, j = q - kq * 48;
+    bsrc[k] = (kq * 48 + d3_col(j)) * 4;
+  }
   auto issue_b = [&](int s, int buf) {
     const int cc = s / 9, tap = s - cc * 9;
-    const float* __restrict__ ws = a.w + ((long)tap * CI + cc * KCH) * 48 + lane * 4;
-    glds16(ws + wave * 256, sB + buf * D3_SB + wave * 256);
-    if (wave < 2) glds16(ws + (wave + 4) * 256, sB + buf * D3_SB + (wave + 4) * 256);
+    const float* __restrict__ ws = a.w + ((long)tap * CI + cc * KCH) * 48;
+    glds16(ws + bsrc[0], sB + buf * D3_SB + wave * 256);
+    if (wave < 2) glds16(ws + bsrc[1], sB + buf * D3_SB + (wave + 4) * 256);
   };
 
   f4 acc[MT][NT];
@@ -1220,7 +1229,8 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
       bf8 Bb[NTT];
 #pragma unroll
       for (int nt = 0; nt < NTT; ++nt) {
-        const f4 w0 = *(const f4*)(sb + pcol[nt] * 4), w1 = *(const f4*)(sb + 48 * 4 + pcol[nt] * 4);
+        const int jc = nt * 16 + (lane & 15);
+        const f4 w0 = *(const f4*)(sb + jc * 4), w1 = *(const f4*)(sb + 48 * 4 + jc * 4);
         Bb[nt] = bf8{(__bf16)w0[0], (__bf16)w0[1], (__bf16)w0[2], (__bf16)w0[3],
                      (__bf16)w1[0], (__bf16)w1[1], (__bf16)w1[2], (__bf16)w1[3]};
       }
@@ -1240,7 +1250,8 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
 #pragma unroll
     for (int nt = 0; nt < NTT; ++nt) {
       u4 bh, bm, bl;
-      split8(*(const f4*)(sb + pcol[nt] * 4), *(const f4*)(sb + 48 * 4 + pcol[nt] * 4), bh, bm, bl);
+      const int jc = nt * 16 + (lane & 15);
+      split8(*(const f4*)(sb + jc * 4), *(const f4*)(sb + 48 * 4 + jc * 4), bh, bm, bl);
       Bh[nt] = __builtin_bit_cast(bf8, bh);
       Bm[nt] = __builtin_bit_cast(bf8, bm);
       Bl[nt] = __builtin_bit_cast(bf8, bl);
@@ -1479,7 +1490,16 @@ __global__ void __launch_bounds__(256) conv1_gdn_kernel(const EngineArgs a) {
 // (packing ICLR17_W_CONV1_X6, then iclr17_split_packed). The weights' split planes
 // [3][32][CO][8] are read from L2 one step ahead, like the x6 GDN γ: no B image in LDS, and no
 // barrier in the main loop.
-constexpr int P1U = 3 * P1 * P1RS;        // u16 elements per split plane (4440)
+// Split-plane rows are 64 u16 (128 bytes, 16 granules of 4 elements); granule j of row r is
+// stored at j ^ 8·((r >> 2) & 1). A fragment read's 32-lane half touches rows r, r+4 (the two
+// output-pixel rows of a 16-lane group) and the next k-group's r', r'+4: the 128-byte stride
+// puts rows two 64-byte bank quarters apart and the swizzle moves r+4 by one more, so the four
+// 64-byte windows fall in distinct quarters (no bank conflicts on the 8-byte reads).
+constexpr int X1RS = 64;                  // u16 per split-plane row
+constexpr int P1U = 3 * P1 * X1RS;        // u16 elements per split plane (7104)
+__host__ __device__ constexpr int x1_off(int row, int gran) {
+  return row * X1RS + ((gran ^ (((row >> 2) & 1) << 3)) << 2);
+}
 
 template <int CO, int EPI>
 __global__ void __launch_bounds__(256, 2) conv1_x6_kernel(const EngineArgs a) {
@@ -1542,7 +1562,8 @@ __global__ void __launch_bounds__(256, 2) conv1_x6_kernel(const EngineArgs a) {
       m[i] = __float_as_uint(r) & 0xffff0000u;
       l[i] = __float_as_uint(r - __uint_as_float(m[i]));
     }
-    const int o = pc * 4;   // u16 offset (row stride 40 = 10 pieces)
+    const int cr = pc / 10, q = pc - cr * 10;
+    const int o = x1_off(cr, q);   // u16 offset of the piece's granule
     *(uint2*)(sp + o) = uint2{__builtin_amdgcn_perm(h[1], h[0], 0x07060302u),
                               __builtin_amdgcn_perm(h[3], h[2], 0x07060302u)};
     *(uint2*)(sp + P1U + o) = uint2{__builtin_amdgcn_perm(m[1], m[0], 0x07060302u),
@@ -1558,15 +1579,12 @@ __global__ void __launch_bounds__(256, 2) conv1_x6_kernel(const EngineArgs a) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
 
-  // Pixel part of a lane's patch offset, per mt: output pixel (my, mx) → row 4·my, column 4·mx.
-  int pix[MT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const int m = mt * 16 + (lane & 15);
-    pix[mt] = (m >> 3) * 4 * P1RS + (m & 7) * 4;
-  }
+  // Output pixel (my, mx) = (2·mt + b, lane & 7), b = (lane >> 3) & 1, reads patch row 4·my
+  // (+ the pair's row) and granule mx (column 4·mx). The swizzle bit of row prow + 4b + 8mt does
+  // not depend on mt.
+  const int mx = lane & 7, b4 = 4 * ((lane >> 3) & 1);
   const int kg = lane >> 4;
-  auto pair_off = [](int p) { return ((p / 9) * P1 + p % 9) * P1RS; };
+  auto pair_row = [](int p) { return (p / 9) * P1 + p % 9; };
 
   auto mfma6 = [&](int mt, const bf8& Ah, const bf8& Am, const bf8& Al, const u4 (&b)[3][NT]) {
 #pragma unroll
@@ -1585,14 +1603,16 @@ __global__ void __launch_bounds__(256, 2) conv1_x6_kernel(const EngineArgs a) {
   // Steps 0..6: 8 consecutive columns of one patch row per lane (two 8-byte reads per plane).
   auto step_rows = [&](int s, const u4 (&b)[3][NT]) {
     const int g = 4 * s + kg;
-    const int po = pair_off(g < 27 ? g : 26);
+    const int r0 = pair_row(g < 27 ? g : 26) + b4;
+    const int lo_off = x1_off(r0, mx), hi_off = x1_off(r0, mx + 1);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      const unsigned short* e = sp + po + pix[mt];
+      const unsigned short* e = sp + mt * 8 * X1RS;
       u4 v[3];
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
-        const uint2 lo2 = *(const uint2*)(e + p * P1U), hi2 = *(const uint2*)(e + p * P1U + 4);
+        const uint2 lo2 = *(const uint2*)(e + p * P1U + lo_off);
+        const uint2 hi2 = *(const uint2*)(e + p * P1U + hi_off);
         v[p] = u4{lo2.x, lo2.y, hi2.x, hi2.y};
       }
       mfma6(mt, __builtin_bit_cast(bf8, v[0]), __builtin_bit_cast(bf8, v[1]),
@@ -1605,7 +1625,7 @@ __global__ void __launch_bounds__(256, 2) conv1_x6_kernel(const EngineArgs a) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int p = 8 * kg + e;
-      po[e] = pair_off(p < 27 ? p : 26) + 8;
+      po[e] = x1_off(pair_row(p < 27 ? p : 26) + b4, mx + 2);   // column 4·mx + 8
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -1614,8 +1634,8 @@ __global__ void __launch_bounds__(256, 2) conv1_x6_kernel(const EngineArgs a) {
       for (int p = 0; p < 3; ++p)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const unsigned lo = sp[p * P1U + po[2 * i] + pix[mt]];
-          const unsigned hi = sp[p * P1U + po[2 * i + 1] + pix[mt]];
+          const unsigned lo = sp[p * P1U + po[2 * i] + mt * 8 * X1RS];
+          const unsigned hi = sp[p * P1U + po[2 * i + 1] + mt * 8 * X1RS];
           v[p][i] = lo | (hi << 16);
         }
       mfma6(mt, __builtin_bit_cast(bf8, v[0]), __builtin_bit_cast(bf8, v[1]),

@@ -220,20 +220,20 @@ def g5_kodak_synth(ref_model, ref_models, out):
         json.dump({"N": N, "weight_seed": seed, "image_seed_base": 100, "images": rows}, f, indent=1)
 
 
-def g8_weights():
-    """The G8 operating point: N=128 weights trained to λ=0.01·255² by
-    tools/train_operating_point.py (x6 training path on the GPU), stored in fp16 and used as
-    the fp32 values they round to."""
-    d = np.load(os.path.join(HERE, "g8_weights_n128.npz"))
+def trained_weights(name):
+    """Operating-point weights trained to λ=0.01·255² by tools/train_operating_point.py (x6
+    training path on the GPU), stored in fp16 and used as the fp32 values they round to."""
+    d = np.load(os.path.join(HERE, name))
     return {k: torch.from_numpy(d[k].astype(np.float32)) for k in d.files}
 
 
-def g8_operating_point(ref_model, ref_models, out):
+def g8_operating_point(ref_model, ref_models, out, N=128, weights="g8_weights_n128.npz",
+                       fixture="g8_kodak24_synth_n128_trained.json", tag="g8"):
     """The reference's testKodak metrics (train.py:171-179) on the 24 Kodak-synth images at a
-    realistic operating point (PSNR ≈ 28 dB, bpp ≈ 0.2, MS-SSIM ≈ 0.92) — where MS-SSIM's
-    product of per-level terms is well conditioned, unlike G5's degenerate 6.6 dB point."""
-    N = 128
-    sd = g8_weights()
+    realistic operating point (PSNR ≈ 27–28 dB, bpp ≈ 0.2–0.3, MS-SSIM ≈ 0.92) — where MS-SSIM's
+    product of per-level terms is well conditioned, unlike G5's degenerate 6.6 dB point. G8: N=128
+    (train.py's default); G9: N=192 (BASELINE C2)."""
+    sd = trained_weights(weights)
     net = ref_model.ImageCompressor(out_channel_N=N)
     assert not set(net.state_dict().keys()) ^ set(sd.keys())
     net.load_state_dict(sd)
@@ -247,15 +247,15 @@ def g8_operating_point(ref_model, ref_models, out):
         msssim = ref_models.ms_ssim(clipped, x, data_range=1.0, size_average=True)
         if i < 2:
             o = oracle.codec_forward(x, sd, training=False)
-            check_equal(f"g8[{i}].y_hat", o[1], y_hat)
-            check_equal(f"g8[{i}].clipped", o[0], clipped)
-            check_equal(f"g8[{i}].ms_ssim", oracle.ms_ssim(clipped, x, 1.0)[0], msssim)
+            check_equal(f"{tag}[{i}].y_hat", o[1], y_hat)
+            check_equal(f"{tag}[{i}].clipped", o[0], clipped)
+            check_equal(f"{tag}[{i}].ms_ssim", oracle.ms_ssim(clipped, x, 1.0)[0], msssim)
         rows.append({"index": i, "height": h, "width": w, "bpp": bpp.item(), "mse": mse.item(),
                      "psnr": psnr.item(), "ms_ssim": msssim.item(),
                      "y_hat_sha256": sha256(y_hat), "y_hat_absmax": y_hat.abs().max().item()})
-        print("g8", rows[-1])
-    with open(os.path.join(out, "g8_kodak24_synth_n128_trained.json"), "w") as f:
-        json.dump({"N": N, "weights": "g8_weights_n128.npz", "train_lambda": 0.01 * 255.0 ** 2,
+        print(tag, rows[-1])
+    with open(os.path.join(out, fixture), "w") as f:
+        json.dump({"N": N, "weights": weights, "train_lambda": 0.01 * 255.0 ** 2,
                    "image_seed_base": 100, "images": rows}, f, indent=1)
 
 
@@ -299,7 +299,11 @@ def main():
              "g4": lambda: g4_train(ref_model, HERE),
              "g5": lambda: g5_kodak_synth(ref_model, ref_models, HERE),
              "g6": lambda: g6_ms_ssim(ref_models, HERE),
-             "g8": lambda: g8_operating_point(ref_model, ref_models, HERE)}
+             "g8": lambda: g8_operating_point(ref_model, ref_models, HERE),
+             "g9": lambda: g8_operating_point(ref_model, ref_models, HERE, N=192,
+                                              weights="g9_weights_n192.npz",
+                                              fixture="g9_kodak24_synth_n192_trained.json",
+                                              tag="g9")}
     for k, fn in steps.items():
         if not args.only or k in args.only.split(","):
             fn()

@@ -1,6 +1,7 @@
-"""G8: the Kodak-synth set at a realistic operating point — N = 128 weights trained to
-λ = 0.01·255² (tools/train_operating_point.py; PSNR ≈ 27.8 dB, bpp ≈ 0.21, MS-SSIM ≈ 0.925),
-values from the reference (tests/golden/gen_goldens.py g8).
+"""G8 / G9: the Kodak-synth set at a realistic operating point — weights trained to
+λ = 0.01·255² (tools/train_operating_point.py): G8 at N = 128 (PSNR ≈ 27.8 dB, bpp ≈ 0.21,
+MS-SSIM ≈ 0.925), G9 at N = 192, BASELINE C2's width (PSNR ≈ 27.2 dB, bpp ≈ 0.27, MS-SSIM ≈
+0.916); values from the reference (tests/golden/gen_goldens.py g8, g9).
 
 * x6 and exact-f32: every image's bpp, PSNR and MS-SSIM against the reference at 1e-5 relative
   (MS-SSIM is well conditioned here, unlike at G5's degenerate 6.6 dB point), the latents
@@ -23,25 +24,28 @@ from oracle import codec_ref as oracle
 pytestmark = pytest.mark.gpu
 
 REL = 1e-5
-# bf16 mode vs the reference, per image (measured: see the printed maxima)
+# bf16 mode vs the reference, worst image of either set (measured: flips 0.28 %, Δbpp 1.0e-3 /
+# 3.7e-3 relative, ΔPSNR 0.017 / 0.061 dB, ΔMS-SSIM 2.2e-4 at N = 128 / 192)
 BF16_MAX_FLIP_RATE = 0.01
-BF16_MAX_DBPP_REL = 2e-3
-BF16_MAX_DPSNR_DB = 0.03
+BF16_MAX_DBPP_REL = 1e-2
+BF16_MAX_DPSNR_DB = 0.1
 BF16_MAX_DMSSSIM = 5e-4
 
 
-def _meta(golden_dir):
-    return json.load(open(os.path.join(golden_dir, "g8_kodak24_synth_n128_trained.json")))
+SETS = ["g8_kodak24_synth_n128_trained.json", "g9_kodak24_synth_n192_trained.json"]
 
 
-def _state(golden_dir):
-    d = np.load(os.path.join(golden_dir, "g8_weights_n128.npz"))
-    return {k: torch.from_numpy(d[k].astype(np.float32)) for k in d.files}
+@pytest.fixture(params=SETS, ids=["G8-N128", "G9-N192"])
+def opset(request, golden_dir):
+    meta = json.load(open(os.path.join(golden_dir, request.param)))
+    d = np.load(os.path.join(golden_dir, meta["weights"]))
+    meta["state"] = {k: torch.from_numpy(d[k].astype(np.float32)) for k in d.files}
+    return meta
 
 
-def _net(golden_dir, device):
-    net = ImageCompressor(out_channel_N=128)
-    net.load_state_dict(_state(golden_dir))
+def _net(meta, device):
+    net = ImageCompressor(out_channel_N=meta["N"])
+    net.load_state_dict(meta["state"])
     return net.to(device).eval()
 
 
@@ -61,15 +65,15 @@ def oracle_metrics_given_latents(y_hat, x, sd):
 
 
 @pytest.mark.parametrize("precision", ["x6", "fp32"])
-def test_g8_all_images(device, golden_dir, precision):
+def test_g8_all_images(device, opset, precision):
     """Per image: the latents equal the oracle's (pinned to the reference) except at legitimate
     near-ties. Without flips, bpp / PSNR / MS-SSIM match the reference's values at 1e-5; with
     k flips (a few per million latents), they match the reference's outputs for the same ŷ —
     the oracle's decoder and rate model on the GPU's latents — at 1e-5."""
     from test_gpu_parity import check_latents
-    meta = _meta(golden_dir)
-    sd = _state(golden_dir)
-    net = _net(golden_dir, device)
+    meta = opset
+    sd = meta["state"]
+    net = _net(meta, device)
     old = kernels.precision()
     kernels.set_precision(precision)
     flips = flipped_images = 0
@@ -90,19 +94,19 @@ def test_g8_all_images(device, golden_dir, precision):
             assert got == pytest.approx(ref, rel=REL), (row["index"], n, got, ref)
     finally:
         kernels.set_precision(old)
-    print(f"G8 {precision}: {flips} near-tie latent flips in {flipped_images} of 24 images "
-          f"({24 * 128 * 32 * 48} latents)")
+    print(f"N={meta['N']} {precision}: {flips} near-tie latent flips in {flipped_images} of 24 "
+          f"images ({24 * meta['N'] * 32 * 48} latents)")
 
 
-def test_g8_testkodak_lines_verbatim(device, golden_dir):
+def test_g8_testkodak_lines_verbatim(device, opset):
     """train.py:171-179 as written on the build's names, for images whose x6 latents equal the
     reference's (checked): bpp / PSNR / MS-SSIM at 1e-5 against the reference's values."""
     ns = {}
     exec("from iclr_17_compression_amd.model import *", ns)
     ms_ssim, np_, torch_ = ns["ms_ssim"], ns["np"], ns["torch"]
-    meta = _meta(golden_dir)
-    sd = _state(golden_dir)
-    net = _net(golden_dir, device)
+    meta = opset
+    sd = meta["state"]
+    net = _net(meta, device)
     done = 0
     for row in meta["images"]:
         input = _image(meta, row).to(device)
@@ -129,9 +133,9 @@ def test_g8_testkodak_lines_verbatim(device, golden_dir):
     assert done == 4
 
 
-def test_g8_bf16_deviation(device, golden_dir):
-    meta = _meta(golden_dir)
-    net = _net(golden_dir, device)
+def test_g8_bf16_deviation(device, opset):
+    meta = opset
+    net = _net(meta, device)
     old = kernels.precision()
     worst = {"flip": 0.0, "dbpp": 0.0, "dpsnr": 0.0, "dms": 0.0}
     try:
@@ -149,7 +153,7 @@ def test_g8_bf16_deviation(device, golden_dir):
             worst["dms"] = max(worst["dms"], abs(ev["ms_ssim"][0].item() - row["ms_ssim"]))
     finally:
         kernels.set_precision(old)
-    print("G8 bf16 vs reference, worst image:", {k: f"{v:.3e}" for k, v in worst.items()})
+    print(f"N={meta['N']} bf16 vs reference, worst image:", {k: f"{v:.3e}" for k, v in worst.items()})
     assert worst["flip"] < BF16_MAX_FLIP_RATE
     assert worst["dbpp"] < BF16_MAX_DBPP_REL
     assert worst["dpsnr"] < BF16_MAX_DPSNR_DB

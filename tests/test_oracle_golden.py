@@ -101,16 +101,15 @@ def test_g5_ms_ssim(golden_dir):
     assert oracle.ms_ssim(clipped, x, 1.0).item() == row["ms_ssim"]
 
 
-def g8_state_dict(golden_dir):
-    d = np.load(os.path.join(golden_dir, "g8_weights_n128.npz"))
-    return {k: torch.from_numpy(d[k].astype(np.float32)) for k in d.files}
-
-
-def test_g8_operating_point(golden_dir):
-    """The trained N=128 operating point (PSNR ≈ 28 dB, bpp ≈ 0.21): the oracle reproduces the
-    reference's bpp, PSNR and MS-SSIM of two Kodak-synth images bit for bit."""
-    meta = json.load(open(os.path.join(golden_dir, "g8_kodak24_synth_n128_trained.json")))
-    sd = g8_state_dict(golden_dir)
+@pytest.mark.parametrize("fixture", ["g8_kodak24_synth_n128_trained.json",
+                                     "g9_kodak24_synth_n192_trained.json"])
+def test_g8_operating_point(golden_dir, fixture):
+    """The trained operating points (G8 N=128, G9 N=192; PSNR ≈ 27–28 dB, bpp ≈ 0.2–0.3): the
+    oracle reproduces the reference's bpp, PSNR and MS-SSIM of two Kodak-synth images bit for
+    bit."""
+    meta = json.load(open(os.path.join(golden_dir, fixture)))
+    d = np.load(os.path.join(golden_dir, meta["weights"]))
+    sd = {k: torch.from_numpy(d[k].astype(np.float32)) for k in d.files}
     for row in meta["images"][:2]:
         x = torch.from_numpy(synth.to_unit_float(
             synth.smooth_image_u8(meta["image_seed_base"] + row["index"], row["height"], row["width"])))[None]

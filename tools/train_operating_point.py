@@ -1,11 +1,13 @@
-"""Trains the codec to a realistic operating point for the G8 fixtures (GPU, x6 training path):
-N = 128 (train.py's default out_channel_N), λ = 0.01·255² (train_lambda 650.25), Adam, ±5 clamp,
+"""Trains the codec to a realistic operating point for the G8 / G9 fixtures (GPU, x6 training
+path): N = 128 (train.py's default out_channel_N; G8) or 192 (BASELINE C2's N; G9), λ = 0.01·255²
+(train_lambda 650.25), Adam, ±5 clamp,
 B = 16 random 256² crops with h/v flips of 96 smooth synthetic photos (synth.smooth_image_u8,
 seeds 20000+, disjoint from the Kodak-synth seeds 100..123). Writes the state dict as
-gpurun_out/op_point/weights_n128.npz (copied to tests/golden/g8_weights_n128.npz by hand) and
+gpurun_out/op_point/weights_n{N}.npz (stored fp16 as tests/golden/g8_weights_n128.npz /
+g9_weights_n192.npz) and
 prints the running loss / PSNR / bpp.
 
-    python tools/train_operating_point.py [--steps 20000]
+    python tools/train_operating_point.py [--steps 20000] [--N 128|192]
 """
 import argparse
 import os
@@ -25,6 +27,7 @@ ap.add_argument("--steps", type=int, default=20000)
 ap.add_argument("--batch", type=int, default=16)
 ap.add_argument("--lr", type=float, default=3e-4)
 ap.add_argument("--out", default="gpurun_out/op_point")
+ap.add_argument("--N", type=int, default=128)
 args = ap.parse_args()
 dev = torch.device("cuda:0")
 torch.manual_seed(17)
@@ -36,7 +39,7 @@ for i in range(96):
     pool.append(torch.from_numpy(synth.to_unit_float(synth.smooth_image_u8(20000 + i, H, W))).to(dev))
 print(f"pool of {len(pool)} images ready", flush=True)
 
-net = ImageCompressor(out_channel_N=128).to(dev).train()
+net = ImageCompressor(out_channel_N=args.N).to(dev).train()
 opt = FusedAdam(list(net.parameters()), lr=args.lr, grad_clip=5)
 lam = 0.01 * 255.0 ** 2
 g = torch.Generator().manual_seed(5)
@@ -81,6 +84,6 @@ with torch.no_grad():
         r = net.evaluate(x, want_msssim=True)
         ev.append((r["bpp"].item(), r["psnr"].item(), r["ms_ssim"].item()))
 print("kodak-synth eval (bpp, psnr, ms_ssim) mean:", np.mean(ev, axis=0).round(5).tolist(), flush=True)
-np.savez(os.path.join(args.out, "weights_n128.npz"),
+np.savez(os.path.join(args.out, f"weights_n{args.N}.npz"),
          **{k: v.detach().cpu().numpy() for k, v in net.state_dict().items()})
 print("saved", flush=True)

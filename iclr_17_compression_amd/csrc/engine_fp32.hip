@@ -1143,13 +1143,11 @@ __device__ __forceinline__ int d3_col(int j) {
   return co * 16 + ry * 4 + rx;
 }
 
-// BF: the bf16 throughput mode (engine_bf16.hip) — the input is ONE bf16 plane (bf16 NHWC), the
-// weights are rounded to bf16 in the loop and each MAC is one bf16 product.
-template <int CI, bool BF = false>
+template <int CI>
 __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) {
   constexpr int KCH = 32, NCH = CI / KCH, NSTEP = 9 * NCH;
   constexpr int MT = 4, NT = 3;
-  constexpr int NPL = BF ? 1 : 3;                         // input planes
+  constexpr int NPL = 3;                                  // input planes
   constexpr int NAI = (NPL * D3_PPX + 15) / 16;           // A wave-instructions per chunk
   constexpr int AI_W = (NAI + 3) / 4;   // x6: 16 (wave 0..3 takes i = w + 4j, i < 61)
   static_assert(3 * 64 * 65 <= D3_LDS, "epilogue block fits the stages");
@@ -1225,27 +1223,6 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
     constexpr int NTT = decltype(ntt)::value;   // tiles this tap touches
     const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
     const float* sb = sB + buf * D3_SB + 2 * g * 48 * 4;
-    if constexpr (BF) {   // one bf16 product: weights rounded to nearest even, the bf16 plane
-      bf8 Bb[NTT];
-#pragma unroll
-      for (int nt = 0; nt < NTT; ++nt) {
-        const int jc = nt * 16 + (lane & 15);
-        const f4 w0 = *(const f4*)(sb + jc * 4), w1 = *(const f4*)(sb + 48 * 4 + jc * 4);
-        Bb[nt] = bf8{(__bf16)w0[0], (__bf16)w0[1], (__bf16)w0[2], (__bf16)w0[3],
-                     (__bf16)w1[0], (__bf16)w1[1], (__bf16)w1[2], (__bf16)w1[3]};
-      }
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const int p = prow + (mt + dy) * D3_PS + dx;
-        const unsigned short* sa =
-            (const unsigned short*)(sA + p * 16 + ((g ^ (((p >> 2) & 1) << 1)) * 4));
-        const bf8 Ab = __builtin_bit_cast(bf8, *(const u4*)(sa));
-#pragma unroll
-        for (int nt = 0; nt < NTT; ++nt)
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ab, Bb[nt], acc[mt][nt], 0, 0, 0);
-      }
-      return;
-    }
     bf8 Bh[NTT], Bm[NTT], Bl[NTT];
 #pragma unroll
     for (int nt = 0; nt < NTT; ++nt) {
@@ -1476,6 +1453,183 @@ __global__ void __launch_bounds__(256) conv1_gdn_kernel(const EngineArgs a) {
   } else {
     static_assert(EPI == EPI_IGDN_BWD, "conv1 kernel epilogues: GDN fwd, IGDN bwd");
     gdn_bwd_epilogue<CO, MT, NT, true>(acc, smem, a, t, wm, ncol0, lane);
+  }
+}
+
+// ------------------------------------------------------------ deconv3 in the bf16 mode
+// synthesis_17.py:23-25 + model.py:59 on a bf16 NHWC input: the all-phase GEMM of
+// deconv3_x6_kernel (48 columns = 16 output phases × 3 channels, d3_col order, dy = −1 / dx = −1
+// taps on the tiles that hold their non-zero weights) with one bf16 product per MAC, but all 9
+// taps of a 32-channel chunk per barrier: the chunk's 18×18 patch and its 9 weight slices are
+// double-buffered by LDS-DMA (153 KB, one workgroup of 8 waves per CU), so a chunk costs one
+// barrier instead of nine. Wave w owns base rows 2w, 2w+1. The accumulation order (chunk, tap)
+// and the operands (weights rounded to bf16 in the loop, one bf16 product per MAC) are those of the
+// per-tap bf16 kernel this replaces, so the results are bit-identical to it.
+template <int CI>
+__global__ void __launch_bounds__(512) deconv3_bf16_kernel(const EngineArgs a) {
+  constexpr int KCH = 32, NCH = CI / KCH, MT = 2, NT = 3, NW = 8;
+  constexpr int NAI = (D3_PPX + 15) / 16;   // 21 patch wave-instructions per chunk (16 px each)
+  constexpr int SA = NAI * 256;             // patch buffer floats
+  constexpr int PB = 9 * D3_SB;             // weight floats per chunk: [tap][kq 8][48][4]
+  constexpr int NBI = PB / 256;             // 54 weight wave-instructions per chunk
+  constexpr int KA = (NAI + NW - 1) / NW, KB = (NBI + NW - 1) / NW;
+  constexpr int LDS = 2 * SA + 2 * PB;
+  static_assert(3 * 64 * 65 + 16 <= LDS, "epilogue block fits");
+  __shared__ __attribute__((aligned(16))) float smem[LDS];
+  float* const sA = smem;
+  float* const sB = smem + 2 * SA;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int bid = blockIdx.x;
+  const int tx = bid % a.tiles_x;
+  bid /= a.tiles_x;
+  const int ty = bid % a.tiles_y;
+  const int b = bid / a.tiles_y;
+
+  // patch DMA: instruction i, slot q = 16i + lane/4 (patch pixel), physical piece lane & 3 ←
+  // logical piece (lane & 3) ^ swizzle(q); -1: zero line
+  int asrc[KA];
+#pragma unroll
+  for (int j = 0; j < KA; ++j) {
+    const int i = wave + NW * j;
+    const int p = i * 16 + (lane >> 2);
+    const int r = p / D3_PS, c = p - r * D3_PS;
+    const int iy = ty * D3_BS - 1 + r, ix = tx * D3_BS - 1 + c;
+    const bool ok = i < NAI && p < D3_PPX && (unsigned)iy < (unsigned)a.Hin &&
+                    (unsigned)ix < (unsigned)a.Win;
+    const int g = (lane & 3) ^ (((p >> 2) & 1) << 1);
+    asrc[j] = ok ? (iy * a.Win + ix) * CI + g * 8 : -1;
+  }
+  // weight DMA: instruction i = tap t (6 per tap), slot (kq, j) ← packed (cc·8 + kq, d3_col(j))
+  int bsrc[KB];
+#pragma unroll
+  for (int j = 0; j < KB; ++j) {
+    const int i = wave + NW * j;
+    const int t = i / 6, w = (i - t * 6) * 64 + lane, kq = w / 48, jj = w - kq * 48;
+    bsrc[j] = t * CI * 48 + (kq * 48 + d3_col(jj)) * 4;
+  }
+  const unsigned short* __restrict__ inb = a.in_split + (long)b * a.Hin * a.Win * CI;
+  auto issue = [&](int cc, int buf) {
+#pragma unroll
+    for (int j = 0; j < KA; ++j) {
+      const int i = wave + NW * j;
+      if (i < NAI)
+        glds16(asrc[j] >= 0 ? (const float*)(inb + asrc[j] + cc * KCH) : g_zero16,
+               sA + buf * SA + i * 256);
+    }
+#pragma unroll
+    for (int j = 0; j < KB; ++j) {
+      const int i = wave + NW * j;
+      if (i < NBI) glds16(a.w + (long)cc * KCH * 48 + bsrc[j], sB + buf * PB + i * 256);
+    }
+  };
+
+  f4 acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4;
+  const int prow = (2 * wave + 1) * D3_PS + 1 + (lane & 15);   // window origin for mt = 0
+  auto compute = [&](int buf, int tap, auto ntt) {
+    constexpr int NTT = decltype(ntt)::value;   // tiles this tap touches
+    const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+    const float* sb = sB + buf * PB + tap * D3_SB + 2 * g * 48 * 4;
+    bf8 Bb[NTT];
+#pragma unroll
+    for (int nt = 0; nt < NTT; ++nt) {
+      const int jc = nt * 16 + (lane & 15);
+      const f4 w0 = *(const f4*)(sb + jc * 4), w1 = *(const f4*)(sb + 48 * 4 + jc * 4);
+      Bb[nt] = bf8{(__bf16)w0[0], (__bf16)w0[1], (__bf16)w0[2], (__bf16)w0[3],
+                   (__bf16)w1[0], (__bf16)w1[1], (__bf16)w1[2], (__bf16)w1[3]};
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int p = prow + (mt + dy) * D3_PS + dx;
+      const unsigned short* sa =
+          (const unsigned short*)(sA + buf * SA + p * 16 + ((g ^ (((p >> 2) & 1) << 1)) * 4));
+      const bf8 Ab = __builtin_bit_cast(bf8, *(const u4*)(sa));
+#pragma unroll
+      for (int nt = 0; nt < NTT; ++nt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ab, Bb[nt], acc[mt][nt], 0, 0, 0);
+    }
+  };
+
+  issue(0, 0);
+  for (int cc = 0; cc < NCH; ++cc) {
+    __syncthreads();   // vmcnt(0) + barrier: chunk cc landed; buffer (cc+1)&1 is free
+    if (cc + 1 < NCH) issue(cc + 1, (cc + 1) & 1);
+    const int buf = cc & 1;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      if (tap < 3)
+        compute(buf, tap, std::integral_constant<int, 1>{});
+      else if (tap == 3 || tap == 6)
+        compute(buf, tap, std::integral_constant<int, 2>{});
+      else
+        compute(buf, tap, std::integral_constant<int, 3>{});
+    }
+  }
+  __syncthreads();     // stage reads done before the epilogue reuses LDS
+
+  // epilogue: column n = co·16 + ry·4 + rx of row m = (by, bx) → output (4by + ry, 4bx + rx);
+  // the waves 2q, 2q+1 store output quadrant q's upper / lower 16 rows
+  constexpr int OS = 4 * D3_BS, SS = OS + 1;
+  float* sO = smem;   // [3][64][65]
+  float* red = smem + 3 * OS * SS;
+  const int H = a.Hout, W = a.Wout;
+  float sse = 0.f;
+  int pcol[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) pcol[nt] = d3_col(nt * 16 + (lane & 15));
+  const int q = wave >> 1, hf = wave & 1, qy = q >> 1, qx = q & 1;
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass == 1 && a.recon == nullptr) break;
+    float* dst = pass == 0 ? a.out : a.recon;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int by = 2 * wave + mt, bx = 4 * g + r;
+          const int co = pcol[nt] >> 4, ph = pcol[nt] & 15;
+          float v = acc[mt][nt][r] + a.bias[co];
+          if (pass == 0) v = fminf(fmaxf(v, 0.0f), 1.0f);
+          sO[(co * OS + by * 4 + (ph >> 2)) * SS + bx * 4 + (ph & 3)] = v;
+        }
+    __syncthreads();
+    const bool sse_pass = pass == (a.sse_unclipped ? 1 : 0) && a.xref != nullptr;
+    for (int k = lane; k < 3 * 16 * 8; k += 64) {
+      const int c4 = k & 7, row = (k >> 3) & 15, co = k >> 7;
+      const int oyl = qy * 32 + hf * 16 + row, oxl = qx * 32 + c4 * 4;
+      const int oy = ty * OS + oyl, ox = tx * OS + oxl;
+      if (oy >= H || ox >= W) continue;
+      const float* sp = sO + (co * OS + oyl) * SS + oxl;
+      const f4 v = f4{sp[0], sp[1], sp[2], sp[3]};
+      const long off = (((long)b * 3 + co) * H + oy) * W + ox;
+      *(f4*)(dst + off) = v;
+      if (sse_pass) {
+        const f4 xr = *(const f4*)(a.xref + off);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = v[e] - xr[e];
+          sse += d * d;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (a.xref != nullptr) {
+    sse = wave_sum(sse);
+    if (lane == 0) red[wave] = sse;
+    __syncthreads();
+    const int ty8 = 2 * ty + qy, tx8 = 2 * tx + qx;
+    const int tiles_x8 = (a.gw + 7) / 8;
+    if (hf == 0 && lane == 0 && ty8 * 8 < a.gh && tx8 * 8 < a.gw)
+      a.partial[(long)b * a.partials_per_image + ty8 * tiles_x8 + tx8] =
+          (double)(red[wave] + red[wave + 1]);
   }
 }
 
@@ -2221,9 +2375,9 @@ static int launch_deconv3_halo(const uint16_t* in, int B, int H, int W, int N, c
   dim3 grid(a.tiles_x * a.tiles_y * B);
   if (bf) {
     if (N == 192)
-      hipLaunchKernelGGL((deconv3_x6_kernel<192, true>), grid, dim3(256), 0, S(stream), a);
+      hipLaunchKernelGGL((deconv3_bf16_kernel<192>), grid, dim3(512), 0, S(stream), a);
     else
-      hipLaunchKernelGGL((deconv3_x6_kernel<128, true>), grid, dim3(256), 0, S(stream), a);
+      hipLaunchKernelGGL((deconv3_bf16_kernel<128>), grid, dim3(512), 0, S(stream), a);
   } else {
     if (N == 192)
       hipLaunchKernelGGL((deconv3_x6_kernel<192>), grid, dim3(256), 0, S(stream), a);

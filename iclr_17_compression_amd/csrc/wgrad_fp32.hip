@@ -147,6 +147,19 @@ __device__ __forceinline__ uint2 tr16(const unsigned short* lds) {
   return __builtin_bit_cast(uint2, v);
 }
 
+// The same transposed read as inline asm, which the compiler does not track: its LDS-DMA alias
+// check would otherwise make every LDS read of stage s wait (vmcnt(0)) for the DMA of stage s+1
+// that was just issued, serialising the copy with the MFMAs. The caller publishes the results
+// with lgkm_wait, which ties each fragment to a full lgkmcnt(0) so no use can precede it.
+__device__ __forceinline__ uint2 tr16a(unsigned lds_byte_addr) {
+  uint2 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(lds_byte_addr) : "memory");
+  return v;
+}
+__device__ __forceinline__ void lgkm_wait(u4& v) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v));
+}
+
 template <int M, int CB, int WM, int WN, int KS>
 __global__ void __launch_bounds__(512) wgrad_x6_kernel(const unsigned short* __restrict__ G6,
                                                           long pg, const unsigned short* __restrict__ X6,
@@ -290,6 +303,7 @@ __global__ void __launch_bounds__(512) wgrad_x6_kernel(const unsigned short* __r
     boff[nt] = (8 * g + q) * CB + (((ch >> 3) ^ frx) << 3) + (ch & 7);
   }
 
+  const unsigned sbase = (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned short*)smem;
   if (nsteps > 0) issue(0);
   for (int s = 0; s < nsteps; ++s) {
     __syncthreads();   // stage s landed for every wave; stage (s+1)&1 is free
@@ -297,34 +311,48 @@ __global__ void __launch_bounds__(512) wgrad_x6_kernel(const unsigned short* __r
       advance();
       issue((s + 1) & 1);
     }
-    const unsigned short* st = smem + (s & 1) * STAGE;
-    bf8 Bf[3][NT];
+    const unsigned st = sbase + (s & 1) * STAGE * 2;   // LDS byte address of the stage
+    auto frag = [&](unsigned a, int rowe) {             // 8 pixels (k) of 4 channels
+      const uint2 lo = tr16a(a), hi = tr16a(a + 8 * rowe);
+      return u4{lo.x, lo.y, hi.x, hi.y};
+    };
+    u4 Bf[3][NT], Af[2][3];
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const unsigned short* b = st + 3 * GPL + pl * XPL + boff[nt];
-        const uint2 lo = tr16(b), hi = tr16(b + 4 * CB);
-        Bf[pl][nt] = __builtin_bit_cast(bf8, u4{lo.x, lo.y, hi.x, hi.y});
-      }
+      for (int nt = 0; nt < NT; ++nt) Bf[pl][nt] = frag(st + 2 * (3 * GPL + pl * XPL + boff[nt]), CB);
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) Af[0][pl] = frag(st + 2 * (pl * GPL + aoff[0]), M);
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) lgkm_wait(Bf[pl][nt]);
+      lgkm_wait(Af[0][pl]);
+    }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      bf8 Af[3];
+      const int cur = mt & 1;
+      if (mt + 1 < MT) {   // the next row tile's fragments load under this one's MFMAs
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) {
-        const unsigned short* a = st + pl * GPL + aoff[mt];
-        const uint2 lo = tr16(a), hi = tr16(a + 4 * M);
-        Af[pl] = __builtin_bit_cast(bf8, u4{lo.x, lo.y, hi.x, hi.y});
+        for (int pl = 0; pl < 3; ++pl) Af[cur ^ 1][pl] = frag(st + 2 * (pl * GPL + aoff[mt + 1]), M);
       }
+      const bf8 A0 = __builtin_bit_cast(bf8, Af[cur][0]), A1 = __builtin_bit_cast(bf8, Af[cur][1]),
+                 A2 = __builtin_bit_cast(bf8, Af[cur][2]);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
+        const bf8 B0 = __builtin_bit_cast(bf8, Bf[0][nt]), B1 = __builtin_bit_cast(bf8, Bf[1][nt]),
+                  B2 = __builtin_bit_cast(bf8, Bf[2][nt]);
         f4 c = acc[mt][nt];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af[2], Bf[0][nt], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af[0], Bf[2][nt], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af[1], Bf[1][nt], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af[1], Bf[0][nt], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af[0], Bf[1][nt], c, 0, 0, 0);
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af[0], Bf[0][nt], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A2, B0, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A0, B2, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A1, B1, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A1, B0, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A0, B1, c, 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A0, B0, c, 0, 0, 0);
+      }
+      if (mt + 1 < MT) {
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) lgkm_wait(Af[cur ^ 1][pl]);
       }
     }
   }
@@ -501,6 +529,209 @@ __global__ void __launch_bounds__(512) gdn_wgrad_x6_kernel(const float* __restri
         const int c = wn * (C / WN) + nt * 16 + (lane & 15);
         out[(long)m * C + c] = acc[mt][nt][r];
       }
+}
+
+// The k5 s2 p2 weight gradient in x6 with one KERNEL ROW per workgroup: workgroup (kh, 64-channel
+// block cb of C, split) accumulates dW[m][cb·64 ..][kh][0..4] for all M rows. A k-step is 32 output
+// pixels — two output rows × 16 columns — whose G rows [32][M] all five taps kw share, and whose
+// X operands for the five taps are columns 2ow − 2 + kw of the same two input rows: one
+// [2 × 36][64] X image serves every kw (the tap picks rows 2k + kw of it). Against a workgroup per
+// tap this moves 64 KB per 1440 MFMAs instead of 74 KB per 864 — the LDS-DMA stream, not the
+// MFMAs, bounded the per-tap kernel. 8 waves: wave (wm, wn) owns rows wm·M/4 .. and columns
+// wn·32 .. of every tap, i.e. 5 × (M/64) × 2 tiles of 16×16 (120 accumulator VGPRs at M = 192).
+// X image: 128-byte rows (64 channels), row r stored at slot r ^ bit4(r) and its 32-byte column
+// pairs XOR-ed with (r >> 1) & 3, so a transposed read's 32-lane half — rows r0 + 2i and
+// r0 + 16 + 2i, one pair each — hits 8 distinct bank windows. Partials land in the same
+// [split][m][c][tap] layout as the per-tap kernels.
+template <int M>
+__global__ void __launch_bounds__(512) wgrad_x6_row_kernel(const unsigned short* __restrict__ G6,
+                                                              long pg, const unsigned short* __restrict__ X6,
+                                                              long pxs, int B, int Ho, int Wo, int Hi,
+                                                              int Wi, int C, int nsplit,
+                                                              float* __restrict__ part) {
+  constexpr int NW = 8, KW = 5, CBX = 64;
+  constexpr int MT = M / 64, NT = 2;                 // per wave: M/4 rows × 32 columns per tap
+  constexpr int XROW = 36, XR = 2 * XROW;            // X image rows (35 used per input row)
+  constexpr int GPL = KP * M, XPL = XR * CBX;        // u16 per plane image
+  constexpr int STAGE = 3 * GPL + 3 * XPL;
+  constexpr int GPR = M / 8;                         // 16-byte pieces per G row
+  constexpr int NGI = KP * GPR / 64, NXI = XR * 8 / 64;
+  constexpr int NI = 3 * NGI + 3 * NXI, NI_W = (NI + NW - 1) / NW;
+  static_assert(M == 192 || M == 128, "M");
+  static_assert(KP * GPR % 64 == 0 && XR * 8 % 64 == 0, "whole DMA instructions");
+  __shared__ __attribute__((aligned(16))) unsigned short smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 3, wn = wave >> 2;
+  // XCD-aware order (as wgrad_x6_kernel): a split's 5·C/64 workgroups share one XCD's L2
+  const int nwg = gridDim.x;
+  const int L = (blockIdx.x % 8) * (nwg / 8) + blockIdx.x / 8;
+  const int tiles = KW * (C / CBX);
+  if (L >= tiles * nsplit) return;   // padding workgroups (before any barrier)
+  const int tile = L % tiles, split = L / tiles;
+  const int kh = tile % KW, cb = tile / KW;
+  const int OHP = (Ho + 1) / 2, OWB = (Wo + 15) / 16;
+  const long NSTEP = (long)B * OHP * OWB;
+  const long per = (NSTEP + nsplit - 1) / nsplit;
+  const long s0 = split * per;
+  const long s1 = s0 + per < NSTEP ? s0 + per : NSTEP;
+  const int nsteps = s1 > s0 ? (int)(s1 - s0) : 0;
+
+  // DMA slots: G slot (row k = 16·dr + dc, physical piece) ← piece ^ swz6(k) of output pixel
+  // (oh0 + dr, ow0 + dc); X slot (physical row R, 16-byte chunk J) ← chunk of logical row
+  // r = R ^ bit4(R): input (2·(oh0 + r / 36) − 2 + kh, 2·ow0 − 2 + r % 36).
+  int sa[NI_W], sb[NI_W];   // G: (dr, dc) / X: (rb, col); and the element offset in the plane row
+#pragma unroll
+  for (int j = 0; j < NI_W; ++j) {
+    const int i = wave + NW * j;
+    if (i < 3 * NGI) {
+      const int pc = (i % NGI) * 64 + lane;
+      const int k = pc / GPR, piece = (pc % GPR) ^ swz6(k, M);
+      sa[j] = ((k >> 4) << 8) | (k & 15);
+      sb[j] = piece * 8;
+    } else {
+      const int ii = i - 3 * NGI;
+      const int R = (ii % NXI) * 8 + (lane >> 3), J = lane & 7;
+      const int r = R ^ ((R >> 4) & 1);
+      const int chunk = ((((J >> 1) ^ ((r >> 1) & 3)) << 1) | (J & 1));
+      sa[j] = ((r / XROW) << 8) | (r % XROW);
+      sb[j] = cb * CBX + chunk * 8;
+    }
+  }
+  auto issue = [&](int s, int buf) {
+    long t = s0 + s;
+    const int owb = (int)(t % OWB);
+    t /= OWB;
+    const int oh0 = (int)(t % OHP) * 2, b = (int)(t / OHP), ow0 = owb * 16;
+    unsigned short* st = smem + buf * STAGE;
+#pragma unroll
+    for (int j = 0; j < NI_W; ++j) {
+      const int i = wave + NW * j;
+      if (NI % NW != 0 && i >= NI) break;   // wave-uniform
+      const void* src = g_wzero;
+      unsigned short* dst;
+      if (i < 3 * NGI) {
+        const int pl = i / NGI;
+        const int oh = oh0 + (sa[j] >> 8), ow = ow0 + (sa[j] & 255);
+        if (oh < Ho && ow < Wo) src = G6 + pl * pg + ((long)(b * Ho + oh) * Wo + ow) * M + sb[j];
+        dst = st + pl * GPL + (i % NGI) * 512;
+      } else {
+        const int ii = i - 3 * NGI, pl = ii / NXI;
+        const int col = sa[j] & 255;
+        const int iy = 2 * (oh0 + (sa[j] >> 8)) - 2 + kh, ix = 2 * ow0 - 2 + col;
+        if (col < 2 * 16 + 3 && (unsigned)iy < (unsigned)Hi && (unsigned)ix < (unsigned)Wi)
+          src = X6 + pl * pxs + ((long)(b * Hi + iy) * Wi + ix) * C + sb[j];
+        dst = st + 3 * GPL + pl * XPL + (ii % NXI) * 512;
+      }
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
+
+  f4 acc[KW][MT][NT];
+#pragma unroll
+  for (int kw = 0; kw < KW; ++kw)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[kw][mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
+  // transposed-read lanes: group g = lane >> 4 takes k-rows 8g .. 8g+7 (two reads of 4); lane
+  // 4q + p of the group addresses k-row q (+4), channels 4p .. 4p+3 of its 16-column block
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const int frg = swz6(8 * g + q, M);
+  int aoff[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int ch = wm * (M / 4) + mt * 16 + 4 * pp;
+    aoff[mt] = (8 * g + q) * M + (((ch >> 3) ^ frg) << 3) + (ch & 7);
+  }
+  // X row of k-row k for tap kw: (k >> 4)·36 + 2·(k & 15) + kw
+  const int k0 = 8 * g + q;
+  const int xr0 = (k0 >> 4) * XROW + 2 * (k0 & 15), xr1 = xr0 + 8;   // k0 + 4 stays in its half
+  auto xoff = [&](int r, int nt) {   // u16 offset in a plane image
+    const int R = r ^ ((r >> 4) & 1);
+    return R * CBX + ((((2 * wn + nt) ^ ((r >> 1) & 3))) << 4) + 4 * pp;
+  };
+  const unsigned sbase = (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned short*)smem;
+  auto frag = [&](unsigned lo_addr, unsigned hi_addr) {
+    const uint2 lo = tr16a(lo_addr), hi = tr16a(hi_addr);
+    return u4{lo.x, lo.y, hi.x, hi.y};
+  };
+
+  if (nsteps > 0) issue(0, 0);
+  for (int s = 0; s < nsteps; ++s) {
+    __syncthreads();   // stage s landed for every wave; stage (s+1)&1 is free
+    if (s + 1 < nsteps) issue(s + 1, (s + 1) & 1);
+    const unsigned st = sbase + (s & 1) * STAGE * 2;
+    const unsigned sx = st + 3 * GPL * 2;
+    u4 Af[MT][3], Bf[2][NT][3];
+    auto load_b = [&](int kw, int buf) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int o0 = xoff(xr0 + kw, nt), o1 = xoff(xr1 + kw, nt);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          Bf[buf][nt][pl] = frag(sx + 2 * (pl * XPL + o0), sx + 2 * (pl * XPL + o1));
+      }
+    };
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        Af[mt][pl] = frag(st + 2 * (pl * GPL + aoff[mt]), st + 2 * (pl * GPL + aoff[mt] + 4 * M));
+    load_b(0, 0);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) lgkm_wait(Af[mt][pl]);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) lgkm_wait(Bf[0][nt][pl]);
+#pragma unroll
+    for (int kw = 0; kw < KW; ++kw) {
+      const int cur = kw & 1;
+      if (kw + 1 < KW) load_b(kw + 1, cur ^ 1);   // the next tap's X fragments under these MFMAs
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const bf8 A0 = __builtin_bit_cast(bf8, Af[mt][0]), A1 = __builtin_bit_cast(bf8, Af[mt][1]),
+                   A2 = __builtin_bit_cast(bf8, Af[mt][2]);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const bf8 B0 = __builtin_bit_cast(bf8, Bf[cur][nt][0]),
+                    B1 = __builtin_bit_cast(bf8, Bf[cur][nt][1]),
+                    B2 = __builtin_bit_cast(bf8, Bf[cur][nt][2]);
+          f4 c = acc[kw][mt][nt];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A2, B0, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A0, B2, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A1, B1, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A1, B0, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A0, B1, c, 0, 0, 0);
+          acc[kw][mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A0, B0, c, 0, 0, 0);
+        }
+      }
+      if (kw + 1 < KW) {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl) lgkm_wait(Bf[cur ^ 1][nt][pl]);
+      }
+    }
+  }
+  // part[split][m][c][tap]
+  float* out = part + (long)split * M * C * 25;
+#pragma unroll
+  for (int kw = 0; kw < KW; ++kw)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = wm * (M / 4) + mt * 16 + 4 * (lane >> 4) + r;
+          const int c = cb * CBX + wn * 32 + nt * 16 + (lane & 15);
+          out[((long)m * C + c) * 25 + kh * 5 + kw] = acc[kw][mt][nt][r];
+        }
 }
 
 // k9 s4 p4 weight gradient in x6 as a 1×1 one: the 243 (c, kh, kw) window values of every
@@ -725,8 +956,7 @@ __global__ void plane_sum_kernel(const float* __restrict__ A, int C, long HW, in
   }
 }
 
-// x6 wgrad: a workgroup owns all M rows and 192 | 128 columns (C % that == 0), one per CU
-int wgrad6_cb(int C) { return C % 192 == 0 ? 192 : 128; }
+// x6 wgrad: one workgroup per CU
 int wgrad6_splits(long P, int tiles) {   // one round of 256 workgroup slots (1 per CU)
   int s = 256 / tiles;
   const long maxs = P / 256 > 1 ? P / 256 : 1;
@@ -762,7 +992,7 @@ int iclr17_sum_rows(const float* part, int T, int C, float* workspace, float* ou
 size_t iclr17_wgrad_workspace_size(int kind, int B, int Ho, int Wo, int M, int C) {
   const long P = (long)B * Ho * Wo;
   if (kind == 9) return (size_t)wgrad9_splits(B * ((Wo + 7) / 8) * ((Ho + 7) / 8)) * M * 243;
-  if (kind == 6) return (size_t)wgrad6_splits(P, 25 * (C / wgrad6_cb(C))) * M * C * 25;
+  if (kind == 6) return (size_t)wgrad6_splits(P, 5 * (C / 64)) * M * C * 25;
   if (kind == 7)   // k9 x6: partials [ns][M][256] + the split im2col [3][P][256] (u16)
     return (size_t)wgrad6_splits(P, 2) * M * 256 + (size_t)P * 256 * 3 / 2;
   const int ntap = kind == 1 ? 1 : 25;
@@ -800,7 +1030,7 @@ int iclr17_wgrad_k5_x6(const uint16_t* G_split, const uint16_t* X_split, int B, 
   ICLR17_REQUIRE(G_split && X_split && workspace && dW, ICLR17_EINVAL, "wgrad_k5_x6: null pointer");
   const long P = (long)B * Ho * Wo;
   ICLR17_REQUIRE(M == C, ICLR17_EUNSUPPORTED, "wgrad_k5_x6: M=%d C=%d (square layers only)", M, C);
-  const int tiles = 25 * (C / wgrad6_cb(C));
+  const int tiles = 5 * (C / 64);   // (kernel row, 64-channel block)
   const int ns = wgrad6_splits(P, tiles);
   const long pg = P * M, pxs = (long)B * 4 * Ho * Wo * C;
   hipStream_t st = S(stream);
@@ -808,9 +1038,9 @@ int iclr17_wgrad_k5_x6(const uint16_t* G_split, const uint16_t* X_split, int B, 
   const unsigned short* g6 = (const unsigned short*)G_split;
   const unsigned short* x6 = (const unsigned short*)X_split;
   if (M == 192)
-    hipLaunchKernelGGL((wgrad_x6_kernel<192, 192, 2, 4, 5>), grid, dim3(512), 0, st, g6, pg, x6, pxs, B, Ho, Wo, 2 * Ho, 2 * Wo, C, ns, workspace);
+    hipLaunchKernelGGL((wgrad_x6_row_kernel<192>), grid, dim3(512), 0, st, g6, pg, x6, pxs, B, Ho, Wo, 2 * Ho, 2 * Wo, C, ns, workspace);
   else
-    hipLaunchKernelGGL((wgrad_x6_kernel<128, 128, 2, 4, 5>), grid, dim3(512), 0, st, g6, pg, x6, pxs, B, Ho, Wo, 2 * Ho, 2 * Wo, C, ns, workspace);
+    hipLaunchKernelGGL((wgrad_x6_row_kernel<128>), grid, dim3(512), 0, st, g6, pg, x6, pxs, B, Ho, Wo, 2 * Ho, 2 * Wo, C, ns, workspace);
   int rc = check_launch("wgrad_k5_x6");
   if (rc) return rc;
   const long n = (long)M * C * 25;

@@ -84,6 +84,7 @@ class Step:
         self.N = net.out_channel_N
         self.enc = net.Encoder.packed()
         self.dec = net.Decoder.packed()
+        self.d3x6 = net.Decoder.packed_x6()
         self.rate = net.bitEstimator.packed()
         gdns = (net.Encoder.gdn1, net.Encoder.gdn2, net.Decoder.igdn1, net.Decoder.igdn2)
         self.w1x6 = net.Encoder.packed_conv1_x6()
@@ -125,7 +126,7 @@ class Step:
             ev(4)
             hs, _, _ = kernels.deconv_igdn_x6(hs, d2, net.Decoder.deconv2.bias, *e4)
             ev(5)
-            clipped, _, _ = kernels.deconv3_x6(hs, d3, net.Decoder.deconv3.bias)
+            clipped, _, _ = kernels.deconv3_x6(hs, self.d3x6, net.Decoder.deconv3.bias)
         else:
             h = kernels.conv1_gdn(self.x, w1, net.Encoder.conv1.bias, g1[0], g1[1], N)
             ev(1)

@@ -200,7 +200,7 @@ def synthesis_forward_train(dec, y_nhwc: Tensor, x_ref: Optional[Tensor] = None,
                                              want_pre=True)
         s2s, s2, v2 = kernels.deconv_igdn_x6(s1s, d2, dec.deconv2.bias, *e2, want_f32=True,
                                              want_pre=True)
-        clipped, recon, sse = kernels.deconv3_x6(s2s, d3, dec.deconv3.bias, x_ref=x_ref,
+        clipped, recon, sse = kernels.deconv3_x6(s2s, dec.packed_x6(), dec.deconv3.bias, x_ref=x_ref,
                                                  want_recon=True, sse_unclipped=x_ref is not None)
         # the split forms of y and s1 are the x6 weight-gradient operands
         return clipped, recon, sse, {"y": y_nhwc, "v1": v1, "s1": s1, "v2": v2, "s2": s2,

@@ -1121,8 +1121,9 @@ constexpr int D3_PS = D3_BS + 2;                // patch side
 constexpr int D3_PPX = D3_PS * D3_PS;           // 324 patch pixels per plane
 constexpr int D3_NAI = (3 * D3_PPX + 15) / 16;  // 61 A wave-instructions per chunk
 constexpr int D3_SA = D3_NAI * 256;             // A stage floats (976 slots × 16)
-constexpr int D3_SB = 32 * 48;                  // B stage floats
-constexpr int D3_LDS = D3_SA + 2 * D3_SB;
+constexpr int D3_SB = 32 * 48;                  // fp32 B stage floats (the bf16 kernel's)
+constexpr int D3_SB6 = 3 * 32 * 48 / 2;         // x6 B stage floats: [3 planes][4 k8][48][8] u16
+constexpr int D3_LDS = D3_SA + 2 * D3_SB6;      // 80,896 B: two workgroups per CU
 
 // Column order of the in-loop-split path: logical column j (tile j / 16, lane j % 16) reads packed
 // column co·16 + ry·4 + rx, taking first the 12 columns with ry = 0, then the 9 with rx = 0 < ry,
@@ -1145,7 +1146,7 @@ __device__ __forceinline__ int d3_col(int j) {
 
 template <int CI>
 __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) {
-  constexpr int KCH = 32, NCH = CI / KCH, NSTEP = 9 * NCH;
+  constexpr int KCH = 32, NCH = CI / KCH;
   constexpr int MT = 4, NT = 3;
   constexpr int NPL = 3;                                  // input planes
   constexpr int NAI = (NPL * D3_PPX + 15) / 16;           // A wave-instructions per chunk
@@ -1191,20 +1192,27 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
       }
     }
   };
-  // B DMA: the stage [k-quad][48][4] holds logical column j (the d3_col order the fragment
-  // reads walk) at slot j, so a 16-lane group reads 16 consecutive 16-byte slots (conflict-free);
-  // each lane fetches the packed column d3_col(j) of its slot.
-  int bsrc[2];
+  // B DMA: the weights arrive pre-split (iclr17_split_packed of the ICLR17_W_DECONV9 packing:
+  // [3][9][CI/8][48][8] bf16), so no wave splits them in the loop. The stage [plane][k8][48][8]
+  // holds logical column j (the d3_col order the fragment reads walk) at slot j, so a 16-lane
+  // group reads 16 consecutive 16-byte slots (conflict-free); each lane fetches the packed
+  // column d3_col(j) of its slot. 9 wave-instructions per tap.
+  const unsigned short* __restrict__ w6 = (const unsigned short*)a.w;
+  constexpr long WPL = 9L * CI * 48;   // u16 per weight plane
+  int bsrc[3];
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int q = (wave + 4 * k) * 64 + lane, kq = q / 48, j = q - kq * 48;
-    bsrc[k] = (kq * 48 + d3_col(j)) * 4;
+  for (int k = 0; k < 3; ++k) {
+    const int q = (wave + 4 * k) * 64 + lane;
+    const int pl = q / 192, r = (q / 48) & 3, j = q % 48;
+    bsrc[k] = (int)(pl * WPL) + (r * 48 + d3_col(j)) * 8;
   }
   auto issue_b = [&](int s, int buf) {
     const int cc = s / 9, tap = s - cc * 9;
-    const float* __restrict__ ws = a.w + ((long)tap * CI + cc * KCH) * 48;
-    glds16(ws + bsrc[0], sB + buf * D3_SB + wave * 256);
-    if (wave < 2) glds16(ws + bsrc[1], sB + buf * D3_SB + (wave + 4) * 256);
+    const unsigned short* __restrict__ ws = w6 + ((long)tap * (CI / 8) + cc * 4) * 48 * 8;
+    float* sb = sB + buf * D3_SB6;
+    glds16((const float*)(ws + bsrc[0]), sb + wave * 256);
+    glds16((const float*)(ws + bsrc[1]), sb + (wave + 4) * 256);
+    if (wave == 0) glds16((const float*)(ws + bsrc[2]), sb + 8 * 256);
   };
 
   f4 acc[MT][NT];
@@ -1222,16 +1230,14 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
   auto compute = [&](int buf, int tap, auto ntt) {
     constexpr int NTT = decltype(ntt)::value;   // tiles this tap touches
     const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
-    const float* sb = sB + buf * D3_SB + 2 * g * 48 * 4;
+    const unsigned short* sb = (const unsigned short*)(sB + buf * D3_SB6) + g * 48 * 8;
     bf8 Bh[NTT], Bm[NTT], Bl[NTT];
 #pragma unroll
     for (int nt = 0; nt < NTT; ++nt) {
-      u4 bh, bm, bl;
       const int jc = nt * 16 + (lane & 15);
-      split8(*(const f4*)(sb + jc * 4), *(const f4*)(sb + 48 * 4 + jc * 4), bh, bm, bl);
-      Bh[nt] = __builtin_bit_cast(bf8, bh);
-      Bm[nt] = __builtin_bit_cast(bf8, bm);
-      Bl[nt] = __builtin_bit_cast(bf8, bl);
+      Bh[nt] = __builtin_bit_cast(bf8, *(const u4*)(sb + jc * 8));
+      Bm[nt] = __builtin_bit_cast(bf8, *(const u4*)(sb + 4 * 48 * 8 + jc * 8));
+      Bl[nt] = __builtin_bit_cast(bf8, *(const u4*)(sb + 8 * 48 * 8 + jc * 8));
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -1256,20 +1262,25 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
 
   issue_a(0);
   issue_b(0, 0);
-  for (int s = 0; s < NSTEP; ++s) {
-    __syncthreads();   // vmcnt(0) + barrier: A (at a chunk start) and B of step s landed
-    const int tap = s - (s / 9) * 9;
-    if (s + 1 < NSTEP && tap != 8) issue_b(s + 1, (s + 1) & 1);
-    if (tap < 3)
-      compute(s & 1, tap, std::integral_constant<int, 1>{});
-    else if (tap == 3 || tap == 6)
-      compute(s & 1, tap, std::integral_constant<int, 2>{});
-    else
-      compute(s & 1, tap, std::integral_constant<int, 3>{});
-    if (tap == 8 && s + 1 < NSTEP) {
-      __syncthreads();   // every wave is done with this chunk's patch
-      issue_a((s + 1) / 9);
-      issue_b(s + 1, (s + 1) & 1);
+  // taps unrolled inside the chunk loop: each tap's code is specialised (no joins between the
+  // three tile counts, whose register shuffles cost more VALU than the split itself)
+  for (int cc = 0; cc < NCH; ++cc) {
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int s = cc * 9 + tap;
+      __syncthreads();   // vmcnt(0) + barrier: A (at a chunk start) and B of step s landed
+      if (tap != 8) issue_b(s + 1, (s + 1) & 1);
+      if (tap < 3)
+        compute(s & 1, tap, std::integral_constant<int, 1>{});
+      else if (tap == 3 || tap == 6)
+        compute(s & 1, tap, std::integral_constant<int, 2>{});
+      else
+        compute(s & 1, tap, std::integral_constant<int, 3>{});
+      if (tap == 8 && cc + 1 < NCH) {
+        __syncthreads();   // every wave is done with this chunk's patch
+        issue_a(cc + 1);
+        issue_b(s + 1, (s + 1) & 1);
+      }
     }
   }
   __syncthreads();     // stage reads done before the epilogue reuses LDS
@@ -2350,13 +2361,14 @@ int iclr17_synthesis_deconv_igdn(const float* in, int B, int h, int w, int N,
                   : launch_deconv5<128>(in, B, h, w, w_packed, bias, beta_eff, gamma_packed, out, pre_out, S(stream));
 }
 
-static int launch_deconv3_halo(const uint16_t* in, int B, int H, int W, int N, const float* w_packed,
+// w: the fp32 ICLR17_W_DECONV9 packing (bf16 mode) or its iclr17_split_packed(9, N, 48) planes (x6)
+static int launch_deconv3_halo(const uint16_t* in, int B, int H, int W, int N, const void* w,
                                const float* bias, const float* x, float* clipped, float* recon,
                                double* sse_partial, int sse_unclipped, void* stream, bool bf) {
   const char* what = bf ? "deconv3_bf16" : "deconv3_x6";
   int rc = check_dims(B, H, W, N);
   if (rc) return rc;
-  ICLR17_REQUIRE(in && w_packed && bias && clipped, ICLR17_EINVAL, "%s: null pointer", what);
+  ICLR17_REQUIRE(in && w && bias && clipped, ICLR17_EINVAL, "%s: null pointer", what);
   ICLR17_REQUIRE(x == nullptr || sse_partial != nullptr, ICLR17_EINVAL,
                  "%s: sse_partial required with x", what);
   ICLR17_REQUIRE(!sse_unclipped || recon != nullptr, ICLR17_EINVAL,
@@ -2365,7 +2377,7 @@ static int launch_deconv3_halo(const uint16_t* in, int B, int H, int W, int N, c
   memset(&a, 0, sizeof(a));
   a.sse_unclipped = sse_unclipped;
   a.in_split = (const unsigned short*)in;
-  a.w = w_packed; a.bias = bias; a.out = clipped; a.recon = recon; a.xref = x;
+  a.w = (const float*)w; a.bias = bias; a.out = clipped; a.recon = recon; a.xref = x;
   a.partial = sse_partial;
   a.B = B; a.Hin = H / 4; a.Win = W / 4; a.Hout = H; a.Wout = W;
   a.gh = H / 4; a.gw = W / 4;
@@ -2388,10 +2400,10 @@ static int launch_deconv3_halo(const uint16_t* in, int B, int H, int W, int N, c
 }
 
 int iclr17_synthesis_deconv3_x6(const uint16_t* in_split, int B, int H, int W, int N,
-                                const float* w_packed, const float* bias, const float* x,
+                                const uint16_t* w_split, const float* bias, const float* x,
                                 float* clipped, float* recon, double* sse_partial,
                                 int sse_unclipped, void* stream) {
-  return launch_deconv3_halo(in_split, B, H, W, N, w_packed, bias, x, clipped, recon, sse_partial,
+  return launch_deconv3_halo(in_split, B, H, W, N, w_split, bias, x, clipped, recon, sse_partial,
                              sse_unclipped, stream, false);
 }
 

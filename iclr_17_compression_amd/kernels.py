@@ -487,13 +487,23 @@ def deconv3(h: Tensor, wp: Tensor, bias: Tensor, x_ref: Optional[Tensor] = None,
     return clipped, recon, partial
 
 
-def deconv3_x6(hs: Tensor, wp: Tensor, bias: Tensor, x_ref: Optional[Tensor] = None,
+def split_deconv3(wp: Tensor, N: int) -> Tensor:
+    """The ICLR17_W_DECONV9 packing of deconv3 split into the x6 weight planes
+    [3][9][N/8][48][8] that ``deconv3_x6`` reads (iclr17_split_packed, taps 9, K N, N 48)."""
+    return split_packed(wp, 9, N, 48)
+
+
+def deconv3_x6(hs: Tensor, w_split: Tensor, bias: Tensor, x_ref: Optional[Tensor] = None,
                want_recon: bool = False, sse_unclipped: bool = False):
-    """deconv3 on a split-form input [3,B,H/4,W/4,N] (the halo-tiled x6 kernel); the same
-    returns as ``deconv3``."""
+    """deconv3 on a split-form input [3,B,H/4,W/4,N] (the halo-tiled x6 kernel); w_split:
+    ``split_deconv3`` of the packed weights (Synthesis_net_17.packed_x6). The same returns as
+    ``deconv3``."""
     _check_split(hs, "activation")
     _, B, h4, w4, N = hs.shape
-    return _deconv3_halo("iclr17_synthesis_deconv3_x6", hs, B, h4, w4, N, wp, bias, x_ref,
+    if (not isinstance(w_split, Tensor) or w_split.dtype != torch.int16
+            or w_split.numel() != 3 * 9 * N * 48):
+        raise Iclr17Error("iclr17: deconv3_x6 takes the split weight planes (split_deconv3)")
+    return _deconv3_halo("iclr17_synthesis_deconv3_x6", hs, B, h4, w4, N, w_split, bias, x_ref,
                          want_recon, sse_unclipped)
 
 

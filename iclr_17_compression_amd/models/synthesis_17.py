@@ -47,6 +47,12 @@ class Synthesis_net_17(nn.Module):
                             lambda: kernels.pack_weight(_lib.ICLR17_W_DECONV9, self.deconv3.weight, N), f)
         return d1, d2, d3, self.igdn1.effective_params(force), self.igdn2.effective_params(force)
 
+    def packed_x6(self, force: bool = False):
+        """deconv3's packed weights split into the x6 planes the halo kernel stages, cached."""
+        d3 = self.packed(force)[2]
+        return self._pack.get("d3x6", (self.deconv3.weight,),
+                              lambda: kernels.split_deconv3(d3, self.out_channel_N), force)
+
     def packed_bf16(self, force: bool = False):
         """deconv1 / deconv2 in the bf16 engine's step layout (4 stride phases), cached."""
         N, f = self.out_channel_N, force
@@ -94,7 +100,7 @@ class Synthesis_net_17(nn.Module):
             q1, q2 = self.igdn1.effective_params_x6(), self.igdn2.effective_params_x6()
             hs, _, _ = kernels.deconv_igdn_x6(y_split, d1, self.deconv1.bias, *q1)
             hs, _, _ = kernels.deconv_igdn_x6(hs, d2, self.deconv2.bias, *q2)
-            return kernels.deconv3_x6(hs, d3, self.deconv3.bias, x_ref=x_ref,
+            return kernels.deconv3_x6(hs, self.packed_x6(), self.deconv3.bias, x_ref=x_ref,
                                       want_recon=want_recon)
         else:
             h = kernels.deconv_igdn(y_nhwc, d1, self.deconv1.bias, g1[0], g1[1])

@@ -194,10 +194,10 @@ int iclr17_synthesis_deconv_igdn_x6(const uint16_t* in_split, int B, int h, int 
                                     const uint16_t* gamma_split, float* out, uint16_t* out_split,
                                     float* pre_out, void* stream);
 /* iclr17_synthesis_deconv3 on a split-form input (the same outputs and sse_partial layout:
- * iclr17_output_partials_per_image(H, W) doubles per image); the packed fp32 weights are split
- * in the loop. */
+ * iclr17_output_partials_per_image(H, W) doubles per image). w_split: the ICLR17_W_DECONV9
+ * packing split by iclr17_split_packed(taps = 9, K = N, N = 48) — [3][9][N/8][48][8]. */
 int iclr17_synthesis_deconv3_x6(const uint16_t* in_split, int B, int H, int W, int N,
-                                const float* w_packed, const float* bias, const float* x,
+                                const uint16_t* w_split, const float* bias, const float* x,
                                 float* clipped, float* recon, double* sse_partial,
                                 int sse_unclipped, void* stream);
 

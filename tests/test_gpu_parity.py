@@ -148,7 +148,7 @@ def test_deconv3_x6(device, N, shape):
     B, H, W = shape
     net, sd = net_for(N, 1, device), sd_for(N, 1)
     F = torch.nn.functional
-    d3 = net.Decoder.packed()[2]
+    d3, d3x6 = net.Decoder.packed()[2], net.Decoder.packed_x6()
     s2 = torch.from_numpy(synth.normal_like(21, (B, N, H // 4, W // 4), 0.6))
     x = image(12, B, H, W)
     with torch.no_grad():
@@ -157,7 +157,7 @@ def test_deconv3_x6(device, N, shape):
         hs = kernels.split_planes(nhwc(s2).contiguous().to(device))
         xd = x.to(device)
         for unclipped in (False, True):
-            clipped, recon, part = kernels.deconv3_x6(hs, d3, net.Decoder.deconv3.bias, x_ref=xd,
+            clipped, recon, part = kernels.deconv3_x6(hs, d3x6, net.Decoder.deconv3.bias, x_ref=xd,
                                                       want_recon=True, sse_unclipped=unclipped)
             assert rel_err(recon, r_out) < REL
             assert rel_err(clipped, r_out.clamp(0, 1)) < REL
@@ -170,7 +170,7 @@ def test_deconv3_x6(device, N, shape):
                                            net.Decoder.deconv3.bias, x_ref=xd, want_recon=True,
                                            sse_unclipped=unclipped)
             assert rel_err(part, part32) < 1e-4
-        c2, r2, p2 = kernels.deconv3_x6(hs, d3, net.Decoder.deconv3.bias)
+        c2, r2, p2 = kernels.deconv3_x6(hs, d3x6, net.Decoder.deconv3.bias)
         assert r2 is None and p2 is None and torch.equal(c2, clipped)
 
 

@@ -30,7 +30,7 @@ LAYER_KERNELS = {
         "conv3_quant_rate": (r"engine_kernel<192, 192, 96, 2, 2, 2, false>", None),
         "deconv1_igdn1": (r"engine_kernel<192, 192, 192, 1, 4, 1, false>", 0),
         "deconv2_igdn2": (r"engine_kernel<192, 192, 192, 1, 4, 1, false>", 1),
-        "deconv3_clamp": (r"deconv3_x6_kernel<192, false>", None),
+        "deconv3_clamp": (r"engine_kernel<192, 48, 48, 4, 1, 3, false>", None),
     },
     "x6": {
         "conv1_gdn1": (r"conv1_x6_kernel<192, 0>", None),
@@ -38,7 +38,7 @@ LAYER_KERNELS = {
         "conv3_quant_rate": (r"engine_kernel<192, 192, 96, 2, 2, 2, true>", None),
         "deconv1_igdn1": (r"engine_kernel<192, 192, 192, 1, 4, 1, true>", 0),
         "deconv2_igdn2": (r"engine_kernel<192, 192, 192, 1, 4, 1, true>", 1),
-        "deconv3_clamp": (r"deconv3_x6_kernel<192, false>", None),
+        "deconv3_clamp": (r"deconv3_x6_kernel<192>", None),
     },
     "bf16": {
         "conv1_gdn1": (r"conv1_bf16_kernel<192>", None),
@@ -46,7 +46,7 @@ LAYER_KERNELS = {
         "conv3_quant_rate": (r"k5_bf16_kernel<0, 8, 96, 192, 192, 2>", None),
         "deconv1_igdn1": (r"k5_bf16_kernel<1, 8, 192, 192, 192, 1>", None),
         "deconv2_igdn2": (r"k5_bf16_kernel<1, 16, 192, 192, 192, 1>", None),
-        "deconv3_clamp": (r"deconv3_x6_kernel<192, true>", None),
+        "deconv3_clamp": (r"deconv3_bf16_kernel<192>", None),
     },
 }
 

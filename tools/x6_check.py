@@ -88,7 +88,7 @@ def numerics():
     r3 = F.conv_transpose2d(s2[:nb].permute(0, 3, 1, 2).double(), d.deconv3.weight.double(),
                             d.deconv3.bias.double(), 4, 4, 3)
     _, f32, _ = kernels.deconv3(s2[:nb].contiguous(), d3, d.deconv3.bias, want_recon=True)
-    _, x6r, _ = kernels.deconv3_x6(kernels.split_planes(s2[:nb].contiguous()), d3, d.deconv3.bias,
+    _, x6r, _ = kernels.deconv3_x6(kernels.split_planes(s2[:nb].contiguous()), d.packed_x6(), d.deconv3.bias,
                                    want_recon=True)
     print("deconv3 fp32:", err(f32, r3))
     print("deconv3 x6  :", err(x6r, r3))
@@ -111,7 +111,7 @@ def timings():
         "deconv2 x6": (timeit(lambda: kernels.deconv_igdn_x6(s1s, d2, net.Decoder.deconv2.bias, *q2x,
                                                              want_split=False, want_f32=True)), fld),
         "deconv3 fp32": (timeit(lambda: kernels.deconv3(s2, d3, net.Decoder.deconv3.bias)), fl3),
-        "deconv3 x6": (timeit(lambda: kernels.deconv3_x6(s2s, d3, net.Decoder.deconv3.bias)), fl3),
+        "deconv3 x6": (timeit(lambda: kernels.deconv3_x6(s2s, net.Decoder.packed_x6(), net.Decoder.deconv3.bias)), fl3),
     }
     print(TAG, " ".join(f"{k}={v[0]:.3f}ms({v[1] / v[0] / 1e9:.1f}TF)" for k, v in t.items()), flush=True)
 

@@ -737,35 +737,36 @@ __global__ void __launch_bounds__(512) wgrad_x6_row_kernel(const unsigned short*
 // k9 s4 p4 weight gradient in x6 as a 1×1 one: the 243 (c, kh, kw) window values of every
 // output pixel, split, as the X operand [3][P][256] (k = c·81 + kh·9 + kw, the PyTorch
 // [M][3][9][9] order; k ≥ 243 zero) — im2col of a 3-channel NCHW image, 8 k per thread.
-__global__ void im2col9_split_kernel(const float* __restrict__ X, int B, int Ho, int Wo,
-                                     unsigned short* __restrict__ planes) {
-  const long P = (long)B * Ho * Wo;
-  const long n = P * 32;
+__global__ void __launch_bounds__(256) im2col9_split_kernel(const float* __restrict__ X, int B,
+                                                            int Ho, int Wo,
+                                                            unsigned short* __restrict__ planes) {
+  // grid: (⌈32·Wo / 256⌉, B·Ho) — one output row per blockIdx.y, 32 k-groups per pixel
+  const int P = B * Ho * Wo;
+  const int row = blockIdx.y, oy = row % Ho, b = row / Ho;   // workgroup-uniform
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int ox = t >> 5, kg = t & 31;
+  if (ox >= Wo) return;
   const int H = Ho * 4, W = Wo * 4;
-  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (long)gridDim.x * blockDim.x) {
-    const long p = t >> 5;
-    const int kg = (int)(t & 31);
-    const int ox = (int)(p % Wo), oy = (int)((p / Wo) % Ho), b = (int)(p / ((long)Wo * Ho));
-    float v[8];
+  const float* __restrict__ xb = X + (long)b * 3 * H * W;
+  float v[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int k = kg * 8 + e;
-      float x = 0.f;
-      if (k < 243) {
-        const int c = k / 81, kh = (k % 81) / 9, kw = k % 9;
-        const int iy = oy * 4 - 4 + kh, ix = ox * 4 - 4 + kw;
-        if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
-          x = X[(((long)b * 3 + c) * H + iy) * W + ix];
-      }
-      v[e] = x;
+  for (int e = 0; e < 8; ++e) {
+    const int k = kg * 8 + e;
+    float x = 0.f;
+    if (k < 243) {
+      const int c = k / 81, kh = (k % 81) / 9, kw = k % 9;
+      const int iy = oy * 4 - 4 + kh, ix = ox * 4 - 4 + kw;
+      if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) x = xb[(c * H + iy) * W + ix];
     }
-    u4 hi, mi, lo;
-    split8(f4{v[0], v[1], v[2], v[3]}, f4{v[4], v[5], v[6], v[7]}, hi, mi, lo);
-    unsigned short* d = planes + p * 256 + kg * 8;
-    *(u4*)d = hi;
-    *(u4*)(d + P * 256) = mi;
-    *(u4*)(d + 2 * P * 256) = lo;
+    v[e] = x;
   }
+  u4 hi, mi, lo;
+  split8(f4{v[0], v[1], v[2], v[3]}, f4{v[4], v[5], v[6], v[7]}, hi, mi, lo);
+  const int p = row * Wo + ox;
+  unsigned short* d = planes + (long)p * 256 + kg * 8;
+  *(u4*)d = hi;
+  *(u4*)(d + (long)P * 256) = mi;
+  *(u4*)(d + 2L * P * 256) = lo;
 }
 
 // Σ over splits of part[s][m][256] → dW[m][243] (fixed split order, 8 loads in flight).
@@ -1049,7 +1050,8 @@ int iclr17_wgrad_k5_x6(const uint16_t* G_split, const uint16_t* X_split, int B, 
 }
 int iclr17_wgrad_k9_x6(const uint16_t* G_split, const float* X, int B, int Ho, int Wo, int M,
                        float* workspace, float* dW, void* stream) {
-  ICLR17_REQUIRE(B > 0 && Ho > 0 && Wo > 0, ICLR17_EINVAL, "wgrad_k9_x6: bad shape");
+  ICLR17_REQUIRE(B > 0 && Ho > 0 && Wo > 0 && (long)B * Ho <= 65535, ICLR17_EINVAL,
+                 "wgrad_k9_x6: bad shape");
   ICLR17_REQUIRE(M == 128 || M == 192, ICLR17_EUNSUPPORTED, "wgrad_k9_x6: M=%d unsupported", M);
   ICLR17_REQUIRE(G_split && X && workspace && dW, ICLR17_EINVAL, "wgrad_k9_x6: null pointer");
   const long P = (long)B * Ho * Wo;
@@ -1058,9 +1060,8 @@ int iclr17_wgrad_k9_x6(const uint16_t* G_split, const float* X, int B, int Ho, i
   float* part = workspace;
   unsigned short* cols = (unsigned short*)(workspace + (long)ns * M * 256);
   hipStream_t st = S(stream);
-  const long nt = P * 32;
-  hipLaunchKernelGGL(im2col9_split_kernel, dim3((unsigned)((nt + 255) / 256 < 65536 ? (nt + 255) / 256 : 65536)),
-                     dim3(256), 0, st, X, B, Ho, Wo, cols);
+  hipLaunchKernelGGL(im2col9_split_kernel, dim3((32 * Wo + 255) / 256, B * Ho), dim3(256), 0, st, X,
+                     B, Ho, Wo, cols);
   int rc = check_launch("wgrad_k9_x6_im2col");
   if (rc) return rc;
   dim3 grid((tiles * ns + 7) / 8 * 8);

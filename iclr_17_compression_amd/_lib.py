@@ -98,6 +98,7 @@ SIGNATURES = {
     "iclr17_bwd_conv_gdn": (_I, [_P, _P, _I, _I, _I, _I] + [_P] * 13),
     "iclr17_bwd_tiles": (_I, [_I, _I, _I]),
     "iclr17_sum_rows": (_I, [_P, _I, _I, _P, _P, _P]),
+    "iclr17_sum_rows2": (_I, [_P, _P, _I, _I, _P, _P, _P, _P]),
     "iclr17_sum_rows_workspace_size": (_SZ, [_I]),
     "iclr17_wgrad_workspace_size": (_SZ, [_I, _I, _I, _I, _I, _I]),
     "iclr17_wgrad_k5": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),

@@ -885,6 +885,31 @@ __global__ void __launch_bounds__(256) wgrad_k9_kernel(const float* __restrict__
       }
 }
 
+// Up to two independent [T][C] matrices per launch pair (blockIdx.z / blockIdx.y picks one).
+struct Rows2 {
+  const float* part[2];
+  float* ws[2];
+  float* out[2];
+};
+// sum_splits_kernel over the workspace of matrix blockIdx.y of a Rows2 (nsplit rows of n)
+__global__ void sum_splits2_kernel(const Rows2 r, int nsplit, long n) {
+  const float* __restrict__ part = r.ws[blockIdx.y];
+  float* __restrict__ out = r.out[blockIdx.y];
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    int k = 0;
+    for (; k + 8 <= nsplit; k += 8) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = part[(long)(k + j) * n + i];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[j];
+    }
+    for (; k < nsplit; ++k) s += part[(long)k * n + i];
+    out[i] = s;
+  }
+}
+
 // out[i] = Σ_s part[s][i], fixed order.
 __global__ void sum_splits_kernel(const float* __restrict__ part, int nsplit, long n,
                                   float* __restrict__ out) {
@@ -909,8 +934,9 @@ __global__ void sum_splits_kernel(const float* __restrict__ part, int nsplit, lo
 // (one workgroup per 64 columns walked thousands of rows serially).
 constexpr int SUM_ROWS_SPLITS = 64;
 
-__global__ void sum_rows_kernel(const float* __restrict__ part, int T, int C, int per,
-                                float* __restrict__ ws) {
+__global__ void sum_rows2_kernel(const Rows2 r, int T, int C, int per) {
+  const float* __restrict__ part = r.part[blockIdx.z];
+  float* __restrict__ ws = r.ws[blockIdx.z];
   __shared__ float red[4][64];
   const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -1145,18 +1171,33 @@ int iclr17_gdn_wgrad_x6(const float* dn, const float* u, long P, int C, float* w
 size_t iclr17_sum_rows_workspace_size(int C) { return (size_t)SUM_ROWS_SPLITS * C; }
 
 // out[c] = Σ_t part[t][c] (fixed order). workspace: iclr17_sum_rows_workspace_size(C) floats.
+static int sum_rows_n(const Rows2& r, int nm, int T, int C, void* stream) {
+  const int per = (T + SUM_ROWS_SPLITS - 1) / SUM_ROWS_SPLITS;
+  const int ns = (T + per - 1) / per;
+  hipLaunchKernelGGL(sum_rows2_kernel, dim3((C + 63) / 64, ns, nm), dim3(256), 0, S(stream), r, T,
+                     C, per);
+  int rc = check_launch("sum_rows");
+  if (rc) return rc;
+  hipLaunchKernelGGL(sum_splits2_kernel, dim3((C + 255) / 256, nm), dim3(256), 0, S(stream), r, ns,
+                     (long)C);
+  return check_launch("sum_rows_splits");
+}
+
 int iclr17_sum_rows(const float* part, int T, int C, float* workspace, float* out, void* stream) {
   ICLR17_REQUIRE(part && workspace && out && T > 0 && C > 0, ICLR17_EINVAL,
                  "sum_rows: bad arguments");
-  const int per = (T + SUM_ROWS_SPLITS - 1) / SUM_ROWS_SPLITS;
-  const int ns = (T + per - 1) / per;
-  hipLaunchKernelGGL(sum_rows_kernel, dim3((C + 63) / 64, ns), dim3(256), 0, S(stream), part, T,
-                     C, per, workspace);
-  int rc = check_launch("sum_rows");
-  if (rc) return rc;
-  hipLaunchKernelGGL(sum_splits_kernel, dim3((C + 255) / 256), dim3(256), 0, S(stream), workspace,
-                     ns, (long)C, out);
-  return check_launch("sum_rows_splits");
+  const Rows2 r{{part, nullptr}, {workspace, nullptr}, {out, nullptr}};
+  return sum_rows_n(r, 1, T, C, stream);
+}
+
+// iclr17_sum_rows of two [T][C] matrices in one launch pair; workspace: twice
+// iclr17_sum_rows_workspace_size(C) floats.
+int iclr17_sum_rows2(const float* part_a, const float* part_b, int T, int C, float* workspace,
+                     float* out_a, float* out_b, void* stream) {
+  ICLR17_REQUIRE(part_a && part_b && workspace && out_a && out_b && T > 0 && C > 0, ICLR17_EINVAL,
+                 "sum_rows2: bad arguments");
+  const Rows2 r{{part_a, part_b}, {workspace, workspace + (long)SUM_ROWS_SPLITS * C}, {out_a, out_b}};
+  return sum_rows_n(r, 2, T, C, stream);
 }
 
 // Bias gradient of a layer whose output gradient is NHWC [P][C]: db[c] = Σ_p G[p][c].

@@ -908,6 +908,19 @@ def sum_rows(part: Tensor) -> Tensor:
     return out
 
 
+def sum_rows2(a: Tensor, b: Tensor):
+    """``sum_rows`` of two [T, C] partial buffers of one shape in one launch pair."""
+    T, C = a.shape
+    if tuple(b.shape) != (T, C):
+        raise Iclr17Error("iclr17: sum_rows2 needs two partial buffers of one shape")
+    oa = torch.empty(C, device=a.device, dtype=torch.float32)
+    ob = torch.empty(C, device=a.device, dtype=torch.float32)
+    ws = torch.empty(2 * query("iclr17_sum_rows_workspace_size", C), device=a.device,
+                     dtype=torch.float32)
+    call("iclr17_sum_rows2", _p(a), _p(b), T, C, _p(ws), _p(oa), _p(ob), _stream(a))
+    return oa, ob
+
+
 def _split_like(t: Tensor) -> Tensor:
     return torch.empty((3,) + tuple(t.shape), device=t.device, dtype=torch.int16)
 
@@ -929,7 +942,7 @@ def bwd_deconv3_igdn(g_recon: Tensor, wp_conv1form: Optional[Tensor], v_saved: T
          _p(w_split), _p(v_saved), _p(beta_eff), _p(gp), _p(gpt), _p(g6), _p(g6t), _p(g_v),
          _p(sp), _p(dn),
          _p(cs_g), _p(cs_d), _stream(g_recon))
-    out = (g_v, dn, sum_rows(cs_g), sum_rows(cs_d))
+    out = (g_v, dn, *sum_rows2(cs_g, cs_d))
     return out + (sp,) if want_split else out
 
 
@@ -949,7 +962,7 @@ def bwd_deconv_igdn(g_v: Optional[Tensor], wp_conv5form: Tensor, v_prev: Tensor,
     call("iclr17_bwd_deconv_igdn", _p(gin), _p(g_split), B, h, w, N, _p(wp_conv5form), _p(v_prev),
          _p(beta_eff), _p(gp), _p(gpt), _p(g6), _p(g6t), _p(g_prev), _p(sp), _p(dn), _p(cs_g), _p(cs_d),
          _stream(v_prev))
-    out = (g_prev, dn, sum_rows(cs_g), sum_rows(cs_d))
+    out = (g_prev, dn, *sum_rows2(cs_g, cs_d))
     return out + (sp,) if want_split else out
 
 
@@ -992,7 +1005,7 @@ def bwd_conv_gdn(g_u: Optional[Tensor], wp_deconv5form: Tensor, u_prev: Tensor, 
     call("iclr17_bwd_conv_gdn", _p(gin), _p(g_split), B, h, w, N, _p(wp_deconv5form), _p(u_prev),
          _p(beta_eff), _p(gp), _p(gpt), _p(g6), _p(g6t), _p(g_prev), _p(sp), _p(dn), _p(cs_g), _p(cs_d),
          _stream(u_prev))
-    out = (g_prev, dn, sum_rows(cs_g), sum_rows(cs_d))
+    out = (g_prev, dn, *sum_rows2(cs_g, cs_d))
     return out + (sp,) if want_split else out
 
 

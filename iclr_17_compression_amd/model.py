@@ -249,6 +249,7 @@ class ImageCompressor(nn.Module):
             self.bitEstimator.packed()
             if x6:
                 self.Encoder.packed_conv1_x6()
+                self.Decoder.packed_x6()
                 for g in gdns:
                     g.effective_params_x6()
             if backward:

@@ -366,6 +366,10 @@ int iclr17_bwd_conv_gdn(const float* g_u, const uint16_t* g_u_split, int B, int 
  * gradient and Σ dn is ∂β_eff. kind 0 (bwd_deconv3_igdn with (H/4, W/4), bwd_deconv_igdn with
  * (h, w)), kind 1 (bwd_conv_gdn with (h, w)). Reduce them with iclr17_sum_rows. */
 int iclr17_bwd_tiles(int kind, int h, int w);
+/* iclr17_sum_rows of two [T][C] matrices in one launch pair (each bitwise as iclr17_sum_rows);
+ * workspace: 2 · iclr17_sum_rows_workspace_size(C) floats. */
+int iclr17_sum_rows2(const float* part_a, const float* part_b, int T, int C, float* workspace,
+                     float* out_a, float* out_b, void* stream);
 int iclr17_sum_rows(const float* part, int T, int C, float* workspace, float* out, void* stream);
 size_t iclr17_sum_rows_workspace_size(int C);   /* floats */
 /* Weight gradients in PyTorch layout [m][c][kh][kw] (split-K, fixed-order reduction):

@@ -737,36 +737,43 @@ __global__ void __launch_bounds__(512) wgrad_x6_row_kernel(const unsigned short*
 // k9 s4 p4 weight gradient in x6 as a 1×1 one: the 243 (c, kh, kw) window values of every
 // output pixel, split, as the X operand [3][P][256] (k = c·81 + kh·9 + kw, the PyTorch
 // [M][3][9][9] order; k ≥ 243 zero) — im2col of a 3-channel NCHW image, 8 k per thread.
+constexpr int I9_OX = 64, I9_COLS = 4 * I9_OX + 8;   // output pixels / window columns per block
 __global__ void __launch_bounds__(256) im2col9_split_kernel(const float* __restrict__ X, int B,
                                                             int Ho, int Wo,
                                                             unsigned short* __restrict__ planes) {
-  // grid: (⌈32·Wo / 256⌉, B·Ho) — one output row per blockIdx.y, 32 k-groups per pixel
+  // grid: (⌈Wo / 64⌉, B·Ho). The block stages the 9 input rows × 264 columns × 3 channels its 64
+  // output pixels read (coalesced, zeros outside the image), then gathers the windows from LDS.
+  __shared__ float win[3][9][I9_COLS];
   const int P = B * Ho * Wo;
   const int row = blockIdx.y, oy = row % Ho, b = row / Ho;   // workgroup-uniform
-  const int t = blockIdx.x * 256 + threadIdx.x;
-  const int ox = t >> 5, kg = t & 31;
-  if (ox >= Wo) return;
+  const int ox0 = blockIdx.x * I9_OX;
   const int H = Ho * 4, W = Wo * 4;
   const float* __restrict__ xb = X + (long)b * 3 * H * W;
-  float v[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int k = kg * 8 + e;
-    float x = 0.f;
-    if (k < 243) {
-      const int c = k / 81, kh = (k % 81) / 9, kw = k % 9;
-      const int iy = oy * 4 - 4 + kh, ix = ox * 4 - 4 + kw;
-      if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) x = xb[(c * H + iy) * W + ix];
-    }
-    v[e] = x;
+  for (int i = threadIdx.x; i < 3 * 9 * I9_COLS; i += 256) {
+    const int c = i / (9 * I9_COLS), r = (i / I9_COLS) % 9, col = i % I9_COLS;
+    const int iy = oy * 4 - 4 + r, ix = ox0 * 4 - 4 + col;
+    win[c][r][col] = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W
+                         ? xb[((long)c * H + iy) * W + ix] : 0.f;
   }
-  u4 hi, mi, lo;
-  split8(f4{v[0], v[1], v[2], v[3]}, f4{v[4], v[5], v[6], v[7]}, hi, mi, lo);
-  const int p = row * Wo + ox;
-  unsigned short* d = planes + (long)p * 256 + kg * 8;
-  *(u4*)d = hi;
-  *(u4*)(d + (long)P * 256) = mi;
-  *(u4*)(d + 2L * P * 256) = lo;
+  __syncthreads();
+  const int nox = Wo - ox0 < I9_OX ? Wo - ox0 : I9_OX;
+  for (int t = threadIdx.x; t < nox * 32; t += 256) {
+    const int ox = t >> 5, kg = t & 31;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = kg * 8 + e;
+      const int c = k / 81, kh = (k % 81) / 9, kw = k % 9;
+      v[e] = k < 243 ? win[c][kh][ox * 4 + kw] : 0.f;
+    }
+    u4 hi, mi, lo;
+    split8(f4{v[0], v[1], v[2], v[3]}, f4{v[4], v[5], v[6], v[7]}, hi, mi, lo);
+    const int p = row * Wo + ox0 + ox;
+    unsigned short* d = planes + (long)p * 256 + kg * 8;
+    *(u4*)d = hi;
+    *(u4*)(d + (long)P * 256) = mi;
+    *(u4*)(d + 2L * P * 256) = lo;
+  }
 }
 
 // Σ over splits of part[s][m][256] → dW[m][243] (fixed split order, 8 loads in flight).
@@ -908,6 +915,33 @@ __global__ void sum_splits2_kernel(const Rows2 r, int nsplit, long n) {
     for (; k < nsplit; ++k) s += part[(long)k * n + i];
     out[i] = s;
   }
+}
+
+// Σ over many splits (≥ 64) of few elements: 4 lanes per element each add a quarter of the splits
+// in order, then the quarters are added in order ((q0 + q1) + q2) + q3 — a fixed tree, so the
+// result is reproducible — on 4× the workgroups of sum_splits_kernel.
+__global__ void __launch_bounds__(256) sum_splits4_kernel(const float* __restrict__ part,
+                                                          int nsplit, long n,
+                                                          float* __restrict__ out) {
+  __shared__ float red[4][64];
+  const int el = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const long i = (long)blockIdx.x * 64 + el;
+  const int q = (nsplit + 3) / 4, k0 = g * q, k1 = k0 + q < nsplit ? k0 + q : nsplit;
+  float s = 0.f;
+  if (i < n) {
+    int k = k0;
+    for (; k + 8 <= k1; k += 8) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = part[(long)(k + j) * n + i];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[j];
+    }
+    for (; k < k1; ++k) s += part[(long)k * n + i];
+  }
+  red[g][el] = s;
+  __syncthreads();
+  if (g == 0 && i < n) out[i] = ((red[0][el] + red[1][el]) + red[2][el]) + red[3][el];
 }
 
 // out[i] = Σ_s part[s][i], fixed order.
@@ -1086,8 +1120,8 @@ int iclr17_wgrad_k9_x6(const uint16_t* G_split, const float* X, int B, int Ho, i
   float* part = workspace;
   unsigned short* cols = (unsigned short*)(workspace + (long)ns * M * 256);
   hipStream_t st = S(stream);
-  hipLaunchKernelGGL(im2col9_split_kernel, dim3((32 * Wo + 255) / 256, B * Ho), dim3(256), 0, st, X,
-                     B, Ho, Wo, cols);
+  hipLaunchKernelGGL(im2col9_split_kernel, dim3((Wo + I9_OX - 1) / I9_OX, B * Ho), dim3(256), 0, st,
+                     X, B, Ho, Wo, cols);
   int rc = check_launch("wgrad_k9_x6_im2col");
   if (rc) return rc;
   dim3 grid((tiles * ns + 7) / 8 * 8);
@@ -1164,7 +1198,7 @@ int iclr17_gdn_wgrad_x6(const float* dn, const float* u, long P, int C, float* w
   int rc = check_launch("gdn_wgrad_x6");
   if (rc) return rc;
   const long n = (long)C * C;
-  hipLaunchKernelGGL(sum_splits_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, workspace, ns, n, dgamma_eff);
+  hipLaunchKernelGGL(sum_splits4_kernel, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, workspace, ns, n, dgamma_eff);
   return check_launch("gdn_wgrad_x6_sum");
 }
 

@@ -131,15 +131,15 @@ __global__ void __launch_bounds__(256) wgrad_k5_kernel(const float* __restrict__
     }
 }
 
-// The same weight gradient in the bf16x6 scheme, from split-form operands (three bf16 planes, the
-// x6 activation format: G = ∂u or a synthesis activation, X = a layer input or ∂v). GEMM as above
-// but on v_mfma_f32_16x16x32_bf16 with K = 32 pixels per step: a workgroup owns one tap, MB rows
-// of M and 64 columns of C; 2×2 waves of (MB/2) × 32. Both tiles arrive by LDS-DMA as
-// [pixel][channel] bf16 rows (per plane), and the k-strided MFMA operands (8 consecutive pixels of
-// one channel) come out of ds_read_b64_tr_b16: a 16-lane group reads 4 pixel rows × 16 channels and
-// lane i receives channel i of the 4 rows — two reads make the 8-deep k-group. Six part products
-// (lo·hi, hi·lo, mid·mid, mid·hi, hi·mid, hi·hi) per 16×16 tile, fp32 accumulation. Partials land
-// in the same [split][m][c][tap] layout as wgrad_k5_kernel.
+// A weight gradient in the bf16x6 scheme as a 1×1 contraction over pixels, from split-form
+// operands (three bf16 planes): dW[m][c] = Σ_p G[p][m]·X[p][c] with G [P][M] and X [P][C] both
+// [pixel][channel] rows — the k9 weight gradients, X being the split im2col of the window.
+// v_mfma_f32_16x16x32_bf16 with K = 32 pixels per step: a workgroup owns all M rows and a CB-column
+// tile of C on 2×4 waves. Both tiles arrive by LDS-DMA as [pixel][channel] bf16 rows (per plane),
+// and the k-strided MFMA operands (8 consecutive pixels of one channel) come out of
+// ds_read_b64_tr_b16: a 16-lane group reads 4 pixel rows × 16 channels and lane i receives
+// channel i of the 4 rows — two reads make the 8-deep k-group. Six part products (lo·hi, hi·lo,
+// mid·mid, mid·hi, hi·mid, hi·hi) per 16×16 tile, fp32 accumulation; partials [split][m][c].
 typedef short s4v __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint2 tr16(const unsigned short* lds) {
@@ -160,13 +160,20 @@ __device__ __forceinline__ void lgkm_wait(u4& v) {
   asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v));
 }
 
-template <int M, int CB, int WM, int WN, int KS>
-__global__ void __launch_bounds__(512) wgrad_x6_kernel(const unsigned short* __restrict__ G6,
-                                                          long pg, const unsigned short* __restrict__ X6,
-                                                          long pxs, int B, int Ho, int Wo, int Hi,
-                                                          int Wi, int C, int nsplit,
-                                                          float* __restrict__ part) {
-  constexpr int NW = WM * WN;                        // 8 waves
+// LDS images are XOR-swizzled by 16-byte piece: piece k of pixel row r sits at k ^ swz6(r). A
+// transposed read's 32-lane half touches rows {q, 8 + q} (+4), two pieces each; swz6 gives them
+// disjoint bank windows (384-byte rows: the row parity already splits the 64 banks in two).
+__device__ __forceinline__ int swz6(int r, int row_elems) {
+  return row_elems == 192 ? 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1))
+                          : 2 * ((r & 3) | (((r >> 3) & 1) << 2));
+}
+
+template <int M, int CB>
+__global__ void __launch_bounds__(512) wgrad_x6_1x1_kernel(const unsigned short* __restrict__ G6,
+                                                              long pg, const unsigned short* __restrict__ X6,
+                                                              long pxs, long P, int C, int nsplit,
+                                                              float* __restrict__ part) {
+  constexpr int WM = 2, WN = 4, NW = WM * WN;        // 8 waves
   constexpr int MT = M / WM / 16, NT = CB / WN / 16; // 16×16 tiles per wave
   constexpr int GPL = KP * M, XPL = KP * CB;         // u16 per plane image
   constexpr int STAGE = 3 * GPL + 3 * XPL;           // u16 per stage
@@ -174,9 +181,7 @@ __global__ void __launch_bounds__(512) wgrad_x6_kernel(const unsigned short* __r
   constexpr int NGI = KP * GPR / 64, NXI = KP * XPR / 64;   // DMA wave-instructions per plane
   constexpr int NI = 3 * NGI + 3 * NXI;
   constexpr int NI_W = (NI + NW - 1) / NW;
-  constexpr int TAPS = KS * KS, STRIDE = KS == 5 ? 2 : 1, PAD = KS / 2;
-  static_assert(KS == 5 || KS == 1, "k5 s2 p2, or 1×1");
-  static_assert(NW == 8 && MT * WM * 16 == M && NT * WN * 16 == CB, "tile shape");
+  static_assert(MT * WM * 16 == M && NT * WN * 16 == CB, "tile shape");
   static_assert(KP * GPR % 64 == 0 && KP * XPR % 64 == 0, "whole DMA instructions");
   static_assert((M == 192 || M == 128) && (CB == 192 || CB == 128), "384- or 256-byte rows");
   __shared__ __attribute__((aligned(16))) unsigned short smem[2 * STAGE];
@@ -184,59 +189,30 @@ __global__ void __launch_bounds__(512) wgrad_x6_kernel(const unsigned short* __r
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   // XCD-aware order: the hardware deals workgroup ids round-robin to the 8 XCDs (id % 8), so
-  // logical workgroup xcd·(n/8) + id/8 puts each split's consecutive tap workgroups on one XCD —
-  // they all read the same G chunk and overlapping X rows, which then hit that XCD's L2.
+  // logical workgroup xcd·(n/8) + id/8 puts a split's column tiles on one XCD (one G chunk).
   const int nwg = gridDim.x;                  // padded to a multiple of 8
   const int L = (blockIdx.x % 8) * (nwg / 8) + blockIdx.x / 8;
-  const int tiles = TAPS * (C / CB);
+  const int tiles = C / CB;
   if (L >= tiles * nsplit) return;            // padding workgroups (before any barrier)
-  const int tile = L % tiles;
-  const int tap = tile % TAPS, ct = tile / TAPS;
-  // LDS images are XOR-swizzled by 16-byte piece: piece k of pixel row r sits at k ^ swz(r). A
-  // transposed read's 32-lane half touches rows {q, 8 + q} (+4), two pieces each; swz gives them
-  // disjoint bank windows (384-byte rows: the row parity already splits the 64 banks in two).
-  auto swz_rows = [](int r, int row_elems) {
-    return row_elems == 192 ? 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1))
-                            : 2 * ((r & 3) | (((r >> 3) & 1) << 2));
-  };
-  auto swzg = [&](int r) { return swz_rows(r, M); };
-  auto swzx = [&](int r) { return swz_rows(r, CB); };
-  const int kh = tap / KS, kw = tap % KS;
-  const int split = L / tiles;
-  const long P = (long)B * Ho * Wo;
+  const int ct = L % tiles, split = L / tiles;
   const long per = ((P + nsplit - 1) / nsplit + KP - 1) / KP * KP;
   const long p0 = split * per;
   const long p1 = p0 + per < P ? p0 + per : P;
   const int nsteps = p1 > p0 ? (int)((p1 - p0 + KP - 1) / KP) : 0;
 
-  // DMA slot j of this wave: instruction i = wave + NW·j, a fixed plane and 16-byte piece column.
-  // G slots: a contiguous [pixel][M] row, 32-bit offset advanced by KP·M per step. X slots: the
-  // tap-shifted source pixel of output pixel p, tracked incrementally as (b, oh, ow); the 32-bit
-  // element offset moves by 2·KP·C while the step stays in the output row, else is recomputed.
-  int pj[NI_W], off[NI_W], ow_[NI_W], oh_[NI_W], b_[NI_W];
-  auto xoff = [&](int j) {
-    const int iy = oh_[j] * STRIDE - PAD + kh, ix = ow_[j] * STRIDE - PAD + kw;
-    return ((b_[j] * Hi + iy) * Wi + ix) * C;
-  };
+  // DMA slot j of this wave: instruction i = wave + NW·j, a fixed plane and 16-byte piece column
+  // of a contiguous [pixel][channel] row; the element offset advances by KP rows per step.
+  long pj[NI_W], off[NI_W];
 #pragma unroll
   for (int j = 0; j < NI_W; ++j) {
     const int i = wave + NW * j;
     const bool isg = i < 3 * NGI;
     const int pc = (isg ? (i % NGI) : ((i - 3 * NGI) % NXI)) * 64 + lane;
     const int prow = isg ? pc / GPR : pc / XPR;
-    const int piece = isg ? (pc % GPR) ^ swzg(prow) : (pc % XPR) ^ swzx(prow);
-    const long p = p0 + prow;
-    pj[j] = (int)p;
-    ow_[j] = (int)(p % Wo);
-    const long qq = p / Wo;
-    oh_[j] = (int)(qq % Ho);
-    b_[j] = (int)(qq / Ho);
-    off[j] = isg ? (int)p * M + piece * 8 : ct * CB + piece * 8;   // X: the channel part only
+    const int piece = isg ? (pc % GPR) ^ swz6(prow, M) : (pc % XPR) ^ swz6(prow, CB);
+    pj[j] = p0 + prow;
+    off[j] = isg ? pj[j] * M + piece * 8 : pj[j] * C + ct * CB + piece * 8;
   }
-  const int p1i = (int)p1;
-  int xo[NI_W];
-#pragma unroll
-  for (int j = 0; j < NI_W; ++j) xo[j] = xoff(j);
   auto issue = [&](int buf) {
     unsigned short* st = smem + buf * STAGE;
 #pragma unroll
@@ -247,13 +223,11 @@ __global__ void __launch_bounds__(512) wgrad_x6_kernel(const unsigned short* __r
       unsigned short* dst;
       if (i < 3 * NGI) {
         const int pl = i / NGI, ii = i % NGI;
-        if (pj[j] < p1i) src = G6 + pl * pg + off[j];
+        if (pj[j] < p1) src = G6 + pl * pg + off[j];
         dst = st + pl * GPL + ii * 512;
       } else {
         const int pl = (i - 3 * NGI) / NXI, ii = (i - 3 * NGI) % NXI;
-        const int iy = oh_[j] * STRIDE - PAD + kh, ix = ow_[j] * STRIDE - PAD + kw;
-        if (pj[j] < p1i && (unsigned)iy < (unsigned)Hi && (unsigned)ix < (unsigned)Wi)
-          src = X6 + pl * pxs + xo[j] + off[j];
+        if (pj[j] < p1) src = X6 + pl * pxs + off[j];
         dst = st + 3 * GPL + pl * XPL + ii * 512;
       }
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
@@ -265,20 +239,7 @@ __global__ void __launch_bounds__(512) wgrad_x6_kernel(const unsigned short* __r
     for (int j = 0; j < NI_W; ++j) {
       const int i = wave + NW * j;
       pj[j] += KP;
-      if (i < 3 * NGI) {
-        off[j] += KP * M;
-      } else {
-        ow_[j] += KP;
-        if (ow_[j] < Wo) {
-          xo[j] += STRIDE * KP * C;
-        } else {
-          do {
-            ow_[j] -= Wo;
-            if (++oh_[j] == Ho) { oh_[j] = 0; ++b_[j]; }
-          } while (ow_[j] >= Wo);
-          xo[j] = xoff(j);
-        }
-      }
+      off[j] += (long)KP * (i < 3 * NGI ? M : C);
     }
   };
 
@@ -290,7 +251,7 @@ __global__ void __launch_bounds__(512) wgrad_x6_kernel(const unsigned short* __r
   // transposed-read lane addresses: group g = lane >> 4 takes pixel rows 8g .. 8g+7 (two reads of
   // 4); lane 4q + p of the group addresses row q, channels 4p .. 4p+3.
   const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
-  const int frg = swzg(8 * g + q), frx = swzx(8 * g + q);   // both ignore row bit 2 (+4 rows)
+  const int frg = swz6(8 * g + q, M), frx = swz6(8 * g + q, CB);   // both ignore row bit 2 (+4 rows)
   int aoff[MT], boff[NT];          // u16 offsets within a plane image (second read: + 4 rows)
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
@@ -356,8 +317,8 @@ __global__ void __launch_bounds__(512) wgrad_x6_kernel(const unsigned short* __r
       }
     }
   }
-  // part[split][m][c][tap]: lane holds rows 4(lane >> 4) + r, column lane & 15 of each tile
-  float* out = part + (long)split * M * C * TAPS;
+  // part[split][m][c]: lane holds rows 4(lane >> 4) + r, column lane & 15 of each tile
+  float* out = part + (long)split * M * C;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -366,20 +327,16 @@ __global__ void __launch_bounds__(512) wgrad_x6_kernel(const unsigned short* __r
       for (int r = 0; r < 4; ++r) {
         const int m = wm * (M / WM) + mt * 16 + 4 * (lane >> 4) + r;
         const int c = ct * CB + wn * (CB / WN) + nt * 16 + (lane & 15);
-        out[((long)m * C + c) * TAPS + tap] = acc[mt][nt][r];
+        out[(long)m * C + c] = acc[mt][nt][r];
       }
 }
 
 // GDN.py:83 γ gradient in x6: dγ_eff[i][j] = Σ_p dn[p][i] · u[p][j]², straight from the fp32
-// tensors. The tiles, LDS images and MFMA loop are wgrad_x6_kernel's (M = CB = C, one tap), but
+// tensors. The tiles, LDS images and MFMA loop are wgrad_x6_1x1_kernel's (M = CB = C), but
 // the workgroup stages the operands itself: each thread loads its fp32 pieces of the next step
 // into registers while the current step computes, squares u, splits both into the three bf16
 // planes and writes them to the idle LDS buffer — no split copies of dn and u² in HBM, which
 // would cost more traffic than the x6 contraction saves. One workgroup per pixel split.
-__device__ __forceinline__ int swz6(int r, int row_elems) {
-  return row_elems == 192 ? 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1))
-                          : 2 * ((r & 3) | (((r >> 3) & 1) << 2));
-}
 
 __device__ __forceinline__ void split4(const f4& x, uint2& hi, uint2& mi, uint2& lo) {
   unsigned h[4], m[4], l[4];
@@ -563,7 +520,7 @@ __global__ void __launch_bounds__(512) wgrad_x6_row_kernel(const unsigned short*
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave & 3, wn = wave >> 2;
-  // XCD-aware order (as wgrad_x6_kernel): a split's 5·C/64 workgroups share one XCD's L2
+  // XCD-aware order (as wgrad_x6_1x1_kernel): a split's 5·C/64 workgroups share one XCD's L2
   const int nwg = gridDim.x;
   const int L = (blockIdx.x % 8) * (nwg / 8) + blockIdx.x / 8;
   const int tiles = KW * (C / CBX);
@@ -1127,9 +1084,9 @@ int iclr17_wgrad_k9_x6(const uint16_t* G_split, const float* X, int B, int Ho, i
   dim3 grid((tiles * ns + 7) / 8 * 8);
   const unsigned short* g6 = (const unsigned short*)G_split;
   if (M == 192)
-    hipLaunchKernelGGL((wgrad_x6_kernel<192, 128, 2, 4, 1>), grid, dim3(512), 0, st, g6, P * M, cols, P * 256, B, Ho, Wo, Ho, Wo, 256, ns, part);
+    hipLaunchKernelGGL((wgrad_x6_1x1_kernel<192, 128>), grid, dim3(512), 0, st, g6, P * M, cols, P * 256, P, 256, ns, part);
   else
-    hipLaunchKernelGGL((wgrad_x6_kernel<128, 128, 2, 4, 1>), grid, dim3(512), 0, st, g6, P * M, cols, P * 256, B, Ho, Wo, Ho, Wo, 256, ns, part);
+    hipLaunchKernelGGL((wgrad_x6_1x1_kernel<128, 128>), grid, dim3(512), 0, st, g6, P * M, cols, P * 256, P, 256, ns, part);
   rc = check_launch("wgrad_k9_x6");
   if (rc) return rc;
   const long n = (long)M * 243;

@@ -31,6 +31,18 @@ int check_launch(const char* what);
     }                                            \
   } while (0)
 
+// ----------------------------------------------------------------------------- LDS-DMA sync
+// Publishes LDS-DMA (global_load_lds) data to the whole workgroup: this wave's DMAs landed
+// (s_waitcnt vmcnt(0)), then the barrier. A bare __syncthreads() is NOT enough: the workgroup
+// release fence waits only for lgkmcnt, and the compiler adds a vmcnt wait before a barrier only
+// when it proves that this wave's own LDS reads after it may alias the DMA. conv1_gdn_kernel's
+// main loop compiled to `s_waitcnt lgkmcnt(0); s_barrier` with the previous step's weight DMA in
+// flight, and one run in ~20 read a stale B stage (a rare run-to-run difference in fp32 conv1).
+__device__ __forceinline__ void dma_barrier() {
+  __builtin_amdgcn_s_waitcnt((0 & 15) | (7 << 4) | (15 << 8));   // vmcnt(0), exp/lgkm untouched
+  __syncthreads();
+}
+
 // ----------------------------------------------------------------------------- MFMA
 __device__ __forceinline__ f4 mfma16(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);

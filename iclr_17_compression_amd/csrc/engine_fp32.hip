@@ -311,7 +311,7 @@ __device__ __forceinline__ void chan_gemm_lds(f4 (&acc)[MT][NT], const float* sX
   issue(0, 0);
 #pragma unroll 2
   for (int kb = 0; kb < KB; ++kb) {
-    __syncthreads();
+    dma_barrier();
     if (kb + 1 < KB) issue(kb + 1, (kb + 1) & 1);
     const float* g = sG + (kb & 1) * GST + goff;
     f4 bf[NT], af[MT];
@@ -1045,7 +1045,7 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
 
   issue(0, 0);
   for (int s = 0; s < nsteps; ++s) {
-    __syncthreads();   // vmcnt(0) + barrier: step s landed for every wave; stage (s+1)&1 is free
+    dma_barrier();   // step s landed for every wave; stage (s+1)&1 is free
     if (s + 1 < nsteps) issue(s + 1, (s + 1) & 1);
     compute(s & 1);
   }
@@ -1268,7 +1268,7 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int s = cc * 9 + tap;
-      __syncthreads();   // vmcnt(0) + barrier: A (at a chunk start) and B of step s landed
+      dma_barrier();   // A (at a chunk start) and B of step s landed
       if (tap != 8) issue_b(s + 1, (s + 1) & 1);
       if (tap < 3)
         compute(s & 1, tap, std::integral_constant<int, 1>{});
@@ -1415,7 +1415,7 @@ __global__ void __launch_bounds__(256) conv1_gdn_kernel(const EngineArgs a) {
     ktab[k] = off;
     if (tid < 64) mtab[tid] = (tid >> 3) * 4 * P1RS + (tid & 7) * 4;
   }
-  __syncthreads();
+  dma_barrier();   // patch (and the tables) published
 
   f4 acc[MT][NT];
 #pragma unroll
@@ -1429,7 +1429,7 @@ __global__ void __launch_bounds__(256) conv1_gdn_kernel(const EngineArgs a) {
 
   const int boff = ((lane >> 4) * CO + ncol0 + (lane & 15)) * 4;
   for (int s = 0; s < 8; ++s) {
-    __syncthreads();   // B stage s landed (and, at s = 0, the patch); stage (s+1)&1 is free
+    dma_barrier();   // B stage s landed (and, at s = 0, the patch); stage (s+1)&1 is free
     if (s + 1 < 8) issue(s + 1, (s + 1) & 1);
     const float* bs = sB + (s & 1) * SB + boff;
 #pragma unroll
@@ -1569,7 +1569,7 @@ __global__ void __launch_bounds__(512) deconv3_bf16_kernel(const EngineArgs a) {
 
   issue(0, 0);
   for (int cc = 0; cc < NCH; ++cc) {
-    __syncthreads();   // vmcnt(0) + barrier: chunk cc landed; buffer (cc+1)&1 is free
+    dma_barrier();   // chunk cc landed; buffer (cc+1)&1 is free
     if (cc + 1 < NCH) issue(cc + 1, (cc + 1) & 1);
     const int buf = cc & 1;
 #pragma unroll
@@ -1714,7 +1714,7 @@ __global__ void __launch_bounds__(256, 2) conv1_x6_kernel(const EngineArgs a) {
         b[p][nt] = *(const u4*)(gb + p * GP + (long)s * 4 * CO * 8 + nt * 128);
   };
   loadb(0, b0);
-  __syncthreads();   // patch landed
+  dma_barrier();   // patch landed
 
   // Split pass: piece pc (4 floats at column 4q of row cr) → 4 bf16 in each plane.
   for (int pc = tid; pc < P1PIECES; pc += 256) {

@@ -106,7 +106,7 @@ __global__ void __launch_bounds__(256) wgrad_k5_kernel(const float* __restrict__
 
   if (nsteps > 0) issue(0, 0);
   for (int s = 0; s < nsteps; ++s) {
-    __syncthreads();   // stage s landed for every wave; stage (s+1)&1 is free
+    dma_barrier();   // stage s landed for every wave; stage (s+1)&1 is free
     if (s + 1 < nsteps) issue(s + 1, (s + 1) & 1);
     const float* g = smem + (s & 1) * STAGE + aoff;
     const float* x = smem + (s & 1) * STAGE + SG + boff;
@@ -267,7 +267,7 @@ __global__ void __launch_bounds__(512) wgrad_x6_1x1_kernel(const unsigned short*
   const unsigned sbase = (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned short*)smem;
   if (nsteps > 0) issue(0);
   for (int s = 0; s < nsteps; ++s) {
-    __syncthreads();   // stage s landed for every wave; stage (s+1)&1 is free
+    dma_barrier();   // stage s landed for every wave; stage (s+1)&1 is free
     if (s + 1 < nsteps) {
       advance();
       issue((s + 1) & 1);
@@ -617,7 +617,7 @@ __global__ void __launch_bounds__(512) wgrad_x6_row_kernel(const unsigned short*
 
   if (nsteps > 0) issue(0, 0);
   for (int s = 0; s < nsteps; ++s) {
-    __syncthreads();   // stage s landed for every wave; stage (s+1)&1 is free
+    dma_barrier();   // stage s landed for every wave; stage (s+1)&1 is free
     if (s + 1 < nsteps) issue(s + 1, (s + 1) & 1);
     const unsigned st = sbase + (s & 1) * STAGE * 2;
     const unsigned sx = st + 3 * GPL * 2;

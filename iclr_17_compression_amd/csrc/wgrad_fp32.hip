@@ -536,8 +536,10 @@ __global__ void __launch_bounds__(512) wgrad_x6_row_kernel(const unsigned short*
 
   // DMA slots: G slot (row k = 16·dr + dc, physical piece) ← piece ^ swz6(k) of output pixel
   // (oh0 + dr, ow0 + dc); X slot (physical row R, 16-byte chunk J) ← chunk of logical row
-  // r = R ^ bit4(R): input (2·(oh0 + r / 36) − 2 + kh, 2·ow0 − 2 + r % 36).
-  int sa[NI_W], sb[NI_W];   // G: (dr, dc) / X: (rb, col); and the element offset in the plane row
+  // r = R ^ bit4(R): input (2·(oh0 + r / 36) − 2 + kh, 2·ow0 − 2 + r % 36). so[j] is the slot's
+  // element offset from the operand base (plane · plane stride + channel piece; 32-bit, the host
+  // checks 3 planes < 2^31 elements), sa[j] its (row, column) within the step's pixel block.
+  int sa[NI_W], so[NI_W];
 #pragma unroll
   for (int j = 0; j < NI_W; ++j) {
     const int i = wave + NW * j;
@@ -545,43 +547,53 @@ __global__ void __launch_bounds__(512) wgrad_x6_row_kernel(const unsigned short*
       const int pc = (i % NGI) * 64 + lane;
       const int k = pc / GPR, piece = (pc % GPR) ^ swz6(k, M);
       sa[j] = ((k >> 4) << 8) | (k & 15);
-      sb[j] = piece * 8;
+      so[j] = (i / NGI) * (int)pg + piece * 8;
     } else {
       const int ii = i - 3 * NGI;
       const int R = (ii % NXI) * 8 + (lane >> 3), J = lane & 7;
       const int r = R ^ ((R >> 4) & 1);
       const int chunk = ((((J >> 1) ^ ((r >> 1) & 3)) << 1) | (J & 1));
       sa[j] = ((r / XROW) << 8) | (r % XROW);
-      sb[j] = cb * CBX + chunk * 8;
+      so[j] = (ii / NXI) * (int)pxs + cb * CBX + chunk * 8;
     }
   }
-  auto issue = [&](int s, int buf) {
-    long t = s0 + s;
-    const int owb = (int)(t % OWB);
-    t /= OWB;
-    const int oh0 = (int)(t % OHP) * 2, b = (int)(t / OHP), ow0 = owb * 16;
+  // position (image, output row pair, 16-column block) of the next step to issue, advanced by one
+  // step per issue: no 64-bit divisions in the loop
+  int owb, ohp, bimg;
+  {
+    const long t = s0 / OWB;
+    owb = (int)(s0 - t * OWB);
+    ohp = (int)(t % OHP);
+    bimg = (int)(t / OHP);
+  }
+  auto issue = [&](int buf, int j0, int j1, bool adv) {
+    const int oh0 = 2 * ohp, ow0 = 16 * owb;
+    const int gpix = (bimg * Ho + oh0) * Wo + ow0;            // G pixel of (oh0, ow0)
+    const int xrow = bimg * Hi + 2 * oh0 - 2 + kh, xcol = 2 * ow0 - 2;
     unsigned short* st = smem + buf * STAGE;
 #pragma unroll
-    for (int j = 0; j < NI_W; ++j) {
+    for (int j = j0; j < j1; ++j) {
       const int i = wave + NW * j;
       if (NI % NW != 0 && i >= NI) break;   // wave-uniform
       const void* src = g_wzero;
       unsigned short* dst;
+      const int dr = sa[j] >> 8, dc = sa[j] & 255;
       if (i < 3 * NGI) {
-        const int pl = i / NGI;
-        const int oh = oh0 + (sa[j] >> 8), ow = ow0 + (sa[j] & 255);
-        if (oh < Ho && ow < Wo) src = G6 + pl * pg + ((long)(b * Ho + oh) * Wo + ow) * M + sb[j];
-        dst = st + pl * GPL + (i % NGI) * 512;
+        if (oh0 + dr < Ho && ow0 + dc < Wo) src = G6 + (unsigned)(so[j] + (gpix + dr * Wo + dc) * M);
+        dst = st + (i / NGI) * GPL + (i % NGI) * 512;
       } else {
-        const int ii = i - 3 * NGI, pl = ii / NXI;
-        const int col = sa[j] & 255;
-        const int iy = 2 * (oh0 + (sa[j] >> 8)) - 2 + kh, ix = 2 * ow0 - 2 + col;
-        if (col < 2 * 16 + 3 && (unsigned)iy < (unsigned)Hi && (unsigned)ix < (unsigned)Wi)
-          src = X6 + pl * pxs + ((long)(b * Hi + iy) * Wi + ix) * C + sb[j];
-        dst = st + 3 * GPL + pl * XPL + (ii % NXI) * 512;
+        const int ii = i - 3 * NGI;
+        const int iy = 2 * (oh0 + dr) - 2 + kh, ix = xcol + dc;
+        if (dc < 2 * 16 + 3 && (unsigned)iy < (unsigned)Hi && (unsigned)ix < (unsigned)Wi)
+          src = X6 + (unsigned)(so[j] + ((xrow + 2 * dr) * Wi + ix) * C);
+        dst = st + 3 * GPL + (ii / NXI) * XPL + (ii % NXI) * 512;
       }
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+    if (adv && ++owb == OWB) {
+      owb = 0;
+      if (++ohp == OHP) { ohp = 0; ++bimg; }
     }
   };
 
@@ -615,10 +627,9 @@ __global__ void __launch_bounds__(512) wgrad_x6_row_kernel(const unsigned short*
     return u4{lo.x, lo.y, hi.x, hi.y};
   };
 
-  if (nsteps > 0) issue(0, 0);
+  if (nsteps > 0) issue(0, 0, NI_W, true);
   for (int s = 0; s < nsteps; ++s) {
     dma_barrier();   // stage s landed for every wave; stage (s+1)&1 is free
-    if (s + 1 < nsteps) issue(s + 1, (s + 1) & 1);
     const unsigned st = sbase + (s & 1) * STAGE * 2;
     const unsigned sx = st + 3 * GPL * 2;
     u4 Af[MT][3], Bf[2][NT][3];
@@ -667,6 +678,10 @@ __global__ void __launch_bounds__(512) wgrad_x6_row_kernel(const unsigned short*
           acc[kw][mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A0, B0, c, 0, 0, 0);
         }
       }
+      // the next stage's DMA goes out two slots per tap behind the MFMAs of taps 0-3: its address
+      // arithmetic fills MFMA gaps instead of delaying the step's first fragment reads after the
+      // barrier, where all 8 waves would run it at once (wgrad_check B=32: 0.405 -> 0.375 ms)
+      if (kw < 4 && s + 1 < nsteps) issue((s + 1) & 1, 2 * kw, 2 * kw + 2 < NI_W ? 2 * kw + 2 : NI_W, kw == 3);
       if (kw + 1 < KW) {
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
@@ -1051,6 +1066,8 @@ int iclr17_wgrad_k5_x6(const uint16_t* G_split, const uint16_t* X_split, int B, 
   const int tiles = 5 * (C / 64);   // (kernel row, 64-channel block)
   const int ns = wgrad6_splits(P, tiles);
   const long pg = P * M, pxs = (long)B * 4 * Ho * Wo * C;
+  ICLR17_REQUIRE(3 * pg < (1L << 31) && 3 * pxs < (1L << 31), ICLR17_EUNSUPPORTED,
+                 "wgrad_k5_x6: split operands of %ld / %ld elements exceed 32-bit offsets", 3 * pg, 3 * pxs);
   hipStream_t st = S(stream);
   dim3 grid((tiles * ns + 7) / 8 * 8);   // 1-D, padded to whole XCD rounds (see the kernel)
   const unsigned short* g6 = (const unsigned short*)G_split;

@@ -101,7 +101,7 @@ class Step:
         ev = (lambda i: events[i].record()) if events is not None else (lambda i: None)
         ev(0)
         if kernels.precision() == "bf16":
-            (w1b, w2b, w3b), (d1b, d2b), (e1, e2, e3, e4) = self.ebf, self.dbf, self.gbf
+            (w1b, w2b, w3b), (d1b, d2b, d3b), (e1, e2, e3, e4) = self.ebf, self.dbf, self.gbf
             h = kernels.conv1_gdn_bf16(self.x, w1b, net.Encoder.conv1.bias, *e1, N)
             ev(1)
             h = kernels.conv2_gdn_bf16(h, w2b, net.Encoder.conv2.bias, *e2)
@@ -112,7 +112,7 @@ class Step:
             ev(4)
             h = kernels.deconv_igdn_bf16(h, d2b, net.Decoder.deconv2.bias, *e4)
             ev(5)
-            clipped, _, _ = kernels.deconv3_bf16(h, d3, net.Decoder.deconv3.bias)
+            clipped, _, _ = kernels.deconv3_bf16(h, d3b, net.Decoder.deconv3.bias)
         elif kernels.precision() == "x6":
             e1, e2, e3, e4 = self.g6
             hs, _, _ = kernels.conv1x6_gdn(self.x, self.w1x6, net.Encoder.conv1.bias, e1[0], e1[2],

@@ -1121,7 +1121,7 @@ constexpr int D3_PS = D3_BS + 2;                // patch side
 constexpr int D3_PPX = D3_PS * D3_PS;           // 324 patch pixels per plane
 constexpr int D3_NAI = (3 * D3_PPX + 15) / 16;  // 61 A wave-instructions per chunk
 constexpr int D3_SA = D3_NAI * 256;             // A stage floats (976 slots × 16)
-constexpr int D3_SB = 32 * 48;                  // fp32 B stage floats (the bf16 kernel's)
+constexpr int D3_SBB = 32 * 48 / 2;             // bf16 B stage floats: [4 k8][48][8] u16 (the bf16 kernel's)
 constexpr int D3_SB6 = 3 * 32 * 48 / 2;         // x6 B stage floats: [3 planes][4 k8][48][8] u16
 constexpr int D3_LDS = D3_SA + 2 * D3_SB6;      // 80,896 B: two workgroups per CU
 
@@ -1481,8 +1481,8 @@ __global__ void __launch_bounds__(512) deconv3_bf16_kernel(const EngineArgs a) {
   constexpr int KCH = 32, NCH = CI / KCH, MT = 2, NT = 3, NW = 8;
   constexpr int NAI = (D3_PPX + 15) / 16;   // 21 patch wave-instructions per chunk (16 px each)
   constexpr int SA = NAI * 256;             // patch buffer floats
-  constexpr int PB = 9 * D3_SB;             // weight floats per chunk: [tap][kq 8][48][4]
-  constexpr int NBI = PB / 256;             // 54 weight wave-instructions per chunk
+  constexpr int PB = 9 * D3_SBB;            // weight floats per chunk: [tap][k8 4][48][8] bf16
+  constexpr int NBI = PB / 256;             // 27 weight wave-instructions per chunk
   constexpr int KA = (NAI + NW - 1) / NW, KB = (NBI + NW - 1) / NW;
   constexpr int LDS = 2 * SA + 2 * PB;
   static_assert(3 * 64 * 65 + 16 <= LDS, "epilogue block fits");
@@ -1512,14 +1512,16 @@ __global__ void __launch_bounds__(512) deconv3_bf16_kernel(const EngineArgs a) {
     const int g = (lane & 3) ^ (((p >> 2) & 1) << 1);
     asrc[j] = ok ? (iy * a.Win + ix) * CI + g * 8 : -1;
   }
-  // weight DMA: instruction i = tap t (6 per tap), slot (kq, j) ← packed (cc·8 + kq, d3_col(j))
+  // weight DMA (iclr17_round_packed of the ICLR17_W_DECONV9 packing: [9][CI/8][48][8] bf16):
+  // instruction i = tap t (3 per tap), slot (k8, j) ← packed (cc·4 + k8, d3_col(j)), u16 offsets
   int bsrc[KB];
 #pragma unroll
   for (int j = 0; j < KB; ++j) {
     const int i = wave + NW * j;
-    const int t = i / 6, w = (i - t * 6) * 64 + lane, kq = w / 48, jj = w - kq * 48;
-    bsrc[j] = t * CI * 48 + (kq * 48 + d3_col(jj)) * 4;
+    const int t = i / 3, w = (i - t * 3) * 64 + lane, k8 = w / 48, jj = w - k8 * 48;
+    bsrc[j] = (t * (CI / 8) * 48 + k8 * 48 + d3_col(jj)) * 8;
   }
+  const unsigned short* __restrict__ wb = (const unsigned short*)a.w;
   const unsigned short* __restrict__ inb = a.in_split + (long)b * a.Hin * a.Win * CI;
   auto issue = [&](int cc, int buf) {
 #pragma unroll
@@ -1532,7 +1534,7 @@ __global__ void __launch_bounds__(512) deconv3_bf16_kernel(const EngineArgs a) {
 #pragma unroll
     for (int j = 0; j < KB; ++j) {
       const int i = wave + NW * j;
-      if (i < NBI) glds16(a.w + (long)cc * KCH * 48 + bsrc[j], sB + buf * PB + i * 256);
+      if (i < NBI) glds16((const float*)(wb + cc * 4 * 48 * 8 + bsrc[j]), sB + buf * PB + i * 256);
     }
   };
 
@@ -1546,15 +1548,10 @@ __global__ void __launch_bounds__(512) deconv3_bf16_kernel(const EngineArgs a) {
   auto compute = [&](int buf, int tap, auto ntt) {
     constexpr int NTT = decltype(ntt)::value;   // tiles this tap touches
     const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
-    const float* sb = sB + buf * PB + tap * D3_SB + 2 * g * 48 * 4;
+    const u4* sb = (const u4*)(sB + buf * PB + tap * D3_SBB) + g * 48;
     bf8 Bb[NTT];
 #pragma unroll
-    for (int nt = 0; nt < NTT; ++nt) {
-      const int jc = nt * 16 + (lane & 15);
-      const f4 w0 = *(const f4*)(sb + jc * 4), w1 = *(const f4*)(sb + 48 * 4 + jc * 4);
-      Bb[nt] = bf8{(__bf16)w0[0], (__bf16)w0[1], (__bf16)w0[2], (__bf16)w0[3],
-                   (__bf16)w1[0], (__bf16)w1[1], (__bf16)w1[2], (__bf16)w1[3]};
-    }
+    for (int nt = 0; nt < NTT; ++nt) Bb[nt] = __builtin_bit_cast(bf8, sb[nt * 16 + (lane & 15)]);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const int p = prow + (mt + dy) * D3_PS + dx;
@@ -2361,7 +2358,8 @@ int iclr17_synthesis_deconv_igdn(const float* in, int B, int h, int w, int N,
                   : launch_deconv5<128>(in, B, h, w, w_packed, bias, beta_eff, gamma_packed, out, pre_out, S(stream));
 }
 
-// w: the fp32 ICLR17_W_DECONV9 packing (bf16 mode) or its iclr17_split_packed(9, N, 48) planes (x6)
+// w: iclr17_round_packed(9, N, 48) of the ICLR17_W_DECONV9 packing (bf16 mode) or its
+// iclr17_split_packed(9, N, 48) planes (x6)
 static int launch_deconv3_halo(const uint16_t* in, int B, int H, int W, int N, const void* w,
                                const float* bias, const float* x, float* clipped, float* recon,
                                double* sse_partial, int sse_unclipped, void* stream, bool bf) {
@@ -2408,10 +2406,10 @@ int iclr17_synthesis_deconv3_x6(const uint16_t* in_split, int B, int H, int W, i
 }
 
 int iclr17_synthesis_deconv3_bf16(const uint16_t* in, int B, int H, int W, int N,
-                                  const float* w_packed, const float* bias, const float* x_ref,
+                                  const uint16_t* w_bf16, const float* bias, const float* x_ref,
                                   float* clipped, float* recon, double* sse_partial,
                                   int sse_unclipped, void* stream) {
-  return launch_deconv3_halo(in, B, H, W, N, w_packed, bias, x_ref, clipped, recon, sse_partial,
+  return launch_deconv3_halo(in, B, H, W, N, w_bf16, bias, x_ref, clipped, recon, sse_partial,
                              sse_unclipped, stream, true);
 }
 

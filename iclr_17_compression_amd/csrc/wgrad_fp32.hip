@@ -566,6 +566,10 @@ __global__ void __launch_bounds__(512) wgrad_x6_row_kernel(const unsigned short*
     ohp = (int)(t % OHP);
     bimg = (int)(t / OHP);
   }
+  // the zero line's address pinned in SGPRs: as a __device__ global it would be re-read from the
+  // GOT by a scalar load at every use, and each such load delays the next lgkmcnt(0) wait
+  const unsigned short* zp = (const unsigned short*)g_wzero;
+  asm volatile("" : "+s"(zp));
   auto issue = [&](int buf, int j0, int j1, bool adv) {
     const int oh0 = 2 * ohp, ow0 = 16 * owb;
     const int gpix = (bimg * Ho + oh0) * Wo + ow0;            // G pixel of (oh0, ow0)
@@ -575,17 +579,18 @@ __global__ void __launch_bounds__(512) wgrad_x6_row_kernel(const unsigned short*
     for (int j = j0; j < j1; ++j) {
       const int i = wave + NW * j;
       if (NI % NW != 0 && i >= NI) break;   // wave-uniform
-      const void* src = g_wzero;
+      const unsigned short* src;
       unsigned short* dst;
       const int dr = sa[j] >> 8, dc = sa[j] & 255;
-      if (i < 3 * NGI) {
-        if (oh0 + dr < Ho && ow0 + dc < Wo) src = G6 + (unsigned)(so[j] + (gpix + dr * Wo + dc) * M);
+      if (i < 3 * NGI) {   // wave-uniform; the bounds checks below are selects, not branches
+        const unsigned short* p = G6 + (unsigned)(so[j] + (gpix + dr * Wo + dc) * M);
+        src = oh0 + dr < Ho && ow0 + dc < Wo ? p : zp;
         dst = st + (i / NGI) * GPL + (i % NGI) * 512;
       } else {
         const int ii = i - 3 * NGI;
         const int iy = 2 * (oh0 + dr) - 2 + kh, ix = xcol + dc;
-        if (dc < 2 * 16 + 3 && (unsigned)iy < (unsigned)Hi && (unsigned)ix < (unsigned)Wi)
-          src = X6 + (unsigned)(so[j] + ((xrow + 2 * dr) * Wi + ix) * C);
+        const unsigned short* p = X6 + (unsigned)(so[j] + ((xrow + 2 * dr) * Wi + ix) * C);
+        src = dc < 2 * 16 + 3 && (unsigned)iy < (unsigned)Hi && (unsigned)ix < (unsigned)Wi ? p : zp;
         dst = st + 3 * GPL + (ii / NXI) * XPL + (ii % NXI) * 512;
       }
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,

@@ -646,13 +646,15 @@ def deconv_igdn_bf16(h: Tensor, w_bf: Tensor, bias: Tensor, beta_eff: Tensor, g_
     return out
 
 
-def deconv3_bf16(h: Tensor, wp: Tensor, bias: Tensor, x_ref: Optional[Tensor] = None,
+def deconv3_bf16(h: Tensor, wb: Tensor, bias: Tensor, x_ref: Optional[Tensor] = None,
                  want_recon: bool = False, sse_unclipped: bool = False):
     """synthesis_17.py:23-25 + model.py:59 in bf16: bf16 NHWC [B,H/4,W/4,N] → the ``deconv3``
-    returns (wp: the fp32 ICLR17_W_DECONV9 packing, rounded to bf16 in the kernel)."""
+    returns (wb: ``round_packed(d3, 9, N, 48)`` of the ICLR17_W_DECONV9 packing d3)."""
     _check_bf16(h, "activation")
     B, h4, w4, N = h.shape
-    return _deconv3_halo("iclr17_synthesis_deconv3_bf16", h, B, h4, w4, N, wp, bias, x_ref,
+    if wb.dtype != torch.int16 or wb.numel() != 9 * N * 48:
+        raise Iclr17Error("iclr17: deconv3_bf16: weights are not round_packed(d3, 9, N, 48)")
+    return _deconv3_halo("iclr17_synthesis_deconv3_bf16", h, B, h4, w4, N, wb, bias, x_ref,
                          want_recon, sse_unclipped)
 
 

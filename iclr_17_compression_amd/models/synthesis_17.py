@@ -54,13 +54,17 @@ class Synthesis_net_17(nn.Module):
                               lambda: kernels.split_deconv3(d3, self.out_channel_N), force)
 
     def packed_bf16(self, force: bool = False):
-        """deconv1 / deconv2 in the bf16 engine's step layout (4 stride phases), cached."""
+        """deconv1 / deconv2 in the bf16 engine's step layout (4 stride phases) and deconv3's
+        all-phase packing rounded to bf16 fragments, cached."""
         N, f = self.out_channel_N, force
         d1 = self._pack.get("d1bf", (self.deconv1.weight,),
                             lambda: kernels.pack_bf16(_lib.ICLR17_BF_DECONV5, self.deconv1.weight, N), f)
         d2 = self._pack.get("d2bf", (self.deconv2.weight,),
                             lambda: kernels.pack_bf16(_lib.ICLR17_BF_DECONV5, self.deconv2.weight, N), f)
-        return d1, d2
+        d3 = self.packed(force)[2]
+        d3b = self._pack.get("d3bf", (self.deconv3.weight,),
+                             lambda: kernels.round_packed(d3, 9, N, 48), f)
+        return d1, d2, d3b
 
     def packed_bwd(self, x6: bool):
         """The deconv weights packed as the convolutions of their input gradients: (deconv3 in
@@ -91,11 +95,11 @@ class Synthesis_net_17(nn.Module):
         ``y_bf16`` (bf16 bit patterns) in the bf16 throughput mode."""
         d1, d2, d3, g1, g2 = self.packed()
         if y_bf16 is not None:
-            b1, b2 = self.packed_bf16()
+            b1, b2, b3 = self.packed_bf16()
             q1, q2 = self.igdn1.effective_params_bf16(), self.igdn2.effective_params_bf16()
             h = kernels.deconv_igdn_bf16(y_bf16, b1, self.deconv1.bias, *q1)
             h = kernels.deconv_igdn_bf16(h, b2, self.deconv2.bias, *q2)
-            return kernels.deconv3_bf16(h, d3, self.deconv3.bias, x_ref=x_ref, want_recon=want_recon)
+            return kernels.deconv3_bf16(h, b3, self.deconv3.bias, x_ref=x_ref, want_recon=want_recon)
         if y_split is not None:
             q1, q2 = self.igdn1.effective_params_x6(), self.igdn2.effective_params_x6()
             hs, _, _ = kernels.deconv_igdn_x6(y_split, d1, self.deconv1.bias, *q1)

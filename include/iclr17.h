@@ -462,9 +462,10 @@ int iclr17_synthesis_deconv_igdn_bf16(const uint16_t* in, int B, int h, int w, i
                                       const float* beta_eff, const uint16_t* gamma_bf16,
                                       uint16_t* out, void* stream);
 /* synthesis_17.py:23-25 deconv3 + model.py:59 clamp: bf16 NHWC [B,H/4,W/4,N] → clipped NCHW
- * fp32 (+ unclipped, + SSE partials as iclr17_synthesis_deconv3) */
+ * fp32 (+ unclipped, + SSE partials as iclr17_synthesis_deconv3). w_bf16: iclr17_round_packed
+ * (taps 9, K N, columns 48) of the ICLR17_W_DECONV9 packing. */
 int iclr17_synthesis_deconv3_bf16(const uint16_t* in, int B, int H, int W, int N,
-                                  const float* w_packed, const float* bias, const float* x_ref,
+                                  const uint16_t* w_bf16, const float* bias, const float* x_ref,
                                   float* clipped, float* recon, double* sse_partial,
                                   int sse_unclipped, void* stream);
 

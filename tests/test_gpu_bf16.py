@@ -124,8 +124,7 @@ def test_bf16_synthesis_layers(device, N, hw):
     h, w = hw
     B = 2 if h * w <= 256 else 4
     net, sd = net_for(N, 1, device), sd_for(N, 1)
-    d1b, d2b = net.Decoder.packed_bf16()
-    d3 = net.Decoder.packed()[2]
+    d1b, d2b, d3 = net.Decoder.packed_bf16()
     q1, q2 = net.Decoder.igdn1.effective_params_bf16(), net.Decoder.igdn2.effective_params_bf16()
     y = torch.round(torch.from_numpy(synth.uniform(5, (B, N, h, w), -4, 4)))
     with torch.no_grad():

@@ -25,8 +25,7 @@ net = ImageCompressor(N)
 net.load_state_dict({k: torch.from_numpy(v) for k, v in synth.trained_like_state_dict(N, 1).items()})
 net = net.to(dev).eval()
 w1, w2, w3 = net.Encoder.packed_bf16()
-d1, d2 = net.Decoder.packed_bf16()
-d3 = net.Decoder.packed()[2]
+d1, d2, d3 = net.Decoder.packed_bf16()
 e1, e2 = net.Encoder.gdn1.effective_params_bf16(), net.Encoder.gdn2.effective_params_bf16()
 q1, q2 = net.Decoder.igdn1.effective_params_bf16(), net.Decoder.igdn2.effective_params_bf16()
 rate = net.bitEstimator.packed()

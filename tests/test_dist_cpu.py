@@ -1,4 +1,4 @@
-"""The multi-process paths (world_size 2, gloo on CPU): batch sharding, the per-image gather,
+"""The multi-process paths (world_size 2 and 8, gloo on CPU): batch sharding, the per-image gather,
 bucketed gradient averaging and max-over-ranks timing — the same functions the RCCL runs use."""
 import os
 import socket
@@ -60,8 +60,8 @@ def _worker(r, w, port, q):
         dist.destroy_process_group()
 
 
-def test_two_rank_gloo():
-    w = 2
+@pytest.mark.parametrize("w", [2, 8])   # 8: the rank count of BASELINE C4 / the 8-GPU bench
+def test_multi_rank_gloo(w):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -71,7 +71,7 @@ def test_two_rank_gloo():
     res = dict(q.get(timeout=120) for _ in range(w))
     for p in ps:
         p.join(timeout=60)
-    assert res == {0: "ok", 1: "ok"}, res
+    assert res == {r: "ok" for r in range(w)}, res
 
 
 def test_shard_range_balanced():

@@ -109,6 +109,39 @@ def test_data_parallel_equals_full_batch(device):
     assert not bad, bad
 
 
+def test_c4_global_batch_shards_lambda_sweep(device):
+    """BASELINE configs[3] (C4) on one GPU: a global batch of 256 crops of 256² sharded 8 × 32 as
+    the 8 ranks would hold it, for each λ of the sweep {0.003, 0.01, 0.03, 0.1} (train_lambda =
+    λ·255²). The all-reduce average of the 8 shard gradients (what dist.GradAllReducer delivers
+    before the clamp + Adam) equals the gradient of the whole 256-crop batch, per tensor at the
+    gradient bar. The ranks' collective itself is covered by tests/test_dist_cpu.py (gloo) and
+    tests/test_gpu_dp_overlap.py; 8 GPUs are not available to the test suite."""
+    N, S, R, PER = 192, 256, 8, 32
+    B = R * PER
+    net, _ = make(N, 7, device)
+    x = torch.from_numpy(synth.to_unit_float(synth.image_u8(11, B, S, S))).to(device)
+    noise = torch.from_numpy(synth.uniform(12, (B, N, S // 16, S // 16), -0.5, 0.5)).to(device)
+
+    def grads(lam, lo, hi):
+        net.zero_grad(set_to_none=True)
+        _, mse, bpp = net.forward_train(x[lo:hi], noise=noise[lo:hi])
+        loss = lam * mse + bpp
+        loss.backward()
+        return loss.item(), {k: p.grad.clone() for k, p in net.named_parameters()}
+
+    for lam_rd in (0.003, 0.01, 0.03, 0.1):
+        lam = lam_rd * 255.0 ** 2
+        full_loss, full = grads(lam, 0, B)
+        shard = [grads(lam, r * PER, (r + 1) * PER) for r in range(R)]
+        mean_loss = sum(s[0] for s in shard) / R
+        errs = {k: grad_err(sum(s[1][k] for s in shard) / R, full[k]) for k in full}
+        print(f"C4 λ={lam_rd}: loss {full_loss:.6f} (shard mean {mean_loss:.6f}), "
+              f"max rel grad err {max(errs.values()):.3e}")
+        assert np.isfinite(full_loss) and mean_loss == pytest.approx(full_loss, rel=METRIC_REL)
+        bad = {k: e for k, e in errs.items() if not e < GRAD_REL}
+        assert not bad, (lam_rd, bad)
+
+
 # ------------------------------------------------------------------------------------- C2
 def _kodak_meta(golden_dir):
     return json.load(open(os.path.join(golden_dir, "g5_kodak24_synth_n192.json")))

@@ -57,18 +57,19 @@ def layer_flops(N: int, H: int, W: int) -> dict:
     return {k: 2.0 * v for k, v in mac.items()}
 
 
-def layer_bytes(N: int, H: int, W: int) -> dict:
-    """Algorithmic HBM bytes per image of each fused kernel (fp32 NHWC activations read once,
-    written once; weights amortised over the batch and ignored)."""
+def layer_bytes(N: int, H: int, W: int, act: int = 4) -> dict:
+    """Algorithmic HBM bytes per image of each fused kernel (NHWC activations of `act` bytes per
+    element — fp32 4, the bf16 mode 2 — read once and written once, the fp32 image and
+    reconstruction; weights amortised over the batch and ignored)."""
     h1, w1, h2, w2, h3, w3 = H // 4, W // 4, H // 8, W // 8, H // 16, W // 16
     f = 4
     return {
-        "conv1_gdn1": f * (3 * H * W + h1 * w1 * N),
-        "conv2_gdn2": f * (h1 * w1 * N + h2 * w2 * N),
-        "conv3_quant_rate": f * (h2 * w2 * N + h3 * w3 * N),
-        "deconv1_igdn1": f * (h3 * w3 * N + h2 * w2 * N),
-        "deconv2_igdn2": f * (h2 * w2 * N + h1 * w1 * N),
-        "deconv3_clamp": f * (h1 * w1 * N + 3 * H * W),
+        "conv1_gdn1": f * 3 * H * W + act * h1 * w1 * N,
+        "conv2_gdn2": act * (h1 * w1 * N + h2 * w2 * N),
+        "conv3_quant_rate": act * (h2 * w2 * N + h3 * w3 * N),
+        "deconv1_igdn1": act * (h3 * w3 * N + h2 * w2 * N),
+        "deconv2_igdn2": act * (h2 * w2 * N + h1 * w1 * N),
+        "deconv3_clamp": act * h1 * w1 * N + f * 3 * H * W,
         "bits_reduce": 0,
     }
 
@@ -561,7 +562,7 @@ def time_eval(net, x, args, world, dev) -> dict:
 
 def roofline(per_layer_ms: dict, prec: str, N: int, S: int, B: int):
     """(dominant layer, per-layer table, roofline object) of one eval pass."""
-    flops, bytes_ = layer_flops(N, S, S), layer_bytes(N, S, S)
+    flops, bytes_ = layer_flops(N, S, S), layer_bytes(N, S, S, 2 if prec == "bf16" else 4)
     dominant = max(LAYERS, key=lambda k: per_layer_ms[k])
     achieved = flops[dominant] * B / (per_layer_ms[dominant] * 1e-3) / 1e12
     layers = {k: {"ms": round(per_layer_ms[k], 4),
@@ -577,10 +578,25 @@ def roofline(per_layer_ms: dict, prec: str, N: int, S: int, B: int):
     for k in LAYERS:
         if flops[k]:
             layers[k]["frac"] = round(flops[k] * B / (per_layer_ms[k] * 1e-3) / 1e12 / peak, 4)
+    # per-layer T_roof = max(F / P_peak, bytes / BW_peak) and the whole chain's
+    # Σ T_roof / Σ T_measured (P_peak the mode's MFMA peak, BW_peak the HBM peak)
+    t_roof = {}
+    for k in LAYERS:
+        if not flops[k]:
+            continue
+        p = BF16_MFMA_PEAK_TFLOPS if prec == "bf16" else (
+            X6_PEAK_TFLOPS if prec == "x6" and k in X6_LAYERS else FP32_MFMA_PEAK_TFLOPS)
+        t_mfma = flops[k] * B / (p * 1e12) * 1e3
+        t_hbm = bytes_[k] * B / (HBM_PEAK_GBS * 1e9) * 1e3
+        t_roof[k] = max(t_mfma, t_hbm)
+        layers[k]["t_roof_ms"] = round(t_roof[k], 4)
+        layers[k]["roof_bound"] = "mfma" if t_mfma >= t_hbm else "hbm"
+    measured = sum(per_layer_ms[k] for k in t_roof)
     traffic, src = pmc_traffic(dominant, N, S, B, prec)
     roof = {"bound": "mfma", "kernel": dominant, "achieved": round(achieved, 2), "peak": round(peak, 1),
             "unit": "TFLOP/s", "peak_basis": note, "frac": round(achieved / peak, 4),
-            "traffic": traffic, "traffic_source": src if traffic is not None else None}
+            "traffic": traffic, "traffic_source": src if traffic is not None else None,
+            "chain_roofline_frac": round(sum(t_roof.values()) / measured, 4)}
     if traffic is None:
         roof["traffic_null_reason"] = src
     return dominant, layers, roof
@@ -652,7 +668,7 @@ def main() -> None:
     ms_per_step = elapsed / args.steps * 1e3
     x6 = prec == "x6"
     flops = layer_flops(N, S, S)
-    bytes_ = layer_bytes(N, S, S)
+    bytes_ = layer_bytes(N, S, S, 2 if prec == "bf16" else 4)
     dominant, layers, roof = roofline(per_layer_ms, prec, N, S, B)
     total_flops = sum(flops.values()) * B
     result = {
@@ -700,7 +716,8 @@ def main() -> None:
             "value": round(pixels / rb["elapsed"] / 1e6, 2), "unit": "Mpix/s",
             "ms_per_step": round(rb["elapsed"] / args.steps * 1e3, 4), "dtype": "bf16",
             "roofline": {k: roof_b[k] for k in ("kernel", "achieved", "peak", "frac", "traffic",
-                                                  "traffic_source", "traffic_null_reason")
+                                                  "traffic_source", "traffic_null_reason",
+                                                  "chain_roofline_frac")
                          if k in roof_b},
             "layers": layers_b,
             "vs_x6": {"latent_flip_rate": flips / r["y_hat"].numel(),

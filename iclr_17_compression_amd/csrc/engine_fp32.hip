@@ -1121,9 +1121,14 @@ constexpr int D3_PS = D3_BS + 2;                // patch side
 constexpr int D3_PPX = D3_PS * D3_PS;           // 324 patch pixels per plane
 constexpr int D3_NAI = (3 * D3_PPX + 15) / 16;  // 61 A wave-instructions per chunk
 constexpr int D3_SA = D3_NAI * 256;             // A stage floats (976 slots × 16)
-constexpr int D3_SBB = 32 * 48 / 2;             // bf16 B stage floats: [4 k8][48][8] u16 (the bf16 kernel's)
 constexpr int D3_SB6 = 3 * 32 * 48 / 2;         // x6 B stage floats: [3 planes][4 k8][48][8] u16
 constexpr int D3_LDS = D3_SA + 2 * D3_SB6;      // 80,896 B: two workgroups per CU
+
+// first weight block (tile-tap) of tap t in the compact per-chunk weight stage: taps 0-2 touch
+// one column tile, taps 3 and 6 two, the others three (see d3_col)
+__host__ __device__ constexpr int d3_boff(int t) {
+  return t <= 3 ? t : (t == 4 ? 5 : (t == 5 ? 8 : (t == 6 ? 11 : (t == 7 ? 13 : (t == 8 ? 16 : 19)))));
+}
 
 // Column order of the in-loop-split path: logical column j (tile j / 16, lane j % 16) reads packed
 // column co·16 + ry·4 + rx, taking first the 12 columns with ry = 0, then the 9 with rx = 0 < ry,
@@ -1193,26 +1198,38 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
     }
   };
   // B DMA: the weights arrive pre-split (iclr17_split_packed of the ICLR17_W_DECONV9 packing:
-  // [3][9][CI/8][48][8] bf16), so no wave splits them in the loop. The stage [plane][k8][48][8]
-  // holds logical column j (the d3_col order the fragment reads walk) at slot j, so a 16-lane
-  // group reads 16 consecutive 16-byte slots (conflict-free); each lane fetches the packed
-  // column d3_col(j) of its slot. 9 wave-instructions per tap.
+  // [3][9][CI/8][48][8] bf16), so no wave splits them in the loop. A tap stages only the column
+  // tiles it touches (the others hold exact zeros for it, see d3_col): tap t's block is
+  // [plane 3][k8 4][16·ntt(t)][8], slot = logical column (the d3_col order the fragment reads
+  // walk), so a 16-lane group reads 16 consecutive 16-byte slots (conflict-free). The three
+  // one-tile taps (dy = −1) share one step: 7 steps of 9 / 6 / 9 / 9 / 6 / 9 / 9 KB per chunk
+  // instead of 9 of 9 KB, 57 DMA pieces instead of 81 and 7 barriers instead of 9.
   const unsigned short* __restrict__ w6 = (const unsigned short*)a.w;
   constexpr long WPL = 9L * CI * 48;   // u16 per weight plane
-  int bsrc[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const int q = (wave + 4 * k) * 64 + lane;
-    const int pl = q / 192, r = (q / 48) & 3, j = q % 48;
-    bsrc[k] = (int)(pl * WPL) + (r * 48 + d3_col(j)) * 8;
-  }
-  auto issue_b = [&](int s, int buf) {
-    const int cc = s / 9, tap = s - cc * 9;
-    const unsigned short* __restrict__ ws = w6 + ((long)tap * (CI / 8) + cc * 4) * 48 * 8;
+  // taps of step st: st = 0 → taps 0, 1, 2; else tap st + 2
+  auto issue_b = [&](int cc, int st, int buf) {
     float* sb = sB + buf * D3_SB6;
-    glds16((const float*)(ws + bsrc[0]), sb + wave * 256);
-    glds16((const float*)(ws + bsrc[1]), sb + (wave + 4) * 256);
-    if (wave == 0) glds16((const float*)(ws + bsrc[2]), sb + 8 * 256);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int piece = wave + 4 * k;
+      if (piece >= 9 || ((st == 1 || st == 4) && piece >= 6)) break;   // wave-uniform
+      const int slot = piece * 64 + lane;
+      int tap, pl, k8, col;
+      if (st == 0) {
+        tap = slot / 192;
+        const int r = slot - tap * 192;
+        pl = r / 64; k8 = (r >> 4) & 3; col = r & 15;
+      } else {
+        tap = st + 2;
+        const int nc = st == 1 || st == 4 ? 32 : 48;   // 16·ntt
+        pl = slot / (4 * nc);
+        const int r = slot - pl * 4 * nc;
+        k8 = r / nc; col = r - k8 * nc;
+      }
+      const unsigned short* src =
+          w6 + pl * WPL + (((long)tap * (CI / 8) + cc * 4 + k8) * 48 + d3_col(col)) * 8;
+      glds16((const float*)src, sb + piece * 256);
+    }
   };
 
   f4 acc[MT][NT];
@@ -1227,17 +1244,19 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
   for (int nt = 0; nt < NT; ++nt)
     pcol[nt] = d3_col(nt * 16 + (lane & 15));
 
-  auto compute = [&](int buf, int tap, auto ntt) {
+  // tap `tap` from its block at u16 offset `boff` of stage buf: [plane][k8][16·NTT][8]
+  auto compute = [&](int buf, int tap, int boff, auto ntt) {
     constexpr int NTT = decltype(ntt)::value;   // tiles this tap touches
+    constexpr int NC = 16 * NTT;
     const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
-    const unsigned short* sb = (const unsigned short*)(sB + buf * D3_SB6) + g * 48 * 8;
+    const unsigned short* sb = (const unsigned short*)(sB + buf * D3_SB6) + boff + g * NC * 8;
     bf8 Bh[NTT], Bm[NTT], Bl[NTT];
 #pragma unroll
     for (int nt = 0; nt < NTT; ++nt) {
       const int jc = nt * 16 + (lane & 15);
       Bh[nt] = __builtin_bit_cast(bf8, *(const u4*)(sb + jc * 8));
-      Bm[nt] = __builtin_bit_cast(bf8, *(const u4*)(sb + 4 * 48 * 8 + jc * 8));
-      Bl[nt] = __builtin_bit_cast(bf8, *(const u4*)(sb + 8 * 48 * 8 + jc * 8));
+      Bm[nt] = __builtin_bit_cast(bf8, *(const u4*)(sb + 4 * NC * 8 + jc * 8));
+      Bl[nt] = __builtin_bit_cast(bf8, *(const u4*)(sb + 8 * NC * 8 + jc * 8));
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -1261,25 +1280,29 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
   };
 
   issue_a(0);
-  issue_b(0, 0);
-  // taps unrolled inside the chunk loop: each tap's code is specialised (no joins between the
-  // three tile counts, whose register shuffles cost more VALU than the split itself)
+  issue_b(0, 0, 0);
+  // steps unrolled inside the chunk loop: each tap's code is specialised (no joins between the
+  // three tile counts, whose register shuffles cost more VALU than the split itself). The
+  // accumulation order (chunk, tap 0..8) is that of the per-tap schedule.
   for (int cc = 0; cc < NCH; ++cc) {
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int s = cc * 9 + tap;
+    for (int st = 0; st < 7; ++st) {
+      const int s = cc * 7 + st;
       dma_barrier();   // A (at a chunk start) and B of step s landed
-      if (tap != 8) issue_b(s + 1, (s + 1) & 1);
-      if (tap < 3)
-        compute(s & 1, tap, std::integral_constant<int, 1>{});
-      else if (tap == 3 || tap == 6)
-        compute(s & 1, tap, std::integral_constant<int, 2>{});
-      else
-        compute(s & 1, tap, std::integral_constant<int, 3>{});
-      if (tap == 8 && cc + 1 < NCH) {
+      if (st != 6) issue_b(cc, st + 1, (s + 1) & 1);
+      if (st == 0) {
+        compute(s & 1, 0, 0, std::integral_constant<int, 1>{});
+        compute(s & 1, 1, 192 * 8, std::integral_constant<int, 1>{});
+        compute(s & 1, 2, 2 * 192 * 8, std::integral_constant<int, 1>{});
+      } else if (st == 1 || st == 4) {
+        compute(s & 1, st + 2, 0, std::integral_constant<int, 2>{});
+      } else {
+        compute(s & 1, st + 2, 0, std::integral_constant<int, 3>{});
+      }
+      if (st == 6 && cc + 1 < NCH) {
         __syncthreads();   // every wave is done with this chunk's patch
         issue_a(cc + 1);
-        issue_b(s + 1, (s + 1) & 1);
+        issue_b(cc + 1, 0, (s + 1) & 1);
       }
     }
   }
@@ -1481,8 +1504,8 @@ __global__ void __launch_bounds__(512) deconv3_bf16_kernel(const EngineArgs a) {
   constexpr int KCH = 32, NCH = CI / KCH, MT = 2, NT = 3, NW = 8;
   constexpr int NAI = (D3_PPX + 15) / 16;   // 21 patch wave-instructions per chunk (16 px each)
   constexpr int SA = NAI * 256;             // patch buffer floats
-  constexpr int PB = 9 * D3_SBB;            // weight floats per chunk: [tap][k8 4][48][8] bf16
-  constexpr int NBI = PB / 256;             // 27 weight wave-instructions per chunk
+  constexpr int NBI = 19;                   // weight blocks per chunk: the 19 tile-taps
+  constexpr int PB = NBI * 256;             // weight floats per chunk: [block][k8 4][16][8] bf16
   constexpr int KA = (NAI + NW - 1) / NW, KB = (NBI + NW - 1) / NW;
   constexpr int LDS = 2 * SA + 2 * PB;
   static_assert(3 * 64 * 65 + 16 <= LDS, "epilogue block fits");
@@ -1512,14 +1535,18 @@ __global__ void __launch_bounds__(512) deconv3_bf16_kernel(const EngineArgs a) {
     const int g = (lane & 3) ^ (((p >> 2) & 1) << 1);
     asrc[j] = ok ? (iy * a.Win + ix) * CI + g * 8 : -1;
   }
-  // weight DMA (iclr17_round_packed of the ICLR17_W_DECONV9 packing: [9][CI/8][48][8] bf16):
-  // instruction i = tap t (3 per tap), slot (k8, j) ← packed (cc·4 + k8, d3_col(j)), u16 offsets
+  // weight DMA (iclr17_round_packed of the ICLR17_W_DECONV9 packing: [9][CI/8][48][8] bf16): only
+  // the column tiles a tap touches (d3_col; the others are exact zeros for it), one 1 KB block
+  // [k8 4][16][8] per tile-tap, taps in order (1, 1, 1, 2, 3, 3, 2, 3, 3 tiles): 19 KB per chunk
+  // instead of 27. Instruction i = block i, slot (k8, c) ← packed (cc·4 + k8, d3_col(16·tt + c)).
   int bsrc[KB];
 #pragma unroll
   for (int j = 0; j < KB; ++j) {
     const int i = wave + NW * j;
-    const int t = i / 3, w = (i - t * 3) * 64 + lane, k8 = w / 48, jj = w - k8 * 48;
-    bsrc[j] = (t * (CI / 8) * 48 + k8 * 48 + d3_col(jj)) * 8;
+    int t = 0;
+    while (t < 8 && d3_boff(t + 1) <= i) ++t;
+    const int tt = i - d3_boff(t), k8 = lane >> 4, c = lane & 15;
+    bsrc[j] = ((t * (CI / 8) + k8) * 48 + d3_col(16 * tt + c)) * 8;
   }
   const unsigned short* __restrict__ wb = (const unsigned short*)a.w;
   const unsigned short* __restrict__ inb = a.in_split + (long)b * a.Hin * a.Win * CI;
@@ -1548,10 +1575,10 @@ __global__ void __launch_bounds__(512) deconv3_bf16_kernel(const EngineArgs a) {
   auto compute = [&](int buf, int tap, auto ntt) {
     constexpr int NTT = decltype(ntt)::value;   // tiles this tap touches
     const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
-    const u4* sb = (const u4*)(sB + buf * PB + tap * D3_SBB) + g * 48;
+    const u4* sb = (const u4*)(sB + buf * PB + d3_boff(tap) * 256) + g * 16 + (lane & 15);
     bf8 Bb[NTT];
 #pragma unroll
-    for (int nt = 0; nt < NTT; ++nt) Bb[nt] = __builtin_bit_cast(bf8, sb[nt * 16 + (lane & 15)]);
+    for (int nt = 0; nt < NTT; ++nt) Bb[nt] = __builtin_bit_cast(bf8, sb[nt * 64]);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const int p = prow + (mt + dy) * D3_PS + dx;

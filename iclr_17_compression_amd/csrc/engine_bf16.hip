@@ -581,7 +581,7 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
 }
 
 template <int MODE, int TH, int NB, int CO, int CI, int EPI>
-__global__ void __launch_bounds__(TH / 2 * 64)
+__global__ void __launch_bounds__(TH / 2 * 64, TH == 8 ? 2 : 1)   // 8-row tiles: two per CU
 k5_bf16_kernel(const K5Args a) {
   using KK = K5<MODE, TH, NB, CO, CI, EPI>;
   __shared__ __attribute__((aligned(16))) unsigned char smem[KK::LDS];

@@ -534,12 +534,23 @@ def time_eval(net, x, args, world, dev) -> dict:
         for _ in range(args.warmup):
             step()
         torch.cuda.synchronize()
+        run = step
+        if args.graph:
+            # the step's launches captured once into a HIP graph (torch.cuda.CUDAGraph on ROCm):
+            # each replay submits the whole chain at once (no per-kernel host launch, shorter
+            # gaps between dependent kernels); outputs land in the graph's own memory pool
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                step()
+            graph.replay()
+            torch.cuda.synchronize()
+            run = graph.replay
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            step()
+            run()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -622,6 +633,9 @@ def main() -> None:
     ap.add_argument("--prefetch", type=int, default=4)
     ap.add_argument("--no-bf16-leg", action="store_true",
                     help="x6 eval: skip the bf16 throughput-mode leg reported as bf16_mode")
+    ap.add_argument("--graph", action="store_true",
+                    help="eval: replay the timed steps from one HIP graph instead of launching them "
+                         "kernel by kernel (x6: 4 % slower, bf16: 1.4 % faster; DESIGN §5)")
     ap.add_argument("--mode", choices=("eval", "train", "kodak", "codec"), default="eval")
     ap.add_argument("--precision", choices=kernels.PRECISIONS, default=None,
                     help="inference contraction mode (default: ICLR17_PRECISION or x6)")
@@ -692,7 +706,8 @@ def main() -> None:
                                 if x6 else ("bf16: bf16 activations and weights, one bf16 product "
                                             "per MAC, fp32 accumulate and epilogues" if prec == "bf16"
                                             else "fp32 (exact-f32 MFMA products)"),
-                   "parallelism": f"dp{world} (images sharded by rank, no data-path collective)"},
+                   "parallelism": f"dp{world} (images sharded by rank, no data-path collective)",
+                   "launch": "hipGraph replay of the whole step" if args.graph else "eager (kernel by kernel)"},
         "roofline": {**roof, "algorithmic_bytes_per_launch": bytes_[dominant] * B,
                      "flop_per_launch": flops[dominant] * B,
                      "whole_step_tflops": round(total_flops / (ms_per_step * 1e-3) / 1e12, 2)},

@@ -36,6 +36,9 @@ namespace bfm {
 #ifndef ICLR17_BF_DECONV16
 #define ICLR17_BF_DECONV16 1
 #endif
+#ifndef ICLR17_BF_C3KS
+#define ICLR17_BF_C3KS 2   // conv3: input-channel halves per tile, one 4-wave group each
+#endif
 #ifndef ICLR17_BF_NST
 #define ICLR17_BF_NST 4   // weight ring stages (F + 2 for F DMA groups in flight)
 #endif
@@ -266,12 +269,21 @@ __device__ __forceinline__ void gdn_epilogue_bf16(f4 (&acc)[NT][MT], unsigned ch
 // rows 2w and 2w + 1 and all NB channels: NB / 32 accumulators of v_mfma_f32_32x32x16_bf16,
 // C[channel][pixel]. The 32×32 tile leaves 24 of every 32 issue cycles beside the MFMA (the
 // 16×16×32 form leaves 8 of 16), room for the fragment reads and the DMA issue of a step.
+// conv3 (the quantiser epilogue) splits K: KS groups of TH / 2 waves in one workgroup each run
+// the whole main loop on their share of the input channels with their own patch buffers and
+// weight ring (the groups' barriers line up: equal step counts), then group 0 adds the other
+// groups' accumulators from LDS in a fixed order and runs the epilogue. conv3's 256 tiles at B=64
+// otherwise hold one wave per SIMD.
+constexpr int k5_threads(int TH, int EPI) { return TH / 2 * 64 * (EPI == BE_QUANT ? ICLR17_BF_C3KS : 1); }
+
 template <int MODE, int TH, int NB, int CO, int CI, int EPI>
 struct K5 {
-  static constexpr int NW = TH / 2, NT_ = NW * 64;
+  static constexpr int KS = EPI == BE_QUANT ? ICLR17_BF_C3KS : 1;   // K-split groups
+  static_assert(k5_threads(TH, EPI) == KS * (TH / 2) * 64, "threads");
+  static constexpr int NW = TH / 2, NT_ = NW * 64;   // waves / threads of one group
   static constexpr int NT = NB / 32;            // 32-channel accumulator tiles per wave
   static constexpr int R = TH * 16;             // pixels per tile
-  static constexpr int NCH = CI / 16;           // 16-channel chunks
+  static constexpr int NCH = CI / 16 / KS;      // 16-channel chunks per group
   static constexpr int SB = 4 * NB * 16;        // weight stage bytes
   static constexpr int NBI = SB / 1024;         // weight DMA wave-instructions per step
   using P = Patch<MODE, TH>;
@@ -285,8 +297,9 @@ struct K5 {
   static constexpr int GOFF = EARLY_G ? MAIN_LDS : 0;
   static constexpr int EPI_LDS = EPI == BE_QUANT ? 64
                                  : (GOFF + GBLK * 1024 > R * OS ? GOFF + GBLK * 1024 : R * OS);
-  static constexpr int LDS = MAIN_LDS > EPI_LDS ? MAIN_LDS : EPI_LDS;
-  static_assert(TH % 2 == 0 && NB % 32 == 0 && SB % 1024 == 0, "tile shape");
+  static constexpr int LDS = KS * MAIN_LDS > EPI_LDS ? KS * MAIN_LDS : EPI_LDS;
+  static_assert(KS == 1 || (KS - 1) * NW * NT * 16 * 64 * 4 <= KS * MAIN_LDS, "K-split exchange");
+  static_assert(TH % 2 == 0 && NB % 32 == 0 && SB % 1024 == 0 && CI % (16 * KS) == 0, "tile shape");
   static_assert(EPI == BE_QUANT || NB == CO, "GDN needs every channel of a pixel in the tile");
 };
 
@@ -299,7 +312,9 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
   constexpr int NT = KK::NT, NW = KK::NW, S = TP::S, NCH = KK::NCH;
   constexpr int SB = KK::SB, NBI = KK::NBI;
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kg = wv / NW, wave = wv - kg * NW;   // K-split group, wave within the group
+  unsigned char* const gsmem = smem + kg * KK::MAIN_LDS;
   const int r32 = lane & 31, h = lane >> 5;
   // LDS-DMA schedule. Every step every wave issues exactly K DMA instructions (weights of step
   // g+F+1 into a four-stage ring, pieces of the next chunk's patch, 1 KB sink loads as padding),
@@ -314,13 +329,13 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
   constexpr int PS = (P::NQI + SI - 1) / SI;          // patch pieces per issuing step
   constexpr int K = (NBI + PS + NW - 1) / NW;         // DMA instructions per wave per step
   constexpr int GS = NCH * S;                         // steps
-  unsigned char* const sP = smem;                     // two patch buffers
-  unsigned char* const sB = smem + 2 * P::BUF;        // NST weight stages
+  unsigned char* const sP = gsmem;                    // two patch buffers
+  unsigned char* const sB = gsmem + 2 * P::BUF;       // NST weight stages
   unsigned char* const sD = sB + NST * SB;            // 1 KB sink of the padding loads
   const long img = (long)b * a.Hin * a.Win;
   const int iy0 = MODE == BM_CONV ? 2 * ty * TH - 2 : ty * TH - 1;
   const int ix0 = MODE == BM_CONV ? 2 * tx * 16 - 2 : tx * 16 - 1;
-  const u16* __restrict__ inb = a.in + img * CI;
+  const u16* __restrict__ inb = a.in + img * CI + kg * (CI / KK::KS);
   // patch piece (wave-instruction) `piece`: this lane's 16-byte slot → source u16 offset or -1
   auto piece_src = [&](int piece) -> int {
     const int byte = (piece * 64 + lane) * 16;
@@ -356,8 +371,8 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
     const int g = q / NB, col = q - g * NB;
     wsrc[k] = (g * CO + nb * NB + col) * 8;
   }
-  // packed weights of this phase: [NCH][S][4][CO][8]
-  const u16* __restrict__ wph = a.w;
+  // packed weights of this phase: [NCH·KS][S][4][CO][8]; K-split group kg starts at chunk kg·NCH
+  const u16* __restrict__ wph = a.w + (long)kg * NCH * S * wstep;
   if (MODE == BM_DECONV) {
     long off = 0;
 #pragma unroll
@@ -545,9 +560,30 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
     }
   } else {
     static_assert(EPI == BE_QUANT, "epilogue");
+    if constexpr (KK::KS > 1) {
+      // K-split: groups 1 .. KS−1 hand their accumulators to group 0 through LDS (the main-loop
+      // buffers are free after the trailing vm_barrier), which adds them in group order
+      float* xs = (float*)smem;   // [group − 1][wave][tile][16][lane]
+      if (kg > 0) {
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+#pragma unroll
+          for (int j = 0; j < 16; ++j) xs[((((kg - 1) * NW + wave) * NT + i) * 16 + j) * 64 + lane] = acc[i][j];
+      }
+      __syncthreads();
+      if (kg == 0) {
+#pragma unroll
+        for (int g = 1; g < KK::KS; ++g)
+#pragma unroll
+          for (int i = 0; i < NT; ++i)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) acc[i][j] += xs[((((g - 1) * NW + wave) * NT + i) * 16 + j) * 64 + lane];
+      }
+      __syncthreads();   // exchange reads done before red[] reuses the area
+    }
     // conv3 + model.py:56 round (half to even) + model.py:71-73 rate, per element
     float bits = 0.f;
-    if (o >= 0) {
+    if (o >= 0 && kg == 0) {
 #pragma unroll
       for (int i = 0; i < NT; ++i)
 #pragma unroll
@@ -569,7 +605,7 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
     }
     bits = wave_sum(bits);
     float* red = (float*)smem;
-    if (lane == 0) red[wave] = bits;
+    if (lane == 0 && kg == 0) red[wave] = bits;
     __syncthreads();
     if (tid == 0) {
       double sum = 0.0;
@@ -581,7 +617,7 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
 }
 
 template <int MODE, int TH, int NB, int CO, int CI, int EPI>
-__global__ void __launch_bounds__(TH / 2 * 64, TH == 8 ? 2 : 1)   // 8-row tiles: two per CU
+__global__ void __launch_bounds__(k5_threads(TH, EPI), (TH == 8 && EPI != BE_QUANT) ? 2 : 1)   // 8-row deconv tiles: two per CU
 k5_bf16_kernel(const K5Args a) {
   using KK = K5<MODE, TH, NB, CO, CI, EPI>;
   __shared__ __attribute__((aligned(16))) unsigned char smem[KK::LDS];
@@ -834,7 +870,7 @@ int launch_conv3(const K5Args& a0, hipStream_t st) {
   constexpr int NB = N / 2;
   a.ppi = a.tiles_x * a.tiles_y * 2;
   hipLaunchKernelGGL((k5_bf16_kernel<BM_CONV, 8, NB, N, N, BE_QUANT>),
-                     dim3(a.tiles_x * a.tiles_y * a.B, 2), dim3(256), 0, st, a);
+                     dim3(a.tiles_x * a.tiles_y * a.B, 2), dim3(k5_threads(8, BE_QUANT)), 0, st, a);
   return check_launch("conv3_quant_rate_bf16");
 }
 

@@ -649,9 +649,19 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU over RCCL ("nccl"). ICLR17_DIST_BACKEND=gloo rehearses the multi-rank
+    # path with several ranks sharing the GPUs there are (device = local rank mod device count)
+    backend = os.environ.get("ICLR17_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and world > 1 and local >= ndev:
+        raise SystemExit(f"bench: LOCAL_RANK {local} but only {ndev} GPUs (one process per GPU)")
+    local = local % max(ndev, 1)
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
 
     if args.mode in ("kodak", "codec"):

@@ -37,6 +37,10 @@ namespace iclr17 {
 
 constexpr int BM = 64;        // output pixels per tile
 
+#ifndef ICLR17_X6_HALO
+#define ICLR17_X6_HALO 1   // x6 deconv1/deconv2: halo-patch A operand, chunk-major steps
+#endif
+
 // conv3 (+ quantiser) output columns per workgroup: 96 at N = 192, 64 at N = 128
 constexpr int conv3_bn(int N) { return N % 96 == 0 ? 96 : 64; }
 
@@ -879,7 +883,12 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   constexpr int API = BMT / 16;                  // x6: A wave-instructions per plane (16 rows each)
   // DMA ring depth: conv3 (+ quantiser) has a third of conv2's MFMAs per step, too few to hide
   // an L2-miss DMA issued one step ahead, so it runs NS stages with a counted vmcnt wait.
-  constexpr int LDS_A = 2 * STAGE;   // two-stage ring (3, 4 stages measured slower: DESIGN.md §5)
+  // x6 IGDN layers (deconv1 / deconv2): halo-patch A operand (see the main loop)
+  constexpr bool HALO = X6 && EPI == EPI_IGDN && BMT == BM && ICLR17_X6_HALO;
+  constexpr int HALO_NI = (3 * 100 * 64 + 1023) / 1024;   // patch DMA wave-instructions (19)
+  constexpr int HALO_PF = HALO_NI * 256;                  // patch floats
+  constexpr int LDS_A = HALO ? HALO_PF + 2 * SB
+                             : 2 * STAGE;   // two-stage ring (3, 4 stages measured slower: DESIGN.md §5)
   constexpr int LDS_XF = BMT * (CO + 8) + GSTAGE_FLOATS(CO);
   constexpr int LDS_XP = gdn_lds_floats(BMT, CO, X6);
   constexpr int LDS_X = (EPI == EPI_GDN || EPI == EPI_IGDN) ? (LDS_XF > LDS_XP ? LDS_XF : LDS_XP)
@@ -1043,11 +1052,105 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
 
-  issue(0, 0);
-  for (int s = 0; s < nsteps; ++s) {
-    dma_barrier();   // step s landed for every wave; stage (s+1)&1 is free
-    if (s + 1 < nsteps) issue(s + 1, (s + 1) & 1);
-    compute(s & 1);
+  if constexpr (HALO) {
+    // x6 deconv (IGDN layers, input stride 1, taps dy, dx ∈ {−1, 0, 1}): chunk-major steps. The
+    // 10×10 input patch of the 8×8 base tile (three bf16 planes, 64 bytes per pixel, 19 KB) is
+    // staged ONCE per 32-channel chunk and every tap reads its shifted window from it, instead
+    // of each (tap, chunk) step DMA-ing its own 64 rows again (100 vs 64·taps staged pixels).
+    // The patch is single-buffered (the chunk boundary is a barrier-bounded refill that the
+    // co-resident workgroup covers); the weight stages stay double-buffered. 16-byte piece g of
+    // patch pixel q sits at g ^ 2·((q / 10) & 1): conflict-free ds_read_b128 lane groups for every
+    // tap offset (checked exhaustively).
+    unsigned short* const sp = (unsigned short*)smem;
+    float* const sbw = smem + HALO_PF;
+    const int gy0 = t.ty * 8 - 1, gx0 = t.tx * 8 - 1;   // patch origin (input coordinates)
+    auto issue_patch = [&](int cc) {
+#pragma unroll
+      for (int j = 0; j < (HALO_NI + 3) / 4; ++j) {
+        const int i = wave + 4 * j;
+        if (i >= HALO_NI) break;   // wave-uniform
+        const int qq = 16 * i + (lane >> 2);            // plane · 100 + patch pixel
+        const int pl = qq / 100, q = qq - pl * 100;
+        const int iy = gy0 + q / 10, ix = gx0 + q % 10;
+        const bool ok = pl < 3 && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
+        const int g = (lane & 3) ^ (2 * ((q / 10) & 1));
+        const unsigned short* src =
+            inb6 + (long)(pl < 3 ? pl : 0) * a.in_plane + ((long)iy * a.Win + ix) * CI + cc * KCH + g * 8;
+        glds16(ok ? (const float*)src : g_zero16, (float*)sp + i * 256);
+      }
+    };
+    auto issue_b = [&](int s, int buf) {   // weights of step s = (chunk, tap) into stage buf
+      const int cc = s / ntaps, tap = t0 + (s - cc * ntaps);
+      float* sb = sbw + buf * SB;
+      const float* __restrict__ ws = a.w + ((long)tap * CI + cc * KCH) * CO;
+#pragma unroll
+      for (int j = 0; j < BI_W; ++j) {
+        const int i = wave + NWV * j;
+        if (NBI % NWV == 0 || i < NBI) glds16(ws + bsrc[j], sb + i * 256);
+      }
+    };
+    // tile pixel of fragment row mt: (ty, tx) = (r >> 3, r & 7); patch pixel at tap (0, 0)
+    int hq[MT], hy[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int r = wm * MT * 16 + mt * 16 + (lane & 15);
+      hy[mt] = (r >> 3) + 1;
+      hq[mt] = hy[mt] * 10 + (r & 7) + 1;
+    }
+    auto compute_halo = [&](int buf, int dy, int dx) {
+      const float* sb = sbw + buf * SB + boff6;
+      bf8 Bh[NT], Bm[NT], Bl[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        u4 bh, bm, bl;
+        split8(*(const f4*)(sb + nt * 64), *(const f4*)(sb + BN * 4 + nt * 64), bh, bm, bl);
+        Bh[nt] = __builtin_bit_cast(bf8, bh);
+        Bm[nt] = __builtin_bit_cast(bf8, bm);
+        Bl[nt] = __builtin_bit_cast(bf8, bl);
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int q = hq[mt] + dy * 10 + dx;
+        const int g = (lane >> 4) ^ (2 * ((hy[mt] + dy) & 1));
+        const unsigned short* pa = sp + q * 32 + g * 8;
+        const bf8 Ah = __builtin_bit_cast(bf8, *(const u4*)(pa));
+        const bf8 Am = __builtin_bit_cast(bf8, *(const u4*)(pa + 100 * 32));
+        const bf8 Al = __builtin_bit_cast(bf8, *(const u4*)(pa + 200 * 32));
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          f4 c = acc[mt][nt];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al, Bh[nt], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bl[nt], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bm[nt], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bh[nt], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bm[nt], c, 0, 0, 0);
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bh[nt], c, 0, 0, 0);
+        }
+      }
+    };
+    issue_patch(0);
+    issue_b(0, 0);
+    for (int cc = 0; cc < NCH; ++cc) {
+      for (int k = 0; k < ntaps; ++k) {
+        const int s = cc * ntaps + k;
+        dma_barrier();   // weights of step s landed (and, at k = 0, chunk cc's patch)
+        if (k + 1 < ntaps) issue_b(s + 1, (s + 1) & 1);
+        const int td = a.tt.dydx[t0 + k];
+        compute_halo(s & 1, (td & 0xff) - 128, ((td >> 8) & 0xff) - 128);
+        if (k + 1 == ntaps && cc + 1 < NCH) {
+          __syncthreads();   // every wave is done with this chunk's patch
+          issue_patch(cc + 1);
+          issue_b(s + 1, (s + 1) & 1);
+        }
+      }
+    }
+  } else {
+    issue(0, 0);
+    for (int s = 0; s < nsteps; ++s) {
+      dma_barrier();   // step s landed for every wave; stage (s+1)&1 is free
+      if (s + 1 < nsteps) issue(s + 1, (s + 1) & 1);
+      compute(s & 1);
+    }
   }
   __syncthreads();     // last stage reads done before the epilogue reuses LDS
 

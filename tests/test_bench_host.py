@@ -56,3 +56,26 @@ def test_roofline_object(prec, kernel_peak, tmp_path, monkeypatch):
     assert roof["achieved"] == pytest.approx(flops / 0.2e-3 / 1e12, rel=1e-3)
     assert roof["frac"] == pytest.approx(roof["achieved"] / kernel_peak, rel=1e-3)
     assert roof["traffic"] is None and roof["traffic_null_reason"]
+
+
+def test_chain_roofline(tmp_path, monkeypatch):
+    """per-layer T_roof = max(F / P_peak, bytes / 8 TB/s) and the chain's
+    Σ T_roof / Σ T; in the bf16 mode activations are 2 bytes, which makes conv1 and deconv3
+    HBM-bound; at measured times equal to T_roof the chain fraction is 1."""
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    N, S, B = 192, 256, 64
+    fl = bench.layer_flops(N, S, S)
+    for prec, act, peak in (("x6", 4, bench.X6_PEAK_TFLOPS), ("bf16", 2, bench.BF16_MFMA_PEAK_TFLOPS)):
+        by = bench.layer_bytes(N, S, S, act)
+        roof_ms = {k: max(fl[k] * B / (peak * 1e12), by[k] * B / (bench.HBM_PEAK_GBS * 1e9)) * 1e3
+                   if fl[k] else 0.01 for k in bench.LAYERS}
+        _, layers, roof = bench.roofline(roof_ms, prec, N, S, B)
+        assert roof["chain_roofline_frac"] == pytest.approx(1.0, rel=1e-3)
+        _, layers2, roof2 = bench.roofline({k: 2 * v for k, v in roof_ms.items()}, prec, N, S, B)
+        assert roof2["chain_roofline_frac"] == pytest.approx(0.5, rel=1e-3)
+        bounds = {k: v.get("roof_bound") for k, v in layers.items() if fl[k]}
+        if prec == "x6":
+            assert set(bounds.values()) == {"mfma"}
+        else:
+            assert bounds["conv1_gdn1"] == "hbm" and bounds["deconv3_clamp"] == "hbm"
+            assert bounds["conv2_gdn2"] == "mfma" and bounds["deconv2_igdn2"] == "mfma"

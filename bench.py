@@ -227,6 +227,7 @@ def run_train(args, net, x, world, dev):
     torch.cuda.synchronize()
     elapsed = idist.max_over_ranks(time.perf_counter() - t0, dev)
     ms = elapsed / args.steps * 1e3
+    comm = allreduce_overlap(args, net, params, reducer, step, ms, dev) if world > 1 else None
     if loader is not None:
         loader.close()
         data_info["step_crops_per_s"] = round(B * args.steps / elapsed, 1)
@@ -255,7 +256,55 @@ def run_train(args, net, x, world, dev):
                      "flop_per_step": flops},
         "bpp_last": round(bpp.item(), 6),
         **({"data_path": data_info} if data_info else {}),
+        **({"allreduce": comm} if comm else {}),
     }
+
+
+def _timed_loop(fn, steps: int, dev) -> float:
+    """ms per call of fn over `steps` calls, barrier + synchronize brackets, max over ranks."""
+    from iclr_17_compression_amd import dist as idist
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    return idist.max_over_ranks(time.perf_counter() - t0, dev) / steps * 1e3
+
+
+def allreduce_overlap(args, net, params, reducer, step, step_ms: float, dev) -> dict:
+    """C4: how much of the gradient all-reduce the backward hides. Measured after the timed
+    region, over as many steps: (1) the bucketed all-reduce of one step's gradients alone
+    (the reducer's own buckets, nothing else running), (2) the same training step with the
+    reducer detached (no all-reduce: each rank keeps its own gradient). exposed = step −
+    no-all-reduce step; overlapped fraction = 1 − exposed / all-reduce time."""
+    keys = [torch.zeros_like(p) for p in params]   # stand-ins with no .grad of their own
+    grads = [torch.ones_like(p) for p in params]
+
+    def ar_only():
+        reducer.launch(keys, grads)
+        reducer.wait()
+
+    ar_ms = _timed_loop(ar_only, args.steps, dev)
+    net._grad_reducer = None
+    reducer_finish = reducer.finish
+    reducer.finish = lambda: None
+    try:
+        local_ms = _timed_loop(step, args.steps, dev)
+    finally:
+        reducer.finish = reducer_finish
+        reducer.attach(net)
+    exposed = max(0.0, step_ms - local_ms)
+    return {"bucket_mb": reducer.bucket_bytes / 2 ** 20,
+            "grad_bytes": sum(p.numel() * 4 for p in params),
+            "allreduce_alone_ms": round(ar_ms, 4), "step_without_allreduce_ms": round(local_ms, 4),
+            "exposed_ms": round(exposed, 4),
+            "overlapped_fraction": round(min(1.0, max(0.0, 1.0 - exposed / ar_ms)), 4) if ar_ms > 0 else None,
+            "method": "all-reduce alone and the step without it, timed after the timed region "
+                      "over as many steps (barrier + synchronize brackets, max over ranks)"}
 
 
 def make_train_dir(spec: str, rank: int):
@@ -519,10 +568,10 @@ def pmc_traffic(layer: str, N: int, S: int, B: int, prec: str):
         e = d.get("layers", {}).get(layer, {})
         if d.get("lib_sha256") == sha and "traffic_bytes" in e:
             return e["traffic_bytes"], (f"profiles/{os.path.basename(f)} (lib {sha}, kernel "
-                                        f"{e.get('kernel')}, trace mean {e.get('mean_ms', 0):.4f} ms)")
+                                        f"{e.get('kernel')}, trace mean {e.get('mean_ms', 0):.4f} ms)"), e.get("mean_ms")
     why = (f"no PMC summary of this build (lib {sha}) for {prec} {layer} at N={N} S={S} B={B}"
            + (f"; summaries of other builds: {', '.join(seen[:3])}" if seen else ""))
-    return None, why
+    return None, why, None
 
 
 def time_eval(net, x, args, world, dev) -> dict:
@@ -603,14 +652,88 @@ def roofline(per_layer_ms: dict, prec: str, N: int, S: int, B: int):
         layers[k]["t_roof_ms"] = round(t_roof[k], 4)
         layers[k]["roof_bound"] = "mfma" if t_mfma >= t_hbm else "hbm"
     measured = sum(per_layer_ms[k] for k in t_roof)
-    traffic, src = pmc_traffic(dominant, N, S, B, prec)
+    traffic, src, prof_ms = pmc_traffic(dominant, N, S, B, prec)
     roof = {"bound": "mfma", "kernel": dominant, "achieved": round(achieved, 2), "peak": round(peak, 1),
             "unit": "TFLOP/s", "peak_basis": note, "frac": round(achieved / peak, 4),
+            "duration": "hip_events: mean over the K steps on the launching stream "
+                        f"({per_layer_ms[dominant]:.4f} ms)",
+            "frac_of_bf16_dense_peak": round(achieved / BF16_MFMA_PEAK_TFLOPS, 4),
             "traffic": traffic, "traffic_source": src if traffic is not None else None,
             "chain_roofline_frac": round(sum(t_roof.values()) / measured, 4)}
+    if prof_ms:   # the SHA-matched rocprof trace mean of the same kernel, and the fraction it gives
+        roof["profile_mean_ms"] = round(prof_ms, 4)
+        roof["frac_from_profile"] = round(flops[dominant] * B / (prof_ms * 1e-3) / 1e12 / peak, 4)
     if traffic is None:
         roof["traffic_null_reason"] = src
     return dominant, layers, roof
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv) -> int:
+    """`python bench.py --gpus N` without torchrun: start N fresh interpreters, one per GPU (rank r
+    on GPU r), with torchrun's environment (RANK / LOCAL_RANK / WORLD_SIZE, MASTER_ADDR
+    127.0.0.1, a free MASTER_PORT). The parent has made no HIP call: it only waits, forwards the
+    children's output (rank 0 prints the JSON line) and returns the first failing exit status,
+    ending the other ranks when one fails."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    while procs:
+        time.sleep(0.2)
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                print(f"bench: a rank exited with status {code}; stopping the others",
+                      file=sys.stderr, flush=True)
+                for q in procs:
+                    q.terminate()
+    return rc if rc >= 0 else 1
+
+
+def check_world(args, world: int, backend: str, ndev: int) -> None:
+    """--gpus must be the process count, and (RCCL) one process per visible GPU."""
+    if world > 1 and args.gpus != world:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE {world}")
+    if backend == "nccl" and not args.dry_run and args.gpus > ndev:
+        raise SystemExit(f"bench: --gpus {args.gpus} but only {ndev} GPUs are visible "
+                         "(one process per GPU over RCCL)")
+
+
+def rank_layout(dev, backend: str) -> dict:
+    """Per-rank device ids (all-gathered) and the RCCL communicator's size, for the JSON line."""
+    world = idist_world()
+    mine = dev.index if dev.type == "cuda" else -1
+    ids = [mine]
+    if world > 1:
+        t = torch.tensor([mine], dtype=torch.int64, device=dev)
+        out = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(out, t)
+        ids = [int(o.item()) for o in out]
+    return {"dist_backend": backend if world > 1 else None,
+            "rccl_world_size": world if (world > 1 and backend == "nccl") else None,
+            "rank_devices": ids}
+
+
+def idist_world() -> int:
+    return dist.get_world_size() if dist.is_initialized() else 1
 
 
 def main() -> None:
@@ -619,6 +742,12 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=64, help="images per GPU")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="strong scaling: images over all GPUs, split evenly by rank (C5: 64 at "
+                         "--size 2048); overrides --batch")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch, rendezvous, barrier and max-over-ranks only (no kernels): checks "
+                         "the multi-rank plumbing on a host without a GPU")
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--N", type=int, default=192)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
@@ -646,23 +775,53 @@ def main() -> None:
     if args.precision:
         kernels.set_precision(args.precision)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU over RCCL ("nccl"). ICLR17_DIST_BACKEND=gloo rehearses the multi-rank
     # path with several ranks sharing the GPUs there are (device = local rank mod device count)
     backend = os.environ.get("ICLR17_DIST_BACKEND", "nccl")
-    ndev = torch.cuda.device_count()
+    ndev = torch.cuda.device_count()   # counts devices without initialising HIP on this image
+    if "WORLD_SIZE" not in os.environ:
+        check_world(args, 1, backend, ndev)
+        if args.gpus > 1:   # no torchrun: start the N ranks here, before any HIP call
+            raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    check_world(args, world, backend, ndev)
     if backend == "nccl" and world > 1 and local >= ndev:
         raise SystemExit(f"bench: LOCAL_RANK {local} but only {ndev} GPUs (one process per GPU)")
     local = local % max(ndev, 1)
+    if args.dry_run:
+        dev = torch.device("cuda", local) if ndev else torch.device("cpu")
+    else:
+        dev = torch.device("cuda", local)
     if world > 1:
-        torch.cuda.set_device(local)
+        if dev.type == "cuda":
+            torch.cuda.set_device(local)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
-    dev = torch.device("cuda", local)
+    layout = rank_layout(dev, backend)
+    if args.global_batch:
+        if args.global_batch % world:
+            raise SystemExit(f"bench: --global-batch {args.global_batch} is not a multiple of {world} ranks")
+        args.batch = args.global_batch // world
+    if args.dry_run:
+        from iclr_17_compression_amd import dist as idist
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        if world > 1:
+            dist.barrier()
+        elapsed = idist.max_over_ranks(time.perf_counter() - t0, dev)
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "batch_per_gpu": args.batch,
+                              "global_batch": args.batch * world,
+                              "scaling": "strong" if args.global_batch else "weak",
+                              "barrier_s": elapsed, **layout}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     if args.mode in ("kodak", "codec"):
         if rank == 0:
@@ -677,8 +836,11 @@ def main() -> None:
     x = torch.from_numpy(synth.to_unit_float(synth.image_u8(1000 + rank, B, S, S))).to(dev)
     if args.mode == "train":
         result = run_train(args, net, x, world, dev)
+        result.update(layout)
+        if args.global_batch:
+            result["scaling"] = "strong"
         if rank == 0 and world == 1 and not args.no_cpu_baseline:   # the CPU leg: N=1 only
-            result["cpu_baseline"] = cpu_baseline_train(N, S, args.cpu_budget)
+            result["cpu_baseline"] = cpu_baseline_train(N, min(S, 256), args.cpu_budget)
         if rank == 0:
             print(json.dumps(result), flush=True)
         if world > 1:
@@ -704,11 +866,14 @@ def main() -> None:
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.global_batch else "weak",
         "vs_baseline": None,
         "dtype": "bf16" if prec == "bf16" else "f32",
         "data": "synthetic (splitmix64 uint8/255 images, seeded trained-like weights)",
-        "config": {"workload": f"eval encode+decode (round quantiser + rate), {B} x {S}x{S}x3 images per GPU, N={N}",
+        **layout,
+        "config": {"workload": (f"eval encode+decode (round quantiser + rate), {B} x {S}x{S}x3 images per GPU"
+                                + (f" ({args.global_batch} over {world} GPUs)" if args.global_batch else "")
+                                + f", N={N}"),
                    "N": N, "image": f"{S}x{S}x3", "batch_per_gpu": B, "global_batch": B * world,
                    "quant": "round",
                    "precision": ("x6: fp32 operands split exactly into 3 bf16 parts, 6 part products "
@@ -750,7 +915,8 @@ def main() -> None:
                       "max_abs_dpsnr_db_per_image": float((psnr(rb["clipped"]) - psnr(r["clipped"])).abs().max())},
         }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:   # the CPU leg: N=1 only
-        result["cpu_baseline"] = cpu_baseline(N, S, S, args.cpu_budget)
+        # per-pixel cost is size-independent: the sample is 256² images at any --size
+        result["cpu_baseline"] = cpu_baseline(N, min(S, 256), min(S, 256), args.cpu_budget)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

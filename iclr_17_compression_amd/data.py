@@ -174,6 +174,11 @@ class TrainLoader:
                  cache: bool = True, cache_bytes: int = 64 << 30):
         if not paths:
             raise FileNotFoundError("TrainLoader: no images")
+        if world > 1 and len(paths) < batch * world:
+            # every rank runs the same step count, and a partial global batch is dropped: fewer
+            # images than one global batch would give zero steps per epoch
+            raise ValueError(f"TrainLoader: {len(paths)} images are fewer than one global batch "
+                             f"({batch} x {world} ranks)")
         self.paths, self.batch, self.size, self.seed = list(paths), batch, size, seed
         self.device, self.rank, self.world = device, rank, world
         self.prefetch = max(1, prefetch)

@@ -137,6 +137,12 @@ class GradAllReducer:
     def launch(self, params: Sequence[Tensor], grads: Sequence[Optional[Tensor]]) -> None:
         """All-reduce (sum, async) these parameters' freshly computed gradients."""
         pairs = [(p, g) for p, g in zip(params, grads) if g is not None and id(p) not in self.launched]
+        for p, g in pairs:
+            if p.grad is not None and p.grad is not g:
+                # finish() replaces p.grad with the average of g: a value p.grad already holds
+                # (zero_grad without set_to_none, gradient accumulation) would be lost
+                raise RuntimeError("GradAllReducer.launch: p.grad already holds a gradient; call "
+                                   "zero_grad(set_to_none=True) before the backward")
         for bucket in bucketize([g for _, g in pairs], self.bucket_bytes):
             ids = {id(g) for g in bucket}
             ps = [p for p, g in pairs if id(g) in ids]
@@ -144,6 +150,14 @@ class GradAllReducer:
             work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, async_op=True)
             self.pending.append((work, flat, ps))
             self.launched.update(id(p) for p in ps)
+
+    def wait(self) -> None:
+        """Make the compute stream wait for every launched reduction and drop the results (the
+        bench's all-reduce-alone timing)."""
+        for work, _, _ in self.pending:
+            work.wait()
+        self.pending.clear()
+        self.launched.clear()
 
     def finish(self) -> None:
         """Wait for the reductions (stream-ordered) and set p.grad = the rank average. Gradients
@@ -156,6 +170,8 @@ class GradAllReducer:
             self.launch(rest, [p.grad for p in rest])
         for work, flat, ps in self.pending:
             work.wait()
+            if any(p.grad is None for p in ps):
+                raise RuntimeError("GradAllReducer.finish: a launched parameter has no .grad")
             flat.mul_(1.0 / w)
             off = 0
             for p in ps:

@@ -129,7 +129,7 @@ class ImageCompressor(nn.Module):
             return self._eval_autograd(input_image)
         out = self.run(input_image, noise=noise)
         _, bpp = kernels.reduce_partials(out["bits_partial"], scale=1.0 / (B * H * W), per_image=False)
-        y_hat = out["y_hat"].permute(0, 3, 1, 2)
+        y_hat = out["y_hat"].permute(0, 3, 1, 2).contiguous()   # NCHW like model.py:56
         clipped = no_backward(out["clipped"], "ImageCompressor (training mode, no grad)", params,
                               input_image)
         return clipped, y_hat, bpp
@@ -143,7 +143,7 @@ class ImageCompressor(nn.Module):
         where torch would give zeros."""
         B, _, H, W = x.shape
         with torch.no_grad():
-            y_hat = self.encode_latents(x)["y_hat"].permute(0, 3, 1, 2)
+            y_hat = self.encode_latents(x)["y_hat"].permute(0, 3, 1, 2).contiguous()
         recon = self.Decoder(y_hat)
         clipped = recon.clamp(0., 1.)                                        # model.py:59
         prob = self.bitEstimator(y_hat + 0.5) - self.bitEstimator(y_hat - 0.5)   # model.py:71-72
@@ -212,7 +212,7 @@ class ImageCompressor(nn.Module):
         split = kernels.split_planes(y_hat) if kernels.precision() == "x6" else None
         ybf = kernels.to_bf16(y_hat) if kernels.precision() == "bf16" else None
         clipped, _, _ = self.Decoder.decode(y_hat, want_recon=False, y_split=split, y_bf16=ybf)
-        return {"y_hat": y_hat.permute(0, 3, 1, 2), "x_hat": clipped}
+        return {"y_hat": y_hat.permute(0, 3, 1, 2).contiguous(), "x_hat": clipped}
 
     @torch.no_grad()
     def evaluate(self, x: torch.Tensor, want_y: bool = False,

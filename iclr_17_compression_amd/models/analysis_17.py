@@ -2,8 +2,8 @@
 
 Layers (and their init, analysis_17.py:14-23) are the reference's: conv9×9/s4 → GDN →
 conv5×5/s2 → GDN → conv5×5/s2 (no bias). ``forward`` runs three fused gfx950 kernels
-(conv1+GDN, conv2+GDN, conv3) on NHWC activations and returns y as an NCHW-shaped
-channels-last tensor.
+(conv1+GDN, conv2+GDN, conv3) on NHWC activations and returns y as a contiguous NCHW
+tensor, like the reference.
 """
 from __future__ import annotations
 
@@ -86,26 +86,35 @@ class Analysis_net_17(nn.Module):
                               lambda: kernels.pack_weight(_lib.ICLR17_W_DECONV9, self.conv1.weight,
                                                           self.out_channel_N))
 
-    def features(self, x):
-        """conv1+gdn1 → conv2+gdn2 as NHWC (the input of conv3); no autograd."""
-        w1, w2, _, g1, g2 = self.packed()
-        h = kernels.conv1_gdn(x, w1, self.conv1.bias, g1[0], g1[1], self.out_channel_N)
-        return kernels.conv2_gdn(h, w2, self.conv2.bias, g2[0], g2[1])
-
     def forward(self, x):
+        """analysis_17.py:31-36 → y, contiguous NCHW like the reference's. Without autograd it
+        runs the very kernels of ``ImageCompressor.forward``'s analysis half in the current
+        precision (conv3 with its quantiser epilogue, y taken before the rounding), so
+        ``torch.round(Encoder(x))`` is bitwise the codec's ŷ (NewTests/testReconSeperateEandD.py:67)."""
         from ..autograd import AnalysisFn, needs_grad
         kernels._check(x, "image", 4)
         params = list(self.parameters())
         if needs_grad(x, params):
             return AnalysisFn.apply(x.contiguous(), self, *params)
-        _, _, w3, _, _ = self.packed()
+        x = x.contiguous()
+        N = self.out_channel_N
+        w1, w2, w3, g1, g2 = self.packed()
+        # the rate epilogue needs a model: a zero one (its bits are discarded, y is all we keep)
+        z = torch.zeros(11 * N, device=x.device)
+        ztab = torch.zeros(N, 65, device=x.device)
         if kernels.precision() == "bf16":
             w1b, w2b, w3b = self.packed_bf16()
             e1, e2 = self.gdn1.effective_params_bf16(), self.gdn2.effective_params_bf16()
-            h = kernels.conv1_gdn_bf16(x.contiguous(), w1b, self.conv1.bias, *e1, self.out_channel_N)
+            h = kernels.conv1_gdn_bf16(x, w1b, self.conv1.bias, *e1, N)
             h = kernels.conv2_gdn_bf16(h, w2b, self.conv2.bias, *e2)
-            z = torch.zeros(11 * self.out_channel_N, device=x.device)   # rate unused: y only
-            y = kernels.conv3_quant_rate_bf16(h, w3b, z, torch.zeros(self.out_channel_N, 65, device=x.device),
-                                              want_y=True)[2]
-            return y.permute(0, 3, 1, 2)
-        return kernels.conv3(self.features(x), w3).permute(0, 3, 1, 2)
+            y = kernels.conv3_quant_rate_bf16(h, w3b, z, ztab, want_y=True)[2]
+        elif kernels.precision() == "x6":
+            e1, e2 = self.gdn1.effective_params_x6(), self.gdn2.effective_params_x6()
+            hs, _, _ = kernels.conv1x6_gdn(x, self.packed_conv1_x6(), self.conv1.bias, e1[0], e1[2], N)
+            hs, _, _ = kernels.conv2_gdn_x6(hs, w2, self.conv2.bias, *e2)
+            y = kernels.conv3_quant_rate_x6(hs, w3, z, want_y=True, rtab=ztab)[2]
+        else:
+            h = kernels.conv1_gdn(x, w1, self.conv1.bias, g1[0], g1[1], N)
+            h = kernels.conv2_gdn(h, w2, self.conv2.bias, g2[0], g2[1])
+            y = kernels.conv3_quant_rate(h, w3, z, want_y=True, rtab=ztab)[2]
+        return y.permute(0, 3, 1, 2).contiguous()

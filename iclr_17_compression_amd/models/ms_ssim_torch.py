@@ -43,7 +43,12 @@ def _check_window(win_size, win_sigma, win):
 
 
 def _to_gpu(X, Y):
-    """(X, Y) on a GPU as contiguous fp32, plus the device to return results on."""
+    """(X, Y) on a GPU as contiguous fp32, plus the device to return results on. The kernels have
+    no backward: with autograd on and an input that requires grad this raises rather than
+    return a value a loss such as 1 − ms_ssim(...) would silently not differentiate."""
+    if torch.is_grad_enabled() and (X.requires_grad or Y.requires_grad):
+        raise Iclr17Error("iclr17: ms_ssim/ssim have no backward on the GPU kernels; call them on "
+                          "detached tensors or under torch.no_grad()")
     if X.dtype != torch.float32:
         raise Iclr17Error(f"iclr17: ssim/ms_ssim take float32 images (got {X.dtype})")
     home = X.device

@@ -25,11 +25,11 @@ def test_traffic_only_from_this_build(tmp_path, monkeypatch):
     monkeypatch.setattr(bench, "REPO", str(tmp_path))
     sha = bench.lib_sha()
     _write(tmp_path, "r01_traffic.json", "0" * 16)
-    t, why = bench.pmc_traffic("deconv2_igdn2", 192, 256, 64, "x6")
-    assert t is None and sha in why and "r01_traffic.json" in why
+    t, why, ms = bench.pmc_traffic("deconv2_igdn2", 192, 256, 64, "x6")
+    assert t is None and ms is None and sha in why and "r01_traffic.json" in why
     _write(tmp_path, "r02_traffic.json", sha)
-    t, src = bench.pmc_traffic("deconv2_igdn2", 192, 256, 64, "x6")
-    assert t == 123.0 and "r02_traffic.json" in src
+    t, src, ms = bench.pmc_traffic("deconv2_igdn2", 192, 256, 64, "x6")
+    assert t == 123.0 and ms == 0.1 and "r02_traffic.json" in src
     # another precision, workload or layer of the same build does not count
     assert bench.pmc_traffic("deconv2_igdn2", 192, 256, 64, "bf16")[0] is None
     assert bench.pmc_traffic("deconv2_igdn2", 192, 256, 32, "x6")[0] is None
@@ -56,6 +56,9 @@ def test_roofline_object(prec, kernel_peak, tmp_path, monkeypatch):
     assert roof["achieved"] == pytest.approx(flops / 0.2e-3 / 1e12, rel=1e-3)
     assert roof["frac"] == pytest.approx(roof["achieved"] / kernel_peak, rel=1e-3)
     assert roof["traffic"] is None and roof["traffic_null_reason"]
+    assert roof["duration"].startswith("hip_events")
+    assert roof["frac_of_bf16_dense_peak"] == pytest.approx(roof["achieved"] / bench.BF16_MFMA_PEAK_TFLOPS, rel=1e-3)
+    assert "frac_from_profile" not in roof
 
 
 def test_chain_roofline(tmp_path, monkeypatch):
@@ -79,3 +82,41 @@ def test_chain_roofline(tmp_path, monkeypatch):
         else:
             assert bounds["conv1_gdn1"] == "hbm" and bounds["deconv3_clamp"] == "hbm"
             assert bounds["conv2_gdn2"] == "mfma" and bounds["deconv2_igdn2"] == "mfma"
+
+
+def _run_bench(args, env_extra, timeout=240):
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra)
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    return subprocess.run([sys.executable, os.path.join(repo, "bench.py"), *args], env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_launcher_spawns_ranks(n):
+    """`python bench.py --gpus N` without torchrun starts N ranks itself (here over gloo, no GPU:
+    --dry-run runs the launch, rendezvous, barrier and max-over-ranks only)."""
+    r = _run_bench(["--gpus", str(n), "--dry-run"], {"ICLR17_DIST_BACKEND": "gloo"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == n and d["global_batch"] == 64 * n and d["scaling"] == "weak"
+    assert len(d["rank_devices"]) == n
+    assert d["dist_backend"] == ("gloo" if n > 1 else None)
+
+
+def test_launcher_strong_scaling_and_errors():
+    r = _run_bench(["--gpus", "2", "--dry-run", "--global-batch", "64"], {"ICLR17_DIST_BACKEND": "gloo"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert d["batch_per_gpu"] == 32 and d["global_batch"] == 64 and d["scaling"] == "strong"
+    # an odd global batch over 2 ranks, and more GPUs than the host has (RCCL), both fail loudly
+    assert _run_bench(["--gpus", "2", "--dry-run", "--global-batch", "63"],
+                      {"ICLR17_DIST_BACKEND": "gloo"}).returncode != 0
+    assert _run_bench(["--gpus", "4096"], {}).returncode != 0
+    # under torchrun, --gpus must equal WORLD_SIZE
+    r = _run_bench(["--gpus", "2", "--dry-run"], {"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0",
+                                                  "ICLR17_DIST_BACKEND": "gloo"})
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr

@@ -475,3 +475,26 @@ def test_batched_packs_match_single(device):
     assert len(single) == len(batched)
     for a, b in zip(single, batched):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("mode", ["x6", "fp32", "bf16"])
+def test_encoder_matches_codec_forward(device, mode):
+    """The separate encode / decode path (NewTests/testReconSeperateEandD.py:67-68): in every
+    precision ``torch.round(net.Encoder(x))`` is bitwise the codec forward's ŷ, the latents are
+    contiguous NCHW like the reference's (model.py:56, 80) so ``.view(B, -1)`` works
+    (model_fc.py:60), and Decoder(round(Encoder(x))) is the forward's reconstruction."""
+    old = kernels.precision()
+    kernels.set_precision(mode)
+    try:
+        net = net_for(192, 1, device)
+        x = image(5, 2, 64, 96).to(device)
+        with torch.no_grad():
+            y = net.Encoder(x)
+            clipped, y_hat, _ = net(x)
+            recon = net.Decoder(torch.round(y))
+    finally:
+        kernels.set_precision(old)
+    assert y.is_contiguous() and y_hat.is_contiguous() and y.shape == (2, 192, 4, 6)
+    assert y.view(2, -1).shape == (2, 192 * 24) and y_hat.view(2, -1).shape == (2, 192 * 24)
+    assert torch.equal(torch.round(y), y_hat)
+    assert torch.equal(recon.clamp(0.0, 1.0), clipped)

@@ -100,3 +100,38 @@ def test_ms_ssim_argument_checks_and_no_cpu_fallback():
     if not torch.cuda.is_available():
         with pytest.raises(Iclr17Error, match="no CPU implementation"):
             ms_ssim(x, x, data_range=1.0, size_average=True)
+
+
+def test_ms_ssim_refuses_a_backward_it_cannot_give():
+    """The GPU MS-SSIM has no backward: an input that requires grad raises (a loss such as
+    λ·(1 − ms_ssim) + bpp would otherwise silently drop that term's gradient); under no_grad or
+    on detached tensors the call proceeds (here to the no-GPU error on a CPU host)."""
+    from iclr_17_compression_amd._lib import Iclr17Error
+    from iclr_17_compression_amd.models import ms_ssim, ssim
+    from iclr_17_compression_amd.models.ms_ssim_torch import MS_SSIM
+    x = torch.rand(1, 3, 176, 176, requires_grad=True)
+    y = torch.rand(1, 3, 176, 176)
+    for fn in (lambda: ms_ssim(x, y, data_range=1.0), lambda: ssim(y, x, data_range=1.0),
+               lambda: MS_SSIM(data_range=1.0)(x, y)):
+        with pytest.raises(Iclr17Error, match="no backward"):
+            fn()
+    if not torch.cuda.is_available():
+        with torch.no_grad(), pytest.raises(Iclr17Error, match="no CPU implementation"):
+            ms_ssim(x, y, data_range=1.0)
+
+
+def test_train_loader_refuses_fewer_images_than_a_global_batch(tmp_path):
+    from iclr_17_compression_amd import data
+    with pytest.raises(ValueError, match="global batch"):
+        data.TrainLoader([str(tmp_path / "a.png")] * 3, 2, 64, 0, "cpu", rank=0, world=2, workers=0)
+
+
+def test_grad_reducer_refuses_a_held_gradient():
+    """GradAllReducer.launch: a parameter whose .grad already holds another value (no
+    set_to_none zero_grad, gradient accumulation) would lose it in finish(): it raises."""
+    from iclr_17_compression_amd import dist as idist
+    p = torch.nn.Parameter(torch.zeros(4))
+    p.grad = torch.ones(4)
+    red = idist.GradAllReducer([p])
+    with pytest.raises(RuntimeError, match="already holds"):
+        red.launch([p], [torch.full((4,), 2.0)])

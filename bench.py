@@ -351,6 +351,8 @@ def kodak_synth_images(meta):
     return out
 
 
+KODAK_ORDERS = {"g9": "g9s_reference_orders_n192.json"}   # tests/golden/gen_g9s.py
+
 KODAK_SETS = {   # --kodak-set: fixture, description of the weights
     "g9": ("g9_kodak24_synth_n192_trained.json",
            "N=192 weights trained to lambda=0.01 (tests/golden/g9_weights_n192.npz)"),
@@ -396,6 +398,23 @@ def run_kodak(args, dev):
             per[i] = {k: ev[k][j].item() for k in ("bpp", "psnr", "ms_ssim")}
     rel = {k: max(abs(per[i][k] - meta["images"][i][k]) / abs(meta["images"][i][k]) for i in range(24))
            for k in ("bpp", "psnr", "ms_ssim")}
+    # ŷ against the reference's, per image (the fixture holds the SHA-256 of the reference's ŷ)
+    import hashlib
+    same = 0
+    with torch.no_grad():
+        for i in range(24):
+            ev = net.evaluate(imgs[i].to(dev))
+            same += hashlib.sha256(ev["y_hat"].cpu().contiguous().numpy().tobytes()).hexdigest() \
+                == meta["images"][i]["y_hat_sha256"]
+    parity = {"max_rel_" + k: v for k, v in rel.items()}
+    parity["images_with_the_reference_latents"] = same
+    if args.kodak_set in KODAK_ORDERS:   # the bar: the reference's own cross-order spread (G8s/G9s)
+        orders = json.load(open(os.path.join(REPO, "tests", "golden", KODAK_ORDERS[args.kodak_set])))
+        sp = orders["set_spread_fp32"]
+        parity["reference_cross_order_spread"] = {
+            "max_rel_" + k: sp["rel_d" + k] for k in ("bpp", "psnr", "ms_ssim")}
+        parity["reference_cross_order_flips"] = orders["total_flips_vs_default"]
+        parity["bar"] = {"max_rel_" + k: max(1e-5, sp["rel_d" + k] + 1e-6) for k in ("bpp", "psnr", "ms_ssim")}
     pixels = 24 * 512 * 768 * args.steps
     return {
         "metric": "Mpixels/s Kodak-24 encode+decode with per-image bpp/PSNR/MS-SSIM (C2)",
@@ -406,7 +425,7 @@ def run_kodak(args, dev):
         "data": f"synthetic Kodak-24 (18 x 512x768 + 6 x 768x512, smooth_image_u8), {weights_note}",
         "config": {"workload": "Kodak-24 eval: encode, round, rate, decode, clamp, per-image bpp/PSNR/MS-SSIM",
                    "N": meta["N"], "precision": kernels.precision()},
-        f"parity_vs_reference_{args.kodak_set.upper()}": {"max_rel_" + k: v for k, v in rel.items()},
+        f"parity_vs_reference_{args.kodak_set.upper()}": parity,
         "dataset_average": {k: sum(per[i][k] for i in range(24)) / 24 for k in ("bpp", "psnr", "ms_ssim")},
     }
 

@@ -48,6 +48,66 @@ __device__ __forceinline__ f4 mfma16(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// Two-level accumulation (ICLR17_SEP_ACC, default on). A long MFMA accumulation chain puts every
+// rounding at the scale of the whole running sum: for conv2 (K = 4800) the exact-f32 16x16x4
+// chain lands ~10x farther from the exact value than the reference's oneDNN conv, and
+// v_mfma_f32_16x16x32_bf16 is not a single correctly rounded C + Σ a·b (tools/mfma_numerics.hip:
+// ~0.6-1.5 ulp of C per instruction, unbiased), so the x6 mode's six part products per k-block
+// landed ~6x farther still. Each 32-deep k-block is therefore summed from zero in a short chain of
+// its own and added to the accumulator with one correctly rounded VALU add; the block sums are
+// ~1/sqrt(K/32) of the total, so their own rounding is small. conv2+GDN2 pre-activations: rms
+// error vs fp64 2e-5 (fp32) / 1.1e-4 (x6) → below oneDNN's 2.1e-6.
+#ifndef ICLR17_SEP_ACC
+#define ICLR17_SEP_ACC 1
+#endif
+constexpr bool kSepAcc = ICLR17_SEP_ACC != 0;
+
+// x6 product of one 32-deep k-block (lo·hi + hi·lo + mid·mid + mid·hi + hi·mid + hi·hi, small
+// terms first) onto acc[mt][nt]. With ICLR17_SEP_ACC the block sum is a fresh six-MFMA chain
+// whose add into acc is deferred to the NEXT call (X6Acc holds it), so the add never waits on
+// its own chain, and a scheduling barrier keeps the chains in program order: at most two block
+// sums are live (letting the scheduler interleave every chain of a k-step, as it does with
+// in-place accumulation, doubled the accumulator registers). Call x6_flush after the last one.
+struct X6Acc {
+  f4 pend;
+  int pm = -1, pn = -1;   // compile-time constants once the callers' loops are unrolled
+};
+// instruction classes that may still move across the barrier (SALU, VMEM, DS); -1: no barrier
+#ifndef ICLR17_X6_SCHED_MASK
+#define ICLR17_X6_SCHED_MASK (0x0004 | 0x0010 | 0x0080)
+#endif
+constexpr int kX6SchedMask = ICLR17_X6_SCHED_MASK;
+
+template <bool SEP, int MT, int NT>
+__device__ __forceinline__ void mfma_x6(f4 (&acc)[MT][NT], X6Acc& st, int mt, int nt,
+                                        const bf8& Ah, const bf8& Am, const bf8& Al,
+                                        const bf8& Bh, const bf8& Bm, const bf8& Bl) {
+  f4 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al, Bh, SEP ? f4{0.f, 0.f, 0.f, 0.f} : acc[mt][nt],
+                                                 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bl, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bm, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bm, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bh, c, 0, 0, 0);
+  if constexpr (SEP) {
+    if (st.pm >= 0) acc[st.pm][st.pn] += st.pend;
+    st.pend = c;
+    st.pm = mt;
+    st.pn = nt;
+    if constexpr (kX6SchedMask >= 0) __builtin_amdgcn_sched_barrier(kX6SchedMask);
+  } else {
+    acc[mt][nt] = c;
+  }
+}
+
+template <bool SEP, int MT, int NT>
+__device__ __forceinline__ void x6_flush(f4 (&acc)[MT][NT], X6Acc& st) {
+  if constexpr (SEP) {
+    if (st.pm >= 0) acc[st.pm][st.pn] += st.pend;
+    st.pm = -1;
+  }
+}
+
 // ----------------------------------------------------------------------------- rate model
 // Packed per-channel BitEstimator parameters, rows of C floats:
 //   0..2  softplus(h1), b1, tanh(a1)     3..5  layer 2     6..8  layer 3

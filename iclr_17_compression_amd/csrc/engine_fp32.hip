@@ -226,6 +226,23 @@ __device__ __forceinline__ void mfma_block(f4 (&acc)[MT][NT], const f4 (&af)[MT]
       for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16(af[mt][e], bf[nt][e], acc[mt][nt]);
 }
 
+// Two-level accumulation of the exact-f32 contractions (common.h, ICLR17_SEP_ACC): a 32-deep
+// k-block (two mfma_block calls) is summed from zero into `part`, then added to acc.
+template <int MT, int NT>
+__device__ __forceinline__ void zero_tile(f4 (&t)[MT][NT]) {
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) t[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
+}
+template <int MT, int NT>
+__device__ __forceinline__ void add_tile(f4 (&acc)[MT][NT], const f4 (&t)[MT][NT]) {
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] += t[mt][nt];
+}
+
 // ----------------------------------------------------------------------------- GDN epilogue
 // Channel contraction of an LDS tile: out[m][i] = Σ_j sX[m][j] · B[j][i], B packed
 // [CO/4][CO][4] (packed[q][i][e] = B[4q+e][i]) and read straight from L2, one k-block ahead.
@@ -358,6 +375,7 @@ __device__ __forceinline__ void chan_gemm_x6(f4 (&acc)[MT][NT], const float* sX,
         b[p][nt] = *(const u4*)(gb + p * GP + (long)kb * 4 * CO * 8 + nt * 128);
   };
   auto block = [&](int kb, const u4 (&b)[3][NT]) {
+    X6Acc st;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       u4 ah, am, al;
@@ -374,15 +392,10 @@ __device__ __forceinline__ void chan_gemm_x6(f4 (&acc)[MT][NT], const float* sX,
       for (int nt = 0; nt < NT; ++nt) {
         const bf8 Bh = __builtin_bit_cast(bf8, b[0][nt]), Bm = __builtin_bit_cast(bf8, b[1][nt]),
                   Bl = __builtin_bit_cast(bf8, b[2][nt]);
-        f4 c = acc[mt][nt];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al, Bh, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bl, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bm, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bh, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bm, c, 0, 0, 0);
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bh, c, 0, 0, 0);
+        mfma_x6<false>(acc, st, mt, nt, Ah, Am, Al, Bh, Bm, Bl);
       }
     }
+    x6_flush<false>(acc, st);
   };
   load(0, b0);
   for (int kb = 0; kb < KB; kb += 2) {
@@ -419,6 +432,7 @@ __device__ __forceinline__ void chan_gemm_x6p(f4 (&acc)[MT][NT], const unsigned 
         b[p][nt] = *(const u4*)(gb + p * GP + (long)kb * 4 * CO * 8 + nt * 128);
   };
   auto block = [&](int kb, const u4 (&b)[3][NT]) {
+    X6Acc st;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const unsigned short* a = arow + mt * 16 * PS + kb * 32;
@@ -429,15 +443,10 @@ __device__ __forceinline__ void chan_gemm_x6p(f4 (&acc)[MT][NT], const unsigned 
       for (int nt = 0; nt < NT; ++nt) {
         const bf8 Bh = __builtin_bit_cast(bf8, b[0][nt]), Bm = __builtin_bit_cast(bf8, b[1][nt]),
                   Bl = __builtin_bit_cast(bf8, b[2][nt]);
-        f4 c = acc[mt][nt];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al, Bh, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bl, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bm, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bh, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bm, c, 0, 0, 0);
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bh, c, 0, 0, 0);
+        mfma_x6<false>(acc, st, mt, nt, Ah, Am, Al, Bh, Bm, Bl);
       }
     }
+    x6_flush<false>(acc, st);
   };
   load(0, b0);
   for (int kb = 0; kb < KB; kb += 2) {
@@ -885,6 +894,9 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   // an L2-miss DMA issued one step ahead, so it runs NS stages with a counted vmcnt wait.
   // x6 IGDN layers (deconv1 / deconv2): halo-patch A operand (see the main loop)
   constexpr bool HALO = X6 && EPI == EPI_IGDN && BMT == BM && ICLR17_X6_HALO;
+  // per-tap two-level accumulation for the encoder layers whose latents are rounded (conv2+GDN2,
+  // conv3+quantiser): their accuracy decides the ŷ flips against the reference
+  constexpr bool TAPSEP = kSepAcc && !HALO && (EPI == EPI_GDN || EPI == EPI_QUANT);
   constexpr int HALO_NI = (3 * 100 * 64 + 1023) / 1024;   // patch DMA wave-instructions (19)
   constexpr int HALO_PF = HALO_NI * 256;                  // patch floats
   constexpr int LDS_A = HALO ? HALO_PF + 2 * SB
@@ -997,6 +1009,7 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   const int boff6 = (2 * (lane >> 4) * BN + wn * (BN / WN) + (lane & 15)) * 4;
 
   auto compute6 = [&](int buf) {
+    X6Acc st;
     const unsigned short* sa = (const unsigned short*)(smem + buf * STAGE);
     const float* sb = smem + buf * STAGE + SA + boff6;
     bf8 Bh[NT], Bm[NT], Bl[NT];
@@ -1015,15 +1028,10 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
       const bf8 Al = __builtin_bit_cast(bf8, *(const u4*)(sa + 2 * BMT * KCH + aoff6[mt]));
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
-        f4 c = acc[mt][nt];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al, Bh[nt], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bl[nt], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bm[nt], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bh[nt], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bm[nt], c, 0, 0, 0);
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bh[nt], c, 0, 0, 0);
+        mfma_x6<false>(acc, st, mt, nt, Ah, Am, Al, Bh[nt], Bm[nt], Bl[nt]);
       }
     }
+    x6_flush<false>(acc, st);
   };
 
   auto compute = [&](int buf) {
@@ -1098,6 +1106,7 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
       hq[mt] = hy[mt] * 10 + (r & 7) + 1;
     }
     auto compute_halo = [&](int buf, int dy, int dx) {
+      X6Acc st;
       const float* sb = sbw + buf * SB + boff6;
       bf8 Bh[NT], Bm[NT], Bl[NT];
 #pragma unroll
@@ -1118,15 +1127,10 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
         const bf8 Al = __builtin_bit_cast(bf8, *(const u4*)(pa + 200 * 32));
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
-          f4 c = acc[mt][nt];
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al, Bh[nt], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bl[nt], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bm[nt], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bh[nt], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bm[nt], c, 0, 0, 0);
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bh[nt], c, 0, 0, 0);
+          mfma_x6<false>(acc, st, mt, nt, Ah, Am, Al, Bh[nt], Bm[nt], Bl[nt]);
         }
       }
+      x6_flush<false>(acc, st);
     };
     issue_patch(0);
     issue_b(0, 0);
@@ -1146,10 +1150,33 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
     }
   } else {
     issue(0, 0);
-    for (int s = 0; s < nsteps; ++s) {
-      dma_barrier();   // step s landed for every wave; stage (s+1)&1 is free
-      if (s + 1 < nsteps) issue(s + 1, (s + 1) & 1);
-      compute(s & 1);
+    if constexpr (TAPSEP) {
+      // two-level accumulation (common.h, ICLR17_SEP_ACC): each tap's NCH steps accumulate in
+      // place from zero, and the tap sum is added to `total` with one correctly rounded add
+      static_assert(NCH % 2 == 0, "stage parity = chunk parity");
+      f4 total[MT][NT];
+      zero_tile<MT, NT>(total);
+      for (int tp = 0; tp < ntaps; ++tp) {
+        zero_tile<MT, NT>(acc);
+#pragma unroll
+        for (int cc = 0; cc < NCH; ++cc) {
+          const int s = tp * NCH + cc;
+          dma_barrier();   // step s landed for every wave; stage (s+1)&1 is free
+          if (s + 1 < nsteps) issue(s + 1, (cc + 1) & 1);
+          compute(cc & 1);
+        }
+        add_tile<MT, NT>(total, acc);
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = total[mt][nt];
+    } else {
+      for (int s = 0; s < nsteps; ++s) {
+        dma_barrier();   // step s landed for every wave; stage (s+1)&1 is free
+        if (s + 1 < nsteps) issue(s + 1, (s + 1) & 1);
+        compute(s & 1);
+      }
     }
   }
   __syncthreads();     // last stage reads done before the epilogue reuses LDS
@@ -1349,6 +1376,7 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
 
   // tap `tap` from its block at u16 offset `boff` of stage buf: [plane][k8][16·NTT][8]
   auto compute = [&](int buf, int tap, int boff, auto ntt) {
+    X6Acc st;
     constexpr int NTT = decltype(ntt)::value;   // tiles this tap touches
     constexpr int NC = 16 * NTT;
     const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
@@ -1371,15 +1399,10 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
       const bf8 Al = __builtin_bit_cast(bf8, *(const u4*)(sa + 2 * D3_PPX * 32));
 #pragma unroll
       for (int nt = 0; nt < NTT; ++nt) {
-        f4 c = acc[mt][nt];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al, Bh[nt], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bl[nt], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bm[nt], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bh[nt], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bm[nt], c, 0, 0, 0);
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bh[nt], c, 0, 0, 0);
+        mfma_x6<false>(acc, st, mt, nt, Ah, Am, Al, Bh[nt], Bm[nt], Bl[nt]);
       }
     }
+    x6_flush<false>(acc, st);
   };
 
   issue_a(0);
@@ -1879,18 +1902,14 @@ __global__ void __launch_bounds__(256, 2) conv1_x6_kernel(const EngineArgs a) {
   auto pair_row = [](int p) { return (p / 9) * P1 + p % 9; };
 
   auto mfma6 = [&](int mt, const bf8& Ah, const bf8& Am, const bf8& Al, const u4 (&b)[3][NT]) {
+    X6Acc st;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       const bf8 Bh = __builtin_bit_cast(bf8, b[0][nt]), Bm = __builtin_bit_cast(bf8, b[1][nt]),
                 Bl = __builtin_bit_cast(bf8, b[2][nt]);
-      f4 c = acc[mt][nt];
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al, Bh, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bl, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bm, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Am, Bh, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bm, c, 0, 0, 0);
-      acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah, Bh, c, 0, 0, 0);
+      mfma_x6<false>(acc, st, mt, nt, Ah, Am, Al, Bh, Bm, Bl);
     }
+    x6_flush<false>(acc, st);
   };
   // Steps 0..6: 8 consecutive columns of one patch row per lane (two 8-byte reads per plane).
   auto step_rows = [&](int s, const u4 (&b)[3][NT]) {

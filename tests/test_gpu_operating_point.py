@@ -3,10 +3,11 @@
 MS-SSIM ≈ 0.925), G9 at N = 192, BASELINE C2's width (PSNR ≈ 27.2 dB, bpp ≈ 0.27, MS-SSIM ≈
 0.916); values from the reference (tests/golden/gen_goldens.py g8, g9).
 
-* x6 and exact-f32: every image's bpp, PSNR and MS-SSIM against the reference at 1e-5 relative
-  (MS-SSIM is well conditioned here, unlike at G5's degenerate 6.6 dB point), the latents
-  against the oracle (near-tie rule of test_gpu_parity.check_latents);
-* testKodak's own lines (train.py:171-179) on the build's names;
+* x6 and exact-f32: every image's bpp, PSNR and MS-SSIM against the reference's own values,
+  unconditionally, at max(1e-5, the reference's own spread across its CPU summation orders:
+  tests/golden/g8s_/g9s_*.json), and the latents held to the reference's own cross-order flip
+  count and to its own distance from exact (fp64) arithmetic;
+* testKodak's own lines (train.py:171-179) on the build's names, every image;
 * the bf16 throughput mode's deviation from the reference at this operating point: latent flip
   rate, Δbpp, ΔPSNR, ΔMS-SSIM per image, with the bounds written below.
 """
@@ -54,60 +55,103 @@ def _image(meta, row):
         synth.smooth_image_u8(meta["image_seed_base"] + row["index"], row["height"], row["width"])))[None]
 
 
-def oracle_metrics_given_latents(y_hat, x, sd):
-    """The reference's bpp / PSNR / MS-SSIM computed (oracle, CPU) from a GIVEN ŷ: what the
-    reference outputs once its latents are these (model.py:55-78, train.py:171-178)."""
-    y_hat = y_hat.detach().cpu().float()
-    clipped = torch.clamp(oracle.synthesis(y_hat, sd), 0.0, 1.0)
-    total_bits, _ = oracle.estimate_bits(y_hat, sd)
-    bpp = total_bits / (x.shape[2] * x.shape[3])
-    return bpp.item(), oracle.psnr(clipped, x).item(), oracle.ms_ssim(clipped, x, 1.0).item()
+ORDERS = {128: "g8s_reference_orders_n128.json", 192: "g9s_reference_orders_n192.json"}
+
+
+def reference_orders(meta, golden_dir):
+    """The reference's own disagreement with itself across CPU summation orders on this set
+    (tests/golden/gen_g9s.py: oneDNN default vs mkldnn-off, oneDNN-AVX2, native-AVX2)."""
+    return json.load(open(os.path.join(golden_dir, ORDERS[meta["N"]])))
+
+
+# added to the reference's cross-order spread on an image whose latents flip: the GPU's own
+# continuous fp32 noise on identical latents (measured ≤ 2e-7 relative on bpp / PSNR / MS-SSIM)
+NOISE_REL = 1e-6
+
+
+def parity_bars(orders):
+    """Per metric, for an image whose ŷ differs from the reference's: max(1e-5, the reference's own
+    largest relative change across its fp32 summation orders on this set + NOISE_REL) (an image
+    with the reference's ŷ is held to 1e-5); the latent-flip budget: the most flips any of the
+    reference's fp32 orders makes against its default order on this set."""
+    sp = orders["set_spread_fp32"]
+    bars = {k: max(REL, sp["rel_d" + k] + NOISE_REL) for k in ("bpp", "psnr", "ms_ssim")}
+    flips = max(v for o, v in orders["total_flips_vs_default"].items() if o != "fp64")
+    return bars, flips, sp["max_abs_dy"]
+
+
+def exact_latents(x, sd, device):
+    """y of the analysis transform (analysis_17.py:31-36) in float64 on the GPU (ATen's native
+    convs, MIOpen off): the value every fp32 summation order approximates."""
+    old = torch.backends.cudnn.enabled
+    torch.backends.cudnn.enabled = False
+    try:
+        with torch.no_grad():
+            return oracle.analysis(x.double().to(device), {k: v.double().to(device) for k, v in sd.items()}).cpu()
+    finally:
+        torch.backends.cudnn.enabled = old
 
 
 @pytest.mark.parametrize("precision", ["x6", "fp32"])
-def test_g8_all_images(device, opset, precision):
-    """Per image: the latents equal the oracle's (pinned to the reference) except at legitimate
-    near-ties. Without flips, bpp / PSNR / MS-SSIM match the reference's values at 1e-5; with
-    k flips (a few per million latents), they match the reference's outputs for the same ŷ —
-    the oracle's decoder and rate model on the GPU's latents — at 1e-5."""
-    from test_gpu_parity import check_latents
+def test_g8_all_images(device, opset, golden_dir, precision):
+    """Every image, unconditionally, against the REFERENCE's own values (the fixture, its default
+    oneDNN order), at max(1e-5, the reference's own cross-order spread on this set) per metric.
+    Latents: each flip against the reference must sit within the reference's own fp32 noise of a
+    rounding boundary; the set's flip count is at most what the reference's own other summation
+    orders produce; and, against exact (fp64) arithmetic, the GPU rounds at most as many latents
+    the wrong way as the reference itself does."""
     meta = opset
     sd = meta["state"]
+    bars, flip_budget, noise = parity_bars(reference_orders(meta, golden_dir))
     net = _net(meta, device)
     old = kernels.precision()
     kernels.set_precision(precision)
-    flips = flipped_images = 0
+    flips = gpu_wrong = ref_wrong = 0
+    worst = {k: 0.0 for k in bars}
     try:
         for row in meta["images"]:
             x = _image(meta, row)
             with torch.no_grad():
                 ev = net.evaluate(x.to(device), want_y=True, want_msssim=True)
             _, r_yhat, _, _, r_y = oracle.codec_forward(x, sd)
-            n = check_latents(ev["y_hat"], ev["y"], r_yhat, r_y, max_rate=2e-5)
-            if n == 0:
-                ref = (row["bpp"], row["psnr"], row["ms_ssim"])
-            else:
-                flips += n
-                flipped_images += 1
-                ref = oracle_metrics_given_latents(ev["y_hat"], x, sd)
-            got = (ev["bpp"][0].item(), ev["psnr"][0].item(), ev["ms_ssim"][0].item())
-            assert got == pytest.approx(ref, rel=REL), (row["index"], n, got, ref)
+            ex = torch.round(exact_latents(x, sd, device)).float()
+            g = ev["y_hat"].cpu()
+            diff = g != r_yhat
+            n = int(diff.sum())
+            if n:
+                tie = (r_y[diff] - (torch.floor(r_y[diff]) + 0.5)).abs().max().item()
+                assert tie <= noise, (row["index"], n, tie, noise)
+            flips += n
+            gpu_wrong += int((g != ex).sum())
+            ref_wrong += int((r_yhat != ex).sum())
+            got = {"bpp": ev["bpp"][0].item(), "psnr": ev["psnr"][0].item(), "ms_ssim": ev["ms_ssim"][0].item()}
+            for k, bar in bars.items():
+                rel = abs(got[k] - row[k]) / abs(row[k])
+                worst[k] = max(worst[k], rel)
+                bar = bar if n else REL   # same latents: the north_star's 1e-5
+                assert rel <= bar, (row["index"], k, n, got[k], row[k], rel, bar)
     finally:
         kernels.set_precision(old)
-    print(f"N={meta['N']} {precision}: {flips} near-tie latent flips in {flipped_images} of 24 "
-          f"images ({24 * meta['N'] * 32 * 48} latents)")
+    with open(os.path.join(os.environ.get("ICLR17_PARITY_OUT", "/tmp"), f"parity_{meta['N']}_{precision}.json"), "w") as f:
+        json.dump({"N": meta["N"], "precision": precision, "flips_vs_reference": flips,
+                   "flip_budget": flip_budget, "gpu_vs_exact": gpu_wrong, "reference_vs_exact": ref_wrong,
+                   "worst_rel": worst, "bars_flip_images": bars, "bar_same_latents": REL}, f)
+    print(f"N={meta['N']} {precision}: {flips} latent flips vs the reference (budget {flip_budget}); "
+          f"vs exact: GPU {gpu_wrong}, reference {ref_wrong}; worst rel "
+          + ", ".join(f"{k} {v:.2e} (bar {bars[k]:.2e})" for k, v in worst.items()))
+    assert flips <= flip_budget
+    assert gpu_wrong <= ref_wrong
 
 
-def test_g8_testkodak_lines_verbatim(device, opset):
-    """train.py:171-179 as written on the build's names, for images whose x6 latents equal the
-    reference's (checked): bpp / PSNR / MS-SSIM at 1e-5 against the reference's values."""
+def test_g8_testkodak_lines_verbatim(device, opset, golden_dir):
+    """train.py:171-179 as written on the build's names, every image, against the reference's
+    values at the same bars as test_g8_all_images (x6, the default precision)."""
     ns = {}
     exec("from iclr_17_compression_amd.model import *", ns)
     ms_ssim, np_, torch_ = ns["ms_ssim"], ns["np"], ns["torch"]
     meta = opset
-    sd = meta["state"]
+    bars, _, _ = parity_bars(reference_orders(meta, golden_dir))
     net = _net(meta, device)
-    done = 0
     for row in meta["images"]:
         input = _image(meta, row).to(device)
         with torch_.no_grad():
@@ -120,17 +164,10 @@ def test_g8_testkodak_lines_verbatim(device, opset):
             msssim = ms_ssim(clipped_recon_image.cpu().detach(), input.cpu(), data_range=1.0, size_average=True)
             msssimDB = -10 * (torch_.log(1-msssim) / np_.log(10))
             # ----
-            y_hat = net.run(input)["y_hat"].permute(0, 3, 1, 2).cpu()
-        if not torch.equal(y_hat, oracle.codec_forward(input.cpu(), sd)[1]):
-            continue   # a near-tie flip: covered by test_g8_all_images
-        assert bpp.item() == pytest.approx(row["bpp"], rel=REL)
-        assert psnr.item() == pytest.approx(row["psnr"], rel=REL)
-        assert msssim.item() == pytest.approx(row["ms_ssim"], rel=REL)
-        assert msssimDB.item() == pytest.approx(-10 * np.log10(1 - row["ms_ssim"]), rel=1e-4)
-        done += 1
-        if done == 4:
-            break
-    assert done == 4
+        assert bpp.item() == pytest.approx(row["bpp"], rel=bars["bpp"]), row["index"]
+        assert psnr.item() == pytest.approx(row["psnr"], rel=bars["psnr"]), row["index"]
+        assert msssim.item() == pytest.approx(row["ms_ssim"], rel=bars["ms_ssim"]), row["index"]
+        assert msssimDB.item() == pytest.approx(-10 * np.log10(1 - row["ms_ssim"]), rel=10 * bars["ms_ssim"])
 
 
 def test_g8_bf16_deviation(device, opset):

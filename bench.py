@@ -495,6 +495,58 @@ def run_codec(args, dev):
     }
 
 
+def run_encdec(args, dev):
+    """The separate encode / decode path (NewTests/testReconSeperateEandD.py:67-68,
+    train_decoder_new.py:66-105): y = net.Encoder(x), ŷ = torch.round(y), x̂ = net.Decoder(ŷ),
+    through the nn.Module surface, each half timed with HIP events on the current stream."""
+    N, S, B = args.N, args.size, args.batch
+    net = ImageCompressor(out_channel_N=N)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in synth.trained_like_state_dict(N, 1).items()})
+    net = net.to(dev).eval()
+    x = torch.from_numpy(synth.to_unit_float(synth.image_u8(0, B, S, S))).to(dev)
+    t_enc, t_dec = [], []
+
+    def step(timed=False):
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        e0.record()
+        y_hat = torch.round(net.Encoder(x))
+        e1.record()
+        recon = net.Decoder(y_hat)
+        e2.record()
+        if timed:
+            t_enc.append((e0, e1))
+            t_dec.append((e1, e2))
+        return y_hat, recon
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            y_hat, recon = step(timed=True)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        _, fwd_yhat, _ = net(x)
+        same = bool(torch.equal(y_hat, fwd_yhat))
+    enc_ms = float(np.mean([a.elapsed_time(b) for a, b in t_enc]))
+    dec_ms = float(np.mean([a.elapsed_time(b) for a, b in t_dec]))
+    px = B * S * S
+    return {
+        "metric": "Mpixels/s separate encode (Encoder) + decode (Decoder) through the module surface",
+        "value": round(px * args.steps / elapsed / 1e6, 2), "unit": "Mpix/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if kernels.precision() == "bf16" else "f32",
+        "data": "synthetic (splitmix64 uint8/255 images, seeded trained-like weights)",
+        "config": {"workload": f"round(Encoder(x)) then Decoder, {B} x {S}x{S}x3, N={N}",
+                   "precision": kernels.precision()},
+        "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
+        "encode_Mpix_per_s": round(px / enc_ms / 1e3, 1), "decode_Mpix_per_s": round(px / dec_ms / 1e3, 1),
+        "round_encoder_equals_forward_latents": same,
+    }
+
+
 def cpu_threads() -> tuple:
     """(threads used, cores in this process's affinity mask): every affinity core, unless the
     box's CPU share is pinned by OMP_NUM_THREADS (16 on the GPU pool, whose affinity mask shows
@@ -784,7 +836,7 @@ def main() -> None:
     ap.add_argument("--graph", action="store_true",
                     help="eval: replay the timed steps from one HIP graph instead of launching them "
                          "kernel by kernel (x6: 4 % slower, bf16: 1.4 % faster; DESIGN §5)")
-    ap.add_argument("--mode", choices=("eval", "train", "kodak", "codec"), default="eval")
+    ap.add_argument("--mode", choices=("eval", "train", "kodak", "codec", "encdec"), default="eval")
     ap.add_argument("--precision", choices=kernels.PRECISIONS, default=None,
                     help="inference contraction mode (default: ICLR17_PRECISION or x6)")
     args = ap.parse_args()
@@ -842,9 +894,9 @@ def main() -> None:
             dist.destroy_process_group()
         return
 
-    if args.mode in ("kodak", "codec"):
+    if args.mode in ("kodak", "codec", "encdec"):
         if rank == 0:
-            run = run_kodak if args.mode == "kodak" else run_codec
+            run = {"kodak": run_kodak, "codec": run_codec, "encdec": run_encdec}[args.mode]
             print(json.dumps(run(args, dev)), flush=True)
         return
     N, S, B = args.N, args.size, args.batch

@@ -37,6 +37,8 @@ X6_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6   # fp32-equivalent: 6 bf16 part prod
 X6_LAYERS = ("conv1_gdn1", "conv2_gdn2", "conv3_quant_rate", "deconv1_igdn1", "deconv2_igdn2",
              "deconv3_clamp")   # every contraction of the x6 eval chain
 HBM_PEAK_GBS = 8000.0
+# deconv2 → deconv3 through the chunk-major split form (ICLR17_D3_CM=0: the NHWC split, for A/B)
+D3_CM = os.environ.get("ICLR17_D3_CM", "1") != "0"
 
 LAYERS = ("conv1_gdn1", "conv2_gdn2", "conv3_quant_rate", "deconv1_igdn1", "deconv2_igdn2",
           "deconv3_clamp", "bits_reduce")
@@ -125,7 +127,7 @@ class Step:
             ev(3)
             hs, _, _ = kernels.deconv_igdn_x6(ys, d1, net.Decoder.deconv1.bias, *e3)
             ev(4)
-            hs, _, _ = kernels.deconv_igdn_x6(hs, d2, net.Decoder.deconv2.bias, *e4)
+            hs, _, _ = kernels.deconv_igdn_x6(hs, d2, net.Decoder.deconv2.bias, *e4, chunk_major=D3_CM)
             ev(5)
             clipped, _, _ = kernels.deconv3_x6(hs, self.d3x6, net.Decoder.deconv3.bias)
         else:
@@ -918,6 +920,18 @@ def main() -> None:
             dist.destroy_process_group()
         return
     prec = kernels.precision()
+    rb = None
+    if prec == "x6" and world == 1 and not args.no_bf16_leg:
+        # the bf16 throughput-mode leg runs first (reported as bf16_mode below). Its step is 4x
+        # shorter and the GPU clock ramps over the first ~50 ms of load (tools/warm_probe.py:
+        # bf16 0.567 → 0.465 ms, x6 2.49 → 2.06 ms per step), so it warms for at least 100 steps
+        # before its timed region; the headline's timed region then starts at steady clocks.
+        kernels.set_precision("bf16")
+        try:
+            rb = time_eval(net, x, argparse.Namespace(**{**vars(args), "warmup": max(args.warmup, 100)}),
+                           world, dev)
+        finally:
+            kernels.set_precision(prec)
     r = time_eval(net, x, args, world, dev)
     elapsed, per_layer_ms, bpp = r["elapsed"], r["per_layer_ms"], r["bpp"]
     pixels = world * B * S * S * args.steps
@@ -960,14 +974,9 @@ def main() -> None:
         "layers": layers,
         "bpp_last": round(bpp.item(), 6),
     }
-    if x6 and world == 1 and not args.no_bf16_leg:
+    if rb is not None:
         # the bf16 throughput mode on the same batch: rate, roofline, and its deviation from the
         # x6 (fp32-exact) results — latent flips, Δbpp, ΔPSNR
-        kernels.set_precision("bf16")
-        try:
-            rb = time_eval(net, x, args, world, dev)
-        finally:
-            kernels.set_precision(prec)
         dom_b, layers_b, roof_b = roofline(rb["per_layer_ms"], "bf16", N, S, B)
         flips = int((rb["y_hat"] != r["y_hat"]).sum().item())
 
@@ -975,6 +984,7 @@ def main() -> None:
             return (10 * torch.log10(1.0 / ((c - x) ** 2).mean(dim=(1, 2, 3)))).double()
         result["bf16_mode"] = {
             "value": round(pixels / rb["elapsed"] / 1e6, 2), "unit": "Mpix/s",
+            "warmup": max(args.warmup, 100),
             "ms_per_step": round(rb["elapsed"] / args.steps * 1e3, 4), "dtype": "bf16",
             "roofline": {k: roof_b[k] for k in ("kernel", "achieved", "peak", "frac", "traffic",
                                                   "traffic_source", "traffic_null_reason",

@@ -58,6 +58,7 @@ SIGNATURES = {
     "iclr17_synthesis_deconv_igdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_synthesis_deconv3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P]),
     "iclr17_synthesis_deconv3_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P]),
+    "iclr17_synthesis_deconv3_x6_cm": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P]),
     "iclr17_output_partials_per_image": (_I, [_I, _I]),
     "iclr17_split_planes": (_I, [_P, ctypes.c_long, _P, _P]),
     "iclr17_split_packed": (_I, [_P, _I, _I, _I, _P, _P]),
@@ -68,6 +69,8 @@ SIGNATURES = {
                                                  _P, _P, _P, _P]),
     "iclr17_synthesis_deconv_igdn_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
                                              _P]),
+    "iclr17_synthesis_deconv_igdn_x6_cm": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
+                                                _P]),
     "iclr17_reduce_partials": (_I, [_P, _I, _I, _P, _P, _D, _P]),
     "iclr17_resized_crop_batch": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P]),
     "iclr17_adam_step": (_I, [_P, _I, ctypes.c_long, _D, _D, _D, _D, ctypes.c_long, _F, _P]),

@@ -198,6 +198,7 @@ def synthesis_forward_train(dec, y_nhwc: Tensor, x_ref: Optional[Tensor] = None,
         e1, e2 = dec.igdn1.effective_params_x6(), dec.igdn2.effective_params_x6()
         s1s, s1, v1 = kernels.deconv_igdn_x6(y_split, d1, dec.deconv1.bias, *e1, want_f32=True,
                                              want_pre=True)
+        # NHWC split (not chunk-major): s2s is also deconv3's x6 weight-gradient operand
         s2s, s2, v2 = kernels.deconv_igdn_x6(s1s, d2, dec.deconv2.bias, *e2, want_f32=True,
                                              want_pre=True)
         clipped, recon, sse = kernels.deconv3_x6(s2s, dec.packed_x6(), dec.deconv3.bias, x_ref=x_ref,

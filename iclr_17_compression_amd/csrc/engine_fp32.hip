@@ -99,6 +99,10 @@ struct EngineArgs {
   long in_plane;                    // plane stride (elements)
   unsigned short* out_split;        // [3][B][Hout][Wout][CO] or nullptr
   long out_plane;
+  // chunk-major split form [3][B][C/32][h][w][32] (deconv2 → deconv3 x6: a 32-channel chunk of a
+  // patch row is contiguous, so the halo kernel's chunks do not share cache lines). out_cm: the
+  // writer (store_tile_rows_split), in_cm: the reader (deconv3_x6_kernel)
+  int out_cm, in_cm;
   const unsigned short* ggamma6;    // x6: γ_eff split, [3][CO/8][CO][8] bf16 (plane CO·CO)
   const unsigned short* ggammaT6;   // x6 backward: the transposed packing of γ_eff, split
 };
@@ -179,6 +183,11 @@ __device__ __forceinline__ void store_tile_rows_split(const EngineArgs& a, const
     u4 hi, mi, lo;
     split8(*(const f4*)(s + m * ld + c8 * 8), *(const f4*)(s + m * ld + c8 * 8 + 4), hi, mi, lo);
     unsigned short* d = a.out_split + p * CO + col0 + c8 * 8;
+    if (a.out_cm) {   // [B][C/32][h][w][32]: image b, chunk c, pixel q of the image
+      const long hw = (long)a.Hout * a.Wout, b = p / hw, q = p - b * hw;
+      const int c = col0 + c8 * 8;
+      d = a.out_split + ((b * (CO / 32) + (c >> 5)) * hw + q) * 32 + (c & 31);
+    }
     *(u4*)d = hi;
     *(u4*)(d + a.out_plane) = mi;
     *(u4*)(d + 2 * a.out_plane) = lo;
@@ -1312,9 +1321,11 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
     const bool ok = i < NAI && pl < NPL && (unsigned)iy < (unsigned)a.Hin &&
                     (unsigned)ix < (unsigned)a.Win;
     const int g = (lane & 3) ^ (((p >> 2) & 1) << 1);
-    asrc[j] = ok ? (iy * a.Win + ix) * CI + g * 8 : -1;
+    // pixel stride: CI (NHWC planes) or 32 (chunk-major planes, a.in_cm)
+    asrc[j] = ok ? (iy * a.Win + ix) * (a.in_cm ? KCH : CI) + g * 8 : -1;
   }
   const unsigned short* __restrict__ inb = a.in_split + (long)b * a.Hin * a.Win * CI;
+  const long cstride = a.in_cm ? (long)a.Hin * a.Win * KCH : KCH;   // chunk stride (elements)
   auto issue_a = [&](int cc) {
 #pragma unroll
     for (int j = 0; j < AI_W; ++j) {
@@ -1322,7 +1333,7 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
       if (i < NAI) {
         const int q = i * 16 + (lane >> 2);
         const int pl = q / D3_PPX;
-        const unsigned short* src = inb + (long)(pl < NPL ? pl : 0) * a.in_plane + asrc[j] + cc * KCH;
+        const unsigned short* src = inb + (long)(pl < NPL ? pl : 0) * a.in_plane + asrc[j] + cc * cstride;
         glds16(asrc[j] >= 0 ? (const float*)src : g_zero16, sA + i * 256);
       }
     }
@@ -2246,6 +2257,7 @@ struct SplitIO {
   long in_plane = 0;
   unsigned short* out = nullptr;
   long out_plane = 0;
+  int out_cm = 0;                           // out in the chunk-major split form
   const unsigned short* gamma6 = nullptr;   // x6: split γ_eff for the GDN contraction
   const unsigned short* gammaT6 = nullptr;  // x6 backward: split transposed γ_eff
 };
@@ -2253,7 +2265,7 @@ struct SplitIO {
 static void apply_split(EngineArgs& a, const SplitIO* x6) {
   if (x6 == nullptr) return;
   a.in_split = x6->in; a.in_plane = x6->in_plane;
-  a.out_split = x6->out; a.out_plane = x6->out_plane;
+  a.out_split = x6->out; a.out_plane = x6->out_plane; a.out_cm = x6->out_cm;
   a.ggamma6 = x6->gamma6;
   a.ggammaT6 = x6->gammaT6;
 }
@@ -2511,7 +2523,8 @@ int iclr17_synthesis_deconv_igdn(const float* in, int B, int h, int w, int N,
 // iclr17_split_packed(9, N, 48) planes (x6)
 static int launch_deconv3_halo(const uint16_t* in, int B, int H, int W, int N, const void* w,
                                const float* bias, const float* x, float* clipped, float* recon,
-                               double* sse_partial, int sse_unclipped, void* stream, bool bf) {
+                               double* sse_partial, int sse_unclipped, void* stream, bool bf,
+                               int in_cm = 0) {
   const char* what = bf ? "deconv3_bf16" : "deconv3_x6";
   int rc = check_dims(B, H, W, N);
   if (rc) return rc;
@@ -2524,6 +2537,7 @@ static int launch_deconv3_halo(const uint16_t* in, int B, int H, int W, int N, c
   memset(&a, 0, sizeof(a));
   a.sse_unclipped = sse_unclipped;
   a.in_split = (const unsigned short*)in;
+  a.in_cm = in_cm;
   a.w = (const float*)w; a.bias = bias; a.out = clipped; a.recon = recon; a.xref = x;
   a.partial = sse_partial;
   a.B = B; a.Hin = H / 4; a.Win = W / 4; a.Hout = H; a.Wout = W;
@@ -2552,6 +2566,14 @@ int iclr17_synthesis_deconv3_x6(const uint16_t* in_split, int B, int H, int W, i
                                 int sse_unclipped, void* stream) {
   return launch_deconv3_halo(in_split, B, H, W, N, w_split, bias, x, clipped, recon, sse_partial,
                              sse_unclipped, stream, false);
+}
+
+int iclr17_synthesis_deconv3_x6_cm(const uint16_t* in_split_cm, int B, int H, int W, int N,
+                                   const uint16_t* w_split, const float* bias, const float* x,
+                                   float* clipped, float* recon, double* sse_partial,
+                                   int sse_unclipped, void* stream) {
+  return launch_deconv3_halo(in_split_cm, B, H, W, N, w_split, bias, x, clipped, recon, sse_partial,
+                             sse_unclipped, stream, false, 1);
 }
 
 int iclr17_synthesis_deconv3_bf16(const uint16_t* in, int B, int H, int W, int N,
@@ -2686,11 +2708,10 @@ int iclr17_analysis_conv3_quant_rate_x6(const uint16_t* in_split, int B, int H, 
                   : launch_conv5<128, EPI_QUANT>(nullptr, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io, rate_table);
 }
 
-int iclr17_synthesis_deconv_igdn_x6(const uint16_t* in_split, int B, int h, int w, int N,
-                                    const float* w_packed, const float* bias,
-                                    const float* beta_eff, const float* gamma_packed,
-                                    const uint16_t* gamma_split, float* out, uint16_t* out_split,
-                                    float* pre_out, void* stream) {
+static int deconv_igdn_x6(const uint16_t* in_split, int B, int h, int w, int N,
+                          const float* w_packed, const float* bias, const float* beta_eff,
+                          const float* gamma_packed, const uint16_t* gamma_split, float* out,
+                          uint16_t* out_split, float* pre_out, void* stream, int out_cm) {
   ICLR17_REQUIRE(B > 0 && h > 0 && w > 0, ICLR17_EINVAL, "deconv_igdn_x6: bad shape");
   ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "channel count N=%d unsupported", N);
   ICLR17_REQUIRE(in_split && w_packed && bias && beta_eff && gamma_packed && gamma_split &&
@@ -2701,9 +2722,28 @@ int iclr17_synthesis_deconv_igdn_x6(const uint16_t* in_split, int B, int h, int 
   io.in_plane = (long)B * h * w * N;
   io.out = (unsigned short*)out_split;
   io.out_plane = (long)B * (2 * h) * (2 * w) * N;
+  io.out_cm = out_cm;
   io.gamma6 = (const unsigned short*)gamma_split;
   return N == 192 ? launch_deconv5<192>(nullptr, B, h, w, w_packed, bias, beta_eff, gamma_packed, out, pre_out, S(stream), nullptr, &io)
                   : launch_deconv5<128>(nullptr, B, h, w, w_packed, bias, beta_eff, gamma_packed, out, pre_out, S(stream), nullptr, &io);
+}
+
+int iclr17_synthesis_deconv_igdn_x6(const uint16_t* in_split, int B, int h, int w, int N,
+                                    const float* w_packed, const float* bias,
+                                    const float* beta_eff, const float* gamma_packed,
+                                    const uint16_t* gamma_split, float* out, uint16_t* out_split,
+                                    float* pre_out, void* stream) {
+  return deconv_igdn_x6(in_split, B, h, w, N, w_packed, bias, beta_eff, gamma_packed, gamma_split,
+                        out, out_split, pre_out, stream, 0);
+}
+
+int iclr17_synthesis_deconv_igdn_x6_cm(const uint16_t* in_split, int B, int h, int w, int N,
+                                       const float* w_packed, const float* bias,
+                                       const float* beta_eff, const float* gamma_packed,
+                                       const uint16_t* gamma_split, float* out,
+                                       uint16_t* out_split_cm, float* pre_out, void* stream) {
+  return deconv_igdn_x6(in_split, B, h, w, N, w_packed, bias, beta_eff, gamma_packed, gamma_split,
+                        out, out_split_cm, pre_out, stream, 1);
 }
 
 static EngineArgs bwd_args(const float* saved, const float* gammaT, float* tout) {

@@ -307,7 +307,10 @@ def split_packed(packed: Tensor, taps: int, K: int, N: int) -> Tensor:
 
 
 def merge_planes(s: Tensor) -> Tensor:
-    """Split form → fp32 (hi + mid + lo, exact). Test/debug helper (torch ops)."""
+    """Split form → fp32 (hi + mid + lo, exact); a chunk-major split [3,B,N/32,h,w,32] comes back
+    as NHWC. Test/debug helper (torch ops)."""
+    if s.dim() == 6:
+        s = s.permute(0, 1, 3, 4, 2, 5).reshape(3, s.shape[1], s.shape[3], s.shape[4], -1)
     u = s.to(torch.int32) & 0xFFFF
     parts = (u << 16).view(torch.float32)
     return parts[0] + parts[1] + parts[2]
@@ -404,18 +407,21 @@ def conv3_quant_rate_x6(hs: Tensor, wp: Tensor, rate_packed: Tensor,
 
 def deconv_igdn_x6(hs: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Tensor,
                    g6: Tensor, want_split: bool = True, want_f32: bool = False,
-                   want_pre: bool = False):
-    """deconv_igdn on a split-form input; returns (split | None, fp32 | None, pre | None)."""
+                   want_pre: bool = False, chunk_major: bool = False):
+    """deconv_igdn on a split-form input; returns (split | None, fp32 | None, pre | None). With
+    ``chunk_major`` the split output is [3, B, N/32, 2h, 2w, 32] — the input form of
+    ``deconv3_x6`` that keeps its 32-channel chunks on separate cache lines."""
     _check_split(hs, "activation")
     _, B, hh, ww, N = hs.shape
     _check_channels(N)
     if not (want_split or want_f32):
         raise Iclr17Error("iclr17: deconv_igdn_x6 needs an output")
-    split = (torch.empty(3, B, 2 * hh, 2 * ww, N, device=hs.device, dtype=torch.int16)
-             if want_split else None)
+    shape = (3, B, N // 32, 2 * hh, 2 * ww, 32) if chunk_major else (3, B, 2 * hh, 2 * ww, N)
+    split = torch.empty(shape, device=hs.device, dtype=torch.int16) if want_split else None
     out = torch.empty(B, 2 * hh, 2 * ww, N, device=hs.device) if want_f32 else None
     pre = torch.empty(B, 2 * hh, 2 * ww, N, device=hs.device) if want_pre else None
-    call("iclr17_synthesis_deconv_igdn_x6", _p(hs), B, hh, ww, N, _p(wp), _p(bias), _p(beta_eff),
+    call("iclr17_synthesis_deconv_igdn_x6_cm" if chunk_major else "iclr17_synthesis_deconv_igdn_x6",
+         _p(hs), B, hh, ww, N, _p(wp), _p(bias), _p(beta_eff),
          _p(gp), _p(g6), _p(out), _p(split), _p(pre), _stream(hs))
     return split, out, pre
 
@@ -495,16 +501,26 @@ def split_deconv3(wp: Tensor, N: int) -> Tensor:
 
 def deconv3_x6(hs: Tensor, w_split: Tensor, bias: Tensor, x_ref: Optional[Tensor] = None,
                want_recon: bool = False, sse_unclipped: bool = False):
-    """deconv3 on a split-form input [3,B,H/4,W/4,N] (the halo-tiled x6 kernel); w_split:
+    """deconv3 on a split-form input — [3,B,H/4,W/4,N], or the chunk-major [3,B,N/32,H/4,W/4,32]
+    of ``deconv_igdn_x6(chunk_major=True)`` — (the halo-tiled x6 kernel); w_split:
     ``split_deconv3`` of the packed weights (Synthesis_net_17.packed_x6). The same returns as
-    ``deconv3``."""
-    _check_split(hs, "activation")
-    _, B, h4, w4, N = hs.shape
+    ``deconv3`` (bit-identical in either input form)."""
+    cm = isinstance(hs, Tensor) and hs.dim() == 6
+    if cm:
+        if hs.dtype != torch.int16 or hs.shape[0] != 3 or hs.shape[5] != 32 or not hs.is_cuda \
+                or not hs.is_contiguous():
+            raise Iclr17Error("iclr17: a chunk-major split activation is a contiguous device int16 "
+                              "tensor [3,B,N/32,h,w,32]")
+        _, B, nch, h4, w4, _ = hs.shape
+        N = 32 * nch
+    else:
+        _check_split(hs, "activation")
+        _, B, h4, w4, N = hs.shape
     if (not isinstance(w_split, Tensor) or w_split.dtype != torch.int16
             or w_split.numel() != 3 * 9 * N * 48):
         raise Iclr17Error("iclr17: deconv3_x6 takes the split weight planes (split_deconv3)")
-    return _deconv3_halo("iclr17_synthesis_deconv3_x6", hs, B, h4, w4, N, w_split, bias, x_ref,
-                         want_recon, sse_unclipped)
+    return _deconv3_halo("iclr17_synthesis_deconv3_x6_cm" if cm else "iclr17_synthesis_deconv3_x6",
+                         hs, B, h4, w4, N, w_split, bias, x_ref, want_recon, sse_unclipped)
 
 
 def _deconv3_halo(fn, hs, B, h4, w4, N, wp, bias, x_ref, want_recon, sse_unclipped):

@@ -103,7 +103,7 @@ class Synthesis_net_17(nn.Module):
         if y_split is not None:
             q1, q2 = self.igdn1.effective_params_x6(), self.igdn2.effective_params_x6()
             hs, _, _ = kernels.deconv_igdn_x6(y_split, d1, self.deconv1.bias, *q1)
-            hs, _, _ = kernels.deconv_igdn_x6(hs, d2, self.deconv2.bias, *q2)
+            hs, _, _ = kernels.deconv_igdn_x6(hs, d2, self.deconv2.bias, *q2, chunk_major=True)
             return kernels.deconv3_x6(hs, self.packed_x6(), self.deconv3.bias, x_ref=x_ref,
                                       want_recon=want_recon)
         else:

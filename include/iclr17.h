@@ -193,6 +193,17 @@ int iclr17_synthesis_deconv_igdn_x6(const uint16_t* in_split, int B, int h, int 
                                     const float* beta_eff, const float* gamma_packed,
                                     const uint16_t* gamma_split, float* out, uint16_t* out_split,
                                     float* pre_out, void* stream);
+/* iclr17_synthesis_deconv_igdn_x6 writing the split output in the CHUNK-MAJOR split form
+ * [3][B][N/32][2h][2w][32] (the fp32 out / pre_out stay NHWC), the input layout of
+ * iclr17_synthesis_deconv3_x6_cm: a 32-channel chunk of a patch row is then contiguous, so
+ * deconv3's per-chunk patch reads do not share 128-byte lines with the next chunk's (the NHWC
+ * planes hold two chunks per line, and the second was refetched from HBM: 2.3x the bytes).
+ * Replaces the same reference lines (synthesis_17.py:19-22). */
+int iclr17_synthesis_deconv_igdn_x6_cm(const uint16_t* in_split, int B, int h, int w, int N,
+                                       const float* w_packed, const float* bias,
+                                       const float* beta_eff, const float* gamma_packed,
+                                       const uint16_t* gamma_split, float* out,
+                                       uint16_t* out_split_cm, float* pre_out, void* stream);
 /* iclr17_synthesis_deconv3 on a split-form input (the same outputs and sse_partial layout:
  * iclr17_output_partials_per_image(H, W) doubles per image). w_split: the ICLR17_W_DECONV9
  * packing split by iclr17_split_packed(taps = 9, K = N, N = 48) — [3][9][N/8][48][8]. */
@@ -200,6 +211,12 @@ int iclr17_synthesis_deconv3_x6(const uint16_t* in_split, int B, int H, int W, i
                                 const uint16_t* w_split, const float* bias, const float* x,
                                 float* clipped, float* recon, double* sse_partial,
                                 int sse_unclipped, void* stream);
+/* iclr17_synthesis_deconv3_x6 reading the chunk-major split form of
+ * iclr17_synthesis_deconv_igdn_x6_cm (synthesis_17.py:23-25); bit-identical results. */
+int iclr17_synthesis_deconv3_x6_cm(const uint16_t* in_split_cm, int B, int H, int W, int N,
+                                   const uint16_t* w_split, const float* bias, const float* x,
+                                   float* clipped, float* recon, double* sse_partial,
+                                   int sse_unclipped, void* stream);
 
 /* ---------------------------------------------------------------- entropy coding (§8 f4)
  * A real bitstream for ŷ with the factorised model the reference only uses to ESTIMATE the rate

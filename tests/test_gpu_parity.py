@@ -498,3 +498,29 @@ def test_encoder_matches_codec_forward(device, mode):
     assert y.view(2, -1).shape == (2, 192 * 24) and y_hat.view(2, -1).shape == (2, 192 * 24)
     assert torch.equal(torch.round(y), y_hat)
     assert torch.equal(recon.clamp(0.0, 1.0), clipped)
+
+
+@pytest.mark.parametrize("N", [192, 128])
+def test_chunk_major_split_deconv2_to_deconv3(device, N):
+    """deconv2+IGDN2 writing the chunk-major split form [3,B,N/32,h,w,32] (what deconv3's halo
+    kernel reads without sharing cache lines between chunks) holds exactly the NHWC split's
+    values, and deconv3_x6 gives bit-identical outputs from either form."""
+    net = net_for(N, 3, device)
+    dec = net.Decoder
+    d1, d2, d3, q1, q2 = dec.packed()
+    e2 = dec.igdn2.effective_params_x6()
+    torch.manual_seed(0)
+    h1 = (torch.randn(2, 8, 12, N) * 0.5).to(device)
+    hs = kernels.split_planes(h1)
+    with torch.no_grad():
+        s_nhwc, f_nhwc, _ = kernels.deconv_igdn_x6(hs, d2, dec.deconv2.bias, *e2, want_f32=True)
+        s_cm, f_cm, _ = kernels.deconv_igdn_x6(hs, d2, dec.deconv2.bias, *e2, want_f32=True,
+                                               chunk_major=True)
+        assert s_cm.shape == (3, 2, N // 32, 16, 24, 32)
+        assert torch.equal(f_nhwc, f_cm)
+        assert torch.equal(kernels.merge_planes(s_cm), kernels.merge_planes(s_nhwc))
+        x = image(9, 2, 64, 96).to(device)
+        a = kernels.deconv3_x6(s_nhwc, dec.packed_x6(), dec.deconv3.bias, x_ref=x, want_recon=True)
+        b = kernels.deconv3_x6(s_cm, dec.packed_x6(), dec.deconv3.bias, x_ref=x, want_recon=True)
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)

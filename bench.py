@@ -249,7 +249,8 @@ def run_train(args, net, x, world, dev):
                    "precision": ("x6: forward, input gradients, weight gradients and GDN γ "
                                  "gradients (bias/β/rate-parameter sums and Adam in fp32)"
                                  if kernels.precision() == "x6" else "exact-f32"),
-                   "parallelism": f"dp{world} (RCCL bucketed grad all-reduce overlapped with the backward)"},
+                   "parallelism": f"dp{world} ({'RCCL' if os.environ.get('ICLR17_DIST_BACKEND', 'nccl') == 'nccl' else 'gloo'} "
+                                  "bucketed grad all-reduce overlapped with the backward)"},
         "roofline": {"bound": "mfma", "kernel": "whole training step", "achieved": round(tflops, 2),
                      "peak": round(tpeak, 1), "unit": "TFLOP/s",
                      "peak_basis": ("bf16 dense MFMA peak / 6 (most of the step runs x6)" if x6t
@@ -921,11 +922,13 @@ def main() -> None:
         return
     prec = kernels.precision()
     rb = None
-    if prec == "x6" and world == 1 and not args.no_bf16_leg:
+    if prec == "x6" and not args.no_bf16_leg:
         # the bf16 throughput-mode leg runs first (reported as bf16_mode below). Its step is 4x
         # shorter and the GPU clock ramps over the first ~50 ms of load (tools/warm_probe.py:
         # bf16 0.567 → 0.465 ms, x6 2.49 → 2.06 ms per step), so it warms for at least 100 steps
-        # before its timed region; the headline's timed region then starts at steady clocks.
+        # before its timed region; the headline's timed region then starts at steady clocks. It
+        # runs at every rank count (max over ranks, whole-job rate) so that 1- and N-GPU
+        # headlines start from the same clock state.
         kernels.set_precision("bf16")
         try:
             rb = time_eval(net, x, argparse.Namespace(**{**vars(args), "warmup": max(args.warmup, 100)}),

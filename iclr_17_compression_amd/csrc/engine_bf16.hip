@@ -39,10 +39,23 @@ namespace bfm {
 #ifndef ICLR17_BF_C3KS
 #define ICLR17_BF_C3KS 2   // conv3: input-channel halves per tile, one 4-wave group each
 #endif
+#ifndef ICLR17_C1P_KBO
+#define ICLR17_C1P_KBO 1   // conv1p: GDN contraction k-block outer (x² fragments read once)
+#endif
+#ifndef ICLR17_K5_STAMPS
+#define ICLR17_K5_STAMPS 0
+#endif
+#ifndef ICLR17_C1P_STAMPS
+#define ICLR17_C1P_STAMPS 0   // diagnostic build: per-phase s_memtime stamps of conv1p
+#endif
 #ifndef ICLR17_BF_NST
 #define ICLR17_BF_NST 4   // weight ring stages (F + 2 for F DMA groups in flight)
 #endif
 
+#if ICLR17_K5_STAMPS
+// diagnostic build: per-wave s_memtime at k5_body entry, main-loop start, main-loop end, exit
+__device__ unsigned long long g_k5_stamps[8192 * 16 * 8];
+#endif
 typedef unsigned short u16;
 typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
 
@@ -60,6 +73,17 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
 }
 
 __device__ __attribute__((aligned(16))) unsigned g_zero16[4] = {0u, 0u, 0u, 0u};
+
+#ifndef ICLR17_BF_SINK4
+#define ICLR17_BF_SINK4 1
+#endif
+// A padding ("sink") load of the counted-vmcnt DMA schedule: one vector-memory instruction like
+// any other, but 4 bytes per lane (256 B into the sink) instead of a 16-byte piece (1 KB)
+__device__ __forceinline__ void sink_load(void* lds_sink) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g_zero16,
+                                   (__attribute__((address_space(3))) void*)lds_sink,
+                                   ICLR17_BF_SINK4 ? 4 : 16, 0, 0);
+}
 
 __device__ __forceinline__ f4 mfma_bf16(const u4& a, const u4& b, const f4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, a),
@@ -170,14 +194,8 @@ __global__ void __launch_bounds__(256) rate_table_kernel(const float* __restrict
   table[i] = element_bits((float)v, rate, C, c);
 }
 
-// ------------------------------------------------------------------------- GDN epilogue
-// GDN / IGDN (models/GDN.py:64-94) on a C[channel][pixel] accumulator tile: acc[nt][mt][j] is
-// channel ncol + nt·16 + 4·(lane >> 4) + j of tile pixel pix0 + mt·16 + (lane & 15). Adds the
-// bias, writes x² as bf16 into an LDS tile [R pixels][CO] (row stride CO·2 + 32 bytes: the
-// 16-lane fragment reads hit distinct banks; the 8-byte writes are 4-way), contracts it
-// with γ_eff (bf16 A fragments from L2, a whole 16-channel block's fragments one block ahead),
-// forms x·rsqrt(β+n) or x·sqrt(β+n) in fp32 and stores the bf16 rows through the same tile,
-// 16 bytes per lane. Entry: LDS free (caller's barrier).
+// ---------------------------------------------------------------- x² / output tile layout
+// [R pixels][CO] bf16 rows of stride CO·2 + 32 bytes: 16-lane fragment reads hit distinct banks
 template <int CO>
 __device__ __forceinline__ int epi_off(int p, int ch) {   // byte offset of (pixel, channel)
   return p * (CO * 2 + 32) + ch * 2;
@@ -185,83 +203,6 @@ __device__ __forceinline__ int epi_off(int p, int ch) {   // byte offset of (pix
 
 template <int CO>
 constexpr int epi_tile_bytes(int R) { return R * (CO * 2 + 32); }
-
-template <int CO, int MT, int NT, int NTHR, bool INV, class PixFn>
-__device__ __forceinline__ void gdn_epilogue_bf16(f4 (&acc)[NT][MT], unsigned char* sq,
-                                                  const float* __restrict__ bias,
-                                                  const float* __restrict__ beta,
-                                                  const u16* __restrict__ gamma, u16* out, int R,
-                                                  int pix0, int ncol, PixFn out_pixel) {
-  typedef const __attribute__((address_space(3))) u4* lu4p;
-  const int tid = threadIdx.x, lane = tid & 63, kg = lane >> 4;
-  constexpr int KB = CO / 32;
-  // γ fragments: k-groups 4·kb + kg, rows ncol + nt·16 + lane & 15
-  const u16* gb = gamma + (kg * CO + ncol + (lane & 15)) * 8;
-#pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    const int ch = ncol + nt * 16 + 4 * kg;
-    const f4 bv = bias ? *(const f4*)(bias + ch) : f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      acc[nt][mt] += bv;
-      const f4 v = acc[nt][mt];
-      const int p = pix0 + mt * 16 + (lane & 15);
-      *(uint2*)(sq + epi_off<CO>(p, ch)) = uint2{pack_bf2(v[0] * v[0], v[1] * v[1]),
-                                                 pack_bf2(v[2] * v[2], v[3] * v[3])};
-    }
-  }
-  u4 gf[KB];
-#pragma unroll
-  for (int kb = 0; kb < KB; ++kb) gf[kb] = *(const u4*)(gb + (long)kb * 4 * CO * 8);
-  __syncthreads();
-  // n[i][p] = Σ_j γ[i][j]·x²[j][p]: A = γ (rows i), B = x² (k = j); γ fragment kb of block nt+1
-  // is loaded into the register fragment kb of block nt frees (about KB iterations ahead)
-  const int pl = pix0 + (lane & 15);
-#pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    f4 nacc[MT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) nacc[mt] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kb = 0; kb < KB; ++kb) {
-      u4 xs[MT];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) xs[mt] = *(lu4p)(sq + epi_off<CO>(pl + mt * 16, 32 * kb + 8 * kg));
-      const u4 gc = gf[kb];
-      if (nt + 1 < NT) gf[kb] = *(const u4*)(gb + (long)kb * 4 * CO * 8 + (nt + 1) * 128);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) nacc[mt] = mfma_bf16(gc, xs[mt], nacc[mt]);
-    }
-    const int ch = ncol + nt * 16 + 4 * kg;
-    const f4 be = *(const f4*)(beta + ch);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float n = nacc[mt][j] + be[j];
-        acc[nt][mt][j] *= INV ? __builtin_amdgcn_sqrtf(n) : __builtin_amdgcn_rsqf(n);
-      }
-  }
-  __syncthreads();   // x² reads done: the tile is rewritten with the output
-#pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    const int ch = ncol + nt * 16 + 4 * kg;
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const f4 y = acc[nt][mt];
-      const int p = pix0 + mt * 16 + (lane & 15);
-      *(uint2*)(sq + epi_off<CO>(p, ch)) = uint2{pack_bf2(y[0], y[1]), pack_bf2(y[2], y[3])};
-    }
-  }
-  __syncthreads();
-  constexpr int PCS = CO * 2 / 16;   // 16-byte pieces per pixel row
-  for (int idx = tid; idx < R * PCS; idx += NTHR) {
-    const int p = idx / PCS, pc = idx - p * PCS;
-    const long o = out_pixel(p);
-    if (o < 0) continue;
-    *(u4*)(out + o * CO + pc * 8) = *(lu4p)(sq + epi_off<CO>(p, pc * 8));
-  }
-}
 
 // ------------------------------------------------------------------------------ kernel
 // One workgroup: a TH × 16 tile of base pixels (conv: output pixels; deconv: input pixels of
@@ -297,7 +238,11 @@ struct K5 {
   static constexpr int GOFF = EARLY_G ? MAIN_LDS : 0;
   static constexpr int EPI_LDS = EPI == BE_QUANT ? 64
                                  : (GOFF + GBLK * 1024 > R * OS ? GOFF + GBLK * 1024 : R * OS);
-  static constexpr int LDS = KS * MAIN_LDS > EPI_LDS ? KS * MAIN_LDS : EPI_LDS;
+  static constexpr int LDS0 = KS * MAIN_LDS > EPI_LDS ? KS * MAIN_LDS : EPI_LDS;
+  // GDN: bias and β_eff staged by two prologue DMAs into their own 2 KB (an epilogue global load
+  // of them waited out a full L2 round trip after the main loop)
+  static constexpr int BBOFF = (LDS0 + 1023) / 1024 * 1024;
+  static constexpr int LDS = EPI == BE_QUANT ? LDS0 : BBOFF + 2048;
   static_assert(KS == 1 || (KS - 1) * NW * NT * 16 * 64 * 4 <= KS * MAIN_LDS, "K-split exchange");
   static_assert(TH % 2 == 0 && NB % 32 == 0 && SB % 1024 == 0 && CI % (16 * KS) == 0, "tile shape");
   static_assert(EPI == BE_QUANT || NB == CO, "GDN needs every channel of a pixel in the tile");
@@ -358,9 +303,13 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
   };
   // patch piece of chunk c1 (valid) or a sink load (not valid: same instruction count)
   auto issue_piece = [&](int c1, int piece, bool valid) {
-    const int src = piece_src(valid ? piece : 0);
-    glds16(src >= 0 && valid ? (const void*)(inb + src + c1 * 16) : (const void*)g_zero16,
-           valid ? sP + (c1 & 1) * P::BUF + piece * 1024 : sD);
+    if (!valid) {
+      sink_load(sD);
+      return;
+    }
+    const int src = piece_src(piece);
+    glds16(src >= 0 ? (const void*)(inb + src + c1 * 16) : (const void*)g_zero16,
+           sP + (c1 & 1) * P::BUF + piece * 1024);
   };
   // weight slots: slot k·NW + wave < NBI of a group copies 1 KB of the step's [4][NB][8] slice
   const long wstep = 4L * CO * 8;                     // u16 per (chunk, step) of the packing
@@ -385,13 +334,17 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
   // weight slot k of step wg; past the last step a load of the last step into the sink
   auto issue_w = [&](int k, int wg) {
     const int slot = k * NW + wave;
-    glds16(wph + (long)(wg < GS ? wg : GS - 1) * wstep + wsrc[k],
-           wg < GS ? sB + (wg % NST) * SB + slot * 1024 : sD);
+    if (wg >= GS) {
+      sink_load(sD);
+      return;
+    }
+    glds16(wph + (long)wg * wstep + wsrc[k], sB + (wg % NST) * SB + slot * 1024);
   };
 
   // ---- per-lane fragment addresses
   // B (pixels): pixel (tile row 2·wave + (r32 >> 4), column r32 & 15), channel half h
   const int prow = 2 * wave + (r32 >> 4), pcol = r32 & 15;
+  const int tpix = prow * 16 + pcol;   // tile pixel of this lane's accumulator column
   const int pbase = (MODE == BM_CONV ? P::off(2 * prow, 2 * pcol) : P::off(prow, pcol)) + h * P::HALF;
   // A (weights): stage [4][NB][8]: lane (k-group 2·tap + h, channel 32·i + r32)
   const int abase = (h * NB + r32) * 16;
@@ -411,6 +364,18 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
       glds16(a.gamma + ((long)(2 * kb + h) * CO + 32 * i + r32) * 8, smem + KK::GOFF + blk * 1024);
     }
   };
+#if ICLR17_K5_STAMPS
+  const unsigned long long st0 = __builtin_amdgcn_s_memtime();
+#endif
+  float* const sbb = (float*)(smem + KK::BBOFF);   // GDN: [bias CO | pad][β_eff CO | pad]
+  if constexpr (EPI != BE_QUANT) {
+    // waves 0 / 1: one 16-byte piece per lane (CO ≤ 256 floats); retired by the first counted wait
+    static_assert(CO <= 256, "bias / β stage");
+    if (wave < 2) {
+      const float* src = wave == 0 ? a.bias : a.beta;
+      glds16(lane * 4 < CO ? (const void*)(src + lane * 4) : (const void*)g_zero16, sbb + wave * 256);
+    }
+  }
   if constexpr (KK::EARLY_G) stage_gamma();   // retired by the loop's first counted wait
   // prologue: chunk 0's patch and the weights of steps 0 .. F-1 (any count per wave), then
   // step F's weights as a full K-group, so the loop's first wait leaves exactly F groups
@@ -423,14 +388,17 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     if (k * NW + wave < NBI) issue_w(k, F);
-    else glds16(g_zero16, sD);
+    else sink_load(sD);
   }
 #pragma unroll
   for (int f = 1; f < F; ++f)   // F−1 more full groups: the first wait keeps F in flight
 #pragma unroll
-    for (int k = 0; k < K; ++k) glds16(g_zero16, sD);
+    for (int k = 0; k < K; ++k) sink_load(sD);
 
   typedef const __attribute__((address_space(3))) u4* lu4p;
+#if ICLR17_K5_STAMPS
+  const unsigned long long st1 = __builtin_amdgcn_s_memtime();
+#endif
   int stage = 0;   // g % NST
   for (int c = 0; c < NCH; ++c) {
     const unsigned char* pbuf = sP + (c & 1) * P::BUF + pbase;
@@ -448,7 +416,7 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
           const int piece = s * PS + slot - NBI;
           issue_piece(c + 1, piece, c + 1 < NCH && piece < P::NQI);
         } else {
-          glds16(g_zero16, sD);
+          sink_load(sD);
         }
       }
       // taps 2s and 2s+1 (the second absent in the last step of an odd tap count): one k16
@@ -474,15 +442,19 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
     }
   }
   vm_barrier();   // the trailing sink loads landed and every wave is done with the stages
+#if ICLR17_K5_STAMPS
+  const unsigned long long st2 = __builtin_amdgcn_s_memtime();
+  unsigned long long st4 = st2, st5 = st2, stg = st2;
+#endif
 
-  // ---- epilogue. acc[i][4m + j]: channel nb·NB + 32i + 8m + 4h + j of tile pixel 32·wave + r32
+  // ---- epilogue. acc[i][4m + j]: channel nb·NB + 32i + 8m + 4h + j of tile pixel tpix
   auto out_pixel = [&](int p) -> long {   // NHWC pixel index, or -1 outside the grid
     const int gy = ty * TH + (p >> 4), gx = tx * 16 + (p & 15);
     if (gy >= a.gh || gx >= a.gw) return -1;
     if (MODE == BM_CONV) return ((long)b * a.Hout + gy) * a.Wout + gx;
     return ((long)b * a.Hout + 2 * gy + (PH >> 1)) * a.Wout + 2 * gx + (PH & 1);
   };
-  const long o = out_pixel(32 * wave + r32);
+  const long o = out_pixel(tpix);
   if constexpr (EPI == BE_GDN || EPI == BE_IGDN) {
     // GDN / IGDN (models/GDN.py:64-94): n[i][p] = Σ_j γ[i][j]·x²[j][p] with γ_eff in bf16 as
     // the A operand from LDS and x² (bias added, squared, rounded to bf16) as the B operand
@@ -497,7 +469,7 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
     for (int i = 0; i < NT; ++i) {
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
-        const f4 bv = *(const f4*)(a.bias + 32 * i + 8 * m + 4 * h);
+        const f4 bv = *(const f4*)(sbb + 32 * i + 8 * m + 4 * h);
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][4 * m + j] += bv[j];
       }
@@ -515,6 +487,9 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
       }
     }
     if constexpr (!KK::EARLY_G) vm_barrier();   // γ of every wave landed
+#if ICLR17_K5_STAMPS
+    stg = __builtin_amdgcn_s_memtime();
+#endif
     const unsigned char* sg = smem + KK::GOFF + lane * 16;
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
@@ -529,7 +504,7 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const int ch = 32 * i + 8 * m + 4 * h;
-        const f4 be = *(const f4*)(a.beta + ch);
+        const f4 be = *(const f4*)(sbb + 256 + ch);
         f4 y;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -541,10 +516,13 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
         for (int j = 0; j < 4; ++j) acc[i][4 * m + j] = y[j];
       }
     }
+#if ICLR17_K5_STAMPS
+    st4 = __builtin_amdgcn_s_memtime();
+#endif
     // y through an LDS tile [pixel][channel] (row stride OS) to whole-row 16-byte stores
     __syncthreads();   // every wave's γ reads done: the tile reuses the γ blocks
     constexpr int OS = KK::OS;
-    unsigned char* const row = smem + (32 * wave + r32) * OS + 8 * h;
+    unsigned char* const row = smem + tpix * OS + 8 * h;
 #pragma unroll
     for (int i = 0; i < NT; ++i)
 #pragma unroll
@@ -552,6 +530,9 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
         *(uint2*)(row + (32 * i + 8 * m) * 2) =
             uint2{pack_bf2(acc[i][4 * m], acc[i][4 * m + 1]), pack_bf2(acc[i][4 * m + 2], acc[i][4 * m + 3])};
     __syncthreads();
+#if ICLR17_K5_STAMPS
+    st5 = __builtin_amdgcn_s_memtime();
+#endif
     constexpr int PCS = CO * 2 / 16;   // 16-byte pieces per pixel row
     for (int idx = tid; idx < KK::R * PCS; idx += KK::NT_) {
       const int p = idx / PCS, pc = idx - p * PCS;
@@ -614,6 +595,14 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
       a.partial[(long)b * a.ppi + tile * (CO / NB) + nb] = sum;
     }
   }
+#if ICLR17_K5_STAMPS
+  const unsigned long long st3 = __builtin_amdgcn_s_memtime();
+  const long wg = blockIdx.x + (long)blockIdx.y * gridDim.x;
+  if (lane == 0 && wg < 8192) {
+    unsigned long long* d = g_k5_stamps + (wg * 16 + wv) * 8;
+    d[0] = st0; d[1] = st1; d[2] = st2; d[3] = st3; d[4] = stg; d[5] = st4; d[6] = st5;
+  }
+#endif
 }
 
 template <int MODE, int TH, int NB, int CO, int CI, int EPI>
@@ -643,141 +632,336 @@ k5_bf16_kernel(const K5Args a) {
 }
 
 // ------------------------------------------------------------------------------ conv1
-// analysis_17.py:14-17 conv1 (3→N, k9 s4 p4) + GDN1 in bf16. An 8×8 output block per
-// workgroup (4 waves, each all 64 pixels × N/4 channels). The 37×37×3 input patch lands in LDS
-// by LDS-DMA as fp32 and is rounded once into one bf16 plane [3·37][40]. K = 243 is reordered
+// analysis_17.py:14-17 conv1 (3→N, k9 s4 p4) + GDN1 in bf16 on 8×8 output blocks. The 37×37×3
+// input patch is rounded once into one bf16 plane [3·37][40]. K = 243 is reordered
 // (ICLR17_W_CONV1_X6 packing): k-group g = 4s + (lane >> 4) is 8 consecutive patch columns of
 // one (channel, kernel row) pair for g < 27, zero for g = 27, and for g = 28..31 the kw = 8
-// column of 8 pairs gathered element-wise. The weight fragments [32][N][8] bf16 come from L2
-// one step ahead (no LDS stage, no barrier in the 8-step loop).
+// column of 8 pairs gathered element-wise; weight fragments [32][N][8] bf16.
 constexpr int C1P = 37;                       // patch side: 8·4 + 9 − 4
 constexpr int C1RS = 40;                      // row stride (elements): 10 16-byte fp32 pieces
 constexpr int C1PIECES = 3 * C1P * 10;        // fp32 16-byte pieces of the patch (1110)
-constexpr int C1NI = (C1PIECES + 63) / 64;    // LDS-DMA wave-instructions (18)
 constexpr int C1U = 3 * C1P * C1RS;           // u16 elements of the bf16 plane (4440)
 
+// ---------------------------------------------------------------- conv1, persistent form
+// One 8×8 block: 64 pixels × CO channels on 8 waves, v_mfma_f32_16x16x32_bf16 (A = weights,
+// B = pixels), the GDN contraction n = γ·x² on the same MFMA through an x² tile in LDS. Round 3
+// made it persistent (bit-identical to the round-2 one-block-per-workgroup kernel, 0.091 →
+// 0.080 ms at B=64) so that nothing per block waits on L2 or HBM. One 8-wave workgroup per CU walks the 8×8 output blocks t = blockIdx.x,
+// + gridDim.x, …:
+//   * each wave holds its weight slice in registers for the whole kernel (wave w: channels
+//     (w & 3)·CO/4 .. +CO/4 of pixel half w >> 2; 8 steps × CO/64 fragments, 96 VGPRs at N = 192)
+//     and γ_eff (bf16, 72 KB) sits in LDS, both loaded once: no per-block weight or γ refetch
+//     from L2 (165 KB per 64-pixel block in the one-block-per-workgroup form);
+//   * the next block's 37×37×3 fp32 patch is loaded into registers while this block computes,
+//     and rounded into the idle bf16 plane after this block's epilogue (double-buffered plane);
+//   * the output rows leave as 16-byte stores that drain during the next block.
+// analysis_17.py:14-17 (conv1) + models/GDN.py:64-94 (GDN1).
+constexpr int C1P_WAVES = 8;
+constexpr int C1P_STK = 20, C1P_STP = 5;   // stamps: blocks per workgroup, phases per block
+#if ICLR17_C1P_STAMPS
+__device__ unsigned long long g_c1p_stamps[1024 * C1P_WAVES * C1P_STK * C1P_STP];
+#endif
+constexpr int C1P_LOADS = (C1PIECES + C1P_WAVES * 64 - 1) / (C1P_WAVES * 64);   // 3 per thread
+
 template <int CO>
-struct C1 {
-  static constexpr int LAND = C1NI * 1024;            // fp32 landing area (bytes)
-  static constexpr int PLANE = C1U * 2;                // bf16 plane (bytes)
-  static constexpr int MAIN = LAND + PLANE;
-  static constexpr int EPI = epi_tile_bytes<CO>(64);
-  static constexpr int LDS = MAIN > EPI ? MAIN : EPI;
+struct C1PL {
+  static constexpr int G = CO * CO * 2;                   // γ_eff bf16 [CO/8][CO][8]
+  static constexpr int PL = C1U * 2;                      // one bf16 plane
+  static constexpr int SQ = epi_tile_bytes<CO>(64);       // x² / output tile
+  static constexpr int BB = CO * 8;                       // bias, β_eff (fp32)
+  static constexpr int ST = ICLR17_C1P_STAMPS ? C1P_WAVES * C1P_STK * C1P_STP * 8 : 0;
+  static constexpr int LDS = G + 2 * PL + SQ + BB + ST;
+  static_assert(G % 1024 == 0 && LDS <= 160 * 1024, "conv1p LDS");
 };
 
-template <int CO>
-__global__ void __launch_bounds__(256, 2) conv1_bf16_kernel(const float* __restrict__ x, int H,
-                                                            int W, const u16* __restrict__ wbf,
-                                                            const float* __restrict__ bias,
-                                                            const float* __restrict__ beta,
-                                                            const u16* __restrict__ gamma,
-                                                            u16* __restrict__ out, int tiles_x,
-                                                            int tiles_y) {
-  constexpr int MT = 4, NT = CO / 4 / 16;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[C1<CO>::LDS];
-  float* sr = (float*)smem;                                // fp32 landing area
-  u16* sp = (u16*)(smem + C1<CO>::LAND);                   // bf16 plane
+// threadIdx.x re-materialised where it is used: keeps the compiler from hoisting per-lane
+// address arithmetic out of a loop into registers it then spills (a scratch reload is a VMEM op,
+// and its vmcnt wait would also wait for every load in flight)
+__device__ __forceinline__ int fresh_tid() {
+  int v;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "v"((int)threadIdx.x));
+  return v;
+}
+
+template <int CO, bool FULL>   // FULL: the output grid is whole 8×8 blocks (no store guard)
+__global__ void __launch_bounds__(C1P_WAVES * 64, 1)
+conv1p_bf16_kernel(const float* __restrict__ x, int H, int W, const u16* __restrict__ wbf,
+                   const float* __restrict__ bias, const float* __restrict__ beta,
+                   const u16* __restrict__ gamma, u16* __restrict__ out, int tiles_x, int tiles_y,
+                   int ntiles) {
+  constexpr int MT = 2, NT = CO / 4 / 16, KB = CO / 32, NTHR = C1P_WAVES * 64;
+  using L = C1PL<CO>;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[L::LDS];
+  typedef const __attribute__((address_space(3))) u4* lu4p;
+  unsigned char* const sg = smem;                          // γ
+  u16* const sp0 = (u16*)(smem + L::G);                    // planes 0, 1
+  unsigned char* const sq = smem + L::G + 2 * L::PL;       // x² / output tile
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  int bid = blockIdx.x;
-  const int tx = bid % tiles_x;
-  bid /= tiles_x;
-  const int ty = bid % tiles_y;
-  const int b = bid / tiles_y;
-  const int ncol = wave * (CO / 4);
-  const int iy0 = ty * 32 - 4, ix0 = tx * 32 - 4;
-  // patch by LDS-DMA: piece (c, r, q) = columns 4q .. 4q+3 of patch row r of channel c; the
-  // patch origin ix0 ≡ 0 (mod 4) and W ≡ 0 (mod 16): a piece is wholly in or out of the image
-#pragma unroll
-  for (int j = 0; j < (C1NI + 3) / 4; ++j) {
-    const int i = wave + 4 * j;
-    if (i < C1NI) {
-      const int pc = i * 64 + lane;
-      const int cr = pc / 10, q = pc - cr * 10;
-      const int c = cr / C1P, r = cr - c * C1P;
-      const int iy = iy0 + r, ix = ix0 + 4 * q;
-      const bool ok = pc < C1PIECES && iy >= 0 && iy < H && ix >= 0 && ix < W;
-      glds16(ok ? (const void*)(x + (((long)b * 3 + c) * H + iy) * W + ix) : (const void*)g_zero16,
-             sr + i * 256);
-    }
+  const int cg = wave & 3, half = wave >> 2;
+  const int ncol = cg * (CO / 4), kg = lane >> 4;
+  // bias and β_eff in LDS: a global load of them inside the block loop would be younger than the
+  // next block's patch loads, and its use would wait (in-order vmcnt) for those HBM reads
+  float* const sbias = (float*)(sq + L::SQ);
+  float* const sbeta = sbias + CO;
+  if (tid < CO) {
+    sbias[tid] = bias[tid];
+    sbeta[tid] = beta[tid];
   }
-  // weight fragments: lane (k-group lane >> 4, channel ncol + nt·16 + lane & 15)
-  const u16* gb = wbf + ((lane >> 4) * CO + ncol + (lane & 15)) * 8;
-  u4 w0[NT], w1[NT];
-  auto loadw = [&](int s, u4 (&w)[NT]) {
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) w[nt] = *(const u4*)(gb + (long)s * 4 * CO * 8 + nt * 128);
-  };
-  loadw(0, w0);
-  vm_barrier();   // patch landed
-  for (int pc = tid; pc < C1PIECES; pc += 256) {   // round once into the bf16 plane
-    const f4 v = *(const f4*)(sr + pc * 4);
-    *(uint2*)(sp + pc * 4) = uint2{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
-  }
-  __syncthreads();
 
-  f4 acc[NT][MT];
+  // γ into LDS (1 KB per wave-instruction), retired by the first vm_barrier
+  for (int blk = wave; blk < L::G / 1024; blk += C1P_WAVES) glds16(gamma + blk * 512 + lane * 8, sg + blk * 1024);
+  // this wave's weight fragments: step s, channel tile nt (k-group 4s + kg, channel ncol + nt·16 + lane & 15)
+  u4 wr[8][NT];
+  {
+    const u16* gb = wbf + (kg * CO + ncol + (lane & 15)) * 8;
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt)
+    for (int s = 0; s < 8; ++s)
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = f4{0.f, 0.f, 0.f, 0.f};
+      for (int nt = 0; nt < NT; ++nt) wr[s][nt] = *(const u4*)(gb + (long)s * 4 * CO * 8 + nt * 128);
+  }
+  // patch pieces of block t into registers: piece (c, r, q) = columns 4q .. 4q+3 of patch row r
+  // of channel c; the patch origin ≡ 0 (mod 4) and W ≡ 0 (mod 16): a piece is wholly in or out
+  f4 pr[C1P_LOADS];
+  int okm = 0;   // bit j: piece j is inside the image
+  // (uniform image base + 32-bit lane offsets: no 64-bit per-lane addresses to hold or spill)
+  // per-lane piece geometry, computed once: offset within the image and (row, column) in the patch
+  int poff[C1P_LOADS], prc[C1P_LOADS];
+#pragma unroll
+  for (int j = 0; j < C1P_LOADS; ++j) {
+    const int pc = tid + j * NTHR;
+    const int cr = pc / 10, q = pc - cr * 10;
+    const int c = cr / C1P, r = cr - c * C1P;
+    poff[j] = (c * H + r) * W + 4 * q;
+    prc[j] = pc < C1PIECES ? r | (4 * q) << 8 : -1;
+  }
+  auto load_patch = [&](int t) {
+    const int tx = t % tiles_x, ty = (t / tiles_x) % tiles_y, b = t / (tiles_x * tiles_y);
+    const int iy0 = ty * 32 - 4, ix0 = tx * 32 - 4;
+    const float* __restrict__ xb = x + (long)b * 3 * H * W;
+    const int o0 = iy0 * W + ix0;
+#pragma unroll
+    for (int j = 0; j < C1P_LOADS; ++j) {
+      const bool ok = prc[j] >= 0 && (unsigned)(iy0 + (prc[j] & 255)) < (unsigned)H &&
+                      (unsigned)(ix0 + (prc[j] >> 8)) < (unsigned)W;
+      // no branch, and no use of the value before store_plane (a select here made the compiler
+      // wait for the load in the middle of this block's main loop)
+      pr[j] = *(const f4*)(xb + (ok ? poff[j] + o0 : 0));
+      okm = j == 0 ? (int)ok : okm | ((int)ok << j);
+    }
+  };
+  auto store_plane = [&](u16* sp) {   // round once into the bf16 plane
+    const int ft = fresh_tid();
+#pragma unroll
+    for (int j = 0; j < C1P_LOADS; ++j) {
+      const int pc = ft + j * NTHR;
+      const f4 v = (okm >> j) & 1 ? pr[j] : f4{0.f, 0.f, 0.f, 0.f};
+      if (pc < C1PIECES) *(uint2*)(sp + pc * 4) = uint2{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+    }
+  };
+  int t = blockIdx.x;
+  load_patch(t);
+  store_plane(sp0);
+  vm_barrier();   // γ landed, plane 0 written
+
   int pix[MT];   // output pixel (my, mx) → patch row 4·my, column 4·mx
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
-    const int m = mt * 16 + (lane & 15);
+    const int m = (MT * half + mt) * 16 + (lane & 15);
     pix[mt] = (m >> 3) * 4 * C1RS + (m & 7) * 4;
   }
-  const int kg = lane >> 4;
   auto pair_off = [](int p) { return ((p / 9) * C1P + p % 9) * C1RS; };
-  auto mfma_all = [&](int mt, const u4& px, const u4 (&w)[NT]) {
+  const int ho = H / 4, wo = W / 4;
+  // Per block: main loop (MFMA, A = the weights in registers, B = the bf16 plane), GDN
+  // epilogue (each pixel half on its 4 waves: x² rows, contraction with γ from LDS, output rows),
+  // next plane, output stores by all waves.
+  f4 acc[NT][MT];
+  auto main_tile = [&](const u16* sp) {
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) acc[nt][mt] = mfma_bf16(w[nt], px, acc[nt][mt]);
-  };
-  auto step_rows = [&](int s, const u4 (&w)[NT]) {
-    const int g = 4 * s + kg;
-    const int po = pair_off(g < 27 ? g : 26);
+    for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const u16* e = sp + po + pix[mt];
-      const uint2 lo2 = *(const uint2*)e, hi2 = *(const uint2*)(e + 4);
-      mfma_all(mt, u4{lo2.x, lo2.y, hi2.x, hi2.y}, w);
+      for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 7; ++s) {
+      const int g = 4 * s + kg;
+      const int po = pair_off(g < 27 ? g : 26);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const u16* e = sp + po + pix[mt];
+        const uint2 lo2 = *(const uint2*)e, hi2 = *(const uint2*)(e + 4);
+        const u4 px = u4{lo2.x, lo2.y, hi2.x, hi2.y};
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[nt][mt] = mfma_bf16(wr[s][nt], px, acc[nt][mt]);
+      }
+      __builtin_amdgcn_sched_barrier(0);   // one step's fragments live at a time (register budget)
     }
-  };
-  auto step_col8 = [&](const u4 (&w)[NT]) {
-    int po[8];
+    int po8[8];   // kw = 8 column: pair offsets of k-group 28 + kg
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int p = 8 * kg + e;
-      po[e] = pair_off(p < 27 ? p : 26) + 8;
+      po8[e] = pair_off(p < 27 ? p : 26) + 8;
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       u4 v;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const unsigned lo = sp[po[2 * i] + pix[mt]], hi = sp[po[2 * i + 1] + pix[mt]];
+        const unsigned lo = sp[po8[2 * i] + pix[mt]], hi = sp[po8[2 * i + 1] + pix[mt]];
         v[i] = lo | (hi << 16);
       }
-      mfma_all(mt, v, w);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[nt][mt] = mfma_bf16(wr[7][nt], v, acc[nt][mt]);
     }
   };
-  loadw(1, w1); step_rows(0, w0);
-  loadw(2, w0); step_rows(1, w1);
-  loadw(3, w1); step_rows(2, w0);
-  loadw(4, w0); step_rows(3, w1);
-  loadw(5, w1); step_rows(4, w0);
-  loadw(6, w0); step_rows(5, w1);
-  loadw(7, w1); step_rows(6, w0);
-  step_col8(w1);
-  __syncthreads();   // plane reads done before the epilogue reuses LDS
-  const int Ho = H / 4, Wo = W / 4;
-  auto out_pixel = [&](int p) -> long {
-    const int oy = ty * 8 + (p >> 3), ox = tx * 8 + (p & 7);
-    if (oy >= Ho || ox >= Wo) return -1;
-    return ((long)b * Ho + oy) * Wo + ox;
+  // GDN epilogue of this half's 32 pixels (bias, x² rows in bf16, n = γ·x² with γ from LDS,
+  // x·rsqrt(β + n)); this half's rows of the x² / output tile
+  const int pix0 = MT * 16 * half;
+  auto epi_tile = [&]() {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int ch = ncol + nt * 16 + 4 * kg;
+      const f4 bv = *(const f4*)(sbias + ch);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        acc[nt][mt] += bv;
+        const f4 v = acc[nt][mt];
+        const int p = pix0 + mt * 16 + (lane & 15);
+        *(uint2*)(sq + epi_off<CO>(p, ch)) = uint2{pack_bf2(v[0] * v[0], v[1] * v[1]),
+                                                   pack_bf2(v[2] * v[2], v[3] * v[3])};
+      }
+    }
+    __syncthreads();   // x² rows of this half complete
+    const int pl = pix0 + (lane & 15);
+    const unsigned char* ga = sg + ((kg * CO + ncol + (lane & 15)) * 8) * 2;
+    if (ICLR17_C1P_KBO) {
+      // k-block outer: each x² fragment is read once for all NT channel tiles (not once per
+      // tile); the same per-accumulator k order, so the same bits
+      f4 nacc[NT][MT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) nacc[nt][mt] = f4{0.f, 0.f, 0.f, 0.f};
+      u4 xs[2][MT], gc[2][NT];
+      auto rd = [&](int kb, int q) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) xs[q][mt] = *(lu4p)(sq + epi_off<CO>(pl + mt * 16, 32 * kb + 8 * kg));
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) gc[q][nt] = *(lu4p)(ga + (kb * 4 * CO * 8 + nt * 128) * 2);
+      };
+      rd(0, 0);
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        if (kb + 1 < KB) rd(kb + 1, (kb + 1) & 1);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) nacc[nt][mt] = mfma_bf16(gc[kb & 1][nt], xs[kb & 1][mt], nacc[nt][mt]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int ch = ncol + nt * 16 + 4 * kg;
+        const f4 be = *(const f4*)(sbeta + ch);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[nt][mt][j] *= __builtin_amdgcn_rsqf(nacc[nt][mt][j] + be[j]);
+      }
+    } else {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      f4 nacc[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) nacc[mt] = f4{0.f, 0.f, 0.f, 0.f};
+      // fragments of k-block kb + 1 read while kb's MFMAs run; no deeper (register budget)
+      u4 xs[2][MT], gc[2];
+      auto rd = [&](int kb, int q) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) xs[q][mt] = *(lu4p)(sq + epi_off<CO>(pl + mt * 16, 32 * kb + 8 * kg));
+        gc[q] = *(lu4p)(ga + (kb * 4 * CO * 8 + nt * 128) * 2);
+      };
+      rd(0, 0);
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        if (kb + 1 < KB) rd(kb + 1, (kb + 1) & 1);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) nacc[mt] = mfma_bf16(gc[kb & 1], xs[kb & 1][mt], nacc[mt]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      const int ch = ncol + nt * 16 + 4 * kg;
+      const f4 be = *(const f4*)(sbeta + ch);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[nt][mt][j] *= __builtin_amdgcn_rsqf(nacc[mt][j] + be[j]);
+    }
+    }
+    __syncthreads();   // x² reads done: the rows are rewritten with the output
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int ch = ncol + nt * 16 + 4 * kg;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const f4 y = acc[nt][mt];
+        const int p = pix0 + mt * 16 + (lane & 15);
+        *(uint2*)(sq + epi_off<CO>(p, ch)) = uint2{pack_bf2(y[0], y[1]), pack_bf2(y[2], y[3])};
+      }
+    }
+    __syncthreads();   // output rows complete (stored by copy_out after the segment barrier)
   };
-  gdn_epilogue_bf16<CO, MT, NT, 256, false>(acc, smem, bias, beta, gamma, out, 64, 0, ncol,
-                                            out_pixel);
+  // the block's output rows by all 512 threads, 16 bytes per piece, the same count on every
+  // wave: the stores sit on the common path, so the vmcnt waits of the next plane count them
+  // exactly and never wait for them
+  auto copy_out = [&](int t) {
+    const int tx = t % tiles_x, ty = (t / tiles_x) % tiles_y, b = t / (tiles_x * tiles_y);
+    u16* __restrict__ ob = out + (long)b * ho * wo * CO;
+    constexpr int Q = CO / 8;                 // 16-byte pieces per pixel row
+    static_assert((64 * Q) % NTHR == 0, "copy_out pieces");
+    const int ft = fresh_tid();
+#pragma unroll
+    for (int j = 0; j < 64 * Q / NTHR; ++j) {
+      const int i = ft + j * NTHR;
+      const int p = i / Q, c8 = i % Q;
+      const int oy = ty * 8 + (p >> 3), ox = tx * 8 + (p & 7);
+      const u4 v = *(lu4p)(sq + epi_off<CO>(p, c8 * 8));
+      if (FULL || (oy < ho && ox < wo)) *(u4*)(ob + (oy * wo + ox) * CO + c8 * 8) = v;
+    }
+  };
+  const int G = gridDim.x;
+#if ICLR17_C1P_STAMPS
+  unsigned long long* const stl = (unsigned long long*)(sbeta + CO);   // [wave][k][phase] in LDS
+  auto stamp = [&](int k, int ph) {
+    const unsigned long long tm = __builtin_amdgcn_s_memtime();
+    if (lane == 0 && k < C1P_STK) stl[(wave * C1P_STK + k) * C1P_STP + ph] = tm;
+  };
+#else
+  auto stamp = [](int, int) {};
+#endif
+  {
+    int k = 0;
+    for (int t = blockIdx.x; t < ntiles; t += G, ++k) {
+      const int tn = t + G;
+      // the next block's patch, in flight during this block (past the last block: a repeat of
+      // this one), rounded into the idle plane after the epilogue
+      load_patch(tn < ntiles ? tn : t);
+      stamp(k, 0);
+      main_tile(sp0 + (k & 1) * C1U);
+      stamp(k, 1);
+      epi_tile();
+      stamp(k, 2);
+      store_plane(sp0 + ((k + 1) & 1) * C1U);
+      stamp(k, 3);
+      copy_out(t);
+      __syncthreads();   // next plane written, output rows read
+      stamp(k, 4);
+    }
+#if ICLR17_C1P_STAMPS
+    __syncthreads();
+    for (int i = tid; i < C1P_WAVES * C1P_STK * C1P_STP; i += NTHR)
+      g_c1p_stamps[(long)blockIdx.x * C1P_WAVES * C1P_STK * C1P_STP + i] = stl[i];
+#endif
+    return;
+  }
 }
 
 // ------------------------------------------------------------------------------ packing
@@ -852,6 +1036,19 @@ __global__ void __launch_bounds__(256) to_bf16_kernel(const float* __restrict__ 
 }
 
 // ------------------------------------------------------------------------------ launchers
+// compute units of the current device (persistent grids), cached per device
+static int cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] <= 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
 template <int N>
 int launch_conv2(const K5Args& a0, hipStream_t st) {
   K5Args a = a0;
@@ -891,6 +1088,21 @@ using namespace iclr17;
 using namespace iclr17::bfm;
 
 extern "C" {
+
+#if ICLR17_C1P_STAMPS
+// diagnostic build only: copy the conv1p stamps ([workgroup][wave][block][phase] s_memtime)
+int iclr17_debug_c1p_stamps(void* dst, size_t bytes) {
+  const size_t n = sizeof(g_c1p_stamps) < bytes ? sizeof(g_c1p_stamps) : bytes;
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_c1p_stamps), n, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
+
+#if ICLR17_K5_STAMPS
+int iclr17_debug_k5_stamps(void* dst, size_t bytes) {
+  const size_t n = sizeof(g_k5_stamps) < bytes ? sizeof(g_k5_stamps) : bytes;
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_k5_stamps), n, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 size_t iclr17_bf16_weight_size(int which, int N) {
   if (N != 128 && N != 192) return 0;
@@ -940,14 +1152,15 @@ int iclr17_analysis_conv1_gdn_bf16(const float* x, int B, int H, int W, int N,
                      H % 16 == 0 && W % 16 == 0,
                  ICLR17_EINVAL, "conv1_gdn_bf16: bad arguments (H, W multiples of 16)");
   const int tiles_y = (H / 4 + 7) / 8, tiles_x = (W / 4 + 7) / 8;
-  const dim3 grid(tiles_x * tiles_y * B);
   hipStream_t st = (hipStream_t)stream;
-  if (N == 192)
-    hipLaunchKernelGGL(conv1_bf16_kernel<192>, grid, dim3(256), 0, st, x, H, W, w_bf16, bias,
-                       beta_eff, gamma_bf16, out, tiles_x, tiles_y);
-  else
-    hipLaunchKernelGGL(conv1_bf16_kernel<128>, grid, dim3(256), 0, st, x, H, W, w_bf16, bias,
-                       beta_eff, gamma_bf16, out, tiles_x, tiles_y);
+  // persistent: one 8-wave workgroup per CU (LDS-bound), walking the blocks
+  const int ntiles = tiles_x * tiles_y * B, ncu = cu_count();
+  const dim3 pgrid(ntiles < ncu ? ntiles : ncu);
+  const bool full = (H / 4) % 8 == 0 && (W / 4) % 8 == 0;
+  auto kern = N == 192 ? (full ? conv1p_bf16_kernel<192, true> : conv1p_bf16_kernel<192, false>)
+                       : (full ? conv1p_bf16_kernel<128, true> : conv1p_bf16_kernel<128, false>);
+  hipLaunchKernelGGL(kern, pgrid, dim3(C1P_WAVES * 64), 0, st, x, H, W, w_bf16, bias, beta_eff,
+                     gamma_bf16, out, tiles_x, tiles_y, ntiles);
   return check_launch("conv1_gdn_bf16");
 }
 

@@ -42,6 +42,9 @@ namespace bfm {
 #ifndef ICLR17_C1P_KBO
 #define ICLR17_C1P_KBO 1   // conv1p: GDN contraction k-block outer (x² fragments read once)
 #endif
+#ifndef ICLR17_BF_DIRECT_Y
+#define ICLR17_BF_DIRECT_Y 1   // k5 GDN epilogue: per-wave y stores (K5::DIRECT_Y)
+#endif
 #ifndef ICLR17_K5_STAMPS
 #define ICLR17_K5_STAMPS 0
 #endif
@@ -83,6 +86,15 @@ __device__ __forceinline__ void sink_load(void* lds_sink) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g_zero16,
                                    (__attribute__((address_space(3))) void*)lds_sink,
                                    ICLR17_BF_SINK4 ? 4 : 16, 0, 0);
+}
+
+// threadIdx.x re-materialised where it is used: keeps the compiler from hoisting per-lane
+// address arithmetic out of a loop into registers it then spills (a scratch reload is a VMEM op,
+// and its vmcnt wait would also wait for every load in flight)
+__device__ __forceinline__ int fresh_tid() {
+  int v;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "v"((int)threadIdx.x));
+  return v;
 }
 
 __device__ __forceinline__ f4 mfma_bf16(const u4& a, const u4& b, const f4& c) {
@@ -239,6 +251,11 @@ struct K5 {
   static constexpr int EPI_LDS = EPI == BE_QUANT ? 64
                                  : (GOFF + GBLK * 1024 > R * OS ? GOFF + GBLK * 1024 : R * OS);
   static constexpr int LDS0 = KS * MAIN_LDS > EPI_LDS ? KS * MAIN_LDS : EPI_LDS;
+  // GDN: each wave stores its own y rows, a channel pair of tiles at a time, through a private
+  // 4 KB [32 px][64 ch] image (no workgroup barrier: the stores overlap other waves' contraction)
+  static constexpr int YOFF = EARLY_G ? 0 : GBLK * 1024;
+  static constexpr bool DIRECT_Y = ICLR17_BF_DIRECT_Y && EPI != BE_QUANT && NT % 2 == 0 &&
+                                   YOFF + NW * 4096 <= LDS0 && (EARLY_G ? NW * 4096 <= MAIN_LDS : true);
   // GDN: bias and β_eff staged by two prologue DMAs into their own 2 KB (an epilogue global load
   // of them waited out a full L2 round trip after the main loop)
   static constexpr int BBOFF = (LDS0 + 1023) / 1024 * 1024;
@@ -491,6 +508,11 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
     stg = __builtin_amdgcn_s_memtime();
 #endif
     const unsigned char* sg = smem + KK::GOFF + lane * 16;
+    // DIRECT_Y: this wave's [32 px][64 ch] bf16 image, 128-byte rows, 16-byte piece pc of pixel
+    // p at slot pc ^ (p & 7) (the 4×16-lane read groups cover the 64 banks; the 8-byte writes
+    // are 2-way)
+    unsigned char* const yb = smem + KK::YOFF + wave * 4096;
+    auto yswz = [](int p, int pc) { return p * 128 + ((pc ^ (p & 7)) << 4); };
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
       f16v n;
@@ -515,10 +537,38 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][4 * m + j] = y[j];
       }
+      if constexpr (KK::DIRECT_Y) {
+        if (i & 1) {   // tiles i − 1, i: channels 32(i − 1) .. 32i + 31, 8 pieces of 16 bytes
+#pragma unroll
+          for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+              const f16v& v = acc[i - 1 + tt];
+              *(uint2*)(yb + yswz(r32, 4 * tt + m) + 8 * h) =
+                  uint2{pack_bf2(v[4 * m], v[4 * m + 1]), pack_bf2(v[4 * m + 2], v[4 * m + 3])};
+            }
+          // wave-local: LDS keeps one wave's accesses in order. Pixel px = (lane >> 3) + 8j of
+          // the wave: tile row 2·wave + (j >> 1), column (lane >> 3) + 8·(j & 1); a uniform image
+          // base and 32-bit offsets (recomputed here, not held through the loop)
+          const int fl = fresh_tid() & 63;
+          u16* const ob = a.out + (long)b * a.Hout * a.Wout * CO;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int px = (fl >> 3) + 8 * j, pc = fl & 7;
+            const u4 v = *(lu4p)(yb + yswz(px, pc));
+            const int gy = ty * TH + 2 * wave + (j >> 1), gx = tx * 16 + (fl >> 3) + 8 * (j & 1);
+            const int oy = MODE == BM_CONV ? gy : 2 * gy + (PH >> 1);
+            const int ox = MODE == BM_CONV ? gx : 2 * gx + (PH & 1);
+            if (gy < a.gh && gx < a.gw) *(u4*)(ob + (oy * a.Wout + ox) * CO + 32 * (i - 1) + 8 * pc) = v;
+          }
+        }
+      }
     }
 #if ICLR17_K5_STAMPS
     st4 = __builtin_amdgcn_s_memtime();
+    st5 = st4;
 #endif
+    if constexpr (!KK::DIRECT_Y) {
     // y through an LDS tile [pixel][channel] (row stride OS) to whole-row 16-byte stores
     __syncthreads();   // every wave's γ reads done: the tile reuses the γ blocks
     constexpr int OS = KK::OS;
@@ -538,6 +588,7 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
       const int p = idx / PCS, pc = idx - p * PCS;
       const long op = out_pixel(p);
       if (op >= 0) *(u4*)(a.out + op * CO + pc * 8) = *(lu4p)(smem + p * OS + pc * 16);
+    }
     }
   } else {
     static_assert(EPI == BE_QUANT, "epilogue");
@@ -674,14 +725,6 @@ struct C1PL {
   static_assert(G % 1024 == 0 && LDS <= 160 * 1024, "conv1p LDS");
 };
 
-// threadIdx.x re-materialised where it is used: keeps the compiler from hoisting per-lane
-// address arithmetic out of a loop into registers it then spills (a scratch reload is a VMEM op,
-// and its vmcnt wait would also wait for every load in flight)
-__device__ __forceinline__ int fresh_tid() {
-  int v;
-  asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "v"((int)threadIdx.x));
-  return v;
-}
 
 template <int CO, bool FULL>   // FULL: the output grid is whole 8×8 blocks (no store guard)
 __global__ void __launch_bounds__(C1P_WAVES * 64, 1)

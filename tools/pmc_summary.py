@@ -41,7 +41,7 @@ LAYER_KERNELS = {
         "deconv3_clamp": (r"deconv3_x6_kernel<192>", None),
     },
     "bf16": {
-        "conv1_gdn1": (r"conv1_bf16_kernel<192>", None),
+        "conv1_gdn1": (r"conv1p_bf16_kernel<192, true>", None),
         "conv2_gdn2": (r"k5_bf16_kernel<0, 16, 192, 192, 192, 0>", None),
         "conv3_quant_rate": (r"k5_bf16_kernel<0, 8, 96, 192, 192, 2>", None),
         "deconv1_igdn1": (r"k5_bf16_kernel<1, 8, 192, 192, 192, 1>", None),

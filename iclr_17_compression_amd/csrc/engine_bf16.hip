@@ -592,56 +592,80 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
     }
   } else {
     static_assert(EPI == BE_QUANT, "epilogue");
-    if constexpr (KK::KS > 1) {
-      // K-split: groups 1 .. KS−1 hand their accumulators to group 0 through LDS (the main-loop
-      // buffers are free after the trailing vm_barrier), which adds them in group order
-      float* xs = (float*)smem;   // [group − 1][wave][tile][16][lane]
-      if (kg > 0) {
+    // conv3 + model.py:56 round (half to even) + model.py:71-73 rate: rows 8m .. 8m + 7 of every
+    // accumulator tile (registers 4m .. 4m + 3 of the lane's half h)
+    float bits = 0.f;
+    auto quant_rows = [&](int m) {
+      if (o < 0) return;
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        const int ch = nb * NB + 32 * i + 8 * m + 4 * h;
+        const f4 y = f4{acc[i][4 * m], acc[i][4 * m + 1], acc[i][4 * m + 2], acc[i][4 * m + 3]};
+        f4 q;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          q[j] = rintf(y[j]);
+          // integer latents: the per-channel table of the same element_bits (bit-identical)
+          bits += fabsf(q[j]) <= (float)RT_K ? a.rtab[(ch + j) * RT_W + (int)q[j] + RT_K]
+                                             : element_bits(q[j], a.rate, CO, ch + j);
+        }
+        if (a.y_f32) *(f4*)(a.y_f32 + o * CO + ch) = y;
+        *(f4*)(a.out_f32 + o * CO + ch) = q;
+        *(uint2*)(a.out + o * CO + ch) = uint2{pack_bf2(q[0], q[1]), pack_bf2(q[2], q[3])};
+      }
+    };
+    int nred = NW;   // bit partials to add, one per finishing wave
+    if constexpr (KK::KS == 2) {
+      // K-split halves exchange HALF their accumulators through LDS (the main-loop buffers are
+      // free after the trailing vm_barrier): group g finalises rows m ∈ {2g, 2g + 1} of every
+      // tile with the other group's partial of those rows (x0 + x1, exact either way round), so
+      // both groups run the quantiser on half the elements
+      float* xs = (float*)smem;   // [group][wave][tile][8][lane]
+      auto put = [&](int r0) {
 #pragma unroll
         for (int i = 0; i < NT; ++i)
 #pragma unroll
-          for (int j = 0; j < 16; ++j) xs[((((kg - 1) * NW + wave) * NT + i) * 16 + j) * 64 + lane] = acc[i][j];
-      }
+          for (int j = 0; j < 8; ++j) xs[(((kg * NW + wave) * NT + i) * 8 + j) * 64 + lane] = acc[i][r0 + j];
+      };
+      auto add = [&](int r0) {
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[i][r0 + j] += xs[((((1 - kg) * NW + wave) * NT + i) * 8 + j) * 64 + lane];
+      };
+      if (kg == 0) put(8); else put(0);   // the rows the other group finalises
       __syncthreads();
-      if (kg == 0) {
-#pragma unroll
-        for (int g = 1; g < KK::KS; ++g)
-#pragma unroll
-          for (int i = 0; i < NT; ++i)
-#pragma unroll
-            for (int j = 0; j < 16; ++j) acc[i][j] += xs[((((g - 1) * NW + wave) * NT + i) * 16 + j) * 64 + lane];
-      }
+      if (kg == 0) add(0); else add(8);
       __syncthreads();   // exchange reads done before red[] reuses the area
+#if ICLR17_K5_STAMPS
+      st4 = __builtin_amdgcn_s_memtime();
+#endif
+      if (kg == 0) {
+        quant_rows(0);
+        quant_rows(1);
+      } else {
+        quant_rows(2);
+        quant_rows(3);
+      }
+      nred = 2 * NW;
+    } else {
+      static_assert(KK::KS == 1, "K split");
+#if ICLR17_K5_STAMPS
+      st4 = __builtin_amdgcn_s_memtime();
+#endif
+#pragma unroll
+      for (int m = 0; m < 4; ++m) quant_rows(m);
     }
-    // conv3 + model.py:56 round (half to even) + model.py:71-73 rate, per element
-    float bits = 0.f;
-    if (o >= 0 && kg == 0) {
-#pragma unroll
-      for (int i = 0; i < NT; ++i)
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          const int ch = nb * NB + 32 * i + 8 * m + 4 * h;
-          const f4 y = f4{acc[i][4 * m], acc[i][4 * m + 1], acc[i][4 * m + 2], acc[i][4 * m + 3]};
-          f4 q;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            q[j] = rintf(y[j]);
-            // integer latents: the per-channel table of the same element_bits (bit-identical)
-            bits += fabsf(q[j]) <= (float)RT_K ? a.rtab[(ch + j) * RT_W + (int)q[j] + RT_K]
-                                               : element_bits(q[j], a.rate, CO, ch + j);
-          }
-          if (a.y_f32) *(f4*)(a.y_f32 + o * CO + ch) = y;
-          *(f4*)(a.out_f32 + o * CO + ch) = q;
-          *(uint2*)(a.out + o * CO + ch) = uint2{pack_bf2(q[0], q[1]), pack_bf2(q[2], q[3])};
-        }
-    }
+#if ICLR17_K5_STAMPS
+    st5 = __builtin_amdgcn_s_memtime();
+#endif
     bits = wave_sum(bits);
     float* red = (float*)smem;
-    if (lane == 0 && kg == 0) red[wave] = bits;
+    if (lane == 0) red[kg * NW + wave] = bits;
     __syncthreads();
     if (tid == 0) {
       double sum = 0.0;
-      for (int w = 0; w < NW; ++w) sum += (double)red[w];
+      for (int w = 0; w < nred; ++w) sum += (double)red[w];
       const int tile = ty * a.tiles_x + tx;
       a.partial[(long)b * a.ppi + tile * (CO / NB) + nb] = sum;
     }

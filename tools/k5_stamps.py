@@ -58,6 +58,11 @@ print(f"  wg life   median {np.median(life):8.0f}")
 if layer != "conv3":   # GDN epilogue split: x² + γ ready | contraction | y tile | stores
     parts = [st[:, :, 4] - st[:, :, 2], st[:, :, 5] - st[:, :, 4], st[:, :, 6] - st[:, :, 5], st[:, :, 3] - st[:, :, 6]]
     print("  epilogue parts (x2+gamma, contraction, y tile, stores):", [int(np.median(v)) for v in parts])
+else:   # K-split exchange | quantiser + rate + stores | bit reduction
+    parts = [st[:, :, 5] - st[:, :, 2], st[:, :, 6] - st[:, :, 5], st[:, :, 3] - st[:, :, 6]]
+    for g in range(2):
+        w = slice(4 * g, 4 * g + 4)
+        print(f"  group {g} epilogue parts (exchange, quant+rate+stores, bits):", [int(np.median(v[:, w])) for v in parts])
 starts = np.sort(st[:, :, 0].min(axis=1) - t0)
 print("  wg start times (cycles) at quantiles 0/.25/.5/.75/1:", [int(np.quantile(starts, q)) for q in (0, .25, .5, .75, 1)])
 if layer.startswith("deconv"):

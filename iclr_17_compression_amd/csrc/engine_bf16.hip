@@ -45,6 +45,9 @@ namespace bfm {
 #ifndef ICLR17_BF_DIRECT_Y
 #define ICLR17_BF_DIRECT_Y 1   // k5 GDN epilogue: per-wave y stores (K5::DIRECT_Y)
 #endif
+#ifndef ICLR17_BF_PAIR
+#define ICLR17_BF_PAIR 0   // deconv1 (8-row tiles): phase order 0, 1, 3, 2 (A/B)
+#endif
 #ifndef ICLR17_K5_STAMPS
 #define ICLR17_K5_STAMPS 0
 #endif
@@ -687,8 +690,11 @@ k5_bf16_kernel(const K5Args a) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[KK::LDS];
   int bid = blockIdx.x;
   const int per_ph = a.tiles_x * a.tiles_y * a.B;
-  const int ph = MODE == BM_DECONV ? bid / per_ph : 0;   // phases dispatched phase-major
-  bid -= ph * per_ph;
+  const int q = MODE == BM_DECONV ? bid / per_ph : 0;   // phases dispatched phase-major
+  bid -= q * per_ph;
+  // two-per-CU tiles (TH = 8): dispatch order 9, 6, 4, 6 taps, so that workgroup i and i + half
+  // the grid (the two a CU holds when the grid is one round) pair a long and a short phase
+  const int ph = (ICLR17_BF_PAIR && TH == 8 && q >= 2) ? 5 - q : q;
   const int tx = bid % a.tiles_x;
   bid /= a.tiles_x;
   const int ty = bid % a.tiles_y;

@@ -229,7 +229,7 @@ def run_train(args, net, x, world, dev):
     torch.cuda.synchronize()
     elapsed = idist.max_over_ranks(time.perf_counter() - t0, dev)
     ms = elapsed / args.steps * 1e3
-    comm = allreduce_overlap(args, net, params, reducer, step, ms, dev) if world > 1 else None
+    comm = allreduce_overlap(args, net, params, opt, reducer, step, ms, dev) if world > 1 else None
     if loader is not None:
         loader.close()
         data_info["step_crops_per_s"] = round(B * args.steps / elapsed, 1)
@@ -278,12 +278,13 @@ def _timed_loop(fn, steps: int, dev) -> float:
     return idist.max_over_ranks(time.perf_counter() - t0, dev) / steps * 1e3
 
 
-def allreduce_overlap(args, net, params, reducer, step, step_ms: float, dev) -> dict:
+def allreduce_overlap(args, net, params, opt, reducer, step, step_ms: float, dev) -> dict:
     """C4: how much of the gradient all-reduce the backward hides. Measured after the timed
     region, over as many steps: (1) the bucketed all-reduce of one step's gradients alone
     (the reducer's own buckets, nothing else running), (2) the same training step with the
     reducer detached (no all-reduce: each rank keeps its own gradient). exposed = step −
-    no-all-reduce step; overlapped fraction = 1 − exposed / all-reduce time."""
+    no-all-reduce step; overlapped fraction = 1 − exposed / all-reduce time. The parameters and
+    the Adam moments are restored after (2), so the ranks leave it with the replicas in sync."""
     keys = [torch.zeros_like(p) for p in params]   # stand-ins with no .grad of their own
     grads = [torch.ones_like(p) for p in params]
 
@@ -292,6 +293,9 @@ def allreduce_overlap(args, net, params, reducer, step, step_ms: float, dev) -> 
         reducer.wait()
 
     ar_ms = _timed_loop(ar_only, args.steps, dev)
+    # (2) applies Adam to each rank's own (un-averaged) gradient: snapshot what it changes
+    snap = [p.detach().clone() for p in params]
+    snap_state = {p: {k: v.clone() for k, v in opt.state[p].items()} for p in params if opt.state[p]}
     net._grad_reducer = None
     reducer_finish = reducer.finish
     reducer.finish = lambda: None
@@ -300,6 +304,14 @@ def allreduce_overlap(args, net, params, reducer, step, step_ms: float, dev) -> 
     finally:
         reducer.finish = reducer_finish
         reducer.attach(net)
+        with torch.no_grad():
+            for p, s in zip(params, snap):
+                p.copy_(s)
+            for p, st in snap_state.items():
+                for k, v in st.items():
+                    opt.state[p][k].copy_(v)
+        for p in params:   # drop the last un-averaged gradients (the copies bumped the version
+            p.grad = None  # counters, so the weight packs rebuild on next use)
     exposed = max(0.0, step_ms - local_ms)
     return {"bucket_mb": reducer.bucket_bytes / 2 ** 20,
             "grad_bytes": sum(p.numel() * 4 for p in params),
@@ -363,11 +375,39 @@ KODAK_SETS = {   # --kodak-set: fixture, description of the weights
 }
 
 
+def kodak_rank_images(rank: int, world: int):
+    """This rank's Kodak-24 images (C2 at N GPUs): the 18 landscape images split by shard_range,
+    the 6 portrait ones by the reversed rank order, so the ranks with fewer landscape images take
+    the portrait ones (8 ranks: 3 images each)."""
+    from iclr_17_compression_amd import dist as idist
+    land = [i for i in range(24) if i not in KODAK_PORTRAIT]
+    lo, hi = idist.shard_range(len(land), rank, world)
+    plo, phi = idist.shard_range(len(KODAK_PORTRAIT), world - 1 - rank, world)
+    return land[lo:hi], list(KODAK_PORTRAIT)[plo:phi]
+
+
+def kodak_table(rows: dict, ncols: int, dev) -> np.ndarray:
+    """The [24, ncols] per-image table from every rank's rows {image index: values}: each rank
+    fills its own rows, the others stay exact zeros, and one all-reduce (sum) assembles it — the
+    result does not depend on the summation order."""
+    from iclr_17_compression_amd import dist as idist
+    table = torch.zeros(24, ncols, dtype=torch.float64, device=dev)
+    for i, vals in rows.items():
+        table[i] = torch.tensor(vals, dtype=torch.float64)
+    if idist.world() > 1:
+        dist.all_reduce(table, op=dist.ReduceOp.SUM)
+    return table.cpu().numpy()
+
+
 def run_kodak(args, dev):
     """C2 (BASELINE configs[1]): Kodak-24 encode/decode at N=192 with testKodak's per-image
     metrics (bpp, PSNR, MS-SSIM on the GPU), synthetic Kodak images (no network); parity against
     the reference's own values: G9 (default; weights trained to λ = 0.01, PSNR ≈ 27 dB) or G5
-    (seeded trained-like weights, a degenerate 6.6 dB point)."""
+    (seeded trained-like weights, a degenerate 6.6 dB point). At N ranks the 24 images are
+    sharded (kodak_rank_images; images are independent, no collective in the data path) and the
+    per-image metrics come back with one fixed-order sum at the end."""
+    from iclr_17_compression_amd import dist as idist
+    world, rank = idist.world(), idist.rank()
     fixture, weights_note = KODAK_SETS[args.kodak_set]
     meta = json.load(open(os.path.join(REPO, "tests", "golden", fixture)))
     net = ImageCompressor(out_channel_N=meta["N"])
@@ -379,57 +419,71 @@ def run_kodak(args, dev):
                              synth.trained_like_state_dict(meta["N"], meta["weight_seed"]).items()})
     net = net.to(dev).eval()
     imgs = kodak_synth_images(meta)
-    land = torch.cat([imgs[i] for i in range(24) if i not in KODAK_PORTRAIT]).to(dev)
-    port = torch.cat([imgs[i] for i in KODAK_PORTRAIT]).to(dev)
+    groups = [g for g in kodak_rank_images(rank, world) if g]
+    batches = [torch.cat([imgs[i] for i in g]).to(dev) for g in groups]
 
     def step():   # the two orientations on concurrent streams (ImageCompressor.evaluate_many)
-        return tuple(net.evaluate_many([land, port], want_msssim=True))
+        return tuple(net.evaluate_many(batches, want_msssim=True))
 
     with torch.no_grad():
         for _ in range(args.warmup):
             step()
         torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            ev_l, ev_p = step()
+            evs = step()
         torch.cuda.synchronize()
-        elapsed = time.perf_counter() - t0
-    land_idx = [i for i in range(24) if i not in KODAK_PORTRAIT]
-    per = {}
-    for ev, idx in ((ev_l, land_idx), (ev_p, list(KODAK_PORTRAIT))):
-        for j, i in enumerate(idx):
-            per[i] = {k: ev[k][j].item() for k in ("bpp", "psnr", "ms_ssim")}
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = idist.max_over_ranks(time.perf_counter() - t0, dev)
+    # per-image metrics and the reference-latent match: rows of this rank's images, summed over
+    # ranks (every other rank contributes exact zeros, so the sum is order-independent)
+    keys = ("bpp", "psnr", "ms_ssim")
+    rows = {}
+    for ev, g in zip(evs, groups):
+        for j, i in enumerate(g):
+            rows[i] = [ev[k][j].item() for k in keys] + [0.0]
+    yfix = {"g9": "g9_y_hat_n192.npz"}.get(args.kodak_set)
+    if yfix:   # ŷ against the reference's own committed latents (tests/golden/gen_yhat.py)
+        yd = np.load(os.path.join(REPO, "tests", "golden", yfix))
+        with torch.no_grad():
+            for i in rows:
+                ev = net.evaluate(imgs[i].to(dev))
+                ref = torch.from_numpy(yd[f"yhat_{i:02d}"].astype(np.float32)).to(dev)
+                rows[i][len(keys)] = float((ev["y_hat"] != ref).sum().item())
+    t = kodak_table(rows, len(keys) + 1, dev)
+    per = {i: {k: float(t[i, c]) for c, k in enumerate(keys)} for i in range(24)}
     rel = {k: max(abs(per[i][k] - meta["images"][i][k]) / abs(meta["images"][i][k]) for i in range(24))
-           for k in ("bpp", "psnr", "ms_ssim")}
-    # ŷ against the reference's, per image (the fixture holds the SHA-256 of the reference's ŷ)
-    import hashlib
-    same = 0
-    with torch.no_grad():
-        for i in range(24):
-            ev = net.evaluate(imgs[i].to(dev))
-            same += hashlib.sha256(ev["y_hat"].cpu().contiguous().numpy().tobytes()).hexdigest() \
-                == meta["images"][i]["y_hat_sha256"]
+           for k in keys}
     parity = {"max_rel_" + k: v for k, v in rel.items()}
-    parity["images_with_the_reference_latents"] = same
+    if yfix:
+        parity["latent_flips_vs_reference_y_hat"] = int(t[:, len(keys)].sum())
+        parity["images_with_the_reference_latents"] = int((t[:, len(keys)] == 0).sum())
     if args.kodak_set in KODAK_ORDERS:   # the bar: the reference's own cross-order spread (G8s/G9s)
         orders = json.load(open(os.path.join(REPO, "tests", "golden", KODAK_ORDERS[args.kodak_set])))
         sp = orders["set_spread_fp32"]
         parity["reference_cross_order_spread"] = {
-            "max_rel_" + k: sp["rel_d" + k] for k in ("bpp", "psnr", "ms_ssim")}
+            "max_rel_" + k: sp["rel_d" + k] for k in keys}
         parity["reference_cross_order_flips"] = orders["total_flips_vs_default"]
-        parity["bar"] = {"max_rel_" + k: max(1e-5, sp["rel_d" + k] + 1e-6) for k in ("bpp", "psnr", "ms_ssim")}
+        parity["reference_images_with_flips_max"] = orders["max_images_with_flips_fp32"]
+        parity["bar"] = {"max_rel_" + k: max(1e-5, sp["rel_d" + k] + 1e-6) for k in keys}
     pixels = 24 * 512 * 768 * args.steps
     return {
         "metric": "Mpixels/s Kodak-24 encode+decode with per-image bpp/PSNR/MS-SSIM (C2)",
-        "value": round(pixels / elapsed / 1e6, 2), "unit": "Mpix/s", "n_gpus": 1,
+        "value": round(pixels / elapsed / 1e6, 2), "unit": "Mpix/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "scaling": "strong", "vs_baseline": None, "dtype": "f32",
         "data": f"synthetic Kodak-24 (18 x 512x768 + 6 x 768x512, smooth_image_u8), {weights_note}",
         "config": {"workload": "Kodak-24 eval: encode, round, rate, decode, clamp, per-image bpp/PSNR/MS-SSIM",
-                   "N": meta["N"], "precision": kernels.precision()},
+                   "N": meta["N"], "precision": kernels.precision(),
+                   "parallelism": f"dp{world} (the 24 images sharded by rank, metrics summed at the end)"},
         f"parity_vs_reference_{args.kodak_set.upper()}": parity,
-        "dataset_average": {k: sum(per[i][k] for i in range(24)) / 24 for k in ("bpp", "psnr", "ms_ssim")},
+        "dataset_average": {k: sum(per[i][k] for i in range(24)) / 24 for k in keys},
     }
 
 
@@ -626,6 +680,18 @@ def lib_sha() -> str:
     return hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest()[:16]
 
 
+def profile_layers(N: int, S: int, B: int, prec: str) -> dict:
+    """Per bench layer, the rocprof trace mean (ms) of its kernel from the committed summary of
+    THIS library build (profiles/*_traffic.json, tools/profile_round.sh), or {}."""
+    sha = lib_sha()
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")), reverse=True):
+        d = json.load(open(f))
+        if (d.get("precision") == prec and d.get("workload") == {"N": N, "S": S, "B": B}
+                and d.get("lib_sha256") == sha):
+            return {k: e["mean_ms"] for k, e in d.get("layers", {}).items() if e.get("mean_ms")}
+    return {}
+
+
 def pmc_traffic(layer: str, N: int, S: int, B: int, prec: str):
     """HBM bytes per launch of `layer` from a committed PMC summary (profiles/*_traffic.json, made
     by tools/profile_round.sh — counters cannot be collected inside this process). Only a summary
@@ -709,9 +775,13 @@ def roofline(per_layer_ms: dict, prec: str, N: int, S: int, B: int):
         peak, note = X6_PEAK_TFLOPS, "bf16 dense MFMA peak / 6 (bf16x6: six bf16 part products per fp32 MAC)"
     else:
         peak, note = FP32_MFMA_PEAK_TFLOPS, "fp32 MFMA dense peak (exact-f32 products)"
+    prof = profile_layers(N, S, B, prec)
     for k in LAYERS:
         if flops[k]:
             layers[k]["frac"] = round(flops[k] * B / (per_layer_ms[k] * 1e-3) / 1e12 / peak, 4)
+            if prof.get(k):   # the same fraction from the SHA-matched rocprof trace mean
+                layers[k]["profile_mean_ms"] = round(prof[k], 4)
+                layers[k]["frac_from_profile"] = round(flops[k] * B / (prof[k] * 1e-3) / 1e12 / peak, 4)
     # per-layer T_roof = max(F / P_peak, bytes / BW_peak) and the whole chain's
     # Σ T_roof / Σ T_measured (P_peak the mode's MFMA peak, BW_peak the HBM peak)
     t_roof = {}
@@ -853,6 +923,8 @@ def main() -> None:
     # path with several ranks sharing the GPUs there are (device = local rank mod device count)
     backend = os.environ.get("ICLR17_DIST_BACKEND", "nccl")
     ndev = torch.cuda.device_count()   # counts devices without initialising HIP on this image
+    if args.dry_run and ndev == 0 and backend == "nccl":
+        backend = "gloo"   # RCCL needs a device; the plumbing dry run falls back to gloo on CPU
     if "WORLD_SIZE" not in os.environ:
         check_world(args, 1, backend, ndev)
         if args.gpus > 1:   # no torchrun: start the N ranks here, before any HIP call
@@ -897,7 +969,15 @@ def main() -> None:
             dist.destroy_process_group()
         return
 
-    if args.mode in ("kodak", "codec", "encdec"):
+    if args.mode == "kodak":   # all ranks: the 24 images are sharded
+        res = run_kodak(args, dev)
+        res.update(layout)
+        if rank == 0:
+            print(json.dumps(res), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    if args.mode in ("codec", "encdec"):
         if rank == 0:
             run = {"kodak": run_kodak, "codec": run_codec, "encdec": run_encdec}[args.mode]
             print(json.dumps(run(args, dev)), flush=True)
@@ -989,7 +1069,8 @@ def main() -> None:
             "value": round(pixels / rb["elapsed"] / 1e6, 2), "unit": "Mpix/s",
             "warmup": max(args.warmup, 100),
             "ms_per_step": round(rb["elapsed"] / args.steps * 1e3, 4), "dtype": "bf16",
-            "roofline": {k: roof_b[k] for k in ("kernel", "achieved", "peak", "frac", "traffic",
+            "roofline": {k: roof_b[k] for k in ("kernel", "achieved", "peak", "frac", "duration",
+                                                  "profile_mean_ms", "frac_from_profile", "traffic",
                                                   "traffic_source", "traffic_null_reason",
                                                   "chain_roofline_frac")
                          if k in roof_b},

@@ -330,15 +330,15 @@ class CodecTrainFn(torch.autograd.Function):
 
 
 class AnalysisFn(torch.autograd.Function):
-    """Analysis_net_17.forward with autograd: y (NCHW view of NHWC storage)."""
+    """Analysis_net_17.forward with autograd: y, contiguous NCHW, from the codec's own analysis
+    kernels (``Analysis_net_17.y_nhwc``), so round(y) is the codec's ŷ with grad on or off."""
 
     @staticmethod
     def forward(ctx, x, enc, *params):
         ctx.set_materialize_grads(False)
-        a2, saved = analysis_features_train(enc, x)   # a2s stays: conv3's x6 weight gradient
-        _, _, w3, _, _ = enc.packed()
+        _, saved = analysis_features_train(enc, x)   # a2s stays: conv3's x6 weight gradient
         ctx.enc, ctx.saved = enc, saved
-        return kernels.conv3(a2, w3).permute(0, 3, 1, 2)
+        return enc.y_nhwc(x, feats=saved).permute(0, 3, 1, 2).contiguous()
 
     @staticmethod
     def backward(ctx, g_y):

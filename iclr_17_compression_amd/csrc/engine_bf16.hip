@@ -100,6 +100,15 @@ __device__ __forceinline__ int fresh_tid() {
   return v;
 }
 
+// Orders one wave's LDS accesses across its lanes (a lane reading what another lane wrote): a
+// wavefront-scope acquire/release fence, which the memory model needs for the cross-lane
+// exchange, plus a wave barrier so the scheduler moves no LDS op across it. DS instructions of
+// one wave already execute in order, so this emits no instruction.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 __device__ __forceinline__ f4 mfma_bf16(const u4& a, const u4& b, const f4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, a),
                                                  __builtin_bit_cast(bf8, b), c, 0, 0, 0);
@@ -550,6 +559,7 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
               *(uint2*)(yb + yswz(r32, 4 * tt + m) + 8 * h) =
                   uint2{pack_bf2(v[4 * m], v[4 * m + 1]), pack_bf2(v[4 * m + 2], v[4 * m + 3])};
             }
+          wave_lds_sync();   // the image's writes before any lane's reads (cross-lane exchange)
           // wave-local: LDS keeps one wave's accesses in order. Pixel px = (lane >> 3) + 8j of
           // the wave: tile row 2·wave + (j >> 1), column (lane >> 3) + 8·(j & 1); a uniform image
           // base and 32-bit offsets (recomputed here, not held through the loop)
@@ -564,6 +574,7 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
             const int ox = MODE == BM_CONV ? gx : 2 * gx + (PH & 1);
             if (gy < a.gh && gx < a.gw) *(u4*)(ob + (oy * a.Wout + ox) * CO + 32 * (i - 1) + 8 * pc) = v;
           }
+          wave_lds_sync();   // every lane's reads before the next tile pair's writes (WAR)
         }
       }
     }

@@ -120,11 +120,14 @@ class GradAllReducer:
         opt.zero_grad(set_to_none=True); loss.backward(); reducer.finish(); opt.step()
     """
 
-    def __init__(self, params: Sequence[Tensor], bucket_mb: float = 4.0):
+    def __init__(self, params: Sequence[Tensor], bucket_mb: float = 4.0, always: bool = False):
         self.params = list(params)
         self.bucket_bytes = int(bucket_mb * 2 ** 20)
         self.pending = []        # (work, flat, params)
         self.launched = set()
+        # always: run the collective path even in a one-rank group (a world-size-1 RCCL
+        # communicator on one GPU exercises launch / RCCL stream / finish ordering; tests)
+        self.always = always
 
     def attach(self, net) -> "GradAllReducer":
         net._grad_reducer = self
@@ -132,7 +135,7 @@ class GradAllReducer:
 
     @property
     def active(self) -> bool:
-        return world() > 1
+        return world() > 1 or (self.always and dist.is_available() and dist.is_initialized())
 
     def launch(self, params: Sequence[Tensor], grads: Sequence[Optional[Tensor]]) -> None:
         """All-reduce (sum, async) these parameters' freshly computed gradients."""
@@ -162,9 +165,9 @@ class GradAllReducer:
     def finish(self) -> None:
         """Wait for the reductions (stream-ordered) and set p.grad = the rank average. Gradients
         no backward launched (parameters outside the fused backward) are reduced here."""
-        w = world()
-        if w == 1:
+        if not self.active:
             return
+        w = world()
         rest = [p for p in self.params if p.grad is not None and id(p) not in self.launched]
         if rest:
             self.launch(rest, [p.grad for p in rest])

@@ -227,10 +227,10 @@ class ImageCompressor(nn.Module):
         bpp = bits / (H * W)
         mse = sse / (3 * H * W)
         psnr = 10.0 * torch.log10(1.0 / mse)
-        res = {"clipped": out["clipped"], "y_hat": out["y_hat"].permute(0, 3, 1, 2),
+        res = {"clipped": out["clipped"], "y_hat": out["y_hat"].permute(0, 3, 1, 2).contiguous(),
                "bpp": bpp, "mse": mse, "psnr": psnr}
         if want_y:
-            res["y"] = out["y"].permute(0, 3, 1, 2)
+            res["y"] = out["y"].permute(0, 3, 1, 2).contiguous()
         if want_msssim:
             ms = kernels.ms_ssim(out["clipped"], x, data_range=1.0)
             res["ms_ssim"] = ms

@@ -87,21 +87,31 @@ class Analysis_net_17(nn.Module):
                                                           self.out_channel_N))
 
     def forward(self, x):
-        """analysis_17.py:31-36 → y, contiguous NCHW like the reference's. Without autograd it
-        runs the very kernels of ``ImageCompressor.forward``'s analysis half in the current
-        precision (conv3 with its quantiser epilogue, y taken before the rounding), so
-        ``torch.round(Encoder(x))`` is bitwise the codec's ŷ (NewTests/testReconSeperateEandD.py:67)."""
+        """analysis_17.py:31-36 → y, contiguous NCHW like the reference's. With or without
+        autograd it runs the very kernels of ``ImageCompressor.forward``'s analysis half in the
+        current precision (conv3 with its quantiser epilogue, y taken before the rounding), so
+        ``torch.round(Encoder(x))`` is bitwise the codec's ŷ (NewTests/testReconSeperateEandD.py:67,
+        which runs with autograd on)."""
         from ..autograd import AnalysisFn, needs_grad
         kernels._check(x, "image", 4)
         params = list(self.parameters())
         if needs_grad(x, params):
             return AnalysisFn.apply(x.contiguous(), self, *params)
-        x = x.contiguous()
+        return self.y_nhwc(x.contiguous()).permute(0, 3, 1, 2).contiguous()
+
+    def y_nhwc(self, x, feats=None):
+        """y (NHWC) through the codec's analysis kernels. ``feats``: the training forward's
+        conv2+GDN2 output (autograd.analysis_features_train), reused for conv3 where it is the
+        codec's own operand (x6: its split form; fp32: the fp32 activation)."""
         N = self.out_channel_N
         w1, w2, w3, g1, g2 = self.packed()
         # the rate epilogue needs a model: a zero one (its bits are discarded, y is all we keep)
         z = torch.zeros(11 * N, device=x.device)
         ztab = torch.zeros(N, 65, device=x.device)
+        if feats is not None and kernels.precision() == "x6" and feats.get("a2s") is not None:
+            return kernels.conv3_quant_rate_x6(feats["a2s"], w3, z, want_y=True, rtab=ztab)[2]
+        if feats is not None and kernels.precision() == "fp32":
+            return kernels.conv3_quant_rate(feats["a2"], w3, z, want_y=True, rtab=ztab)[2]
         if kernels.precision() == "bf16":
             w1b, w2b, w3b = self.packed_bf16()
             e1, e2 = self.gdn1.effective_params_bf16(), self.gdn2.effective_params_bf16()
@@ -117,4 +127,4 @@ class Analysis_net_17(nn.Module):
             h = kernels.conv1_gdn(x, w1, self.conv1.bias, g1[0], g1[1], N)
             h = kernels.conv2_gdn(h, w2, self.conv2.bias, g2[0], g2[1])
             y = kernels.conv3_quant_rate(h, w3, z, want_y=True, rtab=ztab)[2]
-        return y.permute(0, 3, 1, 2).contiguous()
+        return y

@@ -107,6 +107,18 @@ def test_launcher_spawns_ranks(n):
     assert d["dist_backend"] == ("gloo" if n > 1 else None)
 
 
+def test_dry_run_default_backend_without_gpu():
+    """--dry-run with the default backend (RCCL) on a host without a GPU falls back to gloo, as
+    its help promises, instead of failing in init_process_group("nccl", device_id=cpu)."""
+    import torch
+    if torch.cuda.device_count():
+        pytest.skip("host has a GPU: the default backend is RCCL there")
+    r = _run_bench(["--gpus", "2", "--dry-run"], {"ICLR17_DIST_BACKEND": "nccl"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert d["n_gpus"] == 2 and d["dist_backend"] == "gloo"
+
+
 def test_launcher_strong_scaling_and_errors():
     r = _run_bench(["--gpus", "2", "--dry-run", "--global-batch", "64"], {"ICLR17_DIST_BACKEND": "gloo"})
     assert r.returncode == 0, r.stderr[-2000:]
@@ -120,3 +132,56 @@ def test_launcher_strong_scaling_and_errors():
     r = _run_bench(["--gpus", "2", "--dry-run"], {"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0",
                                                   "ICLR17_DIST_BACKEND": "gloo"})
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+def test_kodak_rank_images_partition():
+    """C2 at N GPUs: every Kodak image on exactly one rank, landscape and portrait batches apart,
+    at most 3 images per rank at 8 ranks."""
+    for w in range(1, 9):
+        seen = []
+        for r in range(w):
+            land, port = bench.kodak_rank_images(r, w)
+            assert not set(land) & set(bench.KODAK_PORTRAIT)
+            assert set(port) <= set(bench.KODAK_PORTRAIT)
+            seen += land + port
+            if w == 8:
+                assert len(land) + len(port) == 3
+        assert sorted(seen) == list(range(24))
+
+
+def _kodak_worker(r, w, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), WORLD_SIZE=str(w))
+    dist.init_process_group("gloo", rank=r, world_size=w)
+    try:
+        land, port_ = bench.kodak_rank_images(r, w)
+        rows = {i: [0.25 + i, 30.0 - i / 7, 0.9 + i / 1000, float(i % 3)] for i in land + port_}
+        t = bench.kodak_table(rows, 4, "cpu")
+        import numpy as np
+        expect = np.array([[0.25 + i, 30.0 - i / 7, 0.9 + i / 1000, float(i % 3)] for i in range(24)])
+        q.put((r, bool(np.array_equal(t, expect))))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((r, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("w", [2, 8])
+def test_kodak_sharded_table_gloo(w):
+    """The sharded Kodak path's per-image table (bench.kodak_table) over gloo ranks: every rank
+    ends with the full 24-row table, bit for bit what one rank would hold."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_kodak_worker, args=(r, w, port, q)) for r in range(w)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(w))
+    for p in ps:
+        p.join(timeout=60)
+    assert all(v is True for v in res.values()), res

@@ -500,6 +500,31 @@ def test_encoder_matches_codec_forward(device, mode):
     assert torch.equal(recon.clamp(0.0, 1.0), clipped)
 
 
+@pytest.mark.parametrize("mode", ["x6", "fp32", "bf16"])
+def test_encoder_with_grad_matches_codec_forward(device, mode):
+    """NewTests/testReconSeperateEandD.py:67 calls ``torch.round(net.Encoder(x))`` with autograd
+    ON, which takes AnalysisFn: its y must be the codec's own (same analysis kernels), contiguous
+    NCHW, and still carry a gradient into the encoder."""
+    old = kernels.precision()
+    kernels.set_precision(mode)
+    try:
+        net = net_for(192, 1, device)
+        x = image(5, 2, 64, 96).to(device)
+        y = net.Encoder(x)
+        assert y.requires_grad
+        with torch.no_grad():
+            _, y_hat, _ = net(x)
+            y_ng = net.Encoder(x)
+        y.sum().backward()
+    finally:
+        kernels.set_precision(old)
+    assert y.is_contiguous() and y.shape == (2, 192, 4, 6)
+    assert torch.equal(y.detach(), y_ng)
+    assert torch.equal(torch.round(y.detach()), y_hat)
+    assert net.Encoder.conv1.weight.grad is not None
+    assert torch.isfinite(net.Encoder.conv1.weight.grad).all()
+
+
 @pytest.mark.parametrize("N", [192, 128])
 def test_chunk_major_split_deconv2_to_deconv3(device, N):
     """deconv2+IGDN2 writing the chunk-major split form [3,B,N/32,h,w,32] (what deconv3's halo

@@ -34,5 +34,5 @@ SETS
 cd "$R"
 python tools/pmc_summary.py "$OUT" "$TAG" "$PREC" || exit 1
 cp "$(find "$OUT/trace" -name '*kernel_stats.csv' | head -1)" "$OUT/${TAG}_kernel_stats.csv"
-tail -1 "$OUT/trace.log" > "$OUT/${TAG}_bench_under_trace.json"
+grep '^{' "$OUT/trace.log" | tail -n 1 > "$OUT/${TAG}_bench_under_trace.json" || echo "no bench JSON line in trace.log" >&2
 exit 0

@@ -88,6 +88,7 @@ class Step:
         self.enc = net.Encoder.packed()
         self.dec = net.Decoder.packed()
         self.d3x6 = net.Decoder.packed_x6()
+        self.dx6k = net.Decoder.packed_x6k() if kernels.X6K else None
         self.rate = net.bitEstimator.packed()
         gdns = (net.Encoder.gdn1, net.Encoder.gdn2, net.Decoder.igdn1, net.Decoder.igdn2)
         self.w1x6 = net.Encoder.packed_conv1_x6()
@@ -125,9 +126,16 @@ class Step:
             ev(2)
             y_hat, partial, _, ys = kernels.conv3_quant_rate_x6(hs, w3, self.rate, rtab=self.rtab)
             ev(3)
-            hs, _, _ = kernels.deconv_igdn_x6(ys, d1, net.Decoder.deconv1.bias, *e3)
-            ev(4)
-            hs, _, _ = kernels.deconv_igdn_x6(hs, d2, net.Decoder.deconv2.bias, *e4, chunk_major=D3_CM)
+            if kernels.X6K:   # the 32x32x16 x6 engine (Synthesis_net_17.decode's x6 path)
+                x1, x2 = self.dx6k
+                hs, _ = kernels.deconv_igdn_x6k(ys, x1, net.Decoder.deconv1.bias, e3[0], e3[2])
+                ev(4)
+                hs, _ = kernels.deconv_igdn_x6k(hs, x2, net.Decoder.deconv2.bias, e4[0], e4[2],
+                                                chunk_major=D3_CM)
+            else:
+                hs, _, _ = kernels.deconv_igdn_x6(ys, d1, net.Decoder.deconv1.bias, *e3)
+                ev(4)
+                hs, _, _ = kernels.deconv_igdn_x6(hs, d2, net.Decoder.deconv2.bias, *e4, chunk_major=D3_CM)
             ev(5)
             clipped, _, _ = kernels.deconv3_x6(hs, self.d3x6, net.Decoder.deconv3.bias)
         else:

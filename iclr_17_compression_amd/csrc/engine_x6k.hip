@@ -1,0 +1,516 @@
+// The x6 (fp32-exact) k5 layers on v_mfma_f32_32x32x16_bf16: the bf16 throughput engine's form
+// (engine_bf16.hip) with six bf16 part products per MAC. synthesis_17.py:15-22 (deconv1/2 +
+// IGDN), models/GDN.py:64-94.
+//
+// Why a second x6 engine: the 16x16x32 x6 engine (engine_fp32.hip, engine_kernel<…, X6>) splits
+// the fp32 weights in VALU inside its main loop and moves its operands by LDS-DMA per tap, so a
+// k-step issues ~2× its MFMA cycles (72 MFMAs × 8 issue cycles + 9 DMA pieces + 165
+// VALU per wave and step, on an MFMA that leaves 8 of 16 cycles for issue). Here:
+//   * v_mfma_f32_32x32x16_bf16 leaves 24 of its 32 cycles for issue;
+//   * the weights arrive pre-split (iclr17_pack_x6k: three bf16 planes in the A-fragment layout),
+//     so the main loop has no VALU at all;
+//   * the input is the producing layer's split form (three bf16 planes), staged per 16-channel
+//     chunk as ONE halo patch that every tap of the chunk reads at a shifted offset;
+//   * a wave owns 32 pixels and every output channel (NT = CO/32 accumulators), so the IGDN
+//     channel contraction runs from the accumulators (no x² tile).
+// One k16 step = one tap × the chunk's 16 channels: 6 MFMAs per (channel tile, step), in the x6
+// engine's product order (lo·hi, hi·lo, mid·mid, mid·hi, hi·mid, hi·hi: small terms first), in
+// place on the accumulator. The dropped terms (mid·lo, lo·mid, lo·lo) are below 2⁻²⁴ of a product.
+//
+// INT_IN (deconv1: its input is ŷ, integers |v| ≤ 127, exact in one bf16): the input's mid and
+// lo planes are zero, so only its hi plane is staged and the three products with a non-zero
+// input part run (lo·hi, mid·hi, hi·hi) — the other three would add exact zeros.
+//
+// Epilogue (IGDN / GDN, x6): x = acc + bias; n = Σ_j γ[i][j]·x_j² with γ split into three bf16
+// planes (the A operand, staged in LDS half the output channels at a time) and x² (rounded to
+// fp32, as conv2d(x², γ) sees it) split in registers into three B planes; y = x·√(β + n)
+// (IGDN) or x / √(β + n) (GDN), correctly rounded sqrt and division. The output leaves in
+// split form (NHWC, or chunk-major [3][B][N/32][h][w][32] for deconv3) and optionally fp32.
+#include <string.h>
+
+#include "common.h"
+#include "k5_common.h"
+
+namespace iclr17 {
+namespace x6k {
+using namespace bfm;
+
+__device__ __attribute__((aligned(16))) unsigned g_zero16x[4] = {0u, 0u, 0u, 0u};
+
+// padding load of the counted-vmcnt DMA schedule (4 bytes per lane into the sink)
+__device__ __forceinline__ void sink4(void* lds_sink) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g_zero16x,
+                                   (__attribute__((address_space(3))) void*)lds_sink, 4, 0, 0);
+}
+
+enum XEpi : int { XE_GDN = 0, XE_IGDN = 1 };
+
+struct XArgs {
+  const u16* in;        // split input [3][B][Hin][Win][CI] (bf16 bits)
+  long in_plane;
+  const u16* w;         // iclr17_pack_x6k weights, [3][…] (plane stride w_plane)
+  long w_plane;
+  const float* bias;    // [CO]
+  const float* beta;    // β_eff [CO]
+  const u16* gamma6;    // γ_eff split [3][CO/8][CO][8]
+  float* out;           // fp32 NHWC [B][Hout][Wout][CO] or null
+  u16* out_split;       // split output: NHWC [3][B][Hout][Wout][CO], or chunk-major
+  long out_plane;       //   [3][B][CO/32][Hout][Wout][32] (out_cm)
+  int out_cm;
+  int B, Hin, Win, Hout, Wout;
+  int gh, gw;           // base grid (conv: output grid; deconv: input grid)
+  int tiles_x, tiles_y;
+};
+
+template <int MODE, int TH, int CO, int CI, bool INT_IN>
+struct XK {
+  static constexpr int NW = TH / 2, NTHR = NW * 64;
+  static constexpr int NT = CO / 32;           // 32-channel accumulator tiles per wave
+  static constexpr int NCH = CI / 16;          // 16-channel chunks
+  using P = Patch<MODE, TH>;
+  static constexpr int PL = INT_IN ? 1 : 3;    // input planes staged
+  static constexpr int PB = PL * P::BYTES;     // patch bytes (planes back to back)
+  static constexpr int NQI = (PB + 1023) / 1024;
+  static constexpr int PBUF = NQI * 1024;
+  static constexpr int SB = 3 * 2 * CO * 16;   // weight stage: [plane 3][half 2][CO][8] bf16
+  static constexpr int NBI = SB / 1024;
+  static constexpr int NST = 4;
+  static constexpr int MAIN = 2 * PBUF + NST * SB + 1024;
+  static constexpr int NTH = NT / 2;           // epilogue: output tiles per pass
+  static constexpr int KB = CO / 16;           // epilogue: 16-channel k-blocks
+  static constexpr int GBL = 3 * NTH * KB;     // epilogue: γ fragment blocks per pass (1 KB)
+  static constexpr int LDS0 = MAIN > GBL * 1024 ? MAIN : GBL * 1024;
+  static constexpr int BBOFF = (LDS0 + 1023) / 1024 * 1024;
+  static constexpr int LDS = BBOFF + 2048;     // + bias, β_eff
+  static_assert(SB % 1024 == 0 && (2 * CO * 16) % 1024 == 0, "weight stage");
+  static_assert(NT % 2 == 0 && CI % 16 == 0, "tile shape");
+  static_assert(LDS <= 160 * 1024, "LDS");
+};
+
+template <int MODE, int TH, int CO, int CI, int EPI, bool INT_IN, int PH>
+__device__ __forceinline__ void x6k_body(const XArgs& a, unsigned char* smem, int b, int ty, int tx) {
+  using KK = XK<MODE, TH, CO, CI, INT_IN>;
+  using P = typename KK::P;
+  using TP = Taps<MODE, PH>;
+  constexpr int NT = KK::NT, NW = KK::NW, NCH = KK::NCH, S = TP::T;   // one tap per step
+  constexpr int SB = KK::SB, NBI = KK::NBI, NST = KK::NST;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, h = lane >> 5;
+  // counted DMA schedule (engine_bf16.hip k5_body): every wave issues exactly K DMA instructions
+  // per step — weight slots of step g+F+1, pieces of the next chunk's patch during steps
+  // 0 .. S-F-1, sink loads as padding — so `s_waitcnt vmcnt(F·K)` + barrier retires all but the
+  // newest F groups
+  constexpr int F = S >= 3 ? 2 : 1, SI = S - F;
+  static_assert(SI >= 1 && NST >= F + 2, "DMA schedule");
+  constexpr int PS = (KK::NQI + SI - 1) / SI;
+  constexpr int K = (NBI + PS + NW - 1) / NW;
+  static_assert(F * K < 64, "vmcnt");
+  constexpr int GS = NCH * S;
+  unsigned char* const sP = smem;
+  unsigned char* const sB = smem + 2 * KK::PBUF;
+  unsigned char* const sD = sB + NST * SB;
+  float* const sbb = (float*)(smem + KK::BBOFF);   // [bias | pad][β_eff | pad]
+  const long img = (long)b * a.Hin * a.Win;
+  const int iy0 = MODE == BM_CONV ? 2 * ty * TH - 2 : ty * TH - 1;
+  const int ix0 = MODE == BM_CONV ? 2 * tx * 16 - 2 : tx * 16 - 1;
+  const u16* __restrict__ inb = a.in + img * CI;
+  // patch piece `piece` (1 KB): this lane's 16-byte slot → source u16 offset, or -1 (zeros)
+  auto piece_src = [&](int piece) -> long {
+    const int byte = (piece * 64 + lane) * 16;
+    const int pl = byte / P::BYTES, rem = byte - pl * P::BYTES;
+    const int pr = rem / P::ROWB, r1 = rem - pr * P::ROWB;
+    int pc, hh;
+    bool ok;
+    if (MODE == BM_CONV) {
+      const int par = r1 / (2 * P::HALF), r2 = r1 - par * 2 * P::HALF;
+      hh = r2 / P::HALF;
+      pc = 2 * ((r2 - hh * P::HALF) / 16) + par;
+      ok = pc < 35;
+    } else {
+      hh = r1 / P::HALF;
+      pc = (r1 - hh * P::HALF) / 16;
+      ok = true;
+    }
+    const int iy = iy0 + pr, ix = ix0 + pc;
+    ok = ok && pl < KK::PL && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
+    return ok ? pl * a.in_plane + (long)(iy * a.Win + ix) * CI + 8 * hh : -1;
+  };
+  auto issue_piece = [&](int c1, int piece, bool valid) {
+    if (!valid) {
+      sink4(sD);
+      return;
+    }
+    const long src = piece_src(piece);
+    glds16(src >= 0 ? (const void*)(inb + src + c1 * 16) : (const void*)g_zero16x,
+           sP + (c1 & 1) * KK::PBUF + piece * 1024);
+  };
+  // weights of this phase: per plane [NCH][S][2][CO][8]; the step's stage [plane][2][CO][8]
+  constexpr long WSTEP = 2L * CO * 8;   // u16 per (chunk, tap) block of one plane
+  const u16* __restrict__ wph = a.w;
+  if (MODE == BM_DECONV) {
+    long off = 0;
+#pragma unroll
+    for (int p = 0; p < PH; ++p) {
+      const int ny = (p >> 1) == 0 ? 3 : 2, nx = (p & 1) == 0 ? 3 : 2;
+      off += (long)NCH * ny * nx * WSTEP;
+    }
+    wph += off;
+  }
+  long wsrc[K];   // slot k of a step: plane + unit offset (16-byte units of [2][CO])
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int q = (k * NW + wave) * 64 + lane;
+    const int pl = q / (2 * CO), u = q - pl * (2 * CO);
+    wsrc[k] = pl * a.w_plane + (long)u * 8;
+  }
+  auto issue_w = [&](int k, int wg) {
+    const int slot = k * NW + wave;
+    if (wg >= GS) {
+      sink4(sD);
+      return;
+    }
+    glds16(wph + (long)wg * WSTEP + wsrc[k], sB + (wg % NST) * SB + slot * 1024);
+  };
+
+  // ---- per-lane fragment addresses
+  // B (pixels): pixel (tile row 2·wave + (r32 >> 4), column r32 & 15), channel half h
+  const int prow = 2 * wave + (r32 >> 4), pcol = r32 & 15;
+  const int tpix = prow * 16 + pcol;
+  const int pbase = (MODE == BM_CONV ? P::off(2 * prow, 2 * pcol) : P::off(prow, pcol)) + h * P::HALF;
+  // A (weights): stage [plane][2][CO][8]: lane (k-group h, channel 32·i + r32)
+  const int abase = (h * CO + r32) * 16;
+  constexpr int APL = 2 * CO * 16;   // stage bytes per plane
+
+  f16v acc[NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[i][j] = 0.f;
+
+  // prologue: bias and β_eff (waves 0 / 1), chunk 0's patch, the weights of steps 0 .. F-1, then
+  // step F's weights as a full K-group and F-1 sink groups (the first wait keeps F in flight)
+  static_assert(CO <= 256, "bias / β stage");
+  if (wave < 2) {
+    const float* src = wave == 0 ? a.bias : a.beta;
+    glds16(lane * 4 < CO ? (const void*)(src + lane * 4) : (const void*)g_zero16x, sbb + wave * 256);
+  }
+  for (int piece = wave; piece < KK::NQI; piece += NW) issue_piece(0, piece, true);
+#pragma unroll
+  for (int f = 0; f < F; ++f)
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (k * NW + wave < NBI) issue_w(k, f);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    if (k * NW + wave < NBI) issue_w(k, F);
+    else sink4(sD);
+  }
+#pragma unroll
+  for (int f = 1; f < F; ++f)
+#pragma unroll
+    for (int k = 0; k < K; ++k) sink4(sD);
+
+  typedef const __attribute__((address_space(3))) u4* lu4p;
+  int stage = 0;
+  for (int c = 0; c < NCH; ++c) {
+    const unsigned char* pbuf = sP + (c & 1) * KK::PBUF + pbase;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int g = c * S + s;
+      wait_vm_barrier<F * K>();   // weights of step g and, at s = 0, chunk c's patch landed;
+                                  // stage (g+F+1) % NST is free
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int slot = k * NW + wave;
+        if ((k + 1) * NW <= NBI || slot < NBI) {
+          issue_w(k, g + F + 1);
+        } else if (s < SI) {
+          const int piece = s * PS + slot - NBI;
+          issue_piece(c + 1, piece, c + 1 < NCH && piece < KK::NQI);
+        } else {
+          sink4(sD);
+        }
+      }
+      const unsigned char* wb = sB + stage * SB + abase;
+      stage = stage + 1 == NST ? 0 : stage + 1;
+      const int to = P::template tap_off<PH>(s);
+      const u4 bh = *(lu4p)(pbuf + to);
+      u4 bm, bl;
+      if constexpr (!INT_IN) {
+        bm = *(lu4p)(pbuf + P::BYTES + to);
+        bl = *(lu4p)(pbuf + 2 * P::BYTES + to);
+      }
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        const u4 ah = *(lu4p)(wb + i * 512);
+        const u4 am = *(lu4p)(wb + APL + i * 512);
+        const u4 al = *(lu4p)(wb + 2 * APL + i * 512);
+        f16v t = mfma32(al, bh, acc[i]);
+        if constexpr (!INT_IN) {
+          t = mfma32(ah, bl, t);
+          t = mfma32(am, bm, t);
+        }
+        t = mfma32(am, bh, t);
+        if constexpr (!INT_IN) t = mfma32(ah, bm, t);
+        acc[i] = mfma32(ah, bh, t);
+      }
+    }
+  }
+  vm_barrier();   // trailing sink loads landed; every wave is done with the stages
+
+  // ---- epilogue. acc[i][4m + j]: channel 32i + 8m + 4h + j of tile pixel tpix
+  const int gy = ty * TH + (tpix >> 4), gx = tx * 16 + (tpix & 15);
+  const bool inside = gy < a.gh && gx < a.gw;
+  const int oy = MODE == BM_CONV ? gy : 2 * gy + (PH >> 1);
+  const int ox = MODE == BM_CONV ? gx : 2 * gx + (PH & 1);
+  const long o = ((long)b * a.Hout + oy) * a.Wout + ox;
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const f4 bv = *(const f4*)(sbb + 32 * i + 8 * m + 4 * h);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][4 * m + j] += bv[j];   // x = conv + bias
+    }
+  constexpr int NTH = KK::NTH, KB = KK::KB;
+#ifdef ICLR17_X6K_NOEPI
+  if (inside) for (int i = 0; i < NT; ++i) for (int m = 0; m < 4; ++m) *(f4*)(a.out + o * CO + 32 * i + 8 * m + 4 * h) = f4{acc[i][4*m], acc[i][4*m+1], acc[i][4*m+2], acc[i][4*m+3]};
+  return;
+#endif
+  auto split_bits = [](float v, unsigned& hb, unsigned& mb, unsigned& lb) {
+    hb = __float_as_uint(v) & 0xffff0000u;
+    const float r = v - __uint_as_float(hb);
+    mb = __float_as_uint(r) & 0xffff0000u;
+    lb = __float_as_uint(r - __uint_as_float(mb));
+  };
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    if (hf) __syncthreads();   // every wave's pass-0 γ reads done before the restage
+    // opaque to the optimiser: pass 1 recomputes the x² planes instead of keeping pass 0's
+    // (12 k-blocks × 3 planes × 4 registers) alive across the passes
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(acc[i][j]));
+    // γ rows 32·(hf·NTH + il) .. of the three planes: block (plane, il, kb), lane (r32, h) ←
+    // γ_p[32(hf·NTH + il) + r32][16kb + 8h .. +7] (the [CO/8][CO][8] packing)
+    for (int blk = wave; blk < KK::GBL; blk += NW) {
+      const int p = blk / (NTH * KB), rem = blk - p * NTH * KB;
+      const int il = rem / KB, kb = rem - il * KB;
+      glds16(a.gamma6 + (long)p * CO * CO + ((2 * kb + h) * CO + 32 * (hf * NTH + il) + r32) * 8,
+             smem + blk * 1024);
+    }
+    vm_barrier();
+    f16v n[NTH];
+#pragma unroll
+    for (int il = 0; il < NTH; ++il)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) n[il][j] = 0.f;
+    const unsigned char* sg = smem + lane * 16;
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      // x² of channels 16kb .. 16kb + 15 as three B planes: the accumulator rows a lane holds are
+      // 4h + 0..3 and 8 + 4h + 0..3 of the 16-channel block; one permlane32 swap per register
+      // pair and plane hands lanes h the 8 consecutive channels 8h .. 8h + 7
+      const int i = kb >> 1, r0 = 8 * (kb & 1);
+      float sq[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sq[j] = acc[i][r0 + j] * acc[i][r0 + j];
+      u4 xp[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {   // plane p of the exact split: hi, then mid, then lo
+        unsigned v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          v[j] = __float_as_uint(sq[j]) & 0xffff0000u;
+          if (p < 2) sq[j] -= __uint_as_float(v[j]);   // remainder for the next plane (exact)
+          else v[j] = __float_as_uint(sq[j]);
+        }
+        const unsigned lo0 = __builtin_amdgcn_perm(v[1], v[0], 0x07060302u);
+        const unsigned lo1 = __builtin_amdgcn_perm(v[3], v[2], 0x07060302u);
+        const unsigned hi0 = __builtin_amdgcn_perm(v[5], v[4], 0x07060302u);
+        const unsigned hi1 = __builtin_amdgcn_perm(v[7], v[6], 0x07060302u);
+        const auto s0 = __builtin_amdgcn_permlane32_swap(lo0, hi0, false, false);
+        const auto s1 = __builtin_amdgcn_permlane32_swap(lo1, hi1, false, false);
+        xp[p] = u4{s0[0], s1[0], s0[1], s1[1]};
+      }
+#pragma unroll
+      for (int il = 0; il < NTH; ++il) {
+        const u4 gh = *(lu4p)(sg + ((0 * NTH + il) * KB + kb) * 1024);
+        const u4 gm = *(lu4p)(sg + ((1 * NTH + il) * KB + kb) * 1024);
+        const u4 gl = *(lu4p)(sg + ((2 * NTH + il) * KB + kb) * 1024);
+        f16v t = mfma32(gl, xp[0], n[il]);
+        t = mfma32(gh, xp[2], t);
+        t = mfma32(gm, xp[1], t);
+        t = mfma32(gm, xp[0], t);
+        t = mfma32(gh, xp[1], t);
+        n[il] = mfma32(gh, xp[0], t);
+      }
+      __builtin_amdgcn_sched_barrier(0);   // one k-block's operands live at a time
+    }
+    // y = x·√(β + n) (IGDN) | x / √(β + n) (GDN); stores
+#pragma unroll
+    for (int il = 0; il < NTH; ++il) {
+      const int i = hf * NTH + il;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int ch = 32 * i + 8 * m + 4 * h;
+        const f4 be = *(const f4*)(sbb + 256 + ch);
+        f4 y;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float s = sqrtf(n[il][4 * m + j] + be[j]);
+          const float x = acc[i][4 * m + j];
+          y[j] = EPI == XE_IGDN ? x * s : x / s;
+        }
+        if (!inside) continue;
+        if (a.out) *(f4*)(a.out + o * CO + ch) = y;
+        if (a.out_split) {
+          unsigned hb[4], mb[4], lb[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) split_bits(y[j], hb[j], mb[j], lb[j]);
+          const long so = a.out_cm ? (((long)b * (CO / 32) + i) * a.Hout + oy) * a.Wout * 32 + (long)ox * 32 + 8 * m + 4 * h
+                                   : o * CO + ch;
+          *(uint2*)(a.out_split + so) = uint2{__builtin_amdgcn_perm(hb[1], hb[0], 0x07060302u),
+                                              __builtin_amdgcn_perm(hb[3], hb[2], 0x07060302u)};
+          *(uint2*)(a.out_split + a.out_plane + so) = uint2{__builtin_amdgcn_perm(mb[1], mb[0], 0x07060302u),
+                                                            __builtin_amdgcn_perm(mb[3], mb[2], 0x07060302u)};
+          *(uint2*)(a.out_split + 2 * a.out_plane + so) = uint2{__builtin_amdgcn_perm(lb[1], lb[0], 0x07060302u),
+                                                                __builtin_amdgcn_perm(lb[3], lb[2], 0x07060302u)};
+        }
+      }
+    }
+  }
+}
+
+template <int MODE, int TH, int CO, int CI, int EPI, bool INT_IN>
+__global__ void __launch_bounds__(TH / 2 * 64, 1) x6k_kernel(const XArgs a) {
+  using KK = XK<MODE, TH, CO, CI, INT_IN>;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[KK::LDS];
+  int bid = blockIdx.x;
+  const int per_ph = a.tiles_x * a.tiles_y * a.B;
+  const int ph = MODE == BM_DECONV ? bid / per_ph : 0;   // phases dispatched phase-major
+  bid -= ph * per_ph;
+  const int tx = bid % a.tiles_x;
+  bid /= a.tiles_x;
+  const int ty = bid % a.tiles_y;
+  const int b = bid / a.tiles_y;
+  if constexpr (MODE == BM_CONV) {
+    x6k_body<MODE, TH, CO, CI, EPI, INT_IN, 0>(a, smem, b, ty, tx);
+  } else {
+    switch (ph) {   // wave-uniform: the tap lists are compile-time per phase
+      case 0: x6k_body<MODE, TH, CO, CI, EPI, INT_IN, 0>(a, smem, b, ty, tx); break;
+      case 1: x6k_body<MODE, TH, CO, CI, EPI, INT_IN, 1>(a, smem, b, ty, tx); break;
+      case 2: x6k_body<MODE, TH, CO, CI, EPI, INT_IN, 2>(a, smem, b, ty, tx); break;
+      default: x6k_body<MODE, TH, CO, CI, EPI, INT_IN, 3>(a, smem, b, ty, tx); break;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- packing
+// W → three planes, per plane [blocks][2][CO][8] bf16 where a block is one (chunk, tap):
+// conv (W[co][ci][5][5]): block c·25 + t, tap t = 5·ky + kx;
+// deconv (W[ci][co][5][5]): the four stride phases back to back, phase p's blocks c·T_p + t with
+// the tap order of Taps<BM_DECONV, p>. Element (block, h, co, j) = W at input channel 16c + 8h + j.
+__global__ void __launch_bounds__(256) pack_x6k_kernel(const float* __restrict__ w, int N, int deconv,
+                                                       long groups, u16* __restrict__ out) {
+  const int nch = N / 16;
+  for (long g = (long)blockIdx.x * 256 + threadIdx.x; g < groups; g += (long)gridDim.x * 256) {
+    const int co = (int)(g % N);
+    long r = g / N;
+    const int h = (int)(r % 2);
+    int u = (int)(r / 2);   // block index
+    int c, ky, kx;
+    if (!deconv) {
+      c = u / 25;
+      const int t = u - c * 25;
+      ky = t / 5;
+      kx = t % 5;
+    } else {
+      int p = 0, T = 9;
+      while (true) {
+        const int ny = (p >> 1) == 0 ? 3 : 2, nx = (p & 1) == 0 ? 3 : 2;
+        T = ny * nx;
+        if (u < nch * T) break;
+        u -= nch * T;
+        ++p;
+      }
+      const int nx = (p & 1) == 0 ? 3 : 2;
+      c = u / T;
+      const int t = u - c * T;
+      ky = (p >> 1) == 0 ? 2 * (t / nx) : 2 * (t / nx) + 1;
+      kx = (p & 1) == 0 ? 2 * (t % nx) : 2 * (t % nx) + 1;
+    }
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int ci = 16 * c + 8 * h + j;
+      v[j] = deconv ? w[(((long)ci * N + co) * 5 + ky) * 5 + kx] : w[(((long)co * N + ci) * 5 + ky) * 5 + kx];
+    }
+    u4 hi, mi, lo;
+    split8(f4{v[0], v[1], v[2], v[3]}, f4{v[4], v[5], v[6], v[7]}, hi, mi, lo);
+    *(u4*)(out + g * 8) = hi;
+    *(u4*)(out + groups * 8 + g * 8) = mi;
+    *(u4*)(out + 2 * groups * 8 + g * 8) = lo;
+  }
+}
+
+template <int N, int TH, bool INT_IN>
+int launch_deconv(const XArgs& a0, hipStream_t st) {
+  XArgs a = a0;
+  a.tiles_y = (a.gh + TH - 1) / TH;
+  a.tiles_x = (a.gw + 15) / 16;
+  hipLaunchKernelGGL((x6k_kernel<BM_DECONV, TH, N, N, XE_IGDN, INT_IN>),
+                     dim3(a.tiles_x * a.tiles_y * a.B * 4), dim3(TH / 2 * 64), 0, st, a);
+  return check_launch("deconv_igdn_x6k");
+}
+
+}  // namespace x6k
+}  // namespace iclr17
+
+using namespace iclr17;
+using namespace iclr17::x6k;
+
+extern "C" {
+
+size_t iclr17_x6k_weight_size(int which, int N) {
+  if (N != 128 && N != 192) return 0;
+  if (which != ICLR17_X6K_CONV5 && which != ICLR17_X6K_DECONV5) return 0;
+  return (size_t)3 * (N / 16) * 25 * 2 * N * 8;   // both: 25 (chunk, tap) blocks per chunk
+}
+
+int iclr17_pack_x6k(int which, const float* w, uint16_t* out, int N, void* stream) {
+  const size_t total = iclr17_x6k_weight_size(which, N);
+  ICLR17_REQUIRE(total > 0, ICLR17_EUNSUPPORTED, "pack_x6k: kind %d, N=%d unsupported", which, N);
+  ICLR17_REQUIRE(w && out, ICLR17_EINVAL, "pack_x6k: null pointer");
+  const long groups = (long)(total / 24);
+  const int blocks = (int)((groups + 255) / 256 < 4096 ? (groups + 255) / 256 : 4096);
+  hipLaunchKernelGGL(pack_x6k_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, N,
+                     which == ICLR17_X6K_DECONV5 ? 1 : 0, groups, out);
+  return check_launch("pack_x6k");
+}
+
+int iclr17_synthesis_deconv_igdn_x6k(const uint16_t* in_split, int B, int h, int w, int N,
+                                     const uint16_t* w_x6k, const float* bias,
+                                     const float* beta_eff, const uint16_t* gamma_split,
+                                     float* out, uint16_t* out_split, int out_cm, int int_in,
+                                     void* stream) {
+  ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "deconv_igdn_x6k: N=%d", N);
+  ICLR17_REQUIRE(in_split && w_x6k && bias && beta_eff && gamma_split && (out || out_split) &&
+                     B > 0 && h > 0 && w > 0,
+                 ICLR17_EINVAL, "deconv_igdn_x6k: bad arguments");
+  XArgs a;
+  memset(&a, 0, sizeof(a));
+  a.in = in_split; a.in_plane = (long)B * h * w * N;
+  a.w = w_x6k; a.w_plane = (long)(N / 16) * 25 * 2 * N * 8;
+  a.bias = bias; a.beta = beta_eff; a.gamma6 = gamma_split;
+  a.out = out; a.out_split = out_split; a.out_plane = (long)B * 4 * h * w * N; a.out_cm = out_cm ? 1 : 0;
+  a.B = B; a.Hin = h; a.Win = w; a.Hout = 2 * h; a.Wout = 2 * w;
+  a.gh = h; a.gw = w;
+  hipStream_t st = (hipStream_t)stream;
+  if (int_in) return N == 192 ? launch_deconv<192, 16, true>(a, st) : launch_deconv<128, 16, true>(a, st);
+  return N == 192 ? launch_deconv<192, 16, false>(a, st) : launch_deconv<128, 16, false>(a, st);
+}
+
+}  // extern "C"

@@ -252,6 +252,9 @@ def deconv_igdn(h: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Tenso
 # ------------------------------------------------------------- x6 (bf16x6) precision mode
 PRECISIONS = ("x6", "fp32", "bf16")
 _precision = os.environ.get("ICLR17_PRECISION", "x6")
+# ICLR17_X6K=1: the x6 decoder layers on the 32x32x16 engine (csrc/engine_x6k.hip) instead of
+# the 16x16x32 engine (A/B; DESIGN §5 has the measurements that keep the default)
+X6K = os.environ.get("ICLR17_X6K", "0") == "1"
 
 
 def precision() -> str:
@@ -424,6 +427,40 @@ def deconv_igdn_x6(hs: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: T
          _p(hs), B, hh, ww, N, _p(wp), _p(bias), _p(beta_eff),
          _p(gp), _p(g6), _p(out), _p(split), _p(pre), _stream(hs))
     return split, out, pre
+
+
+def pack_x6k(which: int, w: Tensor, N: int) -> Tensor:
+    """k5 weights → three exact bf16 planes in the x6k engine's A-fragment step layout
+    (ICLR17_X6K_CONV5 / ICLR17_X6K_DECONV5)."""
+    _check(w, "weight", 4)
+    size = query("iclr17_x6k_weight_size", which, N)
+    if size == 0:
+        raise Iclr17Error(f"iclr17: pack_x6k: kind {which}, N={N} unsupported")
+    out = torch.empty(size, device=w.device, dtype=torch.int16)
+    call("iclr17_pack_x6k", which, _p(w.detach().contiguous()), _p(out), N, _stream(w))
+    return out
+
+
+def deconv_igdn_x6k(hs: Tensor, wx: Tensor, bias: Tensor, beta_eff: Tensor, g6: Tensor,
+                    want_split: bool = True, want_f32: bool = False, chunk_major: bool = False,
+                    int_in: bool = False):
+    """synthesis_17.py:15-22 on the 32x32x16 x6 engine (csrc/engine_x6k.hip): split input
+    [3,B,h,w,N] → (split | None, fp32 | None). wx: ``pack_x6k(ICLR17_X6K_DECONV5, …)``; g6: the
+    IGDN's split γ. ``int_in``: the input is ŷ (integers exact in one bf16; its other planes are
+    zero and are not read)."""
+    _check_split(hs, "activation")
+    _, B, hh, ww, N = hs.shape
+    _check_channels(N)
+    if not (want_split or want_f32):
+        raise Iclr17Error("iclr17: deconv_igdn_x6k needs an output")
+    if wx.numel() != query("iclr17_x6k_weight_size", _lib.ICLR17_X6K_DECONV5, N):
+        raise Iclr17Error("iclr17: deconv_igdn_x6k needs the ICLR17_X6K_DECONV5 packing")
+    shape = (3, B, N // 32, 2 * hh, 2 * ww, 32) if chunk_major else (3, B, 2 * hh, 2 * ww, N)
+    split = torch.empty(shape, device=hs.device, dtype=torch.int16) if want_split else None
+    out = torch.empty(B, 2 * hh, 2 * ww, N, device=hs.device) if want_f32 else None
+    call("iclr17_synthesis_deconv_igdn_x6k", _p(hs), B, hh, ww, N, _p(wx), _p(bias),
+         _p(beta_eff), _p(g6), _p(out), _p(split), int(chunk_major), int(int_in), _stream(hs))
+    return split, out
 
 
 def ms_ssim(x: Tensor, y: Tensor, data_range: float = 1.0) -> Tensor:

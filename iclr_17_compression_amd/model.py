@@ -250,6 +250,8 @@ class ImageCompressor(nn.Module):
             if x6:
                 self.Encoder.packed_conv1_x6()
                 self.Decoder.packed_x6()
+                if kernels.X6K and not backward:
+                    self.Decoder.packed_x6k()
                 for g in gdns:
                     g.effective_params_x6()
             if backward:

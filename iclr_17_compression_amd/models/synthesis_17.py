@@ -53,6 +53,16 @@ class Synthesis_net_17(nn.Module):
         return self._pack.get("d3x6", (self.deconv3.weight,),
                               lambda: kernels.split_deconv3(d3, self.out_channel_N), force)
 
+    def packed_x6k(self, force: bool = False):
+        """deconv1 / deconv2 split into the x6k engine's three bf16 weight planes (4 stride
+        phases), cached until the weights change."""
+        N, f = self.out_channel_N, force
+        d1 = self._pack.get("d1x6k", (self.deconv1.weight,),
+                            lambda: kernels.pack_x6k(_lib.ICLR17_X6K_DECONV5, self.deconv1.weight, N), f)
+        d2 = self._pack.get("d2x6k", (self.deconv2.weight,),
+                            lambda: kernels.pack_x6k(_lib.ICLR17_X6K_DECONV5, self.deconv2.weight, N), f)
+        return d1, d2
+
     def packed_bf16(self, force: bool = False):
         """deconv1 / deconv2 in the bf16 engine's step layout (4 stride phases) and deconv3's
         all-phase packing rounded to bf16 fragments, cached."""
@@ -102,8 +112,14 @@ class Synthesis_net_17(nn.Module):
             return kernels.deconv3_bf16(h, b3, self.deconv3.bias, x_ref=x_ref, want_recon=want_recon)
         if y_split is not None:
             q1, q2 = self.igdn1.effective_params_x6(), self.igdn2.effective_params_x6()
-            hs, _, _ = kernels.deconv_igdn_x6(y_split, d1, self.deconv1.bias, *q1)
-            hs, _, _ = kernels.deconv_igdn_x6(hs, d2, self.deconv2.bias, *q2, chunk_major=True)
+            if kernels.X6K:   # the 32x32x16 x6 engine (csrc/engine_x6k.hip)
+                x1, x2 = self.packed_x6k()
+                hs, _ = kernels.deconv_igdn_x6k(y_split, x1, self.deconv1.bias, q1[0], q1[2])
+                hs, _ = kernels.deconv_igdn_x6k(hs, x2, self.deconv2.bias, q2[0], q2[2],
+                                                chunk_major=True)
+            else:
+                hs, _, _ = kernels.deconv_igdn_x6(y_split, d1, self.deconv1.bias, *q1)
+                hs, _, _ = kernels.deconv_igdn_x6(hs, d2, self.deconv2.bias, *q2, chunk_major=True)
             return kernels.deconv3_x6(hs, self.packed_x6(), self.deconv3.bias, x_ref=x_ref,
                                       want_recon=want_recon)
         else:

@@ -435,6 +435,26 @@ int iclr17_rate_param_grad(const float* partial, int T, int C, const float* h1, 
                            float* db2, float* da2, float* dh3, float* db3, float* da3, float* dh4,
                            float* db4, void* stream);
 
+/* ------------------------------------------------------------------ x6 k5 engine (32x32x16)
+ * The x6 scheme (fp32-exact part products, as above) on v_mfma_f32_32x32x16_bf16 in the bf16
+ * engine's form (csrc/engine_x6k.hip): halo patch of the split input per 16-channel chunk,
+ * weights pre-split into three bf16 planes, a wave owns 32 pixels × all N channels, IGDN
+ * contraction from the accumulators. Replaces iclr17_synthesis_deconv_igdn_x6[_cm] on the
+ * inference path (synthesis_17.py:15-22; models/GDN.py:64-94, inverse). */
+#define ICLR17_X6K_CONV5 40   /* conv2/conv3 W[co][ci][5][5] → [3][N/16·25][2][N][8] bf16 planes */
+#define ICLR17_X6K_DECONV5 41 /* deconv1/2 W[ci][co][5][5] → [3][4 phases: N/16·T_p][2][N][8] */
+size_t iclr17_x6k_weight_size(int which, int N);   /* uint16 elements (3 planes); 0 = unsupported */
+int iclr17_pack_x6k(int which, const float* w, uint16_t* out, int N, void* stream);
+/* synthesis_17.py:15-22 deconv + IGDN in x6: split input [3][B][h][w][N] → out fp32 NHWC
+ * [B][2h][2w][N] (or NULL) and/or the split output (NHWC, or chunk-major
+ * [3][B][N/32][2h][2w][32] with out_cm). int_in: the input is integer-valued (ŷ, |v| ≤ 127;
+ * exact in its hi plane), only that plane is read. γ: iclr17_split_packed of the GDN packing. */
+int iclr17_synthesis_deconv_igdn_x6k(const uint16_t* in_split, int B, int h, int w, int N,
+                                     const uint16_t* w_x6k, const float* bias,
+                                     const float* beta_eff, const uint16_t* gamma_split,
+                                     float* out, uint16_t* out_split, int out_cm, int int_in,
+                                     void* stream);
+
 /* ------------------------------------------------------------------ bf16 throughput mode
  * The codec forward with bf16 activations (NHWC [B][h][w][N], round to nearest even), bf16
  * weights and γ, ONE v_mfma_f32_16x16x32_bf16 product per MAC with fp32 accumulation, fp32

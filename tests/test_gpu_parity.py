@@ -549,3 +549,44 @@ def test_chunk_major_split_deconv2_to_deconv3(device, N):
         b = kernels.deconv3_x6(s_cm, dec.packed_x6(), dec.deconv3.bias, x_ref=x, want_recon=True)
     for u, v in zip(a, b):
         assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("N", [192, 128])
+@pytest.mark.parametrize("hw", [(5, 7), (20, 34)])
+def test_x6k_deconv_igdn(device, N, hw):
+    """deconv + IGDN on the 32x32x16 x6 engine (csrc/engine_x6k.hip) against the oracle
+    (synthesis_17.py:15-22, GDN.py:64-94 inverse), on grids that are and are not whole 16×16
+    tiles: fp32 output at the fp32 bar; the split output merges to it exactly, in both the NHWC
+    and the chunk-major form; on an integer input (ŷ) the int_in form (only the hi plane read,
+    three products per MAC) is bit-identical to the full six-product form; and it agrees with
+    the 16x16x32 x6 engine to fp32 summation-order noise."""
+    net, sd = net_for(N, 1, device), sd_for(N, 1)
+    dec = net.Decoder
+    F = torch.nn.functional
+    h, w = hw
+    x1, x2 = dec.packed_x6k()
+    d1, d2 = dec.packed()[:2]
+    q1, q2 = dec.igdn1.effective_params_x6(), dec.igdn2.effective_params_x6()
+    yq = torch.round(torch.from_numpy(synth.uniform(5, (2, N, h, w), -6, 6)))
+    act = torch.from_numpy(synth.normal_like(6, (2, N, h, w), 0.7))
+    with torch.no_grad():
+        for inp, lay, wx, wp, q, key in ((yq, "deconv1", x1, d1, q1, "igdn1"),
+                                         (act, "deconv2", x2, d2, q2, "igdn2")):
+            ins = kernels.split_planes(nhwc(inp).contiguous().to(device))
+            s, f = kernels.deconv_igdn_x6k(ins, wx, getattr(dec, lay).bias, q[0], q[2], want_f32=True)
+            r_v = F.conv_transpose2d(inp, sd[f"Decoder.{lay}.weight"], sd[f"Decoder.{lay}.bias"],
+                                     stride=2, padding=2, output_padding=1)
+            r_s = oracle.gdn(r_v, sd[f"Decoder.{key}.beta"], sd[f"Decoder.{key}.gamma"], True)
+            assert f.shape == (2, 2 * h, 2 * w, N)
+            assert rel_err(f, nhwc(r_s)) < REL, lay
+            assert torch.equal(kernels.merge_planes(s), f)
+            scm, _ = kernels.deconv_igdn_x6k(ins, wx, getattr(dec, lay).bias, q[0], q[2],
+                                             chunk_major=True)
+            assert scm.shape == (3, 2, N // 32, 2 * h, 2 * w, 32)
+            assert torch.equal(scm.permute(0, 1, 3, 4, 2, 5).reshape(s.shape), s)
+            _, f_old, _ = kernels.deconv_igdn_x6(ins, wp, getattr(dec, lay).bias, *q, want_f32=True)
+            assert rel_err(f, f_old) < 2e-6, lay
+            if lay == "deconv1":
+                si, fi = kernels.deconv_igdn_x6k(ins, wx, dec.deconv1.bias, q[0], q[2], want_f32=True,
+                                                 int_in=True)
+                assert torch.equal(fi, f) and torch.equal(si, s)

@@ -1,0 +1,50 @@
+"""Times deconv2+IGDN2 (B=64, 32×32 → 64×64, N=192) on the 16x16x32 x6 engine and on the
+32x32x16 x6k engine, interleaved, with HIP events; a short program for PMC passes
+(tools/pmc_kernel.sh TOOL=tools/x6k_time.py)."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from iclr_17_compression_amd import kernels, synth  # noqa: E402
+from iclr_17_compression_amd.model import ImageCompressor  # noqa: E402
+
+N, B = 192, 64
+REPS = int(os.environ.get("REPS", "20"))
+dev = torch.device("cuda", 0)
+net = ImageCompressor(out_channel_N=N)
+net.load_state_dict({k: torch.from_numpy(v) for k, v in synth.trained_like_state_dict(N, 1).items()})
+net = net.to(dev).eval()
+dec = net.Decoder
+d1, d2 = dec.packed()[:2]
+x1, x2 = dec.packed_x6k()
+q1, q2 = dec.igdn1.effective_params_x6(), dec.igdn2.effective_params_x6()
+act = torch.from_numpy(synth.normal_like(6, (B, 32, 32, N), 0.7)).to(dev)
+yq = torch.round(torch.from_numpy(synth.uniform(5, (B, 16, 16, N), -6, 6))).to(dev)
+hs, ys = kernels.split_planes(act), kernels.split_planes(yq)
+runs = {
+    "deconv2_old": lambda: kernels.deconv_igdn_x6(hs, d2, dec.deconv2.bias, *q2, chunk_major=True),
+    "deconv2_x6k": lambda: kernels.deconv_igdn_x6k(hs, x2, dec.deconv2.bias, q2[0], q2[2], chunk_major=True),
+    "deconv1_old": lambda: kernels.deconv_igdn_x6(ys, d1, dec.deconv1.bias, *q1),
+    "deconv1_x6k": lambda: kernels.deconv_igdn_x6k(ys, x1, dec.deconv1.bias, q1[0], q1[2]),
+    "deconv1_x6k_int": lambda: kernels.deconv_igdn_x6k(ys, x1, dec.deconv1.bias, q1[0], q1[2], int_in=True),
+}
+sel = os.environ.get("ONLY", "").split(",") if os.environ.get("ONLY") else list(runs)
+with torch.no_grad():
+    for k in sel:
+        for _ in range(3):
+            runs[k]()
+    torch.cuda.synchronize()
+    t = {k: [] for k in sel}
+    for _ in range(REPS):
+        for k in sel:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            runs[k]()
+            e1.record()
+            t[k].append((e0, e1))
+    torch.cuda.synchronize()
+for k in sel:
+    ms = sorted(a.elapsed_time(b) for a, b in t[k])
+    print(f"{k}: median {ms[len(ms) // 2]:.4f} ms, min {ms[0]:.4f}")

@@ -88,7 +88,7 @@ class Step:
         self.enc = net.Encoder.packed()
         self.dec = net.Decoder.packed()
         self.d3x6 = net.Decoder.packed_x6()
-        self.dx6k = net.Decoder.packed_x6k() if kernels.X6K else None
+        self.dx6k = net.Decoder.packed_x6k()
         self.rate = net.bitEstimator.packed()
         gdns = (net.Encoder.gdn1, net.Encoder.gdn2, net.Decoder.igdn1, net.Decoder.igdn2)
         self.w1x6 = net.Encoder.packed_conv1_x6()
@@ -126,15 +126,15 @@ class Step:
             ev(2)
             y_hat, partial, _, ys = kernels.conv3_quant_rate_x6(hs, w3, self.rate, rtab=self.rtab)
             ev(3)
-            if kernels.X6K:   # the 32x32x16 x6 engine (Synthesis_net_17.decode's x6 path)
-                x1, x2 = self.dx6k
-                hs, _ = kernels.deconv_igdn_x6k(ys, x1, net.Decoder.deconv1.bias, e3[0], e3[2])
-                ev(4)
+            # Synthesis_net_17.decode's x6 path: deconv1 on ŷ in the x6k engine's integer-input
+            # form, deconv2 on the 16x16x32 engine (or the x6k one with ICLR17_X6K=1)
+            x1, x2 = self.dx6k
+            hs, _ = kernels.deconv_igdn_x6k(ys, x1, net.Decoder.deconv1.bias, e3[0], e3[2], int_in=True)
+            ev(4)
+            if kernels.X6K:
                 hs, _ = kernels.deconv_igdn_x6k(hs, x2, net.Decoder.deconv2.bias, e4[0], e4[2],
                                                 chunk_major=D3_CM)
             else:
-                hs, _, _ = kernels.deconv_igdn_x6(ys, d1, net.Decoder.deconv1.bias, *e3)
-                ev(4)
                 hs, _, _ = kernels.deconv_igdn_x6(hs, d2, net.Decoder.deconv2.bias, *e4, chunk_major=D3_CM)
             ev(5)
             clipped, _, _ = kernels.deconv3_x6(hs, self.d3x6, net.Decoder.deconv3.bias)
@@ -518,7 +518,7 @@ def run_codec(args, dev):
         y = kernels.rans_decode(words, offsets, cum, B, h, w, N)
         e2.record()
         split = kernels.split_planes(y) if kernels.precision() == "x6" else None
-        clipped, _, _ = net.Decoder.decode(y, want_recon=False, y_split=split)
+        clipped, _, _ = net.Decoder.decode(y, want_recon=False, y_split=split, y_integral=True)
         if timed:
             t_enc.append((e0, e1))
             t_dec.append((e1, e2))

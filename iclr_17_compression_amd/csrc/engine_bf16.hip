@@ -55,6 +55,9 @@ namespace bfm {
 #ifndef ICLR17_C1P_STAMPS
 #define ICLR17_C1P_STAMPS 0   // diagnostic build: per-phase s_memtime stamps of conv1p
 #endif
+#ifndef ICLR17_BF_RTAB_LDS
+#define ICLR17_BF_RTAB_LDS 1   // conv3: the rate table rows of the tile in LDS (not L2 gathers)
+#endif
 #ifndef ICLR17_BF_NST
 #define ICLR17_BF_NST 4   // weight ring stages (F + 2 for F DMA groups in flight)
 #endif
@@ -506,6 +509,18 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
     // conv3 + model.py:56 round (half to even) + model.py:71-73 rate: rows 8m .. 8m + 7 of every
     // accumulator tile (registers 4m .. 4m + 3 of the lane's half h)
     float bits = 0.f;
+    // the rate table rows of this tile's NB channels: staged in LDS after the K-split exchange
+    // area (KS == 2, ICLR17_BF_RTAB_LDS) or read from L2
+    constexpr bool RT_LDS = ICLR17_BF_RTAB_LDS && KK::KS == 2;
+    constexpr int XS_BYTES = (KK::KS * NW * NT * 8 * 64 * 4 + 1023) / 1024 * 1024;
+    constexpr int RTU = NB * RT_W / 4, RTP = (RTU + 63) / 64;   // 16-byte units, 1 KB pieces
+    static_assert(!RT_LDS || (NB * RT_W % 4 == 0 && XS_BYTES + RTP * 1024 <= KK::KS * KK::MAIN_LDS),
+                  "rate table stage");
+    const float* const stab = (const float*)(smem + XS_BYTES);
+    auto rtab_at = [&](int cl, int v, int c) -> float {
+      if constexpr (RT_LDS) return stab[cl * RT_W + v + RT_K];
+      else return a.rtab[c * RT_W + v + RT_K];
+    };
     auto quant_rows = [&](int m) {
       if (o < 0) return;
 #pragma unroll
@@ -517,7 +532,7 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
         for (int j = 0; j < 4; ++j) {
           q[j] = rintf(y[j]);
           // integer latents: the per-channel table of the same element_bits (bit-identical)
-          bits += fabsf(q[j]) <= (float)RT_K ? a.rtab[(ch + j) * RT_W + (int)q[j] + RT_K]
+          bits += fabsf(q[j]) <= (float)RT_K ? rtab_at(ch - nb * NB + j, (int)q[j], ch + j)
                                              : element_bits(q[j], a.rate, CO, ch + j);
         }
         if (a.y_f32) *(f4*)(a.y_f32 + o * CO + ch) = y;
@@ -546,8 +561,16 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
       };
       if (kg == 0) put(8); else put(0);   // the rows the other group finalises
       __syncthreads();
+      if constexpr (RT_LDS) {   // no DMA in flight at the barrier above; landed by the one below
+        for (int pc = wv; pc < RTP; pc += KK::KS * NW) {
+          const int u = pc * 64 + lane;
+          glds16(u < RTU ? (const void*)(a.rtab + (long)nb * NB * RT_W + u * 4) : (const void*)g_zero16,
+                 smem + XS_BYTES + pc * 1024);
+        }
+      }
       if (kg == 0) add(0); else add(8);
-      __syncthreads();   // exchange reads done before red[] reuses the area
+      if constexpr (RT_LDS) vm_barrier();   // table landed; exchange reads done before red[] reuse
+      else __syncthreads();                 // exchange reads done before red[] reuses the area
 #if ICLR17_K5_STAMPS
       st4 = __builtin_amdgcn_s_memtime();
 #endif

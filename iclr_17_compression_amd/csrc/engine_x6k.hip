@@ -28,6 +28,8 @@
 // split form (NHWC, or chunk-major [3][B][N/32][h][w][32] for deconv3) and optionally fp32.
 #include <string.h>
 
+#include <type_traits>
+
 #include "common.h"
 #include "k5_common.h"
 
@@ -384,9 +386,13 @@ __device__ __forceinline__ void x6k_body(const XArgs& a, unsigned char* smem, in
   }
 }
 
-template <int MODE, int TH, int CO, int CI, int EPI, bool INT_IN>
+// INT_OK: the caller guarantees an integer-valued input (ŷ). A workgroup then checks that every
+// value of its input window is below 256 in magnitude (so exact in the hi plane: the mid and lo
+// planes are zero) and runs the INT_IN body; otherwise (and for Inf / NaN) the full body.
+template <int MODE, int TH, int CO, int CI, int EPI, bool INT_OK>
 __global__ void __launch_bounds__(TH / 2 * 64, 1) x6k_kernel(const XArgs a) {
-  using KK = XK<MODE, TH, CO, CI, INT_IN>;
+  using KK = XK<MODE, TH, CO, CI, false>;
+  static_assert(KK::LDS >= XK<MODE, TH, CO, CI, true>::LDS, "LDS");
   __shared__ __attribute__((aligned(16))) unsigned char smem[KK::LDS];
   int bid = blockIdx.x;
   const int per_ph = a.tiles_x * a.tiles_y * a.B;
@@ -396,16 +402,43 @@ __global__ void __launch_bounds__(TH / 2 * 64, 1) x6k_kernel(const XArgs a) {
   bid /= a.tiles_x;
   const int ty = bid % a.tiles_y;
   const int b = bid / a.tiles_y;
-  if constexpr (MODE == BM_CONV) {
-    x6k_body<MODE, TH, CO, CI, EPI, INT_IN, 0>(a, smem, b, ty, tx);
-  } else {
-    switch (ph) {   // wave-uniform: the tap lists are compile-time per phase
-      case 0: x6k_body<MODE, TH, CO, CI, EPI, INT_IN, 0>(a, smem, b, ty, tx); break;
-      case 1: x6k_body<MODE, TH, CO, CI, EPI, INT_IN, 1>(a, smem, b, ty, tx); break;
-      case 2: x6k_body<MODE, TH, CO, CI, EPI, INT_IN, 2>(a, smem, b, ty, tx); break;
-      default: x6k_body<MODE, TH, CO, CI, EPI, INT_IN, 3>(a, smem, b, ty, tx); break;
+  bool small = false;
+  if constexpr (INT_OK) {
+    // the hi plane of the window the patch stages, all CI channels, 8 values per 16-byte load:
+    // |v| < 256 ⇔ (bits & 0x7fff) < 0x4380 (256 in bf16; Inf / NaN compare above it)
+    using P = Patch<MODE, TH>;
+    constexpr int COLS = MODE == BM_CONV ? 35 : 18, PER = COLS * CI / 8;
+    const int iy0 = MODE == BM_CONV ? 2 * ty * TH - 2 : ty * TH - 1;
+    const int ix0 = MODE == BM_CONV ? 2 * tx * 16 - 2 : tx * 16 - 1;
+    const u16* inb = a.in + (long)b * a.Hin * a.Win * CI;
+    unsigned bad = 0;
+    for (int u = threadIdx.x; u < P::ROWS * PER; u += TH / 2 * 64) {
+      const int r = u / PER, rem = u - r * PER, c = rem / (CI / 8), k8 = rem - c * (CI / 8);
+      const int iy = iy0 + r, ix = ix0 + c;
+      if ((unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win) {
+        const u4 v = *(const u4*)(inb + ((long)iy * a.Win + ix) * CI + 8 * k8);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          bad |= (unsigned)((v[e] & 0x7fffu) >= 0x4380u) | (unsigned)(((v[e] >> 16) & 0x7fffu) >= 0x4380u);
+      }
     }
+    small = __syncthreads_or(bad) == 0;
   }
+  auto run = [&](auto int_in) {
+    constexpr bool II = decltype(int_in)::value;
+    if constexpr (MODE == BM_CONV) {
+      x6k_body<MODE, TH, CO, CI, EPI, II, 0>(a, smem, b, ty, tx);
+    } else {
+      switch (ph) {   // wave-uniform: the tap lists are compile-time per phase
+        case 0: x6k_body<MODE, TH, CO, CI, EPI, II, 0>(a, smem, b, ty, tx); break;
+        case 1: x6k_body<MODE, TH, CO, CI, EPI, II, 1>(a, smem, b, ty, tx); break;
+        case 2: x6k_body<MODE, TH, CO, CI, EPI, II, 2>(a, smem, b, ty, tx); break;
+        default: x6k_body<MODE, TH, CO, CI, EPI, II, 3>(a, smem, b, ty, tx); break;
+      }
+    }
+  };
+  if (INT_OK && small) run(std::true_type{});
+  else run(std::false_type{});
 }
 
 // ---------------------------------------------------------------------------- packing

@@ -69,7 +69,8 @@ class ImageCompressor(nn.Module):
         y_hat, bits_partial, y_split = q["y_hat"], q["bits_partial"], q["y_split"]
         clipped, recon, sse_partial = self.Decoder.decode(y_hat, x_ref=x if x_ref_sse else None,
                                                           want_recon=want_recon, y_split=y_split,
-                                                          y_bf16=q.get("y_bf16"))
+                                                          y_bf16=q.get("y_bf16"),
+                                                          y_integral=not training)
         return {"clipped": clipped, "y_hat": y_hat, "bits_partial": bits_partial,
                 "sse_partial": sse_partial, "recon": recon, "y": q["y"]}
 
@@ -211,7 +212,8 @@ class ImageCompressor(nn.Module):
                                     K, P)
         split = kernels.split_planes(y_hat) if kernels.precision() == "x6" else None
         ybf = kernels.to_bf16(y_hat) if kernels.precision() == "bf16" else None
-        clipped, _, _ = self.Decoder.decode(y_hat, want_recon=False, y_split=split, y_bf16=ybf)
+        clipped, _, _ = self.Decoder.decode(y_hat, want_recon=False, y_split=split, y_bf16=ybf,
+                                            y_integral=True)
         return {"y_hat": y_hat.permute(0, 3, 1, 2).contiguous(), "x_hat": clipped}
 
     @torch.no_grad()
@@ -250,7 +252,7 @@ class ImageCompressor(nn.Module):
             if x6:
                 self.Encoder.packed_conv1_x6()
                 self.Decoder.packed_x6()
-                if kernels.X6K and not backward:
+                if not backward:
                     self.Decoder.packed_x6k()
                 for g in gdns:
                     g.effective_params_x6()

@@ -99,10 +99,12 @@ class Synthesis_net_17(nn.Module):
         the latent is already channels-last, e.g. the Encoder's own output)."""
         return y.permute(0, 2, 3, 1).contiguous()
 
-    def decode(self, y_nhwc, x_ref=None, want_recon=True, y_split=None, y_bf16=None):
+    def decode(self, y_nhwc, x_ref=None, want_recon=True, y_split=None, y_bf16=None,
+               y_integral=False):
         """NHWC latent → (clipped NCHW, unclipped NCHW | None, SSE partials | None).
         With ``y_split`` (the latent in x6 split form) the three layers run in the x6 mode, with
-        ``y_bf16`` (bf16 bit patterns) in the bf16 throughput mode."""
+        ``y_bf16`` (bf16 bit patterns) in the bf16 throughput mode. ``y_integral``: the latent
+        is ŷ = round(y) (model.py:56), so deconv1 runs the x6k engine's integer-input form."""
         d1, d2, d3, g1, g2 = self.packed()
         if y_bf16 is not None:
             b1, b2, b3 = self.packed_bf16()
@@ -112,13 +114,16 @@ class Synthesis_net_17(nn.Module):
             return kernels.deconv3_bf16(h, b3, self.deconv3.bias, x_ref=x_ref, want_recon=want_recon)
         if y_split is not None:
             q1, q2 = self.igdn1.effective_params_x6(), self.igdn2.effective_params_x6()
-            if kernels.X6K:   # the 32x32x16 x6 engine (csrc/engine_x6k.hip)
-                x1, x2 = self.packed_x6k()
-                hs, _ = kernels.deconv_igdn_x6k(y_split, x1, self.deconv1.bias, q1[0], q1[2])
-                hs, _ = kernels.deconv_igdn_x6k(hs, x2, self.deconv2.bias, q2[0], q2[2],
-                                                chunk_major=True)
+            if y_integral or kernels.X6K:
+                # ŷ: three of the six part products vanish (csrc/engine_x6k.hip, int_in)
+                hs, _ = kernels.deconv_igdn_x6k(y_split, self.packed_x6k()[0], self.deconv1.bias,
+                                                q1[0], q1[2], int_in=y_integral)
             else:
                 hs, _, _ = kernels.deconv_igdn_x6(y_split, d1, self.deconv1.bias, *q1)
+            if kernels.X6K:   # deconv2 on the 32x32x16 x6 engine (A/B; the same MFMA rate)
+                hs, _ = kernels.deconv_igdn_x6k(hs, self.packed_x6k()[1], self.deconv2.bias, q2[0],
+                                                q2[2], chunk_major=True)
+            else:
                 hs, _, _ = kernels.deconv_igdn_x6(hs, d2, self.deconv2.bias, *q2, chunk_major=True)
             return kernels.deconv3_x6(hs, self.packed_x6(), self.deconv3.bias, x_ref=x_ref,
                                       want_recon=want_recon)

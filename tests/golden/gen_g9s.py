@@ -18,7 +18,7 @@ gen_goldens.py does) under several summation orders of its own:
 
 and writes, per image and per order, the latent flip count against the default order and the
 raw relative Δbpp, ΔPSNR and ΔMS-SSIM, plus the distance of every flipped y from its rounding
-boundary. Only these numbers are committed (tests/golden/g9s_*.json); they are data, not
+boundary, and per fp32 order the number of latents it rounds differently from the float64 run. Only these numbers are committed (tests/golden/g9s_*.json); they are data, not
 reference source. tests/test_gpu_operating_point.py holds the GPU to this floor.
 
     python tests/golden/gen_g9s.py [--sets g8,g9] [--orders ...]
@@ -119,6 +119,11 @@ def summarise(set_name: str, runs: dict) -> dict:
         rows.append(r)
     total = {o: sum(r["orders"][o]["latent_flips"] for r in rows) for o in rows[0]["orders"]}
     fp32_orders = [o for o in rows[0]["orders"] if o != "fp64"]
+    # each fp32 order's latents rounded differently from the float64 run (the exact value the
+    # orders approximate): how many latents the reference itself rounds "wrong", order by order
+    wrong = ({o: int(sum(int((runs[o]["y_hat"][i] != runs["fp64"]["y_hat"][i]).sum())
+                         for i in range(len(rows)))) for o in ["default"] + fp32_orders}
+             if "fp64" in runs else {})
     return {
         "note": ("the reference (model.py:46-80) under several CPU summation orders of its own, "
                  "each compared with the default (oneDNN) order the fixture holds; generated by "
@@ -126,6 +131,8 @@ def summarise(set_name: str, runs: dict) -> dict:
         "fixture": fixture, "N": meta["N"], "orders": list(runs),
         "latents_per_set": int(sum(v.size for v in base["y_hat"])),
         "total_flips_vs_default": total,
+        "total_wrong_vs_fp64": wrong,
+        "max_wrong_vs_fp64_fp32": max(wrong.values()) if wrong else None,
         "max_images_with_flips_fp32": max(sum(1 for r in rows if r["orders"][o]["latent_flips"])
                                           for o in fp32_orders),
         "set_spread_fp32": {k: max(r["fp32_spread"][k] for r in rows) for k in

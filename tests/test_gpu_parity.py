@@ -590,3 +590,12 @@ def test_x6k_deconv_igdn(device, N, hw):
                 si, fi = kernels.deconv_igdn_x6k(ins, wx, dec.deconv1.bias, q[0], q[2], want_f32=True,
                                                  int_in=True)
                 assert torch.equal(fi, f) and torch.equal(si, s)
+                # a latent beyond bf16's 8 significant bits (300): the workgroups that see it run
+                # the six-product form, and the result still equals the full form's
+                big = inp.clone()
+                big[1, 7, h // 2, w // 2] = 300.0
+                bs = kernels.split_planes(nhwc(big).contiguous().to(device))
+                _, fb = kernels.deconv_igdn_x6k(bs, wx, dec.deconv1.bias, q[0], q[2], want_f32=True)
+                _, fbi = kernels.deconv_igdn_x6k(bs, wx, dec.deconv1.bias, q[0], q[2], want_f32=True,
+                                                 int_in=True)
+                assert torch.equal(fbi, fb) and not torch.equal(fb, f)

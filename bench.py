@@ -126,10 +126,12 @@ class Step:
             ev(2)
             y_hat, partial, _, ys = kernels.conv3_quant_rate_x6(hs, w3, self.rate, rtab=self.rtab)
             ev(3)
-            # Synthesis_net_17.decode's x6 path: deconv1 on ŷ in the x6k engine's integer-input
-            # form, deconv2 on the 16x16x32 engine (or the x6k one with ICLR17_X6K=1)
+            # Synthesis_net_17.decode's x6 path (ICLR17_X6K=1: deconv1 / deconv2 on the x6k engine)
             x1, x2 = self.dx6k
-            hs, _ = kernels.deconv_igdn_x6k(ys, x1, net.Decoder.deconv1.bias, e3[0], e3[2], int_in=True)
+            if kernels.X6K:   # deconv1 on ŷ in the x6k engine's integer-input form (A/B)
+                hs, _ = kernels.deconv_igdn_x6k(ys, x1, net.Decoder.deconv1.bias, e3[0], e3[2], int_in=True)
+            else:
+                hs, _, _ = kernels.deconv_igdn_x6(ys, d1, net.Decoder.deconv1.bias, *e3)
             ev(4)
             if kernels.X6K:
                 hs, _ = kernels.deconv_igdn_x6k(hs, x2, net.Decoder.deconv2.bias, e4[0], e4[2],

@@ -411,17 +411,23 @@ __global__ void __launch_bounds__(TH / 2 * 64, 1) x6k_kernel(const XArgs a) {
     const int iy0 = MODE == BM_CONV ? 2 * ty * TH - 2 : ty * TH - 1;
     const int ix0 = MODE == BM_CONV ? 2 * tx * 16 - 2 : tx * 16 - 1;
     const u16* inb = a.in + (long)b * a.Hin * a.Win * CI;
-    unsigned bad = 0;
-    for (int u = threadIdx.x; u < P::ROWS * PER; u += TH / 2 * 64) {
+    // every load issued before the first compare (one memory latency, not one per load)
+    constexpr int NTHR = TH / 2 * 64, IT = (P::ROWS * PER + NTHR - 1) / NTHR;
+    u4 v[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int u = threadIdx.x + it * NTHR;
       const int r = u / PER, rem = u - r * PER, c = rem / (CI / 8), k8 = rem - c * (CI / 8);
       const int iy = iy0 + r, ix = ix0 + c;
-      if ((unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win) {
-        const u4 v = *(const u4*)(inb + ((long)iy * a.Win + ix) * CI + 8 * k8);
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          bad |= (unsigned)((v[e] & 0x7fffu) >= 0x4380u) | (unsigned)(((v[e] >> 16) & 0x7fffu) >= 0x4380u);
-      }
+      const bool ok = u < P::ROWS * PER && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
+      v[it] = ok ? *(const u4*)(inb + ((long)iy * a.Win + ix) * CI + 8 * k8) : u4{0u, 0u, 0u, 0u};
     }
+    unsigned bad = 0;
+#pragma unroll
+    for (int it = 0; it < IT; ++it)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        bad |= (unsigned)((v[it][e] & 0x7fffu) >= 0x4380u) | (unsigned)(((v[it][e] >> 16) & 0x7fffu) >= 0x4380u);
     small = __syncthreads_or(bad) == 0;
   }
   auto run = [&](auto int_in) {

@@ -114,8 +114,12 @@ class Synthesis_net_17(nn.Module):
             return kernels.deconv3_bf16(h, b3, self.deconv3.bias, x_ref=x_ref, want_recon=want_recon)
         if y_split is not None:
             q1, q2 = self.igdn1.effective_params_x6(), self.igdn2.effective_params_x6()
-            if y_integral or kernels.X6K:
-                # ŷ: three of the six part products vanish (csrc/engine_x6k.hip, int_in)
+            if kernels.X6K:
+                # deconv1 on the x6k engine; on ŷ three of its six part products vanish (int_in),
+                # and the six-product form gives the same bits on any integer input, so
+                # Decoder(round(y)) reproduces the codec's reconstruction without knowing its
+                # input is ŷ. Not the default: faster alone (0.154 vs 0.171 ms at B=64), slower in
+                # the chain (one 140 KB workgroup per CU shares no CU with conv3 / deconv2)
                 hs, _ = kernels.deconv_igdn_x6k(y_split, self.packed_x6k()[0], self.deconv1.bias,
                                                 q1[0], q1[2], int_in=y_integral)
             else:

@@ -17,8 +17,17 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name: str) -> str:
-    name = re.sub(r"\(.*", "", name)
-    return re.sub(r"^.*?(iclr17::)", r"\1", name)[:160]
+    """Kernel name without its trailing argument list (an anonymous namespace stays)."""
+    name = name.strip()
+    if name.endswith(")"):
+        depth = 0
+        for i in range(len(name) - 1, -1, -1):
+            depth += {")": 1, "(": -1}.get(name[i], 0)
+            if depth == 0:
+                name = name[:i]
+                break
+    name = re.sub(r"^void ", "", name)
+    return name.replace("(anonymous namespace)::", "")[:160]
 
 
 def main() -> None:

@@ -39,6 +39,7 @@ X6_LAYERS = ("conv1_gdn1", "conv2_gdn2", "conv3_quant_rate", "deconv1_igdn1", "d
 HBM_PEAK_GBS = 8000.0
 # deconv2 → deconv3 through the chunk-major split form (ICLR17_D3_CM=0: the NHWC split, for A/B)
 D3_CM = os.environ.get("ICLR17_D3_CM", "1") != "0"
+FOLD_BITS = os.environ.get("ICLR17_FOLD_BITS", "1") != "0"   # bpp's reduction inside deconv3 (A/B)
 
 LAYERS = ("conv1_gdn1", "conv2_gdn2", "conv3_quant_rate", "deconv1_igdn1", "deconv2_igdn2",
           "deconv3_clamp", "bits_reduce")
@@ -116,7 +117,13 @@ class Step:
             ev(4)
             h = kernels.deconv_igdn_bf16(h, d2b, net.Decoder.deconv2.bias, *e4)
             ev(5)
-            clipped, _, _ = kernels.deconv3_bf16(h, d3b, net.Decoder.deconv3.bias)
+            # bpp's reduction (model.py:71-78) inside deconv3's kernel (ImageCompressor.forward)
+            if FOLD_BITS:
+                clipped, _, _, bpp = kernels.deconv3_bf16(h, d3b, net.Decoder.deconv3.bias,
+                                                          bits=(partial, self.scale))
+            else:
+                clipped, _, _ = kernels.deconv3_bf16(h, d3b, net.Decoder.deconv3.bias)
+                bpp = None
         elif kernels.precision() == "x6":
             e1, e2, e3, e4 = self.g6
             hs, _, _ = kernels.conv1x6_gdn(self.x, self.w1x6, net.Encoder.conv1.bias, e1[0], e1[2],
@@ -139,7 +146,12 @@ class Step:
             else:
                 hs, _, _ = kernels.deconv_igdn_x6(hs, d2, net.Decoder.deconv2.bias, *e4, chunk_major=D3_CM)
             ev(5)
-            clipped, _, _ = kernels.deconv3_x6(hs, self.d3x6, net.Decoder.deconv3.bias)
+            if D3_CM and FOLD_BITS:
+                clipped, _, _, bpp = kernels.deconv3_x6(hs, self.d3x6, net.Decoder.deconv3.bias,
+                                                        bits=(partial, self.scale))
+            else:
+                clipped, _, _ = kernels.deconv3_x6(hs, self.d3x6, net.Decoder.deconv3.bias)
+                bpp = None
         else:
             h = kernels.conv1_gdn(self.x, w1, net.Encoder.conv1.bias, g1[0], g1[1], N)
             ev(1)
@@ -152,9 +164,11 @@ class Step:
             h = kernels.deconv_igdn(h, d2, net.Decoder.deconv2.bias, q2[0], q2[1])
             ev(5)
             clipped, _, _ = kernels.deconv3(h, d3, net.Decoder.deconv3.bias)
+            bpp = None
         ev(6)
         self.last_partial = partial
-        _, bpp = kernels.reduce_partials(partial, self.scale, per_image=False)
+        if bpp is None:   # the separate reduction kernel (fp32 chain, or ICLR17_FOLD_BITS=0)
+            _, bpp = kernels.reduce_partials(partial, self.scale, per_image=False)
         ev(7)
         return clipped, y_hat, bpp
 

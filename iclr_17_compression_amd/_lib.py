@@ -61,6 +61,10 @@ SIGNATURES = {
     "iclr17_synthesis_deconv3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P]),
     "iclr17_synthesis_deconv3_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P]),
     "iclr17_synthesis_deconv3_x6_cm": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P]),
+    "iclr17_synthesis_deconv3_x6_cm_bits": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I,
+                                                 _P, _I, _P, _P, _D, _P]),
+    "iclr17_synthesis_deconv3_bf16_bits": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I,
+                                                _P, _I, _P, _P, _D, _P]),
     "iclr17_output_partials_per_image": (_I, [_I, _I]),
     "iclr17_split_planes": (_I, [_P, ctypes.c_long, _P, _P]),
     "iclr17_split_packed": (_I, [_P, _I, _I, _I, _P, _P]),

@@ -105,7 +105,55 @@ struct EngineArgs {
   int out_cm, in_cm;
   const unsigned short* ggamma6;    // x6: γ_eff split, [3][CO/8][CO][8] bf16 (plane CO·CO)
   const unsigned short* ggammaT6;   // x6 backward: the transposed packing of γ_eff, split
+  // deconv3 (x6 / bf16): conv3's bit partials [B][fold_T] reduced by workgroup 0 before its tile
+  // (fold_bits: reduce_partials_kernel's arithmetic and order), or nullptr
+  const double* fold_partial;
+  int fold_T;
+  double* fold_per_image;   // [B] or nullptr
+  float* fold_total;        // scale · Σ, 0-dim
+  double fold_scale;
 };
+
+// iclr17_reduce_partials inside the last kernel of the eval chain (deconv3): the per-image sums of
+// conv3's T bit partials and scale · their total, by workgroup 0 before its own tile, which saves
+// the chain a kernel launch and boundary. Arithmetic and order are reduce_partials_kernel's
+// (csrc/aux.hip): per image a lane-strided sum over t ≡ lane (mod 64) in t order, a fixed xor
+// butterfly, then the images added in order by thread 0 — so the results are bit-identical.
+// The loads of a wave's images go out together (one memory latency for the common T ≤ 64).
+template <int NTHR>
+__device__ __forceinline__ void fold_bits(const EngineArgs& a, double* img /* LDS, 64 doubles */) {
+  constexpr int NW = NTHR / 64, KI = (64 + NW - 1) / NW;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int T = a.fold_T;
+  double acc = 0.0;
+  for (int b0 = 0; b0 < a.B; b0 += 64) {
+    const int nb = a.B - b0 < 64 ? a.B - b0 : 64;
+    double v[KI];
+#pragma unroll
+    for (int k = 0; k < KI; ++k) {
+      const int b = wave + k * NW;
+      v[k] = b < nb && lane < T ? a.fold_partial[(long)(b0 + b) * T + lane] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < KI; ++k) {
+      const int b = wave + k * NW;
+      if (b >= nb) continue;
+      double s = 0.0 + v[k];
+      for (int t = lane + 64; t < T; t += 64) s += a.fold_partial[(long)(b0 + b) * T + t];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+      if (lane == 0) {
+        img[b] = s;
+        if (a.fold_per_image) a.fold_per_image[b0 + b] = s;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int b = 0; b < nb; ++b) acc += img[b];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && a.fold_total) *a.fold_total = (float)(acc * a.fold_scale);
+}
 
 struct TileInfo {
   int b, ty, tx, py, px, nb;
@@ -1297,6 +1345,7 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
   constexpr int AI_W = (NAI + 3) / 4;   // x6: 16 (wave 0..3 takes i = w + 4j, i < 61)
   static_assert(3 * 64 * 65 <= D3_LDS, "epilogue block fits the stages");
   __shared__ __attribute__((aligned(16))) float smem[D3_LDS];
+  if (a.fold_partial != nullptr && blockIdx.x == 0) fold_bits<256>(a, (double*)smem);
   float* const sA = smem;
   float* const sB = smem + D3_SA;
 
@@ -1647,6 +1696,7 @@ __global__ void __launch_bounds__(512) deconv3_bf16_kernel(const EngineArgs a) {
   constexpr int LDS = 2 * SA + 2 * PB;
   static_assert(3 * 64 * 65 + 16 <= LDS, "epilogue block fits");
   __shared__ __attribute__((aligned(16))) float smem[LDS];
+  if (a.fold_partial != nullptr && blockIdx.x == 0) fold_bits<512>(a, (double*)smem);
   float* const sA = smem;
   float* const sB = smem + 2 * SA;
 
@@ -2521,10 +2571,18 @@ int iclr17_synthesis_deconv_igdn(const float* in, int B, int h, int w, int N,
 
 // w: iclr17_round_packed(9, N, 48) of the ICLR17_W_DECONV9 packing (bf16 mode) or its
 // iclr17_split_packed(9, N, 48) planes (x6)
+struct FoldBits {
+  const double* partial;
+  int T;
+  double* per_image;
+  float* total;
+  double scale;
+};
+
 static int launch_deconv3_halo(const uint16_t* in, int B, int H, int W, int N, const void* w,
                                const float* bias, const float* x, float* clipped, float* recon,
                                double* sse_partial, int sse_unclipped, void* stream, bool bf,
-                               int in_cm = 0) {
+                               int in_cm = 0, const FoldBits* fold = nullptr) {
   const char* what = bf ? "deconv3_bf16" : "deconv3_x6";
   int rc = check_dims(B, H, W, N);
   if (rc) return rc;
@@ -2545,6 +2603,12 @@ static int launch_deconv3_halo(const uint16_t* in, int B, int H, int W, int N, c
   a.in_plane = (long)B * a.Hin * a.Win * N;
   a.tiles_y = (a.gh + D3_BS - 1) / D3_BS; a.tiles_x = (a.gw + D3_BS - 1) / D3_BS;
   a.partials_per_image = ((a.gh + 7) / 8) * ((a.gw + 7) / 8);
+  if (fold != nullptr) {
+    ICLR17_REQUIRE(fold->partial && fold->T > 0 && fold->total, ICLR17_EINVAL,
+                   "%s: bits fold needs the partials, their count and a total", what);
+    a.fold_partial = fold->partial; a.fold_T = fold->T; a.fold_per_image = fold->per_image;
+    a.fold_total = fold->total; a.fold_scale = fold->scale;
+  }
   dim3 grid(a.tiles_x * a.tiles_y * B);
   if (bf) {
     if (N == 192)
@@ -2574,6 +2638,28 @@ int iclr17_synthesis_deconv3_x6_cm(const uint16_t* in_split_cm, int B, int H, in
                                    int sse_unclipped, void* stream) {
   return launch_deconv3_halo(in_split_cm, B, H, W, N, w_split, bias, x, clipped, recon, sse_partial,
                              sse_unclipped, stream, false, 1);
+}
+
+int iclr17_synthesis_deconv3_x6_cm_bits(const uint16_t* in_split_cm, int B, int H, int W, int N,
+                                        const uint16_t* w_split, const float* bias, const float* x,
+                                        float* clipped, float* recon, double* sse_partial,
+                                        int sse_unclipped, const double* bits_partial, int bits_T,
+                                        double* bits_per_image, float* bpp_total, double bits_scale,
+                                        void* stream) {
+  const FoldBits f = {bits_partial, bits_T, bits_per_image, bpp_total, bits_scale};
+  return launch_deconv3_halo(in_split_cm, B, H, W, N, w_split, bias, x, clipped, recon, sse_partial,
+                             sse_unclipped, stream, false, 1, &f);
+}
+
+int iclr17_synthesis_deconv3_bf16_bits(const uint16_t* in, int B, int H, int W, int N,
+                                       const uint16_t* w_bf16, const float* bias, const float* x_ref,
+                                       float* clipped, float* recon, double* sse_partial,
+                                       int sse_unclipped, const double* bits_partial, int bits_T,
+                                       double* bits_per_image, float* bpp_total, double bits_scale,
+                                       void* stream) {
+  const FoldBits f = {bits_partial, bits_T, bits_per_image, bpp_total, bits_scale};
+  return launch_deconv3_halo(in, B, H, W, N, w_bf16, bias, x_ref, clipped, recon, sse_partial,
+                             sse_unclipped, stream, true, 0, &f);
 }
 
 int iclr17_synthesis_deconv3_bf16(const uint16_t* in, int B, int H, int W, int N,

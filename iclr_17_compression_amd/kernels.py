@@ -537,11 +537,14 @@ def split_deconv3(wp: Tensor, N: int) -> Tensor:
 
 
 def deconv3_x6(hs: Tensor, w_split: Tensor, bias: Tensor, x_ref: Optional[Tensor] = None,
-               want_recon: bool = False, sse_unclipped: bool = False):
+               want_recon: bool = False, sse_unclipped: bool = False,
+               bits: Optional[Tuple[Tensor, float]] = None):
     """deconv3 on a split-form input — [3,B,H/4,W/4,N], or the chunk-major [3,B,N/32,H/4,W/4,32]
     of ``deconv_igdn_x6(chunk_major=True)`` — (the halo-tiled x6 kernel); w_split:
     ``split_deconv3`` of the packed weights (Synthesis_net_17.packed_x6). The same returns as
-    ``deconv3`` (bit-identical in either input form)."""
+    ``deconv3`` (bit-identical in either input form). ``bits`` = (conv3's bit partials [B, T],
+    scale), chunk-major input only: the kernel also performs ``reduce_partials(partial, scale,
+    per_image=False)`` (bit-identical) and a fourth value, the 0-dim total, is returned."""
     cm = isinstance(hs, Tensor) and hs.dim() == 6
     if cm:
         if hs.dtype != torch.int16 or hs.shape[0] != 3 or hs.shape[5] != 32 or not hs.is_cuda \
@@ -556,11 +559,13 @@ def deconv3_x6(hs: Tensor, w_split: Tensor, bias: Tensor, x_ref: Optional[Tensor
     if (not isinstance(w_split, Tensor) or w_split.dtype != torch.int16
             or w_split.numel() != 3 * 9 * N * 48):
         raise Iclr17Error("iclr17: deconv3_x6 takes the split weight planes (split_deconv3)")
+    if bits is not None and not cm:
+        raise Iclr17Error("iclr17: deconv3_x6 folds the bit reduction only on the chunk-major input")
     return _deconv3_halo("iclr17_synthesis_deconv3_x6_cm" if cm else "iclr17_synthesis_deconv3_x6",
-                         hs, B, h4, w4, N, w_split, bias, x_ref, want_recon, sse_unclipped)
+                         hs, B, h4, w4, N, w_split, bias, x_ref, want_recon, sse_unclipped, bits)
 
 
-def _deconv3_halo(fn, hs, B, h4, w4, N, wp, bias, x_ref, want_recon, sse_unclipped):
+def _deconv3_halo(fn, hs, B, h4, w4, N, wp, bias, x_ref, want_recon, sse_unclipped, bits=None):
     _check_channels(N)
     H, W = 4 * h4, 4 * w4
     _check_image_dims(H, W)
@@ -573,9 +578,19 @@ def _deconv3_halo(fn, hs, B, h4, w4, N, wp, bias, x_ref, want_recon, sse_unclipp
             raise Iclr17Error("iclr17: reference image shape mismatch")
         x_ref = x_ref.contiguous()
         partial = torch.empty(B, output_partials_per_image(H, W), device=hs.device, dtype=torch.float64)
-    call(fn, _p(hs), B, H, W, N, _p(wp), _p(bias), _p(x_ref), _p(clipped), _p(recon),
-         _p(partial), int(sse_unclipped), _stream(hs))
-    return clipped, recon, partial
+    if bits is None:
+        call(fn, _p(hs), B, H, W, N, _p(wp), _p(bias), _p(x_ref), _p(clipped), _p(recon),
+             _p(partial), int(sse_unclipped), _stream(hs))
+        return clipped, recon, partial
+    bp, scale = bits
+    _check_f64(bp)
+    if bp.shape[0] != B:
+        raise Iclr17Error("iclr17: bit partials are not [B, T]")
+    total = torch.empty((), device=hs.device, dtype=torch.float32)
+    call(fn + "_bits", _p(hs), B, H, W, N, _p(wp), _p(bias), _p(x_ref), _p(clipped), _p(recon),
+         _p(partial), int(sse_unclipped), _p(bp.contiguous()), bp.shape[1], None, _p(total),
+         ctypes.c_double(scale), _stream(hs))
+    return clipped, recon, partial, total
 
 
 # ------------------------------------------------------------ bf16 throughput precision mode
@@ -700,7 +715,8 @@ def deconv_igdn_bf16(h: Tensor, w_bf: Tensor, bias: Tensor, beta_eff: Tensor, g_
 
 
 def deconv3_bf16(h: Tensor, wb: Tensor, bias: Tensor, x_ref: Optional[Tensor] = None,
-                 want_recon: bool = False, sse_unclipped: bool = False):
+                 want_recon: bool = False, sse_unclipped: bool = False,
+                 bits: Optional[Tuple[Tensor, float]] = None):
     """synthesis_17.py:23-25 + model.py:59 in bf16: bf16 NHWC [B,H/4,W/4,N] → the ``deconv3``
     returns (wb: ``round_packed(d3, 9, N, 48)`` of the ICLR17_W_DECONV9 packing d3)."""
     _check_bf16(h, "activation")
@@ -708,7 +724,7 @@ def deconv3_bf16(h: Tensor, wb: Tensor, bias: Tensor, x_ref: Optional[Tensor] = 
     if wb.dtype != torch.int16 or wb.numel() != 9 * N * 48:
         raise Iclr17Error("iclr17: deconv3_bf16: weights are not round_packed(d3, 9, N, 48)")
     return _deconv3_halo("iclr17_synthesis_deconv3_bf16", h, B, h4, w4, N, wb, bias, x_ref,
-                         want_recon, sse_unclipped)
+                         want_recon, sse_unclipped, bits)
 
 
 # ---------------------------------------------------------------- entropy coding (§8 f4)

@@ -128,8 +128,12 @@ class ImageCompressor(nn.Module):
         B, _, H, W = input_image.shape
         if not self.training and needs_grad(input_image, params):
             return self._eval_autograd(input_image)
-        out = self.run(input_image, noise=noise)
-        _, bpp = kernels.reduce_partials(out["bits_partial"], scale=1.0 / (B * H * W), per_image=False)
+        # run() with bpp's reduction (model.py:71-78) folded into deconv3's kernel
+        q = self.encode_latents(input_image.contiguous(), noise, self.training)
+        clipped, _, _, bpp = self.Decoder.decode(q["y_hat"], want_recon=False, y_split=q["y_split"],
+                                                 y_bf16=q.get("y_bf16"), y_integral=not self.training,
+                                                 bits=(q["bits_partial"], 1.0 / (B * H * W)))
+        out = {"clipped": clipped, "y_hat": q["y_hat"]}
         y_hat = out["y_hat"].permute(0, 3, 1, 2).contiguous()   # NCHW like model.py:56
         clipped = no_backward(out["clipped"], "ImageCompressor (training mode, no grad)", params,
                               input_image)

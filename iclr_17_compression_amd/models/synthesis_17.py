@@ -100,18 +100,21 @@ class Synthesis_net_17(nn.Module):
         return y.permute(0, 2, 3, 1).contiguous()
 
     def decode(self, y_nhwc, x_ref=None, want_recon=True, y_split=None, y_bf16=None,
-               y_integral=False):
+               y_integral=False, bits=None):
         """NHWC latent → (clipped NCHW, unclipped NCHW | None, SSE partials | None).
         With ``y_split`` (the latent in x6 split form) the three layers run in the x6 mode, with
         ``y_bf16`` (bf16 bit patterns) in the bf16 throughput mode. ``y_integral``: the latent
-        is ŷ = round(y) (model.py:56), so deconv1 runs the x6k engine's integer-input form."""
+        is ŷ = round(y) (model.py:56), so deconv1 runs the x6k engine's integer-input form.
+        ``bits`` = (conv3's bit partials, scale): a fourth output, ``reduce_partials``' 0-dim total,
+        computed inside deconv3's kernel in the x6 and bf16 modes (one launch fewer)."""
         d1, d2, d3, g1, g2 = self.packed()
         if y_bf16 is not None:
             b1, b2, b3 = self.packed_bf16()
             q1, q2 = self.igdn1.effective_params_bf16(), self.igdn2.effective_params_bf16()
             h = kernels.deconv_igdn_bf16(y_bf16, b1, self.deconv1.bias, *q1)
             h = kernels.deconv_igdn_bf16(h, b2, self.deconv2.bias, *q2)
-            return kernels.deconv3_bf16(h, b3, self.deconv3.bias, x_ref=x_ref, want_recon=want_recon)
+            return kernels.deconv3_bf16(h, b3, self.deconv3.bias, x_ref=x_ref, want_recon=want_recon,
+                                        bits=bits)
         if y_split is not None:
             q1, q2 = self.igdn1.effective_params_x6(), self.igdn2.effective_params_x6()
             if kernels.X6K:
@@ -130,11 +133,14 @@ class Synthesis_net_17(nn.Module):
             else:
                 hs, _, _ = kernels.deconv_igdn_x6(hs, d2, self.deconv2.bias, *q2, chunk_major=True)
             return kernels.deconv3_x6(hs, self.packed_x6(), self.deconv3.bias, x_ref=x_ref,
-                                      want_recon=want_recon)
+                                      want_recon=want_recon, bits=bits)
         else:
             h = kernels.deconv_igdn(y_nhwc, d1, self.deconv1.bias, g1[0], g1[1])
             h = kernels.deconv_igdn(h, d2, self.deconv2.bias, g2[0], g2[1])
-        return kernels.deconv3(h, d3, self.deconv3.bias, x_ref=x_ref, want_recon=want_recon)
+        out = kernels.deconv3(h, d3, self.deconv3.bias, x_ref=x_ref, want_recon=want_recon)
+        if bits is None:
+            return out
+        return (*out, kernels.reduce_partials(bits[0], bits[1], per_image=False)[1])
 
     def forward(self, x):
         from ..autograd import SynthesisFn, needs_grad

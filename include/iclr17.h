@@ -217,6 +217,17 @@ int iclr17_synthesis_deconv3_x6_cm(const uint16_t* in_split_cm, int B, int H, in
                                    const uint16_t* w_split, const float* bias, const float* x,
                                    float* clipped, float* recon, double* sse_partial,
                                    int sse_unclipped, void* stream);
+/* iclr17_synthesis_deconv3_x6_cm that also performs iclr17_reduce_partials(bits_partial, B,
+ * bits_T, bits_per_image, bpp_total, bits_scale) of conv3's bit partials (model.py:71-78: the
+ * per-image bits and bpp = scale·Σ), in its workgroup 0 with reduce_partials' arithmetic and order
+ * (bit-identical): the eval chain ends on deconv3 instead of one more launch. bits_per_image may
+ * be NULL. */
+int iclr17_synthesis_deconv3_x6_cm_bits(const uint16_t* in_split_cm, int B, int H, int W, int N,
+                                        const uint16_t* w_split, const float* bias, const float* x,
+                                        float* clipped, float* recon, double* sse_partial,
+                                        int sse_unclipped, const double* bits_partial, int bits_T,
+                                        double* bits_per_image, float* bpp_total, double bits_scale,
+                                        void* stream);
 
 /* ---------------------------------------------------------------- entropy coding (§8 f4)
  * A real bitstream for ŷ with the factorised model the reference only uses to ESTIMATE the rate
@@ -505,6 +516,14 @@ int iclr17_synthesis_deconv3_bf16(const uint16_t* in, int B, int H, int W, int N
                                   const uint16_t* w_bf16, const float* bias, const float* x_ref,
                                   float* clipped, float* recon, double* sse_partial,
                                   int sse_unclipped, void* stream);
+/* iclr17_synthesis_deconv3_bf16 with the bit reduction folded in, as
+ * iclr17_synthesis_deconv3_x6_cm_bits. */
+int iclr17_synthesis_deconv3_bf16_bits(const uint16_t* in, int B, int H, int W, int N,
+                                       const uint16_t* w_bf16, const float* bias, const float* x_ref,
+                                       float* clipped, float* recon, double* sse_partial,
+                                       int sse_unclipped, const double* bits_partial, int bits_T,
+                                       double* bits_per_image, float* bpp_total, double bits_scale,
+                                       void* stream);
 
 #ifdef __cplusplus
 }

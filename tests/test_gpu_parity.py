@@ -599,3 +599,27 @@ def test_x6k_deconv_igdn(device, N, hw):
                 _, fbi = kernels.deconv_igdn_x6k(bs, wx, dec.deconv1.bias, q[0], q[2], want_f32=True,
                                                  int_in=True)
                 assert torch.equal(fbi, fb) and not torch.equal(fb, f)
+
+
+@pytest.mark.parametrize("T", [4, 8, 100])
+def test_deconv3_bits_fold(device, T):
+    """bpp's reduction folded into deconv3 (x6 chunk-major and bf16 kernels, workgroup 0) equals
+    the separate reduce_partials kernel bit for bit, for batches of more than 64 images and for
+    more than 64 partials per image; the images are the kernels' own outputs, unchanged."""
+    N, B = 128, 70
+    net = net_for(N, 2, device)
+    dec = net.Decoder
+    torch.manual_seed(1)
+    part = (torch.rand(B, T, dtype=torch.float64) * 50.0).to(device)
+    _, ref = kernels.reduce_partials(part, 1.0 / 12345.0, per_image=False)
+    h = (torch.randn(B, 4, 4, N) * 0.5).to(device)
+    hs = kernels.split_planes(h).reshape(3, B, 4, 4, N // 32, 32).permute(0, 1, 4, 2, 3, 5).contiguous()
+    with torch.no_grad():
+        c0, _, _ = kernels.deconv3_x6(hs, dec.packed_x6(), dec.deconv3.bias)
+        c1, _, _, tot = kernels.deconv3_x6(hs, dec.packed_x6(), dec.deconv3.bias, bits=(part, 1.0 / 12345.0))
+        assert torch.equal(c0, c1) and torch.equal(tot, ref)
+        hb = kernels.to_bf16(h)
+        b3 = dec.packed_bf16()[2]
+        c2, _, _ = kernels.deconv3_bf16(hb, b3, dec.deconv3.bias)
+        c3, _, _, tot2 = kernels.deconv3_bf16(hb, b3, dec.deconv3.bias, bits=(part, 1.0 / 12345.0))
+        assert torch.equal(c2, c3) and torch.equal(tot2, ref)

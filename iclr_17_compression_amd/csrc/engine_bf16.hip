@@ -26,6 +26,7 @@
 //   * Epilogues: GDN / IGDN (x² → bf16 tile in LDS, the channel contraction n = γ·x² on the same
 //     MFMA with γ bf16 from L2, then x/√(β+n) or x·√(β+n) in fp32), and the quantiser + rate of
 //     conv3 (round half-to-even, the factorised CDF twice, −log₂, per-workgroup bit sums).
+#include <stdlib.h>
 #include <string.h>
 
 #include "common.h"
@@ -54,6 +55,9 @@ namespace bfm {
 #endif
 #ifndef ICLR17_C1P_STAMPS
 #define ICLR17_C1P_STAMPS 0   // diagnostic build: per-phase s_memtime stamps of conv1p
+#endif
+#ifndef ICLR17_BF_PERSIST
+#define ICLR17_BF_PERSIST 0   // deconv (16-row tiles): persistent workgroups (k5p_bf16_kernel; A/B: no gain)
 #endif
 #ifndef ICLR17_BF_RTAB_LDS
 #define ICLR17_BF_RTAB_LDS 1   // conv3: the rate table rows of the tile in LDS (not L2 gathers)
@@ -141,7 +145,7 @@ constexpr int epi_tile_bytes(int R) { return R * (CO * 2 + 32); }
 // otherwise hold one wave per SIMD.
 constexpr int k5_threads(int TH, int EPI) { return TH / 2 * 64 * (EPI == BE_QUANT ? ICLR17_BF_C3KS : 1); }
 
-template <int MODE, int TH, int NB, int CO, int CI, int EPI>
+template <int MODE, int TH, int NB, int CO, int CI, int EPI, bool PERSIST = false>
 struct K5 {
   static constexpr int KS = EPI == BE_QUANT ? ICLR17_BF_C3KS : 1;   // K-split groups
   static_assert(k5_threads(TH, EPI) == KS * (TH / 2) * 64, "threads");
@@ -153,34 +157,47 @@ struct K5 {
   static constexpr int NBI = SB / 1024;         // weight DMA wave-instructions per step
   using P = Patch<MODE, TH>;
   static constexpr int NST = ICLR17_BF_NST;     // weight stages (ring)
-  static constexpr int MAIN_LDS = 2 * P::BUF + NST * SB + 1024;
+  // persistent (k5p_bf16_kernel): no sink in the main-loop area (it lives in the y-image area)
+  static constexpr int MAIN_LDS = 2 * P::BUF + NST * SB + (PERSIST ? 0 : 1024);
   static constexpr int GBLK = (CO / 32) * (CO / 16);   // GDN: γ fragment blocks, 1 KB each
   static constexpr int OS = CO * 2 + 16;               // GDN: output tile row stride (bytes)
   // γ staged beside the main-loop buffers, by DMAs issued in the prologue, where that still
   // fits one workgroup per CU (the 8-wave tiles run one per CU anyway); else after the loop
-  static constexpr bool EARLY_G = EPI != BE_QUANT && NW == 8 && MAIN_LDS + GBLK * 1024 <= 160 * 1024;
+  static constexpr bool EARLY_G = PERSIST ||
+                                  (EPI != BE_QUANT && NW == 8 && MAIN_LDS + GBLK * 1024 <= 160 * 1024);
   static constexpr int GOFF = EARLY_G ? MAIN_LDS : 0;
   static constexpr int EPI_LDS = EPI == BE_QUANT ? 64
                                  : (GOFF + GBLK * 1024 > R * OS ? GOFF + GBLK * 1024 : R * OS);
   static constexpr int LDS0 = KS * MAIN_LDS > EPI_LDS ? KS * MAIN_LDS : EPI_LDS;
   // GDN: each wave stores its own y rows, a channel pair of tiles at a time, through a private
   // 4 KB [32 px][64 ch] image (no workgroup barrier: the stores overlap other waves' contraction)
-  static constexpr int YOFF = EARLY_G ? 0 : GBLK * 1024;
-  static constexpr bool DIRECT_Y = ICLR17_BF_DIRECT_Y && EPI != BE_QUANT && NT % 2 == 0 &&
-                                   YOFF + NW * 4096 <= LDS0 && (EARLY_G ? NW * 4096 <= MAIN_LDS : true);
+  // persistent: the main-loop buffers, γ, the per-wave 2 KB [32 px][32 ch] y images (the padding
+  // sink in their first 1 KB) and bias / β_eff, side by side: the next tile's patch and first
+  // weight stages stream in while this tile's epilogue runs
+  static constexpr int YOFF = PERSIST ? GOFF + GBLK * 1024 : (EARLY_G ? 0 : GBLK * 1024);
+  static constexpr bool DIRECT_Y = PERSIST || (ICLR17_BF_DIRECT_Y && EPI != BE_QUANT && NT % 2 == 0 &&
+                                   YOFF + NW * 4096 <= LDS0 && (EARLY_G ? NW * 4096 <= MAIN_LDS : true));
   // GDN: bias and β_eff staged by two prologue DMAs into their own 2 KB (an epilogue global load
   // of them waited out a full L2 round trip after the main loop)
-  static constexpr int BBOFF = (LDS0 + 1023) / 1024 * 1024;
+  static constexpr int BBOFF = PERSIST ? YOFF + NW * 2048 : (LDS0 + 1023) / 1024 * 1024;
   static constexpr int LDS = EPI == BE_QUANT ? LDS0 : BBOFF + 2048;
+  static_assert(!PERSIST || (EPI != BE_QUANT && KS == 1 && NW * 2048 >= 1024 && LDS <= 160 * 1024),
+                "persistent layout");
   static_assert(KS == 1 || (KS - 1) * NW * NT * 16 * 64 * 4 <= KS * MAIN_LDS, "K-split exchange");
   static_assert(TH % 2 == 0 && NB % 32 == 0 && SB % 1024 == 0 && CI % (16 * KS) == 0, "tile shape");
   static_assert(EPI == BE_QUANT || NB == CO, "GDN needs every channel of a pixel in the tile");
 };
 
-template <int MODE, int TH, int NB, int CO, int CI, int EPI, int PH>
+template <int MODE, int TH, int NB, int CO, int CI, int EPI, bool PERSIST>
+__device__ void k5_prefetch_tile(const K5Args& a, unsigned char* smem, int t);
+
+// PERSIST (k5p_bf16_kernel): the kernel has staged bias / β_eff and γ once and this tile's
+// patch and first weight stages (k5_prefetch_tile); after the main loop the next tile's
+// (next_t ≥ 0) are prefetched, then the epilogue runs
+template <int MODE, int TH, int NB, int CO, int CI, int EPI, int PH, bool PERSIST = false>
 __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, int b, int ty, int tx,
-                                        int nb) {
-  using KK = K5<MODE, TH, NB, CO, CI, EPI>;
+                                        int nb, int next_t = -1) {
+  using KK = K5<MODE, TH, NB, CO, CI, EPI, PERSIST>;
   using P = typename KK::P;
   using TP = Taps<MODE, PH>;
   constexpr int NT = KK::NT, NW = KK::NW, S = TP::S, NCH = KK::NCH;
@@ -205,7 +222,7 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
   constexpr int GS = NCH * S;                         // steps
   unsigned char* const sP = gsmem;                    // two patch buffers
   unsigned char* const sB = gsmem + 2 * P::BUF;       // NST weight stages
-  unsigned char* const sD = sB + NST * SB;            // 1 KB sink of the padding loads
+  unsigned char* const sD = PERSIST ? smem + KK::YOFF : sB + NST * SB;   // sink of the padding loads
   const long img = (long)b * a.Hin * a.Win;
   const int iy0 = MODE == BM_CONV ? 2 * ty * TH - 2 : ty * TH - 1;
   const int ix0 = MODE == BM_CONV ? 2 * tx * 16 - 2 : tx * 16 - 1;
@@ -297,7 +314,7 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
   const unsigned long long st0 = __builtin_amdgcn_s_memtime();
 #endif
   float* const sbb = (float*)(smem + KK::BBOFF);   // GDN: [bias CO | pad][β_eff CO | pad]
-  if constexpr (EPI != BE_QUANT) {
+  if constexpr (EPI != BE_QUANT && !PERSIST) {
     // waves 0 / 1: one 16-byte piece per lane (CO ≤ 256 floats); retired by the first counted wait
     static_assert(CO <= 256, "bias / β stage");
     if (wave < 2) {
@@ -305,9 +322,11 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
       glds16(lane * 4 < CO ? (const void*)(src + lane * 4) : (const void*)g_zero16, sbb + wave * 256);
     }
   }
-  if constexpr (KK::EARLY_G) stage_gamma();   // retired by the loop's first counted wait
+  if constexpr (KK::EARLY_G && !PERSIST) stage_gamma();   // retired by the loop's first counted wait
   // prologue: chunk 0's patch and the weights of steps 0 .. F-1 (any count per wave), then
   // step F's weights as a full K-group, so the loop's first wait leaves exactly F groups
+  // (persistent: issued before, by k5_prefetch_tile, and landed: the kernel's vm_barrier)
+  if constexpr (!PERSIST) {
   for (int piece = wave; piece < P::NQI; piece += NW) issue_piece(0, piece, true);
 #pragma unroll
   for (int f = 0; f < F; ++f)
@@ -323,6 +342,7 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
   for (int f = 1; f < F; ++f)   // F−1 more full groups: the first wait keeps F in flight
 #pragma unroll
     for (int k = 0; k < K; ++k) sink_load(sD);
+  }
 
   typedef const __attribute__((address_space(3))) u4* lu4p;
 #if ICLR17_K5_STAMPS
@@ -371,6 +391,9 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
     }
   }
   vm_barrier();   // the trailing sink loads landed and every wave is done with the stages
+  if constexpr (PERSIST) {
+    if (next_t >= 0) k5_prefetch_tile<MODE, TH, NB, CO, CI, EPI, PERSIST>(a, smem, next_t);
+  }
 #if ICLR17_K5_STAMPS
   const unsigned long long st2 = __builtin_amdgcn_s_memtime();
   unsigned long long st4 = st2, st5 = st2, stg = st2;
@@ -449,7 +472,29 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][4 * m + j] = y[j];
       }
-      if constexpr (KK::DIRECT_Y) {
+      if constexpr (PERSIST) {
+        // tile i through this wave's 2 KB [32 px][32 ch] image (16-byte piece pc of pixel p at
+        // slot pc ^ (p & 3)): pixel px = (lane >> 2) + 16j is tile row 2·wave + j, column lane >> 2
+        unsigned char* const y1 = smem + KK::YOFF + wave * 2048;
+        auto ysw1 = [](int p, int pc) { return p * 64 + ((pc ^ (p & 3)) << 4); };
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+          *(uint2*)(y1 + ysw1(r32, m) + 8 * h) =
+              uint2{pack_bf2(acc[i][4 * m], acc[i][4 * m + 1]), pack_bf2(acc[i][4 * m + 2], acc[i][4 * m + 3])};
+        wave_lds_sync();   // the image's writes before any lane's reads (cross-lane exchange)
+        const int fl = fresh_tid() & 63;
+        u16* const ob = a.out + (long)b * a.Hout * a.Wout * CO;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int px = (fl >> 2) + 16 * j, pc = fl & 3;
+          const u4 v = *(lu4p)(y1 + ysw1(px, pc));
+          const int gy = ty * TH + 2 * wave + j, gx = tx * 16 + (fl >> 2);
+          const int oy = MODE == BM_CONV ? gy : 2 * gy + (PH >> 1);
+          const int ox = MODE == BM_CONV ? gx : 2 * gx + (PH & 1);
+          if (gy < a.gh && gx < a.gw) *(u4*)(ob + (oy * a.Wout + ox) * CO + 32 * i + 8 * pc) = v;
+        }
+        wave_lds_sync();   // every lane's reads before the next tile's writes (WAR)
+      } else if constexpr (KK::DIRECT_Y) {
         if (i & 1) {   // tiles i − 1, i: channels 32(i − 1) .. 32i + 31, 8 pieces of 16 bytes
 #pragma unroll
           for (int tt = 0; tt < 2; ++tt)
@@ -640,6 +685,128 @@ k5_bf16_kernel(const K5Args a) {
       case 2: k5_body<MODE, TH, NB, CO, CI, EPI, 2>(a, smem, b, ty, tx, nb); break;
       default: k5_body<MODE, TH, NB, CO, CI, EPI, 3>(a, smem, b, ty, tx, nb); break;
     }
+  }
+}
+
+// ------------------------------------------------------------------ persistent k5 (deconv2)
+// Tile t → (stride phase, image, tile row, tile column), phase-major as k5_bf16_kernel.
+__device__ __forceinline__ void k5_tile(const K5Args& a, int t, int& ph, int& b, int& ty, int& tx) {
+  const int per_ph = a.tiles_x * a.tiles_y * a.B;
+  ph = t / per_ph;
+  t -= ph * per_ph;
+  tx = t % a.tiles_x;
+  t /= a.tiles_x;
+  ty = t % a.tiles_y;
+  b = t / a.tiles_y;
+}
+
+// Tile t's chunk-0 patch and the weights of steps 0 .. F (its phase's F), any count per wave:
+// the kernel's vm_barrier before the tile retires them (no counted group structure needed)
+template <int MODE, int TH, int NB, int CO, int CI, int EPI, int PH>
+__device__ __forceinline__ void k5_prefetch(const K5Args& a, unsigned char* smem, int b, int ty, int tx) {
+  using KK = K5<MODE, TH, NB, CO, CI, EPI, true>;
+  using P = typename KK::P;
+  using TP = Taps<MODE, PH>;
+  constexpr int NW = KK::NW, S = TP::S, NCH = KK::NCH, NST = KK::NST;
+  constexpr int F = (S >= 6 && NST >= 5) ? 3 : (S >= 3 ? 2 : 1);
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int iy0 = MODE == BM_CONV ? 2 * ty * TH - 2 : ty * TH - 1;
+  const int ix0 = MODE == BM_CONV ? 2 * tx * 16 - 2 : tx * 16 - 1;
+  const u16* __restrict__ inb = a.in + (long)b * a.Hin * a.Win * CI;
+  for (int piece = wave; piece < P::NQI; piece += NW) {
+    const int byte = (piece * 64 + lane) * 16;
+    const int pr = byte / P::ROWB, rem = byte - pr * P::ROWB;
+    int pc, hh;
+    bool ok;
+    if (MODE == BM_CONV) {
+      const int par = rem / (2 * P::HALF), r2 = rem - par * 2 * P::HALF;
+      hh = r2 / P::HALF;
+      pc = 2 * ((r2 - hh * P::HALF) / 16) + par;
+      ok = pc < 35;
+    } else {
+      hh = rem / P::HALF;
+      pc = (rem - hh * P::HALF) / 16;
+      ok = true;
+    }
+    const int iy = iy0 + pr, ix = ix0 + pc;
+    ok = ok && pr < P::ROWS && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
+    glds16(ok ? (const void*)(inb + (iy * a.Win + ix) * CI + 8 * hh) : (const void*)g_zero16,
+           smem + piece * 1024);   // patch buffer 0 (chunk 0)
+  }
+  const long wstep = 4L * CO * 8;
+  const u16* __restrict__ wph = a.w;
+  if (MODE == BM_DECONV) {
+    long off = 0;
+#pragma unroll
+    for (int p = 0; p < PH; ++p) {
+      const int ny = (p >> 1) == 0 ? 3 : 2, nx = (p & 1) == 0 ? 3 : 2;
+      off += (long)NCH * ((ny * nx + 1) / 2) * wstep;
+    }
+    wph += off;
+  }
+  unsigned char* const sB = smem + 2 * P::BUF;
+#pragma unroll
+  for (int f = 0; f <= F; ++f)
+    for (int slot = wave; slot < KK::NBI; slot += NW) {
+      const int q = slot * 64 + lane;
+      const int g = q / NB, col = q - g * NB;
+      glds16(wph + (long)f * wstep + (g * CO + col) * 8, sB + f * KK::SB + slot * 1024);
+    }
+}
+
+template <int MODE, int TH, int NB, int CO, int CI, int EPI, bool PERSIST>
+__device__ void k5_prefetch_tile(const K5Args& a, unsigned char* smem, int t) {
+  int ph, b, ty, tx;
+  k5_tile(a, t, ph, b, ty, tx);
+  switch (ph) {
+    case 0: k5_prefetch<MODE, TH, NB, CO, CI, EPI, 0>(a, smem, b, ty, tx); break;
+    case 1: k5_prefetch<MODE, TH, NB, CO, CI, EPI, 1>(a, smem, b, ty, tx); break;
+    case 2: k5_prefetch<MODE, TH, NB, CO, CI, EPI, 2>(a, smem, b, ty, tx); break;
+    default: k5_prefetch<MODE, TH, NB, CO, CI, EPI, 3>(a, smem, b, ty, tx); break;
+  }
+}
+
+// deconv (all four stride phases) as one persistent 8-wave workgroup per CU walking the tiles
+// t = blockIdx.x, + gridDim.x, …: bias / β_eff and γ are staged once per workgroup, and each
+// tile's patch and first weight stages stream in during the previous tile's epilogue (LDS:
+// K5<…, PERSIST>); the tile body is k5_bf16_kernel's, so the outputs are bit-identical to it.
+// At B = 64 (deconv2: 4 phases × 256 tiles) each workgroup takes one tile of every phase.
+template <int MODE, int TH, int NB, int CO, int CI, int EPI>
+__global__ void __launch_bounds__(TH / 2 * 64, 1) k5p_bf16_kernel(const K5Args a) {
+  static_assert(MODE == BM_DECONV, "persistent k5: the deconvolutions");
+  using KK = K5<MODE, TH, NB, CO, CI, EPI, true>;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[KK::LDS];
+  constexpr int NW = KK::NW, KB16 = CO / 16;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r32 = lane & 31, h = lane >> 5;
+  const int total = 4 * a.tiles_x * a.tiles_y * a.B;
+  int t = blockIdx.x;
+  if (t >= total) return;
+  // once per workgroup: bias and β_eff (waves 0 / 1), γ fragments (k5_body's stage_gamma layout)
+  static_assert(CO <= 256, "bias / β stage");
+  if (wave < 2) {
+    const float* src = wave == 0 ? a.bias : a.beta;
+    glds16(lane * 4 < CO ? (const void*)(src + lane * 4) : (const void*)g_zero16,
+           smem + KK::BBOFF + wave * 1024);
+  }
+  for (int blk = wave; blk < KK::GBLK; blk += NW) {
+    const int i = blk / KB16, kb = blk - i * KB16;
+    glds16(a.gamma + ((long)(2 * kb + h) * CO + 32 * i + r32) * 8, smem + KK::GOFF + blk * 1024);
+  }
+  k5_prefetch_tile<MODE, TH, NB, CO, CI, EPI, true>(a, smem, t);
+  while (t < total) {
+    vm_barrier();   // this tile's patch and first weights (and the previous tile's stores) landed
+    const int tn = t + gridDim.x;
+    int ph, b, ty, tx;
+    k5_tile(a, t, ph, b, ty, tx);
+    const int nx = tn < total ? tn : -1;
+    switch (ph) {   // wave-uniform
+      case 0: k5_body<MODE, TH, NB, CO, CI, EPI, 0, true>(a, smem, b, ty, tx, 0, nx); break;
+      case 1: k5_body<MODE, TH, NB, CO, CI, EPI, 1, true>(a, smem, b, ty, tx, 0, nx); break;
+      case 2: k5_body<MODE, TH, NB, CO, CI, EPI, 2, true>(a, smem, b, ty, tx, 0, nx); break;
+      default: k5_body<MODE, TH, NB, CO, CI, EPI, 3, true>(a, smem, b, ty, tx, 0, nx); break;
+    }
+    t = tn;
   }
 }
 
@@ -1080,8 +1247,19 @@ int launch_deconv(const K5Args& a0, hipStream_t st) {
   K5Args a = a0;
   a.tiles_y = (a.gh + TH - 1) / TH;
   a.tiles_x = (a.gw + 15) / 16;
+  const int tiles = a.tiles_x * a.tiles_y * a.B * 4;
+  if constexpr (TH == 16) {   // one workgroup per CU walking the tiles (ICLR17_BF_PERSIST=0: off)
+    static const bool persist = getenv("ICLR17_BF_PERSIST") ? atoi(getenv("ICLR17_BF_PERSIST")) != 0
+                                                             : ICLR17_BF_PERSIST != 0;
+    if (persist) {
+      const int ncu = cu_count();
+      hipLaunchKernelGGL((k5p_bf16_kernel<BM_DECONV, TH, N, N, N, BE_IGDN>),
+                         dim3(tiles < ncu ? tiles : ncu, 1), dim3(TH / 2 * 64), 0, st, a);
+      return check_launch("deconv_igdn_bf16 (persistent)");
+    }
+  }
   hipLaunchKernelGGL((k5_bf16_kernel<BM_DECONV, TH, N, N, N, BE_IGDN>),
-                     dim3(a.tiles_x * a.tiles_y * a.B * 4, 1), dim3(TH / 2 * 64), 0, st, a);
+                     dim3(tiles, 1), dim3(TH / 2 * 64), 0, st, a);
   return check_launch("deconv_igdn_bf16");
 }
 

@@ -222,18 +222,6 @@ __device__ __forceinline__ void x6k_body(const XArgs& a, unsigned char* smem, in
       const int g = c * S + s;
       wait_vm_barrier<F * K>();   // weights of step g and, at s = 0, chunk c's patch landed;
                                   // stage (g+F+1) % NST is free
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const int slot = k * NW + wave;
-        if ((k + 1) * NW <= NBI || slot < NBI) {
-          issue_w(k, g + F + 1);
-        } else if (s < SI) {
-          const int piece = s * PS + slot - NBI;
-          issue_piece(c + 1, piece, c + 1 < NCH && piece < KK::NQI);
-        } else {
-          sink4(sD);
-        }
-      }
       const unsigned char* wb = sB + stage * SB + abase;
       stage = stage + 1 == NST ? 0 : stage + 1;
       const int to = P::template tap_off<PH>(s);
@@ -256,6 +244,20 @@ __device__ __forceinline__ void x6k_body(const XArgs& a, unsigned char* smem, in
         t = mfma32(am, bh, t);
         if constexpr (!INT_IN) t = mfma32(ah, bm, t);
         acc[i] = mfma32(ah, bh, t);
+      }
+      // the step's DMA group after its fragment reads: an LDS read after an LDS-DMA of unknown
+      // destination makes the compiler wait for that DMA (s_waitcnt vmcnt(0)) first
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int slot = k * NW + wave;
+        if ((k + 1) * NW <= NBI || slot < NBI) {
+          issue_w(k, g + F + 1);
+        } else if (s < SI) {
+          const int piece = s * PS + slot - NBI;
+          issue_piece(c + 1, piece, c + 1 < NCH && piece < KK::NQI);
+        } else {
+          sink4(sD);
+        }
       }
     }
   }

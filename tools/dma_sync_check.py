@@ -272,7 +272,9 @@ def counted_barriers(body):
                 p = min(p, int(m.group(1)))
         elif op == "s_barrier":
             at_barrier.setdefault(off, set()).add((hist, p, since))
-            hist = (0,) + hist[:-1]
+            # nothing of this wave outstanding (p = 0, e.g. after vm_barrier's vmcnt(0)): the
+            # intervals before are settled, and the next one starts like the kernel's first
+            hist = (0,) * HIST if p == 0 else (0,) + hist[:-1]
         consts = _consts_after(consts, op, ln)
         if op in ("s_cbranch_vccnz", "s_cbranch_vccz"):
             edges = _branch_edges(consts, op, succ[i])

@@ -32,7 +32,7 @@ SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ
 SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_LDS}
 SETS
 cd "$R"
-python tools/pmc_summary.py "$OUT" "$TAG" "$PREC" || exit 1
+python tools/pmc_summary.py "$OUT" "$TAG" "$PREC" ${PMC_NSB:-} || exit 1
 cp "$(find "$OUT/trace" -name '*kernel_stats.csv' | head -1)" "$OUT/${TAG}_kernel_stats.csv"
 grep '^{' "$OUT/trace.log" | tail -n 1 > "$OUT/${TAG}_bench_under_trace.json" || echo "no bench JSON line in trace.log" >&2
 exit 0

@@ -173,6 +173,31 @@ class Step:
         return clipped, y_hat, bpp
 
 
+class SplitStep:
+    """The eval step with the batch split into n parts launched on n HIP streams: the images are
+    independent (no exchange), so one part's phase-locked prologue / epilogue bursts can overlap
+    another part's main loops. Same kernels, same per-image results as Step."""
+
+    def __init__(self, net: ImageCompressor, x: torch.Tensor, n: int):
+        B = x.shape[0]
+        if n < 2 or B % n:
+            raise SystemExit(f"--streams {n}: the batch ({B}) must split evenly into >= 2 parts")
+        self.parts = [Step(net, xs.contiguous()) for xs in x.chunk(n)]
+        self.side = [torch.cuda.Stream(device=x.device) for _ in range(n - 1)]
+
+    def __call__(self):
+        main = torch.cuda.current_stream()
+        for s in self.side:
+            s.wait_stream(main)
+        out = [self.parts[0]()]
+        for s, p in zip(self.side, self.parts[1:]):
+            with torch.cuda.stream(s):
+                out.append(p())
+        for s in self.side:
+            main.wait_stream(s)
+        return out
+
+
 def train_flops(N: int, H: int, W: int) -> float:
     """Algorithmic FLOPs of one training step per image: forward + input gradients (no conv1
     dgrad) + weight gradients + GDN backward (two channel contractions + the parameter GEMM)."""
@@ -743,11 +768,12 @@ def time_eval(net, x, args, world, dev) -> dict:
     pass of K steps with HIP-event brackets per layer on the launching stream (outside the
     wall-clock region, so the brackets cannot perturb it). Elapsed is the max over ranks."""
     step = Step(net, x)
+    streams = args.bf16_streams if kernels.precision() == "bf16" else args.streams
     with torch.no_grad():
+        run = SplitStep(net, x, streams) if streams > 1 else step
         for _ in range(args.warmup):
-            step()
+            run()
         torch.cuda.synchronize()
-        run = step
         if args.graph:
             # the step's launches captured once into a HIP graph (torch.cuda.CUDAGraph on ROCm):
             # each replay submits the whole chain at once (no per-kernel host launch, shorter
@@ -769,6 +795,9 @@ def time_eval(net, x, args, world, dev) -> dict:
             dist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
+        if run is not step and not args.graph:   # the one-stream step of the per-layer pass, warm
+            for _ in range(3):
+                step()
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(8)] for _ in range(args.steps)]
         for i in range(args.steps):
             clipped, y_hat, bpp = step(evs[i])
@@ -930,6 +959,11 @@ def main() -> None:
     ap.add_argument("--prefetch", type=int, default=4)
     ap.add_argument("--no-bf16-leg", action="store_true",
                     help="x6 eval: skip the bf16 throughput-mode leg reported as bf16_mode")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="eval: split the batch over this many HIP streams in the timed region "
+                         "(independent images; per-layer timings stay one stream)")
+    ap.add_argument("--bf16-streams", type=int, default=1,
+                    help="the same for the bf16 leg / --precision bf16")
     ap.add_argument("--graph", action="store_true",
                     help="eval: replay the timed steps from one HIP graph instead of launching them "
                          "kernel by kernel (x6: 4 % slower, bf16: 1.4 % faster; DESIGN §5)")
@@ -1074,7 +1108,9 @@ def main() -> None:
                                             "per MAC, fp32 accumulate and epilogues" if prec == "bf16"
                                             else "fp32 (exact-f32 MFMA products)"),
                    "parallelism": f"dp{world} (images sharded by rank, no data-path collective)",
-                   "launch": "hipGraph replay of the whole step" if args.graph else "eager (kernel by kernel)"},
+                   "launch": ("hipGraph replay of the whole step" if args.graph else
+                              "eager (kernel by kernel)" + (f", batch split over {args.streams} HIP streams"
+                                                            if args.streams > 1 else ""))},
         "roofline": {**roof, "algorithmic_bytes_per_launch": bytes_[dominant] * B,
                      "flop_per_launch": flops[dominant] * B,
                      "whole_step_tflops": round(total_flops / (ms_per_step * 1e-3) / 1e12, 2)},
@@ -1093,6 +1129,7 @@ def main() -> None:
             "value": round(pixels / rb["elapsed"] / 1e6, 2), "unit": "Mpix/s",
             "warmup": max(args.warmup, 100),
             "ms_per_step": round(rb["elapsed"] / args.steps * 1e3, 4), "dtype": "bf16",
+            "streams": args.bf16_streams,
             "roofline": {k: roof_b[k] for k in ("kernel", "achieved", "peak", "frac", "duration",
                                                   "profile_mean_ms", "frac_from_profile", "traffic",
                                                   "traffic_source", "traffic_null_reason",

@@ -62,6 +62,9 @@ namespace bfm {
 #ifndef ICLR17_BF_RTAB_LDS
 #define ICLR17_BF_RTAB_LDS 1   // conv3: the rate table rows of the tile in LDS (not L2 gathers)
 #endif
+#ifndef ICLR17_BF_C3ST
+#define ICLR17_BF_C3ST 1   // conv3: ŷ stored from an LDS tile as contiguous pixel rows (QST)
+#endif
 #ifndef ICLR17_BF_NST
 #define ICLR17_BF_NST 4   // weight ring stages (F + 2 for F DMA groups in flight)
 #endif
@@ -566,23 +569,70 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
       if constexpr (RT_LDS) return stab[cl * RT_W + v + RT_K];
       else return a.rtab[c * RT_W + v + RT_K];
     };
+    // ŷ through an LDS tile [R px][NB ch] (row stride NB + 4 floats: a 16-lane b128 write group
+    // covers 64 distinct banks), then stored by every wave as 16-byte chunks of contiguous
+    // pixel rows: the accumulator layout would store 32 pixels × 32 bytes per wave-instruction
+    constexpr bool QST = ICLR17_BF_C3ST && RT_LDS;
+    constexpr int QS = NB + 4, QOFF = XS_BYTES + RTP * 1024;
+    static_assert(!QST || QOFF + KK::R * QS * 4 <= KK::KS * KK::MAIN_LDS, "ŷ tile");
+    float* const sq = (float*)(smem + QOFF);
+    // Every element's table entry is read unconditionally (index clamped), and the elements
+    // outside the table (|ŷ| > RT_K, or NaN) are recomputed in ONE rarely-taken block after them:
+    // a per-element `lookup ? table : element_bits` put 2 KB of inlined element_bits between
+    // consecutive lookups, and every skip over it missed the instruction cache (≈ 10k cycles of
+    // the epilogue). The bits are then added in the same element order as before.
     auto quant_rows = [&](int m) {
       if (o < 0) return;
+      f4 qv[NT], bv[NT];
+      bool slow = false;
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        const int ch = nb * NB + 32 * i + 8 * m + 4 * h;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float q = rintf(acc[i][4 * m + j]);
+          qv[i][j] = q;
+          const float qc = fminf(fmaxf(q, -(float)RT_K), (float)RT_K);
+          bv[i][j] = rtab_at(ch - nb * NB + j, (int)qc, ch + j);
+          slow |= !(fabsf(q) <= (float)RT_K);
+        }
+      }
+      if (slow) {
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (!(fabsf(qv[i][j]) <= (float)RT_K))
+              bv[i][j] = element_bits(qv[i][j], a.rate, CO, nb * NB + 32 * i + 8 * m + 4 * h + j);
+      }
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
         const int ch = nb * NB + 32 * i + 8 * m + 4 * h;
         const f4 y = f4{acc[i][4 * m], acc[i][4 * m + 1], acc[i][4 * m + 2], acc[i][4 * m + 3]};
-        f4 q;
+        const f4 q = qv[i];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          q[j] = rintf(y[j]);
-          // integer latents: the per-channel table of the same element_bits (bit-identical)
-          bits += fabsf(q[j]) <= (float)RT_K ? rtab_at(ch - nb * NB + j, (int)q[j], ch + j)
-                                             : element_bits(q[j], a.rate, CO, ch + j);
-        }
+        for (int j = 0; j < 4; ++j) bits += bv[i][j];
         if (a.y_f32) *(f4*)(a.y_f32 + o * CO + ch) = y;
-        *(f4*)(a.out_f32 + o * CO + ch) = q;
-        *(uint2*)(a.out + o * CO + ch) = uint2{pack_bf2(q[0], q[1]), pack_bf2(q[2], q[3])};
+        if constexpr (QST) {
+          *(f4*)(sq + tpix * QS + (ch - nb * NB)) = q;
+        } else {
+          *(f4*)(a.out_f32 + o * CO + ch) = q;
+          *(uint2*)(a.out + o * CO + ch) = uint2{pack_bf2(q[0], q[1]), pack_bf2(q[2], q[3])};
+        }
+      }
+    };
+    auto store_tile = [&]() {   // QST: after the barrier that publishes sq
+      constexpr int NCK = NB / 4, TOT = KK::R * NCK, NTH = KK::KS * KK::NT_;
+      static_assert(TOT % NTH == 0, "ŷ store split");
+#pragma unroll
+      for (int it = 0; it < TOT / NTH; ++it) {
+        const int idx = it * NTH + tid, p = idx / NCK, k = idx - p * NCK;
+        const long op = out_pixel(p);
+        if (op < 0) continue;
+        const f4 q = *(const f4*)(sq + p * QS + 4 * k);
+        const long e = op * CO + nb * NB + 4 * k;
+        *(f4*)(a.out_f32 + e) = q;
+        *(uint2*)(a.out + e) = uint2{pack_bf2(q[0], q[1]), pack_bf2(q[2], q[3])};
       }
     };
     int nred = NW;   // bit partials to add, one per finishing wave
@@ -625,6 +675,10 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
       } else {
         quant_rows(2);
         quant_rows(3);
+      }
+      if constexpr (QST) {
+        __syncthreads();   // ŷ tile complete
+        store_tile();
       }
       nred = 2 * NW;
     } else {

@@ -779,7 +779,9 @@ __device__ __forceinline__ void rate_bwd_epilogue(f4 (&acc)[MT][NT], float* smem
         float v = pg[nt][k];
         v += __shfl_xor(v, 16, 64);
         v += __shfl_xor(v, 32, 64);
-        if (lane < 16) a.rpart[((long)blockIdx.x * 11 + k) * CO + ncol0 + nt * 16 + lane] = v;
+        // row = the tile's linear index
+        const long row = ((long)t.b * a.tiles_y + t.ty) * a.tiles_x + t.tx;
+        if (lane < 16) a.rpart[(row * 11 + k) * CO + ncol0 + nt * 16 + lane] = v;
       }
   }
 }
@@ -795,6 +797,14 @@ __device__ __forceinline__ void quant_epilogue(f4 (&acc)[MT][NT], float* smem, c
   float* sO = smem;
   float bits = 0.f;
   const int cbase = t.nb * BN;
+  // Integer latents: the per-channel table of the same element_bits, read for every element
+  // (index clamped, loads all in flight); the others (noise mode, |ŷ| > 32, no table) are
+  // evaluated in one block after them — a per-element `table ? lookup : element_bits` branch
+  // skipped 2 KB of inlined element_bits per element, an instruction-cache miss each time.
+  // The bits are added in the same element order either way.
+  float yv[MT][NT][4], bv[MT][NT][4];
+  bool slow = false;
+  const bool table = a.rtab != nullptr && a.qmode == ICLR17_QUANT_ROUND;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -814,12 +824,32 @@ __device__ __forceinline__ void quant_epilogue(f4 (&acc)[MT][NT], float* smem, c
           const float u = ok ? a.noise[(((long)t.b * CO + col) * a.Hout + gy) * a.Wout + gx] : 0.f;
           yh = y + u;
         }
-        if (ok) {   // integer latents: the per-channel table of the same element_bits
-          bits += (a.rtab != nullptr && a.qmode == ICLR17_QUANT_ROUND && fabsf(yh) <= 32.f)
-                      ? a.rtab[col * 65 + (int)yh + 32]
-                      : element_bits(yh, a.rate, CO, col);
-        }
+        yv[mt][nt][r] = yh;
+        bv[mt][nt][r] = table ? a.rtab[col * 65 + (int)fminf(fmaxf(yh, -32.f), 32.f) + 32] : 0.f;
+        slow |= ok && !(table && fabsf(yh) <= 32.f);
         sO[row * OS + lcol] = yh;
+      }
+  if (slow) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float yh = yv[mt][nt][r];
+          if (!(table && fabsf(yh) <= 32.f))
+            bv[mt][nt][r] = element_bits(yh, a.rate, CO, ncol0 + nt * 16 + (lane & 15));
+        }
+  }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * MT * 16 + mt * 16 + 4 * (lane >> 4) + r;
+        const int gy = t.ty * 8 + (row >> 3), gx = t.tx * 8 + (row & 7);
+        if (gy < a.gh && gx < a.gw) bits += bv[mt][nt][r];
       }
   __syncthreads();
   store_tile_rows<BN>(a, t, sO, OS, a.yhat, CO, cbase);

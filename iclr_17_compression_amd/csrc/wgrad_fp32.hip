@@ -498,8 +498,8 @@ __global__ void __launch_bounds__(512) gdn_wgrad_x6_kernel(const float* __restri
 // wn·32 .. of every tap, i.e. 5 × (M/64) × 2 tiles of 16×16 (120 accumulator VGPRs at M = 192).
 // X image: 128-byte rows (64 channels), row r stored at slot r ^ bit4(r) and its 32-byte column
 // pairs XOR-ed with (r >> 1) & 3, so a transposed read's 32-lane half — rows r0 + 2i and
-// r0 + 16 + 2i, one pair each — hits 8 distinct bank windows. Partials land in the same
-// [split][m][c][tap] layout as the per-tap kernels.
+// r0 + 16 + 2i, one pair each — hits 8 distinct bank windows. Partials land as
+// [split][tap][m][c] (sum_splits_tap_kernel reorders them into [m][c][tap]).
 template <int M>
 __global__ void __launch_bounds__(512) wgrad_x6_row_kernel(const unsigned short* __restrict__ G6,
                                                               long pg, const unsigned short* __restrict__ X6,
@@ -695,7 +695,9 @@ __global__ void __launch_bounds__(512) wgrad_x6_row_kernel(const unsigned short*
       }
     }
   }
-  // part[split][m][c][tap]
+  // part[split][tap][m][c]: a store instruction writes four 64-byte runs of c (the [m][c][tap]
+  // order of the per-tap kernels scattered every lane 100 bytes apart); sum_splits_tap_kernel
+  // adds the splits and writes PyTorch's [m][c][kh][kw]
   float* out = part + (long)split * M * C * 25;
 #pragma unroll
   for (int kw = 0; kw < KW; ++kw)
@@ -707,7 +709,7 @@ __global__ void __launch_bounds__(512) wgrad_x6_row_kernel(const unsigned short*
         for (int r = 0; r < 4; ++r) {
           const int m = wm * (M / 4) + mt * 16 + 4 * (lane >> 4) + r;
           const int c = cb * CBX + wn * 32 + nt * 16 + (lane & 15);
-          out[((long)m * C + c) * 25 + kh * 5 + kw] = acc[kw][mt][nt][r];
+          out[((long)(kh * 5 + kw) * M + m) * C + c] = acc[kw][mt][nt][r];
         }
 }
 
@@ -939,6 +941,27 @@ __global__ void sum_splits_kernel(const float* __restrict__ part, int nsplit, lo
   }
 }
 
+// dW[m][c][tap] = Σ_s part[s][tap][m][c] (wgrad_x6_row_kernel's partials), the splits added in
+// order as sum_splits_kernel does: reads coalesced along c, one scattered write per element.
+__global__ void sum_splits_tap_kernel(const float* __restrict__ part, int nsplit, int M, int C,
+                                      float* __restrict__ out) {
+  const long n = (long)M * C * 25;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    int k = 0;
+    for (; k + 8 <= nsplit; k += 8) {   // 8 loads in flight, added in split order
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = part[(long)(k + j) * n + i];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[j];
+    }
+    for (; k < nsplit; ++k) s += part[(long)k * n + i];
+    const long mc = i % ((long)M * C);
+    out[mc * 25 + i / ((long)M * C)] = s;
+  }
+}
+
 // out[c] = Σ_t part[t][c] in two fixed-order levels (bitwise reproducible): workgroup (column
 // block, split s) sums rows [s·per, (s+1)·per) — 4 lane groups strided, combined in order — into
 // ws[s][c]; then sum_splits adds the splits in order. Enough workgroups to be bandwidth-bound
@@ -1084,7 +1107,7 @@ int iclr17_wgrad_k5_x6(const uint16_t* G_split, const uint16_t* X_split, int B, 
   int rc = check_launch("wgrad_k5_x6");
   if (rc) return rc;
   const long n = (long)M * C * 25;
-  hipLaunchKernelGGL(sum_splits_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, workspace, ns, n, dW);
+  hipLaunchKernelGGL(sum_splits_tap_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, workspace, ns, M, C, dW);
   return check_launch("wgrad_k5_x6_sum");
 }
 int iclr17_wgrad_k9_x6(const uint16_t* G_split, const float* X, int B, int Ho, int Wo, int M,

@@ -100,6 +100,13 @@ class Step:
         self.rtab = net.bitEstimator.rate_table()
 
     def __call__(self, events=None):
+        for _ in self.layers(events):
+            pass
+        return self.out
+
+    def layers(self, events=None):
+        """The step as a generator: yields after each layer's launch (SplitStep interleaves the
+        batch parts layer by layer); the outputs land in self.out."""
         net, N = self.net, self.N
         w1, w2, w3, g1, g2 = self.enc
         d1, d2, d3, q1, q2 = self.dec
@@ -109,14 +116,19 @@ class Step:
             (w1b, w2b, w3b), (d1b, d2b, d3b), (e1, e2, e3, e4) = self.ebf, self.dbf, self.gbf
             h = kernels.conv1_gdn_bf16(self.x, w1b, net.Encoder.conv1.bias, *e1, N)
             ev(1)
+            yield
             h = kernels.conv2_gdn_bf16(h, w2b, net.Encoder.conv2.bias, *e2)
             ev(2)
+            yield
             y_hat, partial, _, ybf = kernels.conv3_quant_rate_bf16(h, w3b, self.rate, self.rtab)
             ev(3)
+            yield
             h = kernels.deconv_igdn_bf16(ybf, d1b, net.Decoder.deconv1.bias, *e3)
             ev(4)
+            yield
             h = kernels.deconv_igdn_bf16(h, d2b, net.Decoder.deconv2.bias, *e4)
             ev(5)
+            yield
             # bpp's reduction (model.py:71-78) inside deconv3's kernel (ImageCompressor.forward)
             if FOLD_BITS:
                 clipped, _, _, bpp = kernels.deconv3_bf16(h, d3b, net.Decoder.deconv3.bias,
@@ -129,10 +141,13 @@ class Step:
             hs, _, _ = kernels.conv1x6_gdn(self.x, self.w1x6, net.Encoder.conv1.bias, e1[0], e1[2],
                                            N)
             ev(1)
+            yield
             hs, _, _ = kernels.conv2_gdn_x6(hs, w2, net.Encoder.conv2.bias, *e2)
             ev(2)
+            yield
             y_hat, partial, _, ys = kernels.conv3_quant_rate_x6(hs, w3, self.rate, rtab=self.rtab)
             ev(3)
+            yield
             # Synthesis_net_17.decode's x6 path (ICLR17_X6K=1: deconv1 / deconv2 on the x6k engine)
             x1, x2 = self.dx6k
             if kernels.X6K:   # deconv1 on ŷ in the x6k engine's integer-input form (A/B)
@@ -140,12 +155,14 @@ class Step:
             else:
                 hs, _, _ = kernels.deconv_igdn_x6(ys, d1, net.Decoder.deconv1.bias, *e3)
             ev(4)
+            yield
             if kernels.X6K:
                 hs, _ = kernels.deconv_igdn_x6k(hs, x2, net.Decoder.deconv2.bias, e4[0], e4[2],
                                                 chunk_major=D3_CM)
             else:
                 hs, _, _ = kernels.deconv_igdn_x6(hs, d2, net.Decoder.deconv2.bias, *e4, chunk_major=D3_CM)
             ev(5)
+            yield
             if D3_CM and FOLD_BITS:
                 clipped, _, _, bpp = kernels.deconv3_x6(hs, self.d3x6, net.Decoder.deconv3.bias,
                                                         bits=(partial, self.scale))
@@ -155,14 +172,19 @@ class Step:
         else:
             h = kernels.conv1_gdn(self.x, w1, net.Encoder.conv1.bias, g1[0], g1[1], N)
             ev(1)
+            yield
             h = kernels.conv2_gdn(h, w2, net.Encoder.conv2.bias, g2[0], g2[1])
             ev(2)
+            yield
             y_hat, partial = kernels.conv3_quant_rate(h, w3, self.rate, rtab=self.rtab)
             ev(3)
+            yield
             h = kernels.deconv_igdn(y_hat, d1, net.Decoder.deconv1.bias, q1[0], q1[1])
             ev(4)
+            yield
             h = kernels.deconv_igdn(h, d2, net.Decoder.deconv2.bias, q2[0], q2[1])
             ev(5)
+            yield
             clipped, _, _ = kernels.deconv3(h, d3, net.Decoder.deconv3.bias)
             bpp = None
         ev(6)
@@ -170,7 +192,8 @@ class Step:
         if bpp is None:   # the separate reduction kernel (fp32 chain, or ICLR17_FOLD_BITS=0)
             _, bpp = kernels.reduce_partials(partial, self.scale, per_image=False)
         ev(7)
-        return clipped, y_hat, bpp
+        self.out = (clipped, y_hat, bpp)
+        yield
 
 
 class SplitStep:
@@ -189,13 +212,23 @@ class SplitStep:
         main = torch.cuda.current_stream()
         for s in self.side:
             s.wait_stream(main)
-        out = [self.parts[0]()]
-        for s, p in zip(self.side, self.parts[1:]):
-            with torch.cuda.stream(s):
-                out.append(p())
+        # layer-interleaved launch order (part 0 layer 1, part 1 layer 1, part 0 layer 2, ...):
+        # each stream's next kernel is queued while the other's runs (tools/streams_eval.py:
+        # interleaved beat one part's whole chain after the other's)
+        active = [(st, p.layers()) for st, p in zip([main] + self.side, self.parts)]
+        while active:
+            nxt = []
+            for st, g in active:
+                with torch.cuda.stream(st):
+                    try:
+                        next(g)
+                        nxt.append((st, g))
+                    except StopIteration:
+                        pass
+            active = nxt
         for s in self.side:
             main.wait_stream(s)
-        return out
+        return [p.out for p in self.parts]
 
 
 def train_flops(N: int, H: int, W: int) -> float:
@@ -780,7 +813,7 @@ def time_eval(net, x, args, world, dev) -> dict:
             # gaps between dependent kernels); outputs land in the graph's own memory pool
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
-                step()
+                run()   # SplitStep: the side streams fork from / join the capture stream
             graph.replay()
             torch.cuda.synchronize()
             run = graph.replay
@@ -795,7 +828,7 @@ def time_eval(net, x, args, world, dev) -> dict:
             dist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
-        if run is not step and not args.graph:   # the one-stream step of the per-layer pass, warm
+        if run is not step:   # the one-stream step of the per-layer pass, warm
             for _ in range(3):
                 step()
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(8)] for _ in range(args.steps)]
@@ -966,7 +999,7 @@ def main() -> None:
                     help="the same for the bf16 leg / --precision bf16")
     ap.add_argument("--graph", action="store_true",
                     help="eval: replay the timed steps from one HIP graph instead of launching them "
-                         "kernel by kernel (x6: 4 % slower, bf16: 1.4 % faster; DESIGN §5)")
+                         "kernel by kernel (round 4: x6 1.5 %, bf16 12 % slower than eager; profiles/r04_ab_streams.log)")
     ap.add_argument("--mode", choices=("eval", "train", "kodak", "codec", "encdec"), default="eval")
     ap.add_argument("--precision", choices=kernels.PRECISIONS, default=None,
                     help="inference contraction mode (default: ICLR17_PRECISION or x6)")
@@ -1074,6 +1107,7 @@ def main() -> None:
         finally:
             kernels.set_precision(prec)
     r = time_eval(net, x, args, world, dev)
+    nstreams = args.bf16_streams if prec == "bf16" else args.streams
     elapsed, per_layer_ms, bpp = r["elapsed"], r["per_layer_ms"], r["bpp"]
     pixels = world * B * S * S * args.steps
     value = pixels / elapsed / 1e6
@@ -1109,8 +1143,8 @@ def main() -> None:
                                             else "fp32 (exact-f32 MFMA products)"),
                    "parallelism": f"dp{world} (images sharded by rank, no data-path collective)",
                    "launch": ("hipGraph replay of the whole step" if args.graph else
-                              "eager (kernel by kernel)" + (f", batch split over {args.streams} HIP streams"
-                                                            if args.streams > 1 else ""))},
+                              "eager (kernel by kernel)" + (f", batch split over {nstreams} HIP streams"
+                                                            if nstreams > 1 else ""))},
         "roofline": {**roof, "algorithmic_bytes_per_launch": bytes_[dominant] * B,
                      "flop_per_launch": flops[dominant] * B,
                      "whole_step_tflops": round(total_flops / (ms_per_step * 1e-3) / 1e12, 2)},

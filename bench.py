@@ -999,7 +999,7 @@ def main() -> None:
                     help="the same for the bf16 leg / --precision bf16")
     ap.add_argument("--graph", action="store_true",
                     help="eval: replay the timed steps from one HIP graph instead of launching them "
-                         "kernel by kernel (round 4: x6 1.5 %, bf16 12 % slower than eager; profiles/r04_ab_streams.log)")
+                         "kernel by kernel (slower than eager: bf16 12 % in round 4, profiles/r04_ab_streams.log; x6 4 % in round 3)")
     ap.add_argument("--mode", choices=("eval", "train", "kodak", "codec", "encdec"), default="eval")
     ap.add_argument("--precision", choices=kernels.PRECISIONS, default=None,
                     help="inference contraction mode (default: ICLR17_PRECISION or x6)")

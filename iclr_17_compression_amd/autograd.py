@@ -228,13 +228,13 @@ def analysis_backward(enc, saved: Dict[str, Tensor], g_y: Tensor,
         dW3 = ws.run(lambda: kernels.wgrad_k5_x6(g_y_split, a2s), g_y_split, a2s, big=True)
         g_u2, dn2, db2, dbe2, g_u2s = kernels.bwd_conv_gdn(g_y, w3t, saved["u2"], *x2[:3],
                                                            g_split=g_y_split, want_split=True,
-                                                           g6=x2[3], g6t=x2[4])
+                                                           g6=x2[3], g6t=x2[4], want_f32=False)
         dW2 = ws.run(lambda: kernels.wgrad_k5_x6(g_u2s, a1s), g_u2s, a1s, big=True)
         dg2 = ws.run(lambda: kernels.gdn_param_grads(dn2, saved["u2"], dbe2, enc.gdn2.beta,
                                                      enc.gdn2.gamma, bb2, gb2), dn2, saved["u2"], dbe2)
         g_u1, dn1, db1, dbe1, g_u1s = kernels.bwd_conv_gdn(g_u2, w2t, saved["u1"], *x1[:3],
                                                            g_split=g_u2s, want_split=True,
-                                                           g6=x1[3], g6t=x1[4])
+                                                           g6=x1[3], g6t=x1[4], want_f32=want_dx)
         dW1 = ws.run(lambda: kernels.wgrad_k9_x6(g_u1s, saved["x"]), g_u1s, saved["x"], big=True)
     else:
         dW3 = ws.run(lambda: kernels.wgrad_k5(g_y, saved["a2"]), g_y, saved["a2"], big=True)
@@ -310,12 +310,12 @@ def synthesis_backward(dec, saved: Dict[str, Tensor], g_recon: Tensor, g_bpp: Op
         dbd3 = ws.run(lambda: kernels.bias_grad_nchw(g_recon), g_recon)
         g_v2, dnq2, dbd2, dbeq2, g_v2s = kernels.bwd_deconv3_igdn(g_recon, None, saved["v2"], *q2[:3],
                                                                   w_split=d3x, want_split=True,
-                                                                  g6=q2[3], g6t=q2[4])
+                                                                  g6=q2[3], g6t=q2[4], want_f32=False)
         dWd2 = ws.run(lambda: kernels.wgrad_k5_x6(s1s, g_v2s), s1s, g_v2s, big=True)
         dq2 = ws.run(gdn_q2, dnq2, saved["v2"], dbeq2)
         g_v1, dnq1, dbd1, dbeq1, g_v1s = kernels.bwd_deconv_igdn(g_v2, d2c, saved["v1"], *q1[:3],
                                                                  g_split=g_v2s, want_split=True,
-                                                                 g6=q1[3], g6t=q1[4])
+                                                                 g6=q1[3], g6t=q1[4], want_f32=False)
         dWd1 = ws.run(lambda: kernels.wgrad_k5_x6(ys, g_v1s), ys, g_v1s, big=True)
         dq1 = ws.run(gdn_q1, dnq1, saved["v1"], dbeq1)
         r = kernels.bwd_deconv_rate(g_v1, d1c, y if g_bpp is not None else None, rate_packed,

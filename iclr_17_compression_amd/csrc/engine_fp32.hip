@@ -685,7 +685,8 @@ __device__ __forceinline__ void gdn_bwd_epilogue(f4 (&g)[MT][NT], float* smem, c
       }
     }
   __syncthreads();
-  store_tile_rows<CO>(a, t, sX, XS, a.out, CO, 0);
+  // the fp32 ∂u is optional beside its split form (the x6 backward hands only the split on)
+  if (a.out != nullptr) store_tile_rows<CO>(a, t, sX, XS, a.out, CO, 0);
   if (a.out_split != nullptr) store_tile_rows_split<CO>(a, t, sX, XS, CO, 0);   // x6 consumer
   if (a.colsum_out != nullptr) tile_colsum<CO>(a, t, sX, XS, a.colsum_out);
 }
@@ -2880,7 +2881,7 @@ int iclr17_bwd_deconv3_igdn(const float* g_recon, int B, int H, int W, int N,
   int rc = check_dims(B, H, W, N);
   if (rc) return rc;
   ICLR17_REQUIRE(g_recon && (w_packed || w_split) && v_saved && beta_eff && gamma_packed &&
-                     gamma_packed_t && g_v && dn, ICLR17_EINVAL, "bwd_deconv3_igdn: null pointer");
+                     gamma_packed_t && (g_v || g_v_split) && dn, ICLR17_EINVAL, "bwd_deconv3_igdn: null pointer");
   EngineArgs b = bwd_args(v_saved, gamma_packed_t, dn);
   b.colsum_out = colsum_gv;
   b.colsum_t = colsum_dn;
@@ -2903,7 +2904,7 @@ int iclr17_bwd_deconv_igdn(const float* g_v, const uint16_t* g_v_split, int B, i
   ICLR17_REQUIRE(B > 0 && h > 0 && w > 0, ICLR17_EINVAL, "bwd_deconv_igdn: bad shape");
   ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "channel count N=%d unsupported", N);
   ICLR17_REQUIRE((g_v || g_v_split) && w_packed && v_prev && beta_eff && gamma_packed &&
-                     gamma_packed_t && g_v_prev && dn, ICLR17_EINVAL,
+                     gamma_packed_t && (g_v_prev || g_v_prev_split) && dn, ICLR17_EINVAL,
                  "bwd_deconv_igdn: null pointer");
   EngineArgs b = bwd_args(v_prev, gamma_packed_t, dn);
   b.colsum_out = colsum_gv;
@@ -2961,7 +2962,7 @@ int iclr17_bwd_conv_gdn(const float* g_u, const uint16_t* g_u_split, int B, int 
   ICLR17_REQUIRE(B > 0 && h > 0 && w > 0, ICLR17_EINVAL, "bwd_conv_gdn: bad shape");
   ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "channel count N=%d unsupported", N);
   ICLR17_REQUIRE((g_u || g_u_split) && w_packed && u_prev && beta_eff && gamma_packed &&
-                     gamma_packed_t && g_u_prev && dn, ICLR17_EINVAL, "bwd_conv_gdn: null pointer");
+                     gamma_packed_t && (g_u_prev || g_u_prev_split) && dn, ICLR17_EINVAL, "bwd_conv_gdn: null pointer");
   EngineArgs b = bwd_args(u_prev, gamma_packed_t, dn);
   b.colsum_out = colsum_gu;
   b.colsum_t = colsum_dn;

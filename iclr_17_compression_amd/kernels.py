@@ -999,13 +999,14 @@ def _split_like(t: Tensor) -> Tensor:
 def bwd_deconv3_igdn(g_recon: Tensor, wp_conv1form: Optional[Tensor], v_saved: Tensor,
                      beta_eff: Tensor, gp: Tensor, gpt: Tensor, w_split: Optional[Tensor] = None,
                      want_split: bool = False, g6: Optional[Tensor] = None,
-                     g6t: Optional[Tensor] = None):
+                     g6t: Optional[Tensor] = None, want_f32: bool = True):
     """deconv3 input-gradient fused with IGDN2 backward →
     (g_v2 NHWC, dn NHWC, Σ g_v2 = ∂bias of deconv2, Σ dn = ∂β_eff of IGDN2[, g_v2 split]).
-    w_split (``pack_conv1_x6`` of the deconv3 weight) runs the contraction in x6."""
+    w_split (``pack_conv1_x6`` of the deconv3 weight) runs the contraction in x6. want_f32=False
+    (with want_split): g_v2 is not written (None), only its split form."""
     B, _, H, W = g_recon.shape
     N = v_saved.shape[3]
-    g_v = torch.empty_like(v_saved)
+    g_v = torch.empty_like(v_saved) if want_f32 or not want_split else None
     dn = torch.empty_like(v_saved)
     sp = _split_like(v_saved) if want_split else None
     cs_g, cs_d = _colsum_buffers(v_saved, 0, H // 4, W // 4)
@@ -1020,12 +1021,13 @@ def bwd_deconv3_igdn(g_recon: Tensor, wp_conv1form: Optional[Tensor], v_saved: T
 def bwd_deconv_igdn(g_v: Optional[Tensor], wp_conv5form: Tensor, v_prev: Tensor, beta_eff: Tensor,
                     gp: Tensor, gpt: Tensor, g_split: Optional[Tensor] = None,
                     want_split: bool = False, g6: Optional[Tensor] = None,
-                    g6t: Optional[Tensor] = None):
+                    g6t: Optional[Tensor] = None, want_f32: bool = True):
     """deconv2 input-gradient fused with IGDN1 backward →
     (g_v1 NHWC, dn NHWC, Σ g_v1 = ∂bias of deconv1, Σ dn = ∂β_eff of IGDN1[, g_v1 split]).
-    g_split (g_v in split form) runs the contraction in x6."""
+    g_split (g_v in split form) runs the contraction in x6. want_f32=False (with want_split):
+    g_v1 is not written (None)."""
     B, h, w, N = v_prev.shape
-    g_prev = torch.empty_like(v_prev)
+    g_prev = torch.empty_like(v_prev) if want_f32 or not want_split else None
     dn = torch.empty_like(v_prev)
     sp = _split_like(v_prev) if want_split else None
     cs_g, cs_d = _colsum_buffers(v_prev, 0, h, w)
@@ -1062,13 +1064,14 @@ def bwd_deconv_rate(g_v1: Optional[Tensor], wp_conv5form: Tensor, y_tilde: Optio
 def bwd_conv_gdn(g_u: Optional[Tensor], wp_deconv5form: Tensor, u_prev: Tensor, beta_eff: Tensor,
                  gp: Tensor, gpt: Tensor, g_split: Optional[Tensor] = None,
                  want_split: bool = False, g6: Optional[Tensor] = None,
-                 g6t: Optional[Tensor] = None):
+                 g6t: Optional[Tensor] = None, want_f32: bool = True):
     """conv3/conv2 input-gradient fused with GDN2/GDN1 backward →
     (g_u_prev NHWC, dn NHWC, Σ g_u_prev = ∂bias of the previous conv, Σ dn = ∂β_eff
-    [, g_u_prev split]). g_split (g_u in split form) runs the contraction in x6."""
+    [, g_u_prev split]). g_split (g_u in split form) runs the contraction in x6. want_f32=False
+    (with want_split): g_u_prev is not written (None)."""
     ref = g_u if g_split is None else g_split[0]
     B, h, w, N = ref.shape
-    g_prev = torch.empty_like(u_prev)
+    g_prev = torch.empty_like(u_prev) if want_f32 or not want_split else None
     dn = torch.empty_like(u_prev)
     sp = _split_like(u_prev) if want_split else None
     cs_g, cs_d = _colsum_buffers(u_prev, 1, h, w)

@@ -342,7 +342,9 @@ int iclr17_rate_bits_partials(int C, int h, int w);
  * Input gradients reuse the forward engine (conv dgrad = transposed conv and vice versa), each
  * fused with the backward of the GDN/IGDN that precedes it; dn = ∂L/∂n (the GDN norm pool)
  * feeds the GDN parameter gradients. Weight packing for the dgrads: deconv weights with
- * ICLR17_W_CONV5 (deconv1/2) or ICLR17_W_CONV1 (deconv3), conv weights with ICLR17_W_DECONV5. */
+ * ICLR17_W_CONV5 (deconv1/2) or ICLR17_W_CONV1 (deconv3), conv weights with ICLR17_W_DECONV5.
+ * In the three GDN-backward entries the fp32 input gradient (g_v / g_v_prev / g_u_prev) may be
+ * NULL when its split form is requested: the x6 backward hands only the split to the next kernel. */
 
 /* ∂recon of λ·mean((recon−x)²) (model.py:61) and/or of a gradient on clamp(recon,0,1)
  * (model.py:59): g_mse, g_clip nullable (device scalar / NCHW tensor). */

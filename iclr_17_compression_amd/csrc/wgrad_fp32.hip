@@ -19,6 +19,9 @@ namespace {
 
 hipStream_t S(void* s) { return (hipStream_t)s; }
 
+#ifndef ICLR17_K9_IM2COL_DMA
+#define ICLR17_K9_IM2COL_DMA 0   // 1: k9 x6 weight gradient through the materialised split im2col (A/B)
+#endif
 constexpr int KP = 32;  // pixels per k-step
 
 __device__ __attribute__((aligned(16))) float g_wzero[4] = {0.f, 0.f, 0.f, 0.f};
@@ -168,18 +171,29 @@ __device__ __forceinline__ int swz6(int r, int row_elems) {
                           : 2 * ((r & 3) | (((r >> 3) & 1) << 2));
 }
 
-template <int M, int CB>
+// IM2COL (the k9 weight gradients): X is not read from a materialised split im2col but built
+// per k-step from the 3-channel NCHW image Xi ([B][3][4·Ho][4·Wo]): each of the 512 threads owns
+// one (pixel, 8-column piece) of the step's [32 px][CB] X image, loads its 8 window values for the
+// NEXT step into registers before the current step's MFMAs, and splits and writes them into the
+// idle stage after them (the G operand still arrives by LDS-DMA). The X image holds the same split
+// values in the same swizzled layout as the DMA'd one, so the partials are bit-identical; the
+// 201 MB im2col write (B=32, 256²) and its re-read leave the k9 weight gradient.
+template <int M, int CB, bool IM2COL = false>
 __global__ void __launch_bounds__(512) wgrad_x6_1x1_kernel(const unsigned short* __restrict__ G6,
                                                               long pg, const unsigned short* __restrict__ X6,
                                                               long pxs, long P, int C, int nsplit,
-                                                              float* __restrict__ part) {
+                                                              float* __restrict__ part,
+                                                              const float* __restrict__ Xi = nullptr,
+                                                              int Ho = 0, int Wo = 0) {
   constexpr int WM = 2, WN = 4, NW = WM * WN;        // 8 waves
   constexpr int MT = M / WM / 16, NT = CB / WN / 16; // 16×16 tiles per wave
   constexpr int GPL = KP * M, XPL = KP * CB;         // u16 per plane image
   constexpr int STAGE = 3 * GPL + 3 * XPL;           // u16 per stage
   constexpr int GPR = M / 8, XPR = CB / 8;           // 16-byte pieces per pixel row
-  constexpr int NGI = KP * GPR / 64, NXI = KP * XPR / 64;   // DMA wave-instructions per plane
+  constexpr int NGI = KP * GPR / 64, NXI = IM2COL ? 0 : KP * XPR / 64;   // DMA wave-instructions per plane
   constexpr int NI = 3 * NGI + 3 * NXI;
+  static_assert(!IM2COL || KP * XPR == NW * 64, "IM2COL: one X piece per thread and step");
+  constexpr int NXD = NXI > 0 ? NXI : 1;             // divisor in the (IM2COL: dead) X-slot paths
   constexpr int NI_W = (NI + NW - 1) / NW;
   static_assert(MT * WM * 16 == M && NT * WN * 16 == CB, "tile shape");
   static_assert(KP * GPR % 64 == 0 && KP * XPR % 64 == 0, "whole DMA instructions");
@@ -207,7 +221,7 @@ __global__ void __launch_bounds__(512) wgrad_x6_1x1_kernel(const unsigned short*
   for (int j = 0; j < NI_W; ++j) {
     const int i = wave + NW * j;
     const bool isg = i < 3 * NGI;
-    const int pc = (isg ? (i % NGI) : ((i - 3 * NGI) % NXI)) * 64 + lane;
+    const int pc = (isg ? (i % NGI) : ((i - 3 * NGI) % NXD)) * 64 + lane;
     const int prow = isg ? pc / GPR : pc / XPR;
     const int piece = isg ? (pc % GPR) ^ swz6(prow, M) : (pc % XPR) ^ swz6(prow, CB);
     pj[j] = p0 + prow;
@@ -226,7 +240,7 @@ __global__ void __launch_bounds__(512) wgrad_x6_1x1_kernel(const unsigned short*
         if (pj[j] < p1) src = G6 + pl * pg + off[j];
         dst = st + pl * GPL + ii * 512;
       } else {
-        const int pl = (i - 3 * NGI) / NXI, ii = (i - 3 * NGI) % NXI;
+        const int pl = (i - 3 * NGI) / NXD, ii = (i - 3 * NGI) % NXD;
         if (pj[j] < p1) src = X6 + pl * pxs + off[j];
         dst = st + 3 * GPL + pl * XPL + ii * 512;
       }
@@ -264,13 +278,58 @@ __global__ void __launch_bounds__(512) wgrad_x6_1x1_kernel(const unsigned short*
     boff[nt] = (8 * g + q) * CB + (((ch >> 3) ^ frx) << 3) + (ch & 7);
   }
 
+  // IM2COL: this thread's X piece — pixel row xpx of the step, logical piece xpc (k = ct·CB +
+  // 8·xpc + e) at its swizzled slot; the window offsets of its 8 k relative to (4·oy, 4·ox)
+  const int xpx = tid / XPR, xpc = tid % XPR;
+  const int xdst = xpx * CB + ((xpc ^ swz6(xpx, CB)) << 3);
+  const int Hi = 4 * Ho, Wi = 4 * Wo;
+  int xdy[8], xdx[8], xoff[8];
+  bool xkv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = ct * CB + xpc * 8 + e;
+    const int c = k / 81, kh = (k % 81) / 9, kw = k % 9;
+    xkv[e] = k < 243;
+    xdy[e] = kh - 4;
+    xdx[e] = kw - 4;
+    xoff[e] = (c * Hi + kh - 4) * Wi + kw - 4;
+  }
+  float xr[8];
+  auto load_x = [&](int s) {
+    const long p = p0 + (long)s * KP + xpx;
+    const int pi = (int)(p < p1 ? p : 0);
+    const int ox = pi % Wo, t2 = pi / Wo, oy = t2 % Ho, b = t2 / Ho;
+    const long base = ((long)b * 3 * Hi + 4 * oy) * Wi + 4 * ox;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int iy = 4 * oy + xdy[e], ix = 4 * ox + xdx[e];
+      const bool ok = p < p1 && xkv[e] && (unsigned)iy < (unsigned)Hi && (unsigned)ix < (unsigned)Wi;
+      xr[e] = ok ? Xi[base + xoff[e]] : 0.f;
+    }
+  };
+  auto store_x = [&](int buf) {
+    u4 hi, mi, lo;
+    split8(f4{xr[0], xr[1], xr[2], xr[3]}, f4{xr[4], xr[5], xr[6], xr[7]}, hi, mi, lo);
+    unsigned short* d = smem + buf * STAGE + 3 * GPL + xdst;
+    *(u4*)d = hi;
+    *(u4*)(d + XPL) = mi;
+    *(u4*)(d + 2 * XPL) = lo;
+  };
+
   const unsigned sbase = (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned short*)smem;
-  if (nsteps > 0) issue(0);
+  if (nsteps > 0) {
+    issue(0);
+    if constexpr (IM2COL) {
+      load_x(0);
+      store_x(0);
+    }
+  }
   for (int s = 0; s < nsteps; ++s) {
     dma_barrier();   // stage s landed for every wave; stage (s+1)&1 is free
     if (s + 1 < nsteps) {
       advance();
       issue((s + 1) & 1);
+      if constexpr (IM2COL) load_x(s + 1);   // under this step's MFMAs
     }
     const unsigned st = sbase + (s & 1) * STAGE * 2;   // LDS byte address of the stage
     auto frag = [&](unsigned a, int rowe) {             // 8 pixels (k) of 4 channels
@@ -315,6 +374,9 @@ __global__ void __launch_bounds__(512) wgrad_x6_1x1_kernel(const unsigned short*
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl) lgkm_wait(Af[cur ^ 1][pl]);
       }
+    }
+    if constexpr (IM2COL) {
+      if (s + 1 < nsteps) store_x((s + 1) & 1);   // published by the next dma_barrier
     }
   }
   // part[split][m][c]: lane holds rows 4(lane >> 4) + r, column lane & 15 of each tile
@@ -1054,8 +1116,8 @@ size_t iclr17_wgrad_workspace_size(int kind, int B, int Ho, int Wo, int M, int C
   const long P = (long)B * Ho * Wo;
   if (kind == 9) return (size_t)wgrad9_splits(B * ((Wo + 7) / 8) * ((Ho + 7) / 8)) * M * 243;
   if (kind == 6) return (size_t)wgrad6_splits(P, 5 * (C / 64)) * M * C * 25;
-  if (kind == 7)   // k9 x6: partials [ns][M][256] + the split im2col [3][P][256] (u16)
-    return (size_t)wgrad6_splits(P, 2) * M * 256 + (size_t)P * 256 * 3 / 2;
+  if (kind == 7)   // k9 x6: partials [ns][M][256] (+ the split im2col [3][P][256] u16 of the A/B build)
+    return (size_t)wgrad6_splits(P, 2) * M * 256 + (ICLR17_K9_IM2COL_DMA ? (size_t)P * 256 * 3 / 2 : 0);
   const int ntap = kind == 1 ? 1 : 25;
   const int tiles = ntap * (C / 64);
   return (size_t)wgrad_splits(P, tiles) * M * C * ntap;
@@ -1120,18 +1182,25 @@ int iclr17_wgrad_k9_x6(const uint16_t* G_split, const float* X, int B, int Ho, i
   const int tiles = 2;   // 256 columns (243 used) in two 128-column tiles
   const int ns = wgrad6_splits(P, tiles);
   float* part = workspace;
-  unsigned short* cols = (unsigned short*)(workspace + (long)ns * M * 256);
   hipStream_t st = S(stream);
-  hipLaunchKernelGGL(im2col9_split_kernel, dim3((Wo + I9_OX - 1) / I9_OX, B * Ho), dim3(256), 0, st,
-                     X, B, Ho, Wo, cols);
-  int rc = check_launch("wgrad_k9_x6_im2col");
-  if (rc) return rc;
   dim3 grid((tiles * ns + 7) / 8 * 8);
   const unsigned short* g6 = (const unsigned short*)G_split;
-  if (M == 192)
-    hipLaunchKernelGGL((wgrad_x6_1x1_kernel<192, 128>), grid, dim3(512), 0, st, g6, P * M, cols, P * 256, P, 256, ns, part);
-  else
-    hipLaunchKernelGGL((wgrad_x6_1x1_kernel<128, 128>), grid, dim3(512), 0, st, g6, P * M, cols, P * 256, P, 256, ns, part);
+  int rc;
+  if (ICLR17_K9_IM2COL_DMA) {   // diagnostic: the materialised split im2col + the 1×1 kernel
+    unsigned short* cols = (unsigned short*)(workspace + (long)ns * M * 256);
+    hipLaunchKernelGGL(im2col9_split_kernel, dim3((Wo + I9_OX - 1) / I9_OX, B * Ho), dim3(256), 0, st,
+                       X, B, Ho, Wo, cols);
+    rc = check_launch("wgrad_k9_x6_im2col");
+    if (rc) return rc;
+    if (M == 192)
+      hipLaunchKernelGGL((wgrad_x6_1x1_kernel<192, 128>), grid, dim3(512), 0, st, g6, P * M, cols, P * 256, P, 256, ns, part, nullptr, 0, 0);
+    else
+      hipLaunchKernelGGL((wgrad_x6_1x1_kernel<128, 128>), grid, dim3(512), 0, st, g6, P * M, cols, P * 256, P, 256, ns, part, nullptr, 0, 0);
+  } else if (M == 192) {
+    hipLaunchKernelGGL((wgrad_x6_1x1_kernel<192, 128, true>), grid, dim3(512), 0, st, g6, P * M, nullptr, 0L, P, 256, ns, part, X, Ho, Wo);
+  } else {
+    hipLaunchKernelGGL((wgrad_x6_1x1_kernel<128, 128, true>), grid, dim3(512), 0, st, g6, P * M, nullptr, 0L, P, 256, ns, part, X, Ho, Wo);
+  }
   rc = check_launch("wgrad_k9_x6");
   if (rc) return rc;
   const long n = (long)M * 243;

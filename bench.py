@@ -40,6 +40,7 @@ HBM_PEAK_GBS = 8000.0
 # deconv2 → deconv3 through the chunk-major split form (ICLR17_D3_CM=0: the NHWC split, for A/B)
 D3_CM = os.environ.get("ICLR17_D3_CM", "1") != "0"
 FOLD_BITS = os.environ.get("ICLR17_FOLD_BITS", "1") != "0"   # bpp's reduction inside deconv3 (A/B)
+W6 = os.environ.get("ICLR17_W6", "1") != "0"   # x6 conv3 with pre-split weights (A/B)
 
 LAYERS = ("conv1_gdn1", "conv2_gdn2", "conv3_quant_rate", "deconv1_igdn1", "deconv2_igdn2",
           "deconv3_clamp", "bits_reduce")
@@ -93,6 +94,7 @@ class Step:
         self.rate = net.bitEstimator.packed()
         gdns = (net.Encoder.gdn1, net.Encoder.gdn2, net.Decoder.igdn1, net.Decoder.igdn2)
         self.w1x6 = net.Encoder.packed_conv1_x6()
+        self.w3s = net.Encoder.packed_w3_split() if W6 else None   # x6 conv3's pre-split weights
         self.g6 = [m.effective_params_x6() for m in gdns]
         self.ebf = net.Encoder.packed_bf16()
         self.dbf = net.Decoder.packed_bf16()
@@ -145,7 +147,8 @@ class Step:
             hs, _, _ = kernels.conv2_gdn_x6(hs, w2, net.Encoder.conv2.bias, *e2)
             ev(2)
             yield
-            y_hat, partial, _, ys = kernels.conv3_quant_rate_x6(hs, w3, self.rate, rtab=self.rtab)
+            y_hat, partial, _, ys = kernels.conv3_quant_rate_x6(hs, w3, self.rate, rtab=self.rtab,
+                                                                w_split=self.w3s)
             ev(3)
             yield
             # Synthesis_net_17.decode's x6 path (ICLR17_X6K=1: deconv1 / deconv2 on the x6k engine)

@@ -73,6 +73,8 @@ SIGNATURES = {
     "iclr17_analysis_conv2_gdn_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_analysis_conv3_quant_rate_x6": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P,
                                                  _P, _P, _P, _P]),
+    "iclr17_analysis_conv3_quant_rate_x6w": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _P, _P, _P, _P,
+                                                  _P, _P, _P, _P]),
     "iclr17_synthesis_deconv_igdn_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
                                              _P]),
     "iclr17_synthesis_deconv_igdn_x6_cm": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,

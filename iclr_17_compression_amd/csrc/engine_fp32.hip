@@ -110,6 +110,10 @@ struct EngineArgs {
   const double* fold_partial;
   int fold_T;
   double* fold_per_image;   // [B] or nullptr
+  // x6 conv3 (W6 instantiation): the weights pre-split into three bf16 planes
+  // (iclr17_split_packed(w_packed, 25, CI, CO): [3][25][CI/8][CO][8]) instead of split per k-step
+  const unsigned short* w6;
+  long w6_plane;
   float* fold_total;        // scale · Σ, 0-dim
   double fold_scale;
 };
@@ -963,15 +967,21 @@ __device__ __forceinline__ void out3_epilogue(f4 (&acc)[MT][NT], float* smem, co
 // columns in VALU. One 32-deep step = per 16×16 tile six v_mfma_f32_16x16x32_bf16:
 // lo·hi + hi·lo + mid·mid + mid·hi + hi·mid + hi·hi (the dropped mid·lo, lo·mid, lo·lo terms are
 // below 2^-24 of the product), accumulated in fp32.
-template <int CI, int CO, int BN, int WM, int WN, int EPI, bool X6, int BMT = BM>
+// W6 (x6 conv3): B arrives pre-split, [3 planes][4 k-groups][BN][8] bf16 per stage (a.w6), and
+// the fragments are read as they are: conv3's 2×2 waves split each weight column for only two
+// row tiles, so the per-step split was 3.7 VALU instructions per MFMA. Same bf16 operands (the
+// split is iclr17_split_packed's, i.e. the same split8 on the same quads): bit-identical output.
+template <int CI, int CO, int BN, int WM, int WN, int EPI, bool X6, int BMT = BM, bool W6 = false>
 __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   constexpr int NWV = WM * WN;                   // waves (4, or 8 for the 128-row tiles)
   constexpr int MT = BMT / WM / 16;
   constexpr int NT = BN / WN / 16;
   constexpr int KCH = 32;                        // input channels per k-step
   constexpr int NCH = CI / KCH;
+  static_assert(!W6 || (X6 && EPI == EPI_QUANT), "pre-split weights: x6 conv3");
   constexpr int SA = X6 ? 3 * BMT * KCH / 2 : BMT * KCH;   // A image floats per stage
-  constexpr int SB = KCH * BN;                   // B image floats per stage: [8 quads][BN][4]
+  constexpr int SB = W6 ? 3 * 4 * BN * 8 / 2     // W6: [3][4][BN][8] bf16
+                        : KCH * BN;              // B image floats per stage: [8 quads][BN][4]
   constexpr int STAGE = SA + SB;
   constexpr int NAI = SA * 4 / 1024;             // A glds wave-instructions per step (8 | 12)
   constexpr int NBI = SB * 4 / 1024;             // B glds wave-instructions per step
@@ -1039,8 +1049,15 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
 #pragma unroll
   for (int j = 0; j < BI_W; ++j) {
     const int i = wave + NWV * j;
-    const int o = i * 256 + lane * 4;   // offset in the LDS image [8 quads][BN][4]
-    bsrc[j] = (BN == CO) ? o : ((o / (BN * 4)) * CO + t.nb * BN) * 4 + o % (BN * 4);
+    if constexpr (W6) {   // u16 offset in the pre-split planes: (plane, k-group, column) of the slot
+      const int o2 = i * 512 + lane * 8;   // u16 offset in the LDS image [3][4][BN][8]
+      const int pl = o2 / (32 * BN), r = o2 - pl * 32 * BN;
+      const int gg = r / (BN * 8), col = (r - gg * BN * 8) / 8;
+      bsrc[j] = (int)(pl * a.w6_plane) + (gg * CO + t.nb * BN + col) * 8;
+    } else {
+      const int o = i * 256 + lane * 4;   // offset in the LDS image [8 quads][BN][4]
+      bsrc[j] = (BN == CO) ? o : ((o / (BN * 4)) * CO + t.nb * BN) * 4 + o % (BN * 4);
+    }
   }
 
   int t0 = 0, ntaps = 1;
@@ -1067,11 +1084,20 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
       }
     }
     float* sb = sa + SA;
-    const float* __restrict__ ws = a.w + ((long)tap * CI + cc * KCH) * CO;   // uniform base
+    if constexpr (W6) {
+      const unsigned short* __restrict__ ws6 = a.w6 + ((long)tap * (CI / 8) + cc * 4) * CO * 8;
 #pragma unroll
-    for (int j = 0; j < BI_W; ++j) {
-      const int i = wave + NWV * j;
-      if (NBI % NWV == 0 || i < NBI) glds16(ws + bsrc[j], sb + i * 256);
+      for (int j = 0; j < BI_W; ++j) {
+        const int i = wave + NWV * j;
+        if (NBI % NWV == 0 || i < NBI) glds16((const float*)(ws6 + bsrc[j]), sb + i * 256);
+      }
+    } else {
+      const float* __restrict__ ws = a.w + ((long)tap * CI + cc * KCH) * CO;   // uniform base
+#pragma unroll
+      for (int j = 0; j < BI_W; ++j) {
+        const int i = wave + NWV * j;
+        if (NBI % NWV == 0 || i < NBI) glds16(ws + bsrc[j], sb + i * 256);
+      }
     }
   };
 
@@ -1101,6 +1127,16 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
     const unsigned short* sa = (const unsigned short*)(smem + buf * STAGE);
     const float* sb = smem + buf * STAGE + SA + boff6;
     bf8 Bh[NT], Bm[NT], Bl[NT];
+    if constexpr (W6) {   // [3][4][BN][8]: lane (k-group lane >> 4, column) reads 16 bytes per plane
+      const unsigned short* sb6 = (const unsigned short*)(smem + buf * STAGE + SA) +
+                                  ((lane >> 4) * BN + wn * (BN / WN) + (lane & 15)) * 8;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        Bh[nt] = __builtin_bit_cast(bf8, *(const u4*)(sb6 + nt * 128));
+        Bm[nt] = __builtin_bit_cast(bf8, *(const u4*)(sb6 + 32 * BN + nt * 128));
+        Bl[nt] = __builtin_bit_cast(bf8, *(const u4*)(sb6 + 64 * BN + nt * 128));
+      }
+    } else {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       u4 bh, bm, bl;
@@ -1108,6 +1144,7 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
       Bh[nt] = __builtin_bit_cast(bf8, bh);
       Bm[nt] = __builtin_bit_cast(bf8, bm);
       Bl[nt] = __builtin_bit_cast(bf8, bl);
+    }
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -1307,9 +1344,9 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   }
 }
 
-template <int CI, int CO, int BN, int WM, int WN, int EPI, bool X6 = false>
+template <int CI, int CO, int BN, int WM, int WN, int EPI, bool X6 = false, bool W6 = false>
 __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
-  engine_body<CI, CO, BN, WM, WN, EPI, X6, BM>(a);
+  engine_body<CI, CO, BN, WM, WN, EPI, X6, BM, W6>(a);
 }
 
 // The same kernel held to 256 VGPRs (2 waves per SIMD) where the compiler would otherwise just
@@ -2341,6 +2378,8 @@ struct SplitIO {
   int out_cm = 0;                           // out in the chunk-major split form
   const unsigned short* gamma6 = nullptr;   // x6: split γ_eff for the GDN contraction
   const unsigned short* gammaT6 = nullptr;  // x6 backward: split transposed γ_eff
+  const unsigned short* w6 = nullptr;       // x6 conv3: pre-split weights (engine W6)
+  long w6_plane = 0;
 };
 
 static void apply_split(EngineArgs& a, const SplitIO* x6) {
@@ -2349,6 +2388,8 @@ static void apply_split(EngineArgs& a, const SplitIO* x6) {
   a.out_split = x6->out; a.out_plane = x6->out_plane; a.out_cm = x6->out_cm;
   a.ggamma6 = x6->gamma6;
   a.ggammaT6 = x6->gammaT6;
+  a.w6 = x6->w6;
+  a.w6_plane = x6->w6_plane;
 }
 
 template <int N, int EPI = EPI_GDN>
@@ -2406,7 +2447,10 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
     constexpr int WN = (BN / 16) % 4 == 0 ? 4 : 2, WM = 4 / WN;
     a.partials_per_image = a.tiles_x * a.tiles_y * (N / BN);
     dim3 grid(a.tiles_x * a.tiles_y * B, N / BN);
-    if (X6in)
+    if (X6in && a.w6 != nullptr)
+      hipLaunchKernelGGL((engine_kernel<N, N, BN, WM, WN, EPI_QUANT, true, true>), grid,
+                         dim3(256), 0, st, a);
+    else if (X6in)
       hipLaunchKernelGGL((engine_kernel<N, N, BN, WM, WN, EPI_QUANT, true>), grid,
                          dim3(256), 0, st, a);
     else
@@ -2821,6 +2865,30 @@ int iclr17_analysis_conv3_quant_rate_x6(const uint16_t* in_split, int B, int H, 
   io.in_plane = (long)B * h * w * N;
   io.out = (unsigned short*)y_hat_split;
   io.out_plane = (long)B * (h / 2) * (w / 2) * N;
+  return N == 192 ? launch_conv5<192, EPI_QUANT>(nullptr, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io, rate_table)
+                  : launch_conv5<128, EPI_QUANT>(nullptr, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io, rate_table);
+}
+
+int iclr17_analysis_conv3_quant_rate_x6w(const uint16_t* in_split, int B, int H, int W, int N,
+                                         const float* w_packed, const uint16_t* w_split,
+                                         int quant_mode, const float* noise,
+                                         const float* rate_packed, const float* rate_table,
+                                         float* y_out, float* y_hat, uint16_t* y_hat_split,
+                                         double* bits_partial, void* stream) {
+  int rc = check_dims(B, H, W, N);
+  if (rc) return rc;
+  ICLR17_REQUIRE(in_split && w_packed && w_split && rate_packed && y_hat && bits_partial,
+                 ICLR17_EINVAL, "conv3_quant_rate_x6w: null pointer");
+  ICLR17_REQUIRE(quant_mode == ICLR17_QUANT_ROUND || (quant_mode == ICLR17_QUANT_NOISE && noise),
+                 ICLR17_EINVAL, "conv3_quant_rate_x6w: bad quant mode %d / missing noise", quant_mode);
+  const int h = H / 8, w = W / 8;
+  SplitIO io;
+  io.in = (const unsigned short*)in_split;
+  io.in_plane = (long)B * h * w * N;
+  io.out = (unsigned short*)y_hat_split;
+  io.out_plane = (long)B * (h / 2) * (w / 2) * N;
+  io.w6 = (const unsigned short*)w_split;
+  io.w6_plane = 25L * N * N;
   return N == 192 ? launch_conv5<192, EPI_QUANT>(nullptr, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io, rate_table)
                   : launch_conv5<128, EPI_QUANT>(nullptr, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io, rate_table);
 }

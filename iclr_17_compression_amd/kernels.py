@@ -383,9 +383,10 @@ def conv2_gdn_x6(hs: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Ten
 
 def conv3_quant_rate_x6(hs: Tensor, wp: Tensor, rate_packed: Tensor,
                         noise: Optional[Tensor] = None, want_y: bool = False,
-                        rtab: Optional[Tensor] = None):
+                        rtab: Optional[Tensor] = None, w_split: Optional[Tensor] = None):
     """conv3_quant_rate on a split-form input. Returns (y_hat, bits_partial, y | None,
-    y_hat_split). rtab as ``conv3_quant_rate``."""
+    y_hat_split). rtab as ``conv3_quant_rate``. w_split (``split_packed(wp, 25, N, N)``, cached by
+    ``Analysis_net_17.packed_w3_split``): the weights pre-split, bit-identical results."""
     _check_split(hs, "activation")
     _, B, h8, w8, N = hs.shape
     _check_channels(N)
@@ -403,8 +404,13 @@ def conv3_quant_rate_x6(hs: Tensor, wp: Tensor, rate_packed: Tensor,
     y = torch.empty_like(y_hat) if want_y else None
     T = rate_partials_per_image(H, W, N)
     partial = torch.empty(B, T, device=hs.device, dtype=torch.float64)
-    call("iclr17_analysis_conv3_quant_rate_x6", _p(hs), B, H, W, N, _p(wp), mode, _p(noise),
-         _p(rate_packed), _p(rtab), _p(y), _p(y_hat), _p(y_hat_split), _p(partial), _stream(hs))
+    if w_split is not None:
+        call("iclr17_analysis_conv3_quant_rate_x6w", _p(hs), B, H, W, N, _p(wp), _p(w_split), mode,
+             _p(noise), _p(rate_packed), _p(rtab), _p(y), _p(y_hat), _p(y_hat_split), _p(partial),
+             _stream(hs))
+    else:
+        call("iclr17_analysis_conv3_quant_rate_x6", _p(hs), B, H, W, N, _p(wp), mode, _p(noise),
+             _p(rate_packed), _p(rtab), _p(y), _p(y_hat), _p(y_hat_split), _p(partial), _stream(hs))
     return y_hat, partial, y, y_hat_split
 
 

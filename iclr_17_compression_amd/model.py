@@ -105,7 +105,7 @@ class ImageCompressor(nn.Module):
             hs, _, _ = kernels.conv2_gdn_x6(hs, w2, self.Encoder.conv2.bias, *e2)
             rt = self.bitEstimator.rate_table() if noise is None else None
             q = kernels.conv3_quant_rate_x6(hs, w3, self.bitEstimator.packed(), noise, want_y=want_y,
-                                            rtab=rt)
+                                            rtab=rt, w_split=self.Encoder.packed_w3_split())
             y_split = q[3]
         else:
             h = kernels.conv1_gdn(x, w1, self.Encoder.conv1.bias, g1[0], g1[1], N)
@@ -255,6 +255,7 @@ class ImageCompressor(nn.Module):
             self.bitEstimator.packed()
             if x6:
                 self.Encoder.packed_conv1_x6()
+                self.Encoder.packed_w3_split()
                 self.Decoder.packed_x6()
                 if not backward:
                     self.Decoder.packed_x6k()

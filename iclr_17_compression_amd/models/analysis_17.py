@@ -48,6 +48,14 @@ class Analysis_net_17(nn.Module):
         g2 = self.gdn2.effective_params(force)
         return w1, w2, w3, g1, g2
 
+    def packed_w3_split(self, force: bool = False):
+        """conv3's packed weights pre-split into the x6 planes (kernels.split_packed), cached:
+        the x6 conv3 then reads its B operand as it is instead of splitting it per k-step."""
+        N = self.out_channel_N
+        w3 = self.packed(force)[2]
+        return self._pack.get("w3x6", (self.conv3.weight,),
+                              lambda: kernels.split_packed(w3, 25, N, N), force)
+
     def packed_conv1_x6(self, force: bool = False):
         """conv1's weights in the x6 kernel's split layout (kernels.pack_conv1_x6), cached."""
         N = self.out_channel_N
@@ -109,7 +117,8 @@ class Analysis_net_17(nn.Module):
         z = torch.zeros(11 * N, device=x.device)
         ztab = torch.zeros(N, 65, device=x.device)
         if feats is not None and kernels.precision() == "x6" and feats.get("a2s") is not None:
-            return kernels.conv3_quant_rate_x6(feats["a2s"], w3, z, want_y=True, rtab=ztab)[2]
+            return kernels.conv3_quant_rate_x6(feats["a2s"], w3, z, want_y=True, rtab=ztab,
+                                               w_split=self.packed_w3_split())[2]
         if feats is not None and kernels.precision() == "fp32":
             return kernels.conv3_quant_rate(feats["a2"], w3, z, want_y=True, rtab=ztab)[2]
         if kernels.precision() == "bf16":
@@ -122,7 +131,8 @@ class Analysis_net_17(nn.Module):
             e1, e2 = self.gdn1.effective_params_x6(), self.gdn2.effective_params_x6()
             hs, _, _ = kernels.conv1x6_gdn(x, self.packed_conv1_x6(), self.conv1.bias, e1[0], e1[2], N)
             hs, _, _ = kernels.conv2_gdn_x6(hs, w2, self.conv2.bias, *e2)
-            y = kernels.conv3_quant_rate_x6(hs, w3, z, want_y=True, rtab=ztab)[2]
+            y = kernels.conv3_quant_rate_x6(hs, w3, z, want_y=True, rtab=ztab,
+                                            w_split=self.packed_w3_split())[2]
         else:
             h = kernels.conv1_gdn(x, w1, self.conv1.bias, g1[0], g1[1], N)
             h = kernels.conv2_gdn(h, w2, self.conv2.bias, g2[0], g2[1])

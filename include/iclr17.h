@@ -187,6 +187,15 @@ int iclr17_analysis_conv3_quant_rate_x6(const uint16_t* in_split, int B, int H, 
                                         const float* rate_packed, const float* rate_table,
                                         float* y_out, float* y_hat, uint16_t* y_hat_split,
                                         double* bits_partial, void* stream);
+/* The same with the weights pre-split: w_split = iclr17_split_packed(w_packed, 25, N, N, …)
+ * ([3][25][N/8][N][8] bf16). Bit-identical to iclr17_analysis_conv3_quant_rate_x6 (the same
+ * split, done once per weight update instead of per k-step in the loop). */
+int iclr17_analysis_conv3_quant_rate_x6w(const uint16_t* in_split, int B, int H, int W, int N,
+                                         const float* w_packed, const uint16_t* w_split,
+                                         int quant_mode, const float* noise,
+                                         const float* rate_packed, const float* rate_table,
+                                         float* y_out, float* y_hat, uint16_t* y_hat_split,
+                                         double* bits_partial, void* stream);
 /* iclr17_synthesis_deconv_igdn on a split-form input. */
 int iclr17_synthesis_deconv_igdn_x6(const uint16_t* in_split, int B, int h, int w, int N,
                                     const float* w_packed, const float* bias,

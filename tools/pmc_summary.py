@@ -35,7 +35,7 @@ LAYER_KERNELS = {
     "x6": {
         "conv1_gdn1": (r"conv1_x6_kernel<192, 0>", None),
         "conv2_gdn2": (r"engine_kernel<192, 192, 192, 1, 4, 0, true>", None),
-        "conv3_quant_rate": (r"engine_kernel<192, 192, 96, 2, 2, 2, true>", None),
+        "conv3_quant_rate": (r"engine_kernel<192, 192, 96, 2, 2, 2, true", None),   # also the W6 form
         "deconv1_igdn1": (r"engine_kernel<192, 192, 192, 1, 4, 1, true>", 0),
         "deconv2_igdn2": (r"engine_kernel<192, 192, 192, 1, 4, 1, true>", 1),
         "deconv3_clamp": (r"deconv3_x6_kernel<192>", None),

@@ -10,7 +10,7 @@ j $S/kodak.json $P/r04_bench_kodak_g9.json
 j $S/kodak_2rank.json $P/r04_bench_kodak_g9_2rank_gloo_1gpu.json
 j $S/encdec_x6.json $P/r04_encdec_x6.json
 j $S/encdec_bf16.json $P/r04_encdec_bf16.json
-[ -f $S/bench_2048.json ] && j $S/bench_2048.json $P/r04_bench_2048.json
+[ -f $S/bench_2048_final.json ] && j $S/bench_2048_final.json $P/r04_bench_2048.json
 for f in $S/parity_*.json; do cp "$f" $P/r04_$(basename "$f"); done
 tail -3 $S/gpu_tests.log > $P/r04_gpu_tests.log
 for t in r04_x6 r04_bf16 r04_2048_x6 r04_2048_bf16; do

@@ -7,6 +7,7 @@ for t in r04_x6 r04_bf16 r04_2048_x6 r04_2048_bf16; do
 done
 timeout -k 10 300 python bench.py > $O/bench_final.json 2> $O/bench_final.err || { tail $O/bench_final.err; exit 1; }
 timeout -k 10 300 python bench.py --mode train --batch 32 > $O/bench_train32.json 2> $O/bench_train32.err || { tail $O/bench_train32.err; exit 1; }
+timeout -k 10 300 python bench.py --size 2048 --batch 8 > $O/bench_2048_final.json 2> $O/bench_2048_final.err || { tail $O/bench_2048_final.err; exit 1; }
 python - <<'PY'
 import json
 d=json.loads(open("gpurun_out/r04z/bench_final.json").read().strip().splitlines()[-1])

@@ -23,29 +23,31 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # bench.py layer → (kernel-name pattern, grid rank among that name's distinct grid sizes or None)
+# engine_kernel names are matched as prefixes: the trailing template arguments (the W6 flag)
+# differ by instantiation
 LAYER_KERNELS = {
     "fp32": {
         "conv1_gdn1": (r"conv1_gdn_kernel<192, 0, false>", None),
-        "conv2_gdn2": (r"engine_kernel<192, 192, 192, 1, 4, 0, false>", None),
-        "conv3_quant_rate": (r"engine_kernel<192, 192, 96, 2, 2, 2, false>", None),
-        "deconv1_igdn1": (r"engine_kernel<192, 192, 192, 1, 4, 1, false>", 0),
-        "deconv2_igdn2": (r"engine_kernel<192, 192, 192, 1, 4, 1, false>", 1),
-        "deconv3_clamp": (r"engine_kernel<192, 48, 48, 4, 1, 3, false>", None),
+        "conv2_gdn2": (r"engine_kernel<192, 192, 192, 1, 4, 0, false", None),
+        "conv3_quant_rate": (r"engine_kernel<192, 192, 96, 2, 2, 2, false", None),
+        "deconv1_igdn1": (r"engine_kernel<192, 192, 192, 1, 4, 1, false", 0),
+        "deconv2_igdn2": (r"engine_kernel<192, 192, 192, 1, 4, 1, false", 1),
+        "deconv3_clamp": (r"engine_kernel<192, 48, 48, 4, 1, 3, false", None),
     },
     "x6": {
         "conv1_gdn1": (r"conv1_x6_kernel<192, 0>", None),
-        "conv2_gdn2": (r"engine_kernel<192, 192, 192, 1, 4, 0, true>", None),
+        "conv2_gdn2": (r"engine_kernel<192, 192, 192, 1, 4, 0, true", None),
         "conv3_quant_rate": (r"engine_kernel<192, 192, 96, 2, 2, 2, true", None),   # also the W6 form
-        "deconv1_igdn1": (r"engine_kernel<192, 192, 192, 1, 4, 1, true>", 0),
-        "deconv2_igdn2": (r"engine_kernel<192, 192, 192, 1, 4, 1, true>", 1),
+        "deconv1_igdn1": (r"engine_kernel<192, 192, 192, 1, 4, 1, true", 0),
+        "deconv2_igdn2": (r"engine_kernel<192, 192, 192, 1, 4, 1, true", 1),
         "deconv3_clamp": (r"deconv3_x6_kernel<192>", None),
     },
     "bf16": {
         "conv1_gdn1": (r"conv1p_bf16_kernel<192, true>", None),
         "conv2_gdn2": (r"k5_bf16_kernel<0, 16, 192, 192, 192, 0>", None),
         "conv3_quant_rate": (r"k5_bf16_kernel<0, 8, 96, 192, 192, 2>", None),
-        "deconv1_igdn1": (r"k5_bf16_kernel<1, 8, 192, 192, 192, 1>", None),
-        "deconv2_igdn2": (r"k5_bf16_kernel<1, 16, 192, 192, 192, 1>", None),
+        "deconv1_igdn1": (r"k5_bf16_kernel<1, ", 0),   # 8-row tiles at 256², 16-row at 2048²
+        "deconv2_igdn2": (r"k5_bf16_kernel<1, ", 1),
         "deconv3_clamp": (r"deconv3_bf16_kernel<192>", None),
     },
 }

@@ -57,6 +57,7 @@ SIGNATURES = {
     "iclr17_analysis_conv3_quant_rate": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_analysis_conv3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P]),
     "iclr17_rate_partials_per_image": (_I, [_I, _I, _I]),
+    "iclr17_conv3_x6_partials_per_image": (_I, [_I, _I, _I, _I, _I]),
     "iclr17_synthesis_deconv_igdn": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_synthesis_deconv3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P]),
     "iclr17_synthesis_deconv3_x6": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P]),

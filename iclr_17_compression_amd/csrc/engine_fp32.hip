@@ -43,6 +43,15 @@ constexpr int BM = 64;        // output pixels per tile
 
 // conv3 (+ quantiser) output columns per workgroup: 96 at N = 192, 64 at N = 128
 constexpr int conv3_bn(int N) { return N % 96 == 0 ? 96 : 64; }
+// x6 conv3 in noise mode (training) on few tiles (B·tiles < 256: B=32 at 256² holds 256
+// workgroups, one wave per SIMD): 48-column tiles on 4×1 waves, twice the workgroups. The bit
+// partials per image follow (tiles × N/48): iclr17_conv3_x6_partials_per_image.
+#ifndef ICLR17_C3_NARROW
+#define ICLR17_C3_NARROW 1
+#endif
+inline bool conv3_narrow(int N, int tiles, int B, int qmode) {
+  return ICLR17_C3_NARROW && N == 192 && qmode == ICLR17_QUANT_NOISE && (long)tiles * B < 256;
+}
 
 enum Epi : int {
   EPI_GDN = 0, EPI_IGDN = 1, EPI_QUANT = 2, EPI_OUT3 = 3, EPI_PLAIN = 4,
@@ -2447,6 +2456,15 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
     constexpr int WN = (BN / 16) % 4 == 0 ? 4 : 2, WM = 4 / WN;
     a.partials_per_image = a.tiles_x * a.tiles_y * (N / BN);
     dim3 grid(a.tiles_x * a.tiles_y * B, N / BN);
+    if constexpr (N == 192) {
+      if (X6in && conv3_narrow(N, a.tiles_x * a.tiles_y, B, qmode)) {
+        a.partials_per_image = a.tiles_x * a.tiles_y * (N / 48);
+        a.w6 = nullptr;   // the narrow instantiation splits its weights per k-step
+        hipLaunchKernelGGL((engine_kernel<N, N, 48, 4, 1, EPI_QUANT, true>),
+                           dim3(a.tiles_x * a.tiles_y * B, N / 48), dim3(256), 0, st, a);
+        return check_launch("conv3_quant_rate (48-column tiles)");
+      }
+    }
     if (X6in && a.w6 != nullptr)
       hipLaunchKernelGGL((engine_kernel<N, N, BN, WM, WN, EPI_QUANT, true, true>), grid,
                          dim3(256), 0, st, a);
@@ -2599,6 +2617,11 @@ int iclr17_analysis_conv2_gdn(const float* in, int B, int H, int W, int N, const
   const int h = H / 4, w = W / 4;
   return N == 192 ? launch_conv5<192, EPI_GDN>(in, B, h, w, w_packed, bias, beta_eff, gamma_packed, out, pre_out, 0, nullptr, nullptr, nullptr, nullptr, S(stream))
                   : launch_conv5<128, EPI_GDN>(in, B, h, w, w_packed, bias, beta_eff, gamma_packed, out, pre_out, 0, nullptr, nullptr, nullptr, nullptr, S(stream));
+}
+
+int iclr17_conv3_x6_partials_per_image(int B, int H, int W, int N, int quant_mode) {
+  const int gh = H / 16, gw = W / 16, tiles = ((gh + 7) / 8) * ((gw + 7) / 8);
+  return tiles * (conv3_narrow(N, tiles, B, quant_mode) ? N / 48 : N / conv3_bn(N));
 }
 
 int iclr17_rate_partials_per_image(int H, int W, int N) {

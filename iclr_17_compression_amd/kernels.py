@@ -402,7 +402,7 @@ def conv3_quant_rate_x6(hs: Tensor, wp: Tensor, rate_packed: Tensor,
     y_hat = torch.empty(B, h8 // 2, w8 // 2, N, device=hs.device, dtype=torch.float32)
     y_hat_split = torch.empty(3, B, h8 // 2, w8 // 2, N, device=hs.device, dtype=torch.int16)
     y = torch.empty_like(y_hat) if want_y else None
-    T = rate_partials_per_image(H, W, N)
+    T = query("iclr17_conv3_x6_partials_per_image", B, H, W, N, mode)
     partial = torch.empty(B, T, device=hs.device, dtype=torch.float64)
     if w_split is not None:
         call("iclr17_analysis_conv3_quant_rate_x6w", _p(hs), B, H, W, N, _p(wp), _p(w_split), mode,

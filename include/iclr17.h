@@ -126,6 +126,10 @@ int iclr17_analysis_conv3_quant_rate(const float* in, int B, int H, int W, int N
                                      float* y_out, float* y_hat, double* bits_partial,
                                      void* stream);
 int iclr17_rate_partials_per_image(int H, int W, int N);
+/* Bit partials per image of the x6 conv3 entries (…_x6, …_x6w): as above, except that in noise
+ * mode on fewer than 256 tiles·images (training at B=32, 256²) the kernel runs 48-column tiles
+ * and writes tiles × N/48 partials. */
+int iclr17_conv3_x6_partials_per_image(int B, int H, int W, int N, int quant_mode);
 /* analysis_17.py:22,35 alone (Analysis_net_17.forward without the quantiser): y NHWC. */
 int iclr17_analysis_conv3(const float* in, int B, int H, int W, int N, const float* w_packed,
                           float* y_out, void* stream);

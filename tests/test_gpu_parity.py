@@ -613,6 +613,30 @@ def test_x6k_deconv_igdn(device, N, hw):
                 assert torch.equal(fbi, fb) and not torch.equal(fb, f)
 
 
+@pytest.mark.parametrize("N,B,hw", [(192, 3, (48, 80)), (128, 2, (32, 32)), (192, 40, (32, 32))])
+def test_conv3_x6_presplit_weights(device, N, B, hw):
+    """x6 conv3 reading its weights pre-split (iclr17_analysis_conv3_quant_rate_x6w, split_packed
+    once) equals the per-k-step split bit for bit — ŷ, y, the split ŷ and the bit partials — in
+    round mode and in noise mode (48-column tiles below 256 tiles·images, 4 partials per tile;
+    B=40 stays on them, N=128 never does); and its y agrees with the oracle's conv3."""
+    net = net_for(N, 1, device)
+    enc = net.Encoder
+    w3, w3s = enc.packed()[2], enc.packed_w3_split()
+    rate, rtab = net.bitEstimator.packed(), net.bitEstimator.rate_table()
+    h, w = hw
+    a2 = torch.from_numpy(synth.normal_like(21, (B, h, w, N), 0.7))
+    hs = kernels.split_planes(a2.to(device))
+    noise = torch.from_numpy(synth.uniform(22, (B, N, h // 2, w // 2), -0.5, 0.5)).to(device)
+    for nz in (None, noise):
+        kw = dict(want_y=True, rtab=rtab if nz is None else None)
+        a = kernels.conv3_quant_rate_x6(hs, w3, rate, nz, **kw)
+        b = kernels.conv3_quant_rate_x6(hs, w3, rate, nz, w_split=w3s, **kw)
+        assert all(torch.equal(x, y) for x, y in zip(a, b))
+    r_y = torch.nn.functional.conv2d(a2.permute(0, 3, 1, 2), sd_for(N, 1)["Encoder.conv3.weight"], None,
+                                     stride=2, padding=2)
+    assert rel_err(b[2].permute(0, 3, 1, 2).cpu(), r_y) < REL
+
+
 @pytest.mark.parametrize("T", [4, 8, 100])
 def test_deconv3_bits_fold(device, T):
     """bpp's reduction folded into deconv3 (x6 chunk-major and bf16 kernels, workgroup 0) equals

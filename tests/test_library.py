@@ -39,6 +39,12 @@ def test_version_and_size_queries():
     assert _lib.query("iclr17_rate_partials_per_image", 256, 256, 128) == 4 * 2   # 64-column tiles
     assert _lib.query("iclr17_output_partials_per_image", 256, 256) == 64
     assert _lib.query("iclr17_rate_bits_partials", 192, 16, 16) == 12
+    # x6 conv3: noise mode on < 256 tiles·images runs 48-column tiles (4 partials per tile)
+    R, Q = _lib.ICLR17_QUANT_ROUND, _lib.ICLR17_QUANT_NOISE
+    assert _lib.query("iclr17_conv3_x6_partials_per_image", 32, 256, 256, 192, R) == 4 * 2
+    assert _lib.query("iclr17_conv3_x6_partials_per_image", 32, 256, 256, 192, Q) == 4 * 4
+    assert _lib.query("iclr17_conv3_x6_partials_per_image", 64, 256, 256, 192, Q) == 4 * 2
+    assert _lib.query("iclr17_conv3_x6_partials_per_image", 2, 256, 256, 128, Q) == 4 * 2
 
 
 def test_argument_validation_without_gpu():

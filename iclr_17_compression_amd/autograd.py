@@ -12,11 +12,16 @@
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Sequence
 
 import torch
 
 from . import kernels
+
+# diagnostic: training conv3 on pre-split weights (ICLR17_TRAIN_W6=1; the 48-column tiles use them
+# only in a -DICLR17_C3N_W6=1 build, DESIGN.md §4: measured, not adopted)
+_TRAIN_W6 = os.environ.get("ICLR17_TRAIN_W6", "0") == "1"
 
 Tensor = torch.Tensor
 
@@ -358,7 +363,8 @@ class CodecTrainFn(torch.autograd.Function):
         rate = be.packed()
         a2s = saved_a.get("a2s")
         if a2s is not None:
-            y_tilde, bits_part, _, y_split = kernels.conv3_quant_rate_x6(a2s, w3, rate, noise)
+            w3s = enc.packed_w3_split() if _TRAIN_W6 else None
+            y_tilde, bits_part, _, y_split = kernels.conv3_quant_rate_x6(a2s, w3, rate, noise, w_split=w3s)
         else:
             (y_tilde, bits_part), y_split = kernels.conv3_quant_rate(a2, w3, rate, noise), None
         clipped, recon, sse_part, saved_s = synthesis_forward_train(dec, y_tilde, x_ref=x,

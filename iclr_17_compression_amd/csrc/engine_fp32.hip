@@ -49,6 +49,13 @@ constexpr int conv3_bn(int N) { return N % 96 == 0 ? 96 : 64; }
 #ifndef ICLR17_C3_NARROW
 #define ICLR17_C3_NARROW 1
 #endif
+#ifndef ICLR17_C3N_W6
+#define ICLR17_C3N_W6 0
+#endif
+// diagnostic build: the narrow conv3 in XCD-contiguous work order (decode_tile_xcd)
+#ifndef ICLR17_C3N_XCD
+#define ICLR17_C3N_XCD 0
+#endif
 inline bool conv3_narrow(int N, int tiles, int B, int qmode) {
   return ICLR17_C3_NARROW && N == 192 && qmode == ICLR17_QUANT_NOISE && (long)tiles * B < 256;
 }
@@ -192,6 +199,30 @@ __device__ __forceinline__ TileInfo decode_tile(const EngineArgs& a) {
   t.nb = blockIdx.y;
   return t;
 }
+
+#if ICLR17_C3N_XCD
+// XCD-contiguous work order (diagnostic build, one-phase grids): dispatch slot L (x fastest) runs
+// on XCD L % 8, so work item (L % 8)·G/8 + L/8 gives each XCD one contiguous range — with the
+// column block fastest, whole images per XCD, whose input then crosses that XCD's L2 once
+// instead of once per XCD.
+template <int TH = 8>
+__device__ __forceinline__ TileInfo decode_tile_xcd(const EngineArgs& a) {
+  const int G = gridDim.x * gridDim.y;
+  int L = blockIdx.x + gridDim.x * blockIdx.y;
+  if (G % 8 == 0) L = (L % 8) * (G / 8) + L / 8;
+  TileInfo t;
+  t.th = TH;
+  int bid = L / gridDim.y;
+  t.tx = bid % a.tiles_x;
+  bid /= a.tiles_x;
+  t.ty = bid % a.tiles_y;
+  t.b = bid / a.tiles_y;
+  t.py = 0;
+  t.px = 0;
+  t.nb = L % gridDim.y;
+  return t;
+}
+#endif
 
 // Row m of a tile → output pixel (NHWC row offset in pixels) or -1 when outside the grid.
 __device__ __forceinline__ long out_pixel(const EngineArgs& a, const TileInfo& t, int m) {
@@ -1029,7 +1060,12 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (scalar branches)
   const int wm = wave / WN, wn = wave % WN;
+#if ICLR17_C3N_XCD
+  constexpr bool XCDW = X6 && EPI == EPI_QUANT && BN == 48;
+  TileInfo t = XCDW ? decode_tile_xcd<BMT / 8>(a) : decode_tile<BMT / 8>(a);
+#else
   TileInfo t = decode_tile<BMT / 8>(a);
+#endif
   const int ph = t.py * a.tt.npx + t.px;
   const int ncol0 = t.nb * BN + wn * (BN / WN);
 
@@ -2459,6 +2495,13 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
     if constexpr (N == 192) {
       if (X6in && conv3_narrow(N, a.tiles_x * a.tiles_y, B, qmode)) {
         a.partials_per_image = a.tiles_x * a.tiles_y * (N / 48);
+#if ICLR17_C3N_W6   // diagnostic build: the narrow tiles on pre-split weights (not adopted)
+        if (a.w6 != nullptr) {
+          hipLaunchKernelGGL((engine_kernel<N, N, 48, 4, 1, EPI_QUANT, true, true>),
+                             dim3(a.tiles_x * a.tiles_y * B, N / 48), dim3(256), 0, st, a);
+          return check_launch("conv3_quant_rate (48-column tiles)");
+        }
+#endif
         a.w6 = nullptr;   // the narrow instantiation splits its weights per k-step
         hipLaunchKernelGGL((engine_kernel<N, N, 48, 4, 1, EPI_QUANT, true>),
                            dim3(a.tiles_x * a.tiles_y * B, N / 48), dim3(256), 0, st, a);

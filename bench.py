@@ -36,6 +36,31 @@ BF16_MFMA_PEAK_TFLOPS = 2516.6  # 256 CU x 4 SIMD x 1024 FLOP/clk (16x16x32 bf16
 X6_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6   # fp32-equivalent: 6 bf16 part products per MAC
 X6_LAYERS = ("conv1_gdn1", "conv2_gdn2", "conv3_quant_rate", "deconv1_igdn1", "deconv2_igdn2",
              "deconv3_clamp")   # every contraction of the x6 eval chain
+H3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3   # fp32-equivalent: 3 fp16 part products per MAC
+# the layers of the h3 eval chain whose main contraction runs in the h3 form (the others in x6)
+H3_LAYERS = ("conv2_gdn2", "conv3_quant_rate", "deconv1_igdn1", "deconv2_igdn2")
+
+
+PRECISION_NOTE = {
+    "h3": ("h3: fp32 operands as two fp16 parts (22 significant bits, power-of-two scaled), 3 part "
+           "products per MAC on v_mfma_f32_*_f16 with fp32 accumulate for conv2, conv3, deconv1 and "
+           "deconv2; x6 for conv1, deconv3 and the GDN contractions"),
+    "x6": ("x6: fp32 operands split exactly into 3 bf16 parts, 6 part products on "
+           "v_mfma_f32_16x16x32_bf16, fp32 accumulate (every contraction)"),
+    "bf16": "bf16: bf16 activations and weights, one bf16 product per MAC, fp32 accumulate and epilogues",
+    "fp32": "fp32 (exact-f32 MFMA products)",
+}
+
+
+def layer_peak(prec: str, k: str):
+    """(peak TFLOP/s, basis) of layer k's main contraction in precision mode prec."""
+    if prec == "bf16":
+        return BF16_MFMA_PEAK_TFLOPS, "bf16 dense MFMA peak (one bf16 product per MAC)"
+    if prec == "h3" and k in H3_LAYERS:
+        return H3_PEAK_TFLOPS, "bf16/f16 dense MFMA peak / 3 (h3: three fp16 part products per fp32 MAC)"
+    if prec in ("x6", "h3") and k in X6_LAYERS:
+        return X6_PEAK_TFLOPS, "bf16 dense MFMA peak / 6 (bf16x6: six bf16 part products per fp32 MAC)"
+    return FP32_MFMA_PEAK_TFLOPS, "fp32 MFMA dense peak (exact-f32 products)"
 HBM_PEAK_GBS = 8000.0
 # deconv2 → deconv3 through the chunk-major split form (ICLR17_D3_CM=0: the NHWC split, for A/B)
 D3_CM = os.environ.get("ICLR17_D3_CM", "1") != "0"
@@ -90,7 +115,8 @@ class Step:
         self.enc = net.Encoder.packed()
         self.dec = net.Decoder.packed()
         self.d3x6 = net.Decoder.packed_x6()
-        self.dx6k = net.Decoder.packed_x6k()
+        self.dh3 = net.Decoder.packed_h3k()
+        self.eh3 = net.Encoder.packed_h3()
         self.rate = net.bitEstimator.packed()
         gdns = (net.Encoder.gdn1, net.Encoder.gdn2, net.Decoder.igdn1, net.Decoder.igdn2)
         self.w1x6 = net.Encoder.packed_conv1_x6()
@@ -138,6 +164,29 @@ class Step:
             else:
                 clipped, _, _ = kernels.deconv3_bf16(h, d3b, net.Decoder.deconv3.bias)
                 bpp = None
+        elif kernels.precision() == "h3":
+            # ImageCompressor.forward in the h3 form: conv1 (x6 contractions, h3 output), conv2 /
+            # conv3 / deconv1 / deconv2 on three fp16 part products per MAC, deconv3 in x6
+            e1, e2, e3, e4 = self.g6
+            (w2h, w3h), (x1, x2) = self.eh3, self.dh3
+            hs, _ = kernels.conv1x6_gdn_h3(self.x, self.w1x6, net.Encoder.conv1.bias, e1[0], e1[2], N)
+            ev(1)
+            yield
+            hs, _, _ = kernels.conv2_gdn_h3(hs, w2h, net.Encoder.conv2.bias, e2[0], e2[2])
+            ev(2)
+            yield
+            y_hat, partial, _, yh = kernels.conv3_quant_rate_h3(hs, w3h, self.rate, rtab=self.rtab)
+            ev(3)
+            yield
+            hs, _, _ = kernels.deconv_igdn_h3(yh, x1, net.Decoder.deconv1.bias, e3[0], e3[2], int_in=True)
+            ev(4)
+            yield
+            _, _, hs = kernels.deconv_igdn_h3(hs, x2, net.Decoder.deconv2.bias, e4[0], e4[2],
+                                              want_h3=False, want_x6=True, chunk_major=True)
+            ev(5)
+            yield
+            clipped, _, _, bpp = kernels.deconv3_x6(hs, self.d3x6, net.Decoder.deconv3.bias,
+                                                    bits=(partial, self.scale))
         elif kernels.precision() == "x6":
             e1, e2, e3, e4 = self.g6
             hs, _, _ = kernels.conv1x6_gdn(self.x, self.w1x6, net.Encoder.conv1.bias, e1[0], e1[2],
@@ -151,19 +200,11 @@ class Step:
                                                                 w_split=self.w3s)
             ev(3)
             yield
-            # Synthesis_net_17.decode's x6 path (ICLR17_X6K=1: deconv1 / deconv2 on the x6k engine)
-            x1, x2 = self.dx6k
-            if kernels.X6K:   # deconv1 on ŷ in the x6k engine's integer-input form (A/B)
-                hs, _ = kernels.deconv_igdn_x6k(ys, x1, net.Decoder.deconv1.bias, e3[0], e3[2], int_in=True)
-            else:
-                hs, _, _ = kernels.deconv_igdn_x6(ys, d1, net.Decoder.deconv1.bias, *e3)
+            # Synthesis_net_17.decode's x6 path
+            hs, _, _ = kernels.deconv_igdn_x6(ys, d1, net.Decoder.deconv1.bias, *e3)
             ev(4)
             yield
-            if kernels.X6K:
-                hs, _ = kernels.deconv_igdn_x6k(hs, x2, net.Decoder.deconv2.bias, e4[0], e4[2],
-                                                chunk_major=D3_CM)
-            else:
-                hs, _, _ = kernels.deconv_igdn_x6(hs, d2, net.Decoder.deconv2.bias, *e4, chunk_major=D3_CM)
+            hs, _, _ = kernels.deconv_igdn_x6(hs, d2, net.Decoder.deconv2.bias, *e4, chunk_major=D3_CM)
             ev(5)
             yield
             if D3_CM and FOLD_BITS:
@@ -320,7 +361,7 @@ def run_train(args, net, x, world, dev):
         data_info["step_crops_per_s"] = round(B * args.steps / elapsed, 1)
     flops = train_flops(args.N, S, S) * B
     tflops = flops / (ms * 1e-3) / 1e12
-    x6t = kernels.precision() == "x6"
+    x6t = kernels.precision() in ("x6", "h3")   # training runs the x6 kernels in both
     tpeak = X6_PEAK_TFLOPS if x6t else FP32_MFMA_PEAK_TFLOPS
     return {
         "metric": "Mpixels/s training (fwd+bwd+Adam), " + METRIC,
@@ -333,7 +374,7 @@ def run_train(args, net, x, world, dev):
                    "N": args.N, "batch_per_gpu": B, "global_batch": B * world,
                    "precision": ("x6: forward, input gradients, weight gradients and GDN γ "
                                  "gradients (bias/β/rate-parameter sums and Adam in fp32)"
-                                 if kernels.precision() == "x6" else "exact-f32"),
+                                 if x6t else "exact-f32"),
                    "parallelism": f"dp{world} ({'RCCL' if os.environ.get('ICLR17_DIST_BACKEND', 'nccl') == 'nccl' else 'gloo'} "
                                   "bucketed grad all-reduce overlapped with the backward)"},
         "roofline": {"bound": "mfma", "kernel": "whole training step", "achieved": round(tflops, 2),
@@ -595,7 +636,9 @@ def run_codec(args, dev):
         y = kernels.rans_decode(words, offsets, cum, B, h, w, N)
         e2.record()
         split = kernels.split_planes(y) if kernels.precision() == "x6" else None
-        clipped, _, _ = net.Decoder.decode(y, want_recon=False, y_split=split, y_integral=True)
+        yh3 = kernels.h3_planes(y) if kernels.precision() == "h3" else None
+        clipped, _, _ = net.Decoder.decode(y, want_recon=False, y_split=split, y_integral=True,
+                                           y_h3=yh3)
         if timed:
             t_enc.append((e0, e1))
             t_dec.append((e1, e2))
@@ -858,27 +901,23 @@ def roofline(per_layer_ms: dict, prec: str, N: int, S: int, B: int):
                   "tflops": round(flops[k] * B / (per_layer_ms[k] * 1e-3) / 1e12, 2) if flops[k] else None,
                   "gbs": round(bytes_[k] * B / (per_layer_ms[k] * 1e-3) / 1e9, 1) if bytes_[k] else None}
               for k in LAYERS}
-    if prec == "bf16":
-        peak, note = BF16_MFMA_PEAK_TFLOPS, "bf16 dense MFMA peak (one bf16 product per MAC)"
-    elif prec == "x6" and dominant in X6_LAYERS:
-        peak, note = X6_PEAK_TFLOPS, "bf16 dense MFMA peak / 6 (bf16x6: six bf16 part products per fp32 MAC)"
-    else:
-        peak, note = FP32_MFMA_PEAK_TFLOPS, "fp32 MFMA dense peak (exact-f32 products)"
+    peak, note = layer_peak(prec, dominant)
     prof = profile_layers(N, S, B, prec)
     for k in LAYERS:
         if flops[k]:
-            layers[k]["frac"] = round(flops[k] * B / (per_layer_ms[k] * 1e-3) / 1e12 / peak, 4)
+            pk = layer_peak(prec, k)[0]
+            layers[k]["peak"] = round(pk, 1)
+            layers[k]["frac"] = round(flops[k] * B / (per_layer_ms[k] * 1e-3) / 1e12 / pk, 4)
             if prof.get(k):   # the same fraction from the SHA-matched rocprof trace mean
                 layers[k]["profile_mean_ms"] = round(prof[k], 4)
-                layers[k]["frac_from_profile"] = round(flops[k] * B / (prof[k] * 1e-3) / 1e12 / peak, 4)
+                layers[k]["frac_from_profile"] = round(flops[k] * B / (prof[k] * 1e-3) / 1e12 / pk, 4)
     # per-layer T_roof = max(F / P_peak, bytes / BW_peak) and the whole chain's
     # Σ T_roof / Σ T_measured (P_peak the mode's MFMA peak, BW_peak the HBM peak)
     t_roof = {}
     for k in LAYERS:
         if not flops[k]:
             continue
-        p = BF16_MFMA_PEAK_TFLOPS if prec == "bf16" else (
-            X6_PEAK_TFLOPS if prec == "x6" and k in X6_LAYERS else FP32_MFMA_PEAK_TFLOPS)
+        p = layer_peak(prec, k)[0]
         t_mfma = flops[k] * B / (p * 1e12) * 1e3
         t_hbm = bytes_[k] * B / (HBM_PEAK_GBS * 1e9) * 1e3
         t_roof[k] = max(t_mfma, t_hbm)
@@ -1096,7 +1135,7 @@ def main() -> None:
         return
     prec = kernels.precision()
     rb = None
-    if prec == "x6" and not args.no_bf16_leg:
+    if prec in ("x6", "h3") and not args.no_bf16_leg:
         # the bf16 throughput-mode leg runs first (reported as bf16_mode below). Its step is 4x
         # shorter and the GPU clock ramps over the first ~50 ms of load (tools/warm_probe.py:
         # bf16 0.567 → 0.465 ms, x6 2.49 → 2.06 ms per step), so it warms for at least 100 steps
@@ -1115,7 +1154,6 @@ def main() -> None:
     pixels = world * B * S * S * args.steps
     value = pixels / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
-    x6 = prec == "x6"
     flops = layer_flops(N, S, S)
     bytes_ = layer_bytes(N, S, S, 2 if prec == "bf16" else 4)
     dominant, layers, roof = roofline(per_layer_ms, prec, N, S, B)
@@ -1139,11 +1177,7 @@ def main() -> None:
                                 + f", N={N}"),
                    "N": N, "image": f"{S}x{S}x3", "batch_per_gpu": B, "global_batch": B * world,
                    "quant": "round",
-                   "precision": ("x6: fp32 operands split exactly into 3 bf16 parts, 6 part products "
-                                 "on v_mfma_f32_16x16x32_bf16, fp32 accumulate (every contraction)")
-                                if x6 else ("bf16: bf16 activations and weights, one bf16 product "
-                                            "per MAC, fp32 accumulate and epilogues" if prec == "bf16"
-                                            else "fp32 (exact-f32 MFMA products)"),
+                   "precision": PRECISION_NOTE[prec],
                    "parallelism": f"dp{world} (images sharded by rank, no data-path collective)",
                    "launch": ("hipGraph replay of the whole step" if args.graph else
                               "eager (kernel by kernel)" + (f", batch split over {nstreams} HIP streams"
@@ -1156,7 +1190,7 @@ def main() -> None:
     }
     if rb is not None:
         # the bf16 throughput mode on the same batch: rate, roofline, and its deviation from the
-        # x6 (fp32-exact) results — latent flips, Δbpp, ΔPSNR
+        # parity mode's (fp32-accurate) results — latent flips, Δbpp, ΔPSNR
         dom_b, layers_b, roof_b = roofline(rb["per_layer_ms"], "bf16", N, S, B)
         flips = int((rb["y_hat"] != r["y_hat"]).sum().item())
 
@@ -1173,7 +1207,7 @@ def main() -> None:
                                                   "chain_roofline_frac")
                          if k in roof_b},
             "layers": layers_b,
-            "vs_x6": {"latent_flip_rate": flips / r["y_hat"].numel(),
+            "vs_parity_mode": {"parity_mode": prec, "latent_flip_rate": flips / r["y_hat"].numel(),
                       "max_abs_dbpp_per_image": float((rb["bpp_img"] - r["bpp_img"]).abs().max()),
                       "max_abs_dpsnr_db_per_image": float((psnr(rb["clipped"]) - psnr(r["clipped"])).abs().max())},
         }

@@ -33,8 +33,8 @@ ICLR17_PACK_RATE = 17
 ICLR17_PACK_SPLIT = 18
 ICLR17_BF_CONV5 = 32
 ICLR17_BF_DECONV5 = 33
-ICLR17_X6K_CONV5 = 40
-ICLR17_X6K_DECONV5 = 41
+ICLR17_H3K_CONV5 = 42
+ICLR17_H3K_DECONV5 = 43
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -125,11 +125,18 @@ SIGNATURES = {
     "iclr17_bias_grad_nhwc": (_I, [_P, ctypes.c_long, _I, _P, _P, _P]),
     "iclr17_bias_grad_nchw": (_I, [_P, _I, _I, ctypes.c_long, _P, _P, _P]),
     "iclr17_rate_param_grad": (_I, [_P, _I, _I] + [_P] * 7 + [_P] * 11 + [_P]),
-    # x6 k5 engine on the 32x32x16 MFMA (csrc/engine_x6k.hip)
-    "iclr17_x6k_weight_size": (_SZ, [_I, _I]),
-    "iclr17_pack_x6k": (_I, [_I, _P, _P, _I, _P]),
-    "iclr17_synthesis_deconv_igdn_x6k": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _I,
-                                              _P]),
+    # h3 form, k5 layers on the 32x32x16 f16 MFMA (csrc/engine_h3.hip)
+    "iclr17_h3k_weight_size": (_SZ, [_I, _I]),
+    "iclr17_pack_h3k": (_I, [_I, _P, _P, _I, _P]),
+    "iclr17_h3_planes": (_I, [_P, ctypes.c_long, _P, _P, _P]),
+    "iclr17_split_packed_h3_size": (_SZ, [_I, _I, _I]),
+    "iclr17_split_packed_h3": (_I, [_P, _I, _I, _I, _P, _P]),
+    "iclr17_analysis_conv1x6_gdn_h3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_analysis_conv2_gdn_h3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_analysis_conv3_quant_rate_h3": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P,
+                                                 _P, _P, _P, _P]),
+    "iclr17_synthesis_deconv_igdn_h3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I,
+                                             _I, _P, _P]),
     # bf16 throughput mode (csrc/engine_bf16.hip)
     "iclr17_bf16_weight_size": (_SZ, [_I, _I]),
     "iclr17_pack_bf16": (_I, [_I, _P, _P, _I, _P]),

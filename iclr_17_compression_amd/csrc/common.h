@@ -176,6 +176,57 @@ __device__ __forceinline__ void split_packed_group(const float* __restrict__ w, 
   *(u4*)(planes + 2 * plane + g * 8) = lo;
 }
 
+// ----------------------------------------------------------------------------- h3 form
+// The h3 operand form: three fp16 part products per MAC on the f16 MFMA instead of the x6 mode's
+// six bf16 ones. An activation x is stored as two fp16 planes of a = x·σ_a (σ_a = 2^kH3SaLog2):
+//   hi = rne16(a),  lo = rne16((a − hi)·2¹¹)      (22 significant bits; a − hi is exact in fp32)
+// a weight w the same way with its own power-of-two σ_w (max|w|·σ_w ∈ [8, 16), chosen per tensor
+// at packing), and a product as
+//   2¹¹·a·v ≈ (hi_w·2¹¹)·hi_a + lo_w·hi_a + hi_w·lo_a                 (lo·lo, < 2⁻²², dropped)
+// accumulated in fp32 and scaled back by 2⁻¹¹/(σ_a·σ_w), a power of two. The lo plane keeps 11
+// more binades below hi, so values down to 2⁻¹³/σ_a keep all 22 bits and smaller ones an absolute
+// error below 2⁻³⁶/σ_a; a ≥ 65520 (|x| ≥ 2^22 at σ_a = 2⁻⁶) does not fit and is reported through
+// the caller's range flag. The f16 MFMA keeps fp16 subnormal operands (tools/h3_numerics.hip) and
+// runs at the bf16 rate; against float64 a K = 1728 / 4800 dot product lands at 0.7× the x6 chain's
+// rms error (fewer roundings of the running sum; profiles/r05_h3_numerics.txt).
+constexpr int kH3SaLog2 = -6;
+constexpr float kH3Sa = 1.0f / 64.0f;
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ unsigned short h16_bits(_Float16 v) {
+  return __builtin_bit_cast(unsigned short, v);
+}
+
+// x → (hi, lo) of a = x·σ_a; ovf |= a does not fit (finite and ≥ 65520 in magnitude)
+__device__ __forceinline__ void h3_split1(float x, unsigned short& hi, unsigned short& lo,
+                                          bool& ovf) {
+  const float a = x * kH3Sa;
+  const _Float16 h = (_Float16)a;
+  const _Float16 l = (_Float16)((a - (float)h) * 2048.0f);
+  hi = h16_bits(h);
+  lo = h16_bits(l);
+  ovf |= fabsf(a) >= 65520.0f && fabsf(a) <= 3.40282347e38f;
+}
+
+// 4 consecutive values → 8 bytes of each plane
+__device__ __forceinline__ void h3_split4(const f4& x, uint2& hi, uint2& lo, bool& ovf) {
+  unsigned short h[4], l[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) h3_split1(x[j], h[j], l[j], ovf);
+  hi = uint2{h[0] | ((unsigned)h[1] << 16), h[2] | ((unsigned)h[3] << 16)};
+  lo = uint2{l[0] | ((unsigned)l[1] << 16), l[2] | ((unsigned)l[3] << 16)};
+}
+
+// 8 fp16 values × 2¹¹ (exact while they stay below 32: the weight scaling guarantees it)
+// (one 8-wide vector multiply: the per-dword form of this compiled to one v_pk_mul_f16 whose
+// result was copied into all four dwords)
+__device__ __forceinline__ u4 h3_x2048(const u4& v) {
+  const h8v k = {(_Float16)2048.0f, (_Float16)2048.0f, (_Float16)2048.0f, (_Float16)2048.0f,
+                 (_Float16)2048.0f, (_Float16)2048.0f, (_Float16)2048.0f, (_Float16)2048.0f};
+  return __builtin_bit_cast(u4, __builtin_bit_cast(h8v, v) * k);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);

@@ -35,55 +35,16 @@
 namespace iclr17 {
 namespace bfm {
 
-#ifndef ICLR17_BF_DECONV16
-#define ICLR17_BF_DECONV16 1
-#endif
-#ifndef ICLR17_BF_C3KS
-#define ICLR17_BF_C3KS 2   // conv3: input-channel halves per tile, one 4-wave group each
-#endif
-#ifndef ICLR17_C1P_KBO
-#define ICLR17_C1P_KBO 1   // conv1p: GDN contraction k-block outer (x² fragments read once)
-#endif
-#ifndef ICLR17_BF_DIRECT_Y
-#define ICLR17_BF_DIRECT_Y 1   // k5 GDN epilogue: per-wave y stores (K5::DIRECT_Y)
-#endif
-#ifndef ICLR17_BF_PAIR
-#define ICLR17_BF_PAIR 0   // deconv1 (8-row tiles): phase order 0, 1, 3, 2 (A/B)
-#endif
-#ifndef ICLR17_K5_STAMPS
-#define ICLR17_K5_STAMPS 0
-#endif
-#ifndef ICLR17_C1P_STAMPS
-#define ICLR17_C1P_STAMPS 0   // diagnostic build: per-phase s_memtime stamps of conv1p
-#endif
-#ifndef ICLR17_BF_PERSIST
-#define ICLR17_BF_PERSIST 0   // deconv (16-row tiles): persistent workgroups (k5p_bf16_kernel; A/B: no gain)
-#endif
-#ifndef ICLR17_BF_RTAB_LDS
-#define ICLR17_BF_RTAB_LDS 1   // conv3: the rate table rows of the tile in LDS (not L2 gathers)
-#endif
-#ifndef ICLR17_BF_C3ST
-#define ICLR17_BF_C3ST 1   // conv3: ŷ stored from an LDS tile as contiguous pixel rows (QST)
-#endif
-#ifndef ICLR17_BF_NST
-#define ICLR17_BF_NST 4   // weight ring stages (F + 2 for F DMA groups in flight)
-#endif
-
-#if ICLR17_K5_STAMPS
-// diagnostic build: per-wave s_memtime at k5_body entry, main-loop start, main-loop end, exit
-__device__ unsigned long long g_k5_stamps[8192 * 16 * 8];
-#endif
+constexpr int kC3KS = 2;   // conv3: input-channel halves per tile, one 4-wave group each
+constexpr int kNST = 4;    // weight ring stages (F + 2 for F DMA groups in flight)
 __device__ __attribute__((aligned(16))) unsigned g_zero16[4] = {0u, 0u, 0u, 0u};
 
-#ifndef ICLR17_BF_SINK4
-#define ICLR17_BF_SINK4 1
-#endif
 // A padding ("sink") load of the counted-vmcnt DMA schedule: one vector-memory instruction like
 // any other, but 4 bytes per lane (256 B into the sink) instead of a 16-byte piece (1 KB)
 __device__ __forceinline__ void sink_load(void* lds_sink) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g_zero16,
                                    (__attribute__((address_space(3))) void*)lds_sink,
-                                   ICLR17_BF_SINK4 ? 4 : 16, 0, 0);
+                                   4, 0, 0);
 }
 
 enum BEpi : int { BE_GDN = 0, BE_IGDN = 1, BE_QUANT = 2 };
@@ -146,11 +107,11 @@ constexpr int epi_tile_bytes(int R) { return R * (CO * 2 + 32); }
 // weight ring (the groups' barriers line up: equal step counts), then group 0 adds the other
 // groups' accumulators from LDS in a fixed order and runs the epilogue. conv3's 256 tiles at B=64
 // otherwise hold one wave per SIMD.
-constexpr int k5_threads(int TH, int EPI) { return TH / 2 * 64 * (EPI == BE_QUANT ? ICLR17_BF_C3KS : 1); }
+constexpr int k5_threads(int TH, int EPI) { return TH / 2 * 64 * (EPI == BE_QUANT ? kC3KS : 1); }
 
-template <int MODE, int TH, int NB, int CO, int CI, int EPI, bool PERSIST = false>
+template <int MODE, int TH, int NB, int CO, int CI, int EPI>
 struct K5 {
-  static constexpr int KS = EPI == BE_QUANT ? ICLR17_BF_C3KS : 1;   // K-split groups
+  static constexpr int KS = EPI == BE_QUANT ? kC3KS : 1;   // K-split groups
   static_assert(k5_threads(TH, EPI) == KS * (TH / 2) * 64, "threads");
   static constexpr int NW = TH / 2, NT_ = NW * 64;   // waves / threads of one group
   static constexpr int NT = NB / 32;            // 32-channel accumulator tiles per wave
@@ -159,48 +120,35 @@ struct K5 {
   static constexpr int SB = 4 * NB * 16;        // weight stage bytes
   static constexpr int NBI = SB / 1024;         // weight DMA wave-instructions per step
   using P = Patch<MODE, TH>;
-  static constexpr int NST = ICLR17_BF_NST;     // weight stages (ring)
-  // persistent (k5p_bf16_kernel): no sink in the main-loop area (it lives in the y-image area)
-  static constexpr int MAIN_LDS = 2 * P::BUF + NST * SB + (PERSIST ? 0 : 1024);
+  static constexpr int NST = kNST;              // weight stages (ring)
+  static constexpr int MAIN_LDS = 2 * P::BUF + NST * SB + 1024;
   static constexpr int GBLK = (CO / 32) * (CO / 16);   // GDN: γ fragment blocks, 1 KB each
   static constexpr int OS = CO * 2 + 16;               // GDN: output tile row stride (bytes)
   // γ staged beside the main-loop buffers, by DMAs issued in the prologue, where that still
   // fits one workgroup per CU (the 8-wave tiles run one per CU anyway); else after the loop
-  static constexpr bool EARLY_G = PERSIST ||
-                                  (EPI != BE_QUANT && NW == 8 && MAIN_LDS + GBLK * 1024 <= 160 * 1024);
+  static constexpr bool EARLY_G = EPI != BE_QUANT && NW == 8 && MAIN_LDS + GBLK * 1024 <= 160 * 1024;
   static constexpr int GOFF = EARLY_G ? MAIN_LDS : 0;
   static constexpr int EPI_LDS = EPI == BE_QUANT ? 64
                                  : (GOFF + GBLK * 1024 > R * OS ? GOFF + GBLK * 1024 : R * OS);
   static constexpr int LDS0 = KS * MAIN_LDS > EPI_LDS ? KS * MAIN_LDS : EPI_LDS;
   // GDN: each wave stores its own y rows, a channel pair of tiles at a time, through a private
   // 4 KB [32 px][64 ch] image (no workgroup barrier: the stores overlap other waves' contraction)
-  // persistent: the main-loop buffers, γ, the per-wave 2 KB [32 px][32 ch] y images (the padding
-  // sink in their first 1 KB) and bias / β_eff, side by side: the next tile's patch and first
-  // weight stages stream in while this tile's epilogue runs
-  static constexpr int YOFF = PERSIST ? GOFF + GBLK * 1024 : (EARLY_G ? 0 : GBLK * 1024);
-  static constexpr bool DIRECT_Y = PERSIST || (ICLR17_BF_DIRECT_Y && EPI != BE_QUANT && NT % 2 == 0 &&
-                                   YOFF + NW * 4096 <= LDS0 && (EARLY_G ? NW * 4096 <= MAIN_LDS : true));
+  static constexpr int YOFF = EARLY_G ? 0 : GBLK * 1024;
+  static constexpr bool DIRECT_Y = EPI != BE_QUANT && NT % 2 == 0 && YOFF + NW * 4096 <= LDS0 &&
+                                   (EARLY_G ? NW * 4096 <= MAIN_LDS : true);
   // GDN: bias and β_eff staged by two prologue DMAs into their own 2 KB (an epilogue global load
   // of them waited out a full L2 round trip after the main loop)
-  static constexpr int BBOFF = PERSIST ? YOFF + NW * 2048 : (LDS0 + 1023) / 1024 * 1024;
+  static constexpr int BBOFF = (LDS0 + 1023) / 1024 * 1024;
   static constexpr int LDS = EPI == BE_QUANT ? LDS0 : BBOFF + 2048;
-  static_assert(!PERSIST || (EPI != BE_QUANT && KS == 1 && NW * 2048 >= 1024 && LDS <= 160 * 1024),
-                "persistent layout");
   static_assert(KS == 1 || (KS - 1) * NW * NT * 16 * 64 * 4 <= KS * MAIN_LDS, "K-split exchange");
   static_assert(TH % 2 == 0 && NB % 32 == 0 && SB % 1024 == 0 && CI % (16 * KS) == 0, "tile shape");
   static_assert(EPI == BE_QUANT || NB == CO, "GDN needs every channel of a pixel in the tile");
 };
 
-template <int MODE, int TH, int NB, int CO, int CI, int EPI, bool PERSIST>
-__device__ void k5_prefetch_tile(const K5Args& a, unsigned char* smem, int t);
-
-// PERSIST (k5p_bf16_kernel): the kernel has staged bias / β_eff and γ once and this tile's
-// patch and first weight stages (k5_prefetch_tile); after the main loop the next tile's
-// (next_t ≥ 0) are prefetched, then the epilogue runs
-template <int MODE, int TH, int NB, int CO, int CI, int EPI, int PH, bool PERSIST = false>
+template <int MODE, int TH, int NB, int CO, int CI, int EPI, int PH>
 __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, int b, int ty, int tx,
-                                        int nb, int next_t = -1) {
-  using KK = K5<MODE, TH, NB, CO, CI, EPI, PERSIST>;
+                                        int nb) {
+  using KK = K5<MODE, TH, NB, CO, CI, EPI>;
   using P = typename KK::P;
   using TP = Taps<MODE, PH>;
   constexpr int NT = KK::NT, NW = KK::NW, S = TP::S, NCH = KK::NCH;
@@ -225,7 +173,7 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
   constexpr int GS = NCH * S;                         // steps
   unsigned char* const sP = gsmem;                    // two patch buffers
   unsigned char* const sB = gsmem + 2 * P::BUF;       // NST weight stages
-  unsigned char* const sD = PERSIST ? smem + KK::YOFF : sB + NST * SB;   // sink of the padding loads
+  unsigned char* const sD = sB + NST * SB;   // sink of the padding loads
   const long img = (long)b * a.Hin * a.Win;
   const int iy0 = MODE == BM_CONV ? 2 * ty * TH - 2 : ty * TH - 1;
   const int ix0 = MODE == BM_CONV ? 2 * tx * 16 - 2 : tx * 16 - 1;
@@ -313,11 +261,8 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
       glds16(a.gamma + ((long)(2 * kb + h) * CO + 32 * i + r32) * 8, smem + KK::GOFF + blk * 1024);
     }
   };
-#if ICLR17_K5_STAMPS
-  const unsigned long long st0 = __builtin_amdgcn_s_memtime();
-#endif
   float* const sbb = (float*)(smem + KK::BBOFF);   // GDN: [bias CO | pad][β_eff CO | pad]
-  if constexpr (EPI != BE_QUANT && !PERSIST) {
+  if constexpr (EPI != BE_QUANT) {
     // waves 0 / 1: one 16-byte piece per lane (CO ≤ 256 floats); retired by the first counted wait
     static_assert(CO <= 256, "bias / β stage");
     if (wave < 2) {
@@ -325,11 +270,9 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
       glds16(lane * 4 < CO ? (const void*)(src + lane * 4) : (const void*)g_zero16, sbb + wave * 256);
     }
   }
-  if constexpr (KK::EARLY_G && !PERSIST) stage_gamma();   // retired by the loop's first counted wait
+  if constexpr (KK::EARLY_G) stage_gamma();   // retired by the loop's first counted wait
   // prologue: chunk 0's patch and the weights of steps 0 .. F-1 (any count per wave), then
   // step F's weights as a full K-group, so the loop's first wait leaves exactly F groups
-  // (persistent: issued before, by k5_prefetch_tile, and landed: the kernel's vm_barrier)
-  if constexpr (!PERSIST) {
   for (int piece = wave; piece < P::NQI; piece += NW) issue_piece(0, piece, true);
 #pragma unroll
   for (int f = 0; f < F; ++f)
@@ -345,12 +288,8 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
   for (int f = 1; f < F; ++f)   // F−1 more full groups: the first wait keeps F in flight
 #pragma unroll
     for (int k = 0; k < K; ++k) sink_load(sD);
-  }
 
   typedef const __attribute__((address_space(3))) u4* lu4p;
-#if ICLR17_K5_STAMPS
-  const unsigned long long st1 = __builtin_amdgcn_s_memtime();
-#endif
   int stage = 0;   // g % NST
   for (int c = 0; c < NCH; ++c) {
     const unsigned char* pbuf = sP + (c & 1) * P::BUF + pbase;
@@ -394,13 +333,6 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
     }
   }
   vm_barrier();   // the trailing sink loads landed and every wave is done with the stages
-  if constexpr (PERSIST) {
-    if (next_t >= 0) k5_prefetch_tile<MODE, TH, NB, CO, CI, EPI, PERSIST>(a, smem, next_t);
-  }
-#if ICLR17_K5_STAMPS
-  const unsigned long long st2 = __builtin_amdgcn_s_memtime();
-  unsigned long long st4 = st2, st5 = st2, stg = st2;
-#endif
 
   // ---- epilogue. acc[i][4m + j]: channel nb·NB + 32i + 8m + 4h + j of tile pixel tpix
   auto out_pixel = [&](int p) -> long {   // NHWC pixel index, or -1 outside the grid
@@ -442,9 +374,6 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
       }
     }
     if constexpr (!KK::EARLY_G) vm_barrier();   // γ of every wave landed
-#if ICLR17_K5_STAMPS
-    stg = __builtin_amdgcn_s_memtime();
-#endif
     const unsigned char* sg = smem + KK::GOFF + lane * 16;
     // DIRECT_Y: this wave's [32 px][64 ch] bf16 image, 128-byte rows, 16-byte piece pc of pixel
     // p at slot pc ^ (p & 7) (the 4×16-lane read groups cover the 64 banks; the 8-byte writes
@@ -475,29 +404,7 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][4 * m + j] = y[j];
       }
-      if constexpr (PERSIST) {
-        // tile i through this wave's 2 KB [32 px][32 ch] image (16-byte piece pc of pixel p at
-        // slot pc ^ (p & 3)): pixel px = (lane >> 2) + 16j is tile row 2·wave + j, column lane >> 2
-        unsigned char* const y1 = smem + KK::YOFF + wave * 2048;
-        auto ysw1 = [](int p, int pc) { return p * 64 + ((pc ^ (p & 3)) << 4); };
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-          *(uint2*)(y1 + ysw1(r32, m) + 8 * h) =
-              uint2{pack_bf2(acc[i][4 * m], acc[i][4 * m + 1]), pack_bf2(acc[i][4 * m + 2], acc[i][4 * m + 3])};
-        wave_lds_sync();   // the image's writes before any lane's reads (cross-lane exchange)
-        const int fl = fresh_tid() & 63;
-        u16* const ob = a.out + (long)b * a.Hout * a.Wout * CO;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int px = (fl >> 2) + 16 * j, pc = fl & 3;
-          const u4 v = *(lu4p)(y1 + ysw1(px, pc));
-          const int gy = ty * TH + 2 * wave + j, gx = tx * 16 + (fl >> 2);
-          const int oy = MODE == BM_CONV ? gy : 2 * gy + (PH >> 1);
-          const int ox = MODE == BM_CONV ? gx : 2 * gx + (PH & 1);
-          if (gy < a.gh && gx < a.gw) *(u4*)(ob + (oy * a.Wout + ox) * CO + 32 * i + 8 * pc) = v;
-        }
-        wave_lds_sync();   // every lane's reads before the next tile's writes (WAR)
-      } else if constexpr (KK::DIRECT_Y) {
+      if constexpr (KK::DIRECT_Y) {
         if (i & 1) {   // tiles i − 1, i: channels 32(i − 1) .. 32i + 31, 8 pieces of 16 bytes
 #pragma unroll
           for (int tt = 0; tt < 2; ++tt)
@@ -526,10 +433,6 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
         }
       }
     }
-#if ICLR17_K5_STAMPS
-    st4 = __builtin_amdgcn_s_memtime();
-    st5 = st4;
-#endif
     if constexpr (!KK::DIRECT_Y) {
     // y through an LDS tile [pixel][channel] (row stride OS) to whole-row 16-byte stores
     __syncthreads();   // every wave's γ reads done: the tile reuses the γ blocks
@@ -542,9 +445,6 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
         *(uint2*)(row + (32 * i + 8 * m) * 2) =
             uint2{pack_bf2(acc[i][4 * m], acc[i][4 * m + 1]), pack_bf2(acc[i][4 * m + 2], acc[i][4 * m + 3])};
     __syncthreads();
-#if ICLR17_K5_STAMPS
-    st5 = __builtin_amdgcn_s_memtime();
-#endif
     constexpr int PCS = CO * 2 / 16;   // 16-byte pieces per pixel row
     for (int idx = tid; idx < KK::R * PCS; idx += KK::NT_) {
       const int p = idx / PCS, pc = idx - p * PCS;
@@ -559,7 +459,7 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
     float bits = 0.f;
     // the rate table rows of this tile's NB channels: staged in LDS after the K-split exchange
     // area (KS == 2, ICLR17_BF_RTAB_LDS) or read from L2
-    constexpr bool RT_LDS = ICLR17_BF_RTAB_LDS && KK::KS == 2;
+    constexpr bool RT_LDS = KK::KS == 2;
     constexpr int XS_BYTES = (KK::KS * NW * NT * 8 * 64 * 4 + 1023) / 1024 * 1024;
     constexpr int RTU = NB * RT_W / 4, RTP = (RTU + 63) / 64;   // 16-byte units, 1 KB pieces
     static_assert(!RT_LDS || (NB * RT_W % 4 == 0 && XS_BYTES + RTP * 1024 <= KK::KS * KK::MAIN_LDS),
@@ -572,7 +472,7 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
     // ŷ through an LDS tile [R px][NB ch] (row stride NB + 4 floats: a 16-lane b128 write group
     // covers 64 distinct banks), then stored by every wave as 16-byte chunks of contiguous
     // pixel rows: the accumulator layout would store 32 pixels × 32 bytes per wave-instruction
-    constexpr bool QST = ICLR17_BF_C3ST && RT_LDS;
+    constexpr bool QST = RT_LDS;
     constexpr int QS = NB + 4, QOFF = XS_BYTES + RTP * 1024;
     static_assert(!QST || QOFF + KK::R * QS * 4 <= KK::KS * KK::MAIN_LDS, "ŷ tile");
     float* const sq = (float*)(smem + QOFF);
@@ -666,9 +566,6 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
       if (kg == 0) add(0); else add(8);
       if constexpr (RT_LDS) vm_barrier();   // table landed; exchange reads done before red[] reuse
       else __syncthreads();                 // exchange reads done before red[] reuses the area
-#if ICLR17_K5_STAMPS
-      st4 = __builtin_amdgcn_s_memtime();
-#endif
       if (kg == 0) {
         quant_rows(0);
         quant_rows(1);
@@ -683,15 +580,9 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
       nred = 2 * NW;
     } else {
       static_assert(KK::KS == 1, "K split");
-#if ICLR17_K5_STAMPS
-      st4 = __builtin_amdgcn_s_memtime();
-#endif
 #pragma unroll
       for (int m = 0; m < 4; ++m) quant_rows(m);
     }
-#if ICLR17_K5_STAMPS
-    st5 = __builtin_amdgcn_s_memtime();
-#endif
     bits = wave_sum(bits);
     float* red = (float*)smem;
     if (lane == 0) red[kg * NW + wave] = bits;
@@ -703,14 +594,6 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
       a.partial[(long)b * a.ppi + tile * (CO / NB) + nb] = sum;
     }
   }
-#if ICLR17_K5_STAMPS
-  const unsigned long long st3 = __builtin_amdgcn_s_memtime();
-  const long wg = blockIdx.x + (long)blockIdx.y * gridDim.x;
-  if (lane == 0 && wg < 8192) {
-    unsigned long long* d = g_k5_stamps + (wg * 16 + wv) * 8;
-    d[0] = st0; d[1] = st1; d[2] = st2; d[3] = st3; d[4] = stg; d[5] = st4; d[6] = st5;
-  }
-#endif
 }
 
 template <int MODE, int TH, int NB, int CO, int CI, int EPI>
@@ -722,9 +605,7 @@ k5_bf16_kernel(const K5Args a) {
   const int per_ph = a.tiles_x * a.tiles_y * a.B;
   const int q = MODE == BM_DECONV ? bid / per_ph : 0;   // phases dispatched phase-major
   bid -= q * per_ph;
-  // two-per-CU tiles (TH = 8): dispatch order 9, 6, 4, 6 taps, so that workgroup i and i + half
-  // the grid (the two a CU holds when the grid is one round) pair a long and a short phase
-  const int ph = (ICLR17_BF_PAIR && TH == 8 && q >= 2) ? 5 - q : q;
+  const int ph = q;
   const int tx = bid % a.tiles_x;
   bid /= a.tiles_x;
   const int ty = bid % a.tiles_y;
@@ -739,128 +620,6 @@ k5_bf16_kernel(const K5Args a) {
       case 2: k5_body<MODE, TH, NB, CO, CI, EPI, 2>(a, smem, b, ty, tx, nb); break;
       default: k5_body<MODE, TH, NB, CO, CI, EPI, 3>(a, smem, b, ty, tx, nb); break;
     }
-  }
-}
-
-// ------------------------------------------------------------------ persistent k5 (deconv2)
-// Tile t → (stride phase, image, tile row, tile column), phase-major as k5_bf16_kernel.
-__device__ __forceinline__ void k5_tile(const K5Args& a, int t, int& ph, int& b, int& ty, int& tx) {
-  const int per_ph = a.tiles_x * a.tiles_y * a.B;
-  ph = t / per_ph;
-  t -= ph * per_ph;
-  tx = t % a.tiles_x;
-  t /= a.tiles_x;
-  ty = t % a.tiles_y;
-  b = t / a.tiles_y;
-}
-
-// Tile t's chunk-0 patch and the weights of steps 0 .. F (its phase's F), any count per wave:
-// the kernel's vm_barrier before the tile retires them (no counted group structure needed)
-template <int MODE, int TH, int NB, int CO, int CI, int EPI, int PH>
-__device__ __forceinline__ void k5_prefetch(const K5Args& a, unsigned char* smem, int b, int ty, int tx) {
-  using KK = K5<MODE, TH, NB, CO, CI, EPI, true>;
-  using P = typename KK::P;
-  using TP = Taps<MODE, PH>;
-  constexpr int NW = KK::NW, S = TP::S, NCH = KK::NCH, NST = KK::NST;
-  constexpr int F = (S >= 6 && NST >= 5) ? 3 : (S >= 3 ? 2 : 1);
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int iy0 = MODE == BM_CONV ? 2 * ty * TH - 2 : ty * TH - 1;
-  const int ix0 = MODE == BM_CONV ? 2 * tx * 16 - 2 : tx * 16 - 1;
-  const u16* __restrict__ inb = a.in + (long)b * a.Hin * a.Win * CI;
-  for (int piece = wave; piece < P::NQI; piece += NW) {
-    const int byte = (piece * 64 + lane) * 16;
-    const int pr = byte / P::ROWB, rem = byte - pr * P::ROWB;
-    int pc, hh;
-    bool ok;
-    if (MODE == BM_CONV) {
-      const int par = rem / (2 * P::HALF), r2 = rem - par * 2 * P::HALF;
-      hh = r2 / P::HALF;
-      pc = 2 * ((r2 - hh * P::HALF) / 16) + par;
-      ok = pc < 35;
-    } else {
-      hh = rem / P::HALF;
-      pc = (rem - hh * P::HALF) / 16;
-      ok = true;
-    }
-    const int iy = iy0 + pr, ix = ix0 + pc;
-    ok = ok && pr < P::ROWS && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
-    glds16(ok ? (const void*)(inb + (iy * a.Win + ix) * CI + 8 * hh) : (const void*)g_zero16,
-           smem + piece * 1024);   // patch buffer 0 (chunk 0)
-  }
-  const long wstep = 4L * CO * 8;
-  const u16* __restrict__ wph = a.w;
-  if (MODE == BM_DECONV) {
-    long off = 0;
-#pragma unroll
-    for (int p = 0; p < PH; ++p) {
-      const int ny = (p >> 1) == 0 ? 3 : 2, nx = (p & 1) == 0 ? 3 : 2;
-      off += (long)NCH * ((ny * nx + 1) / 2) * wstep;
-    }
-    wph += off;
-  }
-  unsigned char* const sB = smem + 2 * P::BUF;
-#pragma unroll
-  for (int f = 0; f <= F; ++f)
-    for (int slot = wave; slot < KK::NBI; slot += NW) {
-      const int q = slot * 64 + lane;
-      const int g = q / NB, col = q - g * NB;
-      glds16(wph + (long)f * wstep + (g * CO + col) * 8, sB + f * KK::SB + slot * 1024);
-    }
-}
-
-template <int MODE, int TH, int NB, int CO, int CI, int EPI, bool PERSIST>
-__device__ void k5_prefetch_tile(const K5Args& a, unsigned char* smem, int t) {
-  int ph, b, ty, tx;
-  k5_tile(a, t, ph, b, ty, tx);
-  switch (ph) {
-    case 0: k5_prefetch<MODE, TH, NB, CO, CI, EPI, 0>(a, smem, b, ty, tx); break;
-    case 1: k5_prefetch<MODE, TH, NB, CO, CI, EPI, 1>(a, smem, b, ty, tx); break;
-    case 2: k5_prefetch<MODE, TH, NB, CO, CI, EPI, 2>(a, smem, b, ty, tx); break;
-    default: k5_prefetch<MODE, TH, NB, CO, CI, EPI, 3>(a, smem, b, ty, tx); break;
-  }
-}
-
-// deconv (all four stride phases) as one persistent 8-wave workgroup per CU walking the tiles
-// t = blockIdx.x, + gridDim.x, …: bias / β_eff and γ are staged once per workgroup, and each
-// tile's patch and first weight stages stream in during the previous tile's epilogue (LDS:
-// K5<…, PERSIST>); the tile body is k5_bf16_kernel's, so the outputs are bit-identical to it.
-// At B = 64 (deconv2: 4 phases × 256 tiles) each workgroup takes one tile of every phase.
-template <int MODE, int TH, int NB, int CO, int CI, int EPI>
-__global__ void __launch_bounds__(TH / 2 * 64, 1) k5p_bf16_kernel(const K5Args a) {
-  static_assert(MODE == BM_DECONV, "persistent k5: the deconvolutions");
-  using KK = K5<MODE, TH, NB, CO, CI, EPI, true>;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[KK::LDS];
-  constexpr int NW = KK::NW, KB16 = CO / 16;
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int r32 = lane & 31, h = lane >> 5;
-  const int total = 4 * a.tiles_x * a.tiles_y * a.B;
-  int t = blockIdx.x;
-  if (t >= total) return;
-  // once per workgroup: bias and β_eff (waves 0 / 1), γ fragments (k5_body's stage_gamma layout)
-  static_assert(CO <= 256, "bias / β stage");
-  if (wave < 2) {
-    const float* src = wave == 0 ? a.bias : a.beta;
-    glds16(lane * 4 < CO ? (const void*)(src + lane * 4) : (const void*)g_zero16,
-           smem + KK::BBOFF + wave * 1024);
-  }
-  for (int blk = wave; blk < KK::GBLK; blk += NW) {
-    const int i = blk / KB16, kb = blk - i * KB16;
-    glds16(a.gamma + ((long)(2 * kb + h) * CO + 32 * i + r32) * 8, smem + KK::GOFF + blk * 1024);
-  }
-  k5_prefetch_tile<MODE, TH, NB, CO, CI, EPI, true>(a, smem, t);
-  while (t < total) {
-    vm_barrier();   // this tile's patch and first weights (and the previous tile's stores) landed
-    const int tn = t + gridDim.x;
-    int ph, b, ty, tx;
-    k5_tile(a, t, ph, b, ty, tx);
-    const int nx = tn < total ? tn : -1;
-    switch (ph) {   // wave-uniform
-      case 0: k5_body<MODE, TH, NB, CO, CI, EPI, 0, true>(a, smem, b, ty, tx, 0, nx); break;
-      case 1: k5_body<MODE, TH, NB, CO, CI, EPI, 1, true>(a, smem, b, ty, tx, 0, nx); break;
-      case 2: k5_body<MODE, TH, NB, CO, CI, EPI, 2, true>(a, smem, b, ty, tx, 0, nx); break;
-      default: k5_body<MODE, TH, NB, CO, CI, EPI, 3, true>(a, smem, b, ty, tx, 0, nx); break;
-    }
-    t = tn;
   }
 }
 
@@ -891,9 +650,6 @@ constexpr int C1U = 3 * C1P * C1RS;           // u16 elements of the bf16 plane 
 // analysis_17.py:14-17 (conv1) + models/GDN.py:64-94 (GDN1).
 constexpr int C1P_WAVES = 8;
 constexpr int C1P_STK = 20, C1P_STP = 5;   // stamps: blocks per workgroup, phases per block
-#if ICLR17_C1P_STAMPS
-__device__ unsigned long long g_c1p_stamps[1024 * C1P_WAVES * C1P_STK * C1P_STP];
-#endif
 constexpr int C1P_LOADS = (C1PIECES + C1P_WAVES * 64 - 1) / (C1P_WAVES * 64);   // 3 per thread
 
 template <int CO>
@@ -1153,15 +909,6 @@ conv1p_bf16_kernel(const float* __restrict__ x, int H, int W, const u16* __restr
     }
   };
   const int G = gridDim.x;
-#if ICLR17_C1P_STAMPS
-  unsigned long long* const stl = (unsigned long long*)(sbeta + CO);   // [wave][k][phase] in LDS
-  auto stamp = [&](int k, int ph) {
-    const unsigned long long tm = __builtin_amdgcn_s_memtime();
-    if (lane == 0 && k < C1P_STK) stl[(wave * C1P_STK + k) * C1P_STP + ph] = tm;
-  };
-#else
-  auto stamp = [](int, int) {};
-#endif
   {
     int k = 0;
     for (int t = blockIdx.x; t < ntiles; t += G, ++k) {
@@ -1180,11 +927,6 @@ conv1p_bf16_kernel(const float* __restrict__ x, int H, int W, const u16* __restr
       __syncthreads();   // next plane written, output rows read
       stamp(k, 4);
     }
-#if ICLR17_C1P_STAMPS
-    __syncthreads();
-    for (int i = tid; i < C1P_WAVES * C1P_STK * C1P_STP; i += NTHR)
-      g_c1p_stamps[(long)blockIdx.x * C1P_WAVES * C1P_STK * C1P_STP + i] = stl[i];
-#endif
     return;
   }
 }
@@ -1302,16 +1044,6 @@ int launch_deconv(const K5Args& a0, hipStream_t st) {
   a.tiles_y = (a.gh + TH - 1) / TH;
   a.tiles_x = (a.gw + 15) / 16;
   const int tiles = a.tiles_x * a.tiles_y * a.B * 4;
-  if constexpr (TH == 16) {   // one workgroup per CU walking the tiles (ICLR17_BF_PERSIST=0: off)
-    static const bool persist = getenv("ICLR17_BF_PERSIST") ? atoi(getenv("ICLR17_BF_PERSIST")) != 0
-                                                             : ICLR17_BF_PERSIST != 0;
-    if (persist) {
-      const int ncu = cu_count();
-      hipLaunchKernelGGL((k5p_bf16_kernel<BM_DECONV, TH, N, N, N, BE_IGDN>),
-                         dim3(tiles < ncu ? tiles : ncu, 1), dim3(TH / 2 * 64), 0, st, a);
-      return check_launch("deconv_igdn_bf16 (persistent)");
-    }
-  }
   hipLaunchKernelGGL((k5_bf16_kernel<BM_DECONV, TH, N, N, N, BE_IGDN>),
                      dim3(tiles, 1), dim3(TH / 2 * 64), 0, st, a);
   return check_launch("deconv_igdn_bf16");
@@ -1325,20 +1057,7 @@ using namespace iclr17::bfm;
 
 extern "C" {
 
-#if ICLR17_C1P_STAMPS
-// diagnostic build only: copy the conv1p stamps ([workgroup][wave][block][phase] s_memtime)
-int iclr17_debug_c1p_stamps(void* dst, size_t bytes) {
-  const size_t n = sizeof(g_c1p_stamps) < bytes ? sizeof(g_c1p_stamps) : bytes;
-  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_c1p_stamps), n, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
-}
-#endif
 
-#if ICLR17_K5_STAMPS
-int iclr17_debug_k5_stamps(void* dst, size_t bytes) {
-  const size_t n = sizeof(g_k5_stamps) < bytes ? sizeof(g_k5_stamps) : bytes;
-  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_k5_stamps), n, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
-}
-#endif
 
 size_t iclr17_bf16_weight_size(int which, int N) {
   if (N != 128 && N != 192) return 0;
@@ -1463,7 +1182,7 @@ int iclr17_synthesis_deconv_igdn_bf16(const uint16_t* in, int B, int h, int w, i
   a.gh = h; a.gw = w;
   hipStream_t st = (hipStream_t)stream;
   // 16-row tiles where the grid stays ≥ 2 rounds of workgroups (deconv2), 8 rows otherwise
-  const bool big = ICLR17_BF_DECONV16 && (long)((h + 15) / 16) * ((w + 15) / 16) * B * 4 >= 512;
+  const bool big = (long)((h + 15) / 16) * ((w + 15) / 16) * B * 4 >= 512;
   if (N == 192) return big ? launch_deconv<192, 16>(a, st) : launch_deconv<192, 8>(a, st);
   return big ? launch_deconv<128, 16>(a, st) : launch_deconv<128, 8>(a, st);
 }

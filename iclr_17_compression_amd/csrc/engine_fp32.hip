@@ -132,6 +132,13 @@ struct EngineArgs {
   long w6_plane;
   float* fold_total;        // scale · Σ, 0-dim
   double fold_scale;
+  // h3 form (common.h): the H3 instantiations read the input as two fp16 planes (in_split) and the
+  // weights pre-split into two fp16 planes (w6, [2][taps][CI/8][CO][8]) whose packing trailer
+  // holds 2⁻¹¹/(σ_a·σ_w) at wscale[1]; any epilogue may also write its output in the h3 form
+  const float* wscale;
+  unsigned short* out_h3;           // [2][B][Hout][Wout][CO] or nullptr
+  long out_h3_plane;
+  int* range;                       // h3 range flag (nullable)
 };
 
 // iclr17_reduce_partials inside the last kernel of the eval chain (deconv3): the per-image sums of
@@ -284,6 +291,26 @@ __device__ __forceinline__ void store_tile_rows_split(const EngineArgs& a, const
     *(u4*)(d + a.out_plane) = mi;
     *(u4*)(d + 2 * a.out_plane) = lo;
   }
+}
+
+// Store an [R][BN] LDS tile as the two fp16 planes of the h3 form (x·σ_a split, common.h), 4
+// channels (8 bytes per plane) per lane; a value the form cannot hold sets the range flag.
+template <int BN, int R = BM, int T = 256>
+__device__ __forceinline__ void store_tile_rows_h3(const EngineArgs& a, const TileInfo& t,
+                                                   const float* s, int ld, int CO, int col0) {
+  constexpr int C4 = BN / 4;
+  bool ovf = false;
+  for (int idx = threadIdx.x; idx < R * C4; idx += T) {
+    const int m = idx / C4, c4 = idx % C4;
+    const long p = out_pixel(a, t, m);
+    if (p < 0) continue;
+    uint2 hb, lb;
+    h3_split4(*(const f4*)(s + m * ld + c4 * 4), hb, lb, ovf);
+    unsigned short* d = a.out_h3 + p * CO + col0 + c4 * 4;
+    *(uint2*)d = hb;
+    *(uint2*)(d + a.out_h3_plane) = lb;
+  }
+  if (ovf && a.range) atomicOr(a.range, 1);
 }
 
 // Column sums of an LDS tile [BM][ld] over the rows inside the output grid → dst[blockIdx.x][CO],
@@ -651,6 +678,7 @@ __device__ __forceinline__ void gdn_epilogue(f4 (&x)[MT][NT], float* smem, const
                                           a.ggamma6);
   if (a.out != nullptr) store_tile_rows<CO, R, T>(a, t, smem, XS, a.out, CO, 0);
   if (a.out_split != nullptr) store_tile_rows_split<CO, R, T>(a, t, smem, XS, CO, 0);
+  if (a.out_h3 != nullptr) store_tile_rows_h3<CO, R, T>(a, t, smem, XS, CO, 0);
   if (a.pre != nullptr) {
     __syncthreads();
     acc_to_lds<MT, NT>(x, smem, XS, wm, ncol0, lane);
@@ -899,6 +927,7 @@ __device__ __forceinline__ void quant_epilogue(f4 (&acc)[MT][NT], float* smem, c
   __syncthreads();
   store_tile_rows<BN>(a, t, sO, OS, a.yhat, CO, cbase);
   if (a.out_split != nullptr) store_tile_rows_split<BN>(a, t, sO, OS, CO, cbase);   // ŷ, x6 form
+  if (a.out_h3 != nullptr) store_tile_rows_h3<BN>(a, t, sO, OS, CO, cbase);         // ŷ, h3 form
   if (a.out != nullptr) {
     __syncthreads();
 #pragma unroll
@@ -1011,16 +1040,26 @@ __device__ __forceinline__ void out3_epilogue(f4 (&acc)[MT][NT], float* smem, co
 // the fragments are read as they are: conv3's 2×2 waves split each weight column for only two
 // row tiles, so the per-step split was 3.7 VALU instructions per MFMA. Same bf16 operands (the
 // split is iclr17_split_packed's, i.e. the same split8 on the same quads): bit-identical output.
-template <int CI, int CO, int BN, int WM, int WN, int EPI, bool X6, int BMT = BM, bool W6 = false>
+// H3 (the h3 form, common.h; conv2 / conv3 of the parity mode): A arrives as two fp16 planes
+// [2][BM][32] (the x6 A image's geometry with two planes: the same bytes as an fp32 A image), B
+// pre-split as two fp16 planes [2][4][BN][8] (the same bytes as an fp32 B stage), and a 32-deep
+// step is three v_mfma_f32_16x16x32_f16 per 16×16 tile, lo_a·hi_w + hi_a·lo_w + hi_a·(hi_w·2¹¹),
+// in place (inside the two-level accumulation where TAPSEP applies); the epilogue scales the
+// contraction by 2⁻¹¹/(σ_a·σ_w) (exact) before the bias.
+template <int CI, int CO, int BN, int WM, int WN, int EPI, bool X6, int BMT = BM, bool W6 = false,
+          bool H3 = false>
 __device__ __forceinline__ void engine_body(const EngineArgs& a) {
+  constexpr bool XS = X6 || H3;                  // 16-bit split-form A planes
+  constexpr int APL = H3 ? 2 : 3;                // A / pre-split B planes
   constexpr int NWV = WM * WN;                   // waves (4, or 8 for the 128-row tiles)
   constexpr int MT = BMT / WM / 16;
   constexpr int NT = BN / WN / 16;
   constexpr int KCH = 32;                        // input channels per k-step
   constexpr int NCH = CI / KCH;
-  static_assert(!W6 || (X6 && EPI == EPI_QUANT), "pre-split weights: x6 conv3");
-  constexpr int SA = X6 ? 3 * BMT * KCH / 2 : BMT * KCH;   // A image floats per stage
-  constexpr int SB = W6 ? 3 * 4 * BN * 8 / 2     // W6: [3][4][BN][8] bf16
+  static_assert(!W6 || (X6 && EPI == EPI_QUANT) || H3, "pre-split weights: x6 conv3, h3");
+  static_assert(!H3 || (W6 && !X6 && (EPI == EPI_GDN || EPI == EPI_QUANT)), "h3: conv2 / conv3");
+  constexpr int SA = XS ? APL * BMT * KCH / 2 : BMT * KCH;   // A image floats per stage
+  constexpr int SB = W6 ? APL * 4 * BN * 8 / 2   // W6: [3][4][BN][8] bf16 | H3: [2][4][BN][8] fp16
                         : KCH * BN;              // B image floats per stage: [8 quads][BN][4]
   constexpr int STAGE = SA + SB;
   constexpr int NAI = SA * 4 / 1024;             // A glds wave-instructions per step (8 | 12)
@@ -1040,7 +1079,7 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   constexpr int LDS_A = HALO ? HALO_PF + 2 * SB
                              : 2 * STAGE;   // two-stage ring (3, 4 stages measured slower: DESIGN.md §5)
   constexpr int LDS_XF = BMT * (CO + 8) + GSTAGE_FLOATS(CO);
-  constexpr int LDS_XP = gdn_lds_floats(BMT, CO, X6);
+  constexpr int LDS_XP = gdn_lds_floats(BMT, CO, XS);
   constexpr int LDS_X = (EPI == EPI_GDN || EPI == EPI_IGDN) ? (LDS_XF > LDS_XP ? LDS_XF : LDS_XP)
                         : (EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD) ? LDS_XF : 0;
   constexpr int LDS_O = BMT * (BN + 4) + 8;
@@ -1078,13 +1117,13 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
 #pragma unroll
   for (int j = 0; j < AI_W; ++j) {
     const int i = wave * AI_W + j;
-    const int row = X6 ? 16 * (i % API) + (lane >> 2) : i * 8 + (lane >> 3);
-    const int c = X6 ? (lane & 3) ^ ((row >> 1) & 3) : (lane & 7) ^ (row & 7);
+    const int row = XS ? 16 * (i % API) + (lane >> 2) : i * 8 + (lane >> 3);
+    const int c = XS ? (lane & 3) ^ ((row >> 1) & 3) : (lane & 7) ^ (row & 7);
     const int gy = t.ty * (BMT / 8) + (row >> 3), gx = t.tx * 8 + (row & 7);
     rval[j] = gy < a.gh && gx < a.gw;
     iy0[j] = gy * a.sin;
     ix0[j] = gx * a.sin;
-    pbase[j] = (iy0[j] * a.Win + ix0[j]) * CI + c * (X6 ? 8 : 4);
+    pbase[j] = (iy0[j] * a.Win + ix0[j]) * CI + c * (XS ? 8 : 4);
   }
   const long img = (long)t.b * a.Hin * a.Win * CI;
   const float* __restrict__ inb = a.in + img;
@@ -1121,7 +1160,7 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
       const bool ok = rval[j] && (unsigned)(iy0[j] + dy) < (unsigned)a.Hin &&
                       (unsigned)(ix0[j] + dx) < (unsigned)a.Win;
       const int i = wave * AI_W + j;
-      if constexpr (X6) {
+      if constexpr (XS) {
         const unsigned short* src = inb6 + (i / API) * a.in_plane + pbase[j] + so;
         glds16(ok ? (const float*)src : g_zero16, sa + i * 256);
       } else {
@@ -1204,7 +1243,36 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
     x6_flush<false>(acc, st);
   };
 
+  // H3: one 32-deep step, three f16 products per tile (B: hi_w, lo_w planes; hi_w·2¹¹ formed here)
+  auto compute_h3 = [&](int buf) {
+    const unsigned short* sa = (const unsigned short*)(smem + buf * STAGE);
+    const unsigned short* sb6 = (const unsigned short*)(smem + buf * STAGE + SA) +
+                                ((lane >> 4) * BN + wn * (BN / WN) + (lane & 15)) * 8;
+    u4 Bh[NT], Bl[NT], Bh11[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      Bh[nt] = *(const u4*)(sb6 + nt * 128);
+      Bl[nt] = *(const u4*)(sb6 + 32 * BN + nt * 128);
+      Bh11[nt] = h3_x2048(Bh[nt]);
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const h8v Ah = __builtin_bit_cast(h8v, *(const u4*)(sa + aoff6[mt]));
+      const h8v Al = __builtin_bit_cast(h8v, *(const u4*)(sa + BMT * KCH + aoff6[mt]));
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        f4 c = __builtin_amdgcn_mfma_f32_16x16x32_f16(Al, __builtin_bit_cast(h8v, Bh[nt]), acc[mt][nt], 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ah, __builtin_bit_cast(h8v, Bl[nt]), c, 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ah, __builtin_bit_cast(h8v, Bh11[nt]), c, 0, 0, 0);
+      }
+    }
+  };
+
   auto compute = [&](int buf) {
+    if constexpr (H3) {
+      compute_h3(buf);
+      return;
+    }
     if constexpr (X6) {
       compute6(buf);
       return;
@@ -1350,6 +1418,13 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
     }
   }
   __syncthreads();     // last stage reads done before the epilogue reuses LDS
+  if constexpr (H3) {   // the h3 contraction carries 2¹¹·σ_a·σ_w: a power of two, removed exactly
+    const float dsc = a.wscale[1];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = acc[mt][nt] * dsc;
+  }
 
   if constexpr (EPI == EPI_GDN || EPI == EPI_IGDN) {
     static_assert(BN == CO, "GDN fusion needs every channel of a pixel in the workgroup");
@@ -1359,7 +1434,7 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
       for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[mt][nt][r] += a.bias[ncol0 + nt * 16 + (lane & 15)];
-    gdn_epilogue<CO, MT, NT, EPI == EPI_IGDN, BMT, NWV * 64, X6>(acc, smem, a, t, wm, ncol0,
+    gdn_epilogue<CO, MT, NT, EPI == EPI_IGDN, BMT, NWV * 64, XS>(acc, smem, a, t, wm, ncol0,
                                                                 lane);
   } else if constexpr (EPI == EPI_QUANT) {
     quant_epilogue<CO, BN, MT, NT, WN>(acc, smem, a, t, wm, ncol0, lane, wave);
@@ -1389,9 +1464,10 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   }
 }
 
-template <int CI, int CO, int BN, int WM, int WN, int EPI, bool X6 = false, bool W6 = false>
+template <int CI, int CO, int BN, int WM, int WN, int EPI, bool X6 = false, bool W6 = false,
+          bool H3 = false>
 __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
-  engine_body<CI, CO, BN, WM, WN, EPI, X6, BM, W6>(a);
+  engine_body<CI, CO, BN, WM, WN, EPI, X6, BM, W6, H3>(a);
 }
 
 // The same kernel held to 256 VGPRs (2 waves per SIMD) where the compiler would otherwise just
@@ -2425,6 +2501,11 @@ struct SplitIO {
   const unsigned short* gammaT6 = nullptr;  // x6 backward: split transposed γ_eff
   const unsigned short* w6 = nullptr;       // x6 conv3: pre-split weights (engine W6)
   long w6_plane = 0;
+  bool h3 = false;                          // the H3 instantiations (in / w6 in the h3 form)
+  const float* wscale = nullptr;            // h3: the weight packing's trailer
+  unsigned short* out_h3 = nullptr;         // h3-form output
+  long out_h3_plane = 0;
+  int* range = nullptr;
 };
 
 static void apply_split(EngineArgs& a, const SplitIO* x6) {
@@ -2435,6 +2516,10 @@ static void apply_split(EngineArgs& a, const SplitIO* x6) {
   a.ggammaT6 = x6->gammaT6;
   a.w6 = x6->w6;
   a.w6_plane = x6->w6_plane;
+  a.wscale = x6->wscale;
+  a.out_h3 = x6->out_h3;
+  a.out_h3_plane = x6->out_h3_plane;
+  a.range = x6->range;
 }
 
 template <int N, int EPI = EPI_GDN>
@@ -2479,6 +2564,7 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
   if (bwd) a = *bwd;
   apply_split(a, x6);
   const bool X6in = a.in_split != nullptr;
+  const bool H3in = x6 != nullptr && x6->h3;
   a.in = in; a.w = wp; a.bias = bias; a.gbeta = beta; a.ggamma = gamma; a.out = out; a.pre = pre;
   a.B = B; a.Hin = Hin; a.Win = Win; a.Hout = Hin / 2; a.Wout = Win / 2;
   a.gh = a.Hout; a.gw = a.Wout; a.tiles_y = (a.gh + 7) / 8; a.tiles_x = (a.gw + 7) / 8;
@@ -2492,6 +2578,11 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
     constexpr int WN = (BN / 16) % 4 == 0 ? 4 : 2, WM = 4 / WN;
     a.partials_per_image = a.tiles_x * a.tiles_y * (N / BN);
     dim3 grid(a.tiles_x * a.tiles_y * B, N / BN);
+    if (H3in) {   // the h3 form (round and noise mode alike on the BN-column tiles)
+      hipLaunchKernelGGL((engine_kernel<N, N, BN, WM, WN, EPI_QUANT, false, true, true>), grid,
+                         dim3(256), 0, st, a);
+      return check_launch("conv3_quant_rate_h3");
+    }
     if constexpr (N == 192) {
       if (X6in && conv3_narrow(N, a.tiles_x * a.tiles_y, B, qmode)) {
         a.partials_per_image = a.tiles_x * a.tiles_y * (N / 48);
@@ -2529,6 +2620,11 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
   } else {
     dim3 grid(a.tiles_x * a.tiles_y * B, 1);
     if constexpr (EPI == EPI_GDN) {
+      if (H3in) {
+        hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI, false, true, true>), grid, dim3(256),
+                           0, st, a);
+        return check_launch("conv2_gdn_h3");
+      }
       if (X6in) {
         hipLaunchKernelGGL((engine_kernel<N, N, N, 1, 4, EPI, true>), grid, dim3(256), 0,
                            st, a);
@@ -2957,6 +3053,86 @@ int iclr17_analysis_conv3_quant_rate_x6w(const uint16_t* in_split, int B, int H,
   io.w6_plane = 25L * N * N;
   return N == 192 ? launch_conv5<192, EPI_QUANT>(nullptr, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io, rate_table)
                   : launch_conv5<128, EPI_QUANT>(nullptr, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io, rate_table);
+}
+
+int iclr17_analysis_conv1x6_gdn_h3(const float* x, int B, int H, int W, int N,
+                                   const uint16_t* w_split, const float* bias,
+                                   const float* beta_eff, const uint16_t* gamma_split,
+                                   float* out, uint16_t* out_h3, int* range_flag, void* stream) {
+  int rc = check_dims(B, H, W, N);
+  if (rc) return rc;
+  ICLR17_REQUIRE(x && w_split && bias && beta_eff && gamma_split && (out || out_h3),
+                 ICLR17_EINVAL, "conv1x6_gdn_h3: null pointer");
+  EngineArgs a;
+  memset(&a, 0, sizeof(a));
+  a.in = x; a.w = (const float*)w_split; a.bias = bias; a.gbeta = beta_eff;
+  a.out = out;
+  a.out_h3 = (unsigned short*)out_h3;
+  a.out_h3_plane = (long)B * (H / 4) * (W / 4) * N;
+  a.range = range_flag;
+  a.ggamma6 = (const unsigned short*)gamma_split;
+  a.B = B; a.Hin = H; a.Win = W; a.Hout = H / 4; a.Wout = W / 4;
+  a.gh = H / 4; a.gw = W / 4; a.tiles_y = (a.gh + 7) / 8; a.tiles_x = (a.gw + 7) / 8;
+  a.sin = 4; a.sout = 1;
+  a.tt.npx = 1; a.tt.nph = 1;
+  dim3 grid(a.tiles_x * a.tiles_y * B, 1);
+  if (N == 192)
+    hipLaunchKernelGGL((conv1_x6_kernel<192, EPI_GDN>), grid, dim3(256), 0, S(stream), a);
+  else
+    hipLaunchKernelGGL((conv1_x6_kernel<128, EPI_GDN>), grid, dim3(256), 0, S(stream), a);
+  return check_launch("conv1x6_gdn_h3");
+}
+
+int iclr17_analysis_conv2_gdn_h3(const uint16_t* in_h3, int B, int H, int W, int N,
+                                 const uint16_t* w_h3, const float* bias, const float* beta_eff,
+                                 const uint16_t* gamma_split, float* out, uint16_t* out_h3,
+                                 uint16_t* out_split, int* range_flag, void* stream) {
+  int rc = check_dims(B, H, W, N);
+  if (rc) return rc;
+  ICLR17_REQUIRE(in_h3 && w_h3 && bias && beta_eff && gamma_split && (out || out_h3 || out_split),
+                 ICLR17_EINVAL, "conv2_gdn_h3: null pointer");
+  const int h = H / 4, w = W / 4;
+  SplitIO io;
+  io.h3 = true;
+  io.in = (const unsigned short*)in_h3;
+  io.in_plane = (long)B * h * w * N;
+  io.out = (unsigned short*)out_split;
+  io.out_plane = (long)B * (h / 2) * (w / 2) * N;
+  io.out_h3 = (unsigned short*)out_h3;
+  io.out_h3_plane = io.out_plane;
+  io.gamma6 = (const unsigned short*)gamma_split;
+  io.w6 = (const unsigned short*)w_h3;
+  io.w6_plane = 25L * N * N;
+  io.wscale = (const float*)(w_h3 + 2 * io.w6_plane);
+  io.range = range_flag;
+  return N == 192 ? launch_conv5<192, EPI_GDN>(nullptr, B, h, w, nullptr, bias, beta_eff, nullptr, out, nullptr, 0, nullptr, nullptr, nullptr, nullptr, S(stream), nullptr, &io)
+                  : launch_conv5<128, EPI_GDN>(nullptr, B, h, w, nullptr, bias, beta_eff, nullptr, out, nullptr, 0, nullptr, nullptr, nullptr, nullptr, S(stream), nullptr, &io);
+}
+
+int iclr17_analysis_conv3_quant_rate_h3(const uint16_t* in_h3, int B, int H, int W, int N,
+                                        const uint16_t* w_h3, int quant_mode, const float* noise,
+                                        const float* rate_packed, const float* rate_table,
+                                        float* y_out, float* y_hat, uint16_t* y_hat_h3,
+                                        double* bits_partial, int* range_flag, void* stream) {
+  int rc = check_dims(B, H, W, N);
+  if (rc) return rc;
+  ICLR17_REQUIRE(in_h3 && w_h3 && rate_packed && y_hat && bits_partial, ICLR17_EINVAL,
+                 "conv3_quant_rate_h3: null pointer");
+  ICLR17_REQUIRE(quant_mode == ICLR17_QUANT_ROUND || (quant_mode == ICLR17_QUANT_NOISE && noise),
+                 ICLR17_EINVAL, "conv3_quant_rate_h3: bad quant mode %d / missing noise", quant_mode);
+  const int h = H / 8, w = W / 8;
+  SplitIO io;
+  io.h3 = true;
+  io.in = (const unsigned short*)in_h3;
+  io.in_plane = (long)B * h * w * N;
+  io.out_h3 = (unsigned short*)y_hat_h3;
+  io.out_h3_plane = (long)B * (h / 2) * (w / 2) * N;
+  io.w6 = (const unsigned short*)w_h3;
+  io.w6_plane = 25L * N * N;
+  io.wscale = (const float*)(w_h3 + 2 * io.w6_plane);
+  io.range = range_flag;
+  return N == 192 ? launch_conv5<192, EPI_QUANT>(nullptr, B, h, w, nullptr, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io, rate_table)
+                  : launch_conv5<128, EPI_QUANT>(nullptr, B, h, w, nullptr, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io, rate_table);
 }
 
 static int deconv_igdn_x6(const uint16_t* in_split, int B, int h, int w, int N,

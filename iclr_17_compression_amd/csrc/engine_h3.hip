@@ -1,31 +1,31 @@
-// The x6 (fp32-exact) k5 layers on v_mfma_f32_32x32x16_bf16: the bf16 throughput engine's form
-// (engine_bf16.hip) with six bf16 part products per MAC. synthesis_17.py:15-22 (deconv1/2 +
-// IGDN), models/GDN.py:64-94.
+// The k5 layers in the h3 form (common.h): three fp16 part products per MAC on
+// v_mfma_f32_32x32x16_f16, half the x6 mode's six bf16 ones, at the same fp32-level accuracy.
+// synthesis_17.py:15-22 (deconv1/2 + IGDN), analysis_17.py:18-21 (conv2 + GDN),
+// models/GDN.py:64-94.
 //
-// Why a second x6 engine: the 16x16x32 x6 engine (engine_fp32.hip, engine_kernel<…, X6>) splits
-// the fp32 weights in VALU inside its main loop and moves its operands by LDS-DMA per tap, so a
-// k-step issues ~2× its MFMA cycles (72 MFMAs × 8 issue cycles + 9 DMA pieces + 165
-// VALU per wave and step, on an MFMA that leaves 8 of 16 cycles for issue). Here:
-//   * v_mfma_f32_32x32x16_bf16 leaves 24 of its 32 cycles for issue;
-//   * the weights arrive pre-split (iclr17_pack_x6k: three bf16 planes in the A-fragment layout),
-//     so the main loop has no VALU at all;
-//   * the input is the producing layer's split form (three bf16 planes), staged per 16-channel
-//     chunk as ONE halo patch that every tap of the chunk reads at a shifted offset;
-//   * a wave owns 32 pixels and every output channel (NT = CO/32 accumulators), so the IGDN
-//     channel contraction runs from the accumulators (no x² tile).
-// One k16 step = one tap × the chunk's 16 channels: 6 MFMAs per (channel tile, step), in the x6
-// engine's product order (lo·hi, hi·lo, mid·mid, mid·hi, hi·mid, hi·hi: small terms first), in
-// place on the accumulator. The dropped terms (mid·lo, lo·mid, lo·lo) are below 2⁻²⁴ of a product.
+// Form (the bf16 throughput engine's, engine_bf16.hip):
+//   * a workgroup of TH/2 waves covers TH × 16 base pixels; wave w owns the 32 pixels of tile rows
+//     2w, 2w+1 and every output channel (NT = CO/32 accumulators of 32×32), so the GDN / IGDN
+//     channel contraction runs straight from the accumulators;
+//   * the input arrives in the h3 form (two fp16 planes, written by the producing layer's
+//     epilogue) and is staged per 16-channel chunk as ONE halo patch by LDS-DMA; every tap of the
+//     chunk reads its fragment at a shifted offset;
+//   * the weights arrive pre-split (iclr17_pack_h3k: hi and lo planes of w·σ_w in the A-fragment
+//     layout), streamed through a 4-stage LDS ring with counted DMA waits; hi·2¹¹ is formed in
+//     registers (4 packed fp16 multiplies per fragment) instead of being a third plane.
+// One k16 step = one tap × the chunk's 16 channels: per 32-channel tile three MFMAs, small terms
+// first: hi_w·lo_a, lo_w·hi_a, (hi_w·2¹¹)·hi_a, in place on the accumulator (the h3 chain's
+// rounding error is 0.7× the x6 chain's: common.h).
 //
-// INT_IN (deconv1: its input is ŷ, integers |v| ≤ 127, exact in one bf16): the input's mid and
-// lo planes are zero, so only its hi plane is staged and the three products with a non-zero
-// input part run (lo·hi, mid·hi, hi·hi) — the other three would add exact zeros.
+// INT_IN (deconv1 on ŷ: integers, exact in the hi plane while |ŷ| < 2048): the lo plane is zero,
+// only the hi plane is staged and the two products with hi_a run. INT_OK kernels check this per
+// workgroup over the input window and fall back to the full body otherwise.
 //
-// Epilogue (IGDN / GDN, x6): x = acc + bias; n = Σ_j γ[i][j]·x_j² with γ split into three bf16
-// planes (the A operand, staged in LDS half the output channels at a time) and x² (rounded to
-// fp32, as conv2d(x², γ) sees it) split in registers into three B planes; y = x·√(β + n)
-// (IGDN) or x / √(β + n) (GDN), correctly rounded sqrt and division. The output leaves in
-// split form (NHWC, or chunk-major [3][B][N/32][h][w][32] for deconv3) and optionally fp32.
+// Epilogue: x = acc·2⁻¹¹/(σ_a·σ_w) + bias (a power-of-two scale: exact), then the GDN / IGDN
+// contraction n = Σ_j γ[i][j]·x_j² in x6 (γ split into three bf16 planes, staged in LDS half the
+// output channels at a time; x² split in registers), y = x·√(β + n) | x / √(β + n), and y stored
+// as fp32 and/or in the h3 form (NHWC, or chunk-major [2][B][N/32][h][w][32]) and/or the x6
+// split form.
 #include <string.h>
 
 #include <type_traits>
@@ -34,47 +34,56 @@
 #include "k5_common.h"
 
 namespace iclr17 {
-namespace x6k {
+namespace h3k {
 using namespace bfm;
 
-__device__ __attribute__((aligned(16))) unsigned g_zero16x[4] = {0u, 0u, 0u, 0u};
+__device__ __attribute__((aligned(16))) unsigned g_zero16h[4] = {0u, 0u, 0u, 0u};
 
 // padding load of the counted-vmcnt DMA schedule (4 bytes per lane into the sink)
 __device__ __forceinline__ void sink4(void* lds_sink) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g_zero16x,
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g_zero16h,
                                    (__attribute__((address_space(3))) void*)lds_sink, 4, 0, 0);
 }
 
-enum XEpi : int { XE_GDN = 0, XE_IGDN = 1 };
+__device__ __forceinline__ f16v mfma32h(const u4& a, const u4& b, const f16v& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8v, a),
+                                                __builtin_bit_cast(h8v, b), c, 0, 0, 0);
+}
 
-struct XArgs {
-  const u16* in;        // split input [3][B][Hin][Win][CI] (bf16 bits)
+enum HEpi : int { HE_GDN = 0, HE_IGDN = 1 };
+
+struct HArgs {
+  const u16* in;        // h3 input [2][B][Hin][Win][CI] (fp16 bits)
   long in_plane;
-  const u16* w;         // iclr17_pack_x6k weights, [3][…] (plane stride w_plane)
+  const u16* w;         // iclr17_pack_h3k weights, [2][…] (plane stride w_plane) + trailer
   long w_plane;
+  const float* wscale;  // the packing's trailer: [0] max|w|, [1] 2⁻¹¹/(σ_a·σ_w)
   const float* bias;    // [CO]
   const float* beta;    // β_eff [CO]
-  const u16* gamma6;    // γ_eff split [3][CO/8][CO][8]
+  const u16* gamma6;    // γ_eff split (x6) [3][CO/8][CO][8]
   float* out;           // fp32 NHWC [B][Hout][Wout][CO] or null
-  u16* out_split;       // split output: NHWC [3][B][Hout][Wout][CO], or chunk-major
-  long out_plane;       //   [3][B][CO/32][Hout][Wout][32] (out_cm)
+  u16* out_h3;          // h3 output: NHWC [2][B][Hout][Wout][CO] or chunk-major (out_cm)
+  long out_h3_plane;    //   [2][B][CO/32][Hout][Wout][32]
+  u16* out_x6;          // x6 split output (NHWC or chunk-major, 3 planes) or null
+  long out_x6_plane;
   int out_cm;
+  int* range;           // set to 1 when a value does not fit the h3 form (nullable)
   int B, Hin, Win, Hout, Wout;
   int gh, gw;           // base grid (conv: output grid; deconv: input grid)
   int tiles_x, tiles_y;
 };
 
 template <int MODE, int TH, int CO, int CI, bool INT_IN>
-struct XK {
+struct HK {
   static constexpr int NW = TH / 2, NTHR = NW * 64;
   static constexpr int NT = CO / 32;           // 32-channel accumulator tiles per wave
   static constexpr int NCH = CI / 16;          // 16-channel chunks
   using P = Patch<MODE, TH>;
-  static constexpr int PL = INT_IN ? 1 : 3;    // input planes staged
+  static constexpr int PL = INT_IN ? 1 : 2;    // input planes staged
   static constexpr int PB = PL * P::BYTES;     // patch bytes (planes back to back)
   static constexpr int NQI = (PB + 1023) / 1024;
   static constexpr int PBUF = NQI * 1024;
-  static constexpr int SB = 3 * 2 * CO * 16;   // weight stage: [plane 3][half 2][CO][8] bf16
+  static constexpr int SB = 2 * 2 * CO * 16;   // weight stage: [plane 2][half 2][CO][8] fp16
   static constexpr int NBI = SB / 1024;
   static constexpr int NST = 4;
   static constexpr int MAIN = 2 * PBUF + NST * SB + 1024;
@@ -84,14 +93,14 @@ struct XK {
   static constexpr int LDS0 = MAIN > GBL * 1024 ? MAIN : GBL * 1024;
   static constexpr int BBOFF = (LDS0 + 1023) / 1024 * 1024;
   static constexpr int LDS = BBOFF + 2048;     // + bias, β_eff
-  static_assert(SB % 1024 == 0 && (2 * CO * 16) % 1024 == 0, "weight stage");
+  static_assert(SB % 1024 == 0, "weight stage");
   static_assert(NT % 2 == 0 && CI % 16 == 0, "tile shape");
   static_assert(LDS <= 160 * 1024, "LDS");
 };
 
 template <int MODE, int TH, int CO, int CI, int EPI, bool INT_IN, int PH>
-__device__ __forceinline__ void x6k_body(const XArgs& a, unsigned char* smem, int b, int ty, int tx) {
-  using KK = XK<MODE, TH, CO, CI, INT_IN>;
+__device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, int b, int ty, int tx) {
+  using KK = HK<MODE, TH, CO, CI, INT_IN>;
   using P = typename KK::P;
   using TP = Taps<MODE, PH>;
   constexpr int NT = KK::NT, NW = KK::NW, NCH = KK::NCH, S = TP::T;   // one tap per step
@@ -144,7 +153,7 @@ __device__ __forceinline__ void x6k_body(const XArgs& a, unsigned char* smem, in
       return;
     }
     const long src = piece_src(piece);
-    glds16(src >= 0 ? (const void*)(inb + src + c1 * 16) : (const void*)g_zero16x,
+    glds16(src >= 0 ? (const void*)(inb + src + c1 * 16) : (const void*)g_zero16h,
            sP + (c1 & 1) * KK::PBUF + piece * 1024);
   };
   // weights of this phase: per plane [NCH][S][2][CO][8]; the step's stage [plane][2][CO][8]
@@ -195,7 +204,7 @@ __device__ __forceinline__ void x6k_body(const XArgs& a, unsigned char* smem, in
   static_assert(CO <= 256, "bias / β stage");
   if (wave < 2) {
     const float* src = wave == 0 ? a.bias : a.beta;
-    glds16(lane * 4 < CO ? (const void*)(src + lane * 4) : (const void*)g_zero16x, sbb + wave * 256);
+    glds16(lane * 4 < CO ? (const void*)(src + lane * 4) : (const void*)g_zero16h, sbb + wave * 256);
   }
   for (int piece = wave; piece < KK::NQI; piece += NW) issue_piece(0, piece, true);
 #pragma unroll
@@ -226,24 +235,16 @@ __device__ __forceinline__ void x6k_body(const XArgs& a, unsigned char* smem, in
       stage = stage + 1 == NST ? 0 : stage + 1;
       const int to = P::template tap_off<PH>(s);
       const u4 bh = *(lu4p)(pbuf + to);
-      u4 bm, bl;
-      if constexpr (!INT_IN) {
-        bm = *(lu4p)(pbuf + P::BYTES + to);
-        bl = *(lu4p)(pbuf + 2 * P::BYTES + to);
-      }
+      u4 bl;
+      if constexpr (!INT_IN) bl = *(lu4p)(pbuf + P::BYTES + to);
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
-        const u4 ah = *(lu4p)(wb + i * 512);
-        const u4 am = *(lu4p)(wb + APL + i * 512);
-        const u4 al = *(lu4p)(wb + 2 * APL + i * 512);
-        f16v t = mfma32(al, bh, acc[i]);
-        if constexpr (!INT_IN) {
-          t = mfma32(ah, bl, t);
-          t = mfma32(am, bm, t);
-        }
-        t = mfma32(am, bh, t);
-        if constexpr (!INT_IN) t = mfma32(ah, bm, t);
-        acc[i] = mfma32(ah, bh, t);
+        const u4 wh = *(lu4p)(wb + i * 512);
+        const u4 wl = *(lu4p)(wb + APL + i * 512);
+        f16v t = acc[i];
+        if constexpr (!INT_IN) t = mfma32h(wh, bl, t);
+        t = mfma32h(wl, bh, t);
+        acc[i] = mfma32h(h3_x2048(wh), bh, t);
       }
       // the step's DMA group after its fragment reads: an LDS read after an LDS-DMA of unknown
       // destination makes the compiler wait for that DMA (s_waitcnt vmcnt(0)) first
@@ -269,25 +270,17 @@ __device__ __forceinline__ void x6k_body(const XArgs& a, unsigned char* smem, in
   const int oy = MODE == BM_CONV ? gy : 2 * gy + (PH >> 1);
   const int ox = MODE == BM_CONV ? gx : 2 * gx + (PH & 1);
   const long o = ((long)b * a.Hout + oy) * a.Wout + ox;
+  const float dsc = a.wscale[1];   // 2⁻¹¹/(σ_a·σ_w): exact
 #pragma unroll
   for (int i = 0; i < NT; ++i)
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       const f4 bv = *(const f4*)(sbb + 32 * i + 8 * m + 4 * h);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][4 * m + j] += bv[j];   // x = conv + bias
+      for (int j = 0; j < 4; ++j) acc[i][4 * m + j] = acc[i][4 * m + j] * dsc + bv[j];   // x = conv + bias
     }
   constexpr int NTH = KK::NTH, KB = KK::KB;
-#ifdef ICLR17_X6K_NOEPI
-  if (inside) for (int i = 0; i < NT; ++i) for (int m = 0; m < 4; ++m) *(f4*)(a.out + o * CO + 32 * i + 8 * m + 4 * h) = f4{acc[i][4*m], acc[i][4*m+1], acc[i][4*m+2], acc[i][4*m+3]};
-  return;
-#endif
-  auto split_bits = [](float v, unsigned& hb, unsigned& mb, unsigned& lb) {
-    hb = __float_as_uint(v) & 0xffff0000u;
-    const float r = v - __uint_as_float(hb);
-    mb = __float_as_uint(r) & 0xffff0000u;
-    lb = __float_as_uint(r - __uint_as_float(mb));
-  };
+  bool ovf = false;
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf) {
     if (hf) __syncthreads();   // every wave's pass-0 γ reads done before the restage
@@ -366,35 +359,49 @@ __device__ __forceinline__ void x6k_body(const XArgs& a, unsigned char* smem, in
         for (int j = 0; j < 4; ++j) {
           const float s = sqrtf(n[il][4 * m + j] + be[j]);
           const float x = acc[i][4 * m + j];
-          y[j] = EPI == XE_IGDN ? x * s : x / s;
+          y[j] = EPI == HE_IGDN ? x * s : x / s;
         }
         if (!inside) continue;
         if (a.out) *(f4*)(a.out + o * CO + ch) = y;
-        if (a.out_split) {
-          unsigned hb[4], mb[4], lb[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) split_bits(y[j], hb[j], mb[j], lb[j]);
+        if (a.out_h3) {
+          uint2 hb, lb;
+          h3_split4(y, hb, lb, ovf);
           const long so = a.out_cm ? (((long)b * (CO / 32) + i) * a.Hout + oy) * a.Wout * 32 + (long)ox * 32 + 8 * m + 4 * h
                                    : o * CO + ch;
-          *(uint2*)(a.out_split + so) = uint2{__builtin_amdgcn_perm(hb[1], hb[0], 0x07060302u),
-                                              __builtin_amdgcn_perm(hb[3], hb[2], 0x07060302u)};
-          *(uint2*)(a.out_split + a.out_plane + so) = uint2{__builtin_amdgcn_perm(mb[1], mb[0], 0x07060302u),
+          *(uint2*)(a.out_h3 + so) = hb;
+          *(uint2*)(a.out_h3 + a.out_h3_plane + so) = lb;
+        }
+        if (a.out_x6) {
+          unsigned hb[4], mb[4], lb[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            hb[j] = __float_as_uint(y[j]) & 0xffff0000u;
+            const float r = y[j] - __uint_as_float(hb[j]);
+            mb[j] = __float_as_uint(r) & 0xffff0000u;
+            lb[j] = __float_as_uint(r - __uint_as_float(mb[j]));
+          }
+          const long so = a.out_cm ? (((long)b * (CO / 32) + i) * a.Hout + oy) * a.Wout * 32 + (long)ox * 32 + 8 * m + 4 * h
+                                   : o * CO + ch;
+          *(uint2*)(a.out_x6 + so) = uint2{__builtin_amdgcn_perm(hb[1], hb[0], 0x07060302u),
+                                           __builtin_amdgcn_perm(hb[3], hb[2], 0x07060302u)};
+          *(uint2*)(a.out_x6 + a.out_x6_plane + so) = uint2{__builtin_amdgcn_perm(mb[1], mb[0], 0x07060302u),
                                                             __builtin_amdgcn_perm(mb[3], mb[2], 0x07060302u)};
-          *(uint2*)(a.out_split + 2 * a.out_plane + so) = uint2{__builtin_amdgcn_perm(lb[1], lb[0], 0x07060302u),
+          *(uint2*)(a.out_x6 + 2 * a.out_x6_plane + so) = uint2{__builtin_amdgcn_perm(lb[1], lb[0], 0x07060302u),
                                                                 __builtin_amdgcn_perm(lb[3], lb[2], 0x07060302u)};
         }
       }
     }
   }
+  if (ovf && a.range) atomicOr(a.range, 1);   // vector atomic, per offending lane (rare)
 }
 
-// INT_OK: the caller guarantees an integer-valued input (ŷ). A workgroup then checks that every
-// value of its input window is below 256 in magnitude (so exact in the hi plane: the mid and lo
-// planes are zero) and runs the INT_IN body; otherwise (and for Inf / NaN) the full body.
+// INT_OK: the caller guarantees an integer-valued input (ŷ). A workgroup then checks that the lo
+// plane of its input window is zero (every value exact in the hi plane) and runs the INT_IN body;
+// otherwise the full body.
 template <int MODE, int TH, int CO, int CI, int EPI, bool INT_OK>
-__global__ void __launch_bounds__(TH / 2 * 64, 1) x6k_kernel(const XArgs a) {
-  using KK = XK<MODE, TH, CO, CI, false>;
-  static_assert(KK::LDS >= XK<MODE, TH, CO, CI, true>::LDS, "LDS");
+__global__ void __launch_bounds__(TH / 2 * 64, 1) h3k_kernel(const HArgs a) {
+  using KK = HK<MODE, TH, CO, CI, false>;
+  static_assert(KK::LDS >= HK<MODE, TH, CO, CI, true>::LDS, "LDS");
   __shared__ __attribute__((aligned(16))) unsigned char smem[KK::LDS];
   int bid = blockIdx.x;
   const int per_ph = a.tiles_x * a.tiles_y * a.B;
@@ -406,13 +413,12 @@ __global__ void __launch_bounds__(TH / 2 * 64, 1) x6k_kernel(const XArgs a) {
   const int b = bid / a.tiles_y;
   bool small = false;
   if constexpr (INT_OK) {
-    // the hi plane of the window the patch stages, all CI channels, 8 values per 16-byte load:
-    // |v| < 256 ⇔ (bits & 0x7fff) < 0x4380 (256 in bf16; Inf / NaN compare above it)
+    // the lo plane of the window the patch stages, all CI channels, 8 values per 16-byte load
     using P = Patch<MODE, TH>;
     constexpr int COLS = MODE == BM_CONV ? 35 : 18, PER = COLS * CI / 8;
     const int iy0 = MODE == BM_CONV ? 2 * ty * TH - 2 : ty * TH - 1;
     const int ix0 = MODE == BM_CONV ? 2 * tx * 16 - 2 : tx * 16 - 1;
-    const u16* inb = a.in + (long)b * a.Hin * a.Win * CI;
+    const u16* inb = a.in + a.in_plane + (long)b * a.Hin * a.Win * CI;
     // every load issued before the first compare (one memory latency, not one per load)
     constexpr int NTHR = TH / 2 * 64, IT = (P::ROWS * PER + NTHR - 1) / NTHR;
     u4 v[IT];
@@ -428,20 +434,19 @@ __global__ void __launch_bounds__(TH / 2 * 64, 1) x6k_kernel(const XArgs a) {
 #pragma unroll
     for (int it = 0; it < IT; ++it)
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        bad |= (unsigned)((v[it][e] & 0x7fffu) >= 0x4380u) | (unsigned)(((v[it][e] >> 16) & 0x7fffu) >= 0x4380u);
+      for (int e = 0; e < 4; ++e) bad |= v[it][e] & 0x7fff7fffu;   // ±0 only
     small = __syncthreads_or(bad) == 0;
   }
   auto run = [&](auto int_in) {
     constexpr bool II = decltype(int_in)::value;
     if constexpr (MODE == BM_CONV) {
-      x6k_body<MODE, TH, CO, CI, EPI, II, 0>(a, smem, b, ty, tx);
+      h3k_body<MODE, TH, CO, CI, EPI, II, 0>(a, smem, b, ty, tx);
     } else {
       switch (ph) {   // wave-uniform: the tap lists are compile-time per phase
-        case 0: x6k_body<MODE, TH, CO, CI, EPI, II, 0>(a, smem, b, ty, tx); break;
-        case 1: x6k_body<MODE, TH, CO, CI, EPI, II, 1>(a, smem, b, ty, tx); break;
-        case 2: x6k_body<MODE, TH, CO, CI, EPI, II, 2>(a, smem, b, ty, tx); break;
-        default: x6k_body<MODE, TH, CO, CI, EPI, II, 3>(a, smem, b, ty, tx); break;
+        case 0: h3k_body<MODE, TH, CO, CI, EPI, II, 0>(a, smem, b, ty, tx); break;
+        case 1: h3k_body<MODE, TH, CO, CI, EPI, II, 1>(a, smem, b, ty, tx); break;
+        case 2: h3k_body<MODE, TH, CO, CI, EPI, II, 2>(a, smem, b, ty, tx); break;
+        default: h3k_body<MODE, TH, CO, CI, EPI, II, 3>(a, smem, b, ty, tx); break;
       }
     }
   };
@@ -450,12 +455,42 @@ __global__ void __launch_bounds__(TH / 2 * 64, 1) x6k_kernel(const XArgs a) {
 }
 
 // ---------------------------------------------------------------------------- packing
-// W → three planes, per plane [blocks][2][CO][8] bf16 where a block is one (chunk, tap):
+// max|w| over the tensor (one workgroup; the weights are ≤ 1 M values): trailer[0]
+__global__ void __launch_bounds__(1024) absmax_kernel(const float* __restrict__ w, long n,
+                                                      float* __restrict__ trailer) {
+  __shared__ float red[16];
+  float m = 0.f;
+  for (long i = threadIdx.x; i < n; i += 1024) m = fmaxf(m, fabsf(w[i]));
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = red[0];
+    for (int i = 1; i < 16; ++i) r = fmaxf(r, red[i]);
+    trailer[0] = r;
+  }
+}
+
+// σ_w = 2^(3 − ⌊log2 max|w|⌋) (max|w|·σ_w ∈ [8, 16), so hi·2¹¹ < 2¹⁵); 1 for an all-zero or
+// non-finite tensor (whose products are then what fp32 makes of them)
+__device__ __forceinline__ int h3_weight_exp(float mx) {
+  if (!(mx > 0.f) || !(mx <= 3.40282347e38f)) return 0;
+  int e;
+  frexpf(mx, &e);   // mx = f·2^e, f ∈ [0.5, 1)
+  return 3 - (e - 1);
+}
+
+// W → two planes, per plane [blocks][2][CO][8] fp16 where a block is one (chunk, tap):
 // conv (W[co][ci][5][5]): block c·25 + t, tap t = 5·ky + kx;
 // deconv (W[ci][co][5][5]): the four stride phases back to back, phase p's blocks c·T_p + t with
 // the tap order of Taps<BM_DECONV, p>. Element (block, h, co, j) = W at input channel 16c + 8h + j.
-__global__ void __launch_bounds__(256) pack_x6k_kernel(const float* __restrict__ w, int N, int deconv,
-                                                       long groups, u16* __restrict__ out) {
+__global__ void __launch_bounds__(256) pack_h3k_kernel(const float* __restrict__ w, int N, int deconv,
+                                                       long groups, u16* __restrict__ out,
+                                                       float* __restrict__ trailer) {
+  const int se = h3_weight_exp(trailer[0]);
+  const float sw = ldexpf(1.0f, se);
+  if (blockIdx.x == 0 && threadIdx.x == 0) trailer[1] = ldexpf(1.0f, -11 - kH3SaLog2 - se);
   const int nch = N / 16;
   for (long g = (long)blockIdx.x * 256 + threadIdx.x; g < groups; g += (long)gridDim.x * 256) {
     const int co = (int)(g % N);
@@ -483,70 +518,170 @@ __global__ void __launch_bounds__(256) pack_x6k_kernel(const float* __restrict__
       ky = (p >> 1) == 0 ? 2 * (t / nx) : 2 * (t / nx) + 1;
       kx = (p & 1) == 0 ? 2 * (t % nx) : 2 * (t % nx) + 1;
     }
-    float v[8];
+    unsigned short hv[8], lv[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int ci = 16 * c + 8 * h + j;
-      v[j] = deconv ? w[(((long)ci * N + co) * 5 + ky) * 5 + kx] : w[(((long)co * N + ci) * 5 + ky) * 5 + kx];
+      const float v = (deconv ? w[(((long)ci * N + co) * 5 + ky) * 5 + kx]
+                              : w[(((long)co * N + ci) * 5 + ky) * 5 + kx]) * sw;
+      const _Float16 hh = (_Float16)v;
+      hv[j] = h16_bits(hh);
+      lv[j] = h16_bits((_Float16)((v - (float)hh) * 2048.0f));
     }
-    u4 hi, mi, lo;
-    split8(f4{v[0], v[1], v[2], v[3]}, f4{v[4], v[5], v[6], v[7]}, hi, mi, lo);
-    *(u4*)(out + g * 8) = hi;
-    *(u4*)(out + groups * 8 + g * 8) = mi;
-    *(u4*)(out + 2 * groups * 8 + g * 8) = lo;
+    u4 H, L;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      H[i] = hv[2 * i] | ((unsigned)hv[2 * i + 1] << 16);
+      L[i] = lv[2 * i] | ((unsigned)lv[2 * i + 1] << 16);
+    }
+    *(u4*)(out + g * 8) = H;
+    *(u4*)(out + groups * 8 + g * 8) = L;
   }
 }
 
-template <int N, int TH, bool INT_IN>
-int launch_deconv(const XArgs& a0, hipStream_t st) {
-  XArgs a = a0;
-  a.tiles_y = (a.gh + TH - 1) / TH;
-  a.tiles_x = (a.gw + 15) / 16;
-  hipLaunchKernelGGL((x6k_kernel<BM_DECONV, TH, N, N, XE_IGDN, INT_IN>),
-                     dim3(a.tiles_x * a.tiles_y * a.B * 4), dim3(TH / 2 * 64), 0, st, a);
-  return check_launch("deconv_igdn_x6k");
+// A packed operand [taps][K/4][N][4] fp32 → two fp16 planes [2][taps][K/8][N][8] of w·σ_w (the
+// H3 engine's B-fragment layout, the x6 split_packed's with two planes), trailer after them
+__global__ void __launch_bounds__(256) split_packed_h3_kernel(const float* __restrict__ w, int K,
+                                                              int N, long groups,
+                                                              u16* __restrict__ out,
+                                                              float* __restrict__ trailer) {
+  const int se = h3_weight_exp(trailer[0]);
+  const float sw = ldexpf(1.0f, se);
+  if (blockIdx.x == 0 && threadIdx.x == 0) trailer[1] = ldexpf(1.0f, -11 - kH3SaLog2 - se);
+  for (long g = (long)blockIdx.x * 256 + threadIdx.x; g < groups; g += (long)gridDim.x * 256) {
+    const long tk = g / N;
+    const int col = (int)(g - tk * N);
+    const long tap = tk / (K / 8);
+    const int k8 = (int)(tk - tap * (K / 8));
+    const float* src = w + ((tap * (K / 4) + 2 * k8) * N + col) * 4;
+    const f4 x0 = *(const f4*)src, x1 = *(const f4*)(src + (long)N * 4);
+    const float v[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+    u4 H, L;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      unsigned short hv[2], lv[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const float x = v[2 * i + e] * sw;
+        const _Float16 hh = (_Float16)x;
+        hv[e] = h16_bits(hh);
+        lv[e] = h16_bits((_Float16)((x - (float)hh) * 2048.0f));
+      }
+      H[i] = hv[0] | ((unsigned)hv[1] << 16);
+      L[i] = lv[0] | ((unsigned)lv[1] << 16);
+    }
+    *(u4*)(out + g * 8) = H;
+    *(u4*)(out + groups * 8 + g * 8) = L;
+  }
 }
 
-}  // namespace x6k
+// fp32 → h3 planes (x·σ_a split): iclr17_h3_planes
+__global__ void __launch_bounds__(256) h3_planes_kernel(const float* __restrict__ x, long n4,
+                                                        long plane, u16* __restrict__ out,
+                                                        int* range) {
+  bool ovf = false;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    uint2 hb, lb;
+    h3_split4(*(const f4*)(x + 4 * i), hb, lb, ovf);
+    *(uint2*)(out + 4 * i) = hb;
+    *(uint2*)(out + plane + 4 * i) = lb;
+  }
+  if (ovf && range) atomicOr(range, 1);
+}
+
+template <int N, int TH, bool INT_OK>
+int launch_deconv(const HArgs& a0, hipStream_t st) {
+  HArgs a = a0;
+  a.tiles_y = (a.gh + TH - 1) / TH;
+  a.tiles_x = (a.gw + 15) / 16;
+  hipLaunchKernelGGL((h3k_kernel<BM_DECONV, TH, N, N, HE_IGDN, INT_OK>),
+                     dim3(a.tiles_x * a.tiles_y * a.B * 4), dim3(TH / 2 * 64), 0, st, a);
+  return check_launch("deconv_igdn_h3");
+}
+
+}  // namespace h3k
 }  // namespace iclr17
 
 using namespace iclr17;
-using namespace iclr17::x6k;
+using namespace iclr17::h3k;
 
 extern "C" {
 
-size_t iclr17_x6k_weight_size(int which, int N) {
+size_t iclr17_h3k_weight_size(int which, int N) {
   if (N != 128 && N != 192) return 0;
-  if (which != ICLR17_X6K_CONV5 && which != ICLR17_X6K_DECONV5) return 0;
-  return (size_t)3 * (N / 16) * 25 * 2 * N * 8;   // both: 25 (chunk, tap) blocks per chunk
+  if (which != ICLR17_H3K_CONV5 && which != ICLR17_H3K_DECONV5) return 0;
+  // two planes of 25 (chunk, tap) blocks per 16-channel chunk, + the 16-byte trailer
+  return (size_t)2 * (N / 16) * 25 * 2 * N * 8 + 8;
 }
 
-int iclr17_pack_x6k(int which, const float* w, uint16_t* out, int N, void* stream) {
-  const size_t total = iclr17_x6k_weight_size(which, N);
-  ICLR17_REQUIRE(total > 0, ICLR17_EUNSUPPORTED, "pack_x6k: kind %d, N=%d unsupported", which, N);
-  ICLR17_REQUIRE(w && out, ICLR17_EINVAL, "pack_x6k: null pointer");
-  const long groups = (long)(total / 24);
+int iclr17_pack_h3k(int which, const float* w, uint16_t* out, int N, void* stream) {
+  const size_t total = iclr17_h3k_weight_size(which, N);
+  ICLR17_REQUIRE(total > 0, ICLR17_EUNSUPPORTED, "pack_h3k: kind %d, N=%d unsupported", which, N);
+  ICLR17_REQUIRE(w && out, ICLR17_EINVAL, "pack_h3k: null pointer");
+  const long groups = (long)((total - 8) / 16);
+  float* trailer = (float*)(out + (total - 8));
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(absmax_kernel, dim3(1), dim3(1024), 0, st, w, (long)N * N * 25, trailer);
+  int rc = check_launch("pack_h3k absmax");
+  if (rc) return rc;
   const int blocks = (int)((groups + 255) / 256 < 4096 ? (groups + 255) / 256 : 4096);
-  hipLaunchKernelGGL(pack_x6k_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, N,
-                     which == ICLR17_X6K_DECONV5 ? 1 : 0, groups, out);
-  return check_launch("pack_x6k");
+  hipLaunchKernelGGL(pack_h3k_kernel, dim3(blocks), dim3(256), 0, st, w, N,
+                     which == ICLR17_H3K_DECONV5 ? 1 : 0, groups, out, trailer);
+  return check_launch("pack_h3k");
 }
 
-int iclr17_synthesis_deconv_igdn_x6k(const uint16_t* in_split, int B, int h, int w, int N,
-                                     const uint16_t* w_x6k, const float* bias,
-                                     const float* beta_eff, const uint16_t* gamma_split,
-                                     float* out, uint16_t* out_split, int out_cm, int int_in,
-                                     void* stream) {
-  ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "deconv_igdn_x6k: N=%d", N);
-  ICLR17_REQUIRE(in_split && w_x6k && bias && beta_eff && gamma_split && (out || out_split) &&
+size_t iclr17_split_packed_h3_size(int taps, int K, int N) {
+  if (taps <= 0 || K <= 0 || K % 8 || N <= 0) return 0;
+  return (size_t)2 * taps * K * N + 8;
+}
+
+int iclr17_split_packed_h3(const float* packed, int taps, int K, int N, uint16_t* planes,
+                           void* stream) {
+  const size_t total = iclr17_split_packed_h3_size(taps, K, N);
+  ICLR17_REQUIRE(packed && planes && total > 0, ICLR17_EINVAL, "split_packed_h3: bad arguments");
+  const long groups = (long)taps * (K / 8) * N;
+  float* trailer = (float*)(planes + (total - 8));
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(absmax_kernel, dim3(1), dim3(1024), 0, st, packed, (long)taps * K * N, trailer);
+  int rc = check_launch("split_packed_h3 absmax");
+  if (rc) return rc;
+  const int blocks = (int)((groups + 255) / 256 < 4096 ? (groups + 255) / 256 : 4096);
+  hipLaunchKernelGGL(split_packed_h3_kernel, dim3(blocks), dim3(256), 0, st, packed, K, N, groups,
+                     planes, trailer);
+  return check_launch("split_packed_h3");
+}
+
+int iclr17_h3_planes(const float* x, long n, uint16_t* planes, int* range_flag, void* stream) {
+  ICLR17_REQUIRE(x && planes && n >= 0 && n % 4 == 0, ICLR17_EINVAL, "h3_planes: bad arguments");
+  if (n == 0) return ICLR17_OK;
+  const long n4 = n / 4;
+  const int blocks = (int)((n4 + 255) / 256 < 8192 ? (n4 + 255) / 256 : 8192);
+  hipLaunchKernelGGL(h3_planes_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, n4, n,
+                     planes, range_flag);
+  return check_launch("h3_planes");
+}
+
+int iclr17_synthesis_deconv_igdn_h3(const uint16_t* in_h3, int B, int h, int w, int N,
+                                    const uint16_t* w_h3k, const float* bias,
+                                    const float* beta_eff, const uint16_t* gamma_split,
+                                    float* out, uint16_t* out_h3, uint16_t* out_x6, int out_cm,
+                                    int int_in, int* range_flag, void* stream) {
+  ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "deconv_igdn_h3: N=%d", N);
+  ICLR17_REQUIRE(in_h3 && w_h3k && bias && beta_eff && gamma_split && (out || out_h3 || out_x6) &&
                      B > 0 && h > 0 && w > 0,
-                 ICLR17_EINVAL, "deconv_igdn_x6k: bad arguments");
-  XArgs a;
+                 ICLR17_EINVAL, "deconv_igdn_h3: bad arguments");
+  HArgs a;
   memset(&a, 0, sizeof(a));
-  a.in = in_split; a.in_plane = (long)B * h * w * N;
-  a.w = w_x6k; a.w_plane = (long)(N / 16) * 25 * 2 * N * 8;
+  a.in = in_h3; a.in_plane = (long)B * h * w * N;
+  const size_t wsz = iclr17_h3k_weight_size(ICLR17_H3K_DECONV5, N);
+  a.w = w_h3k; a.w_plane = (long)(wsz - 8) / 2;
+  a.wscale = (const float*)(w_h3k + (wsz - 8));
   a.bias = bias; a.beta = beta_eff; a.gamma6 = gamma_split;
-  a.out = out; a.out_split = out_split; a.out_plane = (long)B * 4 * h * w * N; a.out_cm = out_cm ? 1 : 0;
+  a.out = out;
+  a.out_h3 = out_h3; a.out_h3_plane = (long)B * 4 * h * w * N;
+  a.out_x6 = out_x6; a.out_x6_plane = (long)B * 4 * h * w * N;
+  a.out_cm = out_cm ? 1 : 0;
+  a.range = range_flag;
   a.B = B; a.Hin = h; a.Win = w; a.Hout = 2 * h; a.Wout = 2 * w;
   a.gh = h; a.gw = w;
   hipStream_t st = (hipStream_t)stream;

@@ -250,11 +250,8 @@ def deconv_igdn(h: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Tenso
 
 
 # ------------------------------------------------------------- x6 (bf16x6) precision mode
-PRECISIONS = ("x6", "fp32", "bf16")
+PRECISIONS = ("x6", "h3", "fp32", "bf16")
 _precision = os.environ.get("ICLR17_PRECISION", "x6")
-# ICLR17_X6K=1: the x6 decoder layers on the 32x32x16 engine (csrc/engine_x6k.hip) instead of
-# the 16x16x32 engine (A/B; DESIGN §5 has the measurements that keep the default)
-X6K = os.environ.get("ICLR17_X6K", "0") == "1"
 
 
 def precision() -> str:
@@ -435,38 +432,183 @@ def deconv_igdn_x6(hs: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: T
     return split, out, pre
 
 
-def pack_x6k(which: int, w: Tensor, N: int) -> Tensor:
-    """k5 weights → three exact bf16 planes in the x6k engine's A-fragment step layout
-    (ICLR17_X6K_CONV5 / ICLR17_X6K_DECONV5)."""
-    _check(w, "weight", 4)
-    size = query("iclr17_x6k_weight_size", which, N)
-    if size == 0:
-        raise Iclr17Error(f"iclr17: pack_x6k: kind {which}, N={N} unsupported")
-    out = torch.empty(size, device=w.device, dtype=torch.int16)
-    call("iclr17_pack_x6k", which, _p(w.detach().contiguous()), _p(out), N, _stream(w))
+# ------------------------------------------------------------------ h3 form (csrc/engine_h3.hip)
+# An h3 activation is an int16 tensor [2, B, h, w, N] (or chunk-major [2, B, N/32, h, w, 32]): the
+# fp16 bit patterns of hi = rne16(x·2^-6) and lo = rne16((x·2^-6 − hi)·2^11) (common.h "h3 form").
+H3_SIGMA_A = 2.0 ** -6
+_range_flags = {}
+
+
+def h3_range_flag(device) -> Tensor:
+    """The device's h3 range flag (int32, 0 = every value fitted the h3 form so far)."""
+    dev = torch.device(device)
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    f = _range_flags.get(dev)
+    if f is None:
+        f = torch.zeros(1, device=dev, dtype=torch.int32)
+        _range_flags[dev] = f
+    return f
+
+
+def check_h3_range(device) -> None:
+    """Raise (and clear the flag) when an h3 kernel met a value of magnitude ≥ 2^22, which the
+    h3 form cannot hold. Synchronises with the device."""
+    f = h3_range_flag(device)
+    if int(f.item()) != 0:
+        f.zero_()
+        raise Iclr17Error("iclr17: an activation of magnitude >= 2^22 does not fit the h3 form; "
+                          "run this input with kernels.set_precision('x6')")
+
+
+def _check_h3(s: Tensor, what: str):
+    if not isinstance(s, Tensor) or s.dtype != torch.int16 or s.dim() != 5 or s.shape[0] != 2:
+        raise Iclr17Error(f"iclr17: {what} must be an h3-form int16 tensor [2,B,h,w,N]")
+    if not s.is_cuda:
+        raise Iclr17Error(f"iclr17: {what} must be a device tensor (there is no CPU path)")
+    if not s.is_contiguous():
+        raise Iclr17Error(f"iclr17: {what} must be contiguous")
+
+
+def h3_planes(x: Tensor) -> Tensor:
+    """fp32 tensor (numel % 4 == 0) → h3 form [2, *x.shape]."""
+    _check(x, "tensor", x.dim())
+    x = x.contiguous()
+    if x.numel() % 4:
+        raise Iclr17Error("iclr17: h3_planes needs a multiple of 4 elements")
+    out = torch.empty((2,) + tuple(x.shape), device=x.device, dtype=torch.int16)
+    call("iclr17_h3_planes", _p(x), x.numel(), _p(out), _p(h3_range_flag(x.device)), _stream(x))
     return out
 
 
-def deconv_igdn_x6k(hs: Tensor, wx: Tensor, bias: Tensor, beta_eff: Tensor, g6: Tensor,
-                    want_split: bool = True, want_f32: bool = False, chunk_major: bool = False,
-                    int_in: bool = False):
-    """synthesis_17.py:15-22 on the 32x32x16 x6 engine (csrc/engine_x6k.hip): split input
-    [3,B,h,w,N] → (split | None, fp32 | None). wx: ``pack_x6k(ICLR17_X6K_DECONV5, …)``; g6: the
-    IGDN's split γ. ``int_in``: the input is ŷ (integers exact in one bf16; its other planes are
-    zero and are not read)."""
-    _check_split(hs, "activation")
+def merge_h3(s: Tensor) -> Tensor:
+    """h3 form → fp32 (hi + lo·2^-11)/σ_a; a chunk-major [2,B,N/32,h,w,32] comes back as NHWC.
+    Test/debug helper (torch ops, exact in fp32)."""
+    if s.dim() == 6:
+        s = s.permute(0, 1, 3, 4, 2, 5).reshape(2, s.shape[1], s.shape[3], s.shape[4], -1)
+    h = s.view(torch.float16).to(torch.float32)
+    return (h[0] + h[1] * (2.0 ** -11)) / H3_SIGMA_A
+
+
+def pack_h3k(which: int, w: Tensor, N: int) -> Tensor:
+    """k5 weights → the h3 engine's two fp16 planes (per-tensor power-of-two scale) + trailer
+    (ICLR17_H3K_CONV5 / ICLR17_H3K_DECONV5)."""
+    _check(w, "weight", 4)
+    size = query("iclr17_h3k_weight_size", which, N)
+    if size == 0:
+        raise Iclr17Error(f"iclr17: pack_h3k: kind {which}, N={N} unsupported")
+    out = torch.empty(size, device=w.device, dtype=torch.int16)
+    call("iclr17_pack_h3k", which, _p(w.detach().contiguous()), _p(out), N, _stream(w))
+    return out
+
+
+def split_packed_h3(packed: Tensor, taps: int, K: int, N: int) -> Tensor:
+    """Packed operand [taps][K/4][N][4] fp32 → the h3 engine's two fp16 planes + trailer (int16,
+    ``iclr17_split_packed_h3_size`` elements): conv2 / conv3 weights of the h3 form."""
+    _check(packed, "packed operand", packed.dim())
+    if packed.numel() != taps * K * N:
+        raise Iclr17Error(f"iclr17: split_packed_h3: {packed.numel()} != {taps}*{K}*{N}")
+    size = query("iclr17_split_packed_h3_size", taps, K, N)
+    if size == 0:
+        raise Iclr17Error("iclr17: split_packed_h3: bad shape")
+    out = torch.empty(size, device=packed.device, dtype=torch.int16)
+    call("iclr17_split_packed_h3", _p(packed.contiguous()), taps, K, N, _p(out), _stream(packed))
+    return out
+
+
+def conv1x6_gdn_h3(x: Tensor, w_split: Tensor, bias: Tensor, beta_eff: Tensor, g6: Tensor, N: int,
+                   want_f32: bool = False):
+    """``conv1x6_gdn`` with the output in the h3 form: returns (h3 [2,B,H/4,W/4,N], fp32 | None)."""
+    _check(x, "image", 4)
+    B, C, H, W = x.shape
+    if C != 3:
+        raise Iclr17Error(f"iclr17: the analysis transform takes 3-channel images (got {C})")
+    _check_image_dims(H, W)
+    _check_channels(N)
+    if w_split.dtype != torch.int16 or w_split.numel() != 3 * 256 * N:
+        raise Iclr17Error("iclr17: conv1x6_gdn_h3 needs the split ICLR17_W_CONV1_X6 packing")
+    x = x.contiguous()
+    h3 = torch.empty(2, B, H // 4, W // 4, N, device=x.device, dtype=torch.int16)
+    out = torch.empty(B, H // 4, W // 4, N, device=x.device) if want_f32 else None
+    call("iclr17_analysis_conv1x6_gdn_h3", _p(x), B, H, W, N, _p(w_split), _p(bias), _p(beta_eff),
+         _p(g6), _p(out), _p(h3), _p(h3_range_flag(x.device)), _stream(x))
+    return h3, out
+
+
+def conv2_gdn_h3(hs: Tensor, wh: Tensor, bias: Tensor, beta_eff: Tensor, g6: Tensor,
+                 want_h3: bool = True, want_f32: bool = False, want_x6: bool = False):
+    """analysis_17.py:18-21 in the h3 form: h3 input [2,B,H/4,W/4,N] → (h3 | None, fp32 | None,
+    x6 split | None). wh: ``split_packed_h3(pack_weight(ICLR17_W_CONV5, w), 25, N, N)``."""
+    _check_h3(hs, "activation")
+    _, B, h4, w4, N = hs.shape
+    _check_channels(N)
+    H, W = 4 * h4, 4 * w4
+    _check_image_dims(H, W)
+    if wh.numel() != query("iclr17_split_packed_h3_size", 25, N, N):
+        raise Iclr17Error("iclr17: conv2_gdn_h3 needs split_packed_h3 of the conv5 packing")
+    if not (want_h3 or want_f32 or want_x6):
+        raise Iclr17Error("iclr17: conv2_gdn_h3 needs an output")
+    h3 = torch.empty(2, B, h4 // 2, w4 // 2, N, device=hs.device, dtype=torch.int16) if want_h3 else None
+    x6 = torch.empty(3, B, h4 // 2, w4 // 2, N, device=hs.device, dtype=torch.int16) if want_x6 else None
+    out = torch.empty(B, h4 // 2, w4 // 2, N, device=hs.device) if want_f32 else None
+    call("iclr17_analysis_conv2_gdn_h3", _p(hs), B, H, W, N, _p(wh), _p(bias), _p(beta_eff), _p(g6),
+         _p(out), _p(h3), _p(x6), _p(h3_range_flag(hs.device)), _stream(hs))
+    return h3, out, x6
+
+
+def conv3_quant_rate_h3(hs: Tensor, wh: Tensor, rate_packed: Tensor,
+                        noise: Optional[Tensor] = None, want_y: bool = False,
+                        rtab: Optional[Tensor] = None, want_h3: bool = True):
+    """analysis_17.py:22 + model.py:48-56,71-73 in the h3 form. Returns (y_hat NHWC, bits_partial
+    [B, rate_partials_per_image], y | None, y_hat h3 | None)."""
+    _check_h3(hs, "activation")
+    _, B, h8, w8, N = hs.shape
+    _check_channels(N)
+    H, W = 8 * h8, 8 * w8
+    _check_image_dims(H, W)
+    if wh.numel() != query("iclr17_split_packed_h3_size", 25, N, N):
+        raise Iclr17Error("iclr17: conv3_quant_rate_h3 needs split_packed_h3 of the conv5 packing")
+    mode = _lib.ICLR17_QUANT_ROUND
+    if noise is not None:
+        _check(noise, "noise", 4)
+        if tuple(noise.shape) != (B, N, h8 // 2, w8 // 2):
+            raise Iclr17Error(f"iclr17: noise must be {(B, N, h8 // 2, w8 // 2)} (got {tuple(noise.shape)})")
+        noise = noise.contiguous()
+        mode = _lib.ICLR17_QUANT_NOISE
+    y_hat = torch.empty(B, h8 // 2, w8 // 2, N, device=hs.device, dtype=torch.float32)
+    y_hat_h3 = torch.empty(2, B, h8 // 2, w8 // 2, N, device=hs.device, dtype=torch.int16) if want_h3 else None
+    y = torch.empty_like(y_hat) if want_y else None
+    T = rate_partials_per_image(H, W, N)
+    partial = torch.empty(B, T, device=hs.device, dtype=torch.float64)
+    call("iclr17_analysis_conv3_quant_rate_h3", _p(hs), B, H, W, N, _p(wh), mode, _p(noise),
+         _p(rate_packed), _p(rtab), _p(y), _p(y_hat), _p(y_hat_h3), _p(partial),
+         _p(h3_range_flag(hs.device)), _stream(hs))
+    return y_hat, partial, y, y_hat_h3
+
+
+def deconv_igdn_h3(hs: Tensor, wh: Tensor, bias: Tensor, beta_eff: Tensor, g6: Tensor,
+                   want_h3: bool = True, want_f32: bool = False, want_x6: bool = False,
+                   chunk_major: bool = False, int_in: bool = False):
+    """synthesis_17.py:15-22 in the h3 form (csrc/engine_h3.hip): h3 input [2,B,h,w,N] →
+    (h3 | None, fp32 | None, x6 split | None). wh: ``pack_h3k(ICLR17_H3K_DECONV5, …)``; g6: the
+    IGDN's split γ. ``int_in``: the input is ŷ (a workgroup whose window has a zero lo plane skips
+    the lo products; same result). ``chunk_major`` applies to the h3 and x6 outputs."""
+    _check_h3(hs, "activation")
     _, B, hh, ww, N = hs.shape
     _check_channels(N)
-    if not (want_split or want_f32):
-        raise Iclr17Error("iclr17: deconv_igdn_x6k needs an output")
-    if wx.numel() != query("iclr17_x6k_weight_size", _lib.ICLR17_X6K_DECONV5, N):
-        raise Iclr17Error("iclr17: deconv_igdn_x6k needs the ICLR17_X6K_DECONV5 packing")
-    shape = (3, B, N // 32, 2 * hh, 2 * ww, 32) if chunk_major else (3, B, 2 * hh, 2 * ww, N)
-    split = torch.empty(shape, device=hs.device, dtype=torch.int16) if want_split else None
+    if not (want_h3 or want_f32 or want_x6):
+        raise Iclr17Error("iclr17: deconv_igdn_h3 needs an output")
+    if wh.numel() != query("iclr17_h3k_weight_size", _lib.ICLR17_H3K_DECONV5, N):
+        raise Iclr17Error("iclr17: deconv_igdn_h3 needs the ICLR17_H3K_DECONV5 packing")
+    def shape(P):
+        return (P, B, N // 32, 2 * hh, 2 * ww, 32) if chunk_major else (P, B, 2 * hh, 2 * ww, N)
+    h3 = torch.empty(shape(2), device=hs.device, dtype=torch.int16) if want_h3 else None
+    x6 = torch.empty(shape(3), device=hs.device, dtype=torch.int16) if want_x6 else None
     out = torch.empty(B, 2 * hh, 2 * ww, N, device=hs.device) if want_f32 else None
-    call("iclr17_synthesis_deconv_igdn_x6k", _p(hs), B, hh, ww, N, _p(wx), _p(bias),
-         _p(beta_eff), _p(g6), _p(out), _p(split), int(chunk_major), int(int_in), _stream(hs))
-    return split, out
+    call("iclr17_synthesis_deconv_igdn_h3", _p(hs), B, hh, ww, N, _p(wh), _p(bias),
+         _p(beta_eff), _p(g6), _p(out), _p(h3), _p(x6), int(chunk_major), int(int_in),
+         _p(h3_range_flag(hs.device)), _stream(hs))
+    return h3, out, x6
 
 
 def ms_ssim(x: Tensor, y: Tensor, data_range: float = 1.0) -> Tensor:

@@ -70,14 +70,16 @@ class ImageCompressor(nn.Module):
         clipped, recon, sse_partial = self.Decoder.decode(y_hat, x_ref=x if x_ref_sse else None,
                                                           want_recon=want_recon, y_split=y_split,
                                                           y_bf16=q.get("y_bf16"),
-                                                          y_integral=not training)
+                                                          y_integral=not training,
+                                                          y_h3=q.get("y_h3"))
         return {"clipped": clipped, "y_hat": y_hat, "bits_partial": bits_partial,
                 "sse_partial": sse_partial, "recon": recon, "y": q["y"]}
 
     def encode_latents(self, x: torch.Tensor, noise: Optional[torch.Tensor] = None,
                        training: bool = False, want_y: bool = False) -> Dict[str, torch.Tensor]:
         """The analysis half of ``run``: conv1+GDN → conv2+GDN → conv3+quantise+rate. Returns
-        ``y_hat`` (NHWC), the bits partials, ``y_split`` (x6 split form, or None) and ``y``."""
+        ``y_hat`` (NHWC), the bits partials, ``y_split`` (x6 split form, or None), ``y_h3`` (the
+        h3 form in the h3 mode, or None) and ``y``."""
         kernels._check(x, "image", 4)
         if training and noise is None:
             noise = self._latent_noise(x)
@@ -97,6 +99,20 @@ class ImageCompressor(nn.Module):
                                                                 self.bitEstimator.rate_table(),
                                                                 want_y=want_y)
             return {"y_hat": y_hat, "bits_partial": bits, "y_split": None, "y_bf16": ybf, "y": y}
+        if kernels.precision() == "h3":
+            # the parity mode on the f16 MFMA: conv1 (x6 contractions) → conv2 and conv3 in the
+            # h3 form (three fp16 part products per MAC), ŷ handed to the decoder in the h3 form
+            e1 = self.Encoder.gdn1.effective_params_x6()
+            e2 = self.Encoder.gdn2.effective_params_x6()
+            w2h, w3h = self.Encoder.packed_h3()
+            hs, _ = kernels.conv1x6_gdn_h3(x, self.Encoder.packed_conv1_x6(), self.Encoder.conv1.bias,
+                                           e1[0], e1[2], N)
+            hs, _, _ = kernels.conv2_gdn_h3(hs, w2h, self.Encoder.conv2.bias, e2[0], e2[2])
+            rt = self.bitEstimator.rate_table() if noise is None else None
+            q = kernels.conv3_quant_rate_h3(hs, w3h, self.bitEstimator.packed(), noise, want_y=want_y,
+                                            rtab=rt)
+            return {"y_hat": q[0], "bits_partial": q[1], "y_split": None, "y_h3": q[3],
+                    "y": q[2] if want_y else None}
         if kernels.precision() != "fp32":
             e1 = self.Encoder.gdn1.effective_params_x6()
             e2 = self.Encoder.gdn2.effective_params_x6()
@@ -132,7 +148,8 @@ class ImageCompressor(nn.Module):
         q = self.encode_latents(input_image.contiguous(), noise, self.training)
         clipped, _, _, bpp = self.Decoder.decode(q["y_hat"], want_recon=False, y_split=q["y_split"],
                                                  y_bf16=q.get("y_bf16"), y_integral=not self.training,
-                                                 bits=(q["bits_partial"], 1.0 / (B * H * W)))
+                                                 bits=(q["bits_partial"], 1.0 / (B * H * W)),
+                                                 y_h3=q.get("y_h3"))
         out = {"clipped": clipped, "y_hat": q["y_hat"]}
         y_hat = out["y_hat"].permute(0, 3, 1, 2).contiguous()   # NCHW like model.py:56
         clipped = no_backward(out["clipped"], "ImageCompressor (training mode, no grad)", params,
@@ -215,9 +232,10 @@ class ImageCompressor(nn.Module):
         y_hat = kernels.rans_decode(words, offsets, self.bitEstimator.entropy_tables(K), B, h, w, N,
                                     K, P)
         split = kernels.split_planes(y_hat) if kernels.precision() == "x6" else None
+        yh3 = kernels.h3_planes(y_hat) if kernels.precision() == "h3" else None
         ybf = kernels.to_bf16(y_hat) if kernels.precision() == "bf16" else None
         clipped, _, _ = self.Decoder.decode(y_hat, want_recon=False, y_split=split, y_bf16=ybf,
-                                            y_integral=True)
+                                            y_integral=True, y_h3=yh3)
         return {"y_hat": y_hat.permute(0, 3, 1, 2).contiguous(), "x_hat": clipped}
 
     @torch.no_grad()
@@ -257,8 +275,9 @@ class ImageCompressor(nn.Module):
                 self.Encoder.packed_conv1_x6()
                 self.Encoder.packed_w3_split()
                 self.Decoder.packed_x6()
-                if not backward:
-                    self.Decoder.packed_x6k()
+                if not backward and kernels.precision() == "h3":
+                    self.Decoder.packed_h3k()
+                    self.Encoder.packed_h3()
                 for g in gdns:
                     g.effective_params_x6()
             if backward:

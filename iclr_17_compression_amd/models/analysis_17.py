@@ -56,6 +56,17 @@ class Analysis_net_17(nn.Module):
         return self._pack.get("w3x6", (self.conv3.weight,),
                               lambda: kernels.split_packed(w3, 25, N, N), force)
 
+    def packed_h3(self, force: bool = False):
+        """conv2 / conv3 weights in the h3 engine's two fp16 planes (kernels.split_packed_h3 of the
+        conv5 packing, per-tensor power-of-two scale in the trailer), cached."""
+        N = self.out_channel_N
+        _, w2, w3, _, _ = self.packed(force)
+        w2h = self._pack.get("w2h3", (self.conv2.weight,),
+                             lambda: kernels.split_packed_h3(w2, 25, N, N), force)
+        w3h = self._pack.get("w3h3", (self.conv3.weight,),
+                             lambda: kernels.split_packed_h3(w3, 25, N, N), force)
+        return w2h, w3h
+
     def packed_conv1_x6(self, force: bool = False):
         """conv1's weights in the x6 kernel's split layout (kernels.pack_conv1_x6), cached."""
         N = self.out_channel_N
@@ -110,7 +121,9 @@ class Analysis_net_17(nn.Module):
     def y_nhwc(self, x, feats=None):
         """y (NHWC) through the codec's analysis kernels. ``feats``: the training forward's
         conv2+GDN2 output (autograd.analysis_features_train), reused for conv3 where it is the
-        codec's own operand (x6: its split form; fp32: the fp32 activation)."""
+        codec's own operand (x6: its split form; fp32: the fp32 activation). In the h3 and bf16
+        modes the codec's own chain runs again (its y is what the codec rounds; the gradient is
+        the training kernels' x6 one, the same function to fp32 rounding)."""
         N = self.out_channel_N
         w1, w2, w3, g1, g2 = self.packed()
         # the rate epilogue needs a model: a zero one (its bits are discarded, y is all we keep)
@@ -127,6 +140,12 @@ class Analysis_net_17(nn.Module):
             h = kernels.conv1_gdn_bf16(x, w1b, self.conv1.bias, *e1, N)
             h = kernels.conv2_gdn_bf16(h, w2b, self.conv2.bias, *e2)
             y = kernels.conv3_quant_rate_bf16(h, w3b, z, ztab, want_y=True)[2]
+        elif kernels.precision() == "h3":
+            e1, e2 = self.gdn1.effective_params_x6(), self.gdn2.effective_params_x6()
+            w2h, w3h = self.packed_h3()
+            hs, _ = kernels.conv1x6_gdn_h3(x, self.packed_conv1_x6(), self.conv1.bias, e1[0], e1[2], N)
+            hs, _, _ = kernels.conv2_gdn_h3(hs, w2h, self.conv2.bias, e2[0], e2[2])
+            y = kernels.conv3_quant_rate_h3(hs, w3h, z, want_y=True, rtab=ztab, want_h3=False)[2]
         elif kernels.precision() == "x6":
             e1, e2 = self.gdn1.effective_params_x6(), self.gdn2.effective_params_x6()
             hs, _, _ = kernels.conv1x6_gdn(x, self.packed_conv1_x6(), self.conv1.bias, e1[0], e1[2], N)

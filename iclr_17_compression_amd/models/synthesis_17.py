@@ -53,14 +53,14 @@ class Synthesis_net_17(nn.Module):
         return self._pack.get("d3x6", (self.deconv3.weight,),
                               lambda: kernels.split_deconv3(d3, self.out_channel_N), force)
 
-    def packed_x6k(self, force: bool = False):
-        """deconv1 / deconv2 split into the x6k engine's three bf16 weight planes (4 stride
-        phases), cached until the weights change."""
+    def packed_h3k(self, force: bool = False):
+        """deconv1 / deconv2 in the h3 engine's two fp16 weight planes (4 stride phases, per-tensor
+        power-of-two scale in the trailer), cached until the weights change."""
         N, f = self.out_channel_N, force
-        d1 = self._pack.get("d1x6k", (self.deconv1.weight,),
-                            lambda: kernels.pack_x6k(_lib.ICLR17_X6K_DECONV5, self.deconv1.weight, N), f)
-        d2 = self._pack.get("d2x6k", (self.deconv2.weight,),
-                            lambda: kernels.pack_x6k(_lib.ICLR17_X6K_DECONV5, self.deconv2.weight, N), f)
+        d1 = self._pack.get("d1h3", (self.deconv1.weight,),
+                            lambda: kernels.pack_h3k(_lib.ICLR17_H3K_DECONV5, self.deconv1.weight, N), f)
+        d2 = self._pack.get("d2h3", (self.deconv2.weight,),
+                            lambda: kernels.pack_h3k(_lib.ICLR17_H3K_DECONV5, self.deconv2.weight, N), f)
         return d1, d2
 
     def packed_bf16(self, force: bool = False):
@@ -100,11 +100,12 @@ class Synthesis_net_17(nn.Module):
         return y.permute(0, 2, 3, 1).contiguous()
 
     def decode(self, y_nhwc, x_ref=None, want_recon=True, y_split=None, y_bf16=None,
-               y_integral=False, bits=None):
+               y_integral=False, bits=None, y_h3=None):
         """NHWC latent → (clipped NCHW, unclipped NCHW | None, SSE partials | None).
         With ``y_split`` (the latent in x6 split form) the three layers run in the x6 mode, with
+        ``y_h3`` (the h3 form) deconv1 / deconv2 run in the h3 form and deconv3 in x6, with
         ``y_bf16`` (bf16 bit patterns) in the bf16 throughput mode. ``y_integral``: the latent
-        is ŷ = round(y) (model.py:56), so deconv1 runs the x6k engine's integer-input form.
+        is ŷ = round(y) (model.py:56), so the h3 deconv1 takes its integer-input form.
         ``bits`` = (conv3's bit partials, scale): a fourth output, ``reduce_partials``' 0-dim total,
         computed inside deconv3's kernel in the x6 and bf16 modes (one launch fewer)."""
         d1, d2, d3, g1, g2 = self.packed()
@@ -115,23 +116,21 @@ class Synthesis_net_17(nn.Module):
             h = kernels.deconv_igdn_bf16(h, b2, self.deconv2.bias, *q2)
             return kernels.deconv3_bf16(h, b3, self.deconv3.bias, x_ref=x_ref, want_recon=want_recon,
                                         bits=bits)
+        if y_h3 is not None:
+            q1, q2 = self.igdn1.effective_params_x6(), self.igdn2.effective_params_x6()
+            w1, w2 = self.packed_h3k()
+            # on ŷ the integer-input form skips the lo products (the same bits: Decoder(round(y))
+            # reproduces the codec's reconstruction without knowing its input is ŷ)
+            hs, _, _ = kernels.deconv_igdn_h3(y_h3, w1, self.deconv1.bias, q1[0], q1[2],
+                                              int_in=y_integral)
+            _, _, s6 = kernels.deconv_igdn_h3(hs, w2, self.deconv2.bias, q2[0], q2[2], want_h3=False,
+                                              want_x6=True, chunk_major=True)
+            return kernels.deconv3_x6(s6, self.packed_x6(), self.deconv3.bias, x_ref=x_ref,
+                                      want_recon=want_recon, bits=bits)
         if y_split is not None:
             q1, q2 = self.igdn1.effective_params_x6(), self.igdn2.effective_params_x6()
-            if kernels.X6K:
-                # deconv1 on the x6k engine; on ŷ three of its six part products vanish (int_in),
-                # and the six-product form gives the same bits on any integer input, so
-                # Decoder(round(y)) reproduces the codec's reconstruction without knowing its
-                # input is ŷ. Not the default: faster alone (0.154 vs 0.171 ms at B=64), slower in
-                # the chain (one 140 KB workgroup per CU shares no CU with conv3 / deconv2)
-                hs, _ = kernels.deconv_igdn_x6k(y_split, self.packed_x6k()[0], self.deconv1.bias,
-                                                q1[0], q1[2], int_in=y_integral)
-            else:
-                hs, _, _ = kernels.deconv_igdn_x6(y_split, d1, self.deconv1.bias, *q1)
-            if kernels.X6K:   # deconv2 on the 32x32x16 x6 engine (A/B; the same MFMA rate)
-                hs, _ = kernels.deconv_igdn_x6k(hs, self.packed_x6k()[1], self.deconv2.bias, q2[0],
-                                                q2[2], chunk_major=True)
-            else:
-                hs, _, _ = kernels.deconv_igdn_x6(hs, d2, self.deconv2.bias, *q2, chunk_major=True)
+            hs, _, _ = kernels.deconv_igdn_x6(y_split, d1, self.deconv1.bias, *q1)
+            hs, _, _ = kernels.deconv_igdn_x6(hs, d2, self.deconv2.bias, *q2, chunk_major=True)
             return kernels.deconv3_x6(hs, self.packed_x6(), self.deconv3.bias, x_ref=x_ref,
                                       want_recon=want_recon, bits=bits)
         else:
@@ -152,6 +151,7 @@ class Synthesis_net_17(nn.Module):
             return SynthesisFn.apply(x, self, *params)
         y = self.to_nhwc(x)
         split = kernels.split_planes(y) if kernels.precision() == "x6" else None
+        yh3 = kernels.h3_planes(y) if kernels.precision() == "h3" else None
         ybf = kernels.to_bf16(y) if kernels.precision() == "bf16" else None
-        _, recon, _ = self.decode(y, want_recon=True, y_split=split, y_bf16=ybf)
+        _, recon, _ = self.decode(y, want_recon=True, y_split=split, y_bf16=ybf, y_h3=yh3)
         return recon

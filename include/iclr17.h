@@ -461,25 +461,63 @@ int iclr17_rate_param_grad(const float* partial, int T, int C, const float* h1, 
                            float* db2, float* da2, float* dh3, float* db3, float* da3, float* dh4,
                            float* db4, void* stream);
 
-/* ------------------------------------------------------------------ x6 k5 engine (32x32x16)
- * The x6 scheme (fp32-exact part products, as above) on v_mfma_f32_32x32x16_bf16 in the bf16
- * engine's form (csrc/engine_x6k.hip): halo patch of the split input per 16-channel chunk,
- * weights pre-split into three bf16 planes, a wave owns 32 pixels × all N channels, IGDN
- * contraction from the accumulators. Replaces iclr17_synthesis_deconv_igdn_x6[_cm] on the
- * inference path (synthesis_17.py:15-22; models/GDN.py:64-94, inverse). */
-#define ICLR17_X6K_CONV5 40   /* conv2/conv3 W[co][ci][5][5] → [3][N/16·25][2][N][8] bf16 planes */
-#define ICLR17_X6K_DECONV5 41 /* deconv1/2 W[ci][co][5][5] → [3][4 phases: N/16·T_p][2][N][8] */
-size_t iclr17_x6k_weight_size(int which, int N);   /* uint16 elements (3 planes); 0 = unsupported */
-int iclr17_pack_x6k(int which, const float* w, uint16_t* out, int N, void* stream);
-/* synthesis_17.py:15-22 deconv + IGDN in x6: split input [3][B][h][w][N] → out fp32 NHWC
- * [B][2h][2w][N] (or NULL) and/or the split output (NHWC, or chunk-major
- * [3][B][N/32][2h][2w][32] with out_cm). int_in: the input is integer-valued (ŷ, |v| ≤ 127;
- * exact in its hi plane), only that plane is read. γ: iclr17_split_packed of the GDN packing. */
-int iclr17_synthesis_deconv_igdn_x6k(const uint16_t* in_split, int B, int h, int w, int N,
-                                     const uint16_t* w_x6k, const float* bias,
-                                     const float* beta_eff, const uint16_t* gamma_split,
-                                     float* out, uint16_t* out_split, int out_cm, int int_in,
-                                     void* stream);
+/* ------------------------------------------------------------------ h3 form (32x32x16 f16)
+ * The parity mode's k5 layers with THREE fp16 part products per MAC on v_mfma_f32_32x32x16_f16
+ * (csrc/engine_h3.hip, csrc/common.h "h3 form"): an activation is stored as two fp16 planes
+ * [2][…] of a = x·2^-6, hi = rne16(a) and lo = rne16((a − hi)·2^11); weights the same way with a
+ * per-tensor power-of-two scale chosen at packing. Against float64 its dot products land closer
+ * than the x6 chain's (tools/h3_numerics.hip). |x| ≥ 2^22 does not fit the form: the kernels then
+ * set *range_flag (nullable) to 1. Halo patch of the h3 input per 16-channel chunk, a wave owns 32
+ * pixels × all N channels, GDN/IGDN contraction (x6) from the accumulators.
+ * Replaces iclr17_synthesis_deconv_igdn_x6[_cm] on the parity path
+ * (synthesis_17.py:15-22; models/GDN.py:64-94, inverse). */
+#define ICLR17_H3K_CONV5 42   /* conv2 W[co][ci][5][5] → [2][N/16·25][2][N][8] fp16 planes + trailer */
+#define ICLR17_H3K_DECONV5 43 /* deconv1/2 W[ci][co][5][5] → [2][4 phases: N/16·T_p][2][N][8] + trailer */
+/* uint16 elements: two planes + an 8-element (16-byte) trailer {max|w|, 2^-11/(σ_a·σ_w)}; 0 =
+ * unsupported */
+size_t iclr17_h3k_weight_size(int which, int N);
+int iclr17_pack_h3k(int which, const float* w, uint16_t* out, int N, void* stream);
+/* fp32 x[n] (n % 4 == 0) → h3 planes [2][n] */
+int iclr17_h3_planes(const float* x, long n, uint16_t* planes, int* range_flag, void* stream);
+/* A packed operand [taps][K/4][N][4] fp32 → two fp16 planes [2][taps][K/8][N][8] of w·σ_w + the
+ * trailer (the h3 conv2 / conv3 weights: the ICLR17_W_CONV5 packing with taps 25, K = N).
+ * iclr17_split_packed_h3_size() uint16 elements (0 = bad arguments). */
+size_t iclr17_split_packed_h3_size(int taps, int K, int N);
+int iclr17_split_packed_h3(const float* packed, int taps, int K, int N, uint16_t* planes,
+                           void* stream);
+/* analysis_17.py:14-17 conv1 + GDN1 (x6 contractions, as iclr17_analysis_conv1x6_gdn) with the
+ * output in the h3 form [2][B][H/4][W/4][N] (and/or fp32). */
+int iclr17_analysis_conv1x6_gdn_h3(const float* x, int B, int H, int W, int N,
+                                   const uint16_t* w_split, const float* bias,
+                                   const float* beta_eff, const uint16_t* gamma_split,
+                                   float* out, uint16_t* out_h3, int* range_flag, void* stream);
+/* analysis_17.py:18-21 conv2 + GDN2 on the h3 form: input [2][B][H/4][W/4][N] → fp32 NHWC and/or
+ * the h3 output and/or the x6 split output [3][B][H/8][W/8][N] (nullable, not all). Three f16
+ * part products per MAC with the two-level accumulation of the x6 conv2 (per-tap sums), GDN
+ * contraction in x6. w_h3: iclr17_split_packed_h3 of the ICLR17_W_CONV5 packing. */
+int iclr17_analysis_conv2_gdn_h3(const uint16_t* in_h3, int B, int H, int W, int N,
+                                 const uint16_t* w_h3, const float* bias, const float* beta_eff,
+                                 const uint16_t* gamma_split, float* out, uint16_t* out_h3,
+                                 uint16_t* out_split, int* range_flag, void* stream);
+/* analysis_17.py:22 + model.py:48-56,71-73 on the h3 form: as iclr17_analysis_conv3_quant_rate
+ * (round or noise mode, rate_table nullable), ŷ also in the h3 form (y_hat_h3, nullable); bit
+ * partials [B][iclr17_rate_partials_per_image] in both modes. */
+int iclr17_analysis_conv3_quant_rate_h3(const uint16_t* in_h3, int B, int H, int W, int N,
+                                        const uint16_t* w_h3, int quant_mode, const float* noise,
+                                        const float* rate_packed, const float* rate_table,
+                                        float* y_out, float* y_hat, uint16_t* y_hat_h3,
+                                        double* bits_partial, int* range_flag, void* stream);
+/* synthesis_17.py:15-22 deconv + IGDN on the h3 form: input [2][B][h][w][N] → fp32 NHWC
+ * [B][2h][2w][N] and/or the h3 output [2][B][2h][2w][N] and/or the x6 split output
+ * [3][B][2h][2w][N] (each nullable, not all; the h3 and x6 outputs chunk-major
+ * [P][B][N/32][2h][2w][32] with out_cm). int_in: the input is integer-valued (ŷ): a workgroup
+ * whose input window has a zero lo plane runs the two products with hi_a only (same result).
+ * γ: iclr17_split_packed of the GDN packing. */
+int iclr17_synthesis_deconv_igdn_h3(const uint16_t* in_h3, int B, int h, int w, int N,
+                                    const uint16_t* w_h3k, const float* bias,
+                                    const float* beta_eff, const uint16_t* gamma_split,
+                                    float* out, uint16_t* out_h3, uint16_t* out_x6, int out_cm,
+                                    int int_in, int* range_flag, void* stream);
 
 /* ------------------------------------------------------------------ bf16 throughput mode
  * The codec forward with bf16 activations (NHWC [B][h][w][N], round to nearest even), bf16

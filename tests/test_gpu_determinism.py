@@ -24,7 +24,7 @@ def poison(dev):
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("precision", ["fp32", "x6", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "x6", "h3", "bf16"])
 def test_eval_chain_bitwise_repeatable(device, golden_dir, precision):
     meta = json.load(open(os.path.join(golden_dir, "g5_kodak24_synth_n192.json")))
     net = ImageCompressor(meta["N"])

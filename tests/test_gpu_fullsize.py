@@ -157,7 +157,7 @@ def _check_latents(y_hat, y, r_yhat, r_y, max_rate=1e-4):
     return check_latents(y_hat, y, r_yhat, r_y, max_rate)
 
 
-@pytest.mark.parametrize("precision", ["x6", "fp32"])
+@pytest.mark.parametrize("precision", ["h3", "x6", "fp32"])
 def test_kodak24_all_images(device, golden_dir, precision):
     meta = _kodak_meta(golden_dir)
     old = kernels.precision()

@@ -112,7 +112,7 @@ def parity_out_dir():
     return d
 
 
-@pytest.mark.parametrize("precision", ["x6", "fp32"])
+@pytest.mark.parametrize("precision", ["h3", "x6", "fp32"])
 def test_g8_all_images(device, opset, golden_dir, precision):
     """Every image, unconditionally, against the REFERENCE's own values (the fixture, its default
     oneDNN order), at max(1e-5, the reference's own cross-order spread on this set) per metric.
@@ -136,13 +136,15 @@ def test_g8_all_images(device, opset, golden_dir, precision):
     flips = gpu_wrong = ref_wrong = same = 0
     worst = {k: 0.0 for k in bars}
     per_image = []
+    wrong_latents = []
     try:
         for row in meta["images"]:
             x = _image(meta, row)
             with torch.no_grad():
-                ev = net.evaluate(x.to(device), want_msssim=True)
+                ev = net.evaluate(x.to(device), want_msssim=True, want_y=True)
             r_yhat, near_idx, near_y = refs[row["index"]]
-            ex = torch.round(exact_latents(x, sd, device)).float()
+            y64 = exact_latents(x, sd, device)
+            ex = torch.round(y64).float()
             g = ev["y_hat"].cpu()
             assert g.shape == r_yhat.shape
             diff = (g != r_yhat).reshape(-1)
@@ -159,6 +161,16 @@ def test_g8_all_images(device, opset, golden_dir, precision):
             same += n == 0
             gpu_wrong += int((g != ex).sum())
             ref_wrong += int((r_yhat != ex).sum())
+            # every latent the GPU or the reference rounds away from exact arithmetic: its fp64 y,
+            # the GPU's y and ŷ, the reference's ŷ (and its y where the fixture holds it)
+            gy = ev["y"].cpu().reshape(-1)
+            for i in torch.nonzero(((g != ex) | (r_yhat != ex)).reshape(-1)).reshape(-1).tolist():
+                k = np.nonzero(near_idx == i)[0]
+                wrong_latents.append({"image": row["index"], "index": i, "y_fp64": float(y64.reshape(-1)[i]),
+                                      "y_gpu": float(gy[i]), "yhat_gpu": float(g.reshape(-1)[i]),
+                                      "yhat_ref": float(r_yhat.reshape(-1)[i]),
+                                      "y_ref": float(near_y[k[0]]) if k.size else None,
+                                      "yhat_exact": float(ex.reshape(-1)[i])})
             got = {"bpp": ev["bpp"][0].item(), "psnr": ev["psnr"][0].item(), "ms_ssim": ev["ms_ssim"][0].item()}
             rels = {}
             for k, bar in bars.items():
@@ -179,7 +191,8 @@ def test_g8_all_images(device, opset, golden_dir, precision):
            "images_with_reference_latents": same, "images_bar": min_same,
            "gpu_vs_exact": gpu_wrong, "reference_vs_exact": ref_wrong,
            "reference_orders_vs_exact": orders["total_wrong_vs_fp64"], "gpu_vs_exact_bar": wrong_bar,
-           "worst_rel": worst, "bars_flip_images": bars, "bar_same_latents": REL, "images": per_image}
+           "worst_rel": worst, "bars_flip_images": bars, "bar_same_latents": REL, "images": per_image,
+           "latents_off_exact": wrong_latents}
     with open(os.path.join(parity_out_dir(), f"parity_{meta['N']}_{precision}.json"), "w") as f:
         json.dump(rec, f, indent=1)
     print(f"N={meta['N']} {precision}: {flips} latent flips vs the reference's y_hat (budget {flip_budget}), "

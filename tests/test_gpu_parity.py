@@ -48,7 +48,7 @@ def nhwc(t):
     return t.permute(0, 2, 3, 1)
 
 
-@pytest.fixture(params=["x6", "fp32"])
+@pytest.fixture(params=["h3", "x6", "fp32"])
 def precision(request):
     """Run a test in each inference contraction mode (kernels.set_precision)."""
     old = kernels.precision()
@@ -563,54 +563,133 @@ def test_chunk_major_split_deconv2_to_deconv3(device, N):
         assert torch.equal(u, v)
 
 
+def test_h3_planes(device):
+    """The h3 form (common.h): hi + lo·2^-11 reproduces x·2^-6 to 2^-22 relative (22 significant
+    bits) wherever lo is a normal fp16, hi is the RNE fp16 of x·2^-6, small values keep an
+    absolute error below 2^-36·2^6, and a value of magnitude ≥ 2^22 sets the range flag."""
+    x = torch.from_numpy(synth.normal_like(3, (8192,), 2.0)) * torch.from_numpy(
+        np.exp(synth.uniform(4, (8192,), -20, 12)).astype(np.float32))
+    x[:8] = torch.tensor([0.0, -0.0, 1.0, -1.0, 4.0e6, -1e-30, 0.1, 1 / 3])
+    flag = kernels.h3_range_flag(device)
+    flag.zero_()
+    s = kernels.h3_planes(x.to(device))
+    assert s.shape == (2, 8192) and s.dtype == torch.int16
+    assert int(flag.item()) == 0
+    back = kernels.merge_h3(s).cpu().double()
+    xd = x.double()
+    err = (back - xd).abs()
+    assert bool((err <= torch.maximum(xd.abs() * 2.0 ** -22, torch.full_like(xd, 2.0 ** -30))).all())
+    hi = s[0].view(torch.float16).float().cpu()
+    assert torch.equal(hi, (x * 2.0 ** -6).to(torch.float16).float())
+    big = torch.tensor([1.0, 2.0 ** 22 * 1.01, -3.0, 5.0], device=device)
+    kernels.h3_planes(big)
+    assert int(flag.item()) == 1
+    with pytest.raises(kernels.Iclr17Error):
+        kernels.check_h3_range(device)
+    assert int(flag.item()) == 0
+
+
+@pytest.mark.parametrize("N", [192, 128])
+def test_h3_encoder_layers(device, N):
+    """conv1 / conv2 / conv3 of the h3 chain against the oracle, each from the oracle's input:
+    conv1's h3 output is the h3 form of its fp32 output; conv2+GDN2 in the h3 form (three fp16
+    part products per MAC, per-tap two-level accumulation) at the fp32 bar and as close to the x6
+    conv2 as two fp32 summation orders, with its h3 / x6 outputs encoding its fp32 output exactly;
+    conv3 + quantiser + rate: y at the fp32 bar, latents within the reference's own near-tie band,
+    ŷ's h3 form exact, bits equal to the x6 kernel's up to summation order."""
+    net, sd = net_for(N, 1, device), sd_for(N, 1)
+    F = torch.nn.functional
+    x = image(11, 2, 64, 96)
+    w1, w2, w3, g1, g2 = net.Encoder.packed()
+    w2h, w3h = net.Encoder.packed_h3()
+    e1, e2 = net.Encoder.gdn1.effective_params_x6(), net.Encoder.gdn2.effective_params_x6()
+    rate, rtab = net.bitEstimator.packed(), net.bitEstimator.rate_table()
+    flag = kernels.h3_range_flag(device)
+    flag.zero_()
+    with torch.no_grad():
+        a1h, a1 = kernels.conv1x6_gdn_h3(x.to(device), net.Encoder.packed_conv1_x6(), net.Encoder.conv1.bias,
+                                         e1[0], e1[2], N, want_f32=True)
+        _, a1x6, _ = kernels.conv1x6_gdn(x.to(device), net.Encoder.packed_conv1_x6(), net.Encoder.conv1.bias,
+                                         e1[0], e1[2], N, want_f32=True)
+        assert torch.equal(a1, a1x6) and torch.equal(a1h, kernels.h3_planes(a1))
+        r_u1 = F.conv2d(x, sd["Encoder.conv1.weight"], sd["Encoder.conv1.bias"], stride=4, padding=4)
+        r_a1 = oracle.gdn(r_u1, sd["Encoder.gdn1.beta"], sd["Encoder.gdn1.gamma"], False)
+        a1r = nhwc(r_a1).contiguous().to(device)
+        a2h, a2, a2s = kernels.conv2_gdn_h3(kernels.h3_planes(a1r), w2h, net.Encoder.conv2.bias, e2[0], e2[2],
+                                            want_f32=True, want_x6=True)
+        r_u2 = F.conv2d(r_a1, sd["Encoder.conv2.weight"], sd["Encoder.conv2.bias"], stride=2, padding=2)
+        r_a2 = oracle.gdn(r_u2, sd["Encoder.gdn2.beta"], sd["Encoder.gdn2.gamma"], False)
+        assert rel_err(a2, nhwc(r_a2)) < REL
+        assert torch.equal(kernels.merge_planes(a2s), a2) and torch.equal(a2h, kernels.h3_planes(a2))
+        _, a2x6, _ = kernels.conv2_gdn_x6(kernels.split_planes(a1r), w2, net.Encoder.conv2.bias, *e2,
+                                          want_f32=True)
+        assert rel_err(a2, a2x6) < 2e-6
+        a2r = nhwc(r_a2).contiguous().to(device)
+        y_hat, part, y, yh = kernels.conv3_quant_rate_h3(kernels.h3_planes(a2r), w3h, rate, want_y=True, rtab=rtab)
+        r_y = F.conv2d(r_a2, sd["Encoder.conv3.weight"], None, stride=2, padding=2)
+        assert rel_err(y, nhwc(r_y)) < REL
+        assert torch.equal(yh, kernels.h3_planes(y_hat))
+        check_latents(y_hat.permute(0, 3, 1, 2), y.permute(0, 3, 1, 2), torch.round(r_y), r_y)
+        yx, px, _, _ = kernels.conv3_quant_rate_x6(kernels.split_planes(a2r), w3, rate, rtab=rtab)
+        if torch.equal(yx, y_hat):
+            assert abs(part.sum().item() - px.sum().item()) <= 1e-9 * px.sum().item()
+    assert int(flag.item()) == 0
+
+
 @pytest.mark.parametrize("N", [192, 128])
 @pytest.mark.parametrize("hw", [(5, 7), (20, 34)])
-def test_x6k_deconv_igdn(device, N, hw):
-    """deconv + IGDN on the 32x32x16 x6 engine (csrc/engine_x6k.hip) against the oracle
-    (synthesis_17.py:15-22, GDN.py:64-94 inverse), on grids that are and are not whole 16×16
-    tiles: fp32 output at the fp32 bar; the split output merges to it exactly, in both the NHWC
-    and the chunk-major form; on an integer input (ŷ) the int_in form (only the hi plane read,
-    three products per MAC) is bit-identical to the full six-product form; and it agrees with
-    the 16x16x32 x6 engine to fp32 summation-order noise."""
+def test_h3_deconv_igdn(device, N, hw):
+    """deconv + IGDN in the h3 form (csrc/engine_h3.hip: three fp16 part products per MAC on the
+    32x32x16 f16 MFMA) against the oracle (synthesis_17.py:15-22, GDN.py:64-94 inverse), on grids
+    that are and are not whole 16×16 tiles: the fp32 output at the fp32 bar and as close to the
+    x6 engine as two exact-f32 summation orders; its h3 and x6 outputs encode exactly that fp32
+    output, in NHWC and chunk-major form; on ŷ the int_in form (hi plane only, two products) is
+    bit-identical to the full form, also with a latent beyond fp16's 11 bits."""
     net, sd = net_for(N, 1, device), sd_for(N, 1)
     dec = net.Decoder
     F = torch.nn.functional
     h, w = hw
-    x1, x2 = dec.packed_x6k()
+    x1, x2 = dec.packed_h3k()
     d1, d2 = dec.packed()[:2]
     q1, q2 = dec.igdn1.effective_params_x6(), dec.igdn2.effective_params_x6()
     yq = torch.round(torch.from_numpy(synth.uniform(5, (2, N, h, w), -6, 6)))
     act = torch.from_numpy(synth.normal_like(6, (2, N, h, w), 0.7))
+    flag = kernels.h3_range_flag(device)
+    flag.zero_()
     with torch.no_grad():
         for inp, lay, wx, wp, q, key in ((yq, "deconv1", x1, d1, q1, "igdn1"),
                                          (act, "deconv2", x2, d2, q2, "igdn2")):
-            ins = kernels.split_planes(nhwc(inp).contiguous().to(device))
-            s, f = kernels.deconv_igdn_x6k(ins, wx, getattr(dec, lay).bias, q[0], q[2], want_f32=True)
+            inh = kernels.h3_planes(nhwc(inp).contiguous().to(device))
+            bias = getattr(dec, lay).bias
+            s, f, s6 = kernels.deconv_igdn_h3(inh, wx, bias, q[0], q[2], want_f32=True, want_x6=True)
             r_v = F.conv_transpose2d(inp, sd[f"Decoder.{lay}.weight"], sd[f"Decoder.{lay}.bias"],
                                      stride=2, padding=2, output_padding=1)
             r_s = oracle.gdn(r_v, sd[f"Decoder.{key}.beta"], sd[f"Decoder.{key}.gamma"], True)
             assert f.shape == (2, 2 * h, 2 * w, N)
             assert rel_err(f, nhwc(r_s)) < REL, lay
-            assert torch.equal(kernels.merge_planes(s), f)
-            scm, _ = kernels.deconv_igdn_x6k(ins, wx, getattr(dec, lay).bias, q[0], q[2],
-                                             chunk_major=True)
-            assert scm.shape == (3, 2, N // 32, 2 * h, 2 * w, 32)
+            assert torch.equal(kernels.merge_planes(s6), f)
+            assert torch.equal(s, kernels.h3_planes(f))
+            scm, _, s6cm = kernels.deconv_igdn_h3(inh, wx, bias, q[0], q[2], want_x6=True,
+                                                  chunk_major=True)
+            assert scm.shape == (2, 2, N // 32, 2 * h, 2 * w, 32)
             assert torch.equal(scm.permute(0, 1, 3, 4, 2, 5).reshape(s.shape), s)
-            _, f_old, _ = kernels.deconv_igdn_x6(ins, wp, getattr(dec, lay).bias, *q, want_f32=True)
+            assert torch.equal(s6cm.permute(0, 1, 3, 4, 2, 5).reshape(s6.shape), s6)
+            _, f_old, _ = kernels.deconv_igdn_x6(kernels.split_planes(nhwc(inp).contiguous().to(device)),
+                                                 wp, bias, *q, want_f32=True)
             assert rel_err(f, f_old) < 2e-6, lay
             if lay == "deconv1":
-                si, fi = kernels.deconv_igdn_x6k(ins, wx, dec.deconv1.bias, q[0], q[2], want_f32=True,
-                                                 int_in=True)
+                si, fi, _ = kernels.deconv_igdn_h3(inh, wx, bias, q[0], q[2], want_f32=True, int_in=True)
                 assert torch.equal(fi, f) and torch.equal(si, s)
-                # a latent beyond bf16's 8 significant bits (300): the workgroups that see it run
-                # the six-product form, and the result still equals the full form's
+                # a latent beyond fp16's 11 significant bits (3001): the workgroups that see it
+                # run the three-product form, and the result still equals the full form's
                 big = inp.clone()
-                big[1, 7, h // 2, w // 2] = 300.0
-                bs = kernels.split_planes(nhwc(big).contiguous().to(device))
-                _, fb = kernels.deconv_igdn_x6k(bs, wx, dec.deconv1.bias, q[0], q[2], want_f32=True)
-                _, fbi = kernels.deconv_igdn_x6k(bs, wx, dec.deconv1.bias, q[0], q[2], want_f32=True,
-                                                 int_in=True)
+                big[1, 7, h // 2, w // 2] = 3001.0
+                bs = kernels.h3_planes(nhwc(big).contiguous().to(device))
+                _, fb, _ = kernels.deconv_igdn_h3(bs, wx, bias, q[0], q[2], want_h3=False, want_f32=True)
+                _, fbi, _ = kernels.deconv_igdn_h3(bs, wx, bias, q[0], q[2], want_h3=False, want_f32=True,
+                                                   int_in=True)
                 assert torch.equal(fbi, fb) and not torch.equal(fb, f)
+    assert int(flag.item()) == 0
 
 
 @pytest.mark.parametrize("N,B,hw", [(192, 3, (48, 80)), (128, 2, (32, 32)), (192, 40, (32, 32))])

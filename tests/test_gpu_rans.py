@@ -86,7 +86,7 @@ def test_bad_input_and_corrupt_streams_fail_loudly(device):
         kernels.rans_decode(words[:-1], torch.clamp(offsets, max=words.numel() - 1), cum, 1, 4, 4, N)
 
 
-@pytest.mark.parametrize("precision", ["x6", "fp32"])
+@pytest.mark.parametrize("precision", ["h3", "x6", "fp32"])
 def test_compress_decompress(device, precision):
     old = kernels.precision()
     kernels.set_precision(precision)

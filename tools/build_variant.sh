@@ -8,6 +8,6 @@ T=$(mktemp -d)
 HF="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function -munsafe-fp-atomics"
 /opt/rocm/bin/hipcc $HF "$@" -c $C/engine_fp32.hip -o $T/engine_fp32.o -Rpass-analysis=kernel-resource-usage 2> ${OUT%.so}.res.txt
 OBJS="$T/engine_fp32.o"
-for f in engine_bf16 engine_x6k aux wgrad_fp32 msssim optim datapath rans; do OBJS="$OBJS $C/$f.o"; done
+for f in engine_bf16 engine_h3 aux wgrad_fp32 msssim optim datapath rans; do OBJS="$OBJS $C/$f.o"; done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT $OBJS
 rm -rf $T

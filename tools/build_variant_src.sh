@@ -10,7 +10,7 @@ HF="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unus
 mkdir -p $(dirname $OUT)
 /opt/rocm/bin/hipcc $HF "$@" -c $C/$SRC.hip -o $T/$SRC.o
 OBJS="$T/$SRC.o"
-for f in engine_fp32 engine_bf16 engine_x6k aux wgrad_fp32 msssim optim datapath rans; do
+for f in engine_fp32 engine_bf16 engine_h3 aux wgrad_fp32 msssim optim datapath rans; do
   [ $f = $SRC ] || OBJS="$OBJS $C/$f.o"
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT $OBJS

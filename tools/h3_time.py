@@ -1,6 +1,6 @@
-"""Times deconv2+IGDN2 (B=64, 32×32 → 64×64, N=192) on the 16x16x32 x6 engine and on the
-32x32x16 x6k engine, interleaved, with HIP events; a short program for PMC passes
-(tools/pmc_kernel.sh TOOL=tools/x6k_time.py)."""
+"""Times deconv1+IGDN1 and deconv2+IGDN2 (B=64, N=192, the bench workload's shapes) on the
+16x16x32 x6 engine and in the h3 form (csrc/engine_h3.hip), interleaved, with HIP events; a short
+program for PMC passes (tools/pmc_kernel.sh TOOL=tools/h3_time.py)."""
 import os
 import sys
 
@@ -18,17 +18,20 @@ net.load_state_dict({k: torch.from_numpy(v) for k, v in synth.trained_like_state
 net = net.to(dev).eval()
 dec = net.Decoder
 d1, d2 = dec.packed()[:2]
-x1, x2 = dec.packed_x6k()
+x1, x2 = dec.packed_h3k()
 q1, q2 = dec.igdn1.effective_params_x6(), dec.igdn2.effective_params_x6()
 act = torch.from_numpy(synth.normal_like(6, (B, 32, 32, N), 0.7)).to(dev)
 yq = torch.round(torch.from_numpy(synth.uniform(5, (B, 16, 16, N), -6, 6))).to(dev)
 hs, ys = kernels.split_planes(act), kernels.split_planes(yq)
+hh, yh = kernels.h3_planes(act), kernels.h3_planes(yq)
 runs = {
     "deconv2_old": lambda: kernels.deconv_igdn_x6(hs, d2, dec.deconv2.bias, *q2, chunk_major=True),
-    "deconv2_x6k": lambda: kernels.deconv_igdn_x6k(hs, x2, dec.deconv2.bias, q2[0], q2[2], chunk_major=True),
+    "deconv2_h3": lambda: kernels.deconv_igdn_h3(hh, x2, dec.deconv2.bias, q2[0], q2[2], want_h3=False,
+                                                 want_x6=True, chunk_major=True),
+    "deconv2_h3_h3out": lambda: kernels.deconv_igdn_h3(hh, x2, dec.deconv2.bias, q2[0], q2[2], chunk_major=True),
     "deconv1_old": lambda: kernels.deconv_igdn_x6(ys, d1, dec.deconv1.bias, *q1),
-    "deconv1_x6k": lambda: kernels.deconv_igdn_x6k(ys, x1, dec.deconv1.bias, q1[0], q1[2]),
-    "deconv1_x6k_int": lambda: kernels.deconv_igdn_x6k(ys, x1, dec.deconv1.bias, q1[0], q1[2], int_in=True),
+    "deconv1_h3": lambda: kernels.deconv_igdn_h3(yh, x1, dec.deconv1.bias, q1[0], q1[2]),
+    "deconv1_h3_int": lambda: kernels.deconv_igdn_h3(yh, x1, dec.deconv1.bias, q1[0], q1[2], int_in=True),
 }
 sel = os.environ.get("ONLY", "").split(",") if os.environ.get("ONLY") else list(runs)
 with torch.no_grad():

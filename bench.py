@@ -38,13 +38,13 @@ X6_LAYERS = ("conv1_gdn1", "conv2_gdn2", "conv3_quant_rate", "deconv1_igdn1", "d
              "deconv3_clamp")   # every contraction of the x6 eval chain
 H3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3   # fp32-equivalent: 3 fp16 part products per MAC
 # the layers of the h3 eval chain whose main contraction runs in the h3 form (the others in x6)
-H3_LAYERS = ("conv2_gdn2", "conv3_quant_rate", "deconv1_igdn1", "deconv2_igdn2")
+H3_LAYERS = ("conv2_gdn2", "conv3_quant_rate", "deconv1_igdn1", "deconv2_igdn2", "deconv3_clamp")
 
 
 PRECISION_NOTE = {
     "h3": ("h3: fp32 operands as two fp16 parts (22 significant bits, power-of-two scaled), 3 part "
-           "products per MAC on v_mfma_f32_*_f16 with fp32 accumulate for conv2, conv3, deconv1 and "
-           "deconv2; x6 for conv1, deconv3 and the GDN contractions"),
+           "products per MAC on v_mfma_f32_*_f16 with fp32 accumulate for conv2, conv3, deconv1, "
+           "deconv2 and deconv3; x6 for conv1 and the GDN contractions"),
     "x6": ("x6: fp32 operands split exactly into 3 bf16 parts, 6 part products on "
            "v_mfma_f32_16x16x32_bf16, fp32 accumulate (every contraction)"),
     "bf16": "bf16: bf16 activations and weights, one bf16 product per MAC, fp32 accumulate and epilogues",
@@ -62,10 +62,6 @@ def layer_peak(prec: str, k: str):
         return X6_PEAK_TFLOPS, "bf16 dense MFMA peak / 6 (bf16x6: six bf16 part products per fp32 MAC)"
     return FP32_MFMA_PEAK_TFLOPS, "fp32 MFMA dense peak (exact-f32 products)"
 HBM_PEAK_GBS = 8000.0
-# deconv2 → deconv3 through the chunk-major split form (ICLR17_D3_CM=0: the NHWC split, for A/B)
-D3_CM = os.environ.get("ICLR17_D3_CM", "1") != "0"
-FOLD_BITS = os.environ.get("ICLR17_FOLD_BITS", "1") != "0"   # bpp's reduction inside deconv3 (A/B)
-W6 = os.environ.get("ICLR17_W6", "1") != "0"   # x6 conv3 with pre-split weights (A/B)
 
 LAYERS = ("conv1_gdn1", "conv2_gdn2", "conv3_quant_rate", "deconv1_igdn1", "deconv2_igdn2",
           "deconv3_clamp", "bits_reduce")
@@ -120,7 +116,7 @@ class Step:
         self.rate = net.bitEstimator.packed()
         gdns = (net.Encoder.gdn1, net.Encoder.gdn2, net.Decoder.igdn1, net.Decoder.igdn2)
         self.w1x6 = net.Encoder.packed_conv1_x6()
-        self.w3s = net.Encoder.packed_w3_split() if W6 else None   # x6 conv3's pre-split weights
+        self.w3s = net.Encoder.packed_w3_split()   # x6 conv3's pre-split weights
         self.g6 = [m.effective_params_x6() for m in gdns]
         self.ebf = net.Encoder.packed_bf16()
         self.dbf = net.Decoder.packed_bf16()
@@ -158,17 +154,13 @@ class Step:
             ev(5)
             yield
             # bpp's reduction (model.py:71-78) inside deconv3's kernel (ImageCompressor.forward)
-            if FOLD_BITS:
-                clipped, _, _, bpp = kernels.deconv3_bf16(h, d3b, net.Decoder.deconv3.bias,
-                                                          bits=(partial, self.scale))
-            else:
-                clipped, _, _ = kernels.deconv3_bf16(h, d3b, net.Decoder.deconv3.bias)
-                bpp = None
+            clipped, _, _, bpp = kernels.deconv3_bf16(h, d3b, net.Decoder.deconv3.bias,
+                                                      bits=(partial, self.scale))
         elif kernels.precision() == "h3":
             # ImageCompressor.forward in the h3 form: conv1 (x6 contractions, h3 output), conv2 /
-            # conv3 / deconv1 / deconv2 on three fp16 part products per MAC, deconv3 in x6
+            # conv3 / deconv1 / deconv2 / deconv3 on three fp16 part products per MAC
             e1, e2, e3, e4 = self.g6
-            (w2h, w3h), (x1, x2) = self.eh3, self.dh3
+            (w2h, w3h), (x1, x2, x3) = self.eh3, self.dh3
             hs, _ = kernels.conv1x6_gdn_h3(self.x, self.w1x6, net.Encoder.conv1.bias, e1[0], e1[2], N)
             ev(1)
             yield
@@ -181,11 +173,11 @@ class Step:
             hs, _, _ = kernels.deconv_igdn_h3(yh, x1, net.Decoder.deconv1.bias, e3[0], e3[2], int_in=True)
             ev(4)
             yield
-            _, _, hs = kernels.deconv_igdn_h3(hs, x2, net.Decoder.deconv2.bias, e4[0], e4[2],
-                                              want_h3=False, want_x6=True, chunk_major=True)
+            hs, _, _ = kernels.deconv_igdn_h3(hs, x2, net.Decoder.deconv2.bias, e4[0], e4[2],
+                                              chunk_major=True)
             ev(5)
             yield
-            clipped, _, _, bpp = kernels.deconv3_x6(hs, self.d3x6, net.Decoder.deconv3.bias,
+            clipped, _, _, bpp = kernels.deconv3_h3(hs, x3, net.Decoder.deconv3.bias,
                                                     bits=(partial, self.scale))
         elif kernels.precision() == "x6":
             e1, e2, e3, e4 = self.g6
@@ -204,15 +196,11 @@ class Step:
             hs, _, _ = kernels.deconv_igdn_x6(ys, d1, net.Decoder.deconv1.bias, *e3)
             ev(4)
             yield
-            hs, _, _ = kernels.deconv_igdn_x6(hs, d2, net.Decoder.deconv2.bias, *e4, chunk_major=D3_CM)
+            hs, _, _ = kernels.deconv_igdn_x6(hs, d2, net.Decoder.deconv2.bias, *e4, chunk_major=True)
             ev(5)
             yield
-            if D3_CM and FOLD_BITS:
-                clipped, _, _, bpp = kernels.deconv3_x6(hs, self.d3x6, net.Decoder.deconv3.bias,
-                                                        bits=(partial, self.scale))
-            else:
-                clipped, _, _ = kernels.deconv3_x6(hs, self.d3x6, net.Decoder.deconv3.bias)
-                bpp = None
+            clipped, _, _, bpp = kernels.deconv3_x6(hs, self.d3x6, net.Decoder.deconv3.bias,
+                                                    bits=(partial, self.scale))
         else:
             h = kernels.conv1_gdn(self.x, w1, net.Encoder.conv1.bias, g1[0], g1[1], N)
             ev(1)
@@ -233,7 +221,7 @@ class Step:
             bpp = None
         ev(6)
         self.last_partial = partial
-        if bpp is None:   # the separate reduction kernel (fp32 chain, or ICLR17_FOLD_BITS=0)
+        if bpp is None:   # the separate reduction kernel (fp32 chain)
             _, bpp = kernels.reduce_partials(partial, self.scale, per_image=False)
         ev(7)
         self.out = (clipped, y_hat, bpp)

@@ -12,76 +12,13 @@
 """
 from __future__ import annotations
 
-import os
 from typing import Dict, List, Optional, Sequence
 
 import torch
 
 from . import kernels
 
-# diagnostic: training conv3 on pre-split weights (ICLR17_TRAIN_W6=1; the 48-column tiles use them
-# only in a -DICLR17_C3N_W6=1 build, DESIGN.md §4: measured, not adopted)
-_TRAIN_W6 = os.environ.get("ICLR17_TRAIN_W6", "0") == "1"
-
 Tensor = torch.Tensor
-
-
-_SIDE_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
-# 0: one stream; 1: every weight-gradient kernel on the side stream; 2: only the small ones (GDN /
-# rate parameter chains, bias sums) — measured: 1 is 5 % slower than 0 (the 129 KB weight-gradient
-# workgroups and the input-gradient ones then compete for CUs)
-WGRAD_STREAM = int(__import__("os").environ.get("ICLR17_WGRAD_STREAM", "0"))
-
-
-class WgradStream:
-    """The weight-gradient half of the fused backward (k5 / k9 weight gradients, GDN and rate
-    parameter chains, their fixed-order reductions) on a second HIP stream, overlapped with the
-    input-gradient chain on the compute stream: nothing on the chain waits for a weight gradient
-    (they feed only the all-reduce and Adam), and the small reduction kernels (~5 µs each) and the
-    gaps between dependent kernels stop adding to the step. Each ``run`` is enqueued right after
-    the compute-stream kernel that produced its inputs; ``join`` makes the compute stream wait for
-    all of it. Same kernels, same operands, so the gradients are bit-identical to one stream.
-    ICLR17_WGRAD_STREAM=0 runs everything on the compute stream (A/B)."""
-
-    def __init__(self, device: torch.device, enabled: bool = True):
-        self.enabled = enabled and WGRAD_STREAM > 0 and device.type == "cuda"
-        self.produced: List[Tensor] = []
-        if self.enabled:
-            self.main = torch.cuda.current_stream(device)
-            side = _SIDE_STREAMS.get(device.index)
-            if side is None:
-                side = _SIDE_STREAMS[device.index] = torch.cuda.Stream(device=device)
-            self.side = side
-
-    def run(self, fn, *reads, big: bool = False):
-        """fn() on the side stream, after everything enqueued on the compute stream so far;
-        ``reads``: the tensors fn reads (the compute stream may free them before fn has run).
-        ``big``: a weight-gradient GEMM (side stream only in mode 1)."""
-        if not self.enabled or (big and WGRAD_STREAM != 1):
-            return fn()
-        self.side.wait_stream(self.main)
-        with torch.cuda.stream(self.side):
-            out = fn()
-        for t in reads:
-            if isinstance(t, Tensor):
-                t.record_stream(self.side)
-        self.produced.append(out)
-        return out
-
-    def join(self, extra: Sequence[Tensor] = ()) -> None:
-        """The compute stream waits for the side stream; its outputs (and ``extra``, tensors the
-        side stream allocated) stay valid for the compute stream's later use."""
-        if not self.enabled:
-            return
-        self.main.wait_stream(self.side)
-        todo = list(self.produced) + list(extra)
-        while todo:
-            t = todo.pop()
-            if isinstance(t, Tensor):
-                t.record_stream(self.main)
-            elif isinstance(t, (list, tuple)):
-                todo.extend(t)
-        self.produced = []
 
 
 class _NoBackward(torch.autograd.Function):
@@ -213,12 +150,9 @@ def conv1_input_grad(enc, g_u1: Tensor) -> Tensor:
 
 
 def analysis_backward(enc, saved: Dict[str, Tensor], g_y: Tensor,
-                      g_y_split: Optional[Tensor] = None, want_dx: bool = False,
-                      ws: Optional[WgradStream] = None) -> Dict[str, Tensor]:
+                      g_y_split: Optional[Tensor] = None, want_dx: bool = False) -> Dict[str, Tensor]:
     """∂L/∂y (NHWC) → parameter gradients of Analysis_net_17 (analysis_17.py:14-39). In the x6
-    mode the input-gradient contractions run on split-form gradients (g_y_split, or split here).
-    ``ws``: the weight gradients go to its side stream (WgradStream)."""
-    ws = ws if ws is not None else WgradStream(g_y.device, enabled=False)
+    mode the input-gradient contractions run on split-form gradients (g_y_split, or split here)."""
     bb1, gb1, _ = enc.gdn1.bounds_f32()
     bb2, gb2, _ = enc.gdn2.bounds_f32()
     w3t, w2t = enc.packed_bwd()
@@ -230,28 +164,28 @@ def analysis_backward(enc, saved: Dict[str, Tensor], g_y: Tensor,
             g_y_split = kernels.split_planes(g_y)
         x2, x1 = enc.gdn2.effective_params_bwd_x6(), enc.gdn1.effective_params_bwd_x6()
         a2s, a1s = _split_of(saved, "a2"), _split_of(saved, "a1")
-        dW3 = ws.run(lambda: kernels.wgrad_k5_x6(g_y_split, a2s), g_y_split, a2s, big=True)
+        dW3 = kernels.wgrad_k5_x6(g_y_split, a2s)
         g_u2, dn2, db2, dbe2, g_u2s = kernels.bwd_conv_gdn(g_y, w3t, saved["u2"], *x2[:3],
                                                            g_split=g_y_split, want_split=True,
                                                            g6=x2[3], g6t=x2[4], want_f32=False)
-        dW2 = ws.run(lambda: kernels.wgrad_k5_x6(g_u2s, a1s), g_u2s, a1s, big=True)
-        dg2 = ws.run(lambda: kernels.gdn_param_grads(dn2, saved["u2"], dbe2, enc.gdn2.beta,
-                                                     enc.gdn2.gamma, bb2, gb2), dn2, saved["u2"], dbe2)
+        dW2 = kernels.wgrad_k5_x6(g_u2s, a1s)
+        dg2 = kernels.gdn_param_grads(dn2, saved["u2"], dbe2, enc.gdn2.beta,
+                                                     enc.gdn2.gamma, bb2, gb2)
         g_u1, dn1, db1, dbe1, g_u1s = kernels.bwd_conv_gdn(g_u2, w2t, saved["u1"], *x1[:3],
                                                            g_split=g_u2s, want_split=True,
                                                            g6=x1[3], g6t=x1[4], want_f32=want_dx)
-        dW1 = ws.run(lambda: kernels.wgrad_k9_x6(g_u1s, saved["x"]), g_u1s, saved["x"], big=True)
+        dW1 = kernels.wgrad_k9_x6(g_u1s, saved["x"])
     else:
-        dW3 = ws.run(lambda: kernels.wgrad_k5(g_y, saved["a2"]), g_y, saved["a2"], big=True)
+        dW3 = kernels.wgrad_k5(g_y, saved["a2"])
         g_u2, dn2, db2, dbe2 = kernels.bwd_conv_gdn(g_y, w3t, saved["u2"], *p2)
-        dW2 = ws.run(lambda: kernels.wgrad_k5(g_u2, saved["a1"]), g_u2, saved["a1"], big=True)
-        dg2 = ws.run(lambda: kernels.gdn_param_grads(dn2, saved["u2"], dbe2, enc.gdn2.beta,
-                                                     enc.gdn2.gamma, bb2, gb2), dn2, saved["u2"], dbe2)
+        dW2 = kernels.wgrad_k5(g_u2, saved["a1"])
+        dg2 = kernels.gdn_param_grads(dn2, saved["u2"], dbe2, enc.gdn2.beta,
+                                                     enc.gdn2.gamma, bb2, gb2)
         g_u1, dn1, db1, dbe1 = kernels.bwd_conv_gdn(g_u2, w2t, saved["u1"], *p1)
-        dW1 = ws.run(lambda: kernels.wgrad_k9(g_u1, saved["x"]), g_u1, saved["x"], big=True)
+        dW1 = kernels.wgrad_k9(g_u1, saved["x"])
     dbeta2, dgamma2 = dg2
-    dbeta1, dgamma1 = ws.run(lambda: kernels.gdn_param_grads(dn1, saved["u1"], dbe1, enc.gdn1.beta,
-                                                             enc.gdn1.gamma, bb1, gb1), dn1, saved["u1"], dbe1)
+    dbeta1, dgamma1 = kernels.gdn_param_grads(dn1, saved["u1"], dbe1, enc.gdn1.beta,
+                                                             enc.gdn1.gamma, bb1, gb1)
     grads = {"conv1.weight": dW1, "conv1.bias": db1, "gdn1.beta": dbeta1, "gdn1.gamma": dgamma1,
              "conv2.weight": dW2, "conv2.bias": db2, "gdn2.beta": dbeta2, "gdn2.gamma": dgamma2,
              "conv3.weight": dW3}
@@ -287,12 +221,11 @@ def synthesis_forward_train(dec, y_nhwc: Tensor, x_ref: Optional[Tensor] = None,
 
 def synthesis_backward(dec, saved: Dict[str, Tensor], g_recon: Tensor, g_bpp: Optional[Tensor] = None,
                        rate_packed: Optional[Tensor] = None, count: float = 0.0,
-                       want_split: bool = False, ws: Optional[WgradStream] = None):
+                       want_split: bool = False):
     """∂L/∂recon (NCHW) → (∂L/∂ỹ NHWC incl. the rate term when g_bpp is given, parameter
     gradients of Synthesis_net_17, rate-parameter partials[, ∂L/∂ỹ in split form (x6 mode,
     else None)]). In the x6 mode the input-gradient contractions run in x6, each kernel handing
     the next its gradient in split form."""
-    ws = ws if ws is not None else WgradStream(g_recon.device, enabled=False)
     x6 = kernels.precision() != "fp32"
     N = dec.out_channel_N
     bq1, gq1, _ = dec.igdn1.bounds_f32()
@@ -311,30 +244,30 @@ def synthesis_backward(dec, saved: Dict[str, Tensor], g_recon: Tensor, g_bpp: Op
     if x6:
         s2s, s1s = _split_of(saved, "s2"), _split_of(saved, "s1")
         ys = saved.get("ys") if saved.get("ys") is not None else kernels.split_planes(y)
-        dWd3 = ws.run(lambda: kernels.wgrad_k9_x6(s2s, g_recon), s2s, g_recon, big=True)
-        dbd3 = ws.run(lambda: kernels.bias_grad_nchw(g_recon), g_recon)
+        dWd3 = kernels.wgrad_k9_x6(s2s, g_recon)
+        dbd3 = kernels.bias_grad_nchw(g_recon)
         g_v2, dnq2, dbd2, dbeq2, g_v2s = kernels.bwd_deconv3_igdn(g_recon, None, saved["v2"], *q2[:3],
                                                                   w_split=d3x, want_split=True,
                                                                   g6=q2[3], g6t=q2[4], want_f32=False)
-        dWd2 = ws.run(lambda: kernels.wgrad_k5_x6(s1s, g_v2s), s1s, g_v2s, big=True)
-        dq2 = ws.run(gdn_q2, dnq2, saved["v2"], dbeq2)
+        dWd2 = kernels.wgrad_k5_x6(s1s, g_v2s)
+        dq2 = gdn_q2()
         g_v1, dnq1, dbd1, dbeq1, g_v1s = kernels.bwd_deconv_igdn(g_v2, d2c, saved["v1"], *q1[:3],
                                                                  g_split=g_v2s, want_split=True,
                                                                  g6=q1[3], g6t=q1[4], want_f32=False)
-        dWd1 = ws.run(lambda: kernels.wgrad_k5_x6(ys, g_v1s), ys, g_v1s, big=True)
-        dq1 = ws.run(gdn_q1, dnq1, saved["v1"], dbeq1)
+        dWd1 = kernels.wgrad_k5_x6(ys, g_v1s)
+        dq1 = gdn_q1()
         r = kernels.bwd_deconv_rate(g_v1, d1c, y if g_bpp is not None else None, rate_packed,
                                     g_bpp, count, h, w, g_split=g_v1s, want_split=want_split)
         g_y, rpart, g_ys = r if want_split else (*r, None)
     else:
-        dWd3 = ws.run(lambda: kernels.wgrad_k9(saved["s2"], g_recon), saved["s2"], g_recon, big=True)
-        dbd3 = ws.run(lambda: kernels.bias_grad_nchw(g_recon), g_recon)
+        dWd3 = kernels.wgrad_k9(saved["s2"], g_recon)
+        dbd3 = kernels.bias_grad_nchw(g_recon)
         g_v2, dnq2, dbd2, dbeq2 = kernels.bwd_deconv3_igdn(g_recon, d3c, saved["v2"], *q2)
-        dWd2 = ws.run(lambda: kernels.wgrad_k5(saved["s1"], g_v2), saved["s1"], g_v2, big=True)
-        dq2 = ws.run(gdn_q2, dnq2, saved["v2"], dbeq2)
+        dWd2 = kernels.wgrad_k5(saved["s1"], g_v2)
+        dq2 = gdn_q2()
         g_v1, dnq1, dbd1, dbeq1 = kernels.bwd_deconv_igdn(g_v2, d2c, saved["v1"], *q1)
-        dWd1 = ws.run(lambda: kernels.wgrad_k5(y, g_v1), y, g_v1, big=True)
-        dq1 = ws.run(gdn_q1, dnq1, saved["v1"], dbeq1)
+        dWd1 = kernels.wgrad_k5(y, g_v1)
+        dq1 = gdn_q1()
         g_y, rpart = kernels.bwd_deconv_rate(g_v1, d1c, y if g_bpp is not None else None,
                                              rate_packed, g_bpp, count, h, w)
     dbq2, dgq2 = dq2
@@ -363,8 +296,7 @@ class CodecTrainFn(torch.autograd.Function):
         rate = be.packed()
         a2s = saved_a.get("a2s")
         if a2s is not None:
-            w3s = enc.packed_w3_split() if _TRAIN_W6 else None
-            y_tilde, bits_part, _, y_split = kernels.conv3_quant_rate_x6(a2s, w3, rate, noise, w_split=w3s)
+            y_tilde, bits_part, _, y_split = kernels.conv3_quant_rate_x6(a2s, w3, rate, noise)
         else:
             (y_tilde, bits_part), y_split = kernels.conv3_quant_rate(a2, w3, rate, noise), None
         clipped, recon, sse_part, saved_s = synthesis_forward_train(dec, y_tilde, x_ref=x,
@@ -385,19 +317,18 @@ class CodecTrainFn(torch.autograd.Function):
             g_recon = torch.zeros_like(ctx.recon)
         else:
             g_recon = kernels.grad_recon(ctx.recon, ctx.x, g_mse, g_clipped)
-        ws = WgradStream(g_recon.device)
         g_y, gs, rpart, g_ys = synthesis_backward(dec, ctx.saved_s, g_recon, g_bpp, ctx.rate,
-                                                  ctx.count, want_split=g_ytilde is None, ws=ws)
+                                                  ctx.count, want_split=g_ytilde is None)
         red = getattr(net, "_grad_reducer", None)
         red = red if red is not None and red.active else None
         if red is not None:   # the synthesis gradients all-reduce during the analysis backward
-            ws.run(lambda: red.launch(list(dec.parameters()), _ordered(dec, "", gs)))
+            red.launch(list(dec.parameters()), _ordered(dec, "", gs))
         if g_ytilde is not None:
             g_y = g_y + g_ytilde.permute(0, 2, 3, 1)
         want_dx = ctx.needs_input_grad[0]
-        rg = (ws.run(lambda: kernels.rate_param_grads(rpart, be.params_in_order()), rpart)
+        rg = (kernels.rate_param_grads(rpart, be.params_in_order())
               if g_bpp is not None else [None] * 11)
-        ga = analysis_backward(enc, ctx.saved_a, g_y.contiguous(), g_ys, want_dx=want_dx, ws=ws)
+        ga = analysis_backward(enc, ctx.saved_a, g_y.contiguous(), g_ys, want_dx=want_dx)
         grads += _ordered(enc, "Encoder.", ga)
         grads += _ordered(dec, "Decoder.", gs)
         names = [n for n, _ in be.named_parameters()]
@@ -405,10 +336,8 @@ class CodecTrainFn(torch.autograd.Function):
         rmap = dict(zip(order, rg))
         grads += [rmap[n] for n in names]
         if red is not None:
-            ws.run(lambda: red.launch(list(enc.parameters()) + list(be.parameters()),
-                                      _ordered(enc, "", ga) + [rmap[n] for n in names]))
-        # the compute stream (finish / clamp + Adam) waits for the weight gradients
-        ws.join(extra=[flat for _, flat, _ in red.pending] if red is not None else ())
+            red.launch(list(enc.parameters()) + list(be.parameters()),
+                       _ordered(enc, "", ga) + [rmap[n] for n in names])
         dx = ga.get("x")
         if dx is not None and g_mse is not None:   # the loss's own x: ∂mse/∂x = −∂mse/∂recon
             dx = dx - kernels.grad_recon(ctx.recon, ctx.x, g_mse, None)

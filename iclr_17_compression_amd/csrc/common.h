@@ -48,7 +48,7 @@ __device__ __forceinline__ f4 mfma16(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// Two-level accumulation (ICLR17_SEP_ACC, default on). A long MFMA accumulation chain puts every
+// Two-level accumulation . A long MFMA accumulation chain puts every
 // rounding at the scale of the whole running sum: for conv2 (K = 4800) the exact-f32 16x16x4
 // chain lands ~10x farther from the exact value than the reference's oneDNN conv, and
 // v_mfma_f32_16x16x32_bf16 is not a single correctly rounded C + Σ a·b (tools/mfma_numerics.hip:
@@ -57,13 +57,10 @@ __device__ __forceinline__ f4 mfma16(float a, float b, f4 c) {
 // its own and added to the accumulator with one correctly rounded VALU add; the block sums are
 // ~1/sqrt(K/32) of the total, so their own rounding is small. conv2+GDN2 pre-activations: rms
 // error vs fp64 2e-5 (fp32) / 1.1e-4 (x6) → below oneDNN's 2.1e-6.
-#ifndef ICLR17_SEP_ACC
-#define ICLR17_SEP_ACC 1
-#endif
-constexpr bool kSepAcc = ICLR17_SEP_ACC != 0;
+constexpr bool kSepAcc = true;
 
 // x6 product of one 32-deep k-block (lo·hi + hi·lo + mid·mid + mid·hi + hi·mid + hi·hi, small
-// terms first) onto acc[mt][nt]. With ICLR17_SEP_ACC the block sum is a fresh six-MFMA chain
+// terms first) onto acc[mt][nt]. With two-level accumulation (SEP) the block sum is a fresh six-MFMA chain
 // whose add into acc is deferred to the NEXT call (X6Acc holds it), so the add never waits on
 // its own chain, and a scheduling barrier keeps the chains in program order: at most two block
 // sums are live (letting the scheduler interleave every chain of a k-step, as it does with
@@ -72,11 +69,8 @@ struct X6Acc {
   f4 pend;
   int pm = -1, pn = -1;   // compile-time constants once the callers' loops are unrolled
 };
-// instruction classes that may still move across the barrier (SALU, VMEM, DS); -1: no barrier
-#ifndef ICLR17_X6_SCHED_MASK
-#define ICLR17_X6_SCHED_MASK (0x0004 | 0x0010 | 0x0080)
-#endif
-constexpr int kX6SchedMask = ICLR17_X6_SCHED_MASK;
+// instruction classes that may still move across the barrier (SALU, VMEM, DS)
+constexpr int kX6SchedMask = 0x0004 | 0x0010 | 0x0080;
 
 template <bool SEP, int MT, int NT>
 __device__ __forceinline__ void mfma_x6(f4 (&acc)[MT][NT], X6Acc& st, int mt, int nt,

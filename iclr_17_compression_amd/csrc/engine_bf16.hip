@@ -458,7 +458,7 @@ __device__ __forceinline__ void k5_body(const K5Args& a, unsigned char* smem, in
     // accumulator tile (registers 4m .. 4m + 3 of the lane's half h)
     float bits = 0.f;
     // the rate table rows of this tile's NB channels: staged in LDS after the K-split exchange
-    // area (KS == 2, ICLR17_BF_RTAB_LDS) or read from L2
+    // area (KS == 2, the rate table rows) or read from L2
     constexpr bool RT_LDS = KK::KS == 2;
     constexpr int XS_BYTES = (KK::KS * NW * NT * 8 * 64 * 4 + 1023) / 1024 * 1024;
     constexpr int RTU = NB * RT_W / 4, RTP = (RTU + 63) / 64;   // 16-byte units, 1 KB pieces
@@ -649,7 +649,6 @@ constexpr int C1U = 3 * C1P * C1RS;           // u16 elements of the bf16 plane 
 //   * the output rows leave as 16-byte stores that drain during the next block.
 // analysis_17.py:14-17 (conv1) + models/GDN.py:64-94 (GDN1).
 constexpr int C1P_WAVES = 8;
-constexpr int C1P_STK = 20, C1P_STP = 5;   // stamps: blocks per workgroup, phases per block
 constexpr int C1P_LOADS = (C1PIECES + C1P_WAVES * 64 - 1) / (C1P_WAVES * 64);   // 3 per thread
 
 template <int CO>
@@ -658,8 +657,7 @@ struct C1PL {
   static constexpr int PL = C1U * 2;                      // one bf16 plane
   static constexpr int SQ = epi_tile_bytes<CO>(64);       // x² / output tile
   static constexpr int BB = CO * 8;                       // bias, β_eff (fp32)
-  static constexpr int ST = ICLR17_C1P_STAMPS ? C1P_WAVES * C1P_STK * C1P_STP * 8 : 0;
-  static constexpr int LDS = G + 2 * PL + SQ + BB + ST;
+  static constexpr int LDS = G + 2 * PL + SQ + BB;
   static_assert(G % 1024 == 0 && LDS <= 160 * 1024, "conv1p LDS");
 };
 
@@ -814,68 +812,38 @@ conv1p_bf16_kernel(const float* __restrict__ x, int H, int W, const u16* __restr
     __syncthreads();   // x² rows of this half complete
     const int pl = pix0 + (lane & 15);
     const unsigned char* ga = sg + ((kg * CO + ncol + (lane & 15)) * 8) * 2;
-    if (ICLR17_C1P_KBO) {
-      // k-block outer: each x² fragment is read once for all NT channel tiles (not once per
-      // tile); the same per-accumulator k order, so the same bits
-      f4 nacc[NT][MT];
+    // k-block outer: each x² fragment is read once for all NT channel tiles (not once per
+    // tile); the same per-accumulator k order, so the same bits
+    f4 nacc[NT][MT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) nacc[nt][mt] = f4{0.f, 0.f, 0.f, 0.f};
+    u4 xs[2][MT], gc[2][NT];
+    auto rd = [&](int kb, int q) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) xs[q][mt] = *(lu4p)(sq + epi_off<CO>(pl + mt * 16, 32 * kb + 8 * kg));
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) gc[q][nt] = *(lu4p)(ga + (kb * 4 * CO * 8 + nt * 128) * 2);
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      if (kb + 1 < KB) rd(kb + 1, (kb + 1) & 1);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) nacc[nt][mt] = f4{0.f, 0.f, 0.f, 0.f};
-      u4 xs[2][MT], gc[2][NT];
-      auto rd = [&](int kb, int q) {
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) xs[q][mt] = *(lu4p)(sq + epi_off<CO>(pl + mt * 16, 32 * kb + 8 * kg));
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) gc[q][nt] = *(lu4p)(ga + (kb * 4 * CO * 8 + nt * 128) * 2);
-      };
-      rd(0, 0);
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb) {
-        if (kb + 1 < KB) rd(kb + 1, (kb + 1) & 1);
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt) nacc[nt][mt] = mfma_bf16(gc[kb & 1][nt], xs[kb & 1][mt], nacc[nt][mt]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const int ch = ncol + nt * 16 + 4 * kg;
-        const f4 be = *(const f4*)(sbeta + ch);
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[nt][mt][j] *= __builtin_amdgcn_rsqf(nacc[nt][mt][j] + be[j]);
-      }
-    } else {
+        for (int mt = 0; mt < MT; ++mt) nacc[nt][mt] = mfma_bf16(gc[kb & 1][nt], xs[kb & 1][mt], nacc[nt][mt]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-      f4 nacc[MT];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) nacc[mt] = f4{0.f, 0.f, 0.f, 0.f};
-      // fragments of k-block kb + 1 read while kb's MFMAs run; no deeper (register budget)
-      u4 xs[2][MT], gc[2];
-      auto rd = [&](int kb, int q) {
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) xs[q][mt] = *(lu4p)(sq + epi_off<CO>(pl + mt * 16, 32 * kb + 8 * kg));
-        gc[q] = *(lu4p)(ga + (kb * 4 * CO * 8 + nt * 128) * 2);
-      };
-      rd(0, 0);
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb) {
-        if (kb + 1 < KB) rd(kb + 1, (kb + 1) & 1);
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) nacc[mt] = mfma_bf16(gc[kb & 1], xs[kb & 1][mt], nacc[mt]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
       const int ch = ncol + nt * 16 + 4 * kg;
       const f4 be = *(const f4*)(sbeta + ch);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[nt][mt][j] *= __builtin_amdgcn_rsqf(nacc[mt][j] + be[j]);
-    }
+        for (int j = 0; j < 4; ++j) acc[nt][mt][j] *= __builtin_amdgcn_rsqf(nacc[nt][mt][j] + be[j]);
     }
     __syncthreads();   // x² reads done: the rows are rewritten with the output
 #pragma unroll
@@ -916,16 +884,11 @@ conv1p_bf16_kernel(const float* __restrict__ x, int H, int W, const u16* __restr
       // the next block's patch, in flight during this block (past the last block: a repeat of
       // this one), rounded into the idle plane after the epilogue
       load_patch(tn < ntiles ? tn : t);
-      stamp(k, 0);
       main_tile(sp0 + (k & 1) * C1U);
-      stamp(k, 1);
       epi_tile();
-      stamp(k, 2);
       store_plane(sp0 + ((k + 1) & 1) * C1U);
-      stamp(k, 3);
       copy_out(t);
       __syncthreads();   // next plane written, output rows read
-      stamp(k, 4);
     }
     return;
   }

@@ -37,27 +37,14 @@ namespace iclr17 {
 
 constexpr int BM = 64;        // output pixels per tile
 
-#ifndef ICLR17_X6_HALO
-#define ICLR17_X6_HALO 1   // x6 deconv1/deconv2: halo-patch A operand, chunk-major steps
-#endif
 
 // conv3 (+ quantiser) output columns per workgroup: 96 at N = 192, 64 at N = 128
 constexpr int conv3_bn(int N) { return N % 96 == 0 ? 96 : 64; }
 // x6 conv3 in noise mode (training) on few tiles (B·tiles < 256: B=32 at 256² holds 256
 // workgroups, one wave per SIMD): 48-column tiles on 4×1 waves, twice the workgroups. The bit
 // partials per image follow (tiles × N/48): iclr17_conv3_x6_partials_per_image.
-#ifndef ICLR17_C3_NARROW
-#define ICLR17_C3_NARROW 1
-#endif
-#ifndef ICLR17_C3N_W6
-#define ICLR17_C3N_W6 0
-#endif
-// diagnostic build: the narrow conv3 in XCD-contiguous work order (decode_tile_xcd)
-#ifndef ICLR17_C3N_XCD
-#define ICLR17_C3N_XCD 0
-#endif
 inline bool conv3_narrow(int N, int tiles, int B, int qmode) {
-  return ICLR17_C3_NARROW && N == 192 && qmode == ICLR17_QUANT_NOISE && (long)tiles * B < 256;
+  return N == 192 && qmode == ICLR17_QUANT_NOISE && (long)tiles * B < 256;
 }
 
 enum Epi : int {
@@ -207,30 +194,6 @@ __device__ __forceinline__ TileInfo decode_tile(const EngineArgs& a) {
   return t;
 }
 
-#if ICLR17_C3N_XCD
-// XCD-contiguous work order (diagnostic build, one-phase grids): dispatch slot L (x fastest) runs
-// on XCD L % 8, so work item (L % 8)·G/8 + L/8 gives each XCD one contiguous range — with the
-// column block fastest, whole images per XCD, whose input then crosses that XCD's L2 once
-// instead of once per XCD.
-template <int TH = 8>
-__device__ __forceinline__ TileInfo decode_tile_xcd(const EngineArgs& a) {
-  const int G = gridDim.x * gridDim.y;
-  int L = blockIdx.x + gridDim.x * blockIdx.y;
-  if (G % 8 == 0) L = (L % 8) * (G / 8) + L / 8;
-  TileInfo t;
-  t.th = TH;
-  int bid = L / gridDim.y;
-  t.tx = bid % a.tiles_x;
-  bid /= a.tiles_x;
-  t.ty = bid % a.tiles_y;
-  t.b = bid / a.tiles_y;
-  t.py = 0;
-  t.px = 0;
-  t.nb = L % gridDim.y;
-  return t;
-}
-#endif
-
 // Row m of a tile → output pixel (NHWC row offset in pixels) or -1 when outside the grid.
 __device__ __forceinline__ long out_pixel(const EngineArgs& a, const TileInfo& t, int m) {
   const int gy = t.ty * t.th + (m >> 3), gx = t.tx * 8 + (m & 7);
@@ -354,7 +317,7 @@ __device__ __forceinline__ void mfma_block(f4 (&acc)[MT][NT], const f4 (&af)[MT]
       for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16(af[mt][e], bf[nt][e], acc[mt][nt]);
 }
 
-// Two-level accumulation of the exact-f32 contractions (common.h, ICLR17_SEP_ACC): a 32-deep
+// Two-level accumulation of the exact-f32 contractions (common.h): a 32-deep
 // k-block (two mfma_block calls) is summed from zero into `part`, then added to acc.
 template <int MT, int NT>
 __device__ __forceinline__ void zero_tile(f4 (&t)[MT][NT]) {
@@ -1070,7 +1033,7 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   // DMA ring depth: conv3 (+ quantiser) has a third of conv2's MFMAs per step, too few to hide
   // an L2-miss DMA issued one step ahead, so it runs NS stages with a counted vmcnt wait.
   // x6 IGDN layers (deconv1 / deconv2): halo-patch A operand (see the main loop)
-  constexpr bool HALO = X6 && EPI == EPI_IGDN && BMT == BM && ICLR17_X6_HALO;
+  constexpr bool HALO = X6 && EPI == EPI_IGDN && BMT == BM;
   // per-tap two-level accumulation for the encoder layers whose latents are rounded (conv2+GDN2,
   // conv3+quantiser): their accuracy decides the ŷ flips against the reference
   constexpr bool TAPSEP = kSepAcc && !HALO && (EPI == EPI_GDN || EPI == EPI_QUANT);
@@ -1099,12 +1062,7 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (scalar branches)
   const int wm = wave / WN, wn = wave % WN;
-#if ICLR17_C3N_XCD
-  constexpr bool XCDW = X6 && EPI == EPI_QUANT && BN == 48;
-  TileInfo t = XCDW ? decode_tile_xcd<BMT / 8>(a) : decode_tile<BMT / 8>(a);
-#else
   TileInfo t = decode_tile<BMT / 8>(a);
-#endif
   const int ph = t.py * a.tt.npx + t.px;
   const int ncol0 = t.nb * BN + wn * (BN / WN);
 
@@ -1389,7 +1347,7 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   } else {
     issue(0, 0);
     if constexpr (TAPSEP) {
-      // two-level accumulation (common.h, ICLR17_SEP_ACC): each tap's NCH steps accumulate in
+      // two-level accumulation (common.h): each tap's NCH steps accumulate in
       // place from zero, and the tap sum is added to `total` with one correctly rounded add
       static_assert(NCH % 2 == 0, "stage parity = chunk parity");
       f4 total[MT][NT];
@@ -1525,12 +1483,19 @@ __device__ __forceinline__ int d3_col(int j) {
   return co * 16 + ry * 4 + rx;
 }
 
-template <int CI>
+// H3: the input in the h3 form (two fp16 planes, chunk-major from the h3 deconv2) and the
+// weights as iclr17_split_packed_h3's two planes; three v_mfma_f32_16x16x32_f16 per tile and tap
+// (lo_a·hi_w, hi_a·lo_w, hi_a·(hi_w·2¹¹)) instead of six bf16 ones, scaled back exactly before
+// the bias. Two thirds of the x6 stage bytes per step (41 A and 6 / 4 B pieces).
+template <int CI, bool H3 = false>
 __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) {
   constexpr int KCH = 32, NCH = CI / KCH;
   constexpr int MT = 4, NT = 3;
-  constexpr int NPL = 3;                                  // input planes
-  constexpr int NAI = (NPL * D3_PPX + 15) / 16;           // A wave-instructions per chunk
+  constexpr int NPL = H3 ? 2 : 3;                         // input (and weight) planes
+  // A wave-instructions per chunk (x6: 61; h3: 41, rounded up to whole rounds of the 4 waves:
+  // the 41-piece form hit a compiler fault, "Operand has incorrect register class"; the three
+  // padding pieces load the zero line)
+  constexpr int NAI = H3 ? ((NPL * D3_PPX + 15) / 16 + 3) / 4 * 4 : (NPL * D3_PPX + 15) / 16;
   constexpr int AI_W = (NAI + 3) / 4;   // x6: 16 (wave 0..3 takes i = w + 4j, i < 61)
   static_assert(3 * 64 * 65 <= D3_LDS, "epilogue block fits the stages");
   __shared__ __attribute__((aligned(16))) float smem[D3_LDS];
@@ -1591,12 +1556,12 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const int piece = wave + 4 * k;
-      if (piece >= 9 || ((st == 1 || st == 4) && piece >= 6)) break;   // wave-uniform
+      if (piece >= 3 * NPL || ((st == 1 || st == 4) && piece >= 2 * NPL)) break;   // wave-uniform
       const int slot = piece * 64 + lane;
       int tap, pl, k8, col;
       if (st == 0) {
-        tap = slot / 192;
-        const int r = slot - tap * 192;
+        tap = slot / (64 * NPL);
+        const int r = slot - tap * 64 * NPL;
         pl = r / 64; k8 = (r >> 4) & 3; col = r & 15;
       } else {
         tap = st + 2;
@@ -1630,6 +1595,30 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
     constexpr int NC = 16 * NTT;
     const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
     const unsigned short* sb = (const unsigned short*)(sB + buf * D3_SB6) + boff + g * NC * 8;
+    if constexpr (H3) {
+      u4 Bh[NTT], Bl[NTT], Bh11[NTT];
+#pragma unroll
+      for (int nt = 0; nt < NTT; ++nt) {
+        const int jc = nt * 16 + (lane & 15);
+        Bh[nt] = *(const u4*)(sb + jc * 8);
+        Bl[nt] = *(const u4*)(sb + 4 * NC * 8 + jc * 8);
+        Bh11[nt] = h3_x2048(Bh[nt]);
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int p = prow + (mt + dy) * D3_PS + dx;
+        const unsigned short* sa =
+            (const unsigned short*)(sA + p * 16 + ((g ^ (((p >> 2) & 1) << 1)) * 4));
+        const h8v Ah = __builtin_bit_cast(h8v, *(const u4*)(sa));
+        const h8v Al = __builtin_bit_cast(h8v, *(const u4*)(sa + D3_PPX * 32));
+#pragma unroll
+        for (int nt = 0; nt < NTT; ++nt) {
+          f4 c = __builtin_amdgcn_mfma_f32_16x16x32_f16(Al, __builtin_bit_cast(h8v, Bh[nt]), acc[mt][nt], 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ah, __builtin_bit_cast(h8v, Bl[nt]), c, 0, 0, 0);
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ah, __builtin_bit_cast(h8v, Bh11[nt]), c, 0, 0, 0);
+        }
+      }
+    } else {
     bf8 Bh[NTT], Bm[NTT], Bl[NTT];
 #pragma unroll
     for (int nt = 0; nt < NTT; ++nt) {
@@ -1652,6 +1641,7 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
       }
     }
     x6_flush<false>(acc, st);
+    }
   };
 
   issue_a(0);
@@ -1667,8 +1657,8 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
       if (st != 6) issue_b(cc, st + 1, (s + 1) & 1);
       if (st == 0) {
         compute(s & 1, 0, 0, std::integral_constant<int, 1>{});
-        compute(s & 1, 1, 192 * 8, std::integral_constant<int, 1>{});
-        compute(s & 1, 2, 2 * 192 * 8, std::integral_constant<int, 1>{});
+        compute(s & 1, 1, 64 * NPL * 8, std::integral_constant<int, 1>{});
+        compute(s & 1, 2, 2 * 64 * NPL * 8, std::integral_constant<int, 1>{});
       } else if (st == 1 || st == 4) {
         compute(s & 1, st + 2, 0, std::integral_constant<int, 2>{});
       } else {
@@ -1682,6 +1672,13 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
     }
   }
   __syncthreads();     // stage reads done before the epilogue reuses LDS
+  if constexpr (H3) {   // 2¹¹·σ_a·σ_w off, exactly
+    const float dsc = a.wscale[1];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = acc[mt][nt] * dsc;
+  }
 
   // epilogue: column n = co·16 + ry·4 + rx of row m = (by, bx) → output (4by + ry, 4bx + rx)
   constexpr int OS = 4 * D3_BS, SS = OS + 1;
@@ -2586,13 +2583,6 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
     if constexpr (N == 192) {
       if (X6in && conv3_narrow(N, a.tiles_x * a.tiles_y, B, qmode)) {
         a.partials_per_image = a.tiles_x * a.tiles_y * (N / 48);
-#if ICLR17_C3N_W6   // diagnostic build: the narrow tiles on pre-split weights (not adopted)
-        if (a.w6 != nullptr) {
-          hipLaunchKernelGGL((engine_kernel<N, N, 48, 4, 1, EPI_QUANT, true, true>),
-                             dim3(a.tiles_x * a.tiles_y * B, N / 48), dim3(256), 0, st, a);
-          return check_launch("conv3_quant_rate (48-column tiles)");
-        }
-#endif
         a.w6 = nullptr;   // the narrow instantiation splits its weights per k-step
         hipLaunchKernelGGL((engine_kernel<N, N, 48, 4, 1, EPI_QUANT, true>),
                            dim3(a.tiles_x * a.tiles_y * B, N / 48), dim3(256), 0, st, a);
@@ -2819,8 +2809,8 @@ struct FoldBits {
 static int launch_deconv3_halo(const uint16_t* in, int B, int H, int W, int N, const void* w,
                                const float* bias, const float* x, float* clipped, float* recon,
                                double* sse_partial, int sse_unclipped, void* stream, bool bf,
-                               int in_cm = 0, const FoldBits* fold = nullptr) {
-  const char* what = bf ? "deconv3_bf16" : "deconv3_x6";
+                               int in_cm = 0, const FoldBits* fold = nullptr, bool h3 = false) {
+  const char* what = bf ? "deconv3_bf16" : (h3 ? "deconv3_h3" : "deconv3_x6");
   int rc = check_dims(B, H, W, N);
   if (rc) return rc;
   ICLR17_REQUIRE(in && w && bias && clipped, ICLR17_EINVAL, "%s: null pointer", what);
@@ -2852,6 +2842,12 @@ static int launch_deconv3_halo(const uint16_t* in, int B, int H, int W, int N, c
       hipLaunchKernelGGL((deconv3_bf16_kernel<192>), grid, dim3(512), 0, S(stream), a);
     else
       hipLaunchKernelGGL((deconv3_bf16_kernel<128>), grid, dim3(512), 0, S(stream), a);
+  } else if (h3) {
+    a.wscale = (const float*)((const uint16_t*)w + 2L * 9 * N * 48);
+    if (N == 192)
+      hipLaunchKernelGGL((deconv3_x6_kernel<192, true>), grid, dim3(256), 0, S(stream), a);
+    else
+      hipLaunchKernelGGL((deconv3_x6_kernel<128, true>), grid, dim3(256), 0, S(stream), a);
   } else {
     if (N == 192)
       hipLaunchKernelGGL((deconv3_x6_kernel<192>), grid, dim3(256), 0, S(stream), a);
@@ -2859,6 +2855,17 @@ static int launch_deconv3_halo(const uint16_t* in, int B, int H, int W, int N, c
       hipLaunchKernelGGL((deconv3_x6_kernel<128>), grid, dim3(256), 0, S(stream), a);
   }
   return check_launch(what);
+}
+
+int iclr17_synthesis_deconv3_h3(const uint16_t* in_h3_cm, int B, int H, int W, int N,
+                                const uint16_t* w_h3, const float* bias, const float* x,
+                                float* clipped, float* recon, double* sse_partial,
+                                int sse_unclipped, const double* bits_partial, int bits_T,
+                                double* bits_per_image, float* bpp_total, double bits_scale,
+                                void* stream) {
+  const FoldBits f = {bits_partial, bits_T, bits_per_image, bpp_total, bits_scale};
+  return launch_deconv3_halo(in_h3_cm, B, H, W, N, w_h3, bias, x, clipped, recon, sse_partial,
+                             sse_unclipped, stream, false, 1, bits_partial ? &f : nullptr, true);
 }
 
 int iclr17_synthesis_deconv3_x6(const uint16_t* in_split, int B, int H, int W, int N,

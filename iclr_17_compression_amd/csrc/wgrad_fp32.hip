@@ -19,9 +19,6 @@ namespace {
 
 hipStream_t S(void* s) { return (hipStream_t)s; }
 
-#ifndef ICLR17_K9_IM2COL_DMA
-#define ICLR17_K9_IM2COL_DMA 0   // 1: k9 x6 weight gradient through the materialised split im2col (A/B)
-#endif
 constexpr int KP = 32;  // pixels per k-step
 
 __device__ __attribute__((aligned(16))) float g_wzero[4] = {0.f, 0.f, 0.f, 0.f};
@@ -775,47 +772,6 @@ __global__ void __launch_bounds__(512) wgrad_x6_row_kernel(const unsigned short*
         }
 }
 
-// k9 s4 p4 weight gradient in x6 as a 1×1 one: the 243 (c, kh, kw) window values of every
-// output pixel, split, as the X operand [3][P][256] (k = c·81 + kh·9 + kw, the PyTorch
-// [M][3][9][9] order; k ≥ 243 zero) — im2col of a 3-channel NCHW image, 8 k per thread.
-constexpr int I9_OX = 64, I9_COLS = 4 * I9_OX + 8;   // output pixels / window columns per block
-__global__ void __launch_bounds__(256) im2col9_split_kernel(const float* __restrict__ X, int B,
-                                                            int Ho, int Wo,
-                                                            unsigned short* __restrict__ planes) {
-  // grid: (⌈Wo / 64⌉, B·Ho). The block stages the 9 input rows × 264 columns × 3 channels its 64
-  // output pixels read (coalesced, zeros outside the image), then gathers the windows from LDS.
-  __shared__ float win[3][9][I9_COLS];
-  const int P = B * Ho * Wo;
-  const int row = blockIdx.y, oy = row % Ho, b = row / Ho;   // workgroup-uniform
-  const int ox0 = blockIdx.x * I9_OX;
-  const int H = Ho * 4, W = Wo * 4;
-  const float* __restrict__ xb = X + (long)b * 3 * H * W;
-  for (int i = threadIdx.x; i < 3 * 9 * I9_COLS; i += 256) {
-    const int c = i / (9 * I9_COLS), r = (i / I9_COLS) % 9, col = i % I9_COLS;
-    const int iy = oy * 4 - 4 + r, ix = ox0 * 4 - 4 + col;
-    win[c][r][col] = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W
-                         ? xb[((long)c * H + iy) * W + ix] : 0.f;
-  }
-  __syncthreads();
-  const int nox = Wo - ox0 < I9_OX ? Wo - ox0 : I9_OX;
-  for (int t = threadIdx.x; t < nox * 32; t += 256) {
-    const int ox = t >> 5, kg = t & 31;
-    float v[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int k = kg * 8 + e;
-      const int c = k / 81, kh = (k % 81) / 9, kw = k % 9;
-      v[e] = k < 243 ? win[c][kh][ox * 4 + kw] : 0.f;
-    }
-    u4 hi, mi, lo;
-    split8(f4{v[0], v[1], v[2], v[3]}, f4{v[4], v[5], v[6], v[7]}, hi, mi, lo);
-    const int p = row * Wo + ox0 + ox;
-    unsigned short* d = planes + (long)p * 256 + kg * 8;
-    *(u4*)d = hi;
-    *(u4*)(d + (long)P * 256) = mi;
-    *(u4*)(d + 2L * P * 256) = lo;
-  }
-}
 
 // Σ over splits of part[s][m][256] → dW[m][243] (fixed split order, 8 loads in flight).
 __global__ void sum_splits_k9_kernel(const float* __restrict__ part, int nsplit, int M,
@@ -1116,8 +1072,8 @@ size_t iclr17_wgrad_workspace_size(int kind, int B, int Ho, int Wo, int M, int C
   const long P = (long)B * Ho * Wo;
   if (kind == 9) return (size_t)wgrad9_splits(B * ((Wo + 7) / 8) * ((Ho + 7) / 8)) * M * 243;
   if (kind == 6) return (size_t)wgrad6_splits(P, 5 * (C / 64)) * M * C * 25;
-  if (kind == 7)   // k9 x6: partials [ns][M][256] (+ the split im2col [3][P][256] u16 of the A/B build)
-    return (size_t)wgrad6_splits(P, 2) * M * 256 + (ICLR17_K9_IM2COL_DMA ? (size_t)P * 256 * 3 / 2 : 0);
+  if (kind == 7)   // k9 x6: partials [ns][M][256]
+    return (size_t)wgrad6_splits(P, 2) * M * 256;
   const int ntap = kind == 1 ? 1 : 25;
   const int tiles = ntap * (C / 64);
   return (size_t)wgrad_splits(P, tiles) * M * C * ntap;
@@ -1186,17 +1142,7 @@ int iclr17_wgrad_k9_x6(const uint16_t* G_split, const float* X, int B, int Ho, i
   dim3 grid((tiles * ns + 7) / 8 * 8);
   const unsigned short* g6 = (const unsigned short*)G_split;
   int rc;
-  if (ICLR17_K9_IM2COL_DMA) {   // diagnostic: the materialised split im2col + the 1×1 kernel
-    unsigned short* cols = (unsigned short*)(workspace + (long)ns * M * 256);
-    hipLaunchKernelGGL(im2col9_split_kernel, dim3((Wo + I9_OX - 1) / I9_OX, B * Ho), dim3(256), 0, st,
-                       X, B, Ho, Wo, cols);
-    rc = check_launch("wgrad_k9_x6_im2col");
-    if (rc) return rc;
-    if (M == 192)
-      hipLaunchKernelGGL((wgrad_x6_1x1_kernel<192, 128>), grid, dim3(512), 0, st, g6, P * M, cols, P * 256, P, 256, ns, part, nullptr, 0, 0);
-    else
-      hipLaunchKernelGGL((wgrad_x6_1x1_kernel<128, 128>), grid, dim3(512), 0, st, g6, P * M, cols, P * 256, P, 256, ns, part, nullptr, 0, 0);
-  } else if (M == 192) {
+  if (M == 192) {
     hipLaunchKernelGGL((wgrad_x6_1x1_kernel<192, 128, true>), grid, dim3(512), 0, st, g6, P * M, nullptr, 0L, P, 256, ns, part, X, Ho, Wo);
   } else {
     hipLaunchKernelGGL((wgrad_x6_1x1_kernel<128, 128, true>), grid, dim3(512), 0, st, g6, P * M, nullptr, 0L, P, 256, ns, part, X, Ho, Wo);

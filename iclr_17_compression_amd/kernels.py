@@ -251,14 +251,17 @@ def deconv_igdn(h: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: Tenso
 
 # ------------------------------------------------------------- x6 (bf16x6) precision mode
 PRECISIONS = ("x6", "h3", "fp32", "bf16")
-_precision = os.environ.get("ICLR17_PRECISION", "x6")
+_precision = os.environ.get("ICLR17_PRECISION", "h3")
 
 
 def precision() -> str:
-    """Inference contraction mode: "x6" (bf16x6 split products on the bf16 MFMA, fp32-accurate;
-    default), "fp32" (exact-f32 MFMA products) or "bf16" (the throughput mode: bf16 activations
-    and weights, one bf16 product per MAC, fp32 accumulation — no parity claim). Training runs
-    the x6 kernels in the x6 and bf16 modes and exact f32 in the fp32 mode."""
+    """Inference contraction mode: "h3" (the parity default: fp32 operands as two fp16 parts,
+    three part products per MAC on the f16 MFMA for conv2, conv3, deconv1, deconv2, x6 for conv1,
+    deconv3 and the GDN contractions; fp32-accurate), "x6" (bf16x6 split products on the bf16
+    MFMA everywhere, fp32-accurate), "fp32" (exact-f32 MFMA products) or "bf16" (the throughput
+    mode: bf16 activations and weights, one bf16 product per MAC, fp32 accumulation — no parity
+    claim). Training runs the x6 kernels in the h3, x6 and bf16 modes and exact f32 in the fp32
+    mode."""
     if _precision not in PRECISIONS:
         raise Iclr17Error(f"iclr17: ICLR17_PRECISION must be one of {PRECISIONS} (got {_precision!r})")
     return _precision
@@ -711,6 +714,47 @@ def deconv3_x6(hs: Tensor, w_split: Tensor, bias: Tensor, x_ref: Optional[Tensor
         raise Iclr17Error("iclr17: deconv3_x6 folds the bit reduction only on the chunk-major input")
     return _deconv3_halo("iclr17_synthesis_deconv3_x6_cm" if cm else "iclr17_synthesis_deconv3_x6",
                          hs, B, h4, w4, N, w_split, bias, x_ref, want_recon, sse_unclipped, bits)
+
+
+def deconv3_h3(hs: Tensor, w_h3: Tensor, bias: Tensor, x_ref: Optional[Tensor] = None,
+               want_recon: bool = False, sse_unclipped: bool = False,
+               bits: Optional[Tuple[Tensor, float]] = None):
+    """deconv3 on the chunk-major h3 input [2,B,N/32,H/4,W/4,32] of ``deconv_igdn_h3(chunk_major
+    =True)`` (the halo-tiled kernel, three fp16 part products per MAC); w_h3: ``split_packed_h3``
+    of the ICLR17_W_DECONV9 packing (Synthesis_net_17.packed_h3). Returns as ``deconv3_x6``."""
+    if (not isinstance(hs, Tensor) or hs.dim() != 6 or hs.dtype != torch.int16 or hs.shape[0] != 2
+            or hs.shape[5] != 32 or not hs.is_cuda or not hs.is_contiguous()):
+        raise Iclr17Error("iclr17: deconv3_h3 takes a contiguous chunk-major h3 activation "
+                          "[2,B,N/32,h,w,32]")
+    _, B, nch, h4, w4, _ = hs.shape
+    N = 32 * nch
+    if (not isinstance(w_h3, Tensor) or w_h3.dtype != torch.int16
+            or w_h3.numel() != query("iclr17_split_packed_h3_size", 9, N, 48)):
+        raise Iclr17Error("iclr17: deconv3_h3 takes split_packed_h3 of the deconv3 packing")
+    _check_channels(N)
+    H, W = 4 * h4, 4 * w4
+    _check_image_dims(H, W)
+    clipped = torch.empty(B, 3, H, W, device=hs.device, dtype=torch.float32)
+    recon = torch.empty_like(clipped) if want_recon else None
+    partial = None
+    if x_ref is not None:
+        _check(x_ref, "reference image", 4)
+        if tuple(x_ref.shape) != (B, 3, H, W):
+            raise Iclr17Error("iclr17: reference image shape mismatch")
+        x_ref = x_ref.contiguous()
+        partial = torch.empty(B, output_partials_per_image(H, W), device=hs.device, dtype=torch.float64)
+    bp, scale, total = None, 0.0, None
+    if bits is not None:
+        bp, scale = bits
+        _check_f64(bp)
+        if bp.shape[0] != B:
+            raise Iclr17Error("iclr17: bit partials are not [B, T]")
+        bp = bp.contiguous()
+        total = torch.empty((), device=hs.device, dtype=torch.float32)
+    call("iclr17_synthesis_deconv3_h3", _p(hs), B, H, W, N, _p(w_h3), _p(bias), _p(x_ref),
+         _p(clipped), _p(recon), _p(partial), int(sse_unclipped), _p(bp),
+         bp.shape[1] if bp is not None else 0, None, _p(total), ctypes.c_double(scale), _stream(hs))
+    return (clipped, recon, partial) if bits is None else (clipped, recon, partial, total)
 
 
 def _deconv3_halo(fn, hs, B, h4, w4, N, wp, bias, x_ref, want_recon, sse_unclipped, bits=None):

@@ -55,13 +55,17 @@ class Synthesis_net_17(nn.Module):
 
     def packed_h3k(self, force: bool = False):
         """deconv1 / deconv2 in the h3 engine's two fp16 weight planes (4 stride phases, per-tensor
-        power-of-two scale in the trailer), cached until the weights change."""
+        power-of-two scale in the trailer) and deconv3's all-phase packing split the same way,
+        cached until the weights change."""
         N, f = self.out_channel_N, force
         d1 = self._pack.get("d1h3", (self.deconv1.weight,),
                             lambda: kernels.pack_h3k(_lib.ICLR17_H3K_DECONV5, self.deconv1.weight, N), f)
         d2 = self._pack.get("d2h3", (self.deconv2.weight,),
                             lambda: kernels.pack_h3k(_lib.ICLR17_H3K_DECONV5, self.deconv2.weight, N), f)
-        return d1, d2
+        d3 = self.packed(force)[2]
+        d3h = self._pack.get("d3h3", (self.deconv3.weight,),
+                             lambda: kernels.split_packed_h3(d3, 9, N, 48), f)
+        return d1, d2, d3h
 
     def packed_bf16(self, force: bool = False):
         """deconv1 / deconv2 in the bf16 engine's step layout (4 stride phases) and deconv3's
@@ -103,7 +107,7 @@ class Synthesis_net_17(nn.Module):
                y_integral=False, bits=None, y_h3=None):
         """NHWC latent → (clipped NCHW, unclipped NCHW | None, SSE partials | None).
         With ``y_split`` (the latent in x6 split form) the three layers run in the x6 mode, with
-        ``y_h3`` (the h3 form) deconv1 / deconv2 run in the h3 form and deconv3 in x6, with
+        ``y_h3`` (the h3 form) the three layers run in the h3 form, with
         ``y_bf16`` (bf16 bit patterns) in the bf16 throughput mode. ``y_integral``: the latent
         is ŷ = round(y) (model.py:56), so the h3 deconv1 takes its integer-input form.
         ``bits`` = (conv3's bit partials, scale): a fourth output, ``reduce_partials``' 0-dim total,
@@ -118,15 +122,14 @@ class Synthesis_net_17(nn.Module):
                                         bits=bits)
         if y_h3 is not None:
             q1, q2 = self.igdn1.effective_params_x6(), self.igdn2.effective_params_x6()
-            w1, w2 = self.packed_h3k()
+            w1, w2, w3 = self.packed_h3k()
             # on ŷ the integer-input form skips the lo products (the same bits: Decoder(round(y))
             # reproduces the codec's reconstruction without knowing its input is ŷ)
             hs, _, _ = kernels.deconv_igdn_h3(y_h3, w1, self.deconv1.bias, q1[0], q1[2],
                                               int_in=y_integral)
-            _, _, s6 = kernels.deconv_igdn_h3(hs, w2, self.deconv2.bias, q2[0], q2[2], want_h3=False,
-                                              want_x6=True, chunk_major=True)
-            return kernels.deconv3_x6(s6, self.packed_x6(), self.deconv3.bias, x_ref=x_ref,
-                                      want_recon=want_recon, bits=bits)
+            hs, _, _ = kernels.deconv_igdn_h3(hs, w2, self.deconv2.bias, q2[0], q2[2], chunk_major=True)
+            return kernels.deconv3_h3(hs, w3, self.deconv3.bias, x_ref=x_ref, want_recon=want_recon,
+                                      bits=bits)
         if y_split is not None:
             q1, q2 = self.igdn1.effective_params_x6(), self.igdn2.effective_params_x6()
             hs, _, _ = kernels.deconv_igdn_x6(y_split, d1, self.deconv1.bias, *q1)

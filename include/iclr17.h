@@ -507,6 +507,17 @@ int iclr17_analysis_conv3_quant_rate_h3(const uint16_t* in_h3, int B, int H, int
                                         const float* rate_packed, const float* rate_table,
                                         float* y_out, float* y_hat, uint16_t* y_hat_h3,
                                         double* bits_partial, int* range_flag, void* stream);
+/* synthesis_17.py:23-25 deconv3 + model.py:59 clamp on the h3 form: the chunk-major h3 input
+ * [2][B][N/32][H/4][W/4][32] (iclr17_synthesis_deconv_igdn_h3 with out_cm) → clipped NCHW fp32
+ * (+ unclipped, + SSE partials as iclr17_synthesis_deconv3); w_h3: iclr17_split_packed_h3 of the
+ * ICLR17_W_DECONV9 packing (taps 9, K N, columns 48). bits_partial non-NULL: the bit reduction
+ * folded in as iclr17_synthesis_deconv3_x6_cm_bits (bits_per_image nullable). */
+int iclr17_synthesis_deconv3_h3(const uint16_t* in_h3_cm, int B, int H, int W, int N,
+                                const uint16_t* w_h3, const float* bias, const float* x,
+                                float* clipped, float* recon, double* sse_partial,
+                                int sse_unclipped, const double* bits_partial, int bits_T,
+                                double* bits_per_image, float* bpp_total, double bits_scale,
+                                void* stream);
 /* synthesis_17.py:15-22 deconv + IGDN on the h3 form: input [2][B][h][w][N] → fp32 NHWC
  * [B][2h][2w][N] and/or the h3 output [2][B][2h][2w][N] and/or the x6 split output
  * [3][B][2h][2w][N] (each nullable, not all; the h3 and x6 outputs chunk-major

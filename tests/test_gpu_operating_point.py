@@ -205,7 +205,7 @@ def test_g8_all_images(device, opset, golden_dir, precision):
 
 def test_g8_testkodak_lines_verbatim(device, opset, golden_dir):
     """train.py:171-179 as written on the build's names, every image, against the reference's
-    values at the same bars as test_g8_all_images (x6, the default precision)."""
+    values at the same bars as test_g8_all_images (h3, the default precision)."""
     ns = {}
     exec("from iclr_17_compression_amd.model import *", ns)
     ms_ssim, np_, torch_ = ns["ms_ssim"], ns["np"], ns["torch"]

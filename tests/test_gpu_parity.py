@@ -649,7 +649,7 @@ def test_h3_deconv_igdn(device, N, hw):
     dec = net.Decoder
     F = torch.nn.functional
     h, w = hw
-    x1, x2 = dec.packed_h3k()
+    x1, x2 = dec.packed_h3k()[:2]
     d1, d2 = dec.packed()[:2]
     q1, q2 = dec.igdn1.effective_params_x6(), dec.igdn2.effective_params_x6()
     yq = torch.round(torch.from_numpy(synth.uniform(5, (2, N, h, w), -6, 6)))
@@ -690,6 +690,40 @@ def test_h3_deconv_igdn(device, N, hw):
                                                    int_in=True)
                 assert torch.equal(fbi, fb) and not torch.equal(fb, f)
     assert int(flag.item()) == 0
+
+
+@pytest.mark.parametrize("N", [192, 128])
+def test_h3_deconv3(device, N):
+    """deconv3 + clamp on the chunk-major h3 input (three fp16 part products per MAC) against the
+    oracle's conv_transpose2d + clamp from the same activation, at the fp32 bar, and against the x6
+    halo kernel to two-summation-order noise; the SSE partials and the folded bit reduction agree
+    with their separate kernels."""
+    net, sd = net_for(N, 3, device), sd_for(N, 3)
+    dec = net.Decoder
+    h = torch.from_numpy(synth.normal_like(7, (2, N, 16, 24), 0.5))
+    x = image(9, 2, 64, 96).to(device)
+    hh = kernels.h3_planes(nhwc(h).contiguous().to(device))
+    hcm = hh.reshape(2, 2, 16, 24, N // 32, 32).permute(0, 1, 4, 2, 3, 5).contiguous()
+    w3 = dec.packed_h3k()[2]
+    torch.manual_seed(1)
+    part = (torch.rand(2, 5, dtype=torch.float64) * 50.0).to(device)
+    with torch.no_grad():
+        c, r, sse = kernels.deconv3_h3(hcm, w3, dec.deconv3.bias, x_ref=x, want_recon=True)
+        c2, r2, sse2, tot = kernels.deconv3_h3(hcm, w3, dec.deconv3.bias, x_ref=x, want_recon=True,
+                                               bits=(part, 1.0 / 777.0))
+        ref_r = torch.nn.functional.conv_transpose2d(kernels.merge_h3(hh).permute(0, 3, 1, 2).cpu(),
+                                                     sd["Decoder.deconv3.weight"], sd["Decoder.deconv3.bias"],
+                                                     stride=4, padding=4, output_padding=3)
+        s6 = kernels.split_planes(nhwc(h).contiguous().to(device))
+        s6cm = s6.reshape(3, 2, 16, 24, N // 32, 32).permute(0, 1, 4, 2, 3, 5).contiguous()
+        c6, r6, _ = kernels.deconv3_x6(s6cm, dec.packed_x6(), dec.deconv3.bias, x_ref=x, want_recon=True)
+    assert rel_err(r, ref_r) < REL and torch.equal(c.cpu(), ref_r.clamp(0, 1)) or rel_err(c, ref_r.clamp(0, 1)) < REL
+    assert rel_err(r, r6) < 2e-6
+    assert torch.equal(c, c2) and torch.equal(r, r2) and torch.equal(sse, sse2)
+    _, ref_tot = kernels.reduce_partials(part, 1.0 / 777.0, per_image=False)
+    assert torch.equal(tot, ref_tot)
+    d = (c - x).double()
+    assert abs(sse.sum().item() - (d * d).sum().item()) <= 1e-6 * (d * d).sum().item()
 
 
 @pytest.mark.parametrize("N,B,hw", [(192, 3, (48, 80)), (128, 2, (32, 32)), (192, 40, (32, 32))])

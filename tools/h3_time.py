@@ -18,7 +18,7 @@ net.load_state_dict({k: torch.from_numpy(v) for k, v in synth.trained_like_state
 net = net.to(dev).eval()
 dec = net.Decoder
 d1, d2 = dec.packed()[:2]
-x1, x2 = dec.packed_h3k()
+x1, x2 = dec.packed_h3k()[:2]
 q1, q2 = dec.igdn1.effective_params_x6(), dec.igdn2.effective_params_x6()
 act = torch.from_numpy(synth.normal_like(6, (B, 32, 32, N), 0.7)).to(dev)
 yq = torch.round(torch.from_numpy(synth.uniform(5, (B, 16, 16, N), -6, 6))).to(dev)

@@ -113,6 +113,7 @@ class Step:
         self.d3x6 = net.Decoder.packed_x6()
         self.dh3 = net.Decoder.packed_h3k()
         self.eh3 = net.Encoder.packed_h3()
+        self.gh3 = [net.Decoder.igdn1.effective_params_h3(), net.Decoder.igdn2.effective_params_h3()]
         self.rate = net.bitEstimator.packed()
         gdns = (net.Encoder.gdn1, net.Encoder.gdn2, net.Decoder.igdn1, net.Decoder.igdn2)
         self.w1x6 = net.Encoder.packed_conv1_x6()
@@ -170,11 +171,11 @@ class Step:
             y_hat, partial, _, yh = kernels.conv3_quant_rate_h3(hs, w3h, self.rate, rtab=self.rtab)
             ev(3)
             yield
-            hs, _, _ = kernels.deconv_igdn_h3(yh, x1, net.Decoder.deconv1.bias, e3[0], e3[2], int_in=True)
+            h3, h4 = self.gh3
+            hs, _, _ = kernels.deconv_igdn_h3(yh, x1, net.Decoder.deconv1.bias, *h3, int_in=True)
             ev(4)
             yield
-            hs, _, _ = kernels.deconv_igdn_h3(hs, x2, net.Decoder.deconv2.bias, e4[0], e4[2],
-                                              chunk_major=True)
+            hs, _, _ = kernels.deconv_igdn_h3(hs, x2, net.Decoder.deconv2.bias, *h4, chunk_major=True)
             ev(5)
             yield
             clipped, _, _, bpp = kernels.deconv3_h3(hs, x3, net.Decoder.deconv3.bias,

@@ -22,8 +22,9 @@
 // workgroup over the input window and fall back to the full body otherwise.
 //
 // Epilogue: x = acc·2⁻¹¹/(σ_a·σ_w) + bias (a power-of-two scale: exact), then the GDN / IGDN
-// contraction n = Σ_j γ[i][j]·x_j² in x6 (γ split into three bf16 planes, staged in LDS half the
-// output channels at a time; x² split in registers), y = x·√(β + n) | x / √(β + n), and y stored
+// contraction n = Σ_j γ[i][j]·x_j² in the h3 form (γ split into two fp16 planes, staged in LDS
+// half the output channels at a time; x² scaled per pixel by a power of two and split in
+// registers), y = x·√(β + n) | x / √(β + n), and y stored
 // as fp32 and/or in the h3 form (NHWC, or chunk-major [2][B][N/32][h][w][32]) and/or the x6
 // split form.
 #include <string.h>
@@ -60,7 +61,9 @@ struct HArgs {
   const float* wscale;  // the packing's trailer: [0] max|w|, [1] 2⁻¹¹/(σ_a·σ_w)
   const float* bias;    // [CO]
   const float* beta;    // β_eff [CO]
-  const u16* gamma6;    // γ_eff split (x6) [3][CO/8][CO][8]
+  const u16* gamma_h3;  // γ_eff in the h3 form (iclr17_split_packed_h3, taps 1): [2][CO/8][CO][8]
+                        // + trailer (gamma_scale: [1] = 2⁻¹¹/(σ_a·σ_γ))
+  const float* gamma_scale;
   float* out;           // fp32 NHWC [B][Hout][Wout][CO] or null
   u16* out_h3;          // h3 output: NHWC [2][B][Hout][Wout][CO] or chunk-major (out_cm)
   long out_h3_plane;    //   [2][B][CO/32][Hout][Wout][32]
@@ -89,7 +92,7 @@ struct HK {
   static constexpr int MAIN = 2 * PBUF + NST * SB + 1024;
   static constexpr int NTH = NT / 2;           // epilogue: output tiles per pass
   static constexpr int KB = CO / 16;           // epilogue: 16-channel k-blocks
-  static constexpr int GBL = 3 * NTH * KB;     // epilogue: γ fragment blocks per pass (1 KB)
+  static constexpr int GBL = 2 * NTH * KB;     // epilogue: γ fragment blocks per pass (1 KB)
   static constexpr int LDS0 = MAIN > GBL * 1024 ? MAIN : GBL * 1024;
   static constexpr int BBOFF = (LDS0 + 1023) / 1024 * 1024;
   static constexpr int LDS = BBOFF + 2048;     // + bias, β_eff
@@ -281,21 +284,44 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
     }
   constexpr int NTH = KK::NTH, KB = KK::KB;
   bool ovf = false;
+  // The channel contraction n_i = Σ_j γ_ij·x_j² in the h3 form. x² of a pixel (rounded to fp32,
+  // as conv2d(x², γ) sees it) is scaled by a power of two s_p that puts the pixel's largest x²
+  // in [2¹³, 2¹⁴) — the pixel is this lane's MFMA column, so the scale is undone per lane — and
+  // split into hi / lo fp16 planes; γ arrives split with its own per-tensor power of two. The
+  // pixel's 192 channels sit in this lane (96) and lane r32 + 32·(1 − h) (the other 96).
+  float mx = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) mx = fmaxf(mx, fabsf(acc[i][j]));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  int ep = 0;   // s_p = 2^ep
+  {
+    const float m2 = mx * mx;
+    if (m2 > 0.f && m2 <= 3.40282347e38f) {
+      int e;
+      frexpf(m2, &e);   // m2 ∈ [2^(e−1), 2^e)
+      ep = 14 - e;
+    }
+  }
+  const float sp = ldexpf(1.0f, ep);
+  // n = acc_n · 2⁻¹¹ / (σ_γ · s_p) = acc_n · gamma_scale[1] · σ_a / s_p (powers of two: exact)
+  const float nsc = ldexpf(a.gamma_scale[1] * kH3Sa, -ep);
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf) {
     if (hf) __syncthreads();   // every wave's pass-0 γ reads done before the restage
     // opaque to the optimiser: pass 1 recomputes the x² planes instead of keeping pass 0's
-    // (12 k-blocks × 3 planes × 4 registers) alive across the passes
+    // (12 k-blocks × 2 planes × 4 registers) alive across the passes
 #pragma unroll
     for (int i = 0; i < NT; ++i)
 #pragma unroll
       for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(acc[i][j]));
-    // γ rows 32·(hf·NTH + il) .. of the three planes: block (plane, il, kb), lane (r32, h) ←
+    // γ rows 32·(hf·NTH + il) .. of the two planes: block (plane, il, kb), lane (r32, h) ←
     // γ_p[32(hf·NTH + il) + r32][16kb + 8h .. +7] (the [CO/8][CO][8] packing)
     for (int blk = wave; blk < KK::GBL; blk += NW) {
       const int p = blk / (NTH * KB), rem = blk - p * NTH * KB;
       const int il = rem / KB, kb = rem - il * KB;
-      glds16(a.gamma6 + (long)p * CO * CO + ((2 * kb + h) * CO + 32 * (hf * NTH + il) + r32) * 8,
+      glds16(a.gamma_h3 + (long)p * CO * CO + ((2 * kb + h) * CO + 32 * (hf * NTH + il) + r32) * 8,
              smem + blk * 1024);
     }
     vm_barrier();
@@ -307,45 +333,44 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
     const unsigned char* sg = smem + lane * 16;
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) {
-      // x² of channels 16kb .. 16kb + 15 as three B planes: the accumulator rows a lane holds are
-      // 4h + 0..3 and 8 + 4h + 0..3 of the 16-channel block; one permlane32 swap per register
-      // pair and plane hands lanes h the 8 consecutive channels 8h .. 8h + 7
+      // x²·s_p of channels 16kb .. 16kb + 15 as the hi / lo B planes: the accumulator rows a lane
+      // holds are 4h + 0..3 and 8 + 4h + 0..3 of the 16-channel block; one permlane32 swap per
+      // register pair and plane hands lanes h the 8 consecutive channels 8h .. 8h + 7
       const int i = kb >> 1, r0 = 8 * (kb & 1);
-      float sq[8];
+      unsigned hv[4], lv[4];   // channel pairs (2q, 2q + 1) of the lane's 8, packed fp16
 #pragma unroll
-      for (int j = 0; j < 8; ++j) sq[j] = acc[i][r0 + j] * acc[i][r0 + j];
-      u4 xp[3];
+      for (int q = 0; q < 4; ++q) {
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        const f2 v = f2{acc[i][r0 + 2 * q] * acc[i][r0 + 2 * q], acc[i][r0 + 2 * q + 1] * acc[i][r0 + 2 * q + 1]} * sp;
+        const h2v hh = __builtin_convertvector(v, h2v);
+        const h2v ll = __builtin_convertvector((v - __builtin_convertvector(hh, f2)) * 2048.0f, h2v);
+        hv[q] = __builtin_bit_cast(unsigned, hh);
+        lv[q] = __builtin_bit_cast(unsigned, ll);
+      }
+      u4 xp[2];
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {   // plane p of the exact split: hi, then mid, then lo
-        unsigned v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          v[j] = __float_as_uint(sq[j]) & 0xffff0000u;
-          if (p < 2) sq[j] -= __uint_as_float(v[j]);   // remainder for the next plane (exact)
-          else v[j] = __float_as_uint(sq[j]);
-        }
-        const unsigned lo0 = __builtin_amdgcn_perm(v[1], v[0], 0x07060302u);
-        const unsigned lo1 = __builtin_amdgcn_perm(v[3], v[2], 0x07060302u);
-        const unsigned hi0 = __builtin_amdgcn_perm(v[5], v[4], 0x07060302u);
-        const unsigned hi1 = __builtin_amdgcn_perm(v[7], v[6], 0x07060302u);
+      for (int pl = 0; pl < 2; ++pl) {
+        const unsigned* v = pl == 0 ? hv : lv;
+        const unsigned lo0 = v[0], lo1 = v[1];
+        const unsigned hi0 = v[2], hi1 = v[3];
         const auto s0 = __builtin_amdgcn_permlane32_swap(lo0, hi0, false, false);
         const auto s1 = __builtin_amdgcn_permlane32_swap(lo1, hi1, false, false);
-        xp[p] = u4{s0[0], s1[0], s0[1], s1[1]};
+        xp[pl] = u4{s0[0], s1[0], s0[1], s1[1]};
       }
 #pragma unroll
       for (int il = 0; il < NTH; ++il) {
         const u4 gh = *(lu4p)(sg + ((0 * NTH + il) * KB + kb) * 1024);
-        const u4 gm = *(lu4p)(sg + ((1 * NTH + il) * KB + kb) * 1024);
-        const u4 gl = *(lu4p)(sg + ((2 * NTH + il) * KB + kb) * 1024);
-        f16v t = mfma32(gl, xp[0], n[il]);
-        t = mfma32(gh, xp[2], t);
-        t = mfma32(gm, xp[1], t);
-        t = mfma32(gm, xp[0], t);
-        t = mfma32(gh, xp[1], t);
-        n[il] = mfma32(gh, xp[0], t);
+        const u4 gl = *(lu4p)(sg + ((1 * NTH + il) * KB + kb) * 1024);
+        f16v t = mfma32h(gh, xp[1], n[il]);
+        t = mfma32h(gl, xp[0], t);
+        n[il] = mfma32h(h3_x2048(gh), xp[0], t);
       }
       __builtin_amdgcn_sched_barrier(0);   // one k-block's operands live at a time
     }
+#pragma unroll
+    for (int il = 0; il < NTH; ++il)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) n[il][j] = n[il][j] * nsc;
     // y = x·√(β + n) (IGDN) | x / √(β + n) (GDN); stores
 #pragma unroll
     for (int il = 0; il < NTH; ++il) {
@@ -663,11 +688,11 @@ int iclr17_h3_planes(const float* x, long n, uint16_t* planes, int* range_flag, 
 
 int iclr17_synthesis_deconv_igdn_h3(const uint16_t* in_h3, int B, int h, int w, int N,
                                     const uint16_t* w_h3k, const float* bias,
-                                    const float* beta_eff, const uint16_t* gamma_split,
+                                    const float* beta_eff, const uint16_t* gamma_h3,
                                     float* out, uint16_t* out_h3, uint16_t* out_x6, int out_cm,
                                     int int_in, int* range_flag, void* stream) {
   ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "deconv_igdn_h3: N=%d", N);
-  ICLR17_REQUIRE(in_h3 && w_h3k && bias && beta_eff && gamma_split && (out || out_h3 || out_x6) &&
+  ICLR17_REQUIRE(in_h3 && w_h3k && bias && beta_eff && gamma_h3 && (out || out_h3 || out_x6) &&
                      B > 0 && h > 0 && w > 0,
                  ICLR17_EINVAL, "deconv_igdn_h3: bad arguments");
   HArgs a;
@@ -676,7 +701,8 @@ int iclr17_synthesis_deconv_igdn_h3(const uint16_t* in_h3, int B, int h, int w, 
   const size_t wsz = iclr17_h3k_weight_size(ICLR17_H3K_DECONV5, N);
   a.w = w_h3k; a.w_plane = (long)(wsz - 8) / 2;
   a.wscale = (const float*)(w_h3k + (wsz - 8));
-  a.bias = bias; a.beta = beta_eff; a.gamma6 = gamma_split;
+  a.bias = bias; a.beta = beta_eff; a.gamma_h3 = gamma_h3;
+  a.gamma_scale = (const float*)(gamma_h3 + 2L * N * N);
   a.out = out;
   a.out_h3 = out_h3; a.out_h3_plane = (long)B * 4 * h * w * N;
   a.out_x6 = out_x6; a.out_x6_plane = (long)B * 4 * h * w * N;

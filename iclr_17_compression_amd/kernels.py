@@ -589,16 +589,19 @@ def conv3_quant_rate_h3(hs: Tensor, wh: Tensor, rate_packed: Tensor,
     return y_hat, partial, y, y_hat_h3
 
 
-def deconv_igdn_h3(hs: Tensor, wh: Tensor, bias: Tensor, beta_eff: Tensor, g6: Tensor,
+def deconv_igdn_h3(hs: Tensor, wh: Tensor, bias: Tensor, beta_eff: Tensor, gh3: Tensor,
                    want_h3: bool = True, want_f32: bool = False, want_x6: bool = False,
                    chunk_major: bool = False, int_in: bool = False):
     """synthesis_17.py:15-22 in the h3 form (csrc/engine_h3.hip): h3 input [2,B,h,w,N] →
-    (h3 | None, fp32 | None, x6 split | None). wh: ``pack_h3k(ICLR17_H3K_DECONV5, …)``; g6: the
-    IGDN's split γ. ``int_in``: the input is ŷ (a workgroup whose window has a zero lo plane skips
-    the lo products; same result). ``chunk_major`` applies to the h3 and x6 outputs."""
+    (h3 | None, fp32 | None, x6 split | None). wh: ``pack_h3k(ICLR17_H3K_DECONV5, …)``; gh3: the
+    IGDN's γ in the h3 form (GDN.effective_params_h3). ``int_in``: the input is ŷ (a workgroup
+    whose window has a zero lo plane skips the lo products; same result). ``chunk_major`` applies
+    to the h3 and x6 outputs."""
     _check_h3(hs, "activation")
     _, B, hh, ww, N = hs.shape
     _check_channels(N)
+    if gh3.dtype != torch.int16 or gh3.numel() != query("iclr17_split_packed_h3_size", 1, N, N):
+        raise Iclr17Error("iclr17: deconv_igdn_h3 needs the IGDN's h3 γ (split_packed_h3, taps 1)")
     if not (want_h3 or want_f32 or want_x6):
         raise Iclr17Error("iclr17: deconv_igdn_h3 needs an output")
     if wh.numel() != query("iclr17_h3k_weight_size", _lib.ICLR17_H3K_DECONV5, N):
@@ -609,7 +612,7 @@ def deconv_igdn_h3(hs: Tensor, wh: Tensor, bias: Tensor, beta_eff: Tensor, g6: T
     x6 = torch.empty(shape(3), device=hs.device, dtype=torch.int16) if want_x6 else None
     out = torch.empty(B, 2 * hh, 2 * ww, N, device=hs.device) if want_f32 else None
     call("iclr17_synthesis_deconv_igdn_h3", _p(hs), B, hh, ww, N, _p(wh), _p(bias),
-         _p(beta_eff), _p(g6), _p(out), _p(h3), _p(x6), int(chunk_major), int(int_in),
+         _p(beta_eff), _p(gh3), _p(out), _p(h3), _p(x6), int(chunk_major), int(int_in),
          _p(h3_range_flag(hs.device)), _stream(hs))
     return h3, out, x6
 

@@ -278,6 +278,8 @@ class ImageCompressor(nn.Module):
                 if not backward and kernels.precision() == "h3":
                     self.Decoder.packed_h3k()
                     self.Encoder.packed_h3()
+                    for g in gdns[2:]:
+                        g.effective_params_h3()
                 for g in gdns:
                     g.effective_params_x6()
             if backward:

@@ -80,6 +80,15 @@ class GDN(nn.Module):
                             lambda: kernels.split_packed(gp, 1, C, C), force=force)
         return be, gp, g6
 
+    def effective_params_h3(self, force: bool = False):
+        """(beta_eff, γ_eff in the h3 form: two fp16 planes + trailer, kernels.split_packed_h3 of
+        the [C/4][C][4] packing) for the h3 inference kernels."""
+        be, gp = self.effective_params(force)
+        C = self.beta.shape[0]
+        gh = self._pack.get("gdnh3", (self.beta, self.gamma),
+                            lambda: kernels.split_packed_h3(gp, 1, C, C), force=force)
+        return be, gh
+
     def effective_params_bf16(self, force: bool = False):
         """(beta_eff, γ_eff rounded to bf16 in the 16x16x32 fragment layout) for the bf16
         throughput kernels."""

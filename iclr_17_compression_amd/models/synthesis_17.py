@@ -121,13 +121,12 @@ class Synthesis_net_17(nn.Module):
             return kernels.deconv3_bf16(h, b3, self.deconv3.bias, x_ref=x_ref, want_recon=want_recon,
                                         bits=bits)
         if y_h3 is not None:
-            q1, q2 = self.igdn1.effective_params_x6(), self.igdn2.effective_params_x6()
+            q1, q2 = self.igdn1.effective_params_h3(), self.igdn2.effective_params_h3()
             w1, w2, w3 = self.packed_h3k()
             # on ŷ the integer-input form skips the lo products (the same bits: Decoder(round(y))
             # reproduces the codec's reconstruction without knowing its input is ŷ)
-            hs, _, _ = kernels.deconv_igdn_h3(y_h3, w1, self.deconv1.bias, q1[0], q1[2],
-                                              int_in=y_integral)
-            hs, _, _ = kernels.deconv_igdn_h3(hs, w2, self.deconv2.bias, q2[0], q2[2], chunk_major=True)
+            hs, _, _ = kernels.deconv_igdn_h3(y_h3, w1, self.deconv1.bias, *q1, int_in=y_integral)
+            hs, _, _ = kernels.deconv_igdn_h3(hs, w2, self.deconv2.bias, *q2, chunk_major=True)
             return kernels.deconv3_h3(hs, w3, self.deconv3.bias, x_ref=x_ref, want_recon=want_recon,
                                       bits=bits)
         if y_split is not None:

@@ -644,7 +644,8 @@ def test_h3_deconv_igdn(device, N, hw):
     that are and are not whole 16×16 tiles: the fp32 output at the fp32 bar and as close to the
     x6 engine as two exact-f32 summation orders; its h3 and x6 outputs encode exactly that fp32
     output, in NHWC and chunk-major form; on ŷ the int_in form (hi plane only, two products) is
-    bit-identical to the full form, also with a latent beyond fp16's 11 bits."""
+    bit-identical to the full form, also with a latent beyond fp16's 11 bits. The IGDN
+    contraction runs in the h3 form too (per-pixel power-of-two scale of x²)."""
     net, sd = net_for(N, 1, device), sd_for(N, 1)
     dec = net.Decoder
     F = torch.nn.functional
@@ -652,16 +653,17 @@ def test_h3_deconv_igdn(device, N, hw):
     x1, x2 = dec.packed_h3k()[:2]
     d1, d2 = dec.packed()[:2]
     q1, q2 = dec.igdn1.effective_params_x6(), dec.igdn2.effective_params_x6()
+    h1, h2 = dec.igdn1.effective_params_h3(), dec.igdn2.effective_params_h3()
     yq = torch.round(torch.from_numpy(synth.uniform(5, (2, N, h, w), -6, 6)))
     act = torch.from_numpy(synth.normal_like(6, (2, N, h, w), 0.7))
     flag = kernels.h3_range_flag(device)
     flag.zero_()
     with torch.no_grad():
-        for inp, lay, wx, wp, q, key in ((yq, "deconv1", x1, d1, q1, "igdn1"),
-                                         (act, "deconv2", x2, d2, q2, "igdn2")):
+        for inp, lay, wx, wp, q, qh, key in ((yq, "deconv1", x1, d1, q1, h1, "igdn1"),
+                                             (act, "deconv2", x2, d2, q2, h2, "igdn2")):
             inh = kernels.h3_planes(nhwc(inp).contiguous().to(device))
             bias = getattr(dec, lay).bias
-            s, f, s6 = kernels.deconv_igdn_h3(inh, wx, bias, q[0], q[2], want_f32=True, want_x6=True)
+            s, f, s6 = kernels.deconv_igdn_h3(inh, wx, bias, *qh, want_f32=True, want_x6=True)
             r_v = F.conv_transpose2d(inp, sd[f"Decoder.{lay}.weight"], sd[f"Decoder.{lay}.bias"],
                                      stride=2, padding=2, output_padding=1)
             r_s = oracle.gdn(r_v, sd[f"Decoder.{key}.beta"], sd[f"Decoder.{key}.gamma"], True)
@@ -669,7 +671,7 @@ def test_h3_deconv_igdn(device, N, hw):
             assert rel_err(f, nhwc(r_s)) < REL, lay
             assert torch.equal(kernels.merge_planes(s6), f)
             assert torch.equal(s, kernels.h3_planes(f))
-            scm, _, s6cm = kernels.deconv_igdn_h3(inh, wx, bias, q[0], q[2], want_x6=True,
+            scm, _, s6cm = kernels.deconv_igdn_h3(inh, wx, bias, *qh, want_x6=True,
                                                   chunk_major=True)
             assert scm.shape == (2, 2, N // 32, 2 * h, 2 * w, 32)
             assert torch.equal(scm.permute(0, 1, 3, 4, 2, 5).reshape(s.shape), s)
@@ -678,15 +680,15 @@ def test_h3_deconv_igdn(device, N, hw):
                                                  wp, bias, *q, want_f32=True)
             assert rel_err(f, f_old) < 2e-6, lay
             if lay == "deconv1":
-                si, fi, _ = kernels.deconv_igdn_h3(inh, wx, bias, q[0], q[2], want_f32=True, int_in=True)
+                si, fi, _ = kernels.deconv_igdn_h3(inh, wx, bias, *qh, want_f32=True, int_in=True)
                 assert torch.equal(fi, f) and torch.equal(si, s)
                 # a latent beyond fp16's 11 significant bits (3001): the workgroups that see it
                 # run the three-product form, and the result still equals the full form's
                 big = inp.clone()
                 big[1, 7, h // 2, w // 2] = 3001.0
                 bs = kernels.h3_planes(nhwc(big).contiguous().to(device))
-                _, fb, _ = kernels.deconv_igdn_h3(bs, wx, bias, q[0], q[2], want_h3=False, want_f32=True)
-                _, fbi, _ = kernels.deconv_igdn_h3(bs, wx, bias, q[0], q[2], want_h3=False, want_f32=True,
+                _, fb, _ = kernels.deconv_igdn_h3(bs, wx, bias, *qh, want_h3=False, want_f32=True)
+                _, fbi, _ = kernels.deconv_igdn_h3(bs, wx, bias, *qh, want_h3=False, want_f32=True,
                                                    int_in=True)
                 assert torch.equal(fbi, fb) and not torch.equal(fb, f)
     assert int(flag.item()) == 0

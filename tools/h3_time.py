@@ -20,18 +20,19 @@ dec = net.Decoder
 d1, d2 = dec.packed()[:2]
 x1, x2 = dec.packed_h3k()[:2]
 q1, q2 = dec.igdn1.effective_params_x6(), dec.igdn2.effective_params_x6()
+h1, h2 = dec.igdn1.effective_params_h3(), dec.igdn2.effective_params_h3()
 act = torch.from_numpy(synth.normal_like(6, (B, 32, 32, N), 0.7)).to(dev)
 yq = torch.round(torch.from_numpy(synth.uniform(5, (B, 16, 16, N), -6, 6))).to(dev)
 hs, ys = kernels.split_planes(act), kernels.split_planes(yq)
 hh, yh = kernels.h3_planes(act), kernels.h3_planes(yq)
 runs = {
     "deconv2_old": lambda: kernels.deconv_igdn_x6(hs, d2, dec.deconv2.bias, *q2, chunk_major=True),
-    "deconv2_h3": lambda: kernels.deconv_igdn_h3(hh, x2, dec.deconv2.bias, q2[0], q2[2], want_h3=False,
+    "deconv2_h3": lambda: kernels.deconv_igdn_h3(hh, x2, dec.deconv2.bias, *h2, want_h3=False,
                                                  want_x6=True, chunk_major=True),
-    "deconv2_h3_h3out": lambda: kernels.deconv_igdn_h3(hh, x2, dec.deconv2.bias, q2[0], q2[2], chunk_major=True),
+    "deconv2_h3_h3out": lambda: kernels.deconv_igdn_h3(hh, x2, dec.deconv2.bias, *h2, chunk_major=True),
     "deconv1_old": lambda: kernels.deconv_igdn_x6(ys, d1, dec.deconv1.bias, *q1),
-    "deconv1_h3": lambda: kernels.deconv_igdn_h3(yh, x1, dec.deconv1.bias, q1[0], q1[2]),
-    "deconv1_h3_int": lambda: kernels.deconv_igdn_h3(yh, x1, dec.deconv1.bias, q1[0], q1[2], int_in=True),
+    "deconv1_h3": lambda: kernels.deconv_igdn_h3(yh, x1, dec.deconv1.bias, *h1),
+    "deconv1_h3_int": lambda: kernels.deconv_igdn_h3(yh, x1, dec.deconv1.bias, *h1, int_in=True),
 }
 sel = os.environ.get("ONLY", "").split(",") if os.environ.get("ONLY") else list(runs)
 with torch.no_grad():

@@ -37,14 +37,15 @@ X6_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6   # fp32-equivalent: 6 bf16 part prod
 X6_LAYERS = ("conv1_gdn1", "conv2_gdn2", "conv3_quant_rate", "deconv1_igdn1", "deconv2_igdn2",
              "deconv3_clamp")   # every contraction of the x6 eval chain
 H3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3   # fp32-equivalent: 3 fp16 part products per MAC
-# the layers of the h3 eval chain whose main contraction runs in the h3 form (the others in x6)
-H3_LAYERS = ("conv2_gdn2", "conv3_quant_rate", "deconv1_igdn1", "deconv2_igdn2", "deconv3_clamp")
+# the layers of the h3 eval chain whose contractions run in the h3 form (all of them)
+H3_LAYERS = ("conv1_gdn1", "conv2_gdn2", "conv3_quant_rate", "deconv1_igdn1", "deconv2_igdn2",
+             "deconv3_clamp")
 
 
 PRECISION_NOTE = {
     "h3": ("h3: fp32 operands as two fp16 parts (22 significant bits, power-of-two scaled), 3 part "
-           "products per MAC on v_mfma_f32_*_f16 with fp32 accumulate for conv2, conv3, deconv1, "
-           "deconv2 and deconv3; x6 for conv1 and the GDN contractions"),
+           "products per MAC on v_mfma_f32_*_f16 with fp32 accumulate for every convolution and "
+           "GDN contraction"),
     "x6": ("x6: fp32 operands split exactly into 3 bf16 parts, 6 part products on "
            "v_mfma_f32_16x16x32_bf16, fp32 accumulate (every contraction)"),
     "bf16": "bf16: bf16 activations and weights, one bf16 product per MAC, fp32 accumulate and epilogues",
@@ -113,6 +114,8 @@ class Step:
         self.d3x6 = net.Decoder.packed_x6()
         self.dh3 = net.Decoder.packed_h3k()
         self.eh3 = net.Encoder.packed_h3()
+        self.w1h3 = net.Encoder.packed_conv1_h3()
+        self.eg3 = [net.Encoder.gdn1.effective_params_h3(), net.Encoder.gdn2.effective_params_h3()]
         self.gh3 = [net.Decoder.igdn1.effective_params_h3(), net.Decoder.igdn2.effective_params_h3()]
         self.rate = net.bitEstimator.packed()
         gdns = (net.Encoder.gdn1, net.Encoder.gdn2, net.Decoder.igdn1, net.Decoder.igdn2)
@@ -158,14 +161,14 @@ class Step:
             clipped, _, _, bpp = kernels.deconv3_bf16(h, d3b, net.Decoder.deconv3.bias,
                                                       bits=(partial, self.scale))
         elif kernels.precision() == "h3":
-            # ImageCompressor.forward in the h3 form: conv1 (x6 contractions, h3 output), conv2 /
-            # conv3 / deconv1 / deconv2 / deconv3 on three fp16 part products per MAC
-            e1, e2, e3, e4 = self.g6
+            # ImageCompressor.forward in the h3 form: every layer (and GDN contraction) on three
+            # fp16 part products per MAC
+            e1, e2 = self.eg3
             (w2h, w3h), (x1, x2, x3) = self.eh3, self.dh3
-            hs, _ = kernels.conv1x6_gdn_h3(self.x, self.w1x6, net.Encoder.conv1.bias, e1[0], e1[2], N)
+            hs, _ = kernels.conv1_gdn_h3(self.x, self.w1h3, net.Encoder.conv1.bias, *e1, N)
             ev(1)
             yield
-            hs, _, _ = kernels.conv2_gdn_h3(hs, w2h, net.Encoder.conv2.bias, e2[0], e2[2])
+            hs, _, _ = kernels.conv2_gdn_h3(hs, w2h, net.Encoder.conv2.bias, *e2)
             ev(2)
             yield
             y_hat, partial, _, yh = kernels.conv3_quant_rate_h3(hs, w3h, self.rate, rtab=self.rtab)

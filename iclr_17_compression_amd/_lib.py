@@ -131,7 +131,7 @@ SIGNATURES = {
     "iclr17_h3_planes": (_I, [_P, ctypes.c_long, _P, _P, _P]),
     "iclr17_split_packed_h3_size": (_SZ, [_I, _I, _I]),
     "iclr17_split_packed_h3": (_I, [_P, _I, _I, _I, _P, _P]),
-    "iclr17_analysis_conv1x6_gdn_h3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_analysis_conv1_gdn_h3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_analysis_conv2_gdn_h3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_analysis_conv3_quant_rate_h3": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P,
                                                  _P, _P, _P, _P]),

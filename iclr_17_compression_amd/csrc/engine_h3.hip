@@ -76,12 +76,43 @@ struct HArgs {
   int tiles_x, tiles_y;
 };
 
+// conv2 (k5 s2 p2) in this engine: 8-channel chunks and two taps per 16-deep step — lane half h of
+// a fragment holds tap 2s + h — so that a chunk's 35×35-pixel patch (both h3 planes) stays at
+// 45 KB and double-buffers beside the weight ring (16-channel chunks would need 157 KB).
+constexpr int HM_CONV8 = 2;
+constexpr int kConv8Steps = 13;   // tap pairs (25 taps + one zero-weight pad)
+
+// Patch of HM_CONV8: per row [column parity 2][20 slots] × 16 bytes (8 channels) — 640-byte rows,
+// so the two rows of a 32-pixel fragment half are 1280 bytes (a multiple of 256) apart and its
+// ds_read_b128 lane groups hit 16 distinct 16-byte slots
+template <int TH>
+struct PatchC8 {
+  static constexpr int ROWS = 2 * TH + 3;
+  static constexpr int ROWB = 640;
+  static constexpr int BYTES = ROWS * ROWB;
+  __host__ __device__ static constexpr int off(int pr, int pc) {
+    return pr * ROWB + (pc & 1) * 320 + (pc >> 1) * 16;
+  }
+  __host__ __device__ static constexpr int tap8(int t) {   // tap t = 5·ky + kx; 25 = the pad
+    return t < 25 ? off(t / 5, t % 5) : 0;
+  }
+};
+template <int MODE, int TH>
+struct HPatch {
+  using type = Patch<MODE, TH>;
+};
+template <int TH>
+struct HPatch<HM_CONV8, TH> {
+  using type = PatchC8<TH>;
+};
+
 template <int MODE, int TH, int CO, int CI, bool INT_IN>
 struct HK {
   static constexpr int NW = TH / 2, NTHR = NW * 64;
   static constexpr int NT = CO / 32;           // 32-channel accumulator tiles per wave
-  static constexpr int NCH = CI / 16;          // 16-channel chunks
-  using P = Patch<MODE, TH>;
+  static constexpr int CCH = MODE == HM_CONV8 ? 8 : 16;   // channels per chunk
+  static constexpr int NCH = CI / CCH;         // chunks
+  using P = typename HPatch<MODE, TH>::type;
   static constexpr int PL = INT_IN ? 1 : 2;    // input planes staged
   static constexpr int PB = PL * P::BYTES;     // patch bytes (planes back to back)
   static constexpr int NQI = (PB + 1023) / 1024;
@@ -97,7 +128,7 @@ struct HK {
   static constexpr int BBOFF = (LDS0 + 1023) / 1024 * 1024;
   static constexpr int LDS = BBOFF + 2048;     // + bias, β_eff
   static_assert(SB % 1024 == 0, "weight stage");
-  static_assert(NT % 2 == 0 && CI % 16 == 0, "tile shape");
+  static_assert(NT % 2 == 0 && CI % CCH == 0, "tile shape");
   static_assert(LDS <= 160 * 1024, "LDS");
 };
 
@@ -105,8 +136,10 @@ template <int MODE, int TH, int CO, int CI, int EPI, bool INT_IN, int PH>
 __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, int b, int ty, int tx) {
   using KK = HK<MODE, TH, CO, CI, INT_IN>;
   using P = typename KK::P;
-  using TP = Taps<MODE, PH>;
-  constexpr int NT = KK::NT, NW = KK::NW, NCH = KK::NCH, S = TP::T;   // one tap per step
+  constexpr bool CONV = MODE != BM_DECONV, C8 = MODE == HM_CONV8;
+  using TP = Taps<CONV ? BM_CONV : BM_DECONV, PH>;
+  // one tap per step (HM_CONV8: a tap pair)
+  constexpr int NT = KK::NT, NW = KK::NW, NCH = KK::NCH, S = C8 ? kConv8Steps : TP::T;
   constexpr int SB = KK::SB, NBI = KK::NBI, NST = KK::NST;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -126,17 +159,21 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
   unsigned char* const sD = sB + NST * SB;
   float* const sbb = (float*)(smem + KK::BBOFF);   // [bias | pad][β_eff | pad]
   const long img = (long)b * a.Hin * a.Win;
-  const int iy0 = MODE == BM_CONV ? 2 * ty * TH - 2 : ty * TH - 1;
-  const int ix0 = MODE == BM_CONV ? 2 * tx * 16 - 2 : tx * 16 - 1;
+  const int iy0 = CONV ? 2 * ty * TH - 2 : ty * TH - 1;
+  const int ix0 = CONV ? 2 * tx * 16 - 2 : tx * 16 - 1;
   const u16* __restrict__ inb = a.in + img * CI;
   // patch piece `piece` (1 KB): this lane's 16-byte slot → source u16 offset, or -1 (zeros)
   auto piece_src = [&](int piece) -> long {
     const int byte = (piece * 64 + lane) * 16;
     const int pl = byte / P::BYTES, rem = byte - pl * P::BYTES;
     const int pr = rem / P::ROWB, r1 = rem - pr * P::ROWB;
-    int pc, hh;
+    int pc, hh = 0;
     bool ok;
-    if (MODE == BM_CONV) {
+    if constexpr (C8) {
+      const int par = r1 / 320, slot = (r1 - par * 320) / 16;
+      pc = 2 * slot + par;
+      ok = slot < 18 && pc < 35;
+    } else if (MODE == BM_CONV) {
       const int par = r1 / (2 * P::HALF), r2 = r1 - par * 2 * P::HALF;
       hh = r2 / P::HALF;
       pc = 2 * ((r2 - hh * P::HALF) / 16) + par;
@@ -156,7 +193,7 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
       return;
     }
     const long src = piece_src(piece);
-    glds16(src >= 0 ? (const void*)(inb + src + c1 * 16) : (const void*)g_zero16h,
+    glds16(src >= 0 ? (const void*)(inb + src + c1 * KK::CCH) : (const void*)g_zero16h,
            sP + (c1 & 1) * KK::PBUF + piece * 1024);
   };
   // weights of this phase: per plane [NCH][S][2][CO][8]; the step's stage [plane][2][CO][8]
@@ -191,7 +228,14 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
   // B (pixels): pixel (tile row 2·wave + (r32 >> 4), column r32 & 15), channel half h
   const int prow = 2 * wave + (r32 >> 4), pcol = r32 & 15;
   const int tpix = prow * 16 + pcol;
-  const int pbase = (MODE == BM_CONV ? P::off(2 * prow, 2 * pcol) : P::off(prow, pcol)) + h * P::HALF;
+  int pbase;
+  if constexpr (C8) pbase = P::off(2 * prow, 2 * pcol);
+  else pbase = (MODE == BM_CONV ? P::off(2 * prow, 2 * pcol) : P::off(prow, pcol)) + h * P::HALF;
+  // the step's tap offset: one tap for every lane, or (HM_CONV8) tap 2s + h for lane half h
+  auto tap_of = [&](int s) -> int {
+    if constexpr (C8) return h ? P::tap8(2 * s + 1) : P::tap8(2 * s);
+    else return P::template tap_off<PH>(s);
+  };
   // A (weights): stage [plane][2][CO][8]: lane (k-group h, channel 32·i + r32)
   const int abase = (h * CO + r32) * 16;
   constexpr int APL = 2 * CO * 16;   // stage bytes per plane
@@ -254,19 +298,19 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
       f.wl[i] = *(lu4p)(wb + APL + i * 512);
     }
   };
-  wait_vm_barrier<F * K>();   // step 0's weights and chunk 0's patch landed
   Frag cur;
-  read_frag(cur, sP + pbase, P::template tap_off<PH>(0), sB + abase);
   int stage = 1;   // stage of step g+1
   for (int c = 0; c < NCH; ++c) {
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       const int g = c * S + s;
-      wait_vm_barrier<(F - 1) * K>();   // step g+1's weights (and patch) landed;
+      wait_vm_barrier<(F - 1) * K>();   // step g+1's weights (and patch) landed (at g = 0 the
+                                        // prologue's padding tail is all that may be in flight);
                                         // stage (g+F+1) % NST is free
+      if (s == 0 && c == 0) read_frag(cur, sP + pbase, tap_of(0), sB + abase);
       Frag nxt;
       read_frag(nxt, sP + ((s + 1 < S ? c : c + 1) & 1) * KK::PBUF + pbase,
-                P::template tap_off<PH>(s + 1 < S ? s + 1 : 0), sB + stage * SB + abase);
+                tap_of(s + 1 < S ? s + 1 : 0), sB + stage * SB + abase);
       stage = stage + 1 == NST ? 0 : stage + 1;
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
@@ -285,18 +329,24 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
   }
   vm_barrier();   // trailing sink loads landed; every wave is done with the stages
 
-  // ---- epilogue. acc[i][4m + j]: channel 32i + 8m + 4h + j of tile pixel tpix
-  const int gy = ty * TH + (tpix >> 4), gx = tx * 16 + (tpix & 15);
+  // ---- epilogue. acc[i][4m + j]: channel 32i + 8m + 4h + j of tile pixel tpix. The lane
+  // indices are re-derived from a fresh threadIdx.x: the main loop's copies otherwise stay live
+  // through it, and the INT_OK kernel spilled them (a scratch op would break the counted vmcnt
+  // groups that tools/dma_sync_check.py proves)
+  const int etid = fresh_tid(), elane = etid & 63, er32 = elane & 31, eh = elane >> 5;
+  const int ewave = __builtin_amdgcn_readfirstlane(etid >> 6);
+  const int etpix = (2 * ewave + (er32 >> 4)) * 16 + (er32 & 15);
+  const int gy = ty * TH + (etpix >> 4), gx = tx * 16 + (etpix & 15);
   const bool inside = gy < a.gh && gx < a.gw;
-  const int oy = MODE == BM_CONV ? gy : 2 * gy + (PH >> 1);
-  const int ox = MODE == BM_CONV ? gx : 2 * gx + (PH & 1);
+  const int oy = CONV ? gy : 2 * gy + (PH >> 1);
+  const int ox = CONV ? gx : 2 * gx + (PH & 1);
   const long o = ((long)b * a.Hout + oy) * a.Wout + ox;
   const float dsc = a.wscale[1];   // 2⁻¹¹/(σ_a·σ_w): exact
 #pragma unroll
   for (int i = 0; i < NT; ++i)
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
-      const f4 bv = *(const f4*)(sbb + 32 * i + 8 * m + 4 * h);
+      const f4 bv = *(const f4*)(sbb + 32 * i + 8 * m + 4 * eh);
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][4 * m + j] = acc[i][4 * m + j] * dsc + bv[j];   // x = conv + bias
     }
@@ -304,9 +354,9 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
   bool ovf = false;
   // The channel contraction n_i = Σ_j γ_ij·x_j² in the h3 form. x² of a pixel (rounded to fp32,
   // as conv2d(x², γ) sees it) is scaled by a power of two s_p that puts the pixel's largest x²
-  // in [2¹³, 2¹⁴) — the pixel is this lane's MFMA column, so the scale is undone per lane — and
+  // in [2¹³, 2¹⁴) — the pixel is this elane's MFMA column, so the scale is undone per elane — and
   // split into hi / lo fp16 planes; γ arrives split with its own per-tensor power of two. The
-  // pixel's 192 channels sit in this lane (96) and lane r32 + 32·(1 − h) (the other 96).
+  // pixel's 192 channels sit in this elane (96) and elane er32 + 32·(1 − eh) (the other 96).
   float mx = 0.f;
 #pragma unroll
   for (int i = 0; i < NT; ++i)
@@ -327,19 +377,19 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
   const float nsc = ldexpf(a.gamma_scale[1] * kH3Sa, -ep);
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf) {
-    if (hf) __syncthreads();   // every wave's pass-0 γ reads done before the restage
+    if (hf) __syncthreads();   // every ewave's pass-0 γ reads done before the restage
     // opaque to the optimiser: pass 1 recomputes the x² planes instead of keeping pass 0's
     // (12 k-blocks × 2 planes × 4 registers) alive across the passes
 #pragma unroll
     for (int i = 0; i < NT; ++i)
 #pragma unroll
       for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(acc[i][j]));
-    // γ rows 32·(hf·NTH + il) .. of the two planes: block (plane, il, kb), lane (r32, h) ←
-    // γ_p[32(hf·NTH + il) + r32][16kb + 8h .. +7] (the [CO/8][CO][8] packing)
-    for (int blk = wave; blk < KK::GBL; blk += NW) {
+    // γ rows 32·(hf·NTH + il) .. of the two planes: block (plane, il, kb), elane (er32, eh) ←
+    // γ_p[32(hf·NTH + il) + er32][16kb + 8h .. +7] (the [CO/8][CO][8] packing)
+    for (int blk = ewave; blk < KK::GBL; blk += NW) {
       const int p = blk / (NTH * KB), rem = blk - p * NTH * KB;
       const int il = rem / KB, kb = rem - il * KB;
-      glds16(a.gamma_h3 + (long)p * CO * CO + ((2 * kb + h) * CO + 32 * (hf * NTH + il) + r32) * 8,
+      glds16(a.gamma_h3 + (long)p * CO * CO + ((2 * kb + eh) * CO + 32 * (hf * NTH + il) + er32) * 8,
              smem + blk * 1024);
     }
     vm_barrier();
@@ -348,14 +398,14 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
     for (int il = 0; il < NTH; ++il)
 #pragma unroll
       for (int j = 0; j < 16; ++j) n[il][j] = 0.f;
-    const unsigned char* sg = smem + lane * 16;
+    const unsigned char* sg = smem + elane * 16;
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) {
-      // x²·s_p of channels 16kb .. 16kb + 15 as the hi / lo B planes: the accumulator rows a lane
+      // x²·s_p of channels 16kb .. 16kb + 15 as the hi / lo B planes: the accumulator rows a elane
       // holds are 4h + 0..3 and 8 + 4h + 0..3 of the 16-channel block; one permlane32 swap per
-      // register pair and plane hands lanes h the 8 consecutive channels 8h .. 8h + 7
+      // register pair and plane hands lanes eh the 8 consecutive channels 8h .. 8h + 7
       const int i = kb >> 1, r0 = 8 * (kb & 1);
-      unsigned hv[4], lv[4];   // channel pairs (2q, 2q + 1) of the lane's 8, packed fp16
+      unsigned hv[4], lv[4];   // channel pairs (2q, 2q + 1) of the elane's 8, packed fp16
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         typedef float f2 __attribute__((ext_vector_type(2)));
@@ -395,7 +445,7 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
       const int i = hf * NTH + il;
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
-        const int ch = 32 * i + 8 * m + 4 * h;
+        const int ch = 32 * i + 8 * m + 4 * eh;
         const f4 be = *(const f4*)(sbb + 256 + ch);
         f4 y;
 #pragma unroll
@@ -409,7 +459,7 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
         if (a.out_h3) {
           uint2 hb, lb;
           h3_split4(y, hb, lb, ovf);
-          const long so = a.out_cm ? (((long)b * (CO / 32) + i) * a.Hout + oy) * a.Wout * 32 + (long)ox * 32 + 8 * m + 4 * h
+          const long so = a.out_cm ? (((long)b * (CO / 32) + i) * a.Hout + oy) * a.Wout * 32 + (long)ox * 32 + 8 * m + 4 * eh
                                    : o * CO + ch;
           *(uint2*)(a.out_h3 + so) = hb;
           *(uint2*)(a.out_h3 + a.out_h3_plane + so) = lb;
@@ -423,7 +473,7 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
             mb[j] = __float_as_uint(r) & 0xffff0000u;
             lb[j] = __float_as_uint(r - __uint_as_float(mb[j]));
           }
-          const long so = a.out_cm ? (((long)b * (CO / 32) + i) * a.Hout + oy) * a.Wout * 32 + (long)ox * 32 + 8 * m + 4 * h
+          const long so = a.out_cm ? (((long)b * (CO / 32) + i) * a.Hout + oy) * a.Wout * 32 + (long)ox * 32 + 8 * m + 4 * eh
                                    : o * CO + ch;
           *(uint2*)(a.out_x6 + so) = uint2{__builtin_amdgcn_perm(hb[1], hb[0], 0x07060302u),
                                            __builtin_amdgcn_perm(hb[3], hb[2], 0x07060302u)};
@@ -456,6 +506,7 @@ __global__ void __launch_bounds__(TH / 2 * 64, 1) h3k_kernel(const HArgs a) {
   const int b = bid / a.tiles_y;
   bool small = false;
   if constexpr (INT_OK) {
+    static_assert(MODE == BM_DECONV, "INT_OK: deconv1");
     // the lo plane of the window the patch stages, all CI channels, 8 values per 16-byte load
     using P = Patch<MODE, TH>;
     constexpr int COLS = MODE == BM_CONV ? 35 : 18, PER = COLS * CI / 8;
@@ -482,7 +533,7 @@ __global__ void __launch_bounds__(TH / 2 * 64, 1) h3k_kernel(const HArgs a) {
   }
   auto run = [&](auto int_in) {
     constexpr bool II = decltype(int_in)::value;
-    if constexpr (MODE == BM_CONV) {
+    if constexpr (MODE != BM_DECONV) {
       h3k_body<MODE, TH, CO, CI, EPI, II, 0>(a, smem, b, ty, tx);
     } else {
       switch (ph) {   // wave-uniform: the tap lists are compile-time per phase
@@ -524,10 +575,12 @@ __device__ __forceinline__ int h3_weight_exp(float mx) {
   return 3 - (e - 1);
 }
 
-// W → two planes, per plane [blocks][2][CO][8] fp16 where a block is one (chunk, tap):
-// conv (W[co][ci][5][5]): block c·25 + t, tap t = 5·ky + kx;
-// deconv (W[ci][co][5][5]): the four stride phases back to back, phase p's blocks c·T_p + t with
-// the tap order of Taps<BM_DECONV, p>. Element (block, h, co, j) = W at input channel 16c + 8h + j.
+// W → two planes, per plane [blocks][2][CO][8] fp16:
+// conv (W[co][ci][5][5], HM_CONV8): block c·13 + p over 8-channel chunks c and tap pairs p;
+// element (block, h, co, j) = W[co][8c + j] at tap t = 2p + h = 5·ky + kx (zero for t = 25);
+// deconv (W[ci][co][5][5]): the four stride phases back to back, phase p's blocks c·T_p + t over
+// 16-channel chunks c with the tap order of Taps<BM_DECONV, p>; element (block, h, co, j) = W at
+// input channel 16c + 8h + j.
 __global__ void __launch_bounds__(256) pack_h3k_kernel(const float* __restrict__ w, int N, int deconv,
                                                        long groups, u16* __restrict__ out,
                                                        float* __restrict__ trailer) {
@@ -540,12 +593,15 @@ __global__ void __launch_bounds__(256) pack_h3k_kernel(const float* __restrict__
     long r = g / N;
     const int h = (int)(r % 2);
     int u = (int)(r / 2);   // block index
-    int c, ky, kx;
+    int c, ky, kx, ci0;
+    bool zero = false;
     if (!deconv) {
-      c = u / 25;
-      const int t = u - c * 25;
-      ky = t / 5;
-      kx = t % 5;
+      c = u / kConv8Steps;
+      const int t = 2 * (u - c * kConv8Steps) + h;
+      zero = t >= 25;
+      ky = zero ? 0 : t / 5;
+      kx = zero ? 0 : t % 5;
+      ci0 = 8 * c;
     } else {
       int p = 0, T = 9;
       while (true) {
@@ -560,13 +616,15 @@ __global__ void __launch_bounds__(256) pack_h3k_kernel(const float* __restrict__
       const int t = u - c * T;
       ky = (p >> 1) == 0 ? 2 * (t / nx) : 2 * (t / nx) + 1;
       kx = (p & 1) == 0 ? 2 * (t % nx) : 2 * (t % nx) + 1;
+      ci0 = 16 * c + 8 * h;
     }
     unsigned short hv[8], lv[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int ci = 16 * c + 8 * h + j;
-      const float v = (deconv ? w[(((long)ci * N + co) * 5 + ky) * 5 + kx]
-                              : w[(((long)co * N + ci) * 5 + ky) * 5 + kx]) * sw;
+      const int ci = ci0 + j;
+      const float v = zero ? 0.f
+                           : (deconv ? w[(((long)ci * N + co) * 5 + ky) * 5 + kx]
+                                     : w[(((long)co * N + ci) * 5 + ky) * 5 + kx]) * sw;
       const _Float16 hh = (_Float16)v;
       hv[j] = h16_bits(hh);
       lv[j] = h16_bits((_Float16)((v - (float)hh) * 2048.0f));
@@ -653,8 +711,10 @@ extern "C" {
 size_t iclr17_h3k_weight_size(int which, int N) {
   if (N != 128 && N != 192) return 0;
   if (which != ICLR17_H3K_CONV5 && which != ICLR17_H3K_DECONV5) return 0;
-  // two planes of 25 (chunk, tap) blocks per 16-channel chunk, + the 16-byte trailer
-  return (size_t)2 * (N / 16) * 25 * 2 * N * 8 + 8;
+  // two planes of 25 (chunk, tap) blocks per 16-channel chunk (deconv) or 13 (chunk, tap pair)
+  // blocks per 8-channel chunk (conv), + the 16-byte trailer
+  return which == ICLR17_H3K_DECONV5 ? (size_t)2 * (N / 16) * 25 * 2 * N * 8 + 8
+                                     : (size_t)2 * (N / 8) * kConv8Steps * 2 * N * 8 + 8;
 }
 
 int iclr17_pack_h3k(int which, const float* w, uint16_t* out, int N, void* stream) {
@@ -702,6 +762,42 @@ int iclr17_h3_planes(const float* x, long n, uint16_t* planes, int* range_flag, 
   hipLaunchKernelGGL(h3_planes_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, n4, n,
                      planes, range_flag);
   return check_launch("h3_planes");
+}
+
+int iclr17_analysis_conv2_gdn_h3(const uint16_t* in_h3, int B, int H, int W, int N,
+                                 const uint16_t* w_h3k, const float* bias, const float* beta_eff,
+                                 const uint16_t* gamma_h3, float* out, uint16_t* out_h3,
+                                 uint16_t* out_x6, int* range_flag, void* stream) {
+  ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "conv2_gdn_h3: N=%d", N);
+  ICLR17_REQUIRE(in_h3 && w_h3k && bias && beta_eff && gamma_h3 && (out || out_h3 || out_x6) &&
+                     B > 0 && H > 0 && W > 0 && H % 16 == 0 && W % 16 == 0,
+                 ICLR17_EINVAL, "conv2_gdn_h3: bad arguments");
+  HArgs a;
+  memset(&a, 0, sizeof(a));
+  const int h = H / 4, w = W / 4;
+  a.in = in_h3; a.in_plane = (long)B * h * w * N;
+  const size_t wsz = iclr17_h3k_weight_size(ICLR17_H3K_CONV5, N);
+  a.w = w_h3k; a.w_plane = (long)(wsz - 8) / 2;
+  a.wscale = (const float*)(w_h3k + (wsz - 8));
+  a.bias = bias; a.beta = beta_eff; a.gamma_h3 = gamma_h3;
+  a.gamma_scale = (const float*)(gamma_h3 + 2L * N * N);
+  a.out = out;
+  a.out_h3 = out_h3; a.out_h3_plane = (long)B * (h / 2) * (w / 2) * N;
+  a.out_x6 = out_x6; a.out_x6_plane = a.out_h3_plane;
+  a.range = range_flag;
+  a.B = B; a.Hin = h; a.Win = w; a.Hout = h / 2; a.Wout = w / 2;
+  a.gh = h / 2; a.gw = w / 2;
+  constexpr int TH = 16;
+  a.tiles_y = (a.gh + TH - 1) / TH;
+  a.tiles_x = (a.gw + 15) / 16;
+  const dim3 grid(a.tiles_x * a.tiles_y * B);
+  if (N == 192)
+    hipLaunchKernelGGL((h3k_kernel<HM_CONV8, TH, 192, 192, HE_GDN, false>), grid, dim3(TH / 2 * 64), 0,
+                       (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL((h3k_kernel<HM_CONV8, TH, 128, 128, HE_GDN, false>), grid, dim3(TH / 2 * 64), 0,
+                       (hipStream_t)stream, a);
+  return check_launch("conv2_gdn_h3");
 }
 
 int iclr17_synthesis_deconv_igdn_h3(const uint16_t* in_h3, int B, int h, int w, int N,

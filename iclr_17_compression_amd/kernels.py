@@ -519,42 +519,55 @@ def split_packed_h3(packed: Tensor, taps: int, K: int, N: int) -> Tensor:
     return out
 
 
-def conv1x6_gdn_h3(x: Tensor, w_split: Tensor, bias: Tensor, beta_eff: Tensor, g6: Tensor, N: int,
-                   want_f32: bool = False):
-    """``conv1x6_gdn`` with the output in the h3 form: returns (h3 [2,B,H/4,W/4,N], fp32 | None)."""
+def pack_conv1_h3(w: Tensor, N: int) -> Tensor:
+    """conv1 weight [N,3,9,9] → the h3 planes conv1_gdn_h3 reads (split_packed_h3 of the
+    ICLR17_W_CONV1_X6 packing: two fp16 planes [2, 256·N] + trailer)."""
+    return split_packed_h3(pack_weight(_lib.ICLR17_W_CONV1_X6, w, N), 1, 256, N)
+
+
+def conv1_gdn_h3(x: Tensor, w_h3: Tensor, bias: Tensor, beta_eff: Tensor, gh3: Tensor, N: int,
+                 want_f32: bool = False):
+    """analysis_17.py:14-17 conv1 + GDN1 in the h3 form (three f16 part products per MAC for the
+    convolution and the GDN contraction; w_h3: ``pack_conv1_h3``, gh3: GDN.effective_params_h3's
+    γ). Returns (h3 [2,B,H/4,W/4,N], fp32 | None)."""
     _check(x, "image", 4)
     B, C, H, W = x.shape
     if C != 3:
         raise Iclr17Error(f"iclr17: the analysis transform takes 3-channel images (got {C})")
     _check_image_dims(H, W)
     _check_channels(N)
-    if w_split.dtype != torch.int16 or w_split.numel() != 3 * 256 * N:
-        raise Iclr17Error("iclr17: conv1x6_gdn_h3 needs the split ICLR17_W_CONV1_X6 packing")
+    if w_h3.dtype != torch.int16 or w_h3.numel() != query("iclr17_split_packed_h3_size", 1, 256, N):
+        raise Iclr17Error("iclr17: conv1_gdn_h3 needs pack_conv1_h3 weights")
+    if gh3.dtype != torch.int16 or gh3.numel() != query("iclr17_split_packed_h3_size", 1, N, N):
+        raise Iclr17Error("iclr17: conv1_gdn_h3 needs γ in the h3 form (effective_params_h3)")
     x = x.contiguous()
     h3 = torch.empty(2, B, H // 4, W // 4, N, device=x.device, dtype=torch.int16)
     out = torch.empty(B, H // 4, W // 4, N, device=x.device) if want_f32 else None
-    call("iclr17_analysis_conv1x6_gdn_h3", _p(x), B, H, W, N, _p(w_split), _p(bias), _p(beta_eff),
-         _p(g6), _p(out), _p(h3), _p(h3_range_flag(x.device)), _stream(x))
+    call("iclr17_analysis_conv1_gdn_h3", _p(x), B, H, W, N, _p(w_h3), _p(bias), _p(beta_eff),
+         _p(gh3), _p(out), _p(h3), _p(h3_range_flag(x.device)), _stream(x))
     return h3, out
 
 
-def conv2_gdn_h3(hs: Tensor, wh: Tensor, bias: Tensor, beta_eff: Tensor, g6: Tensor,
+def conv2_gdn_h3(hs: Tensor, wk: Tensor, bias: Tensor, beta_eff: Tensor, gh3: Tensor,
                  want_h3: bool = True, want_f32: bool = False, want_x6: bool = False):
-    """analysis_17.py:18-21 in the h3 form: h3 input [2,B,H/4,W/4,N] → (h3 | None, fp32 | None,
-    x6 split | None). wh: ``split_packed_h3(pack_weight(ICLR17_W_CONV5, w), 25, N, N)``."""
+    """analysis_17.py:18-21 conv2 + GDN2 in the h3 form on the h3 engine (csrc/engine_h3.hip):
+    h3 input [2,B,H/4,W/4,N] → (h3 | None, fp32 | None, x6 split | None). wk:
+    ``pack_h3k(ICLR17_H3K_CONV5, w)``; gh3: GDN.effective_params_h3's γ."""
     _check_h3(hs, "activation")
     _, B, h4, w4, N = hs.shape
     _check_channels(N)
     H, W = 4 * h4, 4 * w4
     _check_image_dims(H, W)
-    if wh.numel() != query("iclr17_split_packed_h3_size", 25, N, N):
-        raise Iclr17Error("iclr17: conv2_gdn_h3 needs split_packed_h3 of the conv5 packing")
+    if wk.numel() != query("iclr17_h3k_weight_size", _lib.ICLR17_H3K_CONV5, N):
+        raise Iclr17Error("iclr17: conv2_gdn_h3 needs pack_h3k(ICLR17_H3K_CONV5) weights")
+    if gh3.dtype != torch.int16 or gh3.numel() != query("iclr17_split_packed_h3_size", 1, N, N):
+        raise Iclr17Error("iclr17: conv2_gdn_h3 needs γ in the h3 form (effective_params_h3)")
     if not (want_h3 or want_f32 or want_x6):
         raise Iclr17Error("iclr17: conv2_gdn_h3 needs an output")
     h3 = torch.empty(2, B, h4 // 2, w4 // 2, N, device=hs.device, dtype=torch.int16) if want_h3 else None
     x6 = torch.empty(3, B, h4 // 2, w4 // 2, N, device=hs.device, dtype=torch.int16) if want_x6 else None
     out = torch.empty(B, h4 // 2, w4 // 2, N, device=hs.device) if want_f32 else None
-    call("iclr17_analysis_conv2_gdn_h3", _p(hs), B, H, W, N, _p(wh), _p(bias), _p(beta_eff), _p(g6),
+    call("iclr17_analysis_conv2_gdn_h3", _p(hs), B, H, W, N, _p(wk), _p(bias), _p(beta_eff), _p(gh3),
          _p(out), _p(h3), _p(x6), _p(h3_range_flag(hs.device)), _stream(hs))
     return h3, out, x6
 

@@ -100,14 +100,14 @@ class ImageCompressor(nn.Module):
                                                                 want_y=want_y)
             return {"y_hat": y_hat, "bits_partial": bits, "y_split": None, "y_bf16": ybf, "y": y}
         if kernels.precision() == "h3":
-            # the parity mode on the f16 MFMA: conv1 (x6 contractions) → conv2 and conv3 in the
-            # h3 form (three fp16 part products per MAC), ŷ handed to the decoder in the h3 form
-            e1 = self.Encoder.gdn1.effective_params_x6()
-            e2 = self.Encoder.gdn2.effective_params_x6()
+            # the parity mode on the f16 MFMA: conv1, conv2 and conv3 (and the GDN contractions)
+            # in the h3 form (three fp16 part products per MAC), ŷ handed on in the h3 form
+            e1 = self.Encoder.gdn1.effective_params_h3()
+            e2 = self.Encoder.gdn2.effective_params_h3()
             w2h, w3h = self.Encoder.packed_h3()
-            hs, _ = kernels.conv1x6_gdn_h3(x, self.Encoder.packed_conv1_x6(), self.Encoder.conv1.bias,
-                                           e1[0], e1[2], N)
-            hs, _, _ = kernels.conv2_gdn_h3(hs, w2h, self.Encoder.conv2.bias, e2[0], e2[2])
+            hs, _ = kernels.conv1_gdn_h3(x, self.Encoder.packed_conv1_h3(), self.Encoder.conv1.bias,
+                                         *e1, N)
+            hs, _, _ = kernels.conv2_gdn_h3(hs, w2h, self.Encoder.conv2.bias, *e2)
             rt = self.bitEstimator.rate_table() if noise is None else None
             q = kernels.conv3_quant_rate_h3(hs, w3h, self.bitEstimator.packed(), noise, want_y=want_y,
                                             rtab=rt)
@@ -278,7 +278,8 @@ class ImageCompressor(nn.Module):
                 if not backward and kernels.precision() == "h3":
                     self.Decoder.packed_h3k()
                     self.Encoder.packed_h3()
-                    for g in gdns[2:]:
+                    self.Encoder.packed_conv1_h3()
+                    for g in gdns:
                         g.effective_params_h3()
                 for g in gdns:
                     g.effective_params_x6()

@@ -57,15 +57,22 @@ class Analysis_net_17(nn.Module):
                               lambda: kernels.split_packed(w3, 25, N, N), force)
 
     def packed_h3(self, force: bool = False):
-        """conv2 / conv3 weights in the h3 engine's two fp16 planes (kernels.split_packed_h3 of the
-        conv5 packing, per-tensor power-of-two scale in the trailer), cached."""
+        """conv2 / conv3 weights in the h3 form, cached: conv2 in the h3 engine's packing
+        (kernels.pack_h3k, ICLR17_H3K_CONV5), conv3 in the engine's two fp16 planes
+        (kernels.split_packed_h3 of the conv5 packing); per-tensor power-of-two scales."""
         N = self.out_channel_N
-        _, w2, w3, _, _ = self.packed(force)
+        _, _, w3, _, _ = self.packed(force)
         w2h = self._pack.get("w2h3", (self.conv2.weight,),
-                             lambda: kernels.split_packed_h3(w2, 25, N, N), force)
+                             lambda: kernels.pack_h3k(_lib.ICLR17_H3K_CONV5, self.conv2.weight, N), force)
         w3h = self._pack.get("w3h3", (self.conv3.weight,),
                              lambda: kernels.split_packed_h3(w3, 25, N, N), force)
         return w2h, w3h
+
+    def packed_conv1_h3(self, force: bool = False):
+        """conv1's weights in the h3 form (kernels.pack_conv1_h3), cached."""
+        N = self.out_channel_N
+        return self._pack.get("w1h3", (self.conv1.weight,),
+                              lambda: kernels.pack_conv1_h3(self.conv1.weight, N), force)
 
     def packed_conv1_x6(self, force: bool = False):
         """conv1's weights in the x6 kernel's split layout (kernels.pack_conv1_x6), cached."""
@@ -141,10 +148,10 @@ class Analysis_net_17(nn.Module):
             h = kernels.conv2_gdn_bf16(h, w2b, self.conv2.bias, *e2)
             y = kernels.conv3_quant_rate_bf16(h, w3b, z, ztab, want_y=True)[2]
         elif kernels.precision() == "h3":
-            e1, e2 = self.gdn1.effective_params_x6(), self.gdn2.effective_params_x6()
+            e1, e2 = self.gdn1.effective_params_h3(), self.gdn2.effective_params_h3()
             w2h, w3h = self.packed_h3()
-            hs, _ = kernels.conv1x6_gdn_h3(x, self.packed_conv1_x6(), self.conv1.bias, e1[0], e1[2], N)
-            hs, _, _ = kernels.conv2_gdn_h3(hs, w2h, self.conv2.bias, e2[0], e2[2])
+            hs, _ = kernels.conv1_gdn_h3(x, self.packed_conv1_h3(), self.conv1.bias, *e1, N)
+            hs, _, _ = kernels.conv2_gdn_h3(hs, w2h, self.conv2.bias, *e2)
             y = kernels.conv3_quant_rate_h3(hs, w3h, z, want_y=True, rtab=ztab, want_h3=False)[2]
         elif kernels.precision() == "x6":
             e1, e2 = self.gdn1.effective_params_x6(), self.gdn2.effective_params_x6()

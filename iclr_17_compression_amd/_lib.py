@@ -35,6 +35,7 @@ ICLR17_BF_CONV5 = 32
 ICLR17_BF_DECONV5 = 33
 ICLR17_H3K_CONV5 = 42
 ICLR17_H3K_DECONV5 = 43
+ICLR17_H3K_CONV1 = 44
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int

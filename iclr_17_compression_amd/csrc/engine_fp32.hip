@@ -126,10 +126,6 @@ struct EngineArgs {
   unsigned short* out_h3;           // [2][B][Hout][Wout][CO] or nullptr
   long out_h3_plane;
   int* range;                       // h3 range flag (nullable)
-  // h3 GDN contraction (gdn_core mode 2): γ_eff in the h3 form (iclr17_split_packed_h3 with taps 1,
-  // [2][CO/8][CO][8] fp16) and its trailer ([1] = 2⁻¹¹/(σ_a·σ_γ))
-  const unsigned short* ggamma_h3;
-  const float* ggamma_scale;
 };
 
 // iclr17_reduce_partials inside the last kernel of the eval chain (deconv3): the per-image sums of
@@ -552,144 +548,24 @@ __device__ __forceinline__ void chan_gemm_x6p(f4 (&acc)[MT][NT], const unsigned 
   }
 }
 
-// LDS floats the GDN core needs for an R-row tile: mode 0 (fp32) the x² tile + γ stages, mode 1
-// (x6) the three bf16 planes of x², mode 2 (h3) the two fp16 planes + per-pixel partial maxima.
-constexpr int gdn_lds_floats(int R, int CO, int G6) {
-  return G6 == 2 ? R * (CO + 8) + 8 * R
-         : G6    ? (3 * R * (CO + 8) + 1) / 2
-                 : R * (CO + 8) + GSTAGE_FLOATS(CO);
-}
-
-__device__ __forceinline__ f4 mfma16h(const u4& a, const u4& b, const f4& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8v, a), __builtin_bit_cast(h8v, b),
-                                                c, 0, 0, 0);
-}
-
-// The channel contraction in the h3 form (common.h): A = the two fp16 planes of the scaled x² tile
-// [2][R][CO+8] in LDS, B = γ_eff's two planes [2][CO/8][CO][8] from L2 (hi·2¹¹ formed on load);
-// three f16 products per tile, as chan_gemm_x6p's six.
-template <int CO, int MT, int NT, int R>
-__device__ __forceinline__ void chan_gemm_h3p(f4 (&acc)[MT][NT], const unsigned short* sP,
-                                              const unsigned short* __restrict__ gh3, int wm,
-                                              int ncol0, int lane) {
-  constexpr int PS = CO + 8;
-  constexpr int KB = CO / 32;
-  constexpr long GP = (long)CO * CO;
-  static_assert(KB % 2 == 0, "k-blocks in pairs (ping-pong B registers)");
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
-  const unsigned short* arow = sP + (wm * MT * 16 + (lane & 15)) * PS + 8 * (lane >> 4);
-  const unsigned short* gb = gh3 + ((lane >> 4) * CO + ncol0 + (lane & 15)) * 8;
-  u4 b0[3][NT], b1[3][NT];   // hi, lo, hi·2¹¹
-  auto load = [&](int kb, u4 (&b)[3][NT]) {
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      b[0][nt] = *(const u4*)(gb + (long)kb * 4 * CO * 8 + nt * 128);
-      b[1][nt] = *(const u4*)(gb + GP + (long)kb * 4 * CO * 8 + nt * 128);
-    }
-  };
-  auto block = [&](int kb, u4 (&b)[3][NT]) {
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) b[2][nt] = h3_x2048(b[0][nt]);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const unsigned short* a = arow + mt * 16 * PS + kb * 32;
-      const u4 Ah = *(const u4*)(a);
-      const u4 Al = *(const u4*)(a + R * PS);
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        f4 c = mfma16h(Al, b[0][nt], acc[mt][nt]);
-        c = mfma16h(Ah, b[1][nt], c);
-        acc[mt][nt] = mfma16h(Ah, b[2][nt], c);
-      }
-    }
-  };
-  load(0, b0);
-  for (int kb = 0; kb < KB; kb += 2) {
-    load(kb + 1, b1);
-    block(kb, b0);
-    if (kb + 2 < KB) load(kb + 2, b0);
-    block(kb + 1, b1);
-  }
+// LDS floats the GDN core needs for an R-row tile (fp32 x² tile + γ stages, or, for the x6
+// contraction, the three split planes of x²).
+constexpr int gdn_lds_floats(int R, int CO, bool G6) {
+  return G6 ? (3 * R * (CO + 8) + 1) / 2 : R * (CO + 8) + GSTAGE_FLOATS(CO);
 }
 
 // x (bias already added) in accumulator layout → GDN(x) (or IGDN) left in LDS sX[BM][CO+4].
 // models/GDN.py:83-90: n = conv2d(x², γ, β) = β + Σ_j γ[i][j]·x_j²;  y = x / √n | x·√n.
 // The caller guarantees smem is free on entry; on return every wave has passed a barrier after
 // the last sX write.
-template <int CO, int MT, int NT, bool INVERSE, int R = BM, int T = 256, int G6 = 0>
+template <int CO, int MT, int NT, bool INVERSE, int R = BM, int T = 256, bool G6 = false>
 __device__ __forceinline__ void gdn_core(const f4 (&x)[MT][NT], float* sX,
                                          const float* __restrict__ gbeta,
                                          const float* __restrict__ gp, int wm, int ncol0,
-                                         int lane, const unsigned short* g6 = nullptr,
-                                         const unsigned short* gh3 = nullptr,
-                                         const float* __restrict__ gsc = nullptr) {
+                                         int lane, const unsigned short* g6 = nullptr) {
   constexpr int XS = CO + 8;
   f4 nacc[MT][NT];
-  if constexpr (G6 == 2) {
-    // h3: x² of a pixel (rounded to fp32, as conv2d(x², γ) sees it) scaled by a power of two s_p
-    // that puts the pixel's largest x² in [2¹³, 2¹⁴) (as the h3 engine's IGDN, engine_h3.hip),
-    // split into hi / lo fp16 planes; the pixel's channels span the 16-lane group × NT tiles of
-    // each of the WNC column waves, whose partial maxima meet in LDS
-    constexpr int WNC = CO / (NT * 16);
-    static_assert(WNC * NT * 16 == CO && WNC <= 8, "column waves");
-    unsigned short* sP = (unsigned short*)sX;
-    float* smx = sX + R * XS;   // [WNC][R]
-    const int wn = ncol0 / (NT * 16);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float m = 0.f;
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) m = fmaxf(m, fabsf(x[mt][nt][r]));
-#pragma unroll
-        for (int off = 1; off < 16; off <<= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
-        if ((lane & 15) == 0) smx[wn * R + wm * MT * 16 + mt * 16 + 4 * (lane >> 4) + r] = m;
-      }
-    __syncthreads();
-    int ep[MT][4];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wm * MT * 16 + mt * 16 + 4 * (lane >> 4) + r;
-        float m = 0.f;
-#pragma unroll
-        for (int w = 0; w < WNC; ++w) m = fmaxf(m, smx[w * R + row]);
-        const float m2 = m * m;
-        int e = 0;
-        ep[mt][r] = 0;
-        if (m2 > 0.f && m2 <= 3.40282347e38f) {
-          frexpf(m2, &e);   // m2 ∈ [2^(e−1), 2^e)
-          ep[mt][r] = 14 - e;
-        }
-        const float sp = ldexpf(1.0f, ep[mt][r]);
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-          const int col = ncol0 + nt * 16 + (lane & 15);
-          const float v = (x[mt][nt][r] * x[mt][nt][r]) * sp;
-          const _Float16 h = (_Float16)v;
-          const _Float16 l = (_Float16)((v - (float)h) * 2048.0f);
-          sP[row * XS + col] = h16_bits(h);
-          sP[(R + row) * XS + col] = h16_bits(l);
-        }
-      }
-    __syncthreads();   // planes of every wave published
-    chan_gemm_h3p<CO, MT, NT, R>(nacc, sP, gh3, wm, ncol0, lane);
-    // n = acc · 2⁻¹¹ / (σ_γ · s_p) = acc · gsc[1] · σ_a / s_p (powers of two: exact)
-    const float gs = gsc[1] * kH3Sa;
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float sc = ldexpf(gs, -ep[mt][r]);
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) nacc[mt][nt][r] *= sc;
-      }
-  } else if constexpr (G6) {
+  if constexpr (G6) {
     // x² (rounded to fp32, as conv2d(x², γ) sees it) split once into three bf16 planes
     unsigned short* sP = (unsigned short*)sX;
 #pragma unroll
@@ -757,12 +633,12 @@ __device__ __forceinline__ void acc_to_lds(const f4 (&v)[MT][NT], float* s, int 
       }
 }
 
-template <int CO, int MT, int NT, bool INVERSE, int R = BM, int T = 256, int G6 = 0>
+template <int CO, int MT, int NT, bool INVERSE, int R = BM, int T = 256, bool G6 = false>
 __device__ __forceinline__ void gdn_epilogue(f4 (&x)[MT][NT], float* smem, const EngineArgs& a,
                                              const TileInfo& t, int wm, int ncol0, int lane) {
   constexpr int XS = CO + 8;
   gdn_core<CO, MT, NT, INVERSE, R, T, G6>(x, smem, a.gbeta, a.ggamma, wm, ncol0, lane,
-                                          a.ggamma6, a.ggamma_h3, a.ggamma_scale);
+                                          a.ggamma6);
   if (a.out != nullptr) store_tile_rows<CO, R, T>(a, t, smem, XS, a.out, CO, 0);
   if (a.out_split != nullptr) store_tile_rows_split<CO, R, T>(a, t, smem, XS, CO, 0);
   if (a.out_h3 != nullptr) store_tile_rows_h3<CO, R, T>(a, t, smem, XS, CO, 0);
@@ -1166,8 +1042,7 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   constexpr int LDS_A = HALO ? HALO_PF + 2 * SB
                              : 2 * STAGE;   // two-stage ring (3, 4 stages measured slower: DESIGN.md §5)
   constexpr int LDS_XF = BMT * (CO + 8) + GSTAGE_FLOATS(CO);
-  constexpr int GM = H3 ? 2 : XS ? 1 : 0;           // GDN contraction form
-  constexpr int LDS_XP = gdn_lds_floats(BMT, CO, GM);
+  constexpr int LDS_XP = gdn_lds_floats(BMT, CO, XS);
   constexpr int LDS_X = (EPI == EPI_GDN || EPI == EPI_IGDN) ? (LDS_XF > LDS_XP ? LDS_XF : LDS_XP)
                         : (EPI == EPI_GDN_BWD || EPI == EPI_IGDN_BWD) ? LDS_XF : 0;
   constexpr int LDS_O = BMT * (BN + 4) + 8;
@@ -1517,7 +1392,7 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
       for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[mt][nt][r] += a.bias[ncol0 + nt * 16 + (lane & 15)];
-    gdn_epilogue<CO, MT, NT, EPI == EPI_IGDN, BMT, NWV * 64, GM>(acc, smem, a, t, wm, ncol0,
+    gdn_epilogue<CO, MT, NT, EPI == EPI_IGDN, BMT, NWV * 64, XS>(acc, smem, a, t, wm, ncol0,
                                                                 lane);
   } else if constexpr (EPI == EPI_QUANT) {
     quant_epilogue<CO, BN, MT, NT, WN>(acc, smem, a, t, wm, ncol0, lane, wave);
@@ -2188,11 +2063,7 @@ __host__ __device__ constexpr int x1_off(int row, int gran) {
   return row * X1RS + ((gran ^ (((row >> 2) & 1) << 3)) << 2);
 }
 
-// H3: the same kernel in the h3 form (common.h): the patch split into two fp16 planes of x·σ_a,
-// the weights pre-split into two fp16 planes (iclr17_split_packed_h3 of the ICLR17_W_CONV1_X6
-// packing), three f16 products per tile instead of six, and the GDN contraction in the h3 form
-// (gdn_core mode 2).
-template <int CO, int EPI, bool H3 = false>
+template <int CO, int EPI>
 __global__ void __launch_bounds__(256, 2) conv1_x6_kernel(const EngineArgs a) {
   constexpr int WN = 4;
   constexpr int MT = BM / 16;
@@ -2231,35 +2102,20 @@ __global__ void __launch_bounds__(256, 2) conv1_x6_kernel(const EngineArgs a) {
   // Weight planes: lane's B fragment base (k-group lane >> 4, column ncol0 + lane & 15).
   constexpr long GP = 32L * CO * 8;                     // plane stride (u16)
   const unsigned short* gb = (const unsigned short*)a.w + ((lane >> 4) * CO + ncol0 + (lane & 15)) * 8;
-  constexpr int NPL = H3 ? 2 : 3;                      // planes (H3: hi, lo; plane 2 = hi·2¹¹)
   u4 b0[3][NT], b1[3][NT];
   auto loadb = [&](int s, u4 (&b)[3][NT]) {
 #pragma unroll
-    for (int p = 0; p < NPL; ++p)
+    for (int p = 0; p < 3; ++p)
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
         b[p][nt] = *(const u4*)(gb + p * GP + (long)s * 4 * CO * 8 + nt * 128);
-    if constexpr (H3) {
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) b[2][nt] = h3_x2048(b[0][nt]);
-    }
   };
   loadb(0, b0);
   dma_barrier();   // patch landed
 
   // Split pass: piece pc (4 floats at column 4q of row cr) → 4 bf16 in each plane.
-  bool ovf = false;
   for (int pc = tid; pc < P1PIECES; pc += 256) {
     const f4 x = *(const f4*)(sr + pc * 4);
-    if constexpr (H3) {
-      uint2 hb, lb;
-      h3_split4(x, hb, lb, ovf);
-      const int cr = pc / 10, q = pc - cr * 10;
-      const int o = x1_off(cr, q);
-      *(uint2*)(sp + o) = hb;
-      *(uint2*)(sp + P1U + o) = lb;
-      continue;
-    }
     unsigned h[4], m[4], l[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -2277,7 +2133,6 @@ __global__ void __launch_bounds__(256, 2) conv1_x6_kernel(const EngineArgs a) {
     *(uint2*)(sp + 2 * P1U + o) = uint2{__builtin_amdgcn_perm(l[1], l[0], 0x07060302u),
                                         __builtin_amdgcn_perm(l[3], l[2], 0x07060302u)};
   }
-  if (H3 && ovf && a.range) atomicOr(a.range, 1);   // vector atomic, per offending lane (rare)
   __syncthreads();   // planes published
 
   f4 acc[MT][NT];
@@ -2294,16 +2149,6 @@ __global__ void __launch_bounds__(256, 2) conv1_x6_kernel(const EngineArgs a) {
   auto pair_row = [](int p) { return (p / 9) * P1 + p % 9; };
 
   auto mfma6 = [&](int mt, const bf8& Ah, const bf8& Am, const bf8& Al, const u4 (&b)[3][NT]) {
-    if constexpr (H3) {   // Ah, Am: the hi / lo fp16 planes; b: hi, lo, hi·2¹¹
-      const u4 ah = __builtin_bit_cast(u4, Ah), al = __builtin_bit_cast(u4, Am);
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        f4 c = mfma16h(al, b[0][nt], acc[mt][nt]);
-        c = mfma16h(ah, b[1][nt], c);
-        acc[mt][nt] = mfma16h(ah, b[2][nt], c);
-      }
-      return;
-    }
     X6Acc st;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
@@ -2321,9 +2166,9 @@ __global__ void __launch_bounds__(256, 2) conv1_x6_kernel(const EngineArgs a) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const unsigned short* e = sp + mt * 8 * X1RS;
-      u4 v[3] = {};
+      u4 v[3];
 #pragma unroll
-      for (int p = 0; p < NPL; ++p) {
+      for (int p = 0; p < 3; ++p) {
         const uint2 lo2 = *(const uint2*)(e + p * P1U + lo_off);
         const uint2 hi2 = *(const uint2*)(e + p * P1U + hi_off);
         v[p] = u4{lo2.x, lo2.y, hi2.x, hi2.y};
@@ -2342,9 +2187,9 @@ __global__ void __launch_bounds__(256, 2) conv1_x6_kernel(const EngineArgs a) {
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      u4 v[3] = {};
+      u4 v[3];
 #pragma unroll
-      for (int p = 0; p < NPL; ++p)
+      for (int p = 0; p < 3; ++p)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const unsigned lo = sp[p * P1U + po[2 * i] + mt * 8 * X1RS];
@@ -2372,13 +2217,6 @@ __global__ void __launch_bounds__(256, 2) conv1_x6_kernel(const EngineArgs a) {
   step_col8(b1);
 
   __syncthreads();  // patch reads done before the epilogue reuses LDS
-  if constexpr (H3) {   // the contraction carries 2¹¹·σ_a·σ_w: a power of two, removed exactly
-    const float dsc = a.wscale[1];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = acc[mt][nt] * dsc;
-  }
   if constexpr (EPI == EPI_GDN) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
@@ -2386,7 +2224,7 @@ __global__ void __launch_bounds__(256, 2) conv1_x6_kernel(const EngineArgs a) {
       for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[mt][nt][r] += a.bias[ncol0 + nt * 16 + (lane & 15)];
-    gdn_epilogue<CO, MT, NT, false, BM, 256, H3 ? 2 : 1>(acc, smem, a, t, wm, ncol0, lane);
+    gdn_epilogue<CO, MT, NT, false, BM, 256, true>(acc, smem, a, t, wm, ncol0, lane);
   } else {
     static_assert(EPI == EPI_IGDN_BWD, "conv1 x6 epilogues: GDN fwd, IGDN bwd");
     gdn_bwd_epilogue<CO, MT, NT, true>(acc, smem, a, t, wm, ncol0, lane);
@@ -2665,8 +2503,6 @@ struct SplitIO {
   unsigned short* out_h3 = nullptr;         // h3-form output
   long out_h3_plane = 0;
   int* range = nullptr;
-  const unsigned short* gamma_h3 = nullptr;   // h3: γ_eff in the h3 form
-  const float* gamma_h3_scale = nullptr;      //   and its trailer
 };
 
 static void apply_split(EngineArgs& a, const SplitIO* x6) {
@@ -2681,8 +2517,6 @@ static void apply_split(EngineArgs& a, const SplitIO* x6) {
   a.out_h3 = x6->out_h3;
   a.out_h3_plane = x6->out_h3_plane;
   a.range = x6->range;
-  a.ggamma_h3 = x6->gamma_h3;
-  a.ggamma_scale = x6->gamma_h3_scale;
 }
 
 template <int N, int EPI = EPI_GDN>
@@ -3221,36 +3055,6 @@ int iclr17_analysis_conv3_quant_rate_x6w(const uint16_t* in_split, int B, int H,
   io.w6_plane = 25L * N * N;
   return N == 192 ? launch_conv5<192, EPI_QUANT>(nullptr, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io, rate_table)
                   : launch_conv5<128, EPI_QUANT>(nullptr, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io, rate_table);
-}
-
-int iclr17_analysis_conv1_gdn_h3(const float* x, int B, int H, int W, int N,
-                                 const uint16_t* w_h3, const float* bias, const float* beta_eff,
-                                 const uint16_t* gamma_h3, float* out, uint16_t* out_h3,
-                                 int* range_flag, void* stream) {
-  int rc = check_dims(B, H, W, N);
-  if (rc) return rc;
-  ICLR17_REQUIRE(x && w_h3 && bias && beta_eff && gamma_h3 && (out || out_h3),
-                 ICLR17_EINVAL, "conv1_gdn_h3: null pointer");
-  EngineArgs a;
-  memset(&a, 0, sizeof(a));
-  a.in = x; a.w = (const float*)w_h3; a.bias = bias; a.gbeta = beta_eff;
-  a.wscale = (const float*)(w_h3 + 2L * 256 * N);   // iclr17_split_packed_h3 trailer
-  a.out = out;
-  a.out_h3 = (unsigned short*)out_h3;
-  a.out_h3_plane = (long)B * (H / 4) * (W / 4) * N;
-  a.range = range_flag;
-  a.ggamma_h3 = (const unsigned short*)gamma_h3;
-  a.ggamma_scale = (const float*)(gamma_h3 + 2L * N * N);
-  a.B = B; a.Hin = H; a.Win = W; a.Hout = H / 4; a.Wout = W / 4;
-  a.gh = H / 4; a.gw = W / 4; a.tiles_y = (a.gh + 7) / 8; a.tiles_x = (a.gw + 7) / 8;
-  a.sin = 4; a.sout = 1;
-  a.tt.npx = 1; a.tt.nph = 1;
-  dim3 grid(a.tiles_x * a.tiles_y * B, 1);
-  if (N == 192)
-    hipLaunchKernelGGL((conv1_x6_kernel<192, EPI_GDN, true>), grid, dim3(256), 0, S(stream), a);
-  else
-    hipLaunchKernelGGL((conv1_x6_kernel<128, EPI_GDN, true>), grid, dim3(256), 0, S(stream), a);
-  return check_launch("conv1_gdn_h3");
 }
 
 int iclr17_analysis_conv3_quant_rate_h3(const uint16_t* in_h3, int B, int H, int W, int N,

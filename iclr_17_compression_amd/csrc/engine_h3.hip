@@ -55,6 +55,7 @@ enum HEpi : int { HE_GDN = 0, HE_IGDN = 1 };
 
 struct HArgs {
   const u16* in;        // h3 input [2][B][Hin][Win][CI] (fp16 bits)
+  const float* img;     // HM_CONV1: the fp32 NCHW image [B][3][Hin][Win]
   long in_plane;
   const u16* w;         // iclr17_pack_h3k weights, [2][…] (plane stride w_plane) + trailer
   long w_plane;
@@ -97,6 +98,28 @@ struct PatchC8 {
     return t < 25 ? off(t / 5, t % 5) : 0;
   }
 };
+// conv1 (k9 s4 p4, 3 input channels) in this engine: the whole 3 × 69 × 69 input window of a
+// 16 × 16-pixel output tile split once into the two h3 planes, [channel][row][80 columns] fp16
+// (160-byte rows: the two pixel rows of a fragment half, 4 input rows apart, land 128 bytes apart
+// mod 256 — their ds_read_b64 lane groups cover all 64 banks); K = 243 reordered as in the x6
+// conv1 kernel (csrc/engine_fp32.hip conv1_x6_kernel): k-group g < 27 = 8 consecutive columns of
+// one (channel, kernel row), g = 27 .. 30 = column 8 of (channel, kernel row) pairs 8(g − 27) + e,
+// g = 31 zero; 16 steps of 16 (lane half h: g = 2s + h).
+constexpr int HM_CONV1 = 3;
+constexpr int kConv1Steps = 16;
+template <int TH>
+struct PatchC1 {
+  static constexpr int ROWS = 4 * TH + 5;
+  static constexpr int ROWB = 160;
+  static constexpr int BYTES = 3 * ROWS * ROWB;   // one plane
+  // byte offset of k-group g's (channel, kernel row) row, g < 27
+  __host__ __device__ static constexpr int rowoff(int g) { return ((g / 9) * ROWS + g % 9) * ROWB; }
+  // byte offset of pair q's column-8 element (−1: a zero-weight pad)
+  __host__ __device__ static constexpr int gath(int q) {
+    return q < 27 ? ((q / 9) * ROWS + q % 9) * ROWB + 16 : -1;
+  }
+};
+
 template <int MODE, int TH>
 struct HPatch {
   using type = Patch<MODE, TH>;
@@ -105,22 +128,28 @@ template <int TH>
 struct HPatch<HM_CONV8, TH> {
   using type = PatchC8<TH>;
 };
+template <int TH>
+struct HPatch<HM_CONV1, TH> {
+  using type = PatchC1<TH>;
+};
 
 template <int MODE, int TH, int CO, int CI, bool INT_IN>
 struct HK {
   static constexpr int NW = TH / 2, NTHR = NW * 64;
   static constexpr int NT = CO / 32;           // 32-channel accumulator tiles per wave
+  static constexpr bool C1 = MODE == HM_CONV1;
   static constexpr int CCH = MODE == HM_CONV8 ? 8 : 16;   // channels per chunk
-  static constexpr int NCH = CI / CCH;         // chunks
+  static constexpr int NCH = C1 ? 1 : CI / CCH;  // chunks (conv1: the whole window, once)
   using P = typename HPatch<MODE, TH>::type;
   static constexpr int PL = INT_IN ? 1 : 2;    // input planes staged
   static constexpr int PB = PL * P::BYTES;     // patch bytes (planes back to back)
-  static constexpr int NQI = (PB + 1023) / 1024;
-  static constexpr int PBUF = NQI * 1024;
+  static constexpr int NQI = C1 ? 0 : (PB + 1023) / 1024;   // patch DMA pieces per chunk
+  static constexpr int PBUF = (PB + 1023) / 1024 * 1024;
+  static constexpr int NPB = C1 ? 1 : 2;       // patch buffers
   static constexpr int SB = 2 * 2 * CO * 16;   // weight stage: [plane 2][half 2][CO][8] fp16
   static constexpr int NBI = SB / 1024;
   static constexpr int NST = 4;
-  static constexpr int MAIN = 2 * PBUF + NST * SB + 1024;
+  static constexpr int MAIN = NPB * PBUF + NST * SB + 1024;
   static constexpr int NTH = NT / 2;           // epilogue: output tiles per pass
   static constexpr int KB = CO / 16;           // epilogue: 16-channel k-blocks
   static constexpr int GBL = 2 * NTH * KB;     // epilogue: γ fragment blocks per pass (1 KB)
@@ -128,7 +157,7 @@ struct HK {
   static constexpr int BBOFF = (LDS0 + 1023) / 1024 * 1024;
   static constexpr int LDS = BBOFF + 2048;     // + bias, β_eff
   static_assert(SB % 1024 == 0, "weight stage");
-  static_assert(NT % 2 == 0 && CI % CCH == 0, "tile shape");
+  static_assert(NT % 2 == 0 && (C1 || CI % CCH == 0), "tile shape");
   static_assert(LDS <= 160 * 1024, "LDS");
 };
 
@@ -136,10 +165,11 @@ template <int MODE, int TH, int CO, int CI, int EPI, bool INT_IN, int PH>
 __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, int b, int ty, int tx) {
   using KK = HK<MODE, TH, CO, CI, INT_IN>;
   using P = typename KK::P;
-  constexpr bool CONV = MODE != BM_DECONV, C8 = MODE == HM_CONV8;
+  constexpr bool CONV = MODE != BM_DECONV, C8 = MODE == HM_CONV8, C1 = MODE == HM_CONV1;
   using TP = Taps<CONV ? BM_CONV : BM_DECONV, PH>;
-  // one tap per step (HM_CONV8: a tap pair)
-  constexpr int NT = KK::NT, NW = KK::NW, NCH = KK::NCH, S = C8 ? kConv8Steps : TP::T;
+  // one tap per step (HM_CONV8: a tap pair; HM_CONV1: two k-groups)
+  constexpr int NT = KK::NT, NW = KK::NW, NCH = KK::NCH;
+  constexpr int S = C1 ? kConv1Steps : C8 ? kConv8Steps : TP::T;
   constexpr int SB = KK::SB, NBI = KK::NBI, NST = KK::NST;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -155,7 +185,7 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
   static_assert(F * K < 64, "vmcnt");
   constexpr int GS = NCH * S;
   unsigned char* const sP = smem;
-  unsigned char* const sB = smem + 2 * KK::PBUF;
+  unsigned char* const sB = smem + KK::NPB * KK::PBUF;
   unsigned char* const sD = sB + NST * SB;
   float* const sbb = (float*)(smem + KK::BBOFF);   // [bias | pad][β_eff | pad]
   const long img = (long)b * a.Hin * a.Win;
@@ -169,11 +199,14 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
     const int pr = rem / P::ROWB, r1 = rem - pr * P::ROWB;
     int pc, hh = 0;
     bool ok;
-    if constexpr (C8) {
+    if constexpr (C1) {   // conv1 stages its window without pieces
+      pc = 0;
+      ok = false;
+    } else if constexpr (C8) {
       const int par = r1 / 320, slot = (r1 - par * 320) / 16;
       pc = 2 * slot + par;
       ok = slot < 18 && pc < 35;
-    } else if (MODE == BM_CONV) {
+    } else if constexpr (MODE == BM_CONV) {
       const int par = r1 / (2 * P::HALF), r2 = r1 - par * 2 * P::HALF;
       hh = r2 / P::HALF;
       pc = 2 * ((r2 - hh * P::HALF) / 16) + par;
@@ -229,11 +262,13 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
   const int prow = 2 * wave + (r32 >> 4), pcol = r32 & 15;
   const int tpix = prow * 16 + pcol;
   int pbase;
-  if constexpr (C8) pbase = P::off(2 * prow, 2 * pcol);
+  if constexpr (C1) pbase = 4 * prow * P::ROWB + 8 * pcol;
+  else if constexpr (C8) pbase = P::off(2 * prow, 2 * pcol);
   else pbase = (MODE == BM_CONV ? P::off(2 * prow, 2 * pcol) : P::off(prow, pcol)) + h * P::HALF;
   // the step's tap offset: one tap for every lane, or (HM_CONV8) tap 2s + h for lane half h
   auto tap_of = [&](int s) -> int {
     if constexpr (C8) return h ? P::tap8(2 * s + 1) : P::tap8(2 * s);
+    else if constexpr (C1) return 0;
     else return P::template tap_off<PH>(s);
   };
   // A (weights): stage [plane][2][CO][8]: lane (k-group h, channel 32·i + r32)
@@ -268,6 +303,35 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
   for (int f = 1; f < F; ++f)
 #pragma unroll
     for (int k = 0; k < K; ++k) sink4(sD);
+  if constexpr (C1) {
+    // the input window (fp32 NCHW image a.img) → the two h3 planes, once: 18 float4 per patch
+    // row (72 columns ≥ 69), every load issued before the first split
+    constexpr int QR = 18, NU = 3 * P::ROWS * QR, IT = (NU + KK::NTHR - 1) / KK::NTHR;
+    const int jy0 = 4 * TH * ty - 4, jx0 = 64 * tx - 4;
+    const float* __restrict__ xb = a.img + (long)b * 3 * a.Hin * a.Win;
+    f4 v[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int u = tid + it * KK::NTHR;
+      const int q = u % QR, cr = u / QR, c = cr / P::ROWS, r = cr - c * P::ROWS;
+      const int iy = jy0 + r, ix = jx0 + 4 * q;
+      const bool ok = u < NU && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
+      v[it] = ok ? *(const f4*)(xb + ((long)c * a.Hin + iy) * a.Win + ix) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+    bool povf = false;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int u = tid + it * KK::NTHR;
+      if (u >= NU) break;
+      const int q = u % QR, cr = u / QR;
+      uint2 hb, lb;
+      h3_split4(v[it], hb, lb, povf);
+      *(uint2*)(sP + cr * P::ROWB + 8 * q) = hb;
+      *(uint2*)(sP + P::BYTES + cr * P::ROWB + 8 * q) = lb;
+    }
+    if (povf && a.range) atomicOr(a.range, 1);   // vector atomic, per offending lane (rare)
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the planes written before the first barrier
+  }
 
   typedef const __attribute__((address_space(3))) u4* lu4p;
   // slot k of step g's DMA group: weights of step g+F+1, the next chunk's patch, or a sink load
@@ -288,10 +352,46 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
   struct Frag {
     u4 bh, bl, wh[NT], wl[NT];
   };
-  auto read_frag = [&](Frag& f, const unsigned char* pb, int to, const unsigned char* wb) {
-    f.bh = *(lu4p)(pb + to);
-    if constexpr (!INT_IN) f.bl = *(lu4p)(pb + P::BYTES + to);
-    else f.bl = u4{0u, 0u, 0u, 0u};
+  typedef unsigned u2e __attribute__((ext_vector_type(2)));
+  typedef const __attribute__((address_space(3))) u2e* lu2p;
+  typedef const __attribute__((address_space(3))) unsigned short* lu16p;
+  // conv1's B fragment of step s from one plane (lane half h: k-group g = 2s + h)
+  auto conv1_b = [&](const unsigned char* pp, int s) -> u4 {
+    u4 v = u4{0u, 0u, 0u, 0u};
+    if constexpr (!C1) return v;
+    else {
+    const int g0 = 2 * s, g1 = 2 * s + 1;
+    if (g0 < 27) {   // 8 columns of one (channel, kernel row): two 8-byte reads
+      const int ro = h ? (g1 < 27 ? P::rowoff(g1) : P::rowoff(g0)) : P::rowoff(g0);
+      const u2e x0 = *(lu2p)(pp + ro), x1 = *(lu2p)(pp + ro + 8);
+      v = u4{x0.x, x0.y, x1.x, x1.y};
+    }
+    if (g1 >= 27) {   // column 8 of eight (channel, kernel row) pairs, element-wise
+      unsigned e[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int oa = g0 >= 27 ? P::gath(8 * (g0 - 27) + j) : -1;
+        const int ob = P::gath(8 * (g1 - 27) + j);
+        const int o = h ? ob : oa;
+        const unsigned x = *(lu16p)(pp + (o >= 0 ? o : 0));
+        e[j] = o >= 0 ? x : 0u;
+      }
+      const u4 w = u4{e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16)};
+      if (g0 >= 27) v = w;
+      else if (h) v = w;   // g0 = 26: the lower half keeps its row read
+    }
+    return v;
+    }
+  };
+  auto read_frag = [&](Frag& f, const unsigned char* pb, int to, const unsigned char* wb, int s) {
+    if constexpr (C1) {
+      f.bh = conv1_b(sP + pbase, s);
+      f.bl = conv1_b(sP + P::BYTES + pbase, s);
+    } else {
+      f.bh = *(lu4p)(pb + to);
+      if constexpr (!INT_IN) f.bl = *(lu4p)(pb + P::BYTES + to);
+      else f.bl = u4{0u, 0u, 0u, 0u};
+    }
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
       f.wh[i] = *(lu4p)(wb + i * 512);
@@ -307,10 +407,10 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
       wait_vm_barrier<(F - 1) * K>();   // step g+1's weights (and patch) landed (at g = 0 the
                                         // prologue's padding tail is all that may be in flight);
                                         // stage (g+F+1) % NST is free
-      if (s == 0 && c == 0) read_frag(cur, sP + pbase, tap_of(0), sB + abase);
+      if (s == 0 && c == 0) read_frag(cur, sP + pbase, tap_of(0), sB + abase, 0);
       Frag nxt;
       read_frag(nxt, sP + ((s + 1 < S ? c : c + 1) & 1) * KK::PBUF + pbase,
-                tap_of(s + 1 < S ? s + 1 : 0), sB + stage * SB + abase);
+                tap_of(s + 1 < S ? s + 1 : 0), sB + stage * SB + abase, s + 1 < S ? s + 1 : 0);
       stage = stage + 1 == NST ? 0 : stage + 1;
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
@@ -443,38 +543,64 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
 #pragma unroll
     for (int il = 0; il < NTH; ++il) {
       const int i = hf * NTH + il;
+      f4 y[4];
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const int ch = 32 * i + 8 * m + 4 * eh;
         const f4 be = *(const f4*)(sbb + 256 + ch);
-        f4 y;
+        // the hardware square root / reciprocal square root (v_sqrt_f32, v_rsq_f32: within an ulp
+        // or two, far inside the h3 form's own 2⁻²² — and a sixth of the IEEE sequences' VALU
+        // work, which set the epilogue's length); n ≥ β_min > 0
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float s = sqrtf(n[il][4 * m + j] + be[j]);
+          const float nn = n[il][4 * m + j] + be[j];
           const float x = acc[i][4 * m + j];
-          y[j] = EPI == HE_IGDN ? x * s : x / s;
+          y[m][j] = EPI == HE_IGDN ? x * __builtin_amdgcn_sqrtf(nn) : x * __builtin_amdgcn_rsqf(nn);
         }
-        if (!inside) continue;
-        if (a.out) *(f4*)(a.out + o * CO + ch) = y;
-        if (a.out_h3) {
-          uint2 hb, lb;
-          h3_split4(y, hb, lb, ovf);
-          const long so = a.out_cm ? (((long)b * (CO / 32) + i) * a.Hout + oy) * a.Wout * 32 + (long)ox * 32 + 8 * m + 4 * eh
-                                   : o * CO + ch;
-          *(uint2*)(a.out_h3 + so) = hb;
-          *(uint2*)(a.out_h3 + a.out_h3_plane + so) = lb;
+        if (inside && a.out) *(f4*)(a.out + o * CO + ch) = y[m];
+      }
+      if (a.out_h3) {
+        // the tile's 32 channels of this pixel in the h3 form, as two 16-byte stores per plane:
+        // lanes eh hold channels 8m + 4eh + 0..3; one permlane32 swap per dword pair (m, m + 2)
+        // hands lane half 0 channels 0 .. 15 and half 1 channels 16 .. 31 (half the store
+        // instructions of 8-byte stores; the epilogue's stores were issue-bound)
+        uint2 hb[4], lb[4];
+        bool ov = false;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) h3_split4(y[m], hb[m], lb[m], ov);
+        ovf |= inside && ov;
+        u4 sv[2][2];
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const uint2 A = pl ? lb[k] : hb[k], B = pl ? lb[k + 2] : hb[k + 2];
+            const auto sx = __builtin_amdgcn_permlane32_swap(A.x, B.x, false, false);
+            const auto sy = __builtin_amdgcn_permlane32_swap(A.y, B.y, false, false);
+            sv[pl][k] = u4{sx[0], sy[0], sx[1], sy[1]};
+          }
+        if (inside) {
+          const long so = a.out_cm ? (((long)b * (CO / 32) + i) * a.Hout + oy) * a.Wout * 32 + (long)ox * 32 + 16 * eh
+                                   : o * CO + 32 * i + 16 * eh;
+          *(u4*)(a.out_h3 + so) = sv[0][0];
+          *(u4*)(a.out_h3 + so + 8) = sv[0][1];
+          *(u4*)(a.out_h3 + a.out_h3_plane + so) = sv[1][0];
+          *(u4*)(a.out_h3 + a.out_h3_plane + so + 8) = sv[1][1];
         }
-        if (a.out_x6) {
+      }
+      if (inside && a.out_x6) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
           unsigned hb[4], mb[4], lb[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            hb[j] = __float_as_uint(y[j]) & 0xffff0000u;
-            const float r = y[j] - __uint_as_float(hb[j]);
+            hb[j] = __float_as_uint(y[m][j]) & 0xffff0000u;
+            const float r = y[m][j] - __uint_as_float(hb[j]);
             mb[j] = __float_as_uint(r) & 0xffff0000u;
             lb[j] = __float_as_uint(r - __uint_as_float(mb[j]));
           }
           const long so = a.out_cm ? (((long)b * (CO / 32) + i) * a.Hout + oy) * a.Wout * 32 + (long)ox * 32 + 8 * m + 4 * eh
-                                   : o * CO + ch;
+                                   : o * CO + 32 * i + 8 * m + 4 * eh;
           *(uint2*)(a.out_x6 + so) = uint2{__builtin_amdgcn_perm(hb[1], hb[0], 0x07060302u),
                                            __builtin_amdgcn_perm(hb[3], hb[2], 0x07060302u)};
           *(uint2*)(a.out_x6 + a.out_x6_plane + so) = uint2{__builtin_amdgcn_perm(mb[1], mb[0], 0x07060302u),
@@ -595,7 +721,13 @@ __global__ void __launch_bounds__(256) pack_h3k_kernel(const float* __restrict__
     int u = (int)(r / 2);   // block index
     int c, ky, kx, ci0;
     bool zero = false;
-    if (!deconv) {
+    if (deconv == 2) {   // conv1 (W[co][3][9][9]): block = step s, k-group g = 2s + h
+      // (kx is the element j, or 8 for the column-8 groups; ci0 + j carries the channel instead)
+      c = 0;
+      ci0 = 0;
+      ky = kx = 0;
+      zero = true;   // resolved per element below
+    } else if (!deconv) {
       c = u / kConv8Steps;
       const int t = 2 * (u - c * kConv8Steps) + h;
       zero = t >= 25;
@@ -622,9 +754,22 @@ __global__ void __launch_bounds__(256) pack_h3k_kernel(const float* __restrict__
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int ci = ci0 + j;
-      const float v = zero ? 0.f
-                           : (deconv ? w[(((long)ci * N + co) * 5 + ky) * 5 + kx]
-                                     : w[(((long)co * N + ci) * 5 + ky) * 5 + kx]) * sw;
+      float v;
+      if (deconv == 2) {
+        const int g = 2 * u + h;
+        int cc = -1, yy = 0, xx = 0;
+        if (g < 27) {
+          cc = g / 9; yy = g % 9; xx = j;
+        } else {
+          const int q = 8 * (g - 27) + j;
+          if (q < 27) { cc = q / 9; yy = q % 9; xx = 8; }
+        }
+        v = cc < 0 ? 0.f : w[(((long)co * 3 + cc) * 9 + yy) * 9 + xx] * sw;
+      } else {
+        v = zero ? 0.f
+                 : (deconv ? w[(((long)ci * N + co) * 5 + ky) * 5 + kx]
+                           : w[(((long)co * N + ci) * 5 + ky) * 5 + kx]) * sw;
+      }
       const _Float16 hh = (_Float16)v;
       hv[j] = h16_bits(hh);
       lv[j] = h16_bits((_Float16)((v - (float)hh) * 2048.0f));
@@ -710,6 +855,7 @@ extern "C" {
 
 size_t iclr17_h3k_weight_size(int which, int N) {
   if (N != 128 && N != 192) return 0;
+  if (which == ICLR17_H3K_CONV1) return (size_t)2 * kConv1Steps * 2 * N * 8 + 8;
   if (which != ICLR17_H3K_CONV5 && which != ICLR17_H3K_DECONV5) return 0;
   // two planes of 25 (chunk, tap) blocks per 16-channel chunk (deconv) or 13 (chunk, tap pair)
   // blocks per 8-channel chunk (conv), + the 16-byte trailer
@@ -724,12 +870,14 @@ int iclr17_pack_h3k(int which, const float* w, uint16_t* out, int N, void* strea
   const long groups = (long)((total - 8) / 16);
   float* trailer = (float*)(out + (total - 8));
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(absmax_kernel, dim3(1), dim3(1024), 0, st, w, (long)N * N * 25, trailer);
+  const long nw = which == ICLR17_H3K_CONV1 ? (long)N * 3 * 81 : (long)N * N * 25;
+  hipLaunchKernelGGL(absmax_kernel, dim3(1), dim3(1024), 0, st, w, nw, trailer);
   int rc = check_launch("pack_h3k absmax");
   if (rc) return rc;
   const int blocks = (int)((groups + 255) / 256 < 4096 ? (groups + 255) / 256 : 4096);
   hipLaunchKernelGGL(pack_h3k_kernel, dim3(blocks), dim3(256), 0, st, w, N,
-                     which == ICLR17_H3K_DECONV5 ? 1 : 0, groups, out, trailer);
+                     which == ICLR17_H3K_DECONV5 ? 1 : which == ICLR17_H3K_CONV1 ? 2 : 0, groups,
+                     out, trailer);
   return check_launch("pack_h3k");
 }
 
@@ -762,6 +910,40 @@ int iclr17_h3_planes(const float* x, long n, uint16_t* planes, int* range_flag, 
   hipLaunchKernelGGL(h3_planes_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, n4, n,
                      planes, range_flag);
   return check_launch("h3_planes");
+}
+
+int iclr17_analysis_conv1_gdn_h3(const float* x, int B, int H, int W, int N,
+                                 const uint16_t* w_h3k, const float* bias, const float* beta_eff,
+                                 const uint16_t* gamma_h3, float* out, uint16_t* out_h3,
+                                 int* range_flag, void* stream) {
+  ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "conv1_gdn_h3: N=%d", N);
+  ICLR17_REQUIRE(x && w_h3k && bias && beta_eff && gamma_h3 && (out || out_h3) && B > 0 &&
+                     H > 0 && W > 0 && H % 16 == 0 && W % 16 == 0,
+                 ICLR17_EINVAL, "conv1_gdn_h3: bad arguments");
+  HArgs a;
+  memset(&a, 0, sizeof(a));
+  a.img = x;
+  const size_t wsz = iclr17_h3k_weight_size(ICLR17_H3K_CONV1, N);
+  a.w = w_h3k; a.w_plane = (long)(wsz - 8) / 2;
+  a.wscale = (const float*)(w_h3k + (wsz - 8));
+  a.bias = bias; a.beta = beta_eff; a.gamma_h3 = gamma_h3;
+  a.gamma_scale = (const float*)(gamma_h3 + 2L * N * N);
+  a.out = out;
+  a.out_h3 = out_h3; a.out_h3_plane = (long)B * (H / 4) * (W / 4) * N;
+  a.range = range_flag;
+  a.B = B; a.Hin = H; a.Win = W; a.Hout = H / 4; a.Wout = W / 4;
+  a.gh = H / 4; a.gw = W / 4;
+  constexpr int TH = 16;
+  a.tiles_y = (a.gh + TH - 1) / TH;
+  a.tiles_x = (a.gw + 15) / 16;
+  const dim3 grid(a.tiles_x * a.tiles_y * B);
+  if (N == 192)
+    hipLaunchKernelGGL((h3k_kernel<HM_CONV1, TH, 192, 3, HE_GDN, false>), grid, dim3(TH / 2 * 64), 0,
+                       (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL((h3k_kernel<HM_CONV1, TH, 128, 3, HE_GDN, false>), grid, dim3(TH / 2 * 64), 0,
+                       (hipStream_t)stream, a);
+  return check_launch("conv1_gdn_h3");
 }
 
 int iclr17_analysis_conv2_gdn_h3(const uint16_t* in_h3, int B, int H, int W, int N,

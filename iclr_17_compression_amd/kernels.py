@@ -494,8 +494,8 @@ def merge_h3(s: Tensor) -> Tensor:
 
 
 def pack_h3k(which: int, w: Tensor, N: int) -> Tensor:
-    """k5 weights → the h3 engine's two fp16 planes (per-tensor power-of-two scale) + trailer
-    (ICLR17_H3K_CONV5 / ICLR17_H3K_DECONV5)."""
+    """conv / deconv weights → the h3 engine's two fp16 planes (per-tensor power-of-two scale) +
+    trailer (ICLR17_H3K_CONV1 / ICLR17_H3K_CONV5 / ICLR17_H3K_DECONV5)."""
     _check(w, "weight", 4)
     size = query("iclr17_h3k_weight_size", which, N)
     if size == 0:
@@ -520,23 +520,22 @@ def split_packed_h3(packed: Tensor, taps: int, K: int, N: int) -> Tensor:
 
 
 def pack_conv1_h3(w: Tensor, N: int) -> Tensor:
-    """conv1 weight [N,3,9,9] → the h3 planes conv1_gdn_h3 reads (split_packed_h3 of the
-    ICLR17_W_CONV1_X6 packing: two fp16 planes [2, 256·N] + trailer)."""
-    return split_packed_h3(pack_weight(_lib.ICLR17_W_CONV1_X6, w, N), 1, 256, N)
+    """conv1 weight [N,3,9,9] → the h3 engine's conv1 packing (pack_h3k, ICLR17_H3K_CONV1)."""
+    return pack_h3k(_lib.ICLR17_H3K_CONV1, w, N)
 
 
 def conv1_gdn_h3(x: Tensor, w_h3: Tensor, bias: Tensor, beta_eff: Tensor, gh3: Tensor, N: int,
                  want_f32: bool = False):
-    """analysis_17.py:14-17 conv1 + GDN1 in the h3 form (three f16 part products per MAC for the
-    convolution and the GDN contraction; w_h3: ``pack_conv1_h3``, gh3: GDN.effective_params_h3's
-    γ). Returns (h3 [2,B,H/4,W/4,N], fp32 | None)."""
+    """analysis_17.py:14-17 conv1 + GDN1 in the h3 form on the h3 engine (three f16 part products
+    per MAC for the convolution and the GDN contraction; w_h3: ``pack_conv1_h3``, gh3:
+    GDN.effective_params_h3's γ). Returns (h3 [2,B,H/4,W/4,N], fp32 | None)."""
     _check(x, "image", 4)
     B, C, H, W = x.shape
     if C != 3:
         raise Iclr17Error(f"iclr17: the analysis transform takes 3-channel images (got {C})")
     _check_image_dims(H, W)
     _check_channels(N)
-    if w_h3.dtype != torch.int16 or w_h3.numel() != query("iclr17_split_packed_h3_size", 1, 256, N):
+    if w_h3.dtype != torch.int16 or w_h3.numel() != query("iclr17_h3k_weight_size", _lib.ICLR17_H3K_CONV1, N):
         raise Iclr17Error("iclr17: conv1_gdn_h3 needs pack_conv1_h3 weights")
     if gh3.dtype != torch.int16 or gh3.numel() != query("iclr17_split_packed_h3_size", 1, N, N):
         raise Iclr17Error("iclr17: conv1_gdn_h3 needs γ in the h3 form (effective_params_h3)")

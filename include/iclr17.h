@@ -473,6 +473,7 @@ int iclr17_rate_param_grad(const float* partial, int T, int C, const float* h1, 
  * (synthesis_17.py:15-22; models/GDN.py:64-94, inverse). */
 #define ICLR17_H3K_CONV5 42   /* conv2 W[co][ci][5][5] → [2][N/8·13][2][N][8] fp16 planes + trailer */
 #define ICLR17_H3K_DECONV5 43 /* deconv1/2 W[ci][co][5][5] → [2][4 phases: N/16·T_p][2][N][8] + trailer */
+#define ICLR17_H3K_CONV1 44   /* conv1 W[co][3][9][9] → [2][16 steps][2][N][8] (reordered K) + trailer */
 /* uint16 elements: two planes + an 8-element (16-byte) trailer {max|w|, 2^-11/(σ_a·σ_w)}; 0 =
  * unsupported */
 size_t iclr17_h3k_weight_size(int which, int N);
@@ -485,19 +486,15 @@ int iclr17_h3_planes(const float* x, long n, uint16_t* planes, int* range_flag, 
 size_t iclr17_split_packed_h3_size(int taps, int K, int N);
 int iclr17_split_packed_h3(const float* packed, int taps, int K, int N, uint16_t* planes,
                            void* stream);
-/* analysis_17.py:14-17 conv1 + GDN1 in the h3 form: the image split into two fp16 planes in LDS,
- * three f16 part products per MAC for the 9×9 convolution and for the GDN contraction; output in
- * the h3 form [2][B][H/4][W/4][N] and/or fp32 NHWC. w_h3: iclr17_split_packed_h3(packing
- * ICLR17_W_CONV1_X6, taps 1, K 256, N); gamma_h3: iclr17_split_packed_h3(γ_eff packing, 1, N, N). */
+/* analysis_17.py:14-17 conv1 + GDN1 on the h3 engine (csrc/engine_h3.hip): 16×16-pixel output tiles
+ * of 8 waves; the tile's 3 × 69 × 69 input window split once into the two h3 planes in LDS, K = 243
+ * reordered into 16 steps of 16, three f16 part products per MAC, GDN contraction in the h3 form;
+ * output in the h3 form [2][B][H/4][W/4][N] and/or fp32 NHWC. w_h3k: iclr17_pack_h3k(ICLR17_H3K_CONV1);
+ * gamma_h3: iclr17_split_packed_h3(γ_eff packing, 1, N, N). */
 int iclr17_analysis_conv1_gdn_h3(const float* x, int B, int H, int W, int N,
-                                 const uint16_t* w_h3, const float* bias, const float* beta_eff,
+                                 const uint16_t* w_h3k, const float* bias, const float* beta_eff,
                                  const uint16_t* gamma_h3, float* out, uint16_t* out_h3,
                                  int* range_flag, void* stream);
-/* analysis_17.py:18-21 conv2 + GDN2 on the h3 engine (csrc/engine_h3.hip): 16×16-pixel tiles of 8
- * waves, 8-channel chunks with two taps per 16-deep MFMA step, three f16 part products per MAC;
- * input [2][B][H/4][W/4][N] (h3) → fp32 NHWC and/or the h3 output [2][B][H/8][W/8][N] and/or the
- * x6 split output [3][B][H/8][W/8][N] (nullable, not all); GDN contraction in the h3 form.
- * w_h3k: iclr17_pack_h3k(ICLR17_H3K_CONV5); gamma_h3: iclr17_split_packed_h3(γ_eff packing, 1, N, N). */
 int iclr17_analysis_conv2_gdn_h3(const uint16_t* in_h3, int B, int H, int W, int N,
                                  const uint16_t* w_h3k, const float* bias, const float* beta_eff,
                                  const uint16_t* gamma_h3, float* out, uint16_t* out_h3,

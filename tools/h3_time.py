@@ -64,3 +64,4 @@ for k in sel:
     ms = sorted(a.elapsed_time(b) for a, b in t[k])
     print(f"{k}: median {ms[len(ms) // 2]:.4f} ms, min {ms[0]:.4f}")
 
+

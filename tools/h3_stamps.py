@@ -1,7 +1,7 @@
 """Per-phase cycle counts of the h3 engine's kernels from a stamped diagnostic build (s_memtime
 at kernel entry, end of prologue, end of main loop, end of epilogue pass 0, end; wave 0 of each
-workgroup; build/diag/h3d.hip with STAMP points, exported diag_stamps). Diagnostic tool:
-ICLR17_LIB=<stamped lib> ONLY=<h3_time run> python tools/h3_stamps.py"""
+workgroup; tools/stamp_build.py builds it). Diagnostic tool:
+ICLR17_LIB=build/diag/lib_st.so ONLY=<h3_time runs> python tools/h3_stamps.py"""
 import ctypes
 import os
 import runpy
@@ -26,16 +26,16 @@ for k in os.environ["ONLY"].split(","):
     buf = np.zeros((4096, 16), dtype=np.uint64)
     lib.diag_stamps(ctypes.c_void_p(buf.ctypes.data), ctypes.c_long(buf.nbytes))
     st = buf.astype(np.int64)
-    used = st[:, 10] > 0
+    used = st[:, 8] > 0
     st = st[used]
-    d = np.diff(st[:, :11], axis=1)
-    names = ["prologue", "main", "γ0 stage", "γ0 contract", "out0", "γ1 sync", "γ1 stage", "γ1 contract", "out1"]
-    wall_ns = (st[:, 12] - st[:, 11]) * 10.0   # s_memrealtime: 100 MHz
-    clk = (st[:, 10] - st[:, 0]) / wall_ns
-    t0 = st[:, 11].min()
-    span_us = (st[:, 12].max() - t0) / 100.0
+    d = np.diff(st[:, :9], axis=1)
+    names = ["prologue", "main", "γ0 stage", "γ0 contract", "out0", "sync+γ1 stage", "γ1 contract", "out1"]
+    wall_ns = (st[:, 10] - st[:, 9]) * 10.0   # s_memrealtime: 100 MHz
+    clk = (st[:, 8] - st[:, 0]) / wall_ns
+    t0 = st[:, 9].min()
+    span_us = (st[:, 10].max() - t0) / 100.0
     print(f"{k}: {used.sum()} WGs, span {span_us:.1f} us, WG mean {wall_ns.mean() / 1000:.2f} us, "
           f"clock {np.median(clk):.2f} GHz; cycles per WG (median): " +
           ", ".join(f"{n} {np.median(d[:, i]):.0f}" for i, n in enumerate(names)))
-    starts = np.sort((st[:, 11] - t0) / 100.0)
+    starts = np.sort((st[:, 9] - t0) / 100.0)
     print("   start-time quantiles (us):", np.round(np.quantile(starts, [0, .25, .5, .75, 1]), 1))

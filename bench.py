@@ -353,7 +353,8 @@ def run_train(args, net, x, world, dev):
         data_info["step_crops_per_s"] = round(B * args.steps / elapsed, 1)
     flops = train_flops(args.N, S, S) * B
     tflops = flops / (ms * 1e-3) / 1e12
-    x6t = kernels.precision() in ("x6", "h3")   # training runs the x6 kernels in both
+    x6t = kernels.precision() in ("x6", "h3")   # the backward runs the x6 kernels in both
+    h3t = kernels.precision() == "h3"           # h3: the forward runs the codec's h3 kernels
     tpeak = X6_PEAK_TFLOPS if x6t else FP32_MFMA_PEAK_TFLOPS
     return {
         "metric": "Mpixels/s training (fwd+bwd+Adam), " + METRIC,
@@ -364,14 +365,18 @@ def run_train(args, net, x, world, dev):
         "data": "synthetic (splitmix64 uint8/255 images, seeded trained-like weights)",
         "config": {"workload": f"train step, {B} x {S}x{S}x3 crops per GPU, N={args.N}, lambda=0.01",
                    "N": args.N, "batch_per_gpu": B, "global_batch": B * world,
-                   "precision": ("x6: forward, input gradients, weight gradients and GDN γ "
+                   "precision": ("h3: forward (the codec's kernels, three fp16 part products per "
+                                 "MAC); x6: input gradients, weight gradients and GDN γ gradients "
+                                 "(bias/β/rate-parameter sums and Adam in fp32)" if h3t else
+                                 "x6: forward, input gradients, weight gradients and GDN γ "
                                  "gradients (bias/β/rate-parameter sums and Adam in fp32)"
                                  if x6t else "exact-f32"),
                    "parallelism": f"dp{world} ({'RCCL' if os.environ.get('ICLR17_DIST_BACKEND', 'nccl') == 'nccl' else 'gloo'} "
                                   "bucketed grad all-reduce overlapped with the backward)"},
         "roofline": {"bound": "mfma", "kernel": "whole training step", "achieved": round(tflops, 2),
                      "peak": round(tpeak, 1), "unit": "TFLOP/s",
-                     "peak_basis": ("bf16 dense MFMA peak / 6 (most of the step runs x6)" if x6t
+                     "peak_basis": ("bf16 dense MFMA peak / 6 (most of the step runs x6; the "
+                                    "h3 forward's FLOPs are priced the same)" if x6t
                                     else "fp32 MFMA dense peak"),
                      "frac": round(tflops / tpeak, 4), "traffic": None,
                      "flop_per_step": flops},

@@ -132,14 +132,14 @@ SIGNATURES = {
     "iclr17_h3_planes": (_I, [_P, ctypes.c_long, _P, _P, _P]),
     "iclr17_split_packed_h3_size": (_SZ, [_I, _I, _I]),
     "iclr17_split_packed_h3": (_I, [_P, _I, _I, _I, _P, _P]),
-    "iclr17_analysis_conv1_gdn_h3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
-    "iclr17_analysis_conv2_gdn_h3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_analysis_conv1_gdn_h3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_analysis_conv2_gdn_h3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_analysis_conv3_quant_rate_h3": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P,
                                                  _P, _P, _P, _P]),
     "iclr17_synthesis_deconv3_h3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P, _I,
                                          _P, _P, _D, _P]),
-    "iclr17_synthesis_deconv_igdn_h3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I,
-                                             _I, _P, _P]),
+    "iclr17_synthesis_deconv_igdn_h3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
+                                             _I, _I, _P, _P]),
     # bf16 throughput mode (csrc/engine_bf16.hip)
     "iclr17_bf16_weight_size": (_SZ, [_I, _I]),
     "iclr17_pack_bf16": (_I, [_I, _P, _P, _I, _P]),

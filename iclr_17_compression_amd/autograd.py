@@ -123,9 +123,19 @@ def _split_of(saved: Dict[str, Tensor], key: str) -> Tensor:
 # ------------------------------------------------------------------------------ analysis
 def analysis_features_train(enc, x: Tensor):
     """conv1+GDN1, conv2+GDN2 keeping the pre-activations the backward needs. In the x6 mode the
-    kernels also hand conv2 (and conv3) their input in split form; "a2s" is then set."""
+    kernels also hand conv2 (and conv3) their input in split form; "a2s" is then set. In the h3
+    mode the forward runs the codec's own h3 kernels, which also write the split forms (the x6
+    weight-gradient operands) and the pre-activations; "a2h" (conv3's h3 input) is then set."""
     w1, w2, _, g1, g2 = enc.packed()
     N = enc.out_channel_N
+    if kernels.precision() == "h3":
+        ge1, ge2 = enc.gdn1.effective_params_h3(), enc.gdn2.effective_params_h3()
+        w2h, _ = enc.packed_h3()
+        a1h, _, a1s, u1 = kernels.conv1_gdn_h3(x, enc.packed_conv1_h3(), enc.conv1.bias, *ge1, N,
+                                               want_x6=True, want_pre=True)
+        a2h, _, a2s, u2 = kernels.conv2_gdn_h3(a1h, w2h, enc.conv2.bias, *ge2, want_x6=True,
+                                               want_pre=True)
+        return None, {"x": x, "u1": u1, "u2": u2, "a1s": a1s, "a2s": a2s, "a2h": a2h}
     if kernels.precision() != "fp32":
         e1, e2 = enc.gdn1.effective_params_x6(), enc.gdn2.effective_params_x6()
         a1s, a1, u1 = kernels.conv1x6_gdn(x, enc.packed_conv1_x6(), enc.conv1.bias, e1[0], e1[2],
@@ -196,8 +206,22 @@ def analysis_backward(enc, saved: Dict[str, Tensor], g_y: Tensor,
 
 # ----------------------------------------------------------------------------- synthesis
 def synthesis_forward_train(dec, y_nhwc: Tensor, x_ref: Optional[Tensor] = None,
-                            y_split: Optional[Tensor] = None):
+                            y_split: Optional[Tensor] = None, y_h3: Optional[Tensor] = None):
     d1, d2, d3, q1, q2 = dec.packed()
+    if kernels.precision() == "h3":
+        # the codec's h3 kernels; their x6 outputs are the weight-gradient operands and the
+        # pre-activations the IGDN backward's
+        if y_h3 is None:
+            y_h3 = kernels.h3_planes(y_nhwc)
+        h1, h2 = dec.igdn1.effective_params_h3(), dec.igdn2.effective_params_h3()
+        x1, x2, x3 = dec.packed_h3k()
+        s1h, _, s1s, v1 = kernels.deconv_igdn_h3(y_h3, x1, dec.deconv1.bias, *h1, want_x6=True,
+                                                 want_pre=True)
+        s2h, _, s2s, v2 = kernels.deconv_igdn_h3(s1h, x2, dec.deconv2.bias, *h2, want_x6=True,
+                                                 want_pre=True, chunk_major=True)
+        clipped, recon, sse = kernels.deconv3_h3(s2h, x3, dec.deconv3.bias, x_ref=x_ref,
+                                                 want_recon=True, sse_unclipped=x_ref is not None)
+        return clipped, recon, sse, {"y": y_nhwc, "v1": v1, "v2": v2, "s1s": s1s, "s2s": s2s}
     if kernels.precision() != "fp32":
         if y_split is None:
             y_split = kernels.split_planes(y_nhwc)
@@ -294,13 +318,17 @@ class CodecTrainFn(torch.autograd.Function):
         a2, saved_a = analysis_features_train(enc, x)
         _, _, w3, _, _ = enc.packed()
         rate = be.packed()
-        a2s = saved_a.get("a2s")
-        if a2s is not None:
+        a2s, a2h, y_h3 = saved_a.get("a2s"), saved_a.get("a2h"), None
+        if a2h is not None:   # h3: conv3 + quantiser on the codec's h3 kernel, ỹ also in h3
+            y_tilde, bits_part, _, y_h3 = kernels.conv3_quant_rate_h3(a2h, enc.packed_h3()[1], rate,
+                                                                      noise)
+            y_split = None
+        elif a2s is not None:
             y_tilde, bits_part, _, y_split = kernels.conv3_quant_rate_x6(a2s, w3, rate, noise)
         else:
             (y_tilde, bits_part), y_split = kernels.conv3_quant_rate(a2, w3, rate, noise), None
         clipped, recon, sse_part, saved_s = synthesis_forward_train(dec, y_tilde, x_ref=x,
-                                                                    y_split=y_split)
+                                                                    y_split=y_split, y_h3=y_h3)
         _, bpp = kernels.reduce_partials(bits_part, 1.0 / (B * H * W), per_image=False)
         _, mse = kernels.reduce_partials(sse_part, 1.0 / (B * 3 * H * W), per_image=False)
         ctx.net = net

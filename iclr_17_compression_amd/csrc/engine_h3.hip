@@ -66,9 +66,10 @@ struct HArgs {
                         // + trailer (gamma_scale: [1] = 2⁻¹¹/(σ_a·σ_γ))
   const float* gamma_scale;
   float* out;           // fp32 NHWC [B][Hout][Wout][CO] or null
+  float* pre;           // the GDN / IGDN input x = conv + bias, fp32 NHWC, or null (training)
   u16* out_h3;          // h3 output: NHWC [2][B][Hout][Wout][CO] or chunk-major (out_cm)
   long out_h3_plane;    //   [2][B][CO/32][Hout][Wout][32]
-  u16* out_x6;          // x6 split output (NHWC or chunk-major, 3 planes) or null
+  u16* out_x6;          // x6 split output (NHWC, 3 planes) or null
   long out_x6_plane;
   int out_cm;
   int* range;           // set to 1 when a value does not fit the h3 form (nullable)
@@ -155,7 +156,7 @@ struct HK {
   static constexpr int GBL = 2 * NTH * KB;     // epilogue: γ fragment blocks per pass (1 KB)
   static constexpr int LDS0 = MAIN > GBL * 1024 ? MAIN : GBL * 1024;
   static constexpr int BBOFF = (LDS0 + 1023) / 1024 * 1024;
-  static constexpr int LDS = BBOFF + 2048;     // + bias, β_eff
+  static constexpr int LDS = BBOFF + 2048 + 256;   // + bias, β_eff, the epilogue's sink
   static_assert(SB % 1024 == 0, "weight stage");
   static_assert(NT % 2 == 0 && (C1 || CI % CCH == 0), "tile shape");
   static_assert(LDS <= 160 * 1024, "LDS");
@@ -475,65 +476,89 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
   const float sp = ldexpf(1.0f, ep);
   // n = acc_n · 2⁻¹¹ / (σ_γ · s_p) = acc_n · gamma_scale[1] · σ_a / s_p (powers of two: exact)
   const float nsc = ldexpf(a.gamma_scale[1] * kH3Sa, -ep);
+  // γ staged in four half-passes q = (pass hf, k-half kh) into two alternating 36-KB buffers: the
+  // rows 32·(hf·NTH + il) .. of both planes for k-blocks kh·KH .. kh·KH + KH − 1; block (plane, il,
+  // kk) ← elane (er32, eh) γ_p[32(hf·NTH + il) + er32][16kb + 8eh .. +7] (the [CO/8][CO][8]
+  // packing). Each wave issues GK pieces per stage (sink loads as padding), so vmcnt(GK) leaves
+  // exactly the newer stage in flight. Stage q+1 lands while stage q is contracted.
+  constexpr int KH = KB / 2, HBL = 2 * NTH * KH, GK = (HBL + NW - 1) / NW;
+  static_assert(KB % 2 == 0 && 2 * HBL * 1024 <= KK::LDS0, "γ half-stages");
+  auto stage_g = [&](int q) {
+    const int hf = q >> 1, kh = q & 1;
+#pragma unroll
+    for (int k = 0; k < GK; ++k) {
+      const int blk = k * NW + ewave;
+      if (blk >= HBL) {   // the epilogue's own sink: the main loop's may lie under a γ buffer
+        sink4((unsigned char*)sbb + 2048);
+        continue;
+      }
+      const int p = blk / (NTH * KH), rem = blk - p * NTH * KH;
+      const int il = rem / KH, kb = kh * KH + rem - il * KH;
+      glds16(a.gamma_h3 + (long)p * CO * CO + ((2 * kb + eh) * CO + 32 * (hf * NTH + il) + er32) * 8,
+             smem + (q & 1) * HBL * 1024 + blk * 1024);
+    }
+  };
+  stage_g(0);
+  stage_g(1);
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf) {
-    if (hf) __syncthreads();   // every ewave's pass-0 γ reads done before the restage
     // opaque to the optimiser: pass 1 recomputes the x² planes instead of keeping pass 0's
     // (12 k-blocks × 2 planes × 4 registers) alive across the passes
 #pragma unroll
     for (int i = 0; i < NT; ++i)
 #pragma unroll
       for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(acc[i][j]));
-    // γ rows 32·(hf·NTH + il) .. of the two planes: block (plane, il, kb), elane (er32, eh) ←
-    // γ_p[32(hf·NTH + il) + er32][16kb + 8h .. +7] (the [CO/8][CO][8] packing)
-    for (int blk = ewave; blk < KK::GBL; blk += NW) {
-      const int p = blk / (NTH * KB), rem = blk - p * NTH * KB;
-      const int il = rem / KB, kb = rem - il * KB;
-      glds16(a.gamma_h3 + (long)p * CO * CO + ((2 * kb + eh) * CO + 32 * (hf * NTH + il) + er32) * 8,
-             smem + blk * 1024);
-    }
-    vm_barrier();
     f16v n[NTH];
 #pragma unroll
     for (int il = 0; il < NTH; ++il)
 #pragma unroll
       for (int j = 0; j < 16; ++j) n[il][j] = 0.f;
-    const unsigned char* sg = smem + elane * 16;
 #pragma unroll
-    for (int kb = 0; kb < KB; ++kb) {
-      // x²·s_p of channels 16kb .. 16kb + 15 as the hi / lo B planes: the accumulator rows a elane
-      // holds are 4h + 0..3 and 8 + 4h + 0..3 of the 16-channel block; one permlane32 swap per
-      // register pair and plane hands lanes eh the 8 consecutive channels 8h .. 8h + 7
-      const int i = kb >> 1, r0 = 8 * (kb & 1);
-      unsigned hv[4], lv[4];   // channel pairs (2q, 2q + 1) of the elane's 8, packed fp16
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        typedef float f2 __attribute__((ext_vector_type(2)));
-        const f2 v = f2{acc[i][r0 + 2 * q] * acc[i][r0 + 2 * q], acc[i][r0 + 2 * q + 1] * acc[i][r0 + 2 * q + 1]} * sp;
-        const h2v hh = __builtin_convertvector(v, h2v);
-        const h2v ll = __builtin_convertvector((v - __builtin_convertvector(hh, f2)) * 2048.0f, h2v);
-        hv[q] = __builtin_bit_cast(unsigned, hh);
-        lv[q] = __builtin_bit_cast(unsigned, ll);
+    for (int kh = 0; kh < 2; ++kh) {
+      const int q = 2 * hf + kh;
+      if (q == 0) {
+        wait_vm_barrier<GK>();   // stage 0 landed (stage 1 in flight)
+      } else {
+        vm_barrier();            // stage q landed (and pass 0's stores), every wave done with
+                                 // the buffer stage q+1 refills
+        if (q + 1 < 4 && q >= 1) stage_g(q + 1);
       }
-      u4 xp[2];
+      const unsigned char* sg = smem + (q & 1) * HBL * 1024 + elane * 16;
 #pragma unroll
-      for (int pl = 0; pl < 2; ++pl) {
-        const unsigned* v = pl == 0 ? hv : lv;
-        const unsigned lo0 = v[0], lo1 = v[1];
-        const unsigned hi0 = v[2], hi1 = v[3];
-        const auto s0 = __builtin_amdgcn_permlane32_swap(lo0, hi0, false, false);
-        const auto s1 = __builtin_amdgcn_permlane32_swap(lo1, hi1, false, false);
-        xp[pl] = u4{s0[0], s1[0], s0[1], s1[1]};
-      }
+      for (int kk = 0; kk < KH; ++kk) {
+        const int kb = kh * KH + kk;
+        // x²·s_p of channels 16kb .. 16kb + 15 as the hi / lo B planes: the accumulator rows a
+        // lane holds are 4h + 0..3 and 8 + 4h + 0..3 of the 16-channel block; one permlane32 swap
+        // per register pair and plane hands lane half eh the 8 consecutive channels 8eh .. 8eh + 7
+        const int i = kb >> 1, r0 = 8 * (kb & 1);
+        unsigned hv[4], lv[4];   // channel pairs (2q, 2q + 1) of the lane's 8, packed fp16
 #pragma unroll
-      for (int il = 0; il < NTH; ++il) {
-        const u4 gh = *(lu4p)(sg + ((0 * NTH + il) * KB + kb) * 1024);
-        const u4 gl = *(lu4p)(sg + ((1 * NTH + il) * KB + kb) * 1024);
-        f16v t = mfma32h(gh, xp[1], n[il]);
-        t = mfma32h(gl, xp[0], t);
-        n[il] = mfma32h(h3_x2048(gh), xp[0], t);
+        for (int qq = 0; qq < 4; ++qq) {
+          typedef float f2 __attribute__((ext_vector_type(2)));
+          const f2 v = f2{acc[i][r0 + 2 * qq] * acc[i][r0 + 2 * qq], acc[i][r0 + 2 * qq + 1] * acc[i][r0 + 2 * qq + 1]} * sp;
+          const h2v hh = __builtin_convertvector(v, h2v);
+          const h2v ll = __builtin_convertvector((v - __builtin_convertvector(hh, f2)) * 2048.0f, h2v);
+          hv[qq] = __builtin_bit_cast(unsigned, hh);
+          lv[qq] = __builtin_bit_cast(unsigned, ll);
+        }
+        u4 xp[2];
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl) {
+          const unsigned* v = pl == 0 ? hv : lv;
+          const auto s0 = __builtin_amdgcn_permlane32_swap(v[0], v[2], false, false);
+          const auto s1 = __builtin_amdgcn_permlane32_swap(v[1], v[3], false, false);
+          xp[pl] = u4{s0[0], s1[0], s0[1], s1[1]};
+        }
+#pragma unroll
+        for (int il = 0; il < NTH; ++il) {
+          const u4 gh = *(lu4p)(sg + ((0 * NTH + il) * KH + kk) * 1024);
+          const u4 gl = *(lu4p)(sg + ((1 * NTH + il) * KH + kk) * 1024);
+          f16v t = mfma32h(gh, xp[1], n[il]);
+          t = mfma32h(gl, xp[0], t);
+          n[il] = mfma32h(h3_x2048(gh), xp[0], t);
+        }
+        __builtin_amdgcn_sched_barrier(0);   // one k-block's operands live at a time
       }
-      __builtin_amdgcn_sched_barrier(0);   // one k-block's operands live at a time
     }
 #pragma unroll
     for (int il = 0; il < NTH; ++il)
@@ -547,6 +572,8 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const int ch = 32 * i + 8 * m + 4 * eh;
+        if (inside && a.pre)
+          *(f4*)(a.pre + o * CO + ch) = f4{acc[i][4 * m], acc[i][4 * m + 1], acc[i][4 * m + 2], acc[i][4 * m + 3]};
         const f4 be = *(const f4*)(sbb + 256 + ch);
         // the hardware square root / reciprocal square root (v_sqrt_f32, v_rsq_f32: within an ulp
         // or two, far inside the h3 form's own 2⁻²² — and a sixth of the IEEE sequences' VALU
@@ -599,8 +626,7 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
             mb[j] = __float_as_uint(r) & 0xffff0000u;
             lb[j] = __float_as_uint(r - __uint_as_float(mb[j]));
           }
-          const long so = a.out_cm ? (((long)b * (CO / 32) + i) * a.Hout + oy) * a.Wout * 32 + (long)ox * 32 + 8 * m + 4 * eh
-                                   : o * CO + 32 * i + 8 * m + 4 * eh;
+          const long so = o * CO + 32 * i + 8 * m + 4 * eh;
           *(uint2*)(a.out_x6 + so) = uint2{__builtin_amdgcn_perm(hb[1], hb[0], 0x07060302u),
                                            __builtin_amdgcn_perm(hb[3], hb[2], 0x07060302u)};
           *(uint2*)(a.out_x6 + a.out_x6_plane + so) = uint2{__builtin_amdgcn_perm(mb[1], mb[0], 0x07060302u),
@@ -914,10 +940,11 @@ int iclr17_h3_planes(const float* x, long n, uint16_t* planes, int* range_flag, 
 
 int iclr17_analysis_conv1_gdn_h3(const float* x, int B, int H, int W, int N,
                                  const uint16_t* w_h3k, const float* bias, const float* beta_eff,
-                                 const uint16_t* gamma_h3, float* out, uint16_t* out_h3,
-                                 int* range_flag, void* stream) {
+                                 const uint16_t* gamma_h3, float* out, float* pre_out,
+                                 uint16_t* out_h3, uint16_t* out_x6, int* range_flag,
+                                 void* stream) {
   ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "conv1_gdn_h3: N=%d", N);
-  ICLR17_REQUIRE(x && w_h3k && bias && beta_eff && gamma_h3 && (out || out_h3) && B > 0 &&
+  ICLR17_REQUIRE(x && w_h3k && bias && beta_eff && gamma_h3 && (out || out_h3 || out_x6) && B > 0 &&
                      H > 0 && W > 0 && H % 16 == 0 && W % 16 == 0,
                  ICLR17_EINVAL, "conv1_gdn_h3: bad arguments");
   HArgs a;
@@ -929,7 +956,9 @@ int iclr17_analysis_conv1_gdn_h3(const float* x, int B, int H, int W, int N,
   a.bias = bias; a.beta = beta_eff; a.gamma_h3 = gamma_h3;
   a.gamma_scale = (const float*)(gamma_h3 + 2L * N * N);
   a.out = out;
+  a.pre = pre_out;
   a.out_h3 = out_h3; a.out_h3_plane = (long)B * (H / 4) * (W / 4) * N;
+  a.out_x6 = out_x6; a.out_x6_plane = a.out_h3_plane;
   a.range = range_flag;
   a.B = B; a.Hin = H; a.Win = W; a.Hout = H / 4; a.Wout = W / 4;
   a.gh = H / 4; a.gw = W / 4;
@@ -948,8 +977,9 @@ int iclr17_analysis_conv1_gdn_h3(const float* x, int B, int H, int W, int N,
 
 int iclr17_analysis_conv2_gdn_h3(const uint16_t* in_h3, int B, int H, int W, int N,
                                  const uint16_t* w_h3k, const float* bias, const float* beta_eff,
-                                 const uint16_t* gamma_h3, float* out, uint16_t* out_h3,
-                                 uint16_t* out_x6, int* range_flag, void* stream) {
+                                 const uint16_t* gamma_h3, float* out, float* pre_out,
+                                 uint16_t* out_h3, uint16_t* out_x6, int* range_flag,
+                                 void* stream) {
   ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "conv2_gdn_h3: N=%d", N);
   ICLR17_REQUIRE(in_h3 && w_h3k && bias && beta_eff && gamma_h3 && (out || out_h3 || out_x6) &&
                      B > 0 && H > 0 && W > 0 && H % 16 == 0 && W % 16 == 0,
@@ -964,6 +994,7 @@ int iclr17_analysis_conv2_gdn_h3(const uint16_t* in_h3, int B, int H, int W, int
   a.bias = bias; a.beta = beta_eff; a.gamma_h3 = gamma_h3;
   a.gamma_scale = (const float*)(gamma_h3 + 2L * N * N);
   a.out = out;
+  a.pre = pre_out;
   a.out_h3 = out_h3; a.out_h3_plane = (long)B * (h / 2) * (w / 2) * N;
   a.out_x6 = out_x6; a.out_x6_plane = a.out_h3_plane;
   a.range = range_flag;
@@ -985,7 +1016,8 @@ int iclr17_analysis_conv2_gdn_h3(const uint16_t* in_h3, int B, int H, int W, int
 int iclr17_synthesis_deconv_igdn_h3(const uint16_t* in_h3, int B, int h, int w, int N,
                                     const uint16_t* w_h3k, const float* bias,
                                     const float* beta_eff, const uint16_t* gamma_h3,
-                                    float* out, uint16_t* out_h3, uint16_t* out_x6, int out_cm,
+                                    float* out, float* pre_out, uint16_t* out_h3, uint16_t* out_x6,
+                                    int out_cm,
                                     int int_in, int* range_flag, void* stream) {
   ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "deconv_igdn_h3: N=%d", N);
   ICLR17_REQUIRE(in_h3 && w_h3k && bias && beta_eff && gamma_h3 && (out || out_h3 || out_x6) &&
@@ -1000,6 +1032,7 @@ int iclr17_synthesis_deconv_igdn_h3(const uint16_t* in_h3, int B, int h, int w, 
   a.bias = bias; a.beta = beta_eff; a.gamma_h3 = gamma_h3;
   a.gamma_scale = (const float*)(gamma_h3 + 2L * N * N);
   a.out = out;
+  a.pre = pre_out;
   a.out_h3 = out_h3; a.out_h3_plane = (long)B * 4 * h * w * N;
   a.out_x6 = out_x6; a.out_x6_plane = (long)B * 4 * h * w * N;
   a.out_cm = out_cm ? 1 : 0;

@@ -525,10 +525,12 @@ def pack_conv1_h3(w: Tensor, N: int) -> Tensor:
 
 
 def conv1_gdn_h3(x: Tensor, w_h3: Tensor, bias: Tensor, beta_eff: Tensor, gh3: Tensor, N: int,
-                 want_f32: bool = False):
+                 want_f32: bool = False, want_h3: bool = True, want_x6: bool = False,
+                 want_pre: bool = False):
     """analysis_17.py:14-17 conv1 + GDN1 in the h3 form on the h3 engine (three f16 part products
     per MAC for the convolution and the GDN contraction; w_h3: ``pack_conv1_h3``, gh3:
-    GDN.effective_params_h3's γ). Returns (h3 [2,B,H/4,W/4,N], fp32 | None)."""
+    GDN.effective_params_h3's γ). Returns (h3 [2,B,H/4,W/4,N] | None, fp32 | None), and with
+    ``want_x6`` / ``want_pre`` (training) also (x6 split | None, GDN1 input conv1 + bias | None)."""
     _check(x, "image", 4)
     B, C, H, W = x.shape
     if C != 3:
@@ -539,19 +541,27 @@ def conv1_gdn_h3(x: Tensor, w_h3: Tensor, bias: Tensor, beta_eff: Tensor, gh3: T
         raise Iclr17Error("iclr17: conv1_gdn_h3 needs pack_conv1_h3 weights")
     if gh3.dtype != torch.int16 or gh3.numel() != query("iclr17_split_packed_h3_size", 1, N, N):
         raise Iclr17Error("iclr17: conv1_gdn_h3 needs γ in the h3 form (effective_params_h3)")
+    if not (want_h3 or want_f32 or want_x6):
+        raise Iclr17Error("iclr17: conv1_gdn_h3 needs an output")
     x = x.contiguous()
-    h3 = torch.empty(2, B, H // 4, W // 4, N, device=x.device, dtype=torch.int16)
+    h3 = torch.empty(2, B, H // 4, W // 4, N, device=x.device, dtype=torch.int16) if want_h3 else None
+    x6 = torch.empty(3, B, H // 4, W // 4, N, device=x.device, dtype=torch.int16) if want_x6 else None
     out = torch.empty(B, H // 4, W // 4, N, device=x.device) if want_f32 else None
+    pre = torch.empty(B, H // 4, W // 4, N, device=x.device) if want_pre else None
     call("iclr17_analysis_conv1_gdn_h3", _p(x), B, H, W, N, _p(w_h3), _p(bias), _p(beta_eff),
-         _p(gh3), _p(out), _p(h3), _p(h3_range_flag(x.device)), _stream(x))
+         _p(gh3), _p(out), _p(pre), _p(h3), _p(x6), _p(h3_range_flag(x.device)), _stream(x))
+    if want_x6 or want_pre:
+        return h3, out, x6, pre
     return h3, out
 
 
 def conv2_gdn_h3(hs: Tensor, wk: Tensor, bias: Tensor, beta_eff: Tensor, gh3: Tensor,
-                 want_h3: bool = True, want_f32: bool = False, want_x6: bool = False):
+                 want_h3: bool = True, want_f32: bool = False, want_x6: bool = False,
+                 want_pre: bool = False):
     """analysis_17.py:18-21 conv2 + GDN2 in the h3 form on the h3 engine (csrc/engine_h3.hip):
     h3 input [2,B,H/4,W/4,N] → (h3 | None, fp32 | None, x6 split | None). wk:
-    ``pack_h3k(ICLR17_H3K_CONV5, w)``; gh3: GDN.effective_params_h3's γ."""
+    ``pack_h3k(ICLR17_H3K_CONV5, w)``; gh3: GDN.effective_params_h3's γ. With ``want_pre``
+    (training) a fourth result: GDN2's input conv2 + bias (fp32 NHWC)."""
     _check_h3(hs, "activation")
     _, B, h4, w4, N = hs.shape
     _check_channels(N)
@@ -566,8 +576,11 @@ def conv2_gdn_h3(hs: Tensor, wk: Tensor, bias: Tensor, beta_eff: Tensor, gh3: Te
     h3 = torch.empty(2, B, h4 // 2, w4 // 2, N, device=hs.device, dtype=torch.int16) if want_h3 else None
     x6 = torch.empty(3, B, h4 // 2, w4 // 2, N, device=hs.device, dtype=torch.int16) if want_x6 else None
     out = torch.empty(B, h4 // 2, w4 // 2, N, device=hs.device) if want_f32 else None
+    pre = torch.empty(B, h4 // 2, w4 // 2, N, device=hs.device) if want_pre else None
     call("iclr17_analysis_conv2_gdn_h3", _p(hs), B, H, W, N, _p(wk), _p(bias), _p(beta_eff), _p(gh3),
-         _p(out), _p(h3), _p(x6), _p(h3_range_flag(hs.device)), _stream(hs))
+         _p(out), _p(pre), _p(h3), _p(x6), _p(h3_range_flag(hs.device)), _stream(hs))
+    if want_pre:
+        return h3, out, x6, pre
     return h3, out, x6
 
 
@@ -603,12 +616,13 @@ def conv3_quant_rate_h3(hs: Tensor, wh: Tensor, rate_packed: Tensor,
 
 def deconv_igdn_h3(hs: Tensor, wh: Tensor, bias: Tensor, beta_eff: Tensor, gh3: Tensor,
                    want_h3: bool = True, want_f32: bool = False, want_x6: bool = False,
-                   chunk_major: bool = False, int_in: bool = False):
+                   chunk_major: bool = False, int_in: bool = False, want_pre: bool = False):
     """synthesis_17.py:15-22 in the h3 form (csrc/engine_h3.hip): h3 input [2,B,h,w,N] →
     (h3 | None, fp32 | None, x6 split | None). wh: ``pack_h3k(ICLR17_H3K_DECONV5, …)``; gh3: the
     IGDN's γ in the h3 form (GDN.effective_params_h3). ``int_in``: the input is ŷ (a workgroup
     whose window has a zero lo plane skips the lo products; same result). ``chunk_major`` applies
-    to the h3 and x6 outputs."""
+    to the h3 output (the x6 output is NHWC). With ``want_pre`` (training) a fourth result: the
+    IGDN input deconv + bias (fp32 NHWC)."""
     _check_h3(hs, "activation")
     _, B, hh, ww, N = hs.shape
     _check_channels(N)
@@ -621,11 +635,14 @@ def deconv_igdn_h3(hs: Tensor, wh: Tensor, bias: Tensor, beta_eff: Tensor, gh3: 
     def shape(P):
         return (P, B, N // 32, 2 * hh, 2 * ww, 32) if chunk_major else (P, B, 2 * hh, 2 * ww, N)
     h3 = torch.empty(shape(2), device=hs.device, dtype=torch.int16) if want_h3 else None
-    x6 = torch.empty(shape(3), device=hs.device, dtype=torch.int16) if want_x6 else None
+    x6 = torch.empty(3, B, 2 * hh, 2 * ww, N, device=hs.device, dtype=torch.int16) if want_x6 else None
     out = torch.empty(B, 2 * hh, 2 * ww, N, device=hs.device) if want_f32 else None
+    pre = torch.empty(B, 2 * hh, 2 * ww, N, device=hs.device) if want_pre else None
     call("iclr17_synthesis_deconv_igdn_h3", _p(hs), B, hh, ww, N, _p(wh), _p(bias),
-         _p(beta_eff), _p(gh3), _p(out), _p(h3), _p(x6), int(chunk_major), int(int_in),
+         _p(beta_eff), _p(gh3), _p(out), _p(pre), _p(h3), _p(x6), int(chunk_major), int(int_in),
          _p(h3_range_flag(hs.device)), _stream(hs))
+    if want_pre:
+        return h3, out, x6, pre
     return h3, out, x6
 
 

@@ -271,18 +271,14 @@ class ImageCompressor(nn.Module):
             self.Encoder.packed()
             self.Decoder.packed()
             self.bitEstimator.packed()
+            h3 = kernels.precision() == "h3"
             if x6:
-                self.Encoder.packed_conv1_x6()
-                self.Encoder.packed_w3_split()
-                self.Decoder.packed_x6()
-                if not backward and kernels.precision() == "h3":
-                    self.Decoder.packed_h3k()
-                    self.Encoder.packed_h3()
-                    self.Encoder.packed_conv1_h3()
+                if not (h3 and backward):   # the x6 forward's (an h3 training step has none)
+                    self.Encoder.packed_conv1_x6()
+                    self.Encoder.packed_w3_split()
+                    self.Decoder.packed_x6()
                     for g in gdns:
-                        g.effective_params_h3()
-                for g in gdns:
-                    g.effective_params_x6()
+                        g.effective_params_x6()
             if backward:
                 self.Encoder.packed_bwd()
                 self.Decoder.packed_bwd(x6)
@@ -291,6 +287,14 @@ class ImageCompressor(nn.Module):
                         g.effective_params_bwd_x6()
                     else:
                         g.effective_params_bwd()
+        if h3:
+            # the h3 layouts (the codec's, and the training forward's in this mode) split the
+            # packs above, which the batch writes only at its exit
+            self.Decoder.packed_h3k()
+            self.Encoder.packed_h3()
+            self.Encoder.packed_conv1_h3()
+            for g in gdns:
+                g.effective_params_h3()
         if not backward:   # eval: the rate table of the round quantiser (+ the bf16 layouts)
             self.bitEstimator.rate_table()
             if kernels.precision() == "bf16":

@@ -128,14 +128,19 @@ class Analysis_net_17(nn.Module):
     def y_nhwc(self, x, feats=None):
         """y (NHWC) through the codec's analysis kernels. ``feats``: the training forward's
         conv2+GDN2 output (autograd.analysis_features_train), reused for conv3 where it is the
-        codec's own operand (x6: its split form; fp32: the fp32 activation). In the h3 and bf16
-        modes the codec's own chain runs again (its y is what the codec rounds; the gradient is
-        the training kernels' x6 one, the same function to fp32 rounding)."""
+        codec's own operand (x6: its split form; fp32: the fp32 activation; h3: its h3 form — the
+        training forward runs the codec's h3 kernels). In the bf16 mode the codec's own chain runs
+        again (its y is what the codec rounds) while the gradient is the training kernels' x6
+        one, a different function at bf16 precision (≈0.3 % of the rounded latents, §3 of
+        DESIGN.md)."""
         N = self.out_channel_N
         w1, w2, w3, g1, g2 = self.packed()
         # the rate epilogue needs a model: a zero one (its bits are discarded, y is all we keep)
         z = torch.zeros(11 * N, device=x.device)
         ztab = torch.zeros(N, 65, device=x.device)
+        if feats is not None and kernels.precision() == "h3" and feats.get("a2h") is not None:
+            return kernels.conv3_quant_rate_h3(feats["a2h"], self.packed_h3()[1], z, want_y=True,
+                                               rtab=ztab, want_h3=False)[2]
         if feats is not None and kernels.precision() == "x6" and feats.get("a2s") is not None:
             return kernels.conv3_quant_rate_x6(feats["a2s"], w3, z, want_y=True, rtab=ztab,
                                                w_split=self.packed_w3_split())[2]

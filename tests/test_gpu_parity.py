@@ -677,7 +677,7 @@ def test_h3_deconv_igdn(device, N, hw):
                                                   chunk_major=True)
             assert scm.shape == (2, 2, N // 32, 2 * h, 2 * w, 32)
             assert torch.equal(scm.permute(0, 1, 3, 4, 2, 5).reshape(s.shape), s)
-            assert torch.equal(s6cm.permute(0, 1, 3, 4, 2, 5).reshape(s6.shape), s6)
+            assert torch.equal(s6cm, s6)   # the x6 output stays NHWC
             _, f_old, _ = kernels.deconv_igdn_x6(kernels.split_planes(nhwc(inp).contiguous().to(device)),
                                                  wp, bias, *q, want_f32=True)
             assert rel_err(f, f_old) < 2e-6, lay

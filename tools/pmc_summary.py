@@ -42,6 +42,14 @@ LAYER_KERNELS = {
         "deconv2_igdn2": (r"engine_kernel<192, 192, 192, 1, 4, 1, true", 1),
         "deconv3_clamp": (r"deconv3_x6_kernel<192>", None),
     },
+    "h3": {
+        "conv1_gdn1": (r"h3k_kernel<3, 16, 192, 3, 0, false>", None),
+        "conv2_gdn2": (r"h3k_kernel<2, 16, 192, 192, 0, false>", None),
+        "conv3_quant_rate": (r"engine_kernel<192, 192, 96, 2, 2, 2, false, true, true>", None),
+        "deconv1_igdn1": (r"h3k_kernel<1, 16, 192, 192, 1, true>", None),
+        "deconv2_igdn2": (r"h3k_kernel<1, 16, 192, 192, 1, false>", None),
+        "deconv3_clamp": (r"deconv3_x6_kernel<192, true>", None),
+    },
     "bf16": {
         "conv1_gdn1": (r"conv1p_bf16_kernel<192, true>", None),
         "conv2_gdn2": (r"k5_bf16_kernel<0, 16, 192, 192, 192, 0>", None),

@@ -615,7 +615,10 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
           *(u4*)(a.out_h3 + a.out_h3_plane + so + 8) = sv[1][1];
         }
       }
-      if (inside && a.out_x6) {
+      if (a.out_x6) {
+        // the x6 split (training's weight-gradient operand), stored like the h3 output: 16 bytes
+        // per lane and plane after the same permlane32 swaps
+        uint2 xp[3][4];
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
           unsigned hb[4], mb[4], lb[4];
@@ -626,13 +629,26 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
             mb[j] = __float_as_uint(r) & 0xffff0000u;
             lb[j] = __float_as_uint(r - __uint_as_float(mb[j]));
           }
-          const long so = o * CO + 32 * i + 8 * m + 4 * eh;
-          *(uint2*)(a.out_x6 + so) = uint2{__builtin_amdgcn_perm(hb[1], hb[0], 0x07060302u),
-                                           __builtin_amdgcn_perm(hb[3], hb[2], 0x07060302u)};
-          *(uint2*)(a.out_x6 + a.out_x6_plane + so) = uint2{__builtin_amdgcn_perm(mb[1], mb[0], 0x07060302u),
-                                                            __builtin_amdgcn_perm(mb[3], mb[2], 0x07060302u)};
-          *(uint2*)(a.out_x6 + 2 * a.out_x6_plane + so) = uint2{__builtin_amdgcn_perm(lb[1], lb[0], 0x07060302u),
-                                                                __builtin_amdgcn_perm(lb[3], lb[2], 0x07060302u)};
+          xp[0][m] = uint2{__builtin_amdgcn_perm(hb[1], hb[0], 0x07060302u), __builtin_amdgcn_perm(hb[3], hb[2], 0x07060302u)};
+          xp[1][m] = uint2{__builtin_amdgcn_perm(mb[1], mb[0], 0x07060302u), __builtin_amdgcn_perm(mb[3], mb[2], 0x07060302u)};
+          xp[2][m] = uint2{__builtin_amdgcn_perm(lb[1], lb[0], 0x07060302u), __builtin_amdgcn_perm(lb[3], lb[2], 0x07060302u)};
+        }
+        u4 sv6[3][2];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const auto sx = __builtin_amdgcn_permlane32_swap(xp[pl][k].x, xp[pl][k + 2].x, false, false);
+            const auto sy = __builtin_amdgcn_permlane32_swap(xp[pl][k].y, xp[pl][k + 2].y, false, false);
+            sv6[pl][k] = u4{sx[0], sy[0], sx[1], sy[1]};
+          }
+        if (inside) {
+          const long so = o * CO + 32 * i + 16 * eh;
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl) {
+            *(u4*)(a.out_x6 + pl * a.out_x6_plane + so) = sv6[pl][0];
+            *(u4*)(a.out_x6 + pl * a.out_x6_plane + so + 8) = sv6[pl][1];
+          }
         }
       }
     }
@@ -701,21 +717,25 @@ __global__ void __launch_bounds__(TH / 2 * 64, 1) h3k_kernel(const HArgs a) {
 }
 
 // ---------------------------------------------------------------------------- packing
-// max|w| over the tensor (one workgroup; the weights are ≤ 1 M values): trailer[0]
-__global__ void __launch_bounds__(1024) absmax_kernel(const float* __restrict__ w, long n,
-                                                      float* __restrict__ trailer) {
-  __shared__ float red[16];
+// max|w| over the tensor into trailer[0] (zeroed by the caller): a grid-stride reduction, one
+// vector atomicMax per wave on the bits of the non-negative float (ordered like the values). One
+// workgroup took 69 µs for conv2's 0.9 M weights, ten of them per training step.
+__global__ void __launch_bounds__(256) absmax_kernel(const float* __restrict__ w, long n,
+                                                     float* __restrict__ trailer) {
   float m = 0.f;
-  for (long i = threadIdx.x; i < n; i += 1024) m = fmaxf(m, fabsf(w[i]));
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    m = fmaxf(m, fabsf(w[i]));
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float r = red[0];
-    for (int i = 1; i < 16; ++i) r = fmaxf(r, red[i]);
-    trailer[0] = r;
-  }
+  if ((threadIdx.x & 63) == 0) atomicMax((unsigned*)trailer, __float_as_uint(m));
+}
+
+static int launch_absmax(const float* w, long n, float* trailer, hipStream_t st) {
+  if (hipMemsetAsync(trailer, 0, sizeof(float), st) != hipSuccess) return check_launch("absmax memset");
+  const long blocks = (n + 4095) / 4096;
+  hipLaunchKernelGGL(absmax_kernel, dim3((unsigned)(blocks < 1024 ? (blocks > 0 ? blocks : 1) : 1024)),
+                     dim3(256), 0, st, w, n, trailer);
+  return check_launch("absmax");
 }
 
 // σ_w = 2^(3 − ⌊log2 max|w|⌋) (max|w|·σ_w ∈ [8, 16), so hi·2¹¹ < 2¹⁵); 1 for an all-zero or
@@ -897,8 +917,7 @@ int iclr17_pack_h3k(int which, const float* w, uint16_t* out, int N, void* strea
   float* trailer = (float*)(out + (total - 8));
   hipStream_t st = (hipStream_t)stream;
   const long nw = which == ICLR17_H3K_CONV1 ? (long)N * 3 * 81 : (long)N * N * 25;
-  hipLaunchKernelGGL(absmax_kernel, dim3(1), dim3(1024), 0, st, w, nw, trailer);
-  int rc = check_launch("pack_h3k absmax");
+  int rc = launch_absmax(w, nw, trailer, st);
   if (rc) return rc;
   const int blocks = (int)((groups + 255) / 256 < 4096 ? (groups + 255) / 256 : 4096);
   hipLaunchKernelGGL(pack_h3k_kernel, dim3(blocks), dim3(256), 0, st, w, N,
@@ -919,8 +938,7 @@ int iclr17_split_packed_h3(const float* packed, int taps, int K, int N, uint16_t
   const long groups = (long)taps * (K / 8) * N;
   float* trailer = (float*)(planes + (total - 8));
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(absmax_kernel, dim3(1), dim3(1024), 0, st, packed, (long)taps * K * N, trailer);
-  int rc = check_launch("split_packed_h3 absmax");
+  int rc = launch_absmax(packed, (long)taps * K * N, trailer, st);
   if (rc) return rc;
   const int blocks = (int)((groups + 255) / 256 < 4096 ? (groups + 255) / 256 : 4096);
   hipLaunchKernelGGL(split_packed_h3_kernel, dim3(blocks), dim3(256), 0, st, packed, K, N, groups,

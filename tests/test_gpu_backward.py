@@ -31,9 +31,10 @@ def make(N, seed, device):
     return net.to(device).train(), oracle.state_dict_to_torch(sd)
 
 
-@pytest.fixture(params=["x6", "fp32"])
+@pytest.fixture(params=["h3", "x6", "fp32"])
 def precision(request):
-    """x6: the input-gradient contractions run in x6 on split-form gradients; fp32: exact f32."""
+    """x6: the input-gradient contractions run in x6 on split-form gradients; h3: the same
+    backward after the forward on the codec's h3 kernels; fp32: exact f32."""
     from iclr_17_compression_amd import kernels
     old = kernels.precision()
     kernels.set_precision(request.param)
@@ -307,3 +308,39 @@ def test_eval_mode_autograd(device):
             assert p.grad is None and (ref is None or ref.abs().max() == 0), k
             continue
         assert grad_err(p.grad, ref) < GRAD_REL, (k, grad_err(p.grad, ref))
+
+
+def test_h3_training_forward_saved_tensors(device):
+    """The h3 training forward (the codec's h3 kernels with their pre-activation and x6 split
+    outputs) hands the backward the x6 forward's tensors to the h3 form's accuracy, at a size with
+    partial tiles (B=2, 48×80: conv2's 12×20 output, deconv1's 3×5 input)."""
+    from iclr_17_compression_amd import autograd, kernels
+    N = 192
+    net, _ = make(N, 3, device)
+    x = torch.from_numpy(synth.to_unit_float(synth.image_u8(7, 2, 48, 80))).to(device)
+    enc, dec = net.Encoder, net.Decoder
+    old = kernels.precision()
+    try:
+        with torch.no_grad():
+            kernels.set_precision("x6")
+            _, sx = autograd.analysis_features_train(enc, x)
+            y = kernels.conv3_quant_rate_x6(sx["a2s"], enc.packed()[2], net.bitEstimator.packed())[0]
+            _, rx, ssex, tx = autograd.synthesis_forward_train(dec, y, x_ref=x)
+            kernels.set_precision("h3")
+            _, sh = autograd.analysis_features_train(enc, x)
+            _, rh, sseh, th = autograd.synthesis_forward_train(dec, y, x_ref=x)
+    finally:
+        kernels.set_precision(old)
+    rel = lambda a, b: ((a - b).abs().max() / b.abs().max()).item()  # noqa: E731
+    for k in ("u1", "u2"):
+        assert rel(sh[k], sx[k]) < 5e-6, k
+    for k in ("a1s", "a2s"):
+        assert rel(kernels.merge_planes(sh[k]), kernels.merge_planes(sx[k])) < 5e-6, k
+    assert torch.equal(kernels.merge_h3(sh["a2h"]), kernels.merge_h3(kernels.h3_planes(
+        kernels.merge_planes(sh["a2s"]))))
+    for k in ("v1", "v2"):
+        assert rel(th[k], tx[k]) < 5e-6, k
+    for k in ("s1s", "s2s"):
+        assert rel(kernels.merge_planes(th[k]), kernels.merge_planes(tx[k])) < 5e-6, k
+    assert rel(rh, rx) < 5e-6
+    assert abs(sseh.double().sum().item() - ssex.double().sum().item()) <= 1e-5 * ssex.double().sum().item()

@@ -29,7 +29,7 @@ for k in os.environ["ONLY"].split(","):
     used = st[:, 8] > 0
     st = st[used]
     d = np.diff(st[:, :9], axis=1)
-    names = ["prologue", "main", "γ0 stage", "γ0 contract", "out0", "sync+γ1 stage", "γ1 contract", "out1"]
+    names = ["prologue", "main", "γ wait", "contract0", "out0", "γ2 wait", "contract1", "out1"]
     wall_ns = (st[:, 10] - st[:, 9]) * 10.0   # s_memrealtime: 100 MHz
     clk = (st[:, 8] - st[:, 0]) / wall_ns
     t0 = st[:, 9].min()

@@ -1,7 +1,8 @@
 """Builds build/diag/lib_st.so: the library with a stamped copy of csrc/engine_h3.hip (s_memtime at
-kernel entry, end of prologue, end of main loop, γ staged / contracted / outputs of each epilogue
-pass; wave 0 of each workgroup into a device array read back by diag_stamps) for
-tools/h3_stamps.py. Diagnostic build only: the product library carries no stamps."""
+kernel entry, end of prologue, end of main loop, γ stage 0 landed, pass-0 contraction done, pass-0
+outputs done, γ stage 2 landed, pass-1 contraction done, end; wave 0 of each workgroup into a
+device array read back by diag_stamps) for tools/h3_stamps.py. Diagnostic build only: the product
+library carries no stamps."""
 import os
 import subprocess
 
@@ -30,13 +31,15 @@ rep('''  Frag cur;
 rep('''  vm_barrier();   // trailing sink loads landed; every wave is done with the stages''',
     '''  vm_barrier();   // trailing sink loads landed; every wave is done with the stages
   STAMP(2);''')
-rep('''    if (hf) __syncthreads();   // every ewave's pass-0 γ reads done before the restage''',
-    '''    if (hf) STAMP(5);
-    if (hf) __syncthreads();   // every ewave's pass-0 γ reads done before the restage''')
-rep('''    vm_barrier();
-    f16v n[NTH];''', '''    vm_barrier();
-    STAMP(3 + 3 * hf);
-    f16v n[NTH];''')
+rep('''  for (int hf = 0; hf < 2; ++hf) {
+    // opaque to the optimiser''', '''  for (int hf = 0; hf < 2; ++hf) {
+    if (hf) STAMP(5);
+    // opaque to the optimiser''')
+rep('''        wait_vm_barrier<GK>();   // stage 0 landed (stage 1 in flight)''',
+    '''        wait_vm_barrier<GK>();   // stage 0 landed (stage 1 in flight)
+        STAMP(3);''')
+rep('''        if (q + 1 < 4 && q >= 1) stage_g(q + 1);''', '''        if (q + 1 < 4 && q >= 1) stage_g(q + 1);
+        if (q == 2) STAMP(6);''')
 rep('''      for (int j = 0; j < 16; ++j) n[il][j] = n[il][j] * nsc;''',
     '''      for (int j = 0; j < 16; ++j) n[il][j] = n[il][j] * nsc;
     STAMP(4 + 3 * hf);''')

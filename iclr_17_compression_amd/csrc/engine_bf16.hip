@@ -87,14 +87,18 @@ __global__ void __launch_bounds__(256) rate_table_kernel(const float* __restrict
 }
 
 // ---------------------------------------------------------------- x² / output tile layout
-// [R pixels][CO] bf16 rows of stride CO·2 + 32 bytes: 16-lane fragment reads hit distinct banks
+// [R pixels][CO] bf16 rows of stride CO·2 + 16 bytes (≡ 4 dwords mod 64 banks at N = 128 and
+// 192): the 16-byte fragment reads of 16 consecutive pixels hit 16 distinct 4-bank slots, and
+// the 8-byte writes of 16 pixels are at most 2-way (CO·2 + 32 had 2-way reads, 4-way writes:
+// 34 % of conv1p's LDS cycles were conflicts, profiles/r05_bf16_traffic.json)
+constexpr int kEpiPad = 16;
 template <int CO>
 __device__ __forceinline__ int epi_off(int p, int ch) {   // byte offset of (pixel, channel)
-  return p * (CO * 2 + 32) + ch * 2;
+  return p * (CO * 2 + kEpiPad) + ch * 2;
 }
 
 template <int CO>
-constexpr int epi_tile_bytes(int R) { return R * (CO * 2 + 32); }
+constexpr int epi_tile_bytes(int R) { return R * (CO * 2 + kEpiPad); }
 
 // ------------------------------------------------------------------------------ kernel
 // One workgroup: a TH × 16 tile of base pixels (conv: output pixels; deconv: input pixels of

@@ -2575,7 +2575,15 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
     constexpr int WN = (BN / 16) % 4 == 0 ? 4 : 2, WM = 4 / WN;
     a.partials_per_image = a.tiles_x * a.tiles_y * (N / BN);
     dim3 grid(a.tiles_x * a.tiles_y * B, N / BN);
-    if (H3in) {   // the h3 form (round and noise mode alike on the BN-column tiles)
+    if (H3in) {   // the h3 form: BN-column tiles, or the narrow ones under conv3_narrow
+      if constexpr (N == 192) {
+        if (conv3_narrow(N, a.tiles_x * a.tiles_y, B, qmode)) {
+          a.partials_per_image = a.tiles_x * a.tiles_y * (N / 48);
+          hipLaunchKernelGGL((engine_kernel<N, N, 48, 4, 1, EPI_QUANT, false, true, true>),
+                             dim3(a.tiles_x * a.tiles_y * B, N / 48), dim3(256), 0, st, a);
+          return check_launch("conv3_quant_rate_h3 (48-column tiles)");
+        }
+      }
       hipLaunchKernelGGL((engine_kernel<N, N, BN, WM, WN, EPI_QUANT, false, true, true>), grid,
                          dim3(256), 0, st, a);
       return check_launch("conv3_quant_rate_h3");

@@ -29,6 +29,7 @@
 // split form.
 #include <string.h>
 
+#include <atomic>
 #include <type_traits>
 
 #include "common.h"
@@ -717,24 +718,53 @@ __global__ void __launch_bounds__(TH / 2 * 64, 1) h3k_kernel(const HArgs a) {
 }
 
 // ---------------------------------------------------------------------------- packing
-// max|w| over the tensor into trailer[0] (zeroed by the caller): a grid-stride reduction, one
-// vector atomicMax per wave on the bits of the non-negative float (ordered like the values). One
+// max|w| over the tensor into trailer[0]: a grid-stride reduction, one vector atomicMax per wave
+// on the bits of the non-negative float (ordered like the values) into a slot of a device-global
+// table, whose last workgroup to finish (a counter beside the slot) writes the maximum to the
+// trailer and zeroes the slot again. The table starts zeroed when the code object loads, so no
+// launch clears it (a memset per pack was ten fill launches per training step); the host deals
+// the slots round-robin, so launches in flight on different streams use different slots. One
 // workgroup took 69 µs for conv2's 0.9 M weights, ten of them per training step.
+constexpr unsigned kAbsmaxSlots = 256;
+__device__ unsigned g_absmax_slot[kAbsmaxSlots][2];   // [0] max bits, [1] workgroups done
+
 __global__ void __launch_bounds__(256) absmax_kernel(const float* __restrict__ w, long n,
-                                                     float* __restrict__ trailer) {
+                                                     float* __restrict__ trailer, unsigned slot) {
+  __shared__ bool last;
+  __shared__ float wmax[4];
   float m = 0.f;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+  const long n4 = ((uintptr_t)w & 15) == 0 ? n / 4 : 0;   // 16-byte loads, then the tail
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    const f4 v = *(const f4*)(w + 4 * i);
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+  }
+  for (long i = 4 * n4 + (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
     m = fmaxf(m, fabsf(w[i]));
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
-  if ((threadIdx.x & 63) == 0) atomicMax((unsigned*)trailer, __float_as_uint(m));
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
+  __syncthreads();
+  // one atomic per workgroup: same-address atomics serialise at the L2 (one per wave of 1024
+  // workgroups made the pass 13 µs)
+  unsigned* s = g_absmax_slot[slot];
+  if (threadIdx.x == 0) {
+    atomicMax(&s[0], __float_as_uint(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]))));
+    __threadfence();
+    last = atomicAdd(&s[1], 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (last && threadIdx.x == 0) {
+    __threadfence();
+    trailer[0] = __uint_as_float(atomicExch(&s[0], 0u));
+    atomicExch(&s[1], 0u);
+  }
 }
 
 static int launch_absmax(const float* w, long n, float* trailer, hipStream_t st) {
-  if (hipMemsetAsync(trailer, 0, sizeof(float), st) != hipSuccess) return check_launch("absmax memset");
-  const long blocks = (n + 4095) / 4096;
-  hipLaunchKernelGGL(absmax_kernel, dim3((unsigned)(blocks < 1024 ? (blocks > 0 ? blocks : 1) : 1024)),
-                     dim3(256), 0, st, w, n, trailer);
+  static std::atomic<unsigned> next{0};
+  const long blocks = (n + 16383) / 16384;   // ≥ 16 values per thread
+  hipLaunchKernelGGL(absmax_kernel, dim3((unsigned)(blocks < 256 ? (blocks > 0 ? blocks : 1) : 256)),
+                     dim3(256), 0, st, w, n, trailer, next.fetch_add(1) % kAbsmaxSlots);
   return check_launch("absmax");
 }
 

@@ -606,7 +606,7 @@ def conv3_quant_rate_h3(hs: Tensor, wh: Tensor, rate_packed: Tensor,
     y_hat = torch.empty(B, h8 // 2, w8 // 2, N, device=hs.device, dtype=torch.float32)
     y_hat_h3 = torch.empty(2, B, h8 // 2, w8 // 2, N, device=hs.device, dtype=torch.int16) if want_h3 else None
     y = torch.empty_like(y_hat) if want_y else None
-    T = rate_partials_per_image(H, W, N)
+    T = query("iclr17_conv3_x6_partials_per_image", B, H, W, N, mode)   # the narrow tiles too
     partial = torch.empty(B, T, device=hs.device, dtype=torch.float64)
     call("iclr17_analysis_conv3_quant_rate_h3", _p(hs), B, H, W, N, _p(wh), mode, _p(noise),
          _p(rate_packed), _p(rtab), _p(y), _p(y_hat), _p(y_hat_h3), _p(partial),

@@ -36,6 +36,9 @@ ICLR17_BF_DECONV5 = 33
 ICLR17_H3K_CONV5 = 42
 ICLR17_H3K_DECONV5 = 43
 ICLR17_H3K_CONV1 = 44
+ICLR17_PACK_H3K = 19
+ICLR17_PACK_SPLIT_H3 = 20
+ICLR17_PACK_H3_MAXJ = 16
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -132,6 +135,7 @@ SIGNATURES = {
     "iclr17_h3_planes": (_I, [_P, ctypes.c_long, _P, _P, _P]),
     "iclr17_split_packed_h3_size": (_SZ, [_I, _I, _I]),
     "iclr17_split_packed_h3": (_I, [_P, _I, _I, _I, _P, _P]),
+    "iclr17_pack_h3_batch": (_I, [_P, _I, _P]),
     "iclr17_analysis_conv1_gdn_h3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_analysis_conv2_gdn_h3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "iclr17_analysis_conv3_quant_rate_h3": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P,

@@ -728,17 +728,19 @@ __global__ void __launch_bounds__(TH / 2 * 64, 1) h3k_kernel(const HArgs a) {
 constexpr unsigned kAbsmaxSlots = 256;
 __device__ unsigned g_absmax_slot[kAbsmaxSlots][2];   // [0] max bits, [1] workgroups done
 
-__global__ void __launch_bounds__(256) absmax_kernel(const float* __restrict__ w, long n,
-                                                     float* __restrict__ trailer, unsigned slot) {
+// workgroup bx of nbx serving one tensor (the single kernel, or one job of the batch kernel)
+__device__ __forceinline__ void absmax_body(const float* __restrict__ w, long n,
+                                            float* __restrict__ trailer, unsigned slot, int bx,
+                                            int nbx) {
   __shared__ bool last;
   __shared__ float wmax[4];
   float m = 0.f;
   const long n4 = ((uintptr_t)w & 15) == 0 ? n / 4 : 0;   // 16-byte loads, then the tail
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+  for (long i = (long)bx * 256 + threadIdx.x; i < n4; i += (long)nbx * 256) {
     const f4 v = *(const f4*)(w + 4 * i);
     m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
   }
-  for (long i = 4 * n4 + (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+  for (long i = 4 * n4 + (long)bx * 256 + threadIdx.x; i < n; i += (long)nbx * 256)
     m = fmaxf(m, fabsf(w[i]));
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
@@ -750,7 +752,7 @@ __global__ void __launch_bounds__(256) absmax_kernel(const float* __restrict__ w
   if (threadIdx.x == 0) {
     atomicMax(&s[0], __float_as_uint(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]))));
     __threadfence();
-    last = atomicAdd(&s[1], 1u) == gridDim.x - 1;
+    last = atomicAdd(&s[1], 1u) == (unsigned)nbx - 1;
   }
   __syncthreads();
   if (last && threadIdx.x == 0) {
@@ -760,11 +762,20 @@ __global__ void __launch_bounds__(256) absmax_kernel(const float* __restrict__ w
   }
 }
 
-static int launch_absmax(const float* w, long n, float* trailer, hipStream_t st) {
-  static std::atomic<unsigned> next{0};
+__global__ void __launch_bounds__(256) absmax_kernel(const float* __restrict__ w, long n,
+                                                     float* __restrict__ trailer, unsigned slot) {
+  absmax_body(w, n, trailer, slot, blockIdx.x, gridDim.x);
+}
+
+static std::atomic<unsigned> g_next_slot{0};
+static int absmax_blocks(long n) {
   const long blocks = (n + 16383) / 16384;   // ≥ 16 values per thread
-  hipLaunchKernelGGL(absmax_kernel, dim3((unsigned)(blocks < 256 ? (blocks > 0 ? blocks : 1) : 256)),
-                     dim3(256), 0, st, w, n, trailer, next.fetch_add(1) % kAbsmaxSlots);
+  return (int)(blocks < 256 ? (blocks > 0 ? blocks : 1) : 256);
+}
+
+static int launch_absmax(const float* w, long n, float* trailer, hipStream_t st) {
+  hipLaunchKernelGGL(absmax_kernel, dim3((unsigned)absmax_blocks(n)), dim3(256), 0, st, w, n,
+                     trailer, g_next_slot.fetch_add(1) % kAbsmaxSlots);
   return check_launch("absmax");
 }
 
@@ -783,14 +794,14 @@ __device__ __forceinline__ int h3_weight_exp(float mx) {
 // deconv (W[ci][co][5][5]): the four stride phases back to back, phase p's blocks c·T_p + t over
 // 16-channel chunks c with the tap order of Taps<BM_DECONV, p>; element (block, h, co, j) = W at
 // input channel 16c + 8h + j.
-__global__ void __launch_bounds__(256) pack_h3k_kernel(const float* __restrict__ w, int N, int deconv,
-                                                       long groups, u16* __restrict__ out,
-                                                       float* __restrict__ trailer) {
+__device__ __forceinline__ void pack_h3k_body(const float* __restrict__ w, int N, int deconv,
+                                              long groups, u16* __restrict__ out,
+                                              float* __restrict__ trailer, int bx, int nbx) {
   const int se = h3_weight_exp(trailer[0]);
   const float sw = ldexpf(1.0f, se);
-  if (blockIdx.x == 0 && threadIdx.x == 0) trailer[1] = ldexpf(1.0f, -11 - kH3SaLog2 - se);
+  if (bx == 0 && threadIdx.x == 0) trailer[1] = ldexpf(1.0f, -11 - kH3SaLog2 - se);
   const int nch = N / 16;
-  for (long g = (long)blockIdx.x * 256 + threadIdx.x; g < groups; g += (long)gridDim.x * 256) {
+  for (long g = (long)bx * 256 + threadIdx.x; g < groups; g += (long)nbx * 256) {
     const int co = (int)(g % N);
     long r = g / N;
     const int h = (int)(r % 2);
@@ -861,16 +872,21 @@ __global__ void __launch_bounds__(256) pack_h3k_kernel(const float* __restrict__
   }
 }
 
+__global__ void __launch_bounds__(256) pack_h3k_kernel(const float* __restrict__ w, int N, int deconv,
+                                                       long groups, u16* __restrict__ out,
+                                                       float* __restrict__ trailer) {
+  pack_h3k_body(w, N, deconv, groups, out, trailer, blockIdx.x, gridDim.x);
+}
+
 // A packed operand [taps][K/4][N][4] fp32 → two fp16 planes [2][taps][K/8][N][8] of w·σ_w (the
 // H3 engine's B-fragment layout, the x6 split_packed's with two planes), trailer after them
-__global__ void __launch_bounds__(256) split_packed_h3_kernel(const float* __restrict__ w, int K,
-                                                              int N, long groups,
-                                                              u16* __restrict__ out,
-                                                              float* __restrict__ trailer) {
+__device__ __forceinline__ void split_packed_h3_body(const float* __restrict__ w, int K, int N,
+                                                     long groups, u16* __restrict__ out,
+                                                     float* __restrict__ trailer, int bx, int nbx) {
   const int se = h3_weight_exp(trailer[0]);
   const float sw = ldexpf(1.0f, se);
-  if (blockIdx.x == 0 && threadIdx.x == 0) trailer[1] = ldexpf(1.0f, -11 - kH3SaLog2 - se);
-  for (long g = (long)blockIdx.x * 256 + threadIdx.x; g < groups; g += (long)gridDim.x * 256) {
+  if (bx == 0 && threadIdx.x == 0) trailer[1] = ldexpf(1.0f, -11 - kH3SaLog2 - se);
+  for (long g = (long)bx * 256 + threadIdx.x; g < groups; g += (long)nbx * 256) {
     const long tk = g / N;
     const int col = (int)(g - tk * N);
     const long tap = tk / (K / 8);
@@ -895,6 +911,50 @@ __global__ void __launch_bounds__(256) split_packed_h3_kernel(const float* __res
     *(u4*)(out + g * 8) = H;
     *(u4*)(out + groups * 8 + g * 8) = L;
   }
+}
+
+__global__ void __launch_bounds__(256) split_packed_h3_kernel(const float* __restrict__ w, int K,
+                                                              int N, long groups,
+                                                              u16* __restrict__ out,
+                                                              float* __restrict__ trailer) {
+  split_packed_h3_body(w, K, N, groups, out, trailer, blockIdx.x, gridDim.x);
+}
+
+// A batch of h3 packs (iclr17_pack_h3_batch): job j owns workgroups [begin[j], begin[j+1]) of
+// each launch — the absmax pass first, then the packing pass, both the single kernels' bodies.
+struct H3Job {
+  const float* src;
+  u16* out;
+  float* trailer;
+  long n, groups;      // absmax values; 16-byte packing groups
+  int kind, N, K, deconv;
+  unsigned slot;
+};
+struct H3Batch {
+  int n;
+  int begin[ICLR17_PACK_H3_MAXJ + 1];
+  H3Job job[ICLR17_PACK_H3_MAXJ];
+};
+
+__device__ __forceinline__ int h3_batch_job(const H3Batch& b, int& bx, int& nbx) {
+  int j = 0;
+  while (j + 1 < b.n && (int)blockIdx.x >= b.begin[j + 1]) ++j;
+  bx = blockIdx.x - b.begin[j];
+  nbx = b.begin[j + 1] - b.begin[j];
+  return j;
+}
+
+__global__ void __launch_bounds__(256) absmax_batch_kernel(const H3Batch b) {
+  int bx, nbx;
+  const H3Job& J = b.job[h3_batch_job(b, bx, nbx)];
+  absmax_body(J.src, J.n, J.trailer, J.slot, bx, nbx);
+}
+
+__global__ void __launch_bounds__(256) pack_h3_batch_kernel(const H3Batch b) {
+  int bx, nbx;
+  const H3Job& J = b.job[h3_batch_job(b, bx, nbx)];
+  if (J.kind == ICLR17_PACK_H3K) pack_h3k_body(J.src, J.N, J.deconv, J.groups, J.out, J.trailer, bx, nbx);
+  else split_packed_h3_body(J.src, J.K, J.N, J.groups, J.out, J.trailer, bx, nbx);
 }
 
 // fp32 → h3 planes (x·σ_a split): iclr17_h3_planes
@@ -974,6 +1034,53 @@ int iclr17_split_packed_h3(const float* packed, int taps, int K, int N, uint16_t
   hipLaunchKernelGGL(split_packed_h3_kernel, dim3(blocks), dim3(256), 0, st, packed, K, N, groups,
                      planes, trailer);
   return check_launch("split_packed_h3");
+}
+
+int iclr17_pack_h3_batch(const iclr17_pack_job* jobs, int n, void* stream) {
+  ICLR17_REQUIRE(jobs && n >= 0 && n <= ICLR17_PACK_H3_MAXJ, ICLR17_EINVAL,
+                 "pack_h3_batch: bad arguments (n=%d)", n);
+  if (n == 0) return ICLR17_OK;
+  H3Batch b;
+  memset(&b, 0, sizeof(b));
+  b.n = n;
+  int pack_begin[ICLR17_PACK_H3_MAXJ + 1];
+  pack_begin[0] = 0;
+  for (int j = 0; j < n; ++j) {
+    const iclr17_pack_job& q = jobs[j];
+    H3Job& J = b.job[j];
+    J.kind = q.kind;
+    J.N = q.N;
+    J.K = q.K;
+    J.src = q.src0;
+    J.out = (u16*)q.dst0;
+    size_t total = 0;
+    if (q.kind == ICLR17_PACK_H3K) {
+      total = iclr17_h3k_weight_size(q.K, q.N);
+      ICLR17_REQUIRE(total > 0, ICLR17_EUNSUPPORTED, "pack_h3_batch: job %d: kind %d, N=%d", j, q.K, q.N);
+      J.n = q.K == ICLR17_H3K_CONV1 ? (long)q.N * 3 * 81 : (long)q.N * q.N * 25;
+      J.deconv = q.K == ICLR17_H3K_DECONV5 ? 1 : q.K == ICLR17_H3K_CONV1 ? 2 : 0;
+    } else if (q.kind == ICLR17_PACK_SPLIT_H3) {
+      total = iclr17_split_packed_h3_size(q.taps, q.K, q.N);
+      ICLR17_REQUIRE(total > 0, ICLR17_EINVAL, "pack_h3_batch: bad split job %d", j);
+      J.n = (long)q.taps * q.K * q.N;
+    } else {
+      ICLR17_REQUIRE(false, ICLR17_EINVAL, "pack_h3_batch: unknown job kind %d", q.kind);
+    }
+    ICLR17_REQUIRE(q.src0 && q.dst0, ICLR17_EINVAL, "pack_h3_batch: null pointer (job %d)", j);
+    J.groups = (long)((total - 8) / 16);
+    J.trailer = (float*)(J.out + (total - 8));
+    J.slot = g_next_slot.fetch_add(1) % kAbsmaxSlots;
+    b.begin[j + 1] = b.begin[j] + absmax_blocks(J.n);
+    const long pb = (J.groups + 255) / 256;
+    pack_begin[j + 1] = pack_begin[j] + (int)(pb < 4096 ? pb : 4096);
+  }
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(absmax_batch_kernel, dim3((unsigned)b.begin[n]), dim3(256), 0, st, b);
+  int rc = check_launch("absmax_batch");
+  if (rc) return rc;
+  memcpy(b.begin, pack_begin, sizeof(pack_begin));
+  hipLaunchKernelGGL(pack_h3_batch_kernel, dim3((unsigned)b.begin[n]), dim3(256), 0, st, b);
+  return check_launch("pack_h3_batch");
 }
 
 int iclr17_h3_planes(const float* x, long n, uint16_t* planes, int* range_flag, void* stream) {

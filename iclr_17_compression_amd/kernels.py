@@ -493,6 +493,31 @@ def merge_h3(s: Tensor) -> Tensor:
     return (h[0] + h[1] * (2.0 ** -11)) / H3_SIGMA_A
 
 
+_deferred_h3: Optional[list] = None   # queued h3 pack jobs inside batched_h3_packs()
+
+
+@contextlib.contextmanager
+def batched_h3_packs():
+    """Inside the block, pack_h3k / split_packed_h3 allocate their outputs and queue the work; on
+    exit it runs as iclr17_pack_h3_batch (two launches instead of two per pack). Nothing may read
+    the outputs inside the block. Re-entrant."""
+    global _deferred_h3
+    if _deferred_h3 is not None:
+        yield
+        return
+    _deferred_h3 = []
+    try:
+        yield
+        jobs = _deferred_h3
+    finally:
+        _deferred_h3 = None
+    for i in range(0, len(jobs), _lib.ICLR17_PACK_H3_MAXJ):
+        part = jobs[i:i + _lib.ICLR17_PACK_H3_MAXJ]
+        arr = (_PackJob * len(part))(*[j[0] for j in part])
+        call("iclr17_pack_h3_batch", ctypes.cast(arr, ctypes.c_void_p), len(part), part[0][2])
+    del jobs   # sources stay alive until here; the stream orders their reuse after the launches
+
+
 def pack_h3k(which: int, w: Tensor, N: int) -> Tensor:
     """conv / deconv weights → the h3 engine's two fp16 planes (per-tensor power-of-two scale) +
     trailer (ICLR17_H3K_CONV1 / ICLR17_H3K_CONV5 / ICLR17_H3K_DECONV5)."""
@@ -501,7 +526,12 @@ def pack_h3k(which: int, w: Tensor, N: int) -> Tensor:
     if size == 0:
         raise Iclr17Error(f"iclr17: pack_h3k: kind {which}, N={N} unsupported")
     out = torch.empty(size, device=w.device, dtype=torch.int16)
-    call("iclr17_pack_h3k", which, _p(w.detach().contiguous()), _p(out), N, _stream(w))
+    w = w.detach().contiguous()
+    if _deferred_h3 is not None:
+        _deferred_h3.append((_PackJob(_lib.ICLR17_PACK_H3K, N, 0, which, _ptr(w), None, _ptr(out),
+                                      None, None), (w, out), _stream(w)))
+        return out
+    call("iclr17_pack_h3k", which, _p(w), _p(out), N, _stream(w))
     return out
 
 
@@ -515,7 +545,12 @@ def split_packed_h3(packed: Tensor, taps: int, K: int, N: int) -> Tensor:
     if size == 0:
         raise Iclr17Error("iclr17: split_packed_h3: bad shape")
     out = torch.empty(size, device=packed.device, dtype=torch.int16)
-    call("iclr17_split_packed_h3", _p(packed.contiguous()), taps, K, N, _p(out), _stream(packed))
+    packed = packed.contiguous()
+    if _deferred_h3 is not None:
+        _deferred_h3.append((_PackJob(_lib.ICLR17_PACK_SPLIT_H3, N, taps, K, _ptr(packed), None,
+                                      _ptr(out), None, None), (packed, out), _stream(packed)))
+        return out
+    call("iclr17_split_packed_h3", _p(packed), taps, K, N, _p(out), _stream(packed))
     return out
 
 

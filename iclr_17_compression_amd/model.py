@@ -289,12 +289,13 @@ class ImageCompressor(nn.Module):
                         g.effective_params_bwd()
         if h3:
             # the h3 layouts (the codec's, and the training forward's in this mode) split the
-            # packs above, which the batch writes only at its exit
-            self.Decoder.packed_h3k()
-            self.Encoder.packed_h3()
-            self.Encoder.packed_conv1_h3()
-            for g in gdns:
-                g.effective_params_h3()
+            # packs above, which the batch writes only at its exit; they form a batch of their own
+            with kernels.batched_h3_packs():
+                self.Decoder.packed_h3k()
+                self.Encoder.packed_h3()
+                self.Encoder.packed_conv1_h3()
+                for g in gdns:
+                    g.effective_params_h3()
         if not backward:   # eval: the rate table of the round quantiser (+ the bf16 layouts)
             self.bitEstimator.rate_table()
             if kernels.precision() == "bf16":

@@ -487,6 +487,15 @@ int iclr17_h3_planes(const float* x, long n, uint16_t* planes, int* range_flag, 
 size_t iclr17_split_packed_h3_size(int taps, int K, int N);
 int iclr17_split_packed_h3(const float* packed, int taps, int K, int N, uint16_t* planes,
                            void* stream);
+/* A batch of h3 packs in two launches (every job's max|w|, then every job's planes), bitwise
+ * those of the single-pack entry points: a training step's h3 layouts without two launches per
+ * pack. jobs (iclr17_pack_job above): ICLR17_PACK_H3K (src0 = w, dst0 = out, N, K = the
+ * ICLR17_H3K_* kind: as iclr17_pack_h3k) or ICLR17_PACK_SPLIT_H3 (src0 = packed, dst0 = planes,
+ * taps, K, N: as iclr17_split_packed_h3). At most ICLR17_PACK_H3_MAXJ jobs. */
+#define ICLR17_PACK_H3K 19
+#define ICLR17_PACK_SPLIT_H3 20
+#define ICLR17_PACK_H3_MAXJ 16
+int iclr17_pack_h3_batch(const iclr17_pack_job* jobs, int n, void* stream);
 /* analysis_17.py:14-17 conv1 + GDN1 on the h3 engine (csrc/engine_h3.hip): 16×16-pixel output
  * tiles of 8 waves; the tile's 3 × 69 × 69 input window split once into the two h3 planes in LDS,
  * K = 243 reordered into 16 steps of 16, three f16 part products per MAC, GDN contraction in the

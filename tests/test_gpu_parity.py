@@ -489,6 +489,40 @@ def test_batched_packs_match_single(device):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("N", [128, 192])
+def test_batched_h3_packs_match_single(device, N):
+    """kernels.batched_h3_packs (iclr17_pack_h3_batch: the max pass and the packing pass of
+    every job in one launch each; more jobs than one call holds, one all-zero tensor) gives
+    bitwise the single-pack results, trailer included."""
+    net = net_for(N, 1, device)
+    enc, dec = net.Encoder, net.Decoder
+    gp = enc.gdn1.effective_params()[1]
+    w3 = enc.packed()[2]
+    d3 = dec.packed()[2]
+    zero = torch.zeros_like(dec.deconv2.weight)
+
+    def all_packs():
+        out = []
+        for _ in range(3):   # 21 jobs: two batch calls
+            out += [kernels.pack_h3k(_lib.ICLR17_H3K_CONV1, enc.conv1.weight, N),
+                    kernels.pack_h3k(_lib.ICLR17_H3K_CONV5, enc.conv2.weight, N),
+                    kernels.pack_h3k(_lib.ICLR17_H3K_DECONV5, dec.deconv1.weight, N),
+                    kernels.split_packed_h3(w3, 25, N, N),
+                    kernels.split_packed_h3(d3, 9, N, 48),
+                    kernels.split_packed_h3(gp, 1, N, N)]
+        out.append(kernels.pack_h3k(_lib.ICLR17_H3K_DECONV5, zero, N))
+        return out
+
+    single = all_packs()
+    with kernels.batched_h3_packs():
+        batched = all_packs()
+    torch.cuda.synchronize()
+    assert len(single) == len(batched)
+    for a, b in zip(single, batched):   # the trailer's last 8 bytes are padding, never written
+        assert torch.equal(a[:-4], b[:-4])
+    assert float(batched[-1][-8:].view(torch.float32)[0]) == 0.0   # max|w| of the zero tensor
+
+
 @pytest.mark.parametrize("mode", ["x6", "fp32", "bf16"])
 def test_encoder_matches_codec_forward(device, mode):
     """The separate encode / decode path (NewTests/testReconSeperateEandD.py:67-68): in every

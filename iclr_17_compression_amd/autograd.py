@@ -126,7 +126,6 @@ def analysis_features_train(enc, x: Tensor):
     kernels also hand conv2 (and conv3) their input in split form; "a2s" is then set. In the h3
     mode the forward runs the codec's own h3 kernels, which also write the split forms (the x6
     weight-gradient operands) and the pre-activations; "a2h" (conv3's h3 input) is then set."""
-    w1, w2, _, g1, g2 = enc.packed()
     N = enc.out_channel_N
     if kernels.precision() == "h3":
         ge1, ge2 = enc.gdn1.effective_params_h3(), enc.gdn2.effective_params_h3()
@@ -136,6 +135,7 @@ def analysis_features_train(enc, x: Tensor):
         a2h, _, a2s, u2 = kernels.conv2_gdn_h3(a1h, w2h, enc.conv2.bias, *ge2, want_x6=True,
                                                want_pre=True)
         return None, {"x": x, "u1": u1, "u2": u2, "a1s": a1s, "a2s": a2s, "a2h": a2h}
+    w1, w2, _, g1, g2 = enc.packed()
     if kernels.precision() != "fp32":
         e1, e2 = enc.gdn1.effective_params_x6(), enc.gdn2.effective_params_x6()
         a1s, a1, u1 = kernels.conv1x6_gdn(x, enc.packed_conv1_x6(), enc.conv1.bias, e1[0], e1[2],
@@ -207,7 +207,6 @@ def analysis_backward(enc, saved: Dict[str, Tensor], g_y: Tensor,
 # ----------------------------------------------------------------------------- synthesis
 def synthesis_forward_train(dec, y_nhwc: Tensor, x_ref: Optional[Tensor] = None,
                             y_split: Optional[Tensor] = None, y_h3: Optional[Tensor] = None):
-    d1, d2, d3, q1, q2 = dec.packed()
     if kernels.precision() == "h3":
         # the codec's h3 kernels; their x6 outputs are the weight-gradient operands and the
         # pre-activations the IGDN backward's
@@ -222,6 +221,7 @@ def synthesis_forward_train(dec, y_nhwc: Tensor, x_ref: Optional[Tensor] = None,
         clipped, recon, sse = kernels.deconv3_h3(s2h, x3, dec.deconv3.bias, x_ref=x_ref,
                                                  want_recon=True, sse_unclipped=x_ref is not None)
         return clipped, recon, sse, {"y": y_nhwc, "v1": v1, "v2": v2, "s1s": s1s, "s2s": s2s}
+    d1, d2, d3, q1, q2 = dec.packed()
     if kernels.precision() != "fp32":
         if y_split is None:
             y_split = kernels.split_planes(y_nhwc)
@@ -316,7 +316,7 @@ class CodecTrainFn(torch.autograd.Function):
         enc, dec, be = net.Encoder, net.Decoder, net.bitEstimator
         B, _, H, W = x.shape
         a2, saved_a = analysis_features_train(enc, x)
-        _, _, w3, _, _ = enc.packed()
+        w3 = enc.packed_w3()
         rate = be.packed()
         a2s, a2h, y_h3 = saved_a.get("a2s"), saved_a.get("a2h"), None
         if a2h is not None:   # h3: conv3 + quantiser on the codec's h3 kernel, ỹ also in h3

@@ -267,11 +267,17 @@ class ImageCompressor(nn.Module):
         batched packing launch pair (kernels.batched_packs)."""
         x6 = kernels.precision() != "fp32"
         gdns = (self.Encoder.gdn1, self.Encoder.gdn2, self.Decoder.igdn1, self.Decoder.igdn2)
+        h3 = kernels.precision() == "h3"
         with kernels.batched_packs():
-            self.Encoder.packed()
-            self.Decoder.packed()
+            if h3 and backward:   # an h3 training step reads only these fp32 packings
+                self.Encoder.packed_w3()
+                self.Decoder.packed_d3()
+                for g in gdns:
+                    g.effective_params()
+            else:
+                self.Encoder.packed()
+                self.Decoder.packed()
             self.bitEstimator.packed()
-            h3 = kernels.precision() == "h3"
             if x6:
                 if not (h3 and backward):   # the x6 forward's (an h3 training step has none)
                     self.Encoder.packed_conv1_x6()

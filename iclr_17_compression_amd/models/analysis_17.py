@@ -42,17 +42,23 @@ class Analysis_net_17(nn.Module):
                             lambda: kernels.pack_weight(_lib.ICLR17_W_CONV1, self.conv1.weight, N), f)
         w2 = self._pack.get("w2", (self.conv2.weight,),
                             lambda: kernels.pack_weight(_lib.ICLR17_W_CONV5, self.conv2.weight, N), f)
-        w3 = self._pack.get("w3", (self.conv3.weight,),
-                            lambda: kernels.pack_weight(_lib.ICLR17_W_CONV5, self.conv3.weight, N), f)
         g1 = self.gdn1.effective_params(force)
         g2 = self.gdn2.effective_params(force)
-        return w1, w2, w3, g1, g2
+        return w1, w2, self.packed_w3(f), g1, g2
+
+    def packed_w3(self, force: bool = False):
+        """conv3's fp32 packing alone (the h3 layouts split it; the h3 training step needs no
+        other fp32 weight packing of this module), cached with ``packed``'s entry."""
+        N = self.out_channel_N
+        return self._pack.get("w3", (self.conv3.weight,),
+                              lambda: kernels.pack_weight(_lib.ICLR17_W_CONV5, self.conv3.weight, N),
+                              force)
 
     def packed_w3_split(self, force: bool = False):
         """conv3's packed weights pre-split into the x6 planes (kernels.split_packed), cached:
         the x6 conv3 then reads its B operand as it is instead of splitting it per k-step."""
         N = self.out_channel_N
-        w3 = self.packed(force)[2]
+        w3 = self.packed_w3(force)
         return self._pack.get("w3x6", (self.conv3.weight,),
                               lambda: kernels.split_packed(w3, 25, N, N), force)
 
@@ -61,7 +67,7 @@ class Analysis_net_17(nn.Module):
         (kernels.pack_h3k, ICLR17_H3K_CONV5), conv3 in the engine's two fp16 planes
         (kernels.split_packed_h3 of the conv5 packing); per-tensor power-of-two scales."""
         N = self.out_channel_N
-        _, _, w3, _, _ = self.packed(force)
+        w3 = self.packed_w3(force)
         w2h = self._pack.get("w2h3", (self.conv2.weight,),
                              lambda: kernels.pack_h3k(_lib.ICLR17_H3K_CONV5, self.conv2.weight, N), force)
         w3h = self._pack.get("w3h3", (self.conv3.weight,),

@@ -43,13 +43,19 @@ class Synthesis_net_17(nn.Module):
                             lambda: kernels.pack_weight(_lib.ICLR17_W_DECONV5, self.deconv1.weight, N), f)
         d2 = self._pack.get("d2", (self.deconv2.weight,),
                             lambda: kernels.pack_weight(_lib.ICLR17_W_DECONV5, self.deconv2.weight, N), f)
-        d3 = self._pack.get("d3", (self.deconv3.weight,),
-                            lambda: kernels.pack_weight(_lib.ICLR17_W_DECONV9, self.deconv3.weight, N), f)
-        return d1, d2, d3, self.igdn1.effective_params(force), self.igdn2.effective_params(force)
+        return d1, d2, self.packed_d3(f), self.igdn1.effective_params(force), self.igdn2.effective_params(force)
+
+    def packed_d3(self, force: bool = False):
+        """deconv3's fp32 packing alone (the h3 layouts split it; the h3 training step needs no
+        other fp32 weight packing of this module), cached with ``packed``'s entry."""
+        N = self.out_channel_N
+        return self._pack.get("d3", (self.deconv3.weight,),
+                              lambda: kernels.pack_weight(_lib.ICLR17_W_DECONV9, self.deconv3.weight, N),
+                              force)
 
     def packed_x6(self, force: bool = False):
         """deconv3's packed weights split into the x6 planes the halo kernel stages, cached."""
-        d3 = self.packed(force)[2]
+        d3 = self.packed_d3(force)
         return self._pack.get("d3x6", (self.deconv3.weight,),
                               lambda: kernels.split_deconv3(d3, self.out_channel_N), force)
 
@@ -62,7 +68,7 @@ class Synthesis_net_17(nn.Module):
                             lambda: kernels.pack_h3k(_lib.ICLR17_H3K_DECONV5, self.deconv1.weight, N), f)
         d2 = self._pack.get("d2h3", (self.deconv2.weight,),
                             lambda: kernels.pack_h3k(_lib.ICLR17_H3K_DECONV5, self.deconv2.weight, N), f)
-        d3 = self.packed(force)[2]
+        d3 = self.packed_d3(force)
         d3h = self._pack.get("d3h3", (self.deconv3.weight,),
                              lambda: kernels.split_packed_h3(d3, 9, N, 48), f)
         return d1, d2, d3h
@@ -75,7 +81,7 @@ class Synthesis_net_17(nn.Module):
                             lambda: kernels.pack_bf16(_lib.ICLR17_BF_DECONV5, self.deconv1.weight, N), f)
         d2 = self._pack.get("d2bf", (self.deconv2.weight,),
                             lambda: kernels.pack_bf16(_lib.ICLR17_BF_DECONV5, self.deconv2.weight, N), f)
-        d3 = self.packed(force)[2]
+        d3 = self.packed_d3(force)
         d3b = self._pack.get("d3bf", (self.deconv3.weight,),
                              lambda: kernels.round_packed(d3, 9, N, 48), f)
         return d1, d2, d3b

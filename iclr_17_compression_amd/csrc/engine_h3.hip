@@ -751,12 +751,13 @@ __device__ __forceinline__ void absmax_body(const float* __restrict__ w, long n,
   unsigned* s = g_absmax_slot[slot];
   if (threadIdx.x == 0) {
     atomicMax(&s[0], __float_as_uint(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]))));
-    __threadfence();
+    // both words are atomics, performed at the memory side: the max lands before the count
+    // once the wave's outstanding memory operations have drained (no L2 write-back fence)
+    __builtin_amdgcn_s_waitcnt(0);
     last = atomicAdd(&s[1], 1u) == (unsigned)nbx - 1;
   }
   __syncthreads();
   if (last && threadIdx.x == 0) {
-    __threadfence();
     trailer[0] = __uint_as_float(atomicExch(&s[0], 0u));
     atomicExch(&s[1], 0u);
   }

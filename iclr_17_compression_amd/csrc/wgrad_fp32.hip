@@ -12,6 +12,7 @@
 // GEMM mapping: M = m (all of it per workgroup, 4 waves × 48/32 rows), N = 64 columns of
 // (tap, c), K = pixels. Both operands are staged through LDS ([pixel][channel] rows, coalesced
 // 16-byte loads); a lane's 4 k-values are 4 consecutive pixels (scalar LDS reads).
+#include <atomic>
 #include "common.h"
 
 namespace iclr17 {
@@ -986,10 +987,20 @@ __global__ void sum_splits_tap_kernel(const float* __restrict__ part, int nsplit
 // (one workgroup per 64 columns walked thousands of rows serially).
 constexpr int SUM_ROWS_SPLITS = 64;
 
-__global__ void sum_rows2_kernel(const Rows2 r, int T, int C, int per) {
+// Split s of matrix blockIdx.z, columns blockIdx.x·64 ..: ws[s][c] = Σ_t part[t][c] over the split's
+// rows. The split rows go out write-through (sc1) and the workgroup of a (column block, matrix)
+// whose arrival on a device-global counter comes last adds them in split order — the order of
+// sum_splits2_kernel, which this folds in (one launch instead of two): the counter's slot is dealt
+// round-robin by the host and reset by that last workgroup (zero when the code object loads).
+constexpr unsigned kRowSlots = 256;
+__device__ unsigned g_rows_done[kRowSlots][8];   // [slot][column block + 4 · matrix]
+static std::atomic<unsigned> g_rows_slot{0};
+
+__global__ void sum_rows2_kernel(const Rows2 r, int T, int C, int per, unsigned slot) {
   const float* __restrict__ part = r.part[blockIdx.z];
   float* __restrict__ ws = r.ws[blockIdx.z];
   __shared__ float red[4][64];
+  __shared__ bool last;
   const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   const int t0 = blockIdx.y * per, t1 = t0 + per < T ? t0 + per : T;
@@ -998,8 +1009,40 @@ __global__ void sum_rows2_kernel(const Rows2 r, int T, int C, int per) {
     for (int t = t0 + g; t < t1; t += 4) s += part[(long)t * C + c];
   red[g][cl] = s;
   __syncthreads();
-  if (g == 0 && c < C)
-    ws[(long)blockIdx.y * C + c] = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
+  if (slot == ~0u) {   // C > 256: sum_splits2_kernel adds the splits
+    if (g == 0 && c < C)
+      ws[(long)blockIdx.y * C + c] = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
+    return;
+  }
+  unsigned* done = &g_rows_done[slot][blockIdx.x + 4 * blockIdx.z];
+  if (g == 0) {
+    if (c < C)
+      __hip_atomic_store(&ws[(long)blockIdx.y * C + c],
+                         ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_s_waitcnt(0);   // the wave's split row has left for memory
+    if (cl == 0) last = atomicAdd(done, 1u) == gridDim.y - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (g == 0 && c < C) {   // eight loads in flight at a time, added in split order
+    const int ns = gridDim.y;
+    float o = 0.f;
+    int k = 0;
+    for (; k + 8 <= ns; k += 8) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[j] = __hip_atomic_load(&ws[(long)(k + j) * C + c], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o += v[j];
+    }
+    for (; k < ns; ++k)
+      o += __hip_atomic_load(&ws[(long)k * C + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    r.out[blockIdx.z][c] = o;
+  }
+  if (threadIdx.x == 0) atomicExch(done, 0u);
 }
 
 // Column sums of a [P][C] row-major matrix (NHWC activations): part[chunk][c].
@@ -1225,10 +1268,11 @@ size_t iclr17_sum_rows_workspace_size(int C) { return (size_t)SUM_ROWS_SPLITS * 
 static int sum_rows_n(const Rows2& r, int nm, int T, int C, void* stream) {
   const int per = (T + SUM_ROWS_SPLITS - 1) / SUM_ROWS_SPLITS;
   const int ns = (T + per - 1) / per;
+  const bool fused = C <= 256;   // g_rows_done holds 4 column blocks per matrix
   hipLaunchKernelGGL(sum_rows2_kernel, dim3((C + 63) / 64, ns, nm), dim3(256), 0, S(stream), r, T,
-                     C, per);
+                     C, per, fused ? g_rows_slot.fetch_add(1) % kRowSlots : ~0u);
   int rc = check_launch("sum_rows");
-  if (rc) return rc;
+  if (rc || fused) return rc;
   hipLaunchKernelGGL(sum_splits2_kernel, dim3((C + 255) / 256, nm), dim3(256), 0, S(stream), r, ns,
                      (long)C);
   return check_launch("sum_rows_splits");

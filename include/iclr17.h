@@ -126,7 +126,7 @@ int iclr17_analysis_conv3_quant_rate(const float* in, int B, int H, int W, int N
                                      float* y_out, float* y_hat, double* bits_partial,
                                      void* stream);
 int iclr17_rate_partials_per_image(int H, int W, int N);
-/* Bit partials per image of the x6 conv3 entries (…_x6, …_x6w): as above, except that in noise
+/* Bit partials per image of the x6 and h3 conv3 entries (…_x6, …_x6w, …_h3): as above, except that in noise
  * mode on fewer than 256 tiles·images (training at B=32, 256²) the kernel runs 48-column tiles
  * and writes tiles × N/48 partials. */
 int iclr17_conv3_x6_partials_per_image(int B, int H, int W, int N, int quant_mode);
@@ -518,7 +518,8 @@ int iclr17_analysis_conv2_gdn_h3(const uint16_t* in_h3, int B, int H, int W, int
                                  void* stream);
 /* analysis_17.py:22 + model.py:48-56,71-73 on the h3 form: as iclr17_analysis_conv3_quant_rate
  * (round or noise mode, rate_table nullable), ŷ also in the h3 form (y_hat_h3, nullable); bit
- * partials [B][iclr17_rate_partials_per_image] in both modes. */
+ * partials [B][iclr17_conv3_x6_partials_per_image(B, H, W, N, quant_mode)] (48-column tiles in
+ * noise mode below 256 tiles·images, as the x6 entries). */
 int iclr17_analysis_conv3_quant_rate_h3(const uint16_t* in_h3, int B, int H, int W, int N,
                                         const uint16_t* w_h3, int quant_mode, const float* noise,
                                         const float* rate_packed, const float* rate_table,

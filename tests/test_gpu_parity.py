@@ -810,3 +810,35 @@ def test_deconv3_bits_fold(device, T):
         c2, _, _ = kernels.deconv3_bf16(hb, b3, dec.deconv3.bias)
         c3, _, _, tot2 = kernels.deconv3_bf16(hb, b3, dec.deconv3.bias, bits=(part, 1.0 / 12345.0))
         assert torch.equal(c2, c3) and torch.equal(tot2, ref)
+
+
+@pytest.mark.parametrize("form", ["h3", "x6"])
+def test_conv3_narrow_tiles_match_wide(device, form):
+    """Noise-mode conv3 at N=192: a batch under 256 tiles·images runs the 48-column tiles
+    (conv3_narrow), one at or above it the 96-column ones. The same images in both batches give
+    bit-equal y, ỹ and its split / h3 form, and per-image bits that agree to summation order
+    (the partial counts differ: tiles·N/48 vs tiles·N/96)."""
+    N, h, w = 192, 32, 32          # conv3 output 16×16: four 8×8 tiles per image
+    Bs, Bw = 3, 64                 # 12 tiles·images < 256 (narrow), 256 (wide)
+    net = net_for(N, 1, device)
+    enc = net.Encoder
+    rate = net.bitEstimator.packed()
+    a2 = torch.from_numpy(synth.normal_like(31, (Bw, h, w, N), 0.7)).to(device)
+    noise = torch.from_numpy(synth.uniform(32, (Bw, N, h // 2, w // 2), -0.5, 0.5)).to(device)
+
+    def run(B):
+        if form == "h3":
+            r = kernels.conv3_quant_rate_h3(kernels.h3_planes(a2[:B].contiguous()), enc.packed_h3()[1],
+                                            rate, noise[:B].contiguous(), want_y=True)
+        else:
+            r = kernels.conv3_quant_rate_x6(kernels.split_planes(a2[:B].contiguous()),
+                                            enc.packed()[2], rate, noise[:B].contiguous(), want_y=True,
+                                            w_split=enc.packed_w3_split())
+        return r
+
+    small, wide = run(Bs), run(Bw)
+    assert small[1].shape[1] == 2 * wide[1].shape[1]       # twice the partials per image
+    assert torch.equal(small[0], wide[0][:Bs]) and torch.equal(small[2], wide[2][:Bs])
+    assert torch.equal(small[3], wide[3][:, :Bs])
+    bs, bw = small[1].sum(1), wide[1][:Bs].sum(1)
+    assert ((bs - bw).abs() <= 1e-6 * bw.abs()).all()   # fp32 per-tile sums in another grouping

@@ -42,6 +42,16 @@ H3_LAYERS = ("conv1_gdn1", "conv2_gdn2", "conv3_quant_rate", "deconv1_igdn1", "d
              "deconv3_clamp")
 
 
+# the JSON line's "dtype": the arithmetic the contractions compute in (every mode accumulates in
+# fp32; the epilogues — GDN square roots, quantiser, rate — are fp32)
+DTYPE = {"h3": "h3", "x6": "f32", "fp32": "f32", "bf16": "bf16"}
+DTYPE_NOTE = {
+    "h3": "h3: fp32 operands rounded to 22 significant bits (two fp16 parts), fp32 accumulate",
+    "x6": "f32: fp32 operands split exactly (24 significant bits) into three bf16 parts, fp32 accumulate",
+    "fp32": "f32: exact-f32 MFMA products",
+    "bf16": "bf16 operands, fp32 accumulate",
+}
+
 PRECISION_NOTE = {
     "h3": ("h3: fp32 operands as two fp16 parts (22 significant bits, power-of-two scaled), 3 part "
            "products per MAC on v_mfma_f32_*_f16 with fp32 accumulate for every convolution and "
@@ -162,7 +172,9 @@ class Step:
                                                       bits=(partial, self.scale))
         elif kernels.precision() == "h3":
             # ImageCompressor.forward in the h3 form: every layer (and GDN contraction) on three
-            # fp16 part products per MAC
+            # fp16 part products per MAC; the chain's range flag cleared first (deconv3 makes the
+            # results NaN when a value did not fit the form)
+            kernels.h3_chain_begin(self.x.device)
             e1, e2 = self.eg3
             (w2h, w3h), (x1, x2, x3) = self.eh3, self.dh3
             hs, _ = kernels.conv1_gdn_h3(self.x, self.w1h3, net.Encoder.conv1.bias, *e1, N)
@@ -361,7 +373,7 @@ def run_train(args, net, x, world, dev):
         "value": round(world * B * S * S * args.steps / elapsed / 1e6, 2),
         "unit": "Mpix/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32",
+        "vs_baseline": None, "dtype": "h3 fwd / f32 bwd" if h3t else "f32",
         "data": "synthetic (splitmix64 uint8/255 images, seeded trained-like weights)",
         "config": {"workload": f"train step, {B} x {S}x{S}x3 crops per GPU, N={args.N}, lambda=0.01",
                    "N": args.N, "batch_per_gpu": B, "global_batch": B * world,
@@ -600,7 +612,7 @@ def run_kodak(args, dev):
         "value": round(pixels / elapsed / 1e6, 2), "unit": "Mpix/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-        "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "scaling": "strong", "vs_baseline": None, "dtype": DTYPE[kernels.precision()],
         "data": f"synthetic Kodak-24 (18 x 512x768 + 6 x 768x512, smooth_image_u8), {weights_note}",
         "config": {"workload": "Kodak-24 eval: encode, round, rate, decode, clamp, per-image bpp/PSNR/MS-SSIM",
                    "N": meta["N"], "precision": kernels.precision(),
@@ -663,7 +675,7 @@ def run_codec(args, dev):
         "value": round(B * S * S * args.steps / elapsed / 1e6, 2), "unit": "Mpix/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32 transforms, u32 rANS state",
+        "scaling": "weak", "vs_baseline": None, "dtype": DTYPE[kernels.precision()] + " transforms, u32 rANS state",
         "data": "synthetic (splitmix64 uint8/255 images, seeded trained-like weights)",
         "config": {"workload": f"image -> bitstream -> image, {B} x {S}x{S}x3, N={N}",
                    "precision": kernels.precision(), "K": kernels.ENTROPY_K,
@@ -719,7 +731,7 @@ def run_encdec(args, dev):
         "value": round(px * args.steps / elapsed / 1e6, 2), "unit": "Mpix/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if kernels.precision() == "bf16" else "f32",
+        "scaling": "weak", "vs_baseline": None, "dtype": DTYPE[kernels.precision()],
         "data": "synthetic (splitmix64 uint8/255 images, seeded trained-like weights)",
         "config": {"workload": f"round(Encoder(x)) then Decoder, {B} x {S}x{S}x3, N={N}",
                    "precision": kernels.precision()},
@@ -1031,6 +1043,8 @@ def main() -> None:
     ap.add_argument("--prefetch", type=int, default=4)
     ap.add_argument("--no-bf16-leg", action="store_true",
                     help="x6 eval: skip the bf16 throughput-mode leg reported as bf16_mode")
+    ap.add_argument("--no-x6-leg", action="store_true",
+                    help="h3 eval: skip the x6 (full fp32 operand) leg reported as x6_mode")
     ap.add_argument("--streams", type=int, default=1,
                     help="eval: split the batch over this many HIP streams in the timed region "
                          "(independent images; per-layer timings stay one stream)")
@@ -1146,6 +1160,17 @@ def main() -> None:
         finally:
             kernels.set_precision(prec)
     r = time_eval(net, x, args, world, dev)
+    kernels.check_finite("bench bpp", r["bpp"])   # h3: NaN when an activation did not fit the form
+    rx = None
+    if prec == "h3" and not args.no_x6_leg:
+        # the x6 mode (full fp32 operands: an exact three-part bf16 split, six products per MAC)
+        # on the same batch after the headline, so that a full-fp32-operand rate stays timed on
+        # the driver's box next to the h3 one (reported as x6_mode below)
+        kernels.set_precision("x6")
+        try:
+            rx = time_eval(net, x, args, world, dev)
+        finally:
+            kernels.set_precision(prec)
     nstreams = args.bf16_streams if prec == "bf16" else args.streams
     elapsed, per_layer_ms, bpp = r["elapsed"], r["per_layer_ms"], r["bpp"]
     pixels = world * B * S * S * args.steps
@@ -1166,7 +1191,8 @@ def main() -> None:
         "higher_is_better": True,
         "scaling": "strong" if args.global_batch else "weak",
         "vs_baseline": None,
-        "dtype": "bf16" if prec == "bf16" else "f32",
+        "dtype": DTYPE[prec],
+        "dtype_note": DTYPE_NOTE[prec],
         "data": "synthetic (splitmix64 uint8/255 images, seeded trained-like weights)",
         **layout,
         "config": {"workload": (f"eval encode+decode (round quantiser + rate), {B} x {S}x{S}x3 images per GPU"
@@ -1207,6 +1233,23 @@ def main() -> None:
             "vs_parity_mode": {"parity_mode": prec, "latent_flip_rate": flips / r["y_hat"].numel(),
                       "max_abs_dbpp_per_image": float((rb["bpp_img"] - r["bpp_img"]).abs().max()),
                       "max_abs_dpsnr_db_per_image": float((psnr(rb["clipped"]) - psnr(r["clipped"])).abs().max())},
+        }
+    if rx is not None:
+        dom_x, layers_x, roof_x = roofline(rx["per_layer_ms"], "x6", N, S, B)
+        result["x6_mode"] = {
+            "value": round(pixels / rx["elapsed"] / 1e6, 2), "unit": "Mpix/s",
+            "ms_per_step": round(rx["elapsed"] / args.steps * 1e3, 4), "dtype": DTYPE["x6"],
+            "dtype_note": DTYPE_NOTE["x6"],
+            "roofline": {k: roof_x[k] for k in ("kernel", "achieved", "peak", "peak_basis", "frac",
+                                                  "duration", "profile_mean_ms", "frac_from_profile",
+                                                  "traffic", "traffic_source", "traffic_null_reason",
+                                                  "chain_roofline_frac")
+                         if k in roof_x},
+            "layers": layers_x,
+            "vs_headline": {"latent_flips": int((rx["y_hat"] != r["y_hat"]).sum().item()),
+                            "latents": r["y_hat"].numel(),
+                            "max_abs_rel_dbpp_per_image": float(((rx["bpp_img"] - r["bpp_img"]).abs()
+                                                                 / r["bpp_img"].abs()).max())},
         }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:   # the CPU leg: N=1 only
         # per-pixel cost is size-independent: the sample is 256² images at any --size

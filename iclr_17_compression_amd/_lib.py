@@ -141,7 +141,7 @@ SIGNATURES = {
     "iclr17_analysis_conv3_quant_rate_h3": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P,
                                                  _P, _P, _P, _P]),
     "iclr17_synthesis_deconv3_h3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P, _I,
-                                         _P, _P, _D, _P]),
+                                         _P, _P, _D, _P, _P]),
     "iclr17_synthesis_deconv_igdn_h3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
                                              _I, _I, _P, _P]),
     # bf16 throughput mode (csrc/engine_bf16.hip)

@@ -128,6 +128,7 @@ def analysis_features_train(enc, x: Tensor):
     weight-gradient operands) and the pre-activations; "a2h" (conv3's h3 input) is then set."""
     N = enc.out_channel_N
     if kernels.precision() == "h3":
+        kernels.h3_chain_begin(x.device)
         ge1, ge2 = enc.gdn1.effective_params_h3(), enc.gdn2.effective_params_h3()
         w2h, _ = enc.packed_h3()
         a1h, _, a1s, u1 = kernels.conv1_gdn_h3(x, enc.packed_conv1_h3(), enc.conv1.bias, *ge1, N,
@@ -210,7 +211,8 @@ def synthesis_forward_train(dec, y_nhwc: Tensor, x_ref: Optional[Tensor] = None,
     if kernels.precision() == "h3":
         # the codec's h3 kernels; their x6 outputs are the weight-gradient operands and the
         # pre-activations the IGDN backward's
-        if y_h3 is None:
+        if y_h3 is None:   # the Decoder on its own: its chain starts here
+            kernels.h3_chain_begin(y_nhwc.device)
             y_h3 = kernels.h3_planes(y_nhwc)
         h1, h2 = dec.igdn1.effective_params_h3(), dec.igdn2.effective_params_h3()
         x1, x2, x3 = dec.packed_h3k()

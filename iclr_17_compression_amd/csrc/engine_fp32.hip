@@ -134,8 +134,10 @@ struct EngineArgs {
 // (csrc/aux.hip): per image a lane-strided sum over t ≡ lane (mod 64) in t order, a fixed xor
 // butterfly, then the images added in order by thread 0 — so the results are bit-identical.
 // The loads of a wave's images go out together (one memory latency for the common T ≤ 64).
+// poison: the h3 range flag was set upstream (deconv3_x6_kernel<CI, true>); every total is NaN.
 template <int NTHR>
-__device__ __forceinline__ void fold_bits(const EngineArgs& a, double* img /* LDS, 64 doubles */) {
+__device__ __forceinline__ void fold_bits(const EngineArgs& a, double* img /* LDS, 64 doubles */,
+                                          bool poison = false) {
   constexpr int NW = NTHR / 64, KI = (64 + NW - 1) / NW;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int T = a.fold_T;
@@ -156,6 +158,7 @@ __device__ __forceinline__ void fold_bits(const EngineArgs& a, double* img /* LD
       for (int t = lane + 64; t < T; t += 64) s += a.fold_partial[(long)(b0 + b) * T + t];
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+      if (poison) s = __builtin_nan("");
       if (lane == 0) {
         img[b] = s;
         if (a.fold_per_image) a.fold_per_image[b0 + b] = s;
@@ -1499,7 +1502,12 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
   constexpr int AI_W = (NAI + 3) / 4;   // x6: 16 (wave 0..3 takes i = w + 4j, i < 61)
   static_assert(3 * 64 * 65 <= D3_LDS, "epilogue block fits the stages");
   __shared__ __attribute__((aligned(16))) float smem[D3_LDS];
-  if (a.fold_partial != nullptr && blockIdx.x == 0) fold_bits<256>(a, (double*)smem);
+  // H3: the range flag of the chain (set by an upstream h3 kernel whose output did not fit the
+  // form, |x| ≥ 2²²) makes every result of this last kernel NaN — the reconstruction, the SSE
+  // partials and the folded bit totals — so an out-of-range input can never pass for a result.
+  // The upstream kernels all completed before this launch, so the flag is final here.
+  const bool poison = H3 && a.range != nullptr && *(const volatile int*)a.range != 0;
+  if (a.fold_partial != nullptr && blockIdx.x == 0) fold_bits<256>(a, (double*)smem, poison);
   float* const sA = smem;
   float* const sB = smem + D3_SA;
 
@@ -1698,6 +1706,7 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
           const int co = pcol[nt] >> 4, ph = pcol[nt] & 15;
           float v = acc[mt][nt][r] + a.bias[co];
           if (pass == 0) v = fminf(fmaxf(v, 0.0f), 1.0f);
+          if (poison) v = __builtin_nanf("");
           sO[(co * OS + by * 4 + (ph >> 2)) * SS + bx * 4 + (ph & 3)] = v;
         }
     __syncthreads();
@@ -2812,7 +2821,8 @@ struct FoldBits {
 static int launch_deconv3_halo(const uint16_t* in, int B, int H, int W, int N, const void* w,
                                const float* bias, const float* x, float* clipped, float* recon,
                                double* sse_partial, int sse_unclipped, void* stream, bool bf,
-                               int in_cm = 0, const FoldBits* fold = nullptr, bool h3 = false) {
+                               int in_cm = 0, const FoldBits* fold = nullptr, bool h3 = false,
+                               const int* range_flag = nullptr) {
   const char* what = bf ? "deconv3_bf16" : (h3 ? "deconv3_h3" : "deconv3_x6");
   int rc = check_dims(B, H, W, N);
   if (rc) return rc;
@@ -2847,6 +2857,7 @@ static int launch_deconv3_halo(const uint16_t* in, int B, int H, int W, int N, c
       hipLaunchKernelGGL((deconv3_bf16_kernel<128>), grid, dim3(512), 0, S(stream), a);
   } else if (h3) {
     a.wscale = (const float*)((const uint16_t*)w + 2L * 9 * N * 48);
+    a.range = const_cast<int*>(range_flag);   // read only (the poison check)
     if (N == 192)
       hipLaunchKernelGGL((deconv3_x6_kernel<192, true>), grid, dim3(256), 0, S(stream), a);
     else
@@ -2865,10 +2876,11 @@ int iclr17_synthesis_deconv3_h3(const uint16_t* in_h3_cm, int B, int H, int W, i
                                 float* clipped, float* recon, double* sse_partial,
                                 int sse_unclipped, const double* bits_partial, int bits_T,
                                 double* bits_per_image, float* bpp_total, double bits_scale,
-                                void* stream) {
+                                const int* range_flag, void* stream) {
   const FoldBits f = {bits_partial, bits_T, bits_per_image, bpp_total, bits_scale};
   return launch_deconv3_halo(in_h3_cm, B, H, W, N, w_h3, bias, x, clipped, recon, sse_partial,
-                             sse_unclipped, stream, false, 1, bits_partial ? &f : nullptr, true);
+                             sse_unclipped, stream, false, 1, bits_partial ? &f : nullptr, true,
+                             range_flag);
 }
 
 int iclr17_synthesis_deconv3_x6(const uint16_t* in_split, int B, int H, int W, int N,

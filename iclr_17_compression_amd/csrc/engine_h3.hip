@@ -471,7 +471,10 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
     if (m2 > 0.f && m2 <= 3.40282347e38f) {
       int e;
       frexpf(m2, &e);   // m2 ∈ [2^(e−1), 2^e)
-      ep = 14 - e;
+      // at most 2^100: a pixel whose largest x² is below 2^-86 (a near-zero pixel, or an x² that
+      // underflowed) keeps s_p and the n scale finite (2^(14−e) overflowed to inf for x² < 2^-113
+      // and made the pixel NaN); its x²·s_p then stays below 2^14 and its n is negligible
+      ep = 14 - e < 100 ? 14 - e : 100;
     }
   }
   const float sp = ldexpf(1.0f, ep);
@@ -751,15 +754,16 @@ __device__ __forceinline__ void absmax_body(const float* __restrict__ w, long n,
   unsigned* s = g_absmax_slot[slot];
   if (threadIdx.x == 0) {
     atomicMax(&s[0], __float_as_uint(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]))));
-    // both words are atomics, performed at the memory side: the max lands before the count
-    // once the wave's outstanding memory operations have drained (no L2 write-back fence)
-    __builtin_amdgcn_s_waitcnt(0);
-    last = atomicAdd(&s[1], 1u) == (unsigned)nbx - 1;
+    // the arrival count is an agent-scope acq_rel read-modify-write: its release orders this
+    // workgroup's max before the count, its acquire orders the last workgroup's read of the
+    // maximum after every other arrival (the memory model's guarantee)
+    last = __hip_atomic_fetch_add(&s[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+           (unsigned)nbx - 1;
   }
   __syncthreads();
   if (last && threadIdx.x == 0) {
     trailer[0] = __uint_as_float(atomicExch(&s[0], 0u));
-    atomicExch(&s[1], 0u);
+    __hip_atomic_store(&s[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -786,7 +790,9 @@ __device__ __forceinline__ int h3_weight_exp(float mx) {
   if (!(mx > 0.f) || !(mx <= 3.40282347e38f)) return 0;
   int e;
   frexpf(mx, &e);   // mx = f·2^e, f ∈ [0.5, 1)
-  return 3 - (e - 1);
+  // at most 2^100 (a tensor with max|w| < 2^-97: σ_w = 2^(4−e) would overflow to inf below
+  // 2^-124; its scaled weights then stay below 8 and every scale finite)
+  return 4 - e < 100 ? 4 - e : 100;
 }
 
 // W → two planes, per plane [blocks][2][CO][8] fp16:

@@ -1020,8 +1020,13 @@ __global__ void sum_rows2_kernel(const Rows2 r, int T, int C, int per, unsigned 
       __hip_atomic_store(&ws[(long)blockIdx.y * C + c],
                          ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl], __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_s_waitcnt(0);   // the wave's split row has left for memory
-    if (cl == 0) last = atomicAdd(done, 1u) == gridDim.y - 1;
+    // the arrival is an agent-scope acq_rel read-modify-write: its release orders the wave's
+    // split row (and the other waves' rows, behind the barrier below the stores) before the count,
+    // its acquire orders the last workgroup's loads of every split row after it (the memory
+    // model's guarantee, not the store-ack timing a bare s_waitcnt gives)
+    if (cl == 0)
+      last = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+             gridDim.y - 1;
   }
   __syncthreads();
   if (!last) return;
@@ -1042,7 +1047,7 @@ __global__ void sum_rows2_kernel(const Rows2 r, int T, int C, int per, unsigned 
       o += __hip_atomic_load(&ws[(long)k * C + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     r.out[blockIdx.z][c] = o;
   }
-  if (threadIdx.x == 0) atomicExch(done, 0u);
+  if (threadIdx.x == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Column sums of a [P][C] row-major matrix (NHWC activations): part[chunk][c].

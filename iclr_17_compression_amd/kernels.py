@@ -255,13 +255,15 @@ _precision = os.environ.get("ICLR17_PRECISION", "h3")
 
 
 def precision() -> str:
-    """Inference contraction mode: "h3" (the parity default: fp32 operands as two fp16 parts,
-    three part products per MAC on the f16 MFMA for conv2, conv3, deconv1, deconv2, x6 for conv1,
-    deconv3 and the GDN contractions; fp32-accurate), "x6" (bf16x6 split products on the bf16
-    MFMA everywhere, fp32-accurate), "fp32" (exact-f32 MFMA products) or "bf16" (the throughput
-    mode: bf16 activations and weights, one bf16 product per MAC, fp32 accumulation — no parity
-    claim). Training runs the x6 kernels in the h3, x6 and bf16 modes and exact f32 in the fp32
-    mode."""
+    """Inference contraction mode: "h3" (the parity default: fp32 operands as two fp16 parts —
+    22 significant bits, power-of-two scaled — three part products per MAC on the f16 MFMA with
+    fp32 accumulation for every contraction of the chain: the six convolutions and the four GDN /
+    IGDN channel contractions; |x| ≥ 2^22 does not fit and makes the chain's results NaN, see
+    h3_chain_begin), "x6" (bf16x6 split products on the bf16 MFMA everywhere, full fp32 operands),
+    "fp32" (exact-f32 MFMA products) or "bf16" (the throughput mode: bf16 activations and weights,
+    one bf16 product per MAC, fp32 accumulation — no parity claim). Training: in the h3 mode the
+    forward runs the h3 kernels and the backward the x6 ones; the x6 and bf16 modes train on the
+    x6 kernels, the fp32 mode on the exact-f32 ones."""
     if _precision not in PRECISIONS:
         raise Iclr17Error(f"iclr17: ICLR17_PRECISION must be one of {PRECISIONS} (got {_precision!r})")
     return _precision
@@ -440,28 +442,55 @@ def deconv_igdn_x6(hs: Tensor, wp: Tensor, bias: Tensor, beta_eff: Tensor, gp: T
 # fp16 bit patterns of hi = rne16(x·2^-6) and lo = rne16((x·2^-6 − hi)·2^11) (common.h "h3 form").
 H3_SIGMA_A = 2.0 ** -6
 _range_flags = {}
+H3_RANGE_MESSAGE = ("iclr17: an activation of magnitude >= 2^22 does not fit the h3 form (the "
+                    "chain's results are NaN); run this input with kernels.set_precision('x6')")
 
 
 def h3_range_flag(device) -> Tensor:
-    """The device's h3 range flag (int32, 0 = every value fitted the h3 form so far)."""
+    """The h3 range flag of the current stream on ``device`` (int32, 0 = every value of the
+    current chain fitted the h3 form). One flag per (device, stream), so chains running
+    concurrently on side streams (ImageCompressor.evaluate_many) do not clear each other's."""
     dev = torch.device(device)
     if dev.index is None:
         dev = torch.device("cuda", torch.cuda.current_device())
-    f = _range_flags.get(dev)
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream)
+    f = _range_flags.get(key)
     if f is None:
         f = torch.zeros(1, device=dev, dtype=torch.int32)
-        _range_flags[dev] = f
+        _range_flags[key] = f
     return f
 
 
+def h3_chain_begin(device) -> None:
+    """Clear the current stream's h3 range flag at the start of a chain of h3 kernels (one fill
+    on the stream; no synchronisation). Every producer sets the flag when a value does not fit;
+    the chain's last kernel (deconv3_h3) reads it and writes NaN results when it is set."""
+    h3_range_flag(device).zero_()
+
+
+def h3_range_overflowed(device) -> bool:
+    """Whether the current stream's last h3 chain met a value of magnitude ≥ 2^22.
+    Synchronises with the device."""
+    return int(h3_range_flag(device).item()) != 0
+
+
 def check_h3_range(device) -> None:
-    """Raise (and clear the flag) when an h3 kernel met a value of magnitude ≥ 2^22, which the
-    h3 form cannot hold. Synchronises with the device."""
-    f = h3_range_flag(device)
-    if int(f.item()) != 0:
-        f.zero_()
-        raise Iclr17Error("iclr17: an activation of magnitude >= 2^22 does not fit the h3 form; "
-                          "run this input with kernels.set_precision('x6')")
+    """Raise Iclr17Error when the current stream's last h3 chain met a value of magnitude
+    ≥ 2^22, which the h3 form cannot hold. Synchronises with the device."""
+    if h3_range_overflowed(device):
+        raise Iclr17Error(H3_RANGE_MESSAGE)
+
+
+def check_finite(what: str, *values) -> None:
+    """For callers that read results anyway (the training driver's log, testKodak, bench): raise
+    Iclr17Error when a result is not finite — in the h3 mode the mark of an activation that did
+    not fit the form (the chain's last kernel writes NaN then), or of a non-finite input."""
+    for v in values:
+        t = torch.as_tensor(v)
+        if not bool(torch.isfinite(t).all()):
+            if precision() == "h3":
+                raise Iclr17Error(f"{H3_RANGE_MESSAGE} [{what}]")
+            raise Iclr17Error(f"iclr17: non-finite {what}")
 
 
 def _check_h3(s: Tensor, what: str):
@@ -785,10 +814,13 @@ def deconv3_x6(hs: Tensor, w_split: Tensor, bias: Tensor, x_ref: Optional[Tensor
 
 def deconv3_h3(hs: Tensor, w_h3: Tensor, bias: Tensor, x_ref: Optional[Tensor] = None,
                want_recon: bool = False, sse_unclipped: bool = False,
-               bits: Optional[Tuple[Tensor, float]] = None):
+               bits: Optional[Tuple[Tensor, float]] = None, bits_per_image: bool = False):
     """deconv3 on the chunk-major h3 input [2,B,N/32,H/4,W/4,32] of ``deconv_igdn_h3(chunk_major
     =True)`` (the halo-tiled kernel, three fp16 part products per MAC); w_h3: ``split_packed_h3``
-    of the ICLR17_W_DECONV9 packing (Synthesis_net_17.packed_h3). Returns as ``deconv3_x6``."""
+    of the ICLR17_W_DECONV9 packing (Synthesis_net_17.packed_h3). Returns as ``deconv3_x6``; with
+    ``bits`` and ``bits_per_image`` a fifth value, the per-image bit sums (float64 [B], those of
+    ``reduce_partials``). The chain's h3 range flag (h3_range_flag) is passed: when an upstream
+    h3 kernel met |x| ≥ 2^22 every output is NaN."""
     if (not isinstance(hs, Tensor) or hs.dim() != 6 or hs.dtype != torch.int16 or hs.shape[0] != 2
             or hs.shape[5] != 32 or not hs.is_cuda or not hs.is_contiguous()):
         raise Iclr17Error("iclr17: deconv3_h3 takes a contiguous chunk-major h3 activation "
@@ -810,7 +842,7 @@ def deconv3_h3(hs: Tensor, w_h3: Tensor, bias: Tensor, x_ref: Optional[Tensor] =
             raise Iclr17Error("iclr17: reference image shape mismatch")
         x_ref = x_ref.contiguous()
         partial = torch.empty(B, output_partials_per_image(H, W), device=hs.device, dtype=torch.float64)
-    bp, scale, total = None, 0.0, None
+    bp, scale, total, per = None, 0.0, None, None
     if bits is not None:
         bp, scale = bits
         _check_f64(bp)
@@ -818,10 +850,15 @@ def deconv3_h3(hs: Tensor, w_h3: Tensor, bias: Tensor, x_ref: Optional[Tensor] =
             raise Iclr17Error("iclr17: bit partials are not [B, T]")
         bp = bp.contiguous()
         total = torch.empty((), device=hs.device, dtype=torch.float32)
+        if bits_per_image:
+            per = torch.empty(B, device=hs.device, dtype=torch.float64)
     call("iclr17_synthesis_deconv3_h3", _p(hs), B, H, W, N, _p(w_h3), _p(bias), _p(x_ref),
          _p(clipped), _p(recon), _p(partial), int(sse_unclipped), _p(bp),
-         bp.shape[1] if bp is not None else 0, None, _p(total), ctypes.c_double(scale), _stream(hs))
-    return (clipped, recon, partial) if bits is None else (clipped, recon, partial, total)
+         bp.shape[1] if bp is not None else 0, _p(per), _p(total), ctypes.c_double(scale),
+         _p(h3_range_flag(hs.device)), _stream(hs))
+    if bits is None:
+        return clipped, recon, partial
+    return (clipped, recon, partial, total, per) if bits_per_image else (clipped, recon, partial, total)
 
 
 def _deconv3_halo(fn, hs, B, h4, w4, N, wp, bias, x_ref, want_recon, sse_unclipped, bits=None):

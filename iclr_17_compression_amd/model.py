@@ -67,13 +67,22 @@ class ImageCompressor(nn.Module):
         x = x.contiguous()
         q = self.encode_latents(x, noise, training, want_y)
         y_hat, bits_partial, y_split = q["y_hat"], q["bits_partial"], q["y_split"]
-        clipped, recon, sse_partial = self.Decoder.decode(y_hat, x_ref=x if x_ref_sse else None,
-                                                          want_recon=want_recon, y_split=y_split,
-                                                          y_bf16=q.get("y_bf16"),
-                                                          y_integral=not training,
-                                                          y_h3=q.get("y_h3"))
-        return {"clipped": clipped, "y_hat": y_hat, "bits_partial": bits_partial,
-                "sse_partial": sse_partial, "recon": recon, "y": q["y"]}
+        out = {"y_hat": y_hat, "bits_partial": bits_partial, "y": q["y"]}
+        if q.get("y_h3") is not None:
+            # h3: the per-image bit sums folded into deconv3's kernel, which writes them (and every
+            # other result) as NaN when a value of the chain did not fit the h3 form
+            B, _, H, W = x.shape
+            clipped, recon, sse_partial, _, out["bits_per_image"] = self.Decoder.decode(
+                y_hat, x_ref=x if x_ref_sse else None, want_recon=want_recon,
+                y_integral=not training, y_h3=q["y_h3"], bits=(bits_partial, 1.0 / (B * H * W)),
+                bits_per_image=True)
+        else:
+            clipped, recon, sse_partial = self.Decoder.decode(y_hat, x_ref=x if x_ref_sse else None,
+                                                              want_recon=want_recon, y_split=y_split,
+                                                              y_bf16=q.get("y_bf16"),
+                                                              y_integral=not training)
+        out.update({"clipped": clipped, "sse_partial": sse_partial, "recon": recon})
+        return out
 
     def encode_latents(self, x: torch.Tensor, noise: Optional[torch.Tensor] = None,
                        training: bool = False, want_y: bool = False) -> Dict[str, torch.Tensor]:
@@ -102,6 +111,7 @@ class ImageCompressor(nn.Module):
         if kernels.precision() == "h3":
             # the parity mode on the f16 MFMA: conv1, conv2 and conv3 (and the GDN contractions)
             # in the h3 form (three fp16 part products per MAC), ŷ handed on in the h3 form
+            kernels.h3_chain_begin(x.device)
             e1 = self.Encoder.gdn1.effective_params_h3()
             e2 = self.Encoder.gdn2.effective_params_h3()
             w2h, w3h = self.Encoder.packed_h3()
@@ -232,6 +242,8 @@ class ImageCompressor(nn.Module):
         y_hat = kernels.rans_decode(words, offsets, self.bitEstimator.entropy_tables(K), B, h, w, N,
                                     K, P)
         split = kernels.split_planes(y_hat) if kernels.precision() == "x6" else None
+        if kernels.precision() == "h3":
+            kernels.h3_chain_begin(y_hat.device)
         yh3 = kernels.h3_planes(y_hat) if kernels.precision() == "h3" else None
         ybf = kernels.to_bf16(y_hat) if kernels.precision() == "bf16" else None
         clipped, _, _ = self.Decoder.decode(y_hat, want_recon=False, y_split=split, y_bf16=ybf,
@@ -240,13 +252,37 @@ class ImageCompressor(nn.Module):
 
     @torch.no_grad()
     def evaluate(self, x: torch.Tensor, want_y: bool = False,
-                 want_msssim: bool = False) -> Dict[str, torch.Tensor]:
+                 want_msssim: bool = False, h3_overflow: str = "nan") -> Dict[str, torch.Tensor]:
         """testKodak-style per-image metrics (train.py:157-190): bpp, MSE of the clipped
         reconstruction and PSNR per image, all from deterministic on-device reductions; with
-        ``want_msssim`` also MS-SSIM (train.py:178, on the GPU) and MS-SSIM-DB (train.py:179)."""
+        ``want_msssim`` also MS-SSIM (train.py:178, on the GPU) and MS-SSIM-DB (train.py:179).
+
+        ``h3_overflow`` (the h3 mode: an activation of magnitude ≥ 2^22 does not fit the form):
+        "nan" (default, no host synchronisation) — the reconstruction, bpp, MSE and PSNR of the
+        batch come back NaN; "raise" — read the range flag (one synchronisation) and raise
+        Iclr17Error; "x6" — read it and, when set, evaluate the batch again in the x6 mode (full
+        fp32 operands) and return those results."""
+        if h3_overflow not in ("nan", "raise", "x6"):
+            raise kernels.Iclr17Error(f"iclr17: h3_overflow must be 'nan', 'raise' or 'x6' "
+                                      f"(got {h3_overflow!r})")
+        res = self._evaluate(x, want_y, want_msssim)
+        if h3_overflow != "nan" and kernels.precision() == "h3" and \
+                kernels.h3_range_overflowed(x.device):
+            if h3_overflow == "raise":
+                raise kernels.Iclr17Error(kernels.H3_RANGE_MESSAGE)
+            kernels.set_precision("x6")
+            try:
+                res = self._evaluate(x, want_y, want_msssim)
+            finally:
+                kernels.set_precision("h3")
+        return res
+
+    def _evaluate(self, x, want_y, want_msssim):
         B, _, H, W = x.shape
         out = self.run(x, training=False, x_ref_sse=True, want_y=want_y)
-        bits, _ = kernels.reduce_partials(out["bits_partial"])
+        bits = out.get("bits_per_image")
+        if bits is None:
+            bits, _ = kernels.reduce_partials(out["bits_partial"])
         sse, _ = kernels.reduce_partials(out["sse_partial"])
         bpp = bits / (H * W)
         mse = sse / (3 * H * W)

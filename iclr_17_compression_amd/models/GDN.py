@@ -1,9 +1,11 @@
 """GDN / IGDN module — surface of the reference models/GDN.py:10-94.
 
-Same constructor, parameters (``beta`` [C], ``gamma`` [C, C]) and re-parametrisation; the
-forward runs the fused gfx950 kernel (per-pixel channel contraction β + γ·x² on the exact-f32
-MFMA, then x/√n or x·√n) through libiclr17.so. Effective (bounded, squared) parameters are
-computed by a packing kernel and cached until the parameters change.
+Same constructor, parameters (``beta`` [C], ``gamma`` [C, C]) and re-parametrisation. The module
+called on its own runs the stand-alone gfx950 kernel (per-pixel channel contraction β + γ·x² on
+the exact-f32 MFMA, then x/√n or x·√n) through libiclr17.so; inside the codec's chain the same
+contraction is fused into the producing convolution's epilogue and runs in the chain's precision
+mode (h3 by default: three fp16 part products per MAC; kernels.precision). Effective (bounded,
+squared) parameters are computed by a packing kernel and cached until the parameters change.
 """
 from __future__ import annotations
 

@@ -159,6 +159,7 @@ class Analysis_net_17(nn.Module):
             h = kernels.conv2_gdn_bf16(h, w2b, self.conv2.bias, *e2)
             y = kernels.conv3_quant_rate_bf16(h, w3b, z, ztab, want_y=True)[2]
         elif kernels.precision() == "h3":
+            kernels.h3_chain_begin(x.device)
             e1, e2 = self.gdn1.effective_params_h3(), self.gdn2.effective_params_h3()
             w2h, w3h = self.packed_h3()
             hs, _ = kernels.conv1_gdn_h3(x, self.packed_conv1_h3(), self.conv1.bias, *e1, N)

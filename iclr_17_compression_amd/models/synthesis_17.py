@@ -110,14 +110,16 @@ class Synthesis_net_17(nn.Module):
         return y.permute(0, 2, 3, 1).contiguous()
 
     def decode(self, y_nhwc, x_ref=None, want_recon=True, y_split=None, y_bf16=None,
-               y_integral=False, bits=None, y_h3=None):
+               y_integral=False, bits=None, y_h3=None, bits_per_image=False):
         """NHWC latent → (clipped NCHW, unclipped NCHW | None, SSE partials | None).
         With ``y_split`` (the latent in x6 split form) the three layers run in the x6 mode, with
         ``y_h3`` (the h3 form) the three layers run in the h3 form, with
         ``y_bf16`` (bf16 bit patterns) in the bf16 throughput mode. ``y_integral``: the latent
         is ŷ = round(y) (model.py:56), so the h3 deconv1 takes its integer-input form.
         ``bits`` = (conv3's bit partials, scale): a fourth output, ``reduce_partials``' 0-dim total,
-        computed inside deconv3's kernel in the x6 and bf16 modes (one launch fewer)."""
+        computed inside deconv3's kernel in the h3, x6 and bf16 modes (one launch fewer); h3 with
+        ``bits_per_image``: a fifth, the per-image sums. In the h3 mode every output is NaN when a
+        value of the chain (since the last kernels.h3_chain_begin) did not fit the h3 form."""
         d1, d2, d3, g1, g2 = self.packed()
         if y_bf16 is not None:
             b1, b2, b3 = self.packed_bf16()
@@ -134,7 +136,7 @@ class Synthesis_net_17(nn.Module):
             hs, _, _ = kernels.deconv_igdn_h3(y_h3, w1, self.deconv1.bias, *q1, int_in=y_integral)
             hs, _, _ = kernels.deconv_igdn_h3(hs, w2, self.deconv2.bias, *q2, chunk_major=True)
             return kernels.deconv3_h3(hs, w3, self.deconv3.bias, x_ref=x_ref, want_recon=want_recon,
-                                      bits=bits)
+                                      bits=bits, bits_per_image=bits_per_image)
         if y_split is not None:
             q1, q2 = self.igdn1.effective_params_x6(), self.igdn2.effective_params_x6()
             hs, _, _ = kernels.deconv_igdn_x6(y_split, d1, self.deconv1.bias, *q1)
@@ -159,6 +161,8 @@ class Synthesis_net_17(nn.Module):
             return SynthesisFn.apply(x, self, *params)
         y = self.to_nhwc(x)
         split = kernels.split_planes(y) if kernels.precision() == "x6" else None
+        if kernels.precision() == "h3":
+            kernels.h3_chain_begin(y.device)
         yh3 = kernels.h3_planes(y) if kernels.precision() == "h3" else None
         ybf = kernels.to_bf16(y) if kernels.precision() == "bf16" else None
         _, recon, _ = self.decode(y, want_recon=True, y_split=split, y_bf16=ybf, y_h3=yh3)

@@ -529,13 +529,16 @@ int iclr17_analysis_conv3_quant_rate_h3(const uint16_t* in_h3, int B, int H, int
  * [2][B][N/32][H/4][W/4][32] (iclr17_synthesis_deconv_igdn_h3 with out_cm) → clipped NCHW fp32
  * (+ unclipped, + SSE partials as iclr17_synthesis_deconv3); w_h3: iclr17_split_packed_h3 of the
  * ICLR17_W_DECONV9 packing (taps 9, K N, columns 48). bits_partial non-NULL: the bit reduction
- * folded in as iclr17_synthesis_deconv3_x6_cm_bits (bits_per_image nullable). */
+ * folded in as iclr17_synthesis_deconv3_x6_cm_bits (bits_per_image nullable). range_flag
+ * (nullable, read only): the chain's h3 range flag; when it is set (an upstream h3 kernel met
+ * |x| ≥ 2^22) every output of this call — clipped, recon, SSE partials, bit totals — is NaN, so
+ * the out-of-range result is loud without a host synchronisation. */
 int iclr17_synthesis_deconv3_h3(const uint16_t* in_h3_cm, int B, int H, int W, int N,
                                 const uint16_t* w_h3, const float* bias, const float* x,
                                 float* clipped, float* recon, double* sse_partial,
                                 int sse_unclipped, const double* bits_partial, int bits_T,
                                 double* bits_per_image, float* bpp_total, double bits_scale,
-                                void* stream);
+                                const int* range_flag, void* stream);
 /* synthesis_17.py:15-22 deconv + IGDN on the h3 engine: input [2][B][h][w][N] → fp32 NHWC
  * [B][2h][2w][N] and/or the h3 output [2][B][2h][2w][N] (chunk-major [2][B][N/32][2h][2w][32]
  * with out_cm) and/or the x6 split output [3][B][2h][2w][N] (NHWC always) — each nullable, not

@@ -2,8 +2,8 @@
 
 * C3 — one training step at its production size, B = 32 crops of 256×256, N = 192, λ = 0.01
   (train_lambda 650.25), fixed noise: the loss terms and all 30 parameter gradients against the
-  oracle's autograd (oracle/codec_ref.py, pinned to the reference's autograd by G4), in the x6
-  and exact-f32 modes. These are the kernels' real launch shapes (split-K partial counts, grid
+  oracle's autograd (oracle/codec_ref.py, pinned to the reference's autograd by G4), in the h3
+  (the default: h3 forward, x6 backward), x6 and exact-f32 modes. These are the kernels' real launch shapes (split-K partial counts, grid
   sizing, partial-sum trees at 32×64²), which the small-shape tests do not reach.
 * Data-parallel semantics (train.py:228 DataParallel → one process per GPU): the
   gradient of the full batch equals the mean of the gradients of its two equal shards, i.e. the
@@ -63,7 +63,7 @@ def c3_case():
             "grads": grads}
 
 
-@pytest.mark.parametrize("precision", ["x6", "fp32"])
+@pytest.mark.parametrize("precision", ["h3", "x6", "fp32"])
 def test_c3_train_step_full_size(device, c3_case, precision):
     old = kernels.precision()
     kernels.set_precision(precision)
@@ -82,7 +82,8 @@ def test_c3_train_step_full_size(device, c3_case, precision):
     assert loss.item() == pytest.approx(c3_case["loss"], rel=METRIC_REL)
     errs = {k: grad_err(p.grad, c3_case["grads"][k]) for k, p in net.named_parameters()}
     print(f"C3 {precision}: max rel grad err {max(errs.values()):.3e} "
-          f"({max(errs, key=errs.get)})")
+          f"({max(errs, key=errs.get)}); rel mse {abs(mse.item() / c3_case['mse'] - 1):.2e}, "
+          f"rel bpp {abs(bpp.item() / c3_case['bpp'] - 1):.2e}")
     bad = {k: e for k, e in errs.items() if not e < GRAD_REL}
     assert not bad, bad
 

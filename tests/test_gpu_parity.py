@@ -433,30 +433,39 @@ def test_errors_are_loud(device):
 
 def test_c5_2048_full_size_properties(device):
     """C5's full image size (2048×2048, N=192), through properties that do not need a CPU
-    reference of that size: the x6 and exact-f32 modes agree (latents bit for bit except at
-    near-ties of the fp32 y, bpp / PSNR within 1e-5 relative); an image's results do not depend on
-    its batch; compress → decompress returns the latents and reconstruction bit for bit."""
+    reference of that size: the h3 (the default) and x6 modes each agree with the exact-f32 mode
+    (latents bit for bit except at near-ties of the fp32 y, bpp / PSNR within 1e-5 relative); an
+    image's results do not depend on its batch; compress → decompress returns the latents and
+    reconstruction bit for bit. At 2048² the activations are 512² per channel, where the h3 range
+    flag (|x| ≥ 2^22) matters most: it must stay clear."""
     net = net_for(192, 1, device)
     x = image(41, 2, 2048, 2048).to(device)
     old = kernels.precision()
+    res = {}
     try:
         kernels.set_precision("fp32")
         ev32 = net.evaluate(x[:1], want_y=True)
-        kernels.set_precision("x6")
-        ev6 = net.evaluate(x[:1], want_y=True)
-        ev6b = net.evaluate(x)                         # the same image inside a batch of two
-        enc = net.compress(x[:1])
-        dec = net.decompress(enc["strings"], enc["shape"])
+        for mode in ("h3", "x6"):
+            kernels.set_precision(mode)
+            ev = net.evaluate(x[:1], want_y=True)
+            evb = net.evaluate(x)                      # the same image inside a batch of two
+            enc = net.compress(x[:1])
+            dec = net.decompress(enc["strings"], enc["shape"])
+            res[mode] = (ev, evb, dec)
+        kernels.check_h3_range(device)
     finally:
         kernels.set_precision(old)
-    n = check_latents(ev6["y_hat"], ev6["y"], ev32["y_hat"].cpu(), ev32["y"].cpu())
-    print("x6 vs fp32 near-tie flips at 2048²:", n)
-    assert ev6["bpp"].item() == pytest.approx(ev32["bpp"].item(), rel=METRIC_REL)
-    assert ev6["psnr"].item() == pytest.approx(ev32["psnr"].item(), rel=METRIC_REL)
-    for k in ("y_hat", "bpp", "clipped"):
-        assert torch.equal(ev6b[k][0], ev6[k][0]), k
-    assert torch.equal(dec["y_hat"].cpu(), ev6["y_hat"].cpu())
-    assert torch.equal(dec["x_hat"].cpu(), ev6["clipped"].cpu())
+    for mode, (ev, evb, dec) in res.items():
+        n = check_latents(ev["y_hat"], ev["y"], ev32["y_hat"].cpu(), ev32["y"].cpu())
+        print(f"{mode} vs fp32 near-tie flips at 2048²: {n}; rel bpp "
+              f"{abs(ev['bpp'].item() / ev32['bpp'].item() - 1):.2e}, rel PSNR "
+              f"{abs(ev['psnr'].item() / ev32['psnr'].item() - 1):.2e}")
+        assert ev["bpp"].item() == pytest.approx(ev32["bpp"].item(), rel=METRIC_REL)
+        assert ev["psnr"].item() == pytest.approx(ev32["psnr"].item(), rel=METRIC_REL)
+        for k in ("y_hat", "bpp", "clipped"):
+            assert torch.equal(evb[k][0], ev[k][0]), (mode, k)
+        assert torch.equal(dec["y_hat"].cpu(), ev["y_hat"].cpu()), mode
+        assert torch.equal(dec["x_hat"].cpu(), ev["clipped"].cpu()), mode
 
 
 def test_batched_packs_match_single(device):
@@ -523,7 +532,7 @@ def test_batched_h3_packs_match_single(device, N):
     assert float(batched[-1][-8:].view(torch.float32)[0]) == 0.0   # max|w| of the zero tensor
 
 
-@pytest.mark.parametrize("mode", ["x6", "fp32", "bf16"])
+@pytest.mark.parametrize("mode", ["h3", "x6", "fp32", "bf16"])
 def test_encoder_matches_codec_forward(device, mode):
     """The separate encode / decode path (NewTests/testReconSeperateEandD.py:67-68): in every
     precision ``torch.round(net.Encoder(x))`` is bitwise the codec forward's ŷ, the latents are
@@ -546,7 +555,7 @@ def test_encoder_matches_codec_forward(device, mode):
     assert torch.equal(recon.clamp(0.0, 1.0), clipped)
 
 
-@pytest.mark.parametrize("mode", ["x6", "fp32", "bf16"])
+@pytest.mark.parametrize("mode", ["h3", "x6", "fp32", "bf16"])
 def test_encoder_with_grad_matches_codec_forward(device, mode):
     """NewTests/testReconSeperateEandD.py:67 calls ``torch.round(net.Encoder(x))`` with autograd
     ON, which takes AnalysisFn: its y must be the codec's own (same analysis kernels), contiguous

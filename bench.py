@@ -645,7 +645,7 @@ def run_codec(args, dev):
         y = kernels.rans_decode(words, offsets, cum, B, h, w, N)
         e2.record()
         split = kernels.split_planes(y) if kernels.precision() == "x6" else None
-        yh3 = kernels.h3_planes(y) if kernels.precision() == "h3" else None
+        yh3 = kernels.h3_planes(y, cm=kernels.DECONV_CM) if kernels.precision() == "h3" else None
         clipped, _, _ = net.Decoder.decode(y, want_recon=False, y_split=split, y_integral=True,
                                            y_h3=yh3)
         if timed:

@@ -133,13 +133,15 @@ SIGNATURES = {
     "iclr17_h3k_weight_size": (_SZ, [_I, _I]),
     "iclr17_pack_h3k": (_I, [_I, _P, _P, _I, _P]),
     "iclr17_h3_planes": (_I, [_P, ctypes.c_long, _P, _P, _P]),
+    "iclr17_h3_planes_cm": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "iclr17_split_packed_h3_size": (_SZ, [_I, _I, _I]),
     "iclr17_split_packed_h3": (_I, [_P, _I, _I, _I, _P, _P]),
     "iclr17_pack_h3_batch": (_I, [_P, _I, _P]),
-    "iclr17_analysis_conv1_gdn_h3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
-    "iclr17_analysis_conv2_gdn_h3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "iclr17_analysis_conv1_gdn_h3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P]),
+    "iclr17_analysis_conv2_gdn_h3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P]),
+    "iclr17_conv3_h3_partials_per_image": (_I, [_I, _I, _I, _I, _I]),
     "iclr17_analysis_conv3_quant_rate_h3": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P,
-                                                 _P, _P, _P, _P]),
+                                                 _P, _I, _P, _P, _P]),
     "iclr17_synthesis_deconv3_h3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P, _I,
                                          _P, _P, _D, _P, _P]),
     "iclr17_synthesis_deconv_igdn_h3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,

@@ -213,7 +213,7 @@ def synthesis_forward_train(dec, y_nhwc: Tensor, x_ref: Optional[Tensor] = None,
         # pre-activations the IGDN backward's
         if y_h3 is None:   # the Decoder on its own: its chain starts here
             kernels.h3_chain_begin(y_nhwc.device)
-            y_h3 = kernels.h3_planes(y_nhwc)
+            y_h3 = kernels.h3_planes(y_nhwc, cm=kernels.DECONV_CM)
         h1, h2 = dec.igdn1.effective_params_h3(), dec.igdn2.effective_params_h3()
         x1, x2, x3 = dec.packed_h3k()
         s1h, _, s1s, v1 = kernels.deconv_igdn_h3(y_h3, x1, dec.deconv1.bias, *h1, want_x6=True,

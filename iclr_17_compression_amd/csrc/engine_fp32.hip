@@ -2584,19 +2584,7 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
     constexpr int WN = (BN / 16) % 4 == 0 ? 4 : 2, WM = 4 / WN;
     a.partials_per_image = a.tiles_x * a.tiles_y * (N / BN);
     dim3 grid(a.tiles_x * a.tiles_y * B, N / BN);
-    if (H3in) {   // the h3 form: BN-column tiles, or the narrow ones under conv3_narrow
-      if constexpr (N == 192) {
-        if (conv3_narrow(N, a.tiles_x * a.tiles_y, B, qmode)) {
-          a.partials_per_image = a.tiles_x * a.tiles_y * (N / 48);
-          hipLaunchKernelGGL((engine_kernel<N, N, 48, 4, 1, EPI_QUANT, false, true, true>),
-                             dim3(a.tiles_x * a.tiles_y * B, N / 48), dim3(256), 0, st, a);
-          return check_launch("conv3_quant_rate_h3 (48-column tiles)");
-        }
-      }
-      hipLaunchKernelGGL((engine_kernel<N, N, BN, WM, WN, EPI_QUANT, false, true, true>), grid,
-                         dim3(256), 0, st, a);
-      return check_launch("conv3_quant_rate_h3");
-    }
+    ICLR17_REQUIRE(!H3in, ICLR17_EINVAL, "conv3: the h3 form runs on the h3 engine (engine_h3.hip)");
     if constexpr (N == 192) {
       if (X6in && conv3_narrow(N, a.tiles_x * a.tiles_y, B, qmode)) {
         a.partials_per_image = a.tiles_x * a.tiles_y * (N / 48);
@@ -3075,32 +3063,6 @@ int iclr17_analysis_conv3_quant_rate_x6w(const uint16_t* in_split, int B, int H,
   io.w6_plane = 25L * N * N;
   return N == 192 ? launch_conv5<192, EPI_QUANT>(nullptr, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io, rate_table)
                   : launch_conv5<128, EPI_QUANT>(nullptr, B, h, w, w_packed, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io, rate_table);
-}
-
-int iclr17_analysis_conv3_quant_rate_h3(const uint16_t* in_h3, int B, int H, int W, int N,
-                                        const uint16_t* w_h3, int quant_mode, const float* noise,
-                                        const float* rate_packed, const float* rate_table,
-                                        float* y_out, float* y_hat, uint16_t* y_hat_h3,
-                                        double* bits_partial, int* range_flag, void* stream) {
-  int rc = check_dims(B, H, W, N);
-  if (rc) return rc;
-  ICLR17_REQUIRE(in_h3 && w_h3 && rate_packed && y_hat && bits_partial, ICLR17_EINVAL,
-                 "conv3_quant_rate_h3: null pointer");
-  ICLR17_REQUIRE(quant_mode == ICLR17_QUANT_ROUND || (quant_mode == ICLR17_QUANT_NOISE && noise),
-                 ICLR17_EINVAL, "conv3_quant_rate_h3: bad quant mode %d / missing noise", quant_mode);
-  const int h = H / 8, w = W / 8;
-  SplitIO io;
-  io.h3 = true;
-  io.in = (const unsigned short*)in_h3;
-  io.in_plane = (long)B * h * w * N;
-  io.out_h3 = (unsigned short*)y_hat_h3;
-  io.out_h3_plane = (long)B * (h / 2) * (w / 2) * N;
-  io.w6 = (const unsigned short*)w_h3;
-  io.w6_plane = 25L * N * N;
-  io.wscale = (const float*)(w_h3 + 2 * io.w6_plane);
-  io.range = range_flag;
-  return N == 192 ? launch_conv5<192, EPI_QUANT>(nullptr, B, h, w, nullptr, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io, rate_table)
-                  : launch_conv5<128, EPI_QUANT>(nullptr, B, h, w, nullptr, nullptr, nullptr, nullptr, y_out, nullptr, quant_mode, noise, rate_packed, y_hat, bits_partial, S(stream), nullptr, &io, rate_table);
 }
 
 static int deconv_igdn_x6(const uint16_t* in_split, int B, int h, int w, int N,

@@ -27,6 +27,8 @@
 // registers), y = x·√(β + n) | x / √(β + n), and y stored
 // as fp32 and/or in the h3 form (NHWC, or chunk-major [2][B][N/32][h][w][32]) and/or the x6
 // split form.
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <atomic>
@@ -39,7 +41,11 @@ namespace iclr17 {
 namespace h3k {
 using namespace bfm;
 
+// One zero line for the padding loads and the zero pieces of the halo patches. (Measured: every
+// wave reading its own 1 KB of a 64 KB zero table instead made conv2 0.345 → 0.46 ms and deconv2
+// 0.415 → 0.45 ms — the one hot, coalesced line is effectively free.)
 __device__ __attribute__((aligned(16))) unsigned g_zero16h[4] = {0u, 0u, 0u, 0u};
+__device__ __forceinline__ const void* zero16(int) { return g_zero16h; }
 
 // padding load of the counted-vmcnt DMA schedule (4 bytes per lane into the sink)
 __device__ __forceinline__ void sink4(void* lds_sink) {
@@ -52,7 +58,9 @@ __device__ __forceinline__ f16v mfma32h(const u4& a, const u4& b, const f16v& c)
                                                 __builtin_bit_cast(h8v, b), c, 0, 0, 0);
 }
 
-enum HEpi : int { HE_GDN = 0, HE_IGDN = 1 };
+// HE_QUANT: conv3 (analysis_17.py:22, no bias) + the quantiser and rate of model.py:48-56,71-73
+// (the engine_fp32.hip EPI_QUANT epilogue's arithmetic), on an output-channel slice of COT channels
+enum HEpi : int { HE_GDN = 0, HE_IGDN = 1, HE_QUANT = 2 };
 
 struct HArgs {
   const u16* in;        // h3 input [2][B][Hin][Win][CI] (fp16 bits)
@@ -69,11 +77,20 @@ struct HArgs {
   float* out;           // fp32 NHWC [B][Hout][Wout][CO] or null
   float* pre;           // the GDN / IGDN input x = conv + bias, fp32 NHWC, or null (training)
   u16* out_h3;          // h3 output: NHWC [2][B][Hout][Wout][CO] or chunk-major (out_cm)
-  long out_h3_plane;    //   [2][B][CO/32][Hout][Wout][32]
+  long out_h3_plane;    //   [2][B][CO/out_cm][Hout][Wout][out_cm]
   u16* out_x6;          // x6 split output (NHWC, 3 planes) or null
   long out_x6_plane;
-  int out_cm;
+  int out_cm;           // the h3 output's chunk-major chunk: 0 (NHWC), 8, 16 or 32
   int* range;           // set to 1 when a value does not fit the h3 form (nullable)
+  // HE_QUANT (conv3 + quantiser + rate): out = y (nullable), yhat = ŷ | ỹ fp32 NHWC, out_h3 = ŷ in
+  // the h3 form (nullable), bits partial sums [B][T] (T = tiles · channel groups)
+  int qmode;
+  const float* noise;   // NCHW [B][CO][Hout][Wout] (noise mode)
+  const float* rate;    // packed [11][CO]
+  const float* rtab;    // round mode, nullable: element_bits of −32..32 [CO][65]
+  float* yhat;
+  double* partial;
+  int T;
   int B, Hin, Win, Hout, Wout;
   int gh, gw;           // base grid (conv: output grid; deconv: input grid)
   int tiles_x, tiles_y;
@@ -159,13 +176,138 @@ struct HK {
   static constexpr int BBOFF = (LDS0 + 1023) / 1024 * 1024;
   static constexpr int LDS = BBOFF + 2048 + 256;   // + bias, β_eff, the epilogue's sink
   static_assert(SB % 1024 == 0, "weight stage");
-  static_assert(NT % 2 == 0 && (C1 || CI % CCH == 0), "tile shape");
+  static_assert(C1 || CI % CCH == 0, "tile shape");
   static_assert(LDS <= 160 * 1024, "LDS");
 };
 
-template <int MODE, int TH, int CO, int CI, int EPI, bool INT_IN, int PH>
-__device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, int b, int ty, int tx) {
-  using KK = HK<MODE, TH, CO, CI, INT_IN>;
+// COT: the output channels of this workgroup (channel group cg: cg·COT .. cg·COT + COT − 1 of CO;
+// COT < CO only for HE_QUANT, whose epilogue needs no other channel of the pixel). SEP: two-level
+// accumulation — each input chunk's K = 200 products summed from zero in a chain of their own and
+// added to the total with one VALU add (the MFMA chain rounds at the scale of its running sum;
+// conv3's output is rounded into ŷ).
+// u16 offset (within a plane) of 8 channels ch .. ch + 7 of output pixel (oy, ox) of image b in the
+// h3 output's layout: NHWC (out_cm = 0) or chunk-major [B][CO/out_cm][Hout][Wout][out_cm]
+__device__ __forceinline__ long h3_out_off(const HArgs& a, int b, int oy, int ox, int CO, int ch) {
+  const int cm = a.out_cm;
+  if (cm == 0) return (((long)b * a.Hout + oy) * a.Wout + ox) * CO + ch;
+  return ((((long)b * (CO / cm) + ch / cm) * a.Hout + oy) * a.Wout + ox) * cm + ch % cm;
+}
+
+// conv3's epilogue (HE_QUANT): y = acc·2⁻¹¹/(σ_a·σ_w) (no bias, analysis_17.py:22), then
+// model.py:48-56 — ŷ = rint(y) (round) or ỹ = y + u (noise, u from the NCHW noise tensor) — and
+// the rate of model.py:71-73 per element (the rate table's lookup for integers |ŷ| ≤ 32 in round
+// mode; element_bits otherwise, evaluated after the lookups as in engine_fp32.hip's EPI_QUANT: a
+// per-element branch inlines 2 KB of element_bits per element). Outputs: ŷ fp32 NHWC, y fp32
+// (nullable), ŷ in the h3 form (nullable; 16-byte stores after permlane32 swaps as the GDN
+// epilogue's), and the workgroup's bit sum — lanes in (tile, register) order, the xor tree of
+// wave_sum, the waves in order in double — at partial[b][tile · (CO / COT) + cg].
+template <int TH, int CO, int COT>
+__device__ __forceinline__ void quant_epilogue(const HArgs& a, f16v (&acc)[COT / 32],
+                                               unsigned char* lds0, unsigned char* scratch, int b,
+                                               int ty, int tx, int cg) {
+  constexpr int NT = COT / 32, NW = TH / 2;
+  const int etid = fresh_tid(), elane = etid & 63, er32 = elane & 31, eh = elane >> 5;
+  const int ewave = __builtin_amdgcn_readfirstlane(etid >> 6);
+  const int gy = ty * TH + 2 * ewave + (er32 >> 4), gx = tx * 16 + (er32 & 15);
+  const bool inside = gy < a.gh && gx < a.gw;
+  const long o = ((long)b * a.Hout + gy) * a.Wout + gx;
+  const float dsc = a.wscale[1];
+  const bool round = a.qmode == ICLR17_QUANT_ROUND;
+  const bool table = a.rtab != nullptr && round;
+  // the slow path's lane-private rows in LDS (the main loop's stages, free now): 16 latents and
+  // their bits (128 bytes per lane), so that element_bits sits in a rolled loop (one inlined copy
+  // per tile, not one per element)
+  float* const lq = (float*)lds0 + etid * 32;
+  float bits = 0.f;
+  bool ovf = false;
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    const int c0 = cg * COT + 32 * i;
+    float q[16], bv[16];
+    bool slow = false;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int c = c0 + 8 * (r >> 2) + 4 * eh + (r & 3);
+      const float y = acc[i][r] * dsc;   // a power of two: exact
+      acc[i][r] = y;
+      const float yh = round ? rintf(y)
+                             : y + (inside ? a.noise[(((long)b * CO + c) * a.Hout + gy) * a.Wout + gx] : 0.f);
+      q[r] = yh;
+      bv[r] = table ? a.rtab[c * 65 + (int)fminf(fmaxf(yh, -32.f), 32.f) + 32] : 0.f;
+      slow |= inside && !(table && fabsf(yh) <= 32.f);
+    }
+    if (slow) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) lq[r] = q[r];
+#pragma unroll 1
+      for (int r = 0; r < 16; ++r) {
+        const float v = lq[r];
+        if (!(table && fabsf(v) <= 32.f))
+          lq[16 + r] = element_bits(v, a.rate, CO, c0 + 8 * (r >> 2) + 4 * eh + (r & 3));
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (!(table && fabsf(q[r]) <= 32.f)) bv[r] = lq[16 + r];
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) bits += inside ? bv[r] : 0.f;
+    f4 yq[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      yq[m] = f4{q[4 * m], q[4 * m + 1], q[4 * m + 2], q[4 * m + 3]};
+      if (inside) {
+        *(f4*)(a.yhat + o * CO + c0 + 8 * m + 4 * eh) = yq[m];
+        if (a.out)
+          *(f4*)(a.out + o * CO + c0 + 8 * m + 4 * eh) =
+              f4{acc[i][4 * m], acc[i][4 * m + 1], acc[i][4 * m + 2], acc[i][4 * m + 3]};
+      }
+    }
+    if (a.out_h3) {
+      uint2 hb[4], lb[4];
+      bool ov = false;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) h3_split4(yq[m], hb[m], lb[m], ov);
+      ovf |= inside && ov;
+      u4 sv[2][2];
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const uint2 A = pl ? lb[k] : hb[k], Bv = pl ? lb[k + 2] : hb[k + 2];
+          const auto sx = __builtin_amdgcn_permlane32_swap(A.x, Bv.x, false, false);
+          const auto sy = __builtin_amdgcn_permlane32_swap(A.y, Bv.y, false, false);
+          sv[pl][k] = u4{sx[0], sy[0], sx[1], sy[1]};
+        }
+      if (inside) {
+        const long s0 = h3_out_off(a, b, gy, gx, CO, c0 + 16 * eh);
+        const long s1 = h3_out_off(a, b, gy, gx, CO, c0 + 16 * eh + 8);
+        *(u4*)(a.out_h3 + s0) = sv[0][0];
+        *(u4*)(a.out_h3 + s1) = sv[0][1];
+        *(u4*)(a.out_h3 + a.out_h3_plane + s0) = sv[1][0];
+        *(u4*)(a.out_h3 + a.out_h3_plane + s1) = sv[1][1];
+      }
+    }
+  }
+  if (ovf && a.range) atomicOr(a.range, 1);   // vector atomic, per offending lane (rare)
+  bits = wave_sum(bits);
+  float* sw = (float*)scratch;
+  if (elane == 0) sw[ewave] = bits;
+  __syncthreads();
+  if (etid == 0) {
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) t += (double)sw[w];
+    a.partial[(long)b * a.T + (ty * a.tiles_x + tx) * (CO / COT) + cg] = t;
+  }
+}
+
+// ICM: the input's chunk-major chunk (the layout of the h3 form below; 0: NHWC, conv1's image).
+template <int MODE, int TH, int CO, int CI, int EPI, bool INT_IN, int PH, int COT = CO,
+          bool SEP = false, int ICM = 0>
+__device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, int b, int ty, int tx,
+                                         int cg = 0) {
+  static_assert(CO % COT == 0 && (COT == CO || EPI == HE_QUANT), "channel groups: conv3 only");
+  using KK = HK<MODE, TH, COT, CI, INT_IN>;
   using P = typename KK::P;
   constexpr bool CONV = MODE != BM_DECONV, C8 = MODE == HM_CONV8, C1 = MODE == HM_CONV1;
   using TP = Taps<CONV ? BM_CONV : BM_DECONV, PH>;
@@ -193,6 +335,12 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
   const long img = (long)b * a.Hin * a.Win;
   const int iy0 = CONV ? 2 * ty * TH - 2 : ty * TH - 1;
   const int ix0 = CONV ? 2 * tx * 16 - 2 : tx * 16 - 1;
+  // input layout: chunk-major [2][B][CI/ICM][h][w][ICM] with ICM = the chunk's channels, so a
+  // patch piece (one pixel's 8 channels) is 16 bytes of a contiguous run of pixels, not 16 bytes
+  // of a 384-byte NHWC pixel (a cache line per piece: conv2 −8 %, conv3 −23 % measured)
+  static_assert(ICM == 0 || ICM == KK::CCH, "chunk-major input: one chunk per layout chunk");
+  const long cstride = ICM ? (long)a.Hin * a.Win * ICM : KK::CCH;   // u16 per chunk
+  constexpr int PXS = ICM ? ICM : CI;                                 // u16 per pixel
   const u16* __restrict__ inb = a.in + img * CI;
   // patch piece `piece` (1 KB): this lane's 16-byte slot → source u16 offset, or -1 (zeros)
   auto piece_src = [&](int piece) -> long {
@@ -220,7 +368,7 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
     }
     const int iy = iy0 + pr, ix = ix0 + pc;
     ok = ok && pl < KK::PL && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
-    return ok ? pl * a.in_plane + (long)(iy * a.Win + ix) * CI + 8 * hh : -1;
+    return ok ? pl * a.in_plane + (long)(iy * a.Win + ix) * PXS + 8 * hh : -1;
   };
   auto issue_piece = [&](int c1, int piece, bool valid) {
     if (!valid) {
@@ -228,7 +376,7 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
       return;
     }
     const long src = piece_src(piece);
-    glds16(src >= 0 ? (const void*)(inb + src + c1 * KK::CCH) : (const void*)g_zero16h,
+    glds16(src >= 0 ? (const void*)(inb + src + c1 * cstride) : zero16(lane),
            sP + (c1 & 1) * KK::PBUF + piece * 1024);
   };
   // weights of this phase: per plane [NCH][S][2][CO][8]; the step's stage [plane][2][CO][8]
@@ -243,12 +391,13 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
     }
     wph += off;
   }
-  long wsrc[K];   // slot k of a step: plane + unit offset (16-byte units of [2][CO])
+  int wsrc[K];   // slot k of a step: plane + unit offset (16-byte units of [2][CO]; the stage
+                // holds units (half, cg·COT .. cg·COT + COT − 1) as [2][COT]); < 2^31 elements
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int q = (k * NW + wave) * 64 + lane;
-    const int pl = q / (2 * CO), u = q - pl * (2 * CO);
-    wsrc[k] = pl * a.w_plane + (long)u * 8;
+    const int pl = q / (2 * COT), u = q - pl * (2 * COT), hu = u / COT;
+    wsrc[k] = (int)(pl * a.w_plane) + (hu * CO + cg * COT + (u - hu * COT)) * 8;
   }
   auto issue_w = [&](int k, int wg) {
     const int slot = k * NW + wave;
@@ -274,10 +423,10 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
     else return P::template tap_off<PH>(s);
   };
   // A (weights): stage [plane][2][CO][8]: lane (k-group h, channel 32·i + r32)
-  const int abase = (h * CO + r32) * 16;
-  constexpr int APL = 2 * CO * 16;   // stage bytes per plane
+  const int abase = (h * COT + r32) * 16;
+  constexpr int APL = 2 * COT * 16;   // stage bytes per plane
 
-  f16v acc[NT];
+  f16v acc[NT], cacc[NT];   // cacc: SEP's chunk sums (unused otherwise)
 #pragma unroll
   for (int i = 0; i < NT; ++i)
 #pragma unroll
@@ -286,9 +435,9 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
   // prologue: bias and β_eff (waves 0 / 1), chunk 0's patch, the weights of steps 0 .. F-1, then
   // step F's weights as a full K-group and F-1 sink groups (the first wait keeps F in flight)
   static_assert(CO <= 256, "bias / β stage");
-  if (wave < 2) {
+  if (EPI != HE_QUANT && wave < 2) {
     const float* src = wave == 0 ? a.bias : a.beta;
-    glds16(lane * 4 < CO ? (const void*)(src + lane * 4) : (const void*)g_zero16h, sbb + wave * 256);
+    glds16(lane * 4 < CO ? (const void*)(src + lane * 4) : zero16(lane), sbb + wave * 256);
   }
   for (int piece = wave; piece < KK::NQI; piece += NW) issue_piece(0, piece, true);
 #pragma unroll
@@ -403,6 +552,12 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
   Frag cur;
   int stage = 1;   // stage of step g+1
   for (int c = 0; c < NCH; ++c) {
+    if constexpr (SEP) {
+#pragma unroll
+      for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) cacc[i][j] = 0.f;
+    }
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       const int g = c * S + s;
@@ -416,10 +571,12 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
       stage = stage + 1 == NST ? 0 : stage + 1;
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
-        f16v t = acc[i];
+        f16v t = SEP ? cacc[i] : acc[i];
         if constexpr (!INT_IN) t = mfma32h(cur.wh[i], cur.bl, t);
         t = mfma32h(cur.wl[i], cur.bh, t);
-        acc[i] = mfma32h(h3_x2048(cur.wh[i]), cur.bh, t);
+        t = mfma32h(h3_x2048(cur.wh[i]), cur.bh, t);
+        if constexpr (SEP) cacc[i] = t;
+        else acc[i] = t;
       }
       // the step's DMA group after the fragment reads: an LDS read after an LDS-DMA of unknown
       // destination makes the compiler wait for that DMA (s_waitcnt vmcnt(0)) first. (Spread
@@ -428,8 +585,19 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
       for (int k = 0; k < K; ++k) dma_k(k, c, s, g);
       cur = nxt;
     }
+    if constexpr (SEP) {   // the chunk's sum into the total (correctly rounded VALU adds)
+#pragma unroll
+      for (int i = 0; i < NT; ++i) acc[i] += cacc[i];
+    }
   }
   vm_barrier();   // trailing sink loads landed; every wave is done with the stages
+  if constexpr (EPI == HE_QUANT) {
+    // (the kernel's LDS is sized by the full-input form: HK<…, false>)
+    using KF = HK<MODE, TH, COT, CI, false>;
+    static_assert(TH / 2 * 64 * 128 <= KF::BBOFF, "the epilogue's lane rows fit the stages");
+    quant_epilogue<TH, CO, COT>(a, acc, smem, smem + KF::BBOFF, b, ty, tx, cg);
+    return;
+  } else {
 
   // ---- epilogue. acc[i][4m + j]: channel 32i + 8m + 4h + j of tile pixel tpix. The lane
   // indices are re-derived from a fresh threadIdx.x: the main loop's copies otherwise stay live
@@ -453,6 +621,7 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
       for (int j = 0; j < 4; ++j) acc[i][4 * m + j] = acc[i][4 * m + j] * dsc + bv[j];   // x = conv + bias
     }
   constexpr int NTH = KK::NTH, KB = KK::KB;
+  static_assert(NT % 2 == 0, "GDN epilogue: pairs of 32-channel tiles");
   bool ovf = false;
   // The channel contraction n_i = Σ_j γ_ij·x_j² in the h3 form. x² of a pixel (rounded to fp32,
   // as conv2d(x², γ) sees it) is scaled by a power of two s_p that puts the pixel's largest x²
@@ -611,12 +780,12 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
             sv[pl][k] = u4{sx[0], sy[0], sx[1], sy[1]};
           }
         if (inside) {
-          const long so = a.out_cm ? (((long)b * (CO / 32) + i) * a.Hout + oy) * a.Wout * 32 + (long)ox * 32 + 16 * eh
-                                   : o * CO + 32 * i + 16 * eh;
-          *(u4*)(a.out_h3 + so) = sv[0][0];
-          *(u4*)(a.out_h3 + so + 8) = sv[0][1];
-          *(u4*)(a.out_h3 + a.out_h3_plane + so) = sv[1][0];
-          *(u4*)(a.out_h3 + a.out_h3_plane + so + 8) = sv[1][1];
+          const long s0 = h3_out_off(a, b, oy, ox, CO, 32 * i + 16 * eh);
+          const long s1 = h3_out_off(a, b, oy, ox, CO, 32 * i + 16 * eh + 8);
+          *(u4*)(a.out_h3 + s0) = sv[0][0];
+          *(u4*)(a.out_h3 + s1) = sv[0][1];
+          *(u4*)(a.out_h3 + a.out_h3_plane + s0) = sv[1][0];
+          *(u4*)(a.out_h3 + a.out_h3_plane + s1) = sv[1][1];
         }
       }
       if (a.out_x6) {
@@ -658,20 +827,27 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
     }
   }
   if (ovf && a.range) atomicOr(a.range, 1);   // vector atomic, per offending lane (rare)
+  }
 }
 
 // INT_OK: the caller guarantees an integer-valued input (ŷ). A workgroup then checks that the lo
 // plane of its input window is zero (every value exact in the hi plane) and runs the INT_IN body;
 // otherwise the full body.
-template <int MODE, int TH, int CO, int CI, int EPI, bool INT_OK>
-__global__ void __launch_bounds__(TH / 2 * 64, 1) h3k_kernel(const HArgs a) {
-  using KK = HK<MODE, TH, CO, CI, false>;
-  static_assert(KK::LDS >= HK<MODE, TH, CO, CI, true>::LDS, "LDS");
+template <int MODE, int TH, int CO, int CI, int EPI, bool INT_OK, int COT = CO, bool SEP = false,
+          int ICM = 0>
+// two waves per SIMD either way: TH = 16 (8 waves) one workgroup per CU, TH = 8 (4 waves) two
+__global__ void __launch_bounds__(TH / 2 * 64, TH == 8 ? 2 : 1) h3k_kernel(const HArgs a) {
+  using KK = HK<MODE, TH, COT, CI, false>;
+  static_assert(KK::LDS >= HK<MODE, TH, COT, CI, true>::LDS, "LDS");
   __shared__ __attribute__((aligned(16))) unsigned char smem[KK::LDS];
   int bid = blockIdx.x;
   const int per_ph = a.tiles_x * a.tiles_y * a.B;
   const int ph = MODE == BM_DECONV ? bid / per_ph : 0;   // phases dispatched phase-major
   bid -= ph * per_ph;
+  // channel groups innermost: consecutive workgroups (dealt round-robin to the 8 XCDs) take
+  // consecutive groups, so an XCD's L2 serves one group's weight slice to all its workgroups
+  const int cg = bid % (CO / COT);
+  bid /= CO / COT;
   const int tx = bid % a.tiles_x;
   bid /= a.tiles_x;
   const int ty = bid % a.tiles_y;
@@ -685,34 +861,53 @@ __global__ void __launch_bounds__(TH / 2 * 64, 1) h3k_kernel(const HArgs a) {
     const int iy0 = MODE == BM_CONV ? 2 * ty * TH - 2 : ty * TH - 1;
     const int ix0 = MODE == BM_CONV ? 2 * tx * 16 - 2 : tx * 16 - 1;
     const u16* inb = a.in + a.in_plane + (long)b * a.Hin * a.Win * CI;
-    // every load issued before the first compare (one memory latency, not one per load)
-    constexpr int NTHR = TH / 2 * 64, IT = (P::ROWS * PER + NTHR - 1) / NTHR;
-    u4 v[IT];
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int u = threadIdx.x + it * NTHR;
-      const int r = u / PER, rem = u - r * PER, c = rem / (CI / 8), k8 = rem - c * (CI / 8);
-      const int iy = iy0 + r, ix = ix0 + c;
-      const bool ok = u < P::ROWS * PER && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
-      v[it] = ok ? *(const u4*)(inb + ((long)iy * a.Win + ix) * CI + 8 * k8) : u4{0u, 0u, 0u, 0u};
-    }
+    // the loads issued in batches of 8 before their compares (one memory latency per batch, not
+    // one per load; all of them at once held 17 × 4 registers at TH = 8 and spilled)
+    constexpr int NTHR = TH / 2 * 64, IT = (P::ROWS * PER + NTHR - 1) / NTHR, IB = 8;
     unsigned bad = 0;
 #pragma unroll
-    for (int it = 0; it < IT; ++it)
+    for (int i0 = 0; i0 < IT; i0 += IB) {
+      u4 v[IB];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) bad |= v[it][e] & 0x7fff7fffu;   // ±0 only
+      for (int k = 0; k < IB; ++k) {
+        const int u = threadIdx.x + (i0 + k) * NTHR;
+        int r, c;
+        long off;
+        if constexpr (ICM != 0) {   // chunk-major: (chunk, row, column, 8-channel half) order
+          constexpr int PR = COLS * ICM / 8;
+          const int q = u / (P::ROWS * PR), rem = u - q * (P::ROWS * PR);
+          r = rem / PR;
+          const int rem2 = rem - r * PR;
+          c = rem2 / (ICM / 8);
+          off = (((long)q * a.Hin + iy0 + r) * a.Win + ix0 + c) * ICM + 8 * (rem2 - c * (ICM / 8));
+        } else {
+          r = u / PER;
+          const int rem = u - r * PER;
+          c = rem / (CI / 8);
+          off = ((long)(iy0 + r) * a.Win + ix0 + c) * CI + 8 * (rem - c * (CI / 8));
+        }
+        const int iy = iy0 + r, ix = ix0 + c;
+        const bool ok = i0 + k < IT && u < P::ROWS * PER && (unsigned)iy < (unsigned)a.Hin &&
+                        (unsigned)ix < (unsigned)a.Win;
+        v[k] = ok ? *(const u4*)(inb + off) : u4{0u, 0u, 0u, 0u};
+      }
+#pragma unroll
+      for (int k = 0; k < IB; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bad |= v[k][e] & 0x7fff7fffu;   // ±0 only
+    }
     small = __syncthreads_or(bad) == 0;
   }
   auto run = [&](auto int_in) {
     constexpr bool II = decltype(int_in)::value;
     if constexpr (MODE != BM_DECONV) {
-      h3k_body<MODE, TH, CO, CI, EPI, II, 0>(a, smem, b, ty, tx);
+      h3k_body<MODE, TH, CO, CI, EPI, II, 0, COT, SEP, ICM>(a, smem, b, ty, tx, cg);
     } else {
       switch (ph) {   // wave-uniform: the tap lists are compile-time per phase
-        case 0: h3k_body<MODE, TH, CO, CI, EPI, II, 0>(a, smem, b, ty, tx); break;
-        case 1: h3k_body<MODE, TH, CO, CI, EPI, II, 1>(a, smem, b, ty, tx); break;
-        case 2: h3k_body<MODE, TH, CO, CI, EPI, II, 2>(a, smem, b, ty, tx); break;
-        default: h3k_body<MODE, TH, CO, CI, EPI, II, 3>(a, smem, b, ty, tx); break;
+        case 0: h3k_body<MODE, TH, CO, CI, EPI, II, 0, CO, false, ICM>(a, smem, b, ty, tx); break;
+        case 1: h3k_body<MODE, TH, CO, CI, EPI, II, 1, CO, false, ICM>(a, smem, b, ty, tx); break;
+        case 2: h3k_body<MODE, TH, CO, CI, EPI, II, 2, CO, false, ICM>(a, smem, b, ty, tx); break;
+        default: h3k_body<MODE, TH, CO, CI, EPI, II, 3, CO, false, ICM>(a, smem, b, ty, tx); break;
       }
     }
   };
@@ -978,15 +1173,61 @@ __global__ void __launch_bounds__(256) h3_planes_kernel(const float* __restrict_
   if (ovf && range) atomicOr(range, 1);
 }
 
-template <int N, int TH, bool INT_OK>
+// fp32 NHWC [B][h][w][N] → the h3 form chunk-major [2][B][N/cm][h][w][cm] (iclr17_h3_planes_cm):
+// a thread per 4 consecutive channels of a pixel
+__global__ void __launch_bounds__(256) h3_planes_cm_kernel(const float* __restrict__ x, long n4,
+                                                           int N, int cm, long hw, long plane,
+                                                           u16* __restrict__ out, int* range) {
+  bool ovf = false;
+  const int q4 = N / 4;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    const long p = i / q4;
+    const int ch = 4 * (int)(i - p * q4);
+    const long b = p / hw, pix = p - b * hw;
+    const long o = ((b * (N / cm) + ch / cm) * hw + pix) * cm + ch % cm;
+    uint2 hb, lb;
+    h3_split4(*(const f4*)(x + 4 * i), hb, lb, ovf);
+    *(uint2*)(out + o) = hb;
+    *(uint2*)(out + plane + o) = lb;
+  }
+  if (ovf && range) atomicOr(range, 1);
+}
+
+// The chain's h3 layouts (the consumer's patch chunk): conv1 → conv2 and conv2 →
+// conv3 chunk-major 8 (HM_CONV8's 8-channel chunks), conv3's ŷ → deconv1 and deconv1 → deconv2
+// chunk-major 16 (the deconv mode's 16-channel chunks), deconv2 → deconv3 chunk-major 32.
+constexpr int kConvCM = 8, kDeconvCM = 16;
+
+template <int N, bool INT_OK>
 int launch_deconv(const HArgs& a0, hipStream_t st) {
+  constexpr int TH = 16;
   HArgs a = a0;
   a.tiles_y = (a.gh + TH - 1) / TH;
   a.tiles_x = (a.gw + 15) / 16;
-  hipLaunchKernelGGL((h3k_kernel<BM_DECONV, TH, N, N, HE_IGDN, INT_OK>),
+  hipLaunchKernelGGL((h3k_kernel<BM_DECONV, TH, N, N, HE_IGDN, INT_OK, N, false, kDeconvCM>),
                      dim3(a.tiles_x * a.tiles_y * a.B * 4), dim3(TH / 2 * 64), 0, st, a);
   return check_launch("deconv_igdn_h3");
 }
+
+// conv3 + quantiser + rate on the h3 engine: 8 × 16-pixel tiles of 4 waves, each workgroup one
+// output-channel slice of 96 (N = 192) or 64 (N = 128) channels — B = 64 gives 256 workgroups
+// (conv3's 16 × 16 output per 256² image is one 16 × 16 tile, 64 workgroups without a split) —
+// and two-level sums per 8-channel chunk. The slice does not change an element's summation order,
+// so an image's results do not depend on its batch. (Measured and left out: 16 × 16 tiles with
+// 64 / 96 / 192 channels, 32-channel slices, and split-K over 2 / 4 / 8 workgroups per tile with
+// a second reducing launch — 0.16–0.44 ms against this form's 0.14.)
+constexpr int kC3TH = 8;
+template <int N>
+constexpr int conv3_cot() { return N == 192 ? 96 : 64; }
+
+template <int N>
+static void launch_conv3(const HArgs& a, hipStream_t st) {
+  constexpr int COT = conv3_cot<N>();
+  hipLaunchKernelGGL((h3k_kernel<HM_CONV8, kC3TH, N, N, HE_QUANT, false, COT, true, kConvCM>),
+                     dim3(a.tiles_x * a.tiles_y * a.B * (N / COT)), dim3(kC3TH / 2 * 64), 0, st, a);
+}
+
+static bool valid_cm(int cm, int N) { return cm == 0 || ((cm == 8 || cm == 16 || cm == 32) && N % cm == 0); }
 
 }  // namespace h3k
 }  // namespace iclr17
@@ -1100,14 +1341,26 @@ int iclr17_h3_planes(const float* x, long n, uint16_t* planes, int* range_flag, 
   return check_launch("h3_planes");
 }
 
+int iclr17_h3_planes_cm(const float* x, int B, int h, int w, int N, int cm, uint16_t* planes,
+                        int* range_flag, void* stream) {
+  ICLR17_REQUIRE(x && planes && B > 0 && h > 0 && w > 0 && N > 0 && N % 4 == 0 && valid_cm(cm, N) &&
+                     cm != 0,
+                 ICLR17_EINVAL, "h3_planes_cm: bad arguments (N=%d, cm=%d)", N, cm);
+  const long n = (long)B * h * w * N, n4 = n / 4;
+  const int blocks = (int)((n4 + 255) / 256 < 8192 ? (n4 + 255) / 256 : 8192);
+  hipLaunchKernelGGL(h3_planes_cm_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, n4, N,
+                     cm, (long)h * w, n, planes, range_flag);
+  return check_launch("h3_planes_cm");
+}
+
 int iclr17_analysis_conv1_gdn_h3(const float* x, int B, int H, int W, int N,
                                  const uint16_t* w_h3k, const float* bias, const float* beta_eff,
                                  const uint16_t* gamma_h3, float* out, float* pre_out,
-                                 uint16_t* out_h3, uint16_t* out_x6, int* range_flag,
+                                 uint16_t* out_h3, int out_cm, uint16_t* out_x6, int* range_flag,
                                  void* stream) {
   ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "conv1_gdn_h3: N=%d", N);
   ICLR17_REQUIRE(x && w_h3k && bias && beta_eff && gamma_h3 && (out || out_h3 || out_x6) && B > 0 &&
-                     H > 0 && W > 0 && H % 16 == 0 && W % 16 == 0,
+                     H > 0 && W > 0 && H % 16 == 0 && W % 16 == 0 && valid_cm(out_cm, N),
                  ICLR17_EINVAL, "conv1_gdn_h3: bad arguments");
   HArgs a;
   memset(&a, 0, sizeof(a));
@@ -1119,7 +1372,7 @@ int iclr17_analysis_conv1_gdn_h3(const float* x, int B, int H, int W, int N,
   a.gamma_scale = (const float*)(gamma_h3 + 2L * N * N);
   a.out = out;
   a.pre = pre_out;
-  a.out_h3 = out_h3; a.out_h3_plane = (long)B * (H / 4) * (W / 4) * N;
+  a.out_h3 = out_h3; a.out_h3_plane = (long)B * (H / 4) * (W / 4) * N; a.out_cm = out_cm;
   a.out_x6 = out_x6; a.out_x6_plane = a.out_h3_plane;
   a.range = range_flag;
   a.B = B; a.Hin = H; a.Win = W; a.Hout = H / 4; a.Wout = W / 4;
@@ -1140,11 +1393,11 @@ int iclr17_analysis_conv1_gdn_h3(const float* x, int B, int H, int W, int N,
 int iclr17_analysis_conv2_gdn_h3(const uint16_t* in_h3, int B, int H, int W, int N,
                                  const uint16_t* w_h3k, const float* bias, const float* beta_eff,
                                  const uint16_t* gamma_h3, float* out, float* pre_out,
-                                 uint16_t* out_h3, uint16_t* out_x6, int* range_flag,
+                                 uint16_t* out_h3, int out_cm, uint16_t* out_x6, int* range_flag,
                                  void* stream) {
   ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "conv2_gdn_h3: N=%d", N);
   ICLR17_REQUIRE(in_h3 && w_h3k && bias && beta_eff && gamma_h3 && (out || out_h3 || out_x6) &&
-                     B > 0 && H > 0 && W > 0 && H % 16 == 0 && W % 16 == 0,
+                     B > 0 && H > 0 && W > 0 && H % 16 == 0 && W % 16 == 0 && valid_cm(out_cm, N),
                  ICLR17_EINVAL, "conv2_gdn_h3: bad arguments");
   HArgs a;
   memset(&a, 0, sizeof(a));
@@ -1157,7 +1410,7 @@ int iclr17_analysis_conv2_gdn_h3(const uint16_t* in_h3, int B, int H, int W, int
   a.gamma_scale = (const float*)(gamma_h3 + 2L * N * N);
   a.out = out;
   a.pre = pre_out;
-  a.out_h3 = out_h3; a.out_h3_plane = (long)B * (h / 2) * (w / 2) * N;
+  a.out_h3 = out_h3; a.out_h3_plane = (long)B * (h / 2) * (w / 2) * N; a.out_cm = out_cm;
   a.out_x6 = out_x6; a.out_x6_plane = a.out_h3_plane;
   a.range = range_flag;
   a.B = B; a.Hin = h; a.Win = w; a.Hout = h / 2; a.Wout = w / 2;
@@ -1167,11 +1420,11 @@ int iclr17_analysis_conv2_gdn_h3(const uint16_t* in_h3, int B, int H, int W, int
   a.tiles_x = (a.gw + 15) / 16;
   const dim3 grid(a.tiles_x * a.tiles_y * B);
   if (N == 192)
-    hipLaunchKernelGGL((h3k_kernel<HM_CONV8, TH, 192, 192, HE_GDN, false>), grid, dim3(TH / 2 * 64), 0,
-                       (hipStream_t)stream, a);
+    hipLaunchKernelGGL((h3k_kernel<HM_CONV8, TH, 192, 192, HE_GDN, false, 192, false, kConvCM>), grid,
+                       dim3(TH / 2 * 64), 0, (hipStream_t)stream, a);
   else
-    hipLaunchKernelGGL((h3k_kernel<HM_CONV8, TH, 128, 128, HE_GDN, false>), grid, dim3(TH / 2 * 64), 0,
-                       (hipStream_t)stream, a);
+    hipLaunchKernelGGL((h3k_kernel<HM_CONV8, TH, 128, 128, HE_GDN, false, 128, false, kConvCM>), grid,
+                       dim3(TH / 2 * 64), 0, (hipStream_t)stream, a);
   return check_launch("conv2_gdn_h3");
 }
 
@@ -1179,11 +1432,10 @@ int iclr17_synthesis_deconv_igdn_h3(const uint16_t* in_h3, int B, int h, int w, 
                                     const uint16_t* w_h3k, const float* bias,
                                     const float* beta_eff, const uint16_t* gamma_h3,
                                     float* out, float* pre_out, uint16_t* out_h3, uint16_t* out_x6,
-                                    int out_cm,
-                                    int int_in, int* range_flag, void* stream) {
+                                    int out_cm, int int_in, int* range_flag, void* stream) {
   ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "deconv_igdn_h3: N=%d", N);
   ICLR17_REQUIRE(in_h3 && w_h3k && bias && beta_eff && gamma_h3 && (out || out_h3 || out_x6) &&
-                     B > 0 && h > 0 && w > 0,
+                     B > 0 && h > 0 && w > 0 && valid_cm(out_cm, N),
                  ICLR17_EINVAL, "deconv_igdn_h3: bad arguments");
   HArgs a;
   memset(&a, 0, sizeof(a));
@@ -1197,13 +1449,54 @@ int iclr17_synthesis_deconv_igdn_h3(const uint16_t* in_h3, int B, int h, int w, 
   a.pre = pre_out;
   a.out_h3 = out_h3; a.out_h3_plane = (long)B * 4 * h * w * N;
   a.out_x6 = out_x6; a.out_x6_plane = (long)B * 4 * h * w * N;
-  a.out_cm = out_cm ? 1 : 0;
+  a.out_cm = out_cm;
   a.range = range_flag;
   a.B = B; a.Hin = h; a.Win = w; a.Hout = 2 * h; a.Wout = 2 * w;
   a.gh = h; a.gw = w;
   hipStream_t st = (hipStream_t)stream;
-  if (int_in) return N == 192 ? launch_deconv<192, 16, true>(a, st) : launch_deconv<128, 16, true>(a, st);
-  return N == 192 ? launch_deconv<192, 16, false>(a, st) : launch_deconv<128, 16, false>(a, st);
+  if (int_in) return N == 192 ? launch_deconv<192, true>(a, st) : launch_deconv<128, true>(a, st);
+  return N == 192 ? launch_deconv<192, false>(a, st) : launch_deconv<128, false>(a, st);
+}
+
+int iclr17_conv3_h3_partials_per_image(int B, int H, int W, int N, int quant_mode) {
+  (void)quant_mode;
+  if (B <= 0 || H <= 0 || W <= 0 || H % 16 || W % 16 || (N != 128 && N != 192)) return 0;
+  return ((H / 16 + kC3TH - 1) / kC3TH) * ((W / 16 + 15) / 16) * (N / (N == 192 ? 96 : 64));
+}
+
+int iclr17_analysis_conv3_quant_rate_h3(const uint16_t* in_h3, int B, int H, int W, int N,
+                                        const uint16_t* w_h3k, int quant_mode, const float* noise,
+                                        const float* rate_packed, const float* rate_table,
+                                        float* y_out, float* y_hat, uint16_t* y_hat_h3, int out_cm,
+                                        double* bits_partial, int* range_flag, void* stream) {
+  ICLR17_REQUIRE(N == 128 || N == 192, ICLR17_EUNSUPPORTED, "conv3_quant_rate_h3: N=%d", N);
+  ICLR17_REQUIRE(B > 0 && H > 0 && W > 0 && H % 16 == 0 && W % 16 == 0 && valid_cm(out_cm, N),
+                 ICLR17_EINVAL, "conv3_quant_rate_h3: bad shape %dx%d / layout %d", H, W, out_cm);
+  ICLR17_REQUIRE(in_h3 && w_h3k && rate_packed && y_hat && bits_partial, ICLR17_EINVAL,
+                 "conv3_quant_rate_h3: null pointer");
+  ICLR17_REQUIRE(quant_mode == ICLR17_QUANT_ROUND || (quant_mode == ICLR17_QUANT_NOISE && noise),
+                 ICLR17_EINVAL, "conv3_quant_rate_h3: bad quant mode %d / missing noise", quant_mode);
+  HArgs a;
+  memset(&a, 0, sizeof(a));
+  const int h = H / 8, w = W / 8;
+  a.in = in_h3; a.in_plane = (long)B * h * w * N;
+  const size_t wsz = iclr17_h3k_weight_size(ICLR17_H3K_CONV5, N);
+  a.w = w_h3k; a.w_plane = (long)(wsz - 8) / 2;
+  a.wscale = (const float*)(w_h3k + (wsz - 8));
+  a.out = y_out;
+  a.out_h3 = y_hat_h3; a.out_h3_plane = (long)B * (h / 2) * (w / 2) * N; a.out_cm = out_cm;
+  a.range = range_flag;
+  a.qmode = quant_mode; a.noise = noise; a.rate = rate_packed;
+  a.rtab = rate_table; a.yhat = y_hat; a.partial = bits_partial;
+  a.B = B; a.Hin = h; a.Win = w; a.Hout = h / 2; a.Wout = w / 2;
+  a.gh = h / 2; a.gw = w / 2;
+  a.tiles_y = (a.gh + kC3TH - 1) / kC3TH;
+  a.tiles_x = (a.gw + 15) / 16;
+  a.T = iclr17_conv3_h3_partials_per_image(B, H, W, N, quant_mode);
+  hipStream_t st = (hipStream_t)stream;
+  if (N == 192) launch_conv3<192>(a, st);
+  else launch_conv3<128>(a, st);
+  return check_launch("conv3_quant_rate_h3");
 }
 
 }  // extern "C"

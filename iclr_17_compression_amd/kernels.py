@@ -493,28 +493,54 @@ def check_finite(what: str, *values) -> None:
             raise Iclr17Error(f"iclr17: non-finite {what}")
 
 
-def _check_h3(s: Tensor, what: str):
-    if not isinstance(s, Tensor) or s.dtype != torch.int16 or s.dim() != 5 or s.shape[0] != 2:
-        raise Iclr17Error(f"iclr17: {what} must be an h3-form int16 tensor [2,B,h,w,N]")
+# The h3 layers read their input chunk-major: [2, B, N/cm, h, w, cm] with cm the chunk the layer
+# stages (conv2 / conv3: 8; deconv1 / deconv2: 16; deconv3: 32), so that a patch piece is 16
+# contiguous bytes; each layer writes the layout its consumer reads (out_cm).
+CONV_CM, DECONV_CM, DECONV3_CM = 8, 16, 32
+
+
+def _check_h3(s: Tensor, what: str, cm: int):
+    """An h3 activation in the chunk-major layout cm; returns (B, h, w, N)."""
+    if (not isinstance(s, Tensor) or s.dtype != torch.int16 or s.dim() != 6 or s.shape[0] != 2
+            or s.shape[5] != cm):
+        raise Iclr17Error(f"iclr17: {what} must be an h3-form int16 tensor in the chunk-major layout "
+                          f"[2,B,N/{cm},h,w,{cm}] (kernels.h3_planes(x, cm={cm}))")
     if not s.is_cuda:
         raise Iclr17Error(f"iclr17: {what} must be a device tensor (there is no CPU path)")
     if not s.is_contiguous():
         raise Iclr17Error(f"iclr17: {what} must be contiguous")
+    return s.shape[1], s.shape[3], s.shape[4], s.shape[2] * cm
 
 
-def h3_planes(x: Tensor) -> Tensor:
-    """fp32 tensor (numel % 4 == 0) → h3 form [2, *x.shape]."""
+def _h3_out(B: int, h: int, w: int, N: int, cm: int, device) -> Tensor:
+    if cm not in (0, 8, 16, 32) or (cm and N % cm):
+        raise Iclr17Error(f"iclr17: h3 output layout must be 0 (NHWC), 8, 16 or 32 (got {cm})")
+    shape = (2, B, N // cm, h, w, cm) if cm else (2, B, h, w, N)
+    return torch.empty(shape, device=device, dtype=torch.int16)
+
+
+def h3_planes(x: Tensor, cm: int = 0) -> Tensor:
+    """fp32 tensor (numel % 4 == 0) → h3 form [2, *x.shape]; with ``cm`` (8, 16, 32) an NHWC
+    [B, h, w, N] tensor → the chunk-major [2, B, N/cm, h, w, cm] the h3 layers read."""
     _check(x, "tensor", x.dim())
     x = x.contiguous()
     if x.numel() % 4:
         raise Iclr17Error("iclr17: h3_planes needs a multiple of 4 elements")
+    if cm:
+        if x.dim() != 4:
+            raise Iclr17Error("iclr17: h3_planes(cm=...) takes an NHWC [B,h,w,N] tensor")
+        B, h, w, N = x.shape
+        out = _h3_out(B, h, w, N, cm, x.device)
+        call("iclr17_h3_planes_cm", _p(x), B, h, w, N, cm, _p(out), _p(h3_range_flag(x.device)),
+             _stream(x))
+        return out
     out = torch.empty((2,) + tuple(x.shape), device=x.device, dtype=torch.int16)
     call("iclr17_h3_planes", _p(x), x.numel(), _p(out), _p(h3_range_flag(x.device)), _stream(x))
     return out
 
 
 def merge_h3(s: Tensor) -> Tensor:
-    """h3 form → fp32 (hi + lo·2^-11)/σ_a; a chunk-major [2,B,N/32,h,w,32] comes back as NHWC.
+    """h3 form → fp32 (hi + lo·2^-11)/σ_a; a chunk-major [2,B,N/cm,h,w,cm] comes back as NHWC.
     Test/debug helper (torch ops, exact in fp32)."""
     if s.dim() == 6:
         s = s.permute(0, 1, 3, 4, 2, 5).reshape(2, s.shape[1], s.shape[3], s.shape[4], -1)
@@ -590,11 +616,12 @@ def pack_conv1_h3(w: Tensor, N: int) -> Tensor:
 
 def conv1_gdn_h3(x: Tensor, w_h3: Tensor, bias: Tensor, beta_eff: Tensor, gh3: Tensor, N: int,
                  want_f32: bool = False, want_h3: bool = True, want_x6: bool = False,
-                 want_pre: bool = False):
+                 want_pre: bool = False, out_cm: int = CONV_CM):
     """analysis_17.py:14-17 conv1 + GDN1 in the h3 form on the h3 engine (three f16 part products
     per MAC for the convolution and the GDN contraction; w_h3: ``pack_conv1_h3``, gh3:
-    GDN.effective_params_h3's γ). Returns (h3 [2,B,H/4,W/4,N] | None, fp32 | None), and with
-    ``want_x6`` / ``want_pre`` (training) also (x6 split | None, GDN1 input conv1 + bias | None)."""
+    GDN.effective_params_h3's γ). Returns (h3 | None — chunk-major [2,B,N/out_cm,H/4,W/4,out_cm],
+    conv2's input —, fp32 | None), and with ``want_x6`` / ``want_pre`` (training) also (x6 split |
+    None, GDN1 input conv1 + bias | None)."""
     _check(x, "image", 4)
     B, C, H, W = x.shape
     if C != 3:
@@ -608,12 +635,12 @@ def conv1_gdn_h3(x: Tensor, w_h3: Tensor, bias: Tensor, beta_eff: Tensor, gh3: T
     if not (want_h3 or want_f32 or want_x6):
         raise Iclr17Error("iclr17: conv1_gdn_h3 needs an output")
     x = x.contiguous()
-    h3 = torch.empty(2, B, H // 4, W // 4, N, device=x.device, dtype=torch.int16) if want_h3 else None
+    h3 = _h3_out(B, H // 4, W // 4, N, out_cm, x.device) if want_h3 else None
     x6 = torch.empty(3, B, H // 4, W // 4, N, device=x.device, dtype=torch.int16) if want_x6 else None
     out = torch.empty(B, H // 4, W // 4, N, device=x.device) if want_f32 else None
     pre = torch.empty(B, H // 4, W // 4, N, device=x.device) if want_pre else None
     call("iclr17_analysis_conv1_gdn_h3", _p(x), B, H, W, N, _p(w_h3), _p(bias), _p(beta_eff),
-         _p(gh3), _p(out), _p(pre), _p(h3), _p(x6), _p(h3_range_flag(x.device)), _stream(x))
+         _p(gh3), _p(out), _p(pre), _p(h3), out_cm, _p(x6), _p(h3_range_flag(x.device)), _stream(x))
     if want_x6 or want_pre:
         return h3, out, x6, pre
     return h3, out
@@ -621,13 +648,13 @@ def conv1_gdn_h3(x: Tensor, w_h3: Tensor, bias: Tensor, beta_eff: Tensor, gh3: T
 
 def conv2_gdn_h3(hs: Tensor, wk: Tensor, bias: Tensor, beta_eff: Tensor, gh3: Tensor,
                  want_h3: bool = True, want_f32: bool = False, want_x6: bool = False,
-                 want_pre: bool = False):
+                 want_pre: bool = False, out_cm: int = CONV_CM):
     """analysis_17.py:18-21 conv2 + GDN2 in the h3 form on the h3 engine (csrc/engine_h3.hip):
-    h3 input [2,B,H/4,W/4,N] → (h3 | None, fp32 | None, x6 split | None). wk:
+    h3 input chunk-major 8 [2,B,N/8,H/4,W/4,8] → (h3 | None — layout out_cm, conv3's input —,
+    fp32 | None, x6 split | None). wk:
     ``pack_h3k(ICLR17_H3K_CONV5, w)``; gh3: GDN.effective_params_h3's γ. With ``want_pre``
     (training) a fourth result: GDN2's input conv2 + bias (fp32 NHWC)."""
-    _check_h3(hs, "activation")
-    _, B, h4, w4, N = hs.shape
+    B, h4, w4, N = _check_h3(hs, "activation", CONV_CM)
     _check_channels(N)
     H, W = 4 * h4, 4 * w4
     _check_image_dims(H, W)
@@ -637,12 +664,12 @@ def conv2_gdn_h3(hs: Tensor, wk: Tensor, bias: Tensor, beta_eff: Tensor, gh3: Te
         raise Iclr17Error("iclr17: conv2_gdn_h3 needs γ in the h3 form (effective_params_h3)")
     if not (want_h3 or want_f32 or want_x6):
         raise Iclr17Error("iclr17: conv2_gdn_h3 needs an output")
-    h3 = torch.empty(2, B, h4 // 2, w4 // 2, N, device=hs.device, dtype=torch.int16) if want_h3 else None
+    h3 = _h3_out(B, h4 // 2, w4 // 2, N, out_cm, hs.device) if want_h3 else None
     x6 = torch.empty(3, B, h4 // 2, w4 // 2, N, device=hs.device, dtype=torch.int16) if want_x6 else None
     out = torch.empty(B, h4 // 2, w4 // 2, N, device=hs.device) if want_f32 else None
     pre = torch.empty(B, h4 // 2, w4 // 2, N, device=hs.device) if want_pre else None
     call("iclr17_analysis_conv2_gdn_h3", _p(hs), B, H, W, N, _p(wk), _p(bias), _p(beta_eff), _p(gh3),
-         _p(out), _p(pre), _p(h3), _p(x6), _p(h3_range_flag(hs.device)), _stream(hs))
+         _p(out), _p(pre), _p(h3), out_cm, _p(x6), _p(h3_range_flag(hs.device)), _stream(hs))
     if want_pre:
         return h3, out, x6, pre
     return h3, out, x6
@@ -650,16 +677,18 @@ def conv2_gdn_h3(hs: Tensor, wk: Tensor, bias: Tensor, beta_eff: Tensor, gh3: Te
 
 def conv3_quant_rate_h3(hs: Tensor, wh: Tensor, rate_packed: Tensor,
                         noise: Optional[Tensor] = None, want_y: bool = False,
-                        rtab: Optional[Tensor] = None, want_h3: bool = True):
-    """analysis_17.py:22 + model.py:48-56,71-73 in the h3 form. Returns (y_hat NHWC, bits_partial
-    [B, rate_partials_per_image], y | None, y_hat h3 | None)."""
-    _check_h3(hs, "activation")
-    _, B, h8, w8, N = hs.shape
+                        rtab: Optional[Tensor] = None, want_h3: bool = True,
+                        out_cm: int = DECONV_CM):
+    """analysis_17.py:22 + model.py:48-56,71-73 in the h3 form on the h3 engine (wh:
+    ``pack_h3k(ICLR17_H3K_CONV5, conv3.weight)``), input chunk-major 8. Returns (y_hat NHWC,
+    bits_partial [B, iclr17_conv3_h3_partials_per_image], y | None, y_hat h3 | None — layout
+    out_cm, deconv1's input)."""
+    B, h8, w8, N = _check_h3(hs, "activation", CONV_CM)
     _check_channels(N)
     H, W = 8 * h8, 8 * w8
     _check_image_dims(H, W)
-    if wh.numel() != query("iclr17_split_packed_h3_size", 25, N, N):
-        raise Iclr17Error("iclr17: conv3_quant_rate_h3 needs split_packed_h3 of the conv5 packing")
+    if wh.dtype != torch.int16 or wh.numel() != query("iclr17_h3k_weight_size", _lib.ICLR17_H3K_CONV5, N):
+        raise Iclr17Error("iclr17: conv3_quant_rate_h3 needs pack_h3k(ICLR17_H3K_CONV5) weights")
     mode = _lib.ICLR17_QUANT_ROUND
     if noise is not None:
         _check(noise, "noise", 4)
@@ -668,27 +697,30 @@ def conv3_quant_rate_h3(hs: Tensor, wh: Tensor, rate_packed: Tensor,
         noise = noise.contiguous()
         mode = _lib.ICLR17_QUANT_NOISE
     y_hat = torch.empty(B, h8 // 2, w8 // 2, N, device=hs.device, dtype=torch.float32)
-    y_hat_h3 = torch.empty(2, B, h8 // 2, w8 // 2, N, device=hs.device, dtype=torch.int16) if want_h3 else None
+    y_hat_h3 = _h3_out(B, h8 // 2, w8 // 2, N, out_cm, hs.device) if want_h3 else None
     y = torch.empty_like(y_hat) if want_y else None
-    T = query("iclr17_conv3_x6_partials_per_image", B, H, W, N, mode)   # the narrow tiles too
+    T = query("iclr17_conv3_h3_partials_per_image", B, H, W, N, mode)
     partial = torch.empty(B, T, device=hs.device, dtype=torch.float64)
     call("iclr17_analysis_conv3_quant_rate_h3", _p(hs), B, H, W, N, _p(wh), mode, _p(noise),
-         _p(rate_packed), _p(rtab), _p(y), _p(y_hat), _p(y_hat_h3), _p(partial),
+         _p(rate_packed), _p(rtab), _p(y), _p(y_hat), _p(y_hat_h3), out_cm, _p(partial),
          _p(h3_range_flag(hs.device)), _stream(hs))
     return y_hat, partial, y, y_hat_h3
 
 
 def deconv_igdn_h3(hs: Tensor, wh: Tensor, bias: Tensor, beta_eff: Tensor, gh3: Tensor,
                    want_h3: bool = True, want_f32: bool = False, want_x6: bool = False,
-                   chunk_major: bool = False, int_in: bool = False, want_pre: bool = False):
-    """synthesis_17.py:15-22 in the h3 form (csrc/engine_h3.hip): h3 input [2,B,h,w,N] →
-    (h3 | None, fp32 | None, x6 split | None). wh: ``pack_h3k(ICLR17_H3K_DECONV5, …)``; gh3: the
-    IGDN's γ in the h3 form (GDN.effective_params_h3). ``int_in``: the input is ŷ (a workgroup
-    whose window has a zero lo plane skips the lo products; same result). ``chunk_major`` applies
-    to the h3 output (the x6 output is NHWC). With ``want_pre`` (training) a fourth result: the
-    IGDN input deconv + bias (fp32 NHWC)."""
-    _check_h3(hs, "activation")
-    _, B, hh, ww, N = hs.shape
+                   chunk_major: bool = False, int_in: bool = False, want_pre: bool = False,
+                   out_cm: Optional[int] = None):
+    """synthesis_17.py:15-22 in the h3 form (csrc/engine_h3.hip): h3 input chunk-major 16
+    [2,B,N/16,h,w,16] → (h3 | None, fp32 | None, x6 split | None). wh: ``pack_h3k(ICLR17_H3K_DECONV5,
+    …)``; gh3: the IGDN's γ in the h3 form (GDN.effective_params_h3). ``int_in``: the input is ŷ
+    (a workgroup whose window has a zero lo plane skips the lo products; same result). The h3
+    output's layout: ``out_cm`` (default 16, deconv2's input), or 32 with ``chunk_major`` (deconv3's
+    input); the x6 output is NHWC. With ``want_pre`` (training) a fourth result: the IGDN input
+    deconv + bias (fp32 NHWC)."""
+    B, hh, ww, N = _check_h3(hs, "activation", DECONV_CM)
+    if out_cm is None:
+        out_cm = DECONV3_CM if chunk_major else DECONV_CM
     _check_channels(N)
     if gh3.dtype != torch.int16 or gh3.numel() != query("iclr17_split_packed_h3_size", 1, N, N):
         raise Iclr17Error("iclr17: deconv_igdn_h3 needs the IGDN's h3 γ (split_packed_h3, taps 1)")
@@ -696,14 +728,12 @@ def deconv_igdn_h3(hs: Tensor, wh: Tensor, bias: Tensor, beta_eff: Tensor, gh3: 
         raise Iclr17Error("iclr17: deconv_igdn_h3 needs an output")
     if wh.numel() != query("iclr17_h3k_weight_size", _lib.ICLR17_H3K_DECONV5, N):
         raise Iclr17Error("iclr17: deconv_igdn_h3 needs the ICLR17_H3K_DECONV5 packing")
-    def shape(P):
-        return (P, B, N // 32, 2 * hh, 2 * ww, 32) if chunk_major else (P, B, 2 * hh, 2 * ww, N)
-    h3 = torch.empty(shape(2), device=hs.device, dtype=torch.int16) if want_h3 else None
+    h3 = _h3_out(B, 2 * hh, 2 * ww, N, out_cm, hs.device) if want_h3 else None
     x6 = torch.empty(3, B, 2 * hh, 2 * ww, N, device=hs.device, dtype=torch.int16) if want_x6 else None
     out = torch.empty(B, 2 * hh, 2 * ww, N, device=hs.device) if want_f32 else None
     pre = torch.empty(B, 2 * hh, 2 * ww, N, device=hs.device) if want_pre else None
     call("iclr17_synthesis_deconv_igdn_h3", _p(hs), B, hh, ww, N, _p(wh), _p(bias),
-         _p(beta_eff), _p(gh3), _p(out), _p(pre), _p(h3), _p(x6), int(chunk_major), int(int_in),
+         _p(beta_eff), _p(gh3), _p(out), _p(pre), _p(h3), _p(x6), out_cm, int(int_in),
          _p(h3_range_flag(hs.device)), _stream(hs))
     if want_pre:
         return h3, out, x6, pre

@@ -244,7 +244,7 @@ class ImageCompressor(nn.Module):
         split = kernels.split_planes(y_hat) if kernels.precision() == "x6" else None
         if kernels.precision() == "h3":
             kernels.h3_chain_begin(y_hat.device)
-        yh3 = kernels.h3_planes(y_hat) if kernels.precision() == "h3" else None
+        yh3 = kernels.h3_planes(y_hat, cm=kernels.DECONV_CM) if kernels.precision() == "h3" else None
         ybf = kernels.to_bf16(y_hat) if kernels.precision() == "bf16" else None
         clipped, _, _ = self.Decoder.decode(y_hat, want_recon=False, y_split=split, y_bf16=ybf,
                                             y_integral=True, y_h3=yh3)

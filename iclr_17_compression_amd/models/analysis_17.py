@@ -63,15 +63,13 @@ class Analysis_net_17(nn.Module):
                               lambda: kernels.split_packed(w3, 25, N, N), force)
 
     def packed_h3(self, force: bool = False):
-        """conv2 / conv3 weights in the h3 form, cached: conv2 in the h3 engine's packing
-        (kernels.pack_h3k, ICLR17_H3K_CONV5), conv3 in the engine's two fp16 planes
-        (kernels.split_packed_h3 of the conv5 packing); per-tensor power-of-two scales."""
+        """conv2 / conv3 weights in the h3 engine's packing (kernels.pack_h3k, ICLR17_H3K_CONV5:
+        two fp16 planes, per-tensor power-of-two scales), cached."""
         N = self.out_channel_N
-        w3 = self.packed_w3(force)
         w2h = self._pack.get("w2h3", (self.conv2.weight,),
                              lambda: kernels.pack_h3k(_lib.ICLR17_H3K_CONV5, self.conv2.weight, N), force)
         w3h = self._pack.get("w3h3", (self.conv3.weight,),
-                             lambda: kernels.split_packed_h3(w3, 25, N, N), force)
+                             lambda: kernels.pack_h3k(_lib.ICLR17_H3K_CONV5, self.conv3.weight, N), force)
         return w2h, w3h
 
     def packed_conv1_h3(self, force: bool = False):

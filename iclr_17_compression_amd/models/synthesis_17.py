@@ -163,7 +163,7 @@ class Synthesis_net_17(nn.Module):
         split = kernels.split_planes(y) if kernels.precision() == "x6" else None
         if kernels.precision() == "h3":
             kernels.h3_chain_begin(y.device)
-        yh3 = kernels.h3_planes(y) if kernels.precision() == "h3" else None
+        yh3 = kernels.h3_planes(y, cm=kernels.DECONV_CM) if kernels.precision() == "h3" else None
         ybf = kernels.to_bf16(y) if kernels.precision() == "bf16" else None
         _, recon, _ = self.decode(y, want_recon=True, y_split=split, y_bf16=ybf, y_h3=yh3)
         return recon

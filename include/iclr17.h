@@ -480,6 +480,10 @@ size_t iclr17_h3k_weight_size(int which, int N);
 int iclr17_pack_h3k(int which, const float* w, uint16_t* out, int N, void* stream);
 /* fp32 x[n] (n % 4 == 0) → h3 planes [2][n] */
 int iclr17_h3_planes(const float* x, long n, uint16_t* planes, int* range_flag, void* stream);
+/* fp32 NHWC x [B][h][w][N] → h3 planes chunk-major [2][B][N/cm][h][w][cm] (cm 8, 16 or 32): the
+ * layout each h3 layer reads (conv2 / conv3: cm 8; deconv1 / deconv2: cm 16; deconv3: cm 32) */
+int iclr17_h3_planes_cm(const float* x, int B, int h, int w, int N, int cm, uint16_t* planes,
+                        int* range_flag, void* stream);
 /* A packed operand [taps][K/4][N][4] fp32 → two fp16 planes [2][taps][K/8][N][8] of w·σ_w + the
  * trailer (the h3 conv3 weights: the ICLR17_W_CONV5 packing with taps 25, K = N; deconv3's
  * ICLR17_W_DECONV9 packing with taps 9, 48 columns; a GDN γ_eff packing with taps 1, K = N).
@@ -499,31 +503,37 @@ int iclr17_pack_h3_batch(const iclr17_pack_job* jobs, int n, void* stream);
 /* analysis_17.py:14-17 conv1 + GDN1 on the h3 engine (csrc/engine_h3.hip): 16×16-pixel output
  * tiles of 8 waves; the tile's 3 × 69 × 69 input window split once into the two h3 planes in LDS,
  * K = 243 reordered into 16 steps of 16, three f16 part products per MAC, GDN contraction in the
- * h3 form. Outputs (each nullable, not all): fp32 NHWC, the h3 form [2][B][H/4][W/4][N], the x6
+ * h3 form. Outputs (each nullable, not all): fp32 NHWC, the h3 form [2][B][H/4][W/4][N] (out_cm
+ * 0) or chunk-major [2][B][N/out_cm][H/4][W/4][out_cm] (out_cm 8, 16, 32; conv2 reads 8), the x6
  * split [3][B][H/4][W/4][N]; pre_out (nullable): GDN1's input conv1 + bias, fp32 NHWC (training).
  * w_h3k: iclr17_pack_h3k(ICLR17_H3K_CONV1); gamma_h3: iclr17_split_packed_h3(γ_eff packing, 1, N, N). */
 int iclr17_analysis_conv1_gdn_h3(const float* x, int B, int H, int W, int N,
                                  const uint16_t* w_h3k, const float* bias, const float* beta_eff,
                                  const uint16_t* gamma_h3, float* out, float* pre_out,
-                                 uint16_t* out_h3, uint16_t* out_x6, int* range_flag,
+                                 uint16_t* out_h3, int out_cm, uint16_t* out_x6, int* range_flag,
                                  void* stream);
 /* analysis_17.py:18-21 conv2 + GDN2 on the h3 engine: 16×16-pixel tiles of 8 waves, 8-channel
- * chunks with two taps per 16-deep MFMA step, three f16 part products per MAC; input [2][B][H/4]
- * [W/4][N] (h3). Outputs as conv1_gdn_h3 at [B][H/8][W/8][N]. w_h3k:
+ * chunks with two taps per 16-deep MFMA step, three f16 part products per MAC; input the h3 form
+ * chunk-major 8, [2][B][N/8][H/4][W/4][8] (a patch piece is 16 contiguous bytes). Outputs as
+ * conv1_gdn_h3 at [B][H/8][W/8][N] (conv3 reads out_cm 8). w_h3k:
  * iclr17_pack_h3k(ICLR17_H3K_CONV5); gamma_h3 as above. */
 int iclr17_analysis_conv2_gdn_h3(const uint16_t* in_h3, int B, int H, int W, int N,
                                  const uint16_t* w_h3k, const float* bias, const float* beta_eff,
                                  const uint16_t* gamma_h3, float* out, float* pre_out,
-                                 uint16_t* out_h3, uint16_t* out_x6, int* range_flag,
+                                 uint16_t* out_h3, int out_cm, uint16_t* out_x6, int* range_flag,
                                  void* stream);
-/* analysis_17.py:22 + model.py:48-56,71-73 on the h3 form: as iclr17_analysis_conv3_quant_rate
- * (round or noise mode, rate_table nullable), ŷ also in the h3 form (y_hat_h3, nullable); bit
- * partials [B][iclr17_conv3_x6_partials_per_image(B, H, W, N, quant_mode)] (48-column tiles in
- * noise mode below 256 tiles·images, as the x6 entries). */
+/* analysis_17.py:22 + model.py:48-56,71-73 on the h3 engine (csrc/engine_h3.hip): as
+ * iclr17_analysis_conv3_quant_rate (round or noise mode, rate_table nullable; y_out nullable), ŷ
+ * also in the h3 form (y_hat_h3 nullable; layout out_cm as conv1_gdn_h3, deconv1 reads 16). Input
+ * the h3 form chunk-major 8 (conv2_gdn_h3 with out_cm 8). 8 × 16-pixel output tiles of 4 waves,
+ * each workgroup one slice of 96 (N = 192) / 64 (N = 128) output channels, 8-channel input chunks
+ * summed two-level. w_h3k: iclr17_pack_h3k(ICLR17_H3K_CONV5) of conv3's weights. Bit partials
+ * [B][iclr17_conv3_h3_partials_per_image(B, H, W, N, quant_mode)]. */
+int iclr17_conv3_h3_partials_per_image(int B, int H, int W, int N, int quant_mode);
 int iclr17_analysis_conv3_quant_rate_h3(const uint16_t* in_h3, int B, int H, int W, int N,
-                                        const uint16_t* w_h3, int quant_mode, const float* noise,
+                                        const uint16_t* w_h3k, int quant_mode, const float* noise,
                                         const float* rate_packed, const float* rate_table,
-                                        float* y_out, float* y_hat, uint16_t* y_hat_h3,
+                                        float* y_out, float* y_hat, uint16_t* y_hat_h3, int out_cm,
                                         double* bits_partial, int* range_flag, void* stream);
 /* synthesis_17.py:23-25 deconv3 + model.py:59 clamp on the h3 form: the chunk-major h3 input
  * [2][B][N/32][H/4][W/4][32] (iclr17_synthesis_deconv_igdn_h3 with out_cm) → clipped NCHW fp32
@@ -539,11 +549,11 @@ int iclr17_synthesis_deconv3_h3(const uint16_t* in_h3_cm, int B, int H, int W, i
                                 int sse_unclipped, const double* bits_partial, int bits_T,
                                 double* bits_per_image, float* bpp_total, double bits_scale,
                                 const int* range_flag, void* stream);
-/* synthesis_17.py:15-22 deconv + IGDN on the h3 engine: input [2][B][h][w][N] → fp32 NHWC
- * [B][2h][2w][N] and/or the h3 output [2][B][2h][2w][N] (chunk-major [2][B][N/32][2h][2w][32]
- * with out_cm) and/or the x6 split output [3][B][2h][2w][N] (NHWC always) — each nullable, not
- * all; pre_out (nullable): the IGDN input deconv + bias, fp32 NHWC (training). int_in: the input
- * is integer-valued (ŷ): a workgroup
+/* synthesis_17.py:15-22 deconv + IGDN on the h3 engine: input the h3 form chunk-major 16,
+ * [2][B][N/16][h][w][16] → fp32 NHWC [B][2h][2w][N] and/or the h3 output (layout out_cm as
+ * conv1_gdn_h3: deconv2 reads 16, deconv3 32) and/or the x6 split output [3][B][2h][2w][N] (NHWC
+ * always) — each nullable, not all; pre_out (nullable): the IGDN input deconv + bias, fp32 NHWC
+ * (training). int_in: the input is integer-valued (ŷ): a workgroup
  * whose input window has an all-zero lo plane (every value exact in the hi plane: integers with
  * |ŷ| < 2¹¹) runs the two products with hi_a only (same result); any other workgroup runs
  * the full three. w_h3k: iclr17_pack_h3k(ICLR17_H3K_DECONV5); gamma_h3:

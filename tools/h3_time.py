@@ -24,19 +24,22 @@ h1, h2 = dec.igdn1.effective_params_h3(), dec.igdn2.effective_params_h3()
 act = torch.from_numpy(synth.normal_like(6, (B, 32, 32, N), 0.7)).to(dev)
 yq = torch.round(torch.from_numpy(synth.uniform(5, (B, 16, 16, N), -6, 6))).to(dev)
 hs, ys = kernels.split_planes(act), kernels.split_planes(yq)
-hh, yh = kernels.h3_planes(act), kernels.h3_planes(yq)
+# each layer's input layout (kernels.CONV_CM / DECONV_CM chunk-major)
+hh8, hh, yh = (kernels.h3_planes(act, cm=kernels.CONV_CM), kernels.h3_planes(act, cm=kernels.DECONV_CM),
+               kernels.h3_planes(yq, cm=kernels.DECONV_CM))
 enc = net.Encoder
 w1h, (w2h, w3h) = enc.packed_conv1_h3(), enc.packed_h3()
 ge1, ge2 = enc.gdn1.effective_params_h3(), enc.gdn2.effective_params_h3()
 g1x = enc.gdn1.effective_params_x6()
 img = torch.from_numpy(synth.uniform(7, (B, 3, 256, 256), 0.0, 1.0)).to(dev)
-a1h = kernels.h3_planes(torch.from_numpy(synth.normal_like(8, (B, 64, 64, N), 0.7)).to(dev))
+a1h = kernels.h3_planes(torch.from_numpy(synth.normal_like(8, (B, 64, 64, N), 0.7)).to(dev),
+                        cm=kernels.CONV_CM)
 rate, rtab = net.bitEstimator.packed(), net.bitEstimator.rate_table()
 runs = {
     "conv1_x6": lambda: kernels.conv1x6_gdn(img, enc.packed_conv1_x6(), enc.conv1.bias, g1x[0], g1x[2], N),
     "conv1_h3": lambda: kernels.conv1_gdn_h3(img, w1h, enc.conv1.bias, *ge1, N),
     "conv2_h3": lambda: kernels.conv2_gdn_h3(a1h, w2h, enc.conv2.bias, *ge2),
-    "conv3_h3": lambda: kernels.conv3_quant_rate_h3(hh, w3h, rate, rtab=rtab),
+    "conv3_h3": lambda: kernels.conv3_quant_rate_h3(hh8, w3h, rate, rtab=rtab),
     "deconv2_old": lambda: kernels.deconv_igdn_x6(hs, d2, dec.deconv2.bias, *q2, chunk_major=True),
     "deconv2_h3": lambda: kernels.deconv_igdn_h3(hh, x2, dec.deconv2.bias, *h2, want_h3=False,
                                                  want_x6=True, chunk_major=True),

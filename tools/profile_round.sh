@@ -12,7 +12,7 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-ARGS="--no-cpu-baseline --no-bf16-leg --precision $PREC ${BENCH_ARGS:-}"
+ARGS="--no-cpu-baseline --no-bf16-leg --no-x6-leg --precision $PREC ${BENCH_ARGS:-}"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o trace -- \
   python "$R/bench.py" --steps 20 --warmup 5 $ARGS > "$OUT/trace.log" 2>&1 || exit 1
 i=0

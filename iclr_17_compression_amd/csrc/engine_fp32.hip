@@ -119,13 +119,11 @@ struct EngineArgs {
   long w6_plane;
   float* fold_total;        // scale · Σ, 0-dim
   double fold_scale;
-  // h3 form (common.h): the H3 instantiations read the input as two fp16 planes (in_split) and the
-  // weights pre-split into two fp16 planes (w6, [2][taps][CI/8][CO][8]) whose packing trailer
-  // holds 2⁻¹¹/(σ_a·σ_w) at wscale[1]; any epilogue may also write its output in the h3 form
+  // deconv3 in the h3 form (deconv3_x6_kernel<CI, true>): the input as two fp16 planes
+  // (in_split) and the weights pre-split into two fp16 planes whose packing trailer holds
+  // 2⁻¹¹/(σ_a·σ_w) at wscale[1]; range: the chain's h3 range flag (read only, the NaN poison)
   const float* wscale;
-  unsigned short* out_h3;           // [2][B][Hout][Wout][CO] or nullptr
-  long out_h3_plane;
-  int* range;                       // h3 range flag (nullable)
+  int* range;
 };
 
 // iclr17_reduce_partials inside the last kernel of the eval chain (deconv3): the per-image sums of
@@ -257,26 +255,6 @@ __device__ __forceinline__ void store_tile_rows_split(const EngineArgs& a, const
     *(u4*)(d + a.out_plane) = mi;
     *(u4*)(d + 2 * a.out_plane) = lo;
   }
-}
-
-// Store an [R][BN] LDS tile as the two fp16 planes of the h3 form (x·σ_a split, common.h), 4
-// channels (8 bytes per plane) per lane; a value the form cannot hold sets the range flag.
-template <int BN, int R = BM, int T = 256>
-__device__ __forceinline__ void store_tile_rows_h3(const EngineArgs& a, const TileInfo& t,
-                                                   const float* s, int ld, int CO, int col0) {
-  constexpr int C4 = BN / 4;
-  bool ovf = false;
-  for (int idx = threadIdx.x; idx < R * C4; idx += T) {
-    const int m = idx / C4, c4 = idx % C4;
-    const long p = out_pixel(a, t, m);
-    if (p < 0) continue;
-    uint2 hb, lb;
-    h3_split4(*(const f4*)(s + m * ld + c4 * 4), hb, lb, ovf);
-    unsigned short* d = a.out_h3 + p * CO + col0 + c4 * 4;
-    *(uint2*)d = hb;
-    *(uint2*)(d + a.out_h3_plane) = lb;
-  }
-  if (ovf && a.range) atomicOr(a.range, 1);
 }
 
 // Column sums of an LDS tile [BM][ld] over the rows inside the output grid → dst[blockIdx.x][CO],
@@ -644,7 +622,6 @@ __device__ __forceinline__ void gdn_epilogue(f4 (&x)[MT][NT], float* smem, const
                                           a.ggamma6);
   if (a.out != nullptr) store_tile_rows<CO, R, T>(a, t, smem, XS, a.out, CO, 0);
   if (a.out_split != nullptr) store_tile_rows_split<CO, R, T>(a, t, smem, XS, CO, 0);
-  if (a.out_h3 != nullptr) store_tile_rows_h3<CO, R, T>(a, t, smem, XS, CO, 0);
   if (a.pre != nullptr) {
     __syncthreads();
     acc_to_lds<MT, NT>(x, smem, XS, wm, ncol0, lane);
@@ -893,7 +870,6 @@ __device__ __forceinline__ void quant_epilogue(f4 (&acc)[MT][NT], float* smem, c
   __syncthreads();
   store_tile_rows<BN>(a, t, sO, OS, a.yhat, CO, cbase);
   if (a.out_split != nullptr) store_tile_rows_split<BN>(a, t, sO, OS, CO, cbase);   // ŷ, x6 form
-  if (a.out_h3 != nullptr) store_tile_rows_h3<BN>(a, t, sO, OS, CO, cbase);         // ŷ, h3 form
   if (a.out != nullptr) {
     __syncthreads();
 #pragma unroll
@@ -1006,26 +982,19 @@ __device__ __forceinline__ void out3_epilogue(f4 (&acc)[MT][NT], float* smem, co
 // the fragments are read as they are: conv3's 2×2 waves split each weight column for only two
 // row tiles, so the per-step split was 3.7 VALU instructions per MFMA. Same bf16 operands (the
 // split is iclr17_split_packed's, i.e. the same split8 on the same quads): bit-identical output.
-// H3 (the h3 form, common.h; conv2 / conv3 of the parity mode): A arrives as two fp16 planes
-// [2][BM][32] (the x6 A image's geometry with two planes: the same bytes as an fp32 A image), B
-// pre-split as two fp16 planes [2][4][BN][8] (the same bytes as an fp32 B stage), and a 32-deep
-// step is three v_mfma_f32_16x16x32_f16 per 16×16 tile, lo_a·hi_w + hi_a·lo_w + hi_a·(hi_w·2¹¹),
-// in place (inside the two-level accumulation where TAPSEP applies); the epilogue scales the
-// contraction by 2⁻¹¹/(σ_a·σ_w) (exact) before the bias.
-template <int CI, int CO, int BN, int WM, int WN, int EPI, bool X6, int BMT = BM, bool W6 = false,
-          bool H3 = false>
+// (The h3 form's convolutions run on the h3 engine, csrc/engine_h3.hip.)
+template <int CI, int CO, int BN, int WM, int WN, int EPI, bool X6, int BMT = BM, bool W6 = false>
 __device__ __forceinline__ void engine_body(const EngineArgs& a) {
-  constexpr bool XS = X6 || H3;                  // 16-bit split-form A planes
-  constexpr int APL = H3 ? 2 : 3;                // A / pre-split B planes
+  constexpr bool XS = X6;                        // 16-bit split-form A planes
+  constexpr int APL = 3;                         // A / pre-split B planes
   constexpr int NWV = WM * WN;                   // waves (4, or 8 for the 128-row tiles)
   constexpr int MT = BMT / WM / 16;
   constexpr int NT = BN / WN / 16;
   constexpr int KCH = 32;                        // input channels per k-step
   constexpr int NCH = CI / KCH;
-  static_assert(!W6 || (X6 && EPI == EPI_QUANT) || H3, "pre-split weights: x6 conv3, h3");
-  static_assert(!H3 || (W6 && !X6 && (EPI == EPI_GDN || EPI == EPI_QUANT)), "h3: conv2 / conv3");
+  static_assert(!W6 || (X6 && EPI == EPI_QUANT), "pre-split weights: x6 conv3");
   constexpr int SA = XS ? APL * BMT * KCH / 2 : BMT * KCH;   // A image floats per stage
-  constexpr int SB = W6 ? APL * 4 * BN * 8 / 2   // W6: [3][4][BN][8] bf16 | H3: [2][4][BN][8] fp16
+  constexpr int SB = W6 ? APL * 4 * BN * 8 / 2   // W6: [3][4][BN][8] bf16
                         : KCH * BN;              // B image floats per stage: [8 quads][BN][4]
   constexpr int STAGE = SA + SB;
   constexpr int NAI = SA * 4 / 1024;             // A glds wave-instructions per step (8 | 12)
@@ -1204,36 +1173,7 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
     x6_flush<false>(acc, st);
   };
 
-  // H3: one 32-deep step, three f16 products per tile (B: hi_w, lo_w planes; hi_w·2¹¹ formed here)
-  auto compute_h3 = [&](int buf) {
-    const unsigned short* sa = (const unsigned short*)(smem + buf * STAGE);
-    const unsigned short* sb6 = (const unsigned short*)(smem + buf * STAGE + SA) +
-                                ((lane >> 4) * BN + wn * (BN / WN) + (lane & 15)) * 8;
-    u4 Bh[NT], Bl[NT], Bh11[NT];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      Bh[nt] = *(const u4*)(sb6 + nt * 128);
-      Bl[nt] = *(const u4*)(sb6 + 32 * BN + nt * 128);
-      Bh11[nt] = h3_x2048(Bh[nt]);
-    }
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const h8v Ah = __builtin_bit_cast(h8v, *(const u4*)(sa + aoff6[mt]));
-      const h8v Al = __builtin_bit_cast(h8v, *(const u4*)(sa + BMT * KCH + aoff6[mt]));
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        f4 c = __builtin_amdgcn_mfma_f32_16x16x32_f16(Al, __builtin_bit_cast(h8v, Bh[nt]), acc[mt][nt], 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ah, __builtin_bit_cast(h8v, Bl[nt]), c, 0, 0, 0);
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ah, __builtin_bit_cast(h8v, Bh11[nt]), c, 0, 0, 0);
-      }
-    }
-  };
-
   auto compute = [&](int buf) {
-    if constexpr (H3) {
-      compute_h3(buf);
-      return;
-    }
     if constexpr (X6) {
       compute6(buf);
       return;
@@ -1379,13 +1319,6 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
     }
   }
   __syncthreads();     // last stage reads done before the epilogue reuses LDS
-  if constexpr (H3) {   // the h3 contraction carries 2¹¹·σ_a·σ_w: a power of two, removed exactly
-    const float dsc = a.wscale[1];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = acc[mt][nt] * dsc;
-  }
 
   if constexpr (EPI == EPI_GDN || EPI == EPI_IGDN) {
     static_assert(BN == CO, "GDN fusion needs every channel of a pixel in the workgroup");
@@ -1425,10 +1358,9 @@ __device__ __forceinline__ void engine_body(const EngineArgs& a) {
   }
 }
 
-template <int CI, int CO, int BN, int WM, int WN, int EPI, bool X6 = false, bool W6 = false,
-          bool H3 = false>
+template <int CI, int CO, int BN, int WM, int WN, int EPI, bool X6 = false, bool W6 = false>
 __global__ void __launch_bounds__(256) engine_kernel(const EngineArgs a) {
-  engine_body<CI, CO, BN, WM, WN, EPI, X6, BM, W6, H3>(a);
+  engine_body<CI, CO, BN, WM, WN, EPI, X6, BM, W6>(a);
 }
 
 // The same kernel held to 256 VGPRs (2 waves per SIMD) where the compiler would otherwise just
@@ -2507,11 +2439,6 @@ struct SplitIO {
   const unsigned short* gammaT6 = nullptr;  // x6 backward: split transposed γ_eff
   const unsigned short* w6 = nullptr;       // x6 conv3: pre-split weights (engine W6)
   long w6_plane = 0;
-  bool h3 = false;                          // the H3 instantiations (in / w6 in the h3 form)
-  const float* wscale = nullptr;            // h3: the weight packing's trailer
-  unsigned short* out_h3 = nullptr;         // h3-form output
-  long out_h3_plane = 0;
-  int* range = nullptr;
 };
 
 static void apply_split(EngineArgs& a, const SplitIO* x6) {
@@ -2522,10 +2449,6 @@ static void apply_split(EngineArgs& a, const SplitIO* x6) {
   a.ggammaT6 = x6->gammaT6;
   a.w6 = x6->w6;
   a.w6_plane = x6->w6_plane;
-  a.wscale = x6->wscale;
-  a.out_h3 = x6->out_h3;
-  a.out_h3_plane = x6->out_h3_plane;
-  a.range = x6->range;
 }
 
 template <int N, int EPI = EPI_GDN>
@@ -2570,7 +2493,6 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
   if (bwd) a = *bwd;
   apply_split(a, x6);
   const bool X6in = a.in_split != nullptr;
-  const bool H3in = x6 != nullptr && x6->h3;
   a.in = in; a.w = wp; a.bias = bias; a.gbeta = beta; a.ggamma = gamma; a.out = out; a.pre = pre;
   a.B = B; a.Hin = Hin; a.Win = Win; a.Hout = Hin / 2; a.Wout = Win / 2;
   a.gh = a.Hout; a.gw = a.Wout; a.tiles_y = (a.gh + 7) / 8; a.tiles_x = (a.gw + 7) / 8;
@@ -2584,7 +2506,6 @@ int launch_conv5(const float* in, int B, int Hin, int Win, const float* wp, cons
     constexpr int WN = (BN / 16) % 4 == 0 ? 4 : 2, WM = 4 / WN;
     a.partials_per_image = a.tiles_x * a.tiles_y * (N / BN);
     dim3 grid(a.tiles_x * a.tiles_y * B, N / BN);
-    ICLR17_REQUIRE(!H3in, ICLR17_EINVAL, "conv3: the h3 form runs on the h3 engine (engine_h3.hip)");
     if constexpr (N == 192) {
       if (X6in && conv3_narrow(N, a.tiles_x * a.tiles_y, B, qmode)) {
         a.partials_per_image = a.tiles_x * a.tiles_y * (N / 48);

@@ -152,7 +152,8 @@ struct HPatch<HM_CONV1, TH> {
   using type = PatchC1<TH>;
 };
 
-template <int MODE, int TH, int CO, int CI, bool INT_IN>
+// NS: weight-ring stages (F + 2 for F DMA groups in flight)
+template <int MODE, int TH, int CO, int CI, bool INT_IN, int NS = 4>
 struct HK {
   static constexpr int NW = TH / 2, NTHR = NW * 64;
   static constexpr int NT = CO / 32;           // 32-channel accumulator tiles per wave
@@ -167,7 +168,7 @@ struct HK {
   static constexpr int NPB = C1 ? 1 : 2;       // patch buffers
   static constexpr int SB = 2 * 2 * CO * 16;   // weight stage: [plane 2][half 2][CO][8] fp16
   static constexpr int NBI = SB / 1024;
-  static constexpr int NST = 4;
+  static constexpr int NST = NS;
   static constexpr int MAIN = NPB * PBUF + NST * SB + 1024;
   static constexpr int NTH = NT / 2;           // epilogue: output tiles per pass
   static constexpr int KB = CO / 16;           // epilogue: 16-channel k-blocks
@@ -307,7 +308,11 @@ template <int MODE, int TH, int CO, int CI, int EPI, bool INT_IN, int PH, int CO
 __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, int b, int ty, int tx,
                                          int cg = 0) {
   static_assert(CO % COT == 0 && (COT == CO || EPI == HE_QUANT), "channel groups: conv3 only");
-  using KK = HK<MODE, TH, COT, CI, INT_IN>;
+  // conv3's short steps (9 MFMAs per wave, one wave per SIMD) keep four DMA groups in flight, so
+  // a weight slot has four steps to arrive instead of two (the other layers' 18-MFMA steps on two
+  // waves per SIMD cover the latency with two)
+  constexpr int NSG = EPI == HE_QUANT ? 6 : 4;
+  using KK = HK<MODE, TH, COT, CI, INT_IN, NSG>;
   using P = typename KK::P;
   constexpr bool CONV = MODE != BM_DECONV, C8 = MODE == HM_CONV8, C1 = MODE == HM_CONV1;
   using TP = Taps<CONV ? BM_CONV : BM_DECONV, PH>;
@@ -322,7 +327,7 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
   // per step — weight slots of step g+F+1, pieces of the next chunk's patch during steps
   // 0 .. S-F-1, sink loads as padding — so `s_waitcnt vmcnt((F-1)·K)` + barrier at step g retires
   // all but the newest F-1 groups: step g+1's stage is complete when step g reads it ahead
-  constexpr int F = S >= 3 ? 2 : 1, SI = S - F;
+  constexpr int F = NSG - 2 < S - 1 ? NSG - 2 : (S >= 3 ? 2 : 1), SI = S - F;
   static_assert(SI >= 1 && NST >= F + 2, "DMA schedule");
   constexpr int PS = (KK::NQI + SI - 1) / SI;
   constexpr int K = (NBI + PS + NW - 1) / NW;
@@ -593,7 +598,7 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
   vm_barrier();   // trailing sink loads landed; every wave is done with the stages
   if constexpr (EPI == HE_QUANT) {
     // (the kernel's LDS is sized by the full-input form: HK<…, false>)
-    using KF = HK<MODE, TH, COT, CI, false>;
+    using KF = HK<MODE, TH, COT, CI, false, NSG>;
     static_assert(TH / 2 * 64 * 128 <= KF::BBOFF, "the epilogue's lane rows fit the stages");
     quant_epilogue<TH, CO, COT>(a, acc, smem, smem + KF::BBOFF, b, ty, tx, cg);
     return;
@@ -837,8 +842,9 @@ template <int MODE, int TH, int CO, int CI, int EPI, bool INT_OK, int COT = CO, 
           int ICM = 0>
 // two waves per SIMD either way: TH = 16 (8 waves) one workgroup per CU, TH = 8 (4 waves) two
 __global__ void __launch_bounds__(TH / 2 * 64, TH == 8 ? 2 : 1) h3k_kernel(const HArgs a) {
-  using KK = HK<MODE, TH, COT, CI, false>;
-  static_assert(KK::LDS >= HK<MODE, TH, COT, CI, true>::LDS, "LDS");
+  constexpr int NSG = EPI == HE_QUANT ? 6 : 4;   // as h3k_body's
+  using KK = HK<MODE, TH, COT, CI, false, NSG>;
+  static_assert(KK::LDS >= HK<MODE, TH, COT, CI, true, NSG>::LDS, "LDS");
   __shared__ __attribute__((aligned(16))) unsigned char smem[KK::LDS];
   int bid = blockIdx.x;
   const int per_ph = a.tiles_x * a.tiles_y * a.B;
@@ -1210,21 +1216,20 @@ int launch_deconv(const HArgs& a0, hipStream_t st) {
 }
 
 // conv3 + quantiser + rate on the h3 engine: 8 × 16-pixel tiles of 4 waves, each workgroup one
-// output-channel slice of 96 (N = 192) or 64 (N = 128) channels — B = 64 gives 256 workgroups
-// (conv3's 16 × 16 output per 256² image is one 16 × 16 tile, 64 workgroups without a split) —
-// and two-level sums per 8-channel chunk. The slice does not change an element's summation order,
-// so an image's results do not depend on its batch. (Measured and left out: 16 × 16 tiles with
-// 64 / 96 / 192 channels, 32-channel slices, and split-K over 2 / 4 / 8 workgroups per tile with
-// a second reducing launch — 0.16–0.44 ms against this form's 0.14.)
-constexpr int kC3TH = 8;
-template <int N>
-constexpr int conv3_cot() { return N == 192 ? 96 : 64; }
+// 64-channel slice of the output channels (B = 64 at N = 192: 384 workgroups; conv3's 16 × 16
+// output per 256² image is one 16 × 16 tile, 64 workgroups without the split), two-level sums per
+// 8-channel chunk, and four DMA groups in flight (h3k_body: NSG). The slice does not change an
+// element's summation order, and it does not depend on the batch, so an image's results do not
+// depend on the batch it is in. Measured (B = 64 eval / B = 32 noise, one box): 64-channel slices
+// 0.114 / 0.119 ms, 96-channel 0.116 / 0.166, 32-channel 0.146 / 0.111; left out earlier: 16 × 16
+// tiles with 64 / 96 / 192 channels and split-K over 2 / 4 / 8 workgroups per tile with a second
+// reducing launch (0.16–0.44 ms).
+constexpr int kC3TH = 8, kC3COT = 64;
 
 template <int N>
 static void launch_conv3(const HArgs& a, hipStream_t st) {
-  constexpr int COT = conv3_cot<N>();
-  hipLaunchKernelGGL((h3k_kernel<HM_CONV8, kC3TH, N, N, HE_QUANT, false, COT, true, kConvCM>),
-                     dim3(a.tiles_x * a.tiles_y * a.B * (N / COT)), dim3(kC3TH / 2 * 64), 0, st, a);
+  hipLaunchKernelGGL((h3k_kernel<HM_CONV8, kC3TH, N, N, HE_QUANT, false, kC3COT, true, kConvCM>),
+                     dim3(a.tiles_x * a.tiles_y * a.B * (N / kC3COT)), dim3(kC3TH / 2 * 64), 0, st, a);
 }
 
 static bool valid_cm(int cm, int N) { return cm == 0 || ((cm == 8 || cm == 16 || cm == 32) && N % cm == 0); }
@@ -1461,7 +1466,7 @@ int iclr17_synthesis_deconv_igdn_h3(const uint16_t* in_h3, int B, int h, int w, 
 int iclr17_conv3_h3_partials_per_image(int B, int H, int W, int N, int quant_mode) {
   (void)quant_mode;
   if (B <= 0 || H <= 0 || W <= 0 || H % 16 || W % 16 || (N != 128 && N != 192)) return 0;
-  return ((H / 16 + kC3TH - 1) / kC3TH) * ((W / 16 + 15) / 16) * (N / (N == 192 ? 96 : 64));
+  return ((H / 16 + kC3TH - 1) / kC3TH) * ((W / 16 + 15) / 16) * (N / kC3COT);
 }
 
 int iclr17_analysis_conv3_quant_rate_h3(const uint16_t* in_h3, int B, int H, int W, int N,

@@ -526,8 +526,8 @@ int iclr17_analysis_conv2_gdn_h3(const uint16_t* in_h3, int B, int H, int W, int
  * iclr17_analysis_conv3_quant_rate (round or noise mode, rate_table nullable; y_out nullable), ŷ
  * also in the h3 form (y_hat_h3 nullable; layout out_cm as conv1_gdn_h3, deconv1 reads 16). Input
  * the h3 form chunk-major 8 (conv2_gdn_h3 with out_cm 8). 8 × 16-pixel output tiles of 4 waves,
- * each workgroup one slice of 96 (N = 192) / 64 (N = 128) output channels, 8-channel input chunks
- * summed two-level. w_h3k: iclr17_pack_h3k(ICLR17_H3K_CONV5) of conv3's weights. Bit partials
+ * each workgroup one 64-channel slice of the output channels, 8-channel input chunks summed
+ * two-level. w_h3k: iclr17_pack_h3k(ICLR17_H3K_CONV5) of conv3's weights. Bit partials
  * [B][iclr17_conv3_h3_partials_per_image(B, H, W, N, quant_mode)]. */
 int iclr17_conv3_h3_partials_per_image(int B, int H, int W, int N, int quant_mode);
 int iclr17_analysis_conv3_quant_rate_h3(const uint16_t* in_h3, int B, int H, int W, int N,

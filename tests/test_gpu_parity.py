@@ -836,7 +836,7 @@ def test_deconv3_bits_fold(device, T):
 def test_conv3_narrow_tiles_match_wide(device, form):
     """Noise-mode conv3 at N=192 on a small and a large batch: x6 takes different tilings (under
     256 tiles·images the 48-column tiles, conv3_narrow, at or above it the 96-column ones), the h3
-    engine the same one (8 × 16 tiles × 96-channel slices) at every batch. The same images in both
+    engine the same one (8 × 16 tiles × 64-channel slices) at every batch. The same images in both
     batches give bit-equal y, ỹ and its split / h3 form (an output element's summation order does
     not depend on the tiling), and per-image bits that agree to summation order (x6: the partial
     counts differ) or bit for bit (h3)."""

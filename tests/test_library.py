@@ -45,10 +45,10 @@ def test_version_and_size_queries():
     assert _lib.query("iclr17_conv3_x6_partials_per_image", 32, 256, 256, 192, Q) == 4 * 4
     assert _lib.query("iclr17_conv3_x6_partials_per_image", 64, 256, 256, 192, Q) == 4 * 2
     assert _lib.query("iclr17_conv3_x6_partials_per_image", 2, 256, 256, 128, Q) == 4 * 2
-    # h3 engine: 8×16 tiles (2 per 256² image) × output-channel slices of 96 (N=192) / 64 (N=128)
-    assert _lib.query("iclr17_conv3_h3_partials_per_image", 64, 256, 256, 192, R) == 2 * 2
-    assert _lib.query("iclr17_conv3_h3_partials_per_image", 32, 256, 256, 192, Q) == 2 * 2
-    assert _lib.query("iclr17_conv3_h3_partials_per_image", 1, 2048, 2048, 192, R) == 128 * 2
+    # h3 engine: 8×16 tiles (2 per 256² image) × 64-channel output slices
+    assert _lib.query("iclr17_conv3_h3_partials_per_image", 64, 256, 256, 192, R) == 2 * 3
+    assert _lib.query("iclr17_conv3_h3_partials_per_image", 32, 256, 256, 192, Q) == 2 * 3
+    assert _lib.query("iclr17_conv3_h3_partials_per_image", 1, 2048, 2048, 192, R) == 128 * 3
     assert _lib.query("iclr17_conv3_h3_partials_per_image", 64, 256, 256, 128, R) == 2 * 2
     assert _lib.query("iclr17_conv3_h3_partials_per_image", 2, 256, 512, 128, Q) == 4 * 2
     assert _lib.query("iclr17_conv3_h3_partials_per_image", 2, 40, 256, 128, Q) == 0

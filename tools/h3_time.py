@@ -35,11 +35,15 @@ img = torch.from_numpy(synth.uniform(7, (B, 3, 256, 256), 0.0, 1.0)).to(dev)
 a1h = kernels.h3_planes(torch.from_numpy(synth.normal_like(8, (B, 64, 64, N), 0.7)).to(dev),
                         cm=kernels.CONV_CM)
 rate, rtab = net.bitEstimator.packed(), net.bitEstimator.rate_table()
+hh8_32 = hh8[:, :32].contiguous()
+noise32 = torch.from_numpy(synth.uniform(9, (32, N, 16, 16), -0.5, 0.5)).to(dev)
 runs = {
     "conv1_x6": lambda: kernels.conv1x6_gdn(img, enc.packed_conv1_x6(), enc.conv1.bias, g1x[0], g1x[2], N),
     "conv1_h3": lambda: kernels.conv1_gdn_h3(img, w1h, enc.conv1.bias, *ge1, N),
     "conv2_h3": lambda: kernels.conv2_gdn_h3(a1h, w2h, enc.conv2.bias, *ge2),
     "conv3_h3": lambda: kernels.conv3_quant_rate_h3(hh8, w3h, rate, rtab=rtab),
+    # the training step's conv3: noise mode at B = 32
+    "conv3_h3_noise32": lambda: kernels.conv3_quant_rate_h3(hh8_32, w3h, rate, noise32),
     "deconv2_old": lambda: kernels.deconv_igdn_x6(hs, d2, dec.deconv2.bias, *q2, chunk_major=True),
     "deconv2_h3": lambda: kernels.deconv_igdn_h3(hh, x2, dec.deconv2.bias, *h2, want_h3=False,
                                                  want_x6=True, chunk_major=True),

@@ -468,7 +468,7 @@ int iclr17_rate_param_grad(const float* partial, int T, int C, const float* h1, 
  * per-tensor power-of-two scale chosen at packing. Against float64 its dot products land closer
  * than the x6 chain's (tools/h3_numerics.hip). |x| ≥ 2^22 does not fit the form: the kernels then
  * set *range_flag (nullable) to 1. Halo patch of the h3 input per 16-channel chunk, a wave owns 32
- * pixels × all N channels, GDN/IGDN contraction (x6) from the accumulators.
+ * pixels × all N channels, GDN/IGDN contraction (in the h3 form) from the accumulators.
  * Replaces iclr17_synthesis_deconv_igdn_x6[_cm] on the parity path
  * (synthesis_17.py:15-22; models/GDN.py:64-94, inverse). */
 #define ICLR17_H3K_CONV5 42   /* conv2 W[co][ci][5][5] → [2][N/8·13][2][N][8] fp16 planes + trailer */

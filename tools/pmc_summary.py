@@ -45,7 +45,7 @@ LAYER_KERNELS = {
     "h3": {   # h3k_kernel<MODE, TH, CO, CI, EPI, INT_OK, COT, SEP, ICM>
         "conv1_gdn1": (r"h3k_kernel<3, 16, 192, 3, 0, false, 192, false, 0>", None),
         "conv2_gdn2": (r"h3k_kernel<2, 16, 192, 192, 0, false, 192, false, 8>", None),
-        "conv3_quant_rate": (r"h3k_kernel<2, 8, 192, 192, 2, false, 96, true, 8>", None),
+        "conv3_quant_rate": (r"h3k_kernel<2, 8, 192, 192, 2, false, 64, true, 8>", None),
         "deconv1_igdn1": (r"h3k_kernel<1, 16, 192, 192, 1, true, 192, false, 16>", None),
         "deconv2_igdn2": (r"h3k_kernel<1, 16, 192, 192, 1, false, 192, false, 16>", None),
         "deconv3_clamp": (r"deconv3_x6_kernel<192, true>", None),

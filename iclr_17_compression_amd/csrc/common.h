@@ -192,24 +192,21 @@ __device__ __forceinline__ unsigned short h16_bits(_Float16 v) {
   return __builtin_bit_cast(unsigned short, v);
 }
 
-// x → (hi, lo) of a = x·σ_a; ovf |= a does not fit (finite and ≥ 65520 in magnitude)
-__device__ __forceinline__ void h3_split1(float x, unsigned short& hi, unsigned short& lo,
-                                          bool& ovf) {
-  const float a = x * kH3Sa;
-  const _Float16 h = (_Float16)a;
-  const _Float16 l = (_Float16)((a - (float)h) * 2048.0f);
-  hi = h16_bits(h);
-  lo = h16_bits(l);
-  ovf |= fabsf(a) >= 65520.0f && fabsf(a) <= 3.40282347e38f;
-}
-
-// 4 consecutive values → 8 bytes of each plane
+// 4 consecutive values x → 8 bytes of each plane of a = x·σ_a: hi = rne16(a), lo = rne16((a − hi)·2¹¹),
+// converted two at a time (v_cvt_pk_f16_f32); ovf |= one of the four does not fit (|a| ≥ 65520 — an
+// infinite value counts too: its results are not finite either way). The check is one compare on
+// the largest |a| of the four (NaN ignored by the max), not two per value: in the GDN epilogues
+// the per-value compares were a tenth of the VALU work
 __device__ __forceinline__ void h3_split4(const f4& x, uint2& hi, uint2& lo, bool& ovf) {
-  unsigned short h[4], l[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) h3_split1(x[j], h[j], l[j], ovf);
-  hi = uint2{h[0] | ((unsigned)h[1] << 16), h[2] | ((unsigned)h[3] << 16)};
-  lo = uint2{l[0] | ((unsigned)l[1] << 16), l[2] | ((unsigned)l[3] << 16)};
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 a0 = f2{x[0], x[1]} * kH3Sa, a1 = f2{x[2], x[3]} * kH3Sa;
+  const h2v h0 = __builtin_convertvector(a0, h2v), h1 = __builtin_convertvector(a1, h2v);
+  const h2v l0 = __builtin_convertvector((a0 - __builtin_convertvector(h0, f2)) * 2048.0f, h2v);
+  const h2v l1 = __builtin_convertvector((a1 - __builtin_convertvector(h1, f2)) * 2048.0f, h2v);
+  hi = uint2{__builtin_bit_cast(unsigned, h0), __builtin_bit_cast(unsigned, h1)};
+  lo = uint2{__builtin_bit_cast(unsigned, l0), __builtin_bit_cast(unsigned, l1)};
+  const float m = fmaxf(fmaxf(fabsf(a0.x), fabsf(a0.y)), fmaxf(fabsf(a1.x), fabsf(a1.y)));
+  ovf |= m >= 65520.0f;
 }
 
 // 8 fp16 values × 2¹¹ (exact while they stay below 32: the weight scaling guarantees it)

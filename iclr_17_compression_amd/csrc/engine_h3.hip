@@ -188,10 +188,12 @@ struct HK {
 // conv3's output is rounded into ŷ).
 // u16 offset (within a plane) of 8 channels ch .. ch + 7 of output pixel (oy, ox) of image b in the
 // h3 output's layout: NHWC (out_cm = 0) or chunk-major [B][CO/out_cm][Hout][Wout][out_cm]
+// (cm is a power of two: shifts and masks, not the integer divisions a runtime divisor compiles to)
 __device__ __forceinline__ long h3_out_off(const HArgs& a, int b, int oy, int ox, int CO, int ch) {
   const int cm = a.out_cm;
   if (cm == 0) return (((long)b * a.Hout + oy) * a.Wout + ox) * CO + ch;
-  return ((((long)b * (CO / cm) + ch / cm) * a.Hout + oy) * a.Wout + ox) * cm + ch % cm;
+  const int sh = __builtin_ctz(cm);
+  return ((((long)b * (CO >> sh) + (ch >> sh)) * a.Hout + oy) * a.Wout + ox << sh) + (ch & (cm - 1));
 }
 
 // conv3's epilogue (HE_QUANT): y = acc·2⁻¹¹/(σ_a·σ_w) (no bias, analysis_17.py:22), then

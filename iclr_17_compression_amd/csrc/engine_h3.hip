@@ -1206,6 +1206,16 @@ __global__ void __launch_bounds__(256) h3_planes_cm_kernel(const float* __restri
 // chunk-major 16 (the deconv mode's 16-channel chunks), deconv2 → deconv3 chunk-major 32.
 constexpr int kConvCM = 8, kDeconvCM = 16;
 
+// Tile height of a conv2 launch: 16 rows (8 waves, one workgroup per CU) unless that leaves CUs
+// idle (fewer workgroups than the 256 CUs: training's B = 32), then 8 rows (4 waves), twice the
+// workgroups. A pixel's arithmetic does not depend on the tile (the same chunk and tap order, the
+// same per-pixel epilogue), so the results are bitwise the same. (The deconv mode at 8 rows
+// spills at N = 192 under the two-workgroups-per-CU register budget, so it keeps 16.)
+constexpr int kCUs = 256;
+inline int h3_tile_rows(int gh, int gw, int B) {
+  return (long)((gh + 15) / 16) * ((gw + 15) / 16) * B < kCUs ? 8 : 16;
+}
+
 template <int N, bool INT_OK>
 int launch_deconv(const HArgs& a0, hipStream_t st) {
   constexpr int TH = 16;
@@ -1422,16 +1432,21 @@ int iclr17_analysis_conv2_gdn_h3(const uint16_t* in_h3, int B, int H, int W, int
   a.range = range_flag;
   a.B = B; a.Hin = h; a.Win = w; a.Hout = h / 2; a.Wout = w / 2;
   a.gh = h / 2; a.gw = w / 2;
-  constexpr int TH = 16;
+  const int TH = h3_tile_rows(a.gh, a.gw, B);
   a.tiles_y = (a.gh + TH - 1) / TH;
   a.tiles_x = (a.gw + 15) / 16;
-  const dim3 grid(a.tiles_x * a.tiles_y * B);
-  if (N == 192)
-    hipLaunchKernelGGL((h3k_kernel<HM_CONV8, TH, 192, 192, HE_GDN, false, 192, false, kConvCM>), grid,
-                       dim3(TH / 2 * 64), 0, (hipStream_t)stream, a);
-  else
-    hipLaunchKernelGGL((h3k_kernel<HM_CONV8, TH, 128, 128, HE_GDN, false, 128, false, kConvCM>), grid,
-                       dim3(TH / 2 * 64), 0, (hipStream_t)stream, a);
+  const dim3 grid(a.tiles_x * a.tiles_y * B), block(TH / 2 * 64);
+  hipStream_t st = (hipStream_t)stream;
+  if (TH == 8) {
+    if (N == 192)
+      hipLaunchKernelGGL((h3k_kernel<HM_CONV8, 8, 192, 192, HE_GDN, false, 192, false, kConvCM>), grid, block, 0, st, a);
+    else
+      hipLaunchKernelGGL((h3k_kernel<HM_CONV8, 8, 128, 128, HE_GDN, false, 128, false, kConvCM>), grid, block, 0, st, a);
+  } else if (N == 192) {
+    hipLaunchKernelGGL((h3k_kernel<HM_CONV8, 16, 192, 192, HE_GDN, false, 192, false, kConvCM>), grid, block, 0, st, a);
+  } else {
+    hipLaunchKernelGGL((h3k_kernel<HM_CONV8, 16, 128, 128, HE_GDN, false, 128, false, kConvCM>), grid, block, 0, st, a);
+  }
   return check_launch("conv2_gdn_h3");
 }
 

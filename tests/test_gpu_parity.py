@@ -832,6 +832,31 @@ def test_deconv3_bits_fold(device, T):
         assert torch.equal(c2, c3) and torch.equal(tot2, ref)
 
 
+@pytest.mark.gpu
+def test_conv2_h3_tile_rows_match(device):
+    """conv2 + GDN2 on the h3 engine takes 8-row tiles when 16-row ones would leave CUs idle (a
+    small batch: training's B = 32 at 256²) and 16-row ones otherwise. The same images in a small
+    (8-row) and a large (16-row) batch give bit-equal h3, fp32, x6 and pre-activation outputs: a
+    pixel's arithmetic does not depend on the tile."""
+    N, h, w = 192, 64, 64              # conv2 output 32×32: four 16×16 tiles per image
+    Bs, Bw = 3, 64                     # 12 tiles·images < 256 CUs (8 rows), 256 (16 rows)
+    net = net_for(N, 1, device)
+    enc = net.Encoder
+    w2h = enc.packed_h3()[0]
+    ge2 = enc.gdn2.effective_params_h3()
+    a1 = torch.from_numpy(synth.normal_like(33, (Bw, h, w, N), 0.7)).to(device)
+
+    def run(B):
+        return kernels.conv2_gdn_h3(kernels.h3_planes(a1[:B].contiguous(), cm=kernels.CONV_CM), w2h,
+                                    enc.conv2.bias, *ge2, want_f32=True, want_x6=True, want_pre=True)
+
+    small, wide = run(Bs), run(Bw)
+    assert torch.equal(small[0], wide[0][:, :Bs])      # h3 planes [2][B][…]
+    assert torch.equal(small[1], wide[1][:Bs])         # fp32
+    assert torch.equal(small[2], wide[2][:, :Bs])      # x6 split [3][B][…]
+    assert torch.equal(small[3], wide[3][:Bs])         # GDN2's input
+
+
 @pytest.mark.parametrize("form", ["h3", "x6"])
 def test_conv3_narrow_tiles_match_wide(device, form):
     """Noise-mode conv3 at N=192 on a small and a large batch: x6 takes different tilings (under

@@ -36,11 +36,15 @@ a1h = kernels.h3_planes(torch.from_numpy(synth.normal_like(8, (B, 64, 64, N), 0.
                         cm=kernels.CONV_CM)
 rate, rtab = net.bitEstimator.packed(), net.bitEstimator.rate_table()
 hh8_32 = hh8[:, :32].contiguous()
+a1h_32 = a1h[:, :32].contiguous()
 noise32 = torch.from_numpy(synth.uniform(9, (32, N, 16, 16), -0.5, 0.5)).to(dev)
 runs = {
     "conv1_x6": lambda: kernels.conv1x6_gdn(img, enc.packed_conv1_x6(), enc.conv1.bias, g1x[0], g1x[2], N),
     "conv1_h3": lambda: kernels.conv1_gdn_h3(img, w1h, enc.conv1.bias, *ge1, N),
     "conv2_h3": lambda: kernels.conv2_gdn_h3(a1h, w2h, enc.conv2.bias, *ge2),
+    # the training step's conv2 (B = 32: 8-row tiles) with its pre-activation and x6 outputs
+    "conv2_h3_train32": lambda: kernels.conv2_gdn_h3(a1h_32, w2h, enc.conv2.bias, *ge2, want_x6=True,
+                                                     want_pre=True),
     "conv3_h3": lambda: kernels.conv3_quant_rate_h3(hh8, w3h, rate, rtab=rtab),
     # the training step's conv3: noise mode at B = 32
     "conv3_h3_noise32": lambda: kernels.conv3_quant_rate_h3(hh8_32, w3h, rate, noise32),

@@ -842,8 +842,11 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
 // otherwise the full body.
 template <int MODE, int TH, int CO, int CI, int EPI, bool INT_OK, int COT = CO, bool SEP = false,
           int ICM = 0>
-// two waves per SIMD either way: TH = 16 (8 waves) one workgroup per CU, TH = 8 (4 waves) two
-__global__ void __launch_bounds__(TH / 2 * 64, TH == 8 ? 2 : 1) h3k_kernel(const HArgs a) {
+// two waves per SIMD: TH = 16 (8 waves) one workgroup per CU, TH = 8 (4 waves) two — except the
+// 8-row deconv, which runs where 16-row tiles would leave CUs idle (one workgroup per CU either
+// way) and at N = 192 spilled under the two-workgroup register budget
+__global__ void __launch_bounds__(TH / 2 * 64, TH == 8 && MODE != BM_DECONV ? 2 : 1)
+h3k_kernel(const HArgs a) {
   constexpr int NSG = EPI == HE_QUANT ? 6 : 4;   // as h3k_body's
   using KK = HK<MODE, TH, COT, CI, false, NSG>;
   static_assert(KK::LDS >= HK<MODE, TH, COT, CI, true, NSG>::LDS, "LDS");
@@ -1206,25 +1209,29 @@ __global__ void __launch_bounds__(256) h3_planes_cm_kernel(const float* __restri
 // chunk-major 16 (the deconv mode's 16-channel chunks), deconv2 → deconv3 chunk-major 32.
 constexpr int kConvCM = 8, kDeconvCM = 16;
 
-// Tile height of a conv2 launch: 16 rows (8 waves, one workgroup per CU) unless that leaves CUs
-// idle (fewer workgroups than the 256 CUs: training's B = 32), then 8 rows (4 waves), twice the
-// workgroups. A pixel's arithmetic does not depend on the tile (the same chunk and tap order, the
-// same per-pixel epilogue), so the results are bitwise the same. (The deconv mode at 8 rows
-// spills at N = 192 under the two-workgroups-per-CU register budget, so it keeps 16.)
+// Tile height of a conv2 / deconv launch: 16 rows (8 waves, one workgroup per CU) unless that
+// leaves CUs idle (fewer workgroups than the 256 CUs: training's B = 32 conv2 and deconv1), then
+// 8 rows (4 waves), twice the workgroups. A pixel's arithmetic does not depend on the tile (the
+// same chunk and tap order, the same per-pixel epilogue), so the results are bitwise the same.
 constexpr int kCUs = 256;
-inline int h3_tile_rows(int gh, int gw, int B) {
-  return (long)((gh + 15) / 16) * ((gw + 15) / 16) * B < kCUs ? 8 : 16;
+inline int h3_tile_rows(int gh, int gw, int B, int phases = 1) {
+  return (long)((gh + 15) / 16) * ((gw + 15) / 16) * B * phases < kCUs ? 8 : 16;
 }
 
-template <int N, bool INT_OK>
-int launch_deconv(const HArgs& a0, hipStream_t st) {
-  constexpr int TH = 16;
+template <int N, bool INT_OK, int TH>
+int launch_deconv_th(const HArgs& a0, hipStream_t st) {
   HArgs a = a0;
   a.tiles_y = (a.gh + TH - 1) / TH;
   a.tiles_x = (a.gw + 15) / 16;
   hipLaunchKernelGGL((h3k_kernel<BM_DECONV, TH, N, N, HE_IGDN, INT_OK, N, false, kDeconvCM>),
                      dim3(a.tiles_x * a.tiles_y * a.B * 4), dim3(TH / 2 * 64), 0, st, a);
   return check_launch("deconv_igdn_h3");
+}
+
+template <int N, bool INT_OK>
+int launch_deconv(const HArgs& a, hipStream_t st) {
+  return h3_tile_rows(a.gh, a.gw, a.B, 4) == 8 ? launch_deconv_th<N, INT_OK, 8>(a, st)
+                                               : launch_deconv_th<N, INT_OK, 16>(a, st);
 }
 
 // conv3 + quantiser + rate on the h3 engine: 8 × 16-pixel tiles of 4 waves, each workgroup one

@@ -857,6 +857,38 @@ def test_conv2_h3_tile_rows_match(device):
     assert torch.equal(small[3], wide[3][:Bs])         # GDN2's input
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("int_in", [False, True])
+def test_deconv_h3_tile_rows_match(device, int_in):
+    """deconv + IGDN on the h3 engine: 8-row tiles on a small batch (deconv1 at B = 3: 12 workgroups
+    of 16 rows would leave CUs idle), 16-row ones on a large one (B = 64); the same images give
+    bit-equal outputs, with the integer-input (ŷ) form and without."""
+    N, h, w = 192, 16, 16
+    Bs, Bw = 3, 64
+    net = net_for(N, 1, device)
+    dec = net.Decoder
+    x1 = dec.packed_h3k()[0]
+    h1 = dec.igdn1.effective_params_h3()
+    if int_in:
+        y = torch.round(torch.from_numpy(synth.uniform(34, (Bw, h, w, N), -6, 6))).to(device)
+    else:
+        y = torch.from_numpy(synth.normal_like(34, (Bw, h, w, N), 2.0)).to(device)
+
+    def run(B):
+        return kernels.deconv_igdn_h3(kernels.h3_planes(y[:B].contiguous(), cm=kernels.DECONV_CM), x1,
+                                      dec.deconv1.bias, *h1, want_f32=True, want_x6=True, want_pre=True,
+                                      int_in=int_in)
+
+    small, wide = run(Bs), run(Bw)
+    for s_, w_ in zip(small, wide):
+        if s_ is None:
+            continue
+        if s_.dim() == 4:
+            assert torch.equal(s_, w_[:Bs])
+        else:                       # planes first: [P][B][…]
+            assert torch.equal(s_, w_[:, :Bs])
+
+
 @pytest.mark.parametrize("form", ["h3", "x6"])
 def test_conv3_narrow_tiles_match_wide(device, form):
     """Noise-mode conv3 at N=192 on a small and a large batch: x6 takes different tilings (under

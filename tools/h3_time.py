@@ -37,6 +37,8 @@ a1h = kernels.h3_planes(torch.from_numpy(synth.normal_like(8, (B, 64, 64, N), 0.
 rate, rtab = net.bitEstimator.packed(), net.bitEstimator.rate_table()
 hh8_32 = hh8[:, :32].contiguous()
 a1h_32 = a1h[:, :32].contiguous()
+yt32 = kernels.h3_planes(torch.from_numpy(synth.normal_like(10, (32, 16, 16, N), 2.0)).to(dev),
+                         cm=kernels.DECONV_CM)
 noise32 = torch.from_numpy(synth.uniform(9, (32, N, 16, 16), -0.5, 0.5)).to(dev)
 runs = {
     "conv1_x6": lambda: kernels.conv1x6_gdn(img, enc.packed_conv1_x6(), enc.conv1.bias, g1x[0], g1x[2], N),
@@ -54,6 +56,9 @@ runs = {
     "deconv2_h3_h3out": lambda: kernels.deconv_igdn_h3(hh, x2, dec.deconv2.bias, *h2, chunk_major=True),
     "deconv1_old": lambda: kernels.deconv_igdn_x6(ys, d1, dec.deconv1.bias, *q1),
     "deconv1_h3": lambda: kernels.deconv_igdn_h3(yh, x1, dec.deconv1.bias, *h1),
+    # the training step's deconv1 (B = 32: 8-row tiles) on ỹ with its pre-activation and x6 outputs
+    "deconv1_h3_train32": lambda: kernels.deconv_igdn_h3(yt32, x1, dec.deconv1.bias, *h1, want_x6=True,
+                                                         want_pre=True),
     "deconv1_h3_int": lambda: kernels.deconv_igdn_h3(yh, x1, dec.deconv1.bias, *h1, int_in=True),
 }
 sel = os.environ.get("ONLY", "").split(",") if os.environ.get("ONLY") else list(runs)

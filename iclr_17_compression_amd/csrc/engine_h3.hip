@@ -195,6 +195,11 @@ __device__ __forceinline__ long h3_out_off(const HArgs& a, int b, int oy, int ox
   const int sh = __builtin_ctz(cm);
   return ((((long)b * (CO >> sh) + (ch >> sh)) * a.Hout + oy) * a.Wout + ox << sh) + (ch & (cm - 1));
 }
+// h3_out_off(…, ch + 32i) − h3_out_off(…, ch) for ch % 32 + 8 ≤ 32: the same for every lane (cm ≤ 32
+// divides 32), so the epilogues compute a lane's two offsets once and step them by i times this
+__device__ __forceinline__ long h3_out_step32(const HArgs& a) {
+  return a.out_cm == 0 ? 32L : 32L * a.Hout * a.Wout;
+}
 
 // conv3's epilogue (HE_QUANT): y = acc·2⁻¹¹/(σ_a·σ_w) (no bias, analysis_17.py:22), then
 // model.py:48-56 — ŷ = rint(y) (round) or ỹ = y + u (noise, u from the NCHW noise tensor) — and
@@ -619,6 +624,8 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
   const int ox = CONV ? gx : 2 * gx + (PH & 1);
   const long o = ((long)b * a.Hout + oy) * a.Wout + ox;
   const float dsc = a.wscale[1];   // 2⁻¹¹/(σ_a·σ_w): exact
+  const long hb0 = h3_out_off(a, b, oy, ox, CO, 16 * eh), hb1 = h3_out_off(a, b, oy, ox, CO, 16 * eh + 8);
+  const long hstep = h3_out_step32(a);
 #pragma unroll
   for (int i = 0; i < NT; ++i)
 #pragma unroll
@@ -748,13 +755,15 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
 #pragma unroll
     for (int il = 0; il < NTH; ++il) {
       const int i = hf * NTH + il;
-      f4 y[4];
+      f4 y[4], bes[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) bes[m] = *(const f4*)(sbb + 256 + 32 * i + 8 * m + 4 * eh);   // one wait
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const int ch = 32 * i + 8 * m + 4 * eh;
         if (inside && a.pre)
           *(f4*)(a.pre + o * CO + ch) = f4{acc[i][4 * m], acc[i][4 * m + 1], acc[i][4 * m + 2], acc[i][4 * m + 3]};
-        const f4 be = *(const f4*)(sbb + 256 + ch);
+        const f4 be = bes[m];
         // the hardware square root / reciprocal square root (v_sqrt_f32, v_rsq_f32: within an ulp
         // or two, far inside the h3 form's own 2⁻²² — and a sixth of the IEEE sequences' VALU
         // work, which set the epilogue's length); n ≥ β_min > 0
@@ -787,8 +796,7 @@ __device__ __forceinline__ void h3k_body(const HArgs& a, unsigned char* smem, in
             sv[pl][k] = u4{sx[0], sy[0], sx[1], sy[1]};
           }
         if (inside) {
-          const long s0 = h3_out_off(a, b, oy, ox, CO, 32 * i + 16 * eh);
-          const long s1 = h3_out_off(a, b, oy, ox, CO, 32 * i + 16 * eh + 8);
+          const long s0 = hb0 + i * hstep, s1 = hb1 + i * hstep;
           *(u4*)(a.out_h3 + s0) = sv[0][0];
           *(u4*)(a.out_h3 + s1) = sv[0][1];
           *(u4*)(a.out_h3 + a.out_h3_plane + s0) = sv[1][0];

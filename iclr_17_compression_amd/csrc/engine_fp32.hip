@@ -1392,6 +1392,14 @@ constexpr int D3_NAI = (3 * D3_PPX + 15) / 16;  // 61 A wave-instructions per ch
 constexpr int D3_SA = D3_NAI * 256;             // A stage floats (976 slots × 16)
 constexpr int D3_SB6 = 3 * 32 * 48 / 2;         // x6 B stage floats: [3 planes][4 k8][48][8] u16
 constexpr int D3_LDS = D3_SA + 2 * D3_SB6;      // 80,896 B: two workgroups per CU
+// deconv3 epilogue tile [3][64][64] fp32 (channel, output row, output column): row stride D3_ES,
+// channel stride D3_EC floats. A write instruction's 16 lanes of a group hold 16 (channel, ry, rx)
+// columns of one base pixel (d3_col order) and the lane groups base columns 16 floats apart; the
+// earlier [3][64][65] tile put those columns on ≈5 banks (6.7 LDS cycles per 32-lane group, 88 %
+// of the kernel's bank-conflict cycles); rows of 67 and channels of 64·67 + 11 floats spread them
+// (1.7 cycles, the best of the strides 64..99 × 64·stride + 0..39), and the store phase's reads
+// (8 columns × 4 rows per group) stay conflict-free.
+constexpr int D3_ES = 67, D3_EC = 64 * D3_ES + 11;
 
 // first weight block (tile-tap) of tap t in the compact per-chunk weight stage: taps 0-2 touch
 // one column tile, taps 3 and 6 two, the others three (see d3_col)
@@ -1432,7 +1440,7 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
   // padding pieces load the zero line)
   constexpr int NAI = H3 ? ((NPL * D3_PPX + 15) / 16 + 3) / 4 * 4 : (NPL * D3_PPX + 15) / 16;
   constexpr int AI_W = (NAI + 3) / 4;   // x6: 16 (wave 0..3 takes i = w + 4j, i < 61)
-  static_assert(3 * 64 * 65 <= D3_LDS, "epilogue block fits the stages");
+  static_assert(3 * D3_EC <= D3_LDS, "epilogue block fits the stages");
   __shared__ __attribute__((aligned(16))) float smem[D3_LDS];
   // H3: the range flag of the chain (set by an upstream h3 kernel whose output did not fit the
   // form, |x| ≥ 2²²) makes every result of this last kernel NaN — the reconstruction, the SSE
@@ -1621,8 +1629,8 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
   }
 
   // epilogue: column n = co·16 + ry·4 + rx of row m = (by, bx) → output (4by + ry, 4bx + rx)
-  constexpr int OS = 4 * D3_BS, SS = OS + 1;
-  float* sO = smem;   // [3][64][65]
+  constexpr int OS = 4 * D3_BS;
+  float* sO = smem;   // [3][64][64], strides D3_EC / D3_ES
   const int H = a.Hout, W = a.Wout;
   float sse = 0.f;
   for (int pass = 0; pass < 2; ++pass) {
@@ -1639,7 +1647,7 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
           float v = acc[mt][nt][r] + a.bias[co];
           if (pass == 0) v = fminf(fmaxf(v, 0.0f), 1.0f);
           if (poison) v = __builtin_nanf("");
-          sO[(co * OS + by * 4 + (ph >> 2)) * SS + bx * 4 + (ph & 3)] = v;
+          sO[co * D3_EC + (by * 4 + (ph >> 2)) * D3_ES + bx * 4 + (ph & 3)] = v;
         }
     __syncthreads();
     // wave w stores output quadrant (qy, qx) = (w >> 1, w & 1): 3 × 32 rows × 8 float4
@@ -1650,7 +1658,7 @@ __global__ void __launch_bounds__(256, 2) deconv3_x6_kernel(const EngineArgs a) 
       const int oyl = qy * 32 + row, oxl = qx * 32 + c4 * 4;
       const int oy = ty * OS + oyl, ox = tx * OS + oxl;
       if (oy >= H || ox >= W) continue;
-      const float* sp = sO + (co * OS + oyl) * SS + oxl;
+      const float* sp = sO + co * D3_EC + oyl * D3_ES + oxl;
       const f4 v = f4{sp[0], sp[1], sp[2], sp[3]};
       const long off = (((long)b * 3 + co) * H + oy) * W + ox;
       *(f4*)(dst + off) = v;
@@ -1821,7 +1829,7 @@ __global__ void __launch_bounds__(512) deconv3_bf16_kernel(const EngineArgs a) {
   constexpr int PB = NBI * 256;             // weight floats per chunk: [block][k8 4][16][8] bf16
   constexpr int KA = (NAI + NW - 1) / NW, KB = (NBI + NW - 1) / NW;
   constexpr int LDS = 2 * SA + 2 * PB;
-  static_assert(3 * 64 * 65 + 16 <= LDS, "epilogue block fits");
+  static_assert(3 * D3_EC + 16 <= LDS, "epilogue block fits");
   __shared__ __attribute__((aligned(16))) float smem[LDS];
   if (a.fold_partial != nullptr && blockIdx.x == 0) fold_bits<512>(a, (double*)smem);
   float* const sA = smem;
@@ -1924,9 +1932,9 @@ __global__ void __launch_bounds__(512) deconv3_bf16_kernel(const EngineArgs a) {
 
   // epilogue: column n = co·16 + ry·4 + rx of row m = (by, bx) → output (4by + ry, 4bx + rx);
   // the waves 2q, 2q+1 store output quadrant q's upper / lower 16 rows
-  constexpr int OS = 4 * D3_BS, SS = OS + 1;
-  float* sO = smem;   // [3][64][65]
-  float* red = smem + 3 * OS * SS;
+  constexpr int OS = 4 * D3_BS;
+  float* sO = smem;   // [3][64][64], strides D3_EC / D3_ES
+  float* red = smem + 3 * D3_EC;
   const int H = a.Hout, W = a.Wout;
   float sse = 0.f;
   int pcol[NT];
@@ -1946,7 +1954,7 @@ __global__ void __launch_bounds__(512) deconv3_bf16_kernel(const EngineArgs a) {
           const int co = pcol[nt] >> 4, ph = pcol[nt] & 15;
           float v = acc[mt][nt][r] + a.bias[co];
           if (pass == 0) v = fminf(fmaxf(v, 0.0f), 1.0f);
-          sO[(co * OS + by * 4 + (ph >> 2)) * SS + bx * 4 + (ph & 3)] = v;
+          sO[co * D3_EC + (by * 4 + (ph >> 2)) * D3_ES + bx * 4 + (ph & 3)] = v;
         }
     __syncthreads();
     const bool sse_pass = pass == (a.sse_unclipped ? 1 : 0) && a.xref != nullptr;
@@ -1955,7 +1963,7 @@ __global__ void __launch_bounds__(512) deconv3_bf16_kernel(const EngineArgs a) {
       const int oyl = qy * 32 + hf * 16 + row, oxl = qx * 32 + c4 * 4;
       const int oy = ty * OS + oyl, ox = tx * OS + oxl;
       if (oy >= H || ox >= W) continue;
-      const float* sp = sO + (co * OS + oyl) * SS + oxl;
+      const float* sp = sO + co * D3_EC + oyl * D3_ES + oxl;
       const f4 v = f4{sp[0], sp[1], sp[2], sp[3]};
       const long off = (((long)b * 3 + co) * H + oy) * W + ox;
       *(f4*)(dst + off) = v;

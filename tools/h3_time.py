@@ -35,6 +35,8 @@ img = torch.from_numpy(synth.uniform(7, (B, 3, 256, 256), 0.0, 1.0)).to(dev)
 a1h = kernels.h3_planes(torch.from_numpy(synth.normal_like(8, (B, 64, 64, N), 0.7)).to(dev),
                         cm=kernels.CONV_CM)
 rate, rtab = net.bitEstimator.packed(), net.bitEstimator.rate_table()
+h64 = kernels.h3_planes(torch.from_numpy(synth.normal_like(11, (B, 64, 64, N), 0.7)).to(dev),
+                        cm=kernels.DECONV3_CM)
 hh8_32 = hh8[:, :32].contiguous()
 a1h_32 = a1h[:, :32].contiguous()
 yt32 = kernels.h3_planes(torch.from_numpy(synth.normal_like(10, (32, 16, 16, N), 2.0)).to(dev),
@@ -54,6 +56,7 @@ runs = {
     "deconv2_h3": lambda: kernels.deconv_igdn_h3(hh, x2, dec.deconv2.bias, *h2, want_h3=False,
                                                  want_x6=True, chunk_major=True),
     "deconv2_h3_h3out": lambda: kernels.deconv_igdn_h3(hh, x2, dec.deconv2.bias, *h2, chunk_major=True),
+    "deconv3_h3": lambda: kernels.deconv3_h3(h64, dec.packed_h3k()[2], dec.deconv3.bias, x_ref=img),
     "deconv1_old": lambda: kernels.deconv_igdn_x6(ys, d1, dec.deconv1.bias, *q1),
     "deconv1_h3": lambda: kernels.deconv_igdn_h3(yh, x1, dec.deconv1.bias, *h1),
     # the training step's deconv1 (B = 32: 8-row tiles) on ỹ with its pre-activation and x6 outputs

@@ -209,6 +209,11 @@ __device__ __forceinline__ long h3_out_step32(const HArgs& a) {
 // (nullable), ŷ in the h3 form (nullable; 16-byte stores after permlane32 swaps as the GDN
 // epilogue's), and the workgroup's bit sum — lanes in (tile, register) order, the xor tree of
 // wave_sum, the waves in order in double — at partial[b][tile · (CO / COT) + cg].
+// The range flag: bit 0 is set by the chain's earlier kernels (conv1 / conv2 / the h3 split of an
+// input) — read here, it makes every output of this kernel NaN (y, ŷ, its h3 form, the bits), so
+// the encoder's own results are loud too, not only the chain's last kernel's; this kernel's own
+// overflow (ŷ's h3 form, deconv1's input) sets bit 1, which it does not read (another workgroup's
+// result would otherwise depend on timing) and deconv3 does.
 template <int TH, int CO, int COT>
 __device__ __forceinline__ void quant_epilogue(const HArgs& a, f16v (&acc)[COT / 32],
                                                unsigned char* lds0, unsigned char* scratch, int b,
@@ -228,6 +233,7 @@ __device__ __forceinline__ void quant_epilogue(const HArgs& a, f16v (&acc)[COT /
   float* const lq = (float*)lds0 + etid * 32;
   float bits = 0.f;
   bool ovf = false;
+  const bool poison = a.range != nullptr && (*(const volatile int*)a.range & 1) != 0;
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
     const int c0 = cg * COT + 32 * i;
@@ -236,7 +242,7 @@ __device__ __forceinline__ void quant_epilogue(const HArgs& a, f16v (&acc)[COT /
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int c = c0 + 8 * (r >> 2) + 4 * eh + (r & 3);
-      const float y = acc[i][r] * dsc;   // a power of two: exact
+      const float y = poison ? __builtin_nanf("") : acc[i][r] * dsc;   // a power of two: exact
       acc[i][r] = y;
       const float yh = round ? rintf(y)
                              : y + (inside ? a.noise[(((long)b * CO + c) * a.Hout + gy) * a.Wout + gx] : 0.f);
@@ -296,8 +302,8 @@ __device__ __forceinline__ void quant_epilogue(const HArgs& a, f16v (&acc)[COT /
       }
     }
   }
-  if (ovf && a.range) atomicOr(a.range, 1);   // vector atomic, per offending lane (rare)
-  bits = wave_sum(bits);
+  if (ovf && a.range) atomicOr(a.range, 2);   // vector atomic, per offending lane (rare)
+  bits = wave_sum(poison ? __builtin_nanf("") : bits);
   float* sw = (float*)scratch;
   if (elane == 0) sw[ewave] = bits;
   __syncthreads();

@@ -206,6 +206,15 @@ class ImageCompressor(nn.Module):
         P little-endian uint32 stream word counts, then the stream words (uint16 LE).
         Returns {"strings": [bytes] * B, "shape": (h, w), "streams_per_image": P, "K": K}."""
         y_hat = self.encode_latents(x)["y_hat"]
+        if kernels.precision() == "h3" and kernels.h3_range_overflowed(x.device):
+            # an activation did not fit the h3 form (conv3 wrote ŷ as NaN): encode from the x6
+            # chain's ŷ instead (full fp32 operands). The flag read is one synchronisation, and
+            # the stream sizes below synchronise anyway.
+            kernels.set_precision("x6")
+            try:
+                y_hat = self.encode_latents(x)["y_hat"]
+            finally:
+                kernels.set_precision("h3")
         B, h, w, N = y_hat.shape
         P = streams_per_image
         words, offsets = kernels.rans_encode(y_hat, self.bitEstimator.entropy_tables(K), K, P)

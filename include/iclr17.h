@@ -467,7 +467,7 @@ int iclr17_rate_param_grad(const float* partial, int T, int C, const float* h1, 
  * [2][…] of a = x·2^-6, hi = rne16(a) and lo = rne16((a − hi)·2^11); weights the same way with a
  * per-tensor power-of-two scale chosen at packing. Against float64 its dot products land closer
  * than the x6 chain's (tools/h3_numerics.hip). |x| ≥ 2^22 does not fit the form: the kernels then
- * set *range_flag (nullable) to 1. Halo patch of the h3 input per 16-channel chunk, a wave owns 32
+ * set *range_flag (nullable) to 1 (conv3_quant_rate_h3: 2). Halo patch of the h3 input per 16-channel chunk, a wave owns 32
  * pixels × all N channels, GDN/IGDN contraction (in the h3 form) from the accumulators.
  * Replaces iclr17_synthesis_deconv_igdn_x6[_cm] on the parity path
  * (synthesis_17.py:15-22; models/GDN.py:64-94, inverse). */
@@ -528,7 +528,9 @@ int iclr17_analysis_conv2_gdn_h3(const uint16_t* in_h3, int B, int H, int W, int
  * the h3 form chunk-major 8 (conv2_gdn_h3 with out_cm 8). 8 × 16-pixel output tiles of 4 waves,
  * each workgroup one 64-channel slice of the output channels, 8-channel input chunks summed
  * two-level. w_h3k: iclr17_pack_h3k(ICLR17_H3K_CONV5) of conv3's weights. Bit partials
- * [B][iclr17_conv3_h3_partials_per_image(B, H, W, N, quant_mode)]. */
+ * [B][iclr17_conv3_h3_partials_per_image(B, H, W, N, quant_mode)]. range_flag: when bit 0 is set
+ * on entry (an earlier h3 kernel of the chain met |x| ≥ 2^22) every output — y, ŷ, its h3 form,
+ * the bit partials — is NaN; this kernel's own overflow (ŷ's h3 form) sets bit 1. */
 int iclr17_conv3_h3_partials_per_image(int B, int H, int W, int N, int quant_mode);
 int iclr17_analysis_conv3_quant_rate_h3(const uint16_t* in_h3, int B, int H, int W, int N,
                                         const uint16_t* w_h3k, int quant_mode, const float* noise,

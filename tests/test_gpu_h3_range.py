@@ -92,9 +92,17 @@ def test_overflow_is_nan_raise_or_x6(device, h3, where):
         assert bool(torch.isnan(ev["clipped"]).all())
         clipped, _, bpp = net(x)                              # the module forward: NaN bpp / recon
         assert bool(torch.isnan(bpp)) and bool(torch.isnan(clipped).all())
-        recon = net.Decoder(torch.round(net.Encoder(x)))      # separate encode / decode
-        if where == "decoder":
-            assert bool(torch.isnan(recon).all())
+        y = net.Encoder(x)                                    # separate encode / decode
+        if where == "encoder":                                # conv3 poisons the encoder's y
+            assert bool(torch.isnan(y).all())
+        recon = net.Decoder(torch.round(y))
+        assert bool(torch.isnan(recon).all())
+        if where == "encoder":                                # compress: rANS from x6's ŷ
+            comp = net.compress(x)
+            kernels.set_precision("x6")
+            comp_ref = net.compress(x)
+            kernels.set_precision("h3")
+            assert comp["strings"] == comp_ref["strings"]
         with pytest.raises(_lib.Iclr17Error, match="2\\^22"):
             net.evaluate(x, h3_overflow="raise")
         fb = net.evaluate(x, want_y=True, h3_overflow="x6")   # the x6 rerun

@@ -833,12 +833,13 @@ def test_deconv3_bits_fold(device, T):
 
 
 @pytest.mark.gpu
-def test_conv2_h3_tile_rows_match(device):
+@pytest.mark.parametrize("N", [192, 128])
+def test_conv2_h3_tile_rows_match(device, N):
     """conv2 + GDN2 on the h3 engine takes 8-row tiles when 16-row ones would leave CUs idle (a
     small batch: training's B = 32 at 256²) and 16-row ones otherwise. The same images in a small
     (8-row) and a large (16-row) batch give bit-equal h3, fp32, x6 and pre-activation outputs: a
     pixel's arithmetic does not depend on the tile."""
-    N, h, w = 192, 64, 64              # conv2 output 32×32: four 16×16 tiles per image
+    h, w = 64, 64                      # conv2 output 32×32: four 16×16 tiles per image
     Bs, Bw = 3, 64                     # 12 tiles·images < 256 CUs (8 rows), 256 (16 rows)
     net = net_for(N, 1, device)
     enc = net.Encoder
@@ -858,12 +859,13 @@ def test_conv2_h3_tile_rows_match(device):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("N", [192, 128])
 @pytest.mark.parametrize("int_in", [False, True])
-def test_deconv_h3_tile_rows_match(device, int_in):
+def test_deconv_h3_tile_rows_match(device, int_in, N):
     """deconv + IGDN on the h3 engine: 8-row tiles on a small batch (deconv1 at B = 3: 12 workgroups
     of 16 rows would leave CUs idle), 16-row ones on a large one (B = 64); the same images give
     bit-equal outputs, with the integer-input (ŷ) form and without."""
-    N, h, w = 192, 16, 16
+    h, w = 16, 16
     Bs, Bw = 3, 64
     net = net_for(N, 1, device)
     dec = net.Decoder

@@ -65,7 +65,7 @@ def main() -> None:
         rows.append(r)
     lib = os.path.join(REPO, "iclr_17_compression_amd", "libiclr17.so")
     out = {"lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16],
-           "workload": "bench.py --mode train --batch 32 (B=32 256², N=192, x6)",
+           "workload": "bench.py --mode train --batch 32 (B=32 256², N=192, h3 forward + x6 backward)",
            "traced_steps": steps, "step_ms_under_trace": round(total / steps, 4), "kernels": rows}
     json.dump(out, open(os.path.join(src, f"{tag}_train_kernels.json"), "w"), indent=1)
     print(f"{len(rows)} kernels, {total / steps:.3f} ms per step under trace")
